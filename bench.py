@@ -1,0 +1,207 @@
+#!/usr/bin/env python3
+"""bench.py — simulated peer-message deliveries/s of the GossipSub dissemination
+hot path on MI355X (BASELINE.json metric), plus the relaxation kernel's
+roofline fraction and the CPU oracle's rate on a bounded sample.
+
+One step = one batch of B messages disseminated over a frozen 1M-peer mesh
+(publish -> flood -> mesh forwarding -> reassembly), inputs resident in HBM.
+Multi-GPU: one process per GPU (torchrun), each simulating its own message
+shard (weak scaling; no data-path collective).
+
+    python bench.py --gpus 1 --steps 20 --warmup 3
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "dst-libp2p-test-node_amd"))
+
+import numpy as np  # noqa: E402
+
+import gossipsim  # noqa: E402
+
+METRIC = "simulated peer-msg deliveries/sec at 100k & 1M peers; % of HBM BW"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--peers", type=int, default=1_000_000)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--fragments", type=int, default=1)
+    ap.add_argument("--msg-size", type=int, default=15000)
+    ap.add_argument("--links", default="5,50,150,40,130", help="stages,bl,bh,ll,lh (topogen.py)")
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--max-heartbeats", type=int, default=400)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU oracle sample budget (0=off)")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
+                    help="per-launch HBM bytes of the relax kernel from a rocprofv3 --pmc pass")
+    return ap.parse_args()
+
+
+def dist_setup():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch = dist = None
+    try:
+        import torch
+        import torch.distributed as dist
+    except ImportError:
+        pass
+    if world > 1:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend)
+    return world, rank, local, torch, dist
+
+
+def allreduce(torch, dist, world, vals, op):
+    if world == 1:
+        return vals
+    dev = "cuda" if torch.cuda.is_available() else "cpu"
+    t = torch.tensor(vals, dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=op)
+    return t.tolist()
+
+
+def barrier_sync(torch, dist, world):
+    if world > 1:
+        dist.barrier()
+    if torch is not None and torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
+def cpu_baseline(sim, args, S, links, budget_s):
+    """Single-threaded CPU oracle on the same graph + mesh, a bounded message sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # checker / baseline only
+    N = args.peers
+    row, col, _ = sim.csr()
+    mesh, cnt = sim.mesh()
+    lat, bw = oracle.topogen_links(S, *links)
+    stage = (np.arange(N) % S).astype(np.uint8)
+    kw = {n: getattr(sim.cfg.c, n) for n, _ in oracle.OrParams._fields_}
+    p = oracle.OrParams(**kw)
+    t, pub, size = gossipsim.shard_messages(10_000, 0, 1, 64, N, args.msg_size)
+    deliv, elapsed, k = 0, 0.0, 0
+    tcs, hps = [], []
+    while k < 64 and (elapsed < budget_s or k == 0):
+        t0 = time.perf_counter()
+        tc, hp, st = oracle.run(p, row, col, mesh, cnt, stage, lat, bw, bw, t[k:k + 1], pub[k:k + 1],
+                                size[k:k + 1])
+        elapsed += time.perf_counter() - t0
+        deliv += st["deliveries"]
+        tcs.append(tc[0])
+        hps.append(hp[0])
+        k += 1
+    # parity of the sampled messages (outside every timed region)
+    res = sim.run((t[:k], pub[:k], size[:k]), collect=True)
+    same = bool((res["t_complete"] == np.stack(tcs)).all() and (res["hops"] == np.stack(hps)).all())
+    return {"value": deliv / elapsed, "unit": "deliveries/s", "cores": 1, "kind": "port",
+            "sample": "oracle/gs_oracle.c or_run (binary-heap event simulation), %d messages on the "
+                      "same %d-peer graph+mesh, %.1f s single-threaded" % (k, N, elapsed),
+            "parity_with_gpu_on_sample": same}
+
+
+def main():
+    args = parse()
+    world, rank, local, torch, dist = dist_setup()
+    S, bl, bh, ll, lh = [int(x) for x in args.links.split(",")]
+    links = (bl, bh, ll, lh)
+    sim = gossipsim.Simulator(peers=args.peers, batch=args.batch, fragments=args.fragments,
+                              seed=args.seed, device=local)
+    t_setup = time.perf_counter()
+    sim.set_topogen_links(S, bl, bh, ll, lh)
+    sim.connect_gossipsub_peers()
+    epochs = sim.mesh_converge(args.max_heartbeats)
+    t_setup = time.perf_counter() - t_setup
+
+    def step(i):
+        sim.run(gossipsim.shard_messages(i, rank, world, args.batch, args.peers, args.msg_size),
+                collect=False)
+
+    for i in range(args.warmup):
+        step(i)
+    sim.reset_stats()
+    sim.set_timing(True)
+    barrier_sync(torch, dist, world)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    barrier_sync(torch, dist, world)
+    elapsed = time.perf_counter() - t0
+    st = sim.stats()
+    sim.set_timing(False)
+    SUM = dist.ReduceOp.SUM if dist is not None else None
+    MAX = dist.ReduceOp.MAX if dist is not None else None
+    (max_elapsed,) = allreduce(torch, dist, world, [elapsed], MAX)
+    tot = allreduce(torch, dist, world, [st["deliveries"], st["frag_deliveries"], st["relaxations"],
+                                         st["bytes_alg"]], SUM)
+    deliveries = tot[0]
+
+    launches = max(1, st["relax_launches"])
+    achieved = st["relax_bytes_alg"] / (st["relax_ms"] / 1e3) / 1e9 if st["relax_ms"] > 0 else None
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            if tj.get("peers") == args.peers and tj.get("batch") == args.batch:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
+            "kernel": "k_relax<1> (Delta-bucket relaxation)",
+            "alg_bytes_per_launch": st["relax_bytes_alg"] / launches,
+            "avg_launch_us": st["relax_ms"] * 1e3 / launches, "launches": st["relax_launches"]}
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        cpu = cpu_baseline(sim, args, S, links, args.cpu_seconds)
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": deliveries / max_elapsed,
+            "unit": "deliveries/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": max_elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (random-ID dial graph + converged mesh, run.sh publish schedule)",
+            "config": {
+                "workload": "%d peers, %d-stage topogen links (%d-%d Mbit, %d-%d ms), CONNECTTO=10, "
+                            "D=6/4/8, F=%d, %d B msgs, %d msgs/step/GPU, message-sharded"
+                            % (args.peers, S, bl, bh, ll, lh, args.fragments, args.msg_size, args.batch),
+                "peers": args.peers, "batch": args.batch, "fragments": args.fragments,
+                "msg_size": args.msg_size, "links": args.links, "parallelism": "msg-shard%d" % world,
+            },
+            "deliveries": int(deliveries),
+            "frag_deliveries": int(tot[1]),
+            "relaxations": int(tot[2]),
+            "bytes_alg": int(tot[3]),
+            "setup_s": t_setup,
+            "mesh_epochs": epochs,
+            "buckets_per_step": st["buckets"] / max(1, args.steps),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,230 @@
+// gs_host.cpp — host-only entry points of the C ABI (no device work):
+// config defaults and the env surface, wire-byte model, topogen link tables,
+// run.sh publish schedule and the awk-compatible arrival-log writer.
+#include <ctype.h>
+#include <errno.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <strings.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/gossipsim.h"
+#include "gs_common.h"
+
+extern "C" void gs_config_default(gs_config* c) {
+  memset(c, 0, sizeof(*c));
+  c->abi_version = GS_ABI_VERSION;
+  c->peers = 100;                 // env.rs:38-41
+  c->connect_to = 10;             // env.rs:43-46
+  c->dial_extra = 1;              // main.rs:337 (defect D4)
+  c->max_connections = 0;         // rust has no cap
+  c->fragments = 1;               // env.rs:64-67
+  c->muxer = GS_MUX_YAMUX;        // env.rs:48-50
+  c->signed_msgs = 1;             // main.rs:397
+  c->d = 6; c->d_lo = 4; c->d_hi = 8;           // main.rs:36-38
+  c->d_lazy = 6;                  // main.rs:235
+  c->d_out = 3;                   // main.rs:234
+  c->gossip_factor_milli = 250;   // main.rs:230
+  c->heartbeat_ns = 1000000000ull;       // main.rs:228
+  c->backoff_ns = 60000000000ull;        // main.rs:229
+  c->flood_publish = 1;           // main.rs:227
+  c->idontwant = 0;
+  c->lazy_gossip = 0;
+  c->self_log = 0;                // rust: no self delivery
+  c->seed = 1;
+  c->device = 0;
+  c->batch = 64;
+}
+
+namespace {
+
+bool env_u64(const char* name, uint64_t* out, char* err, size_t n, bool* bad) {
+  const char* v = getenv(name);
+  if (!v || !*v) return false;
+  char* end = nullptr;
+  errno = 0;
+  unsigned long long x = strtoull(v, &end, 10);
+  if (errno || *end) {  // rust's parse().unwrap_or(default) keeps the default
+    (void)err; (void)n; (void)bad;
+    return false;
+  }
+  *out = x;
+  return true;
+}
+
+bool env_bool(const char* name, uint32_t* out) {
+  const char* v = getenv(name);
+  if (!v || !*v) return false;
+  if (!strcasecmp(v, "true") || !strcmp(v, "1")) { *out = 1; return true; }
+  if (!strcasecmp(v, "false") || !strcmp(v, "0")) { *out = 0; return true; }
+  return false;
+}
+
+void set_err(char* err, size_t n, const std::string& s) {
+  if (err && n) { snprintf(err, n, "%s", s.c_str()); }
+}
+
+}  // namespace
+
+// Mirrors get_peer_details (rust-test-node/src/env.rs:27-87) plus the nim
+// GOSSIPSUB_* names (nim-test-node/gossipsub-queues/main.nim:252-284).
+extern "C" gs_status gs_config_from_env(gs_config* c, char* err, size_t err_len) {
+  if (!c) return GS_EINVAL;
+  bool bad = false;
+  uint64_t x;
+  if (env_u64("PEERS", &x, err, err_len, &bad)) c->peers = (uint32_t)x;
+  if (env_u64("CONNECTTO", &x, err, err_len, &bad)) c->connect_to = (uint32_t)x;
+  if (env_u64("FRAGMENTS", &x, err, err_len, &bad)) c->fragments = (uint32_t)x;
+  if (env_u64("MAXCONNECTIONS", &x, err, err_len, &bad)) c->max_connections = (uint32_t)x;
+  if (env_u64("GOSSIPSUB_D", &x, err, err_len, &bad)) c->d = (uint32_t)x;
+  if (env_u64("GOSSIPSUB_D_LOW", &x, err, err_len, &bad)) c->d_lo = (uint32_t)x;
+  if (env_u64("GOSSIPSUB_D_HIGH", &x, err, err_len, &bad)) c->d_hi = (uint32_t)x;
+  if (env_u64("GOSSIPSUB_D_LAZY", &x, err, err_len, &bad)) c->d_lazy = (uint32_t)x;
+  if (env_u64("GOSSIPSUB_D_OUT", &x, err, err_len, &bad)) c->d_out = (uint32_t)x;
+  if (env_u64("GOSSIPSUB_HEARTBEAT_MS", &x, err, err_len, &bad)) c->heartbeat_ns = x * 1000000ull;
+  if (env_u64("GOSSIPSUB_PRUNE_BACKOFF_SEC", &x, err, err_len, &bad)) c->backoff_ns = x * 1000000000ull;
+  if (env_u64("GS_SEED", &x, err, err_len, &bad)) c->seed = x;
+  if (env_u64("GS_BATCH", &x, err, err_len, &bad)) c->batch = (uint32_t)x;
+  if (env_u64("GS_DEVICE", &x, err, err_len, &bad)) c->device = (int32_t)x;
+  if (env_u64("GS_IDONTWANT", &x, err, err_len, &bad)) c->idontwant = (uint32_t)x;
+  const char* gf = getenv("GOSSIPSUB_GOSSIP_FACTOR");
+  if (gf && *gf) {
+    char* end = nullptr;
+    double f = strtod(gf, &end);
+    if (!*end && f >= 0.0 && f <= 1.0) c->gossip_factor_milli = (uint32_t)(f * 1000.0 + 0.5);
+  }
+  env_bool("GOSSIPSUB_FLOOD_PUBLISH", &c->flood_publish);
+  env_bool("SELFTRIGGER", &c->self_log);
+  const char* mx = getenv("MUXER");
+  if (mx && *mx) {
+    std::string m(mx);
+    for (auto& ch : m) ch = (char)tolower((unsigned char)ch);  // env.rs:50 to_lowercase
+    if (m == "yamux") c->muxer = GS_MUX_YAMUX;
+    else if (m == "quic") c->muxer = GS_MUX_QUIC;
+    else if (m == "mplex") c->muxer = GS_MUX_MPLEX;  // nim only
+    else { set_err(err, err_len, "Unknown muxer type: " + m); return GS_EINVAL; }  // env.rs:69-71
+  }
+  if (c->connect_to >= c->peers) {  // env.rs:73-75
+    set_err(err, err_len, "Not enough peers to make target connections. Network size: " +
+                              std::to_string(c->peers));
+    return GS_EINVAL;
+  }
+  return GS_OK;
+}
+
+namespace {
+uint64_t varint_len(uint64_t x) { uint64_t n = 1; while (x >= 128) { x >>= 7; n++; } return n; }
+uint64_t pb_field(uint64_t len) { return 1 + varint_len(len) + len; }
+uint64_t cdiv(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+}  // namespace
+
+// Per-hop wire bytes of one fragment:
+// protobuf RPC{publish: Message{from, data, seqno, topic, signature}}
+// length-prefixed, then the MUXER stack (rust-test-node/src/main.rs:418-440).
+extern "C" uint64_t gs_wire_bytes(uint64_t payload, uint32_t muxer, uint32_t signed_msgs) {
+  uint64_t body = pb_field(payload) + pb_field(4);               // data, topic "test"
+  if (signed_msgs) body += pb_field(38) + pb_field(8) + pb_field(64);  // from, seqno, sig
+  const uint64_t rpc = pb_field(body);
+  const uint64_t frame = varint_len(rpc) + rpc;
+  if (muxer == GS_MUX_QUIC) return frame + cdiv(frame, 1415) * 65;
+  const uint64_t mux = (muxer == GS_MUX_MPLEX) ? frame + cdiv(frame, 1048576) * 4
+                                               : frame + cdiv(frame, 16384) * 12;
+  const uint64_t noise = mux + cdiv(mux, 65519) * 18;
+  return noise + cdiv(noise, 1460) * 40;
+}
+
+// shadow/topogen.py:39-71 restated: stage i bandwidth ceil(i*bj + bl) Mbit
+// (44,49-51); self-loop max((S-i)*lj, ll) ms (55); edge i<j
+// min(ceil((S-j)*lj + ll), lh) ms (60); injector node S, 1 ms to all (64-69).
+extern "C" gs_status gs_topogen_links(uint32_t S, uint32_t bl, uint32_t bh, uint32_t ll,
+                                      uint32_t lh, uint32_t mode, uint64_t* lat_ns,
+                                      uint64_t* bw_bps) {
+  if (S == 0 || S > 255 || bl > bh || ll > lh || mode > GS_LINKS_SHORTEST || !lat_ns || !bw_bps)
+    return GS_EINVAL;
+  const uint64_t bj = (bh - bl) / S, lj = (lh - ll) / S;
+  const uint32_t V = S + 1;
+  std::vector<uint64_t> g((size_t)V * V, 0);
+  for (uint32_t i = 0; i < S; i++) {
+    bw_bps[i] = ((uint64_t)i * bj + bl) * 1000000ull;
+    uint64_t self = (uint64_t)(S - i) * lj;
+    g[(size_t)i * V + i] = self < ll ? ll : self;
+    for (uint32_t j = i + 1; j < S; j++) {
+      uint64_t e = (uint64_t)(S - j) * lj + ll;
+      g[(size_t)i * V + j] = g[(size_t)j * V + i] = e > lh ? lh : e;
+    }
+  }
+  for (uint32_t i = 0; i <= S; i++) g[(size_t)i * V + S] = g[(size_t)S * V + i] = 1;
+  if (mode == GS_LINKS_DIRECT) {
+    for (uint32_t i = 0; i < S; i++)
+      for (uint32_t j = 0; j < S; j++) lat_ns[(size_t)i * S + j] = g[(size_t)i * V + j] * 1000000ull;
+    return GS_OK;
+  }
+  // Shadow use_shortest_path (upstream, not vendored): shortest non-empty path.
+  std::vector<uint64_t> d((size_t)V * V);
+  for (uint32_t i = 0; i < V; i++)
+    for (uint32_t j = 0; j < V; j++) d[(size_t)i * V + j] = i == j ? 0 : g[(size_t)i * V + j];
+  for (uint32_t k = 0; k < V; k++)
+    for (uint32_t i = 0; i < V; i++)
+      for (uint32_t j = 0; j < V; j++) {
+        uint64_t via = d[(size_t)i * V + k] + d[(size_t)k * V + j];
+        if (via < d[(size_t)i * V + j]) d[(size_t)i * V + j] = via;
+      }
+  for (uint32_t i = 0; i < S; i++)
+    for (uint32_t j = 0; j < S; j++) {
+      uint64_t v = d[(size_t)i * V + j];
+      if (i == j) {
+        v = g[(size_t)i * V + i];
+        for (uint32_t k = 0; k < V; k++) {
+          if (k == i) continue;
+          uint64_t rt = d[(size_t)i * V + k] + d[(size_t)k * V + i];
+          if (rt < v) v = rt;
+        }
+      }
+      lat_ns[(size_t)i * S + j] = v * 1000000ull;
+    }
+  return GS_OK;
+}
+
+// shadow/run.sh:34-36 + shadow/README.md:76-78: publisher_id, rotation 0/1,
+// inter_message_delay. tx_time is the publish instant (main.rs:105-111).
+extern "C" gs_status gs_schedule_runsh(uint32_t n_msgs, uint32_t peers, uint32_t publisher_id,
+                                       uint32_t rotation, uint64_t t0_ns, uint64_t delay_ns,
+                                       uint32_t msg_size, gs_publish* out) {
+  if (!out || peers == 0) return GS_EINVAL;
+  for (uint32_t i = 0; i < n_msgs; i++) {
+    out[i].t_pub_ns = t0_ns + (uint64_t)i * delay_ns;
+    out[i].publisher = (uint32_t)(((uint64_t)publisher_id + (uint64_t)i * rotation) % peers);
+    out[i].msg_size = msg_size;
+  }
+  return GS_OK;
+}
+
+// The grep view of Shadow's per-host stdout (shadow/run.sh:61) for the line
+// printed at rust-test-node/src/main.rs:93. Paths use `peer<id>` so that the
+// split regex of shadow/summary_latency.awk:17 recovers the id (defect D3).
+extern "C" gs_status gs_write_latency_log(const char* path, const gs_publish* sched,
+                                          uint64_t n_msgs, uint32_t peers,
+                                          const uint64_t* t_complete_ns, uint32_t self_log) {
+  if (!path || !sched || !t_complete_ns) return GS_EINVAL;
+  FILE* f = fopen(path, "w");
+  if (!f) return GS_EINVAL;
+  std::vector<char> buf(1 << 20);
+  setvbuf(f, buf.data(), _IOFBF, buf.size());
+  for (uint32_t u = 0; u < peers; u++) {
+    uint64_t line = 0;
+    for (uint64_t m = 0; m < n_msgs; m++) {
+      const uint64_t t = t_complete_ns[m * peers + u];
+      if (t == GS_UNDELIVERED) continue;
+      if (u == sched[m].publisher && !self_log) continue;
+      const uint64_t tx = sched[m].t_pub_ns;
+      const int64_t ms = ((int64_t)t - (int64_t)tx) / 1000000;  // i64 division, main.rs:91-93
+      fprintf(f, "shadow.data/hosts/peer%u/main.1000.stdout:%llu:%lld milliseconds: %lld\n", u,
+              (unsigned long long)++line, (long long)tx, (long long)ms);
+    }
+  }
+  if (fclose(f)) return GS_EINVAL;
+  return GS_OK;
+}

@@ -1,0 +1,115 @@
+// gs_internal.h — context layout and kernel-launch entry points shared by the
+// translation units of libgossipsim (not part of the C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/gossipsim.h"
+#include "gs_common.h"
+
+#define GS_HIP(call)                                                                   \
+  do {                                                                                 \
+    hipError_t e_ = (call);                                                            \
+    if (e_ != hipSuccess) throw gs::Error(GS_EDEVICE, std::string(#call) + ": " +      \
+                                                          hipGetErrorString(e_));      \
+  } while (0)
+
+namespace gs {
+
+struct Error {
+  gs_status code;
+  std::string msg;
+  Error(gs_status c, std::string m) : code(c), msg(std::move(m)) {}
+};
+
+// Device-side error word bits (set by kernels, checked by the host).
+enum : uint32_t { ERR_TIME = 1, ERR_HOPS = 2, ERR_MESH = 4, ERR_DEG = 8 };
+
+// Device buffer owned by a context.
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  void alloc(size_t count) {
+    if (count <= n && p) return;
+    release();
+    if (count == 0) return;
+    GS_HIP(hipMalloc((void**)&p, count * sizeof(T)));
+    n = count;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  ~DevBuf() { release(); }
+};
+
+// Counters written by kernels: index constants into Ctx::d_counters.
+enum : uint32_t {
+  C_FD = 0, C_R = 1, C_DELIV = 2, C_LAT_SUM = 3, C_LAT_MAX = 4, C_BUCKETS = 5,
+  C_R_FWD = 6, C_MESH_CHANGES = 7, C_MESH_WAKE = 8, C_ERR = 9, C_COUNT = 16
+};
+
+struct Ctx {
+  gs_config cfg{};
+  std::string last_error;
+  hipStream_t stream = nullptr;
+  bool timing = false;
+
+  // links
+  uint32_t S = 0;
+  std::vector<uint64_t> lat_ns, bw_up, bw_dn;
+  std::vector<uint8_t> stage_host;
+  bool links_set = false;
+
+  // graph (device resident)
+  bool topo_built = false, mesh_built = false;
+  uint32_t k = 0;            // dials per peer
+  uint64_t nnz = 0;
+  uint32_t max_degree = 0;
+  DevBuf<uint8_t> d_stage;
+  DevBuf<uint32_t> d_dial;   // [N*k]
+  DevBuf<uint8_t> d_acc;     // [N*k] dial accepted
+  DevBuf<uint64_t> d_row;    // [N+1]
+  DevBuf<uint32_t> d_col;    // [nnz]
+  DevBuf<uint8_t> d_flags;   // [nnz] F_OUT | F_MESH
+  DevBuf<uint32_t> d_rev;    // [nnz] index of the reverse entry
+  DevBuf<uint32_t> d_until;  // [nnz] back-off: graft refused while epoch < until
+  DevBuf<uint8_t> d_prop;    // [nnz] per-epoch GRAFT/PRUNE/ACCEPT bits
+  DevBuf<uint32_t> d_mesh;   // [N*MESH_W] packed stage<<24|peer, EMPTY padded
+  DevBuf<uint8_t> d_mcnt;    // [N]
+
+  // dissemination (per batch)
+  DevBuf<uint64_t> d_keys;   // [N * B * FP] peer-major (u, m, f)
+  DevBuf<uint64_t> d_busy;   // [N * B] uplink FIFO end per (u, m) (F > 1)
+  DevBuf<uint32_t> d_pub;    // [B]
+  DevBuf<uint64_t> d_tpub;   // [B]
+  DevBuf<uint64_t> d_tc;     // [B * N] message-major completion times
+  DevBuf<uint8_t> d_hops;    // [B * N]
+  DevBuf<uint32_t> d_tables; // lat[S*S] | ser_up[S] | ser_dn[S] (u32 ns)
+  DevBuf<uint64_t> d_ctrl;   // [4] triple-buffered next-min keys + spare
+  DevBuf<uint64_t> d_counters;  // [C_COUNT]
+  uint64_t* h_pinned = nullptr; // pinned host mirror of ctrl + counters
+
+  // stats
+  gs_stats stats{};
+  std::vector<hipEvent_t> ev_pool;
+  int num_cus = 0;
+
+  ~Ctx();
+  void fail(gs_status c, const std::string& m) { throw Error(c, m); }
+};
+
+// ---- launchers (gs_topology.hip / gs_mesh.hip / gs_relax.hip) ----
+void launch_topology(Ctx& c);
+uint32_t run_mesh(Ctx& c, uint32_t max_heartbeats);
+void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_result_sink* sink);
+
+// small device helpers
+void device_exclusive_scan(Ctx& c, const uint64_t* in, uint64_t* out, uint32_t n);
+uint64_t read_counter(Ctx& c, uint32_t idx);
+
+}  // namespace gs

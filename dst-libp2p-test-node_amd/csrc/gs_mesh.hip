@@ -1,0 +1,283 @@
+// gs_mesh.hip — GossipSub heartbeat mesh maintenance (GRAFT/PRUNE to
+// D / D_lo / D_hi) as synchronous epochs on gfx950.
+//
+// The reference runs libp2p-gossipsub's heartbeat every 1 s
+// (rust-test-node/src/main.rs:228) with mesh_n/low/high 6/4/8, outbound min 3,
+// prune back-off 60 s (main.rs:229-236); scoring is inert (main.rs:260-269).
+// Each epoch is three one-thread-per-peer kernels over the CSR:
+//   A  heartbeat decisions (graft to D below D_lo, prune to D above D_hi
+//      keeping D_out outbound, graft outbound peers when short),
+//   B  GRAFT handling at the receiver in (latency, id) order (back-off and
+//      D_hi-unless-outbound rejections),
+//   C  PRUNEs and rejections applied, both ends back off.
+// Random choices use per-(peer, epoch, candidate) keys: take the r smallest.
+#include "gs_internal.h"
+
+namespace gs {
+namespace {
+
+constexpr int TB = 256;
+constexpr uint32_t SEL_MAX = 16;   // r <= D <= 16 picks per heartbeat
+
+struct MeshArgs {
+  const uint64_t* row;
+  const uint32_t* col;
+  const uint32_t* rev;
+  uint8_t* flags;
+  uint8_t* prop;
+  uint32_t* until;
+  const uint8_t* stage;
+  const uint32_t* lat;  // S*S ns
+  uint64_t* counters;
+  uint64_t seed;
+  uint32_t N, S, epoch, bo, d, d_lo, d_hi, d_out;
+};
+
+// Insert (key, e) into a bounded ascending list of length <= r.
+__device__ __forceinline__ void top_insert(uint64_t* kk, uint32_t* ee, uint32_t& n, uint32_t r,
+                                           uint64_t key, uint32_t e) {
+  if (r == 0) return;
+  if (n == r) {
+    if (kk[n - 1] < key || (kk[n - 1] == key && ee[n - 1] < e)) return;
+    n--;
+  }
+  int32_t j = (int32_t)n - 1;
+  while (j >= 0 && (kk[j] > key || (kk[j] == key && ee[j] > e))) {
+    kk[j + 1] = kk[j];
+    ee[j + 1] = ee[j];
+    j--;
+  }
+  kk[j + 1] = key;
+  ee[j + 1] = e;
+  n++;
+}
+
+__global__ __launch_bounds__(TB) void k_heartbeat(MeshArgs a) {
+  const uint32_t u = blockIdx.x * TB + threadIdx.x;
+  if (u >= a.N) return;
+  const uint64_t b = a.row[u], en = a.row[u + 1];
+  uint32_t m = 0, o = 0;
+  for (uint64_t e = b; e < en; e++) {
+    const uint8_t f = a.flags[e];
+    if (f & F_MESH) { m++; o += f & F_OUT; }
+  }
+  uint32_t mm = m, oo = o;
+  uint64_t kk[SEL_MAX];
+  uint32_t ee[SEL_MAX];
+  uint32_t n = 0;
+  if (m < a.d_lo) {  // graft mesh_n - |mesh| random eligible peers
+    const uint32_t want = a.d - m;
+    for (uint64_t e = b; e < en; e++)
+      if (!(a.flags[e] & F_MESH) && a.epoch > a.until[e])
+        top_insert(kk, ee, n, want, rng(a.seed, P_GRAFT, u, a.epoch, a.col[e]), (uint32_t)(e - b));
+    for (uint32_t q = 0; q < n; q++) {
+      a.prop[b + ee[q]] |= PR_GRAFT;
+      mm++;
+      oo += a.flags[b + ee[q]] & F_OUT;
+    }
+  }
+  if (mm > a.d_hi) {  // prune down to mesh_n, keep mesh_outbound_min outbound
+    // walk the mesh in ascending (key, entry) order by repeated selection
+    const uint32_t excess = mm - a.d;
+    uint32_t removed = 0;
+    uint64_t pk = 0;
+    int64_t pe = -1;
+    for (uint32_t q = 0; q < m && removed < excess; q++) {
+      uint64_t bk = INF64;
+      int64_t be = -1;
+      for (uint64_t e = b; e < en; e++) {
+        if (!(a.flags[e] & F_MESH)) continue;
+        const uint64_t k = rng(a.seed, P_PRUNE, u, a.epoch, a.col[e]);
+        const int64_t le = (int64_t)(e - b);
+        const bool after = k > pk || (k == pk && le > pe);
+        const bool better = be < 0 || k < bk || (k == bk && le < be);
+        if (after && better) { bk = k; be = le; }
+      }
+      pk = bk;
+      pe = be;
+      const uint64_t e = b + (uint64_t)be;
+      if (a.flags[e] & F_OUT) {
+        if (oo <= a.d_out) continue;
+        oo--;
+      }
+      a.prop[e] |= PR_PRUNE;
+      removed++;
+      mm--;
+    }
+  }
+  if (mm >= a.d_lo && oo < a.d_out) {  // graft outbound peers
+    n = 0;
+    const uint32_t want = a.d_out - oo;
+    for (uint64_t e = b; e < en; e++) {
+      const uint8_t f = a.flags[e];
+      if ((f & F_OUT) && !(f & F_MESH) && !(a.prop[e] & PR_GRAFT) && a.epoch > a.until[e])
+        top_insert(kk, ee, n, want, rng(a.seed, P_OUT_GRAFT, u, a.epoch, a.col[e]),
+                   (uint32_t)(e - b));
+    }
+    for (uint32_t q = 0; q < n; q++) a.prop[b + ee[q]] |= PR_GRAFT;
+  }
+}
+
+__global__ __launch_bounds__(TB) void k_handle_graft(MeshArgs a) {
+  const uint32_t w = blockIdx.x * TB + threadIdx.x;
+  if (w >= a.N) return;
+  const uint64_t b = a.row[w], en = a.row[w + 1];
+  uint32_t c = 0;
+  const uint32_t sw = a.stage[w];
+  for (uint64_t e = b; e < en; e++) {
+    const uint8_t f = a.flags[e], p = a.prop[e];
+    c += (((f & F_MESH) && !(p & PR_PRUNE)) || (p & PR_GRAFT)) ? 1u : 0u;
+  }
+  // GRAFTs arrive in (latency u->w, id) order: one pass per distinct latency
+  // level (<= S levels), each pass in ascending id.
+  int64_t prev = -1;
+  for (;;) {
+    int64_t level = -1;
+    for (uint64_t e = b; e < en; e++)
+      if (a.prop[a.rev[e]] & PR_GRAFT) {
+        const int64_t l = a.lat[a.stage[a.col[e]] * a.S + sw];
+        if (l > prev && (level < 0 || l < level)) level = l;
+      }
+    if (level < 0) break;
+    for (uint64_t e = b; e < en; e++) {  // entry (w -> u)
+      if (!(a.prop[a.rev[e]] & PR_GRAFT) || (int64_t)a.lat[a.stage[a.col[e]] * a.S + sw] != level)
+        continue;
+      const uint8_t f = a.flags[e], p = a.prop[e];
+      const bool in_mesh = ((f & F_MESH) && !(p & PR_PRUNE)) || (p & PR_GRAFT);
+      if (in_mesh) { a.prop[a.rev[e]] |= PR_ACCEPT; continue; }
+      if (a.epoch < a.until[e] || (c >= a.d_hi && !(f & F_OUT))) {
+        a.until[e] = a.epoch + a.bo;  // PRUNE back, both ends back off
+        continue;
+      }
+      a.prop[a.rev[e]] |= PR_ACCEPT;
+      a.flags[e] = f | F_MESH;
+      c++;
+    }
+    prev = level;
+  }
+}
+
+__global__ __launch_bounds__(TB) void k_apply(MeshArgs a) {
+  const uint32_t u = blockIdx.x * TB + threadIdx.x;
+  uint64_t changes = 0;
+  if (u < a.N) {
+    for (uint64_t e = a.row[u]; e < a.row[u + 1]; e++) {
+      const uint8_t p = a.prop[e];
+      uint8_t f = a.flags[e];
+      if (p & PR_GRAFT) {
+        changes++;
+        if (p & PR_ACCEPT) f |= F_MESH;
+        else { f &= (uint8_t)~F_MESH; a.until[e] = a.epoch + a.bo; }
+      }
+      if (p & PR_PRUNE) { changes++; f &= (uint8_t)~F_MESH; a.until[e] = a.epoch + a.bo; }
+      if (a.prop[a.rev[e]] & PR_PRUNE) { f &= (uint8_t)~F_MESH; a.until[e] = a.epoch + a.bo; }
+      a.flags[e] = f;
+    }
+  }
+  // one atomic per wave
+  for (int off = 32; off > 0; off >>= 1) changes += __shfl_xor(changes, off);
+  if ((threadIdx.x & 63) == 0 && changes)
+    atomicAdd((unsigned long long*)&a.counters[C_MESH_CHANGES], (unsigned long long)changes);
+}
+
+// Quiescent epoch: earliest back-off expiry that can wake a hungry peer.
+__global__ __launch_bounds__(TB) void k_wake(MeshArgs a) {
+  const uint32_t u = blockIdx.x * TB + threadIdx.x;
+  uint64_t wake = INF64;
+  if (u < a.N) {
+    const uint64_t b = a.row[u], en = a.row[u + 1];
+    uint32_t m = 0, o = 0;
+    for (uint64_t e = b; e < en; e++)
+      if (a.flags[e] & F_MESH) { m++; o += a.flags[e] & F_OUT; }
+    const bool need_any = m < a.d_lo;
+    const bool need_out = !need_any && m <= a.d_hi && o < a.d_out;
+    if (need_any || need_out)
+      for (uint64_t e = b; e < en; e++) {
+        const uint8_t f = a.flags[e];
+        if ((f & F_MESH) || (need_out && !(f & F_OUT))) continue;
+        if (a.until[e] >= a.epoch + 1 && (uint64_t)a.until[e] + 1 < wake) wake = (uint64_t)a.until[e] + 1;
+      }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint64_t x = __shfl_xor(wake, off);
+    wake = x < wake ? x : wake;
+  }
+  if ((threadIdx.x & 63) == 0 && wake != INF64)
+    atomicMin((unsigned long long*)&a.counters[C_MESH_WAKE], (unsigned long long)wake);
+}
+
+__global__ __launch_bounds__(TB) void k_clear_mesh(uint64_t nnz, uint8_t* flags, uint32_t* until) {
+  const uint64_t e = (uint64_t)blockIdx.x * TB + threadIdx.x;
+  if (e >= nnz) return;
+  flags[e] &= (uint8_t)~F_MESH;
+  until[e] = 0;
+}
+
+// ELL extraction: packed stage<<24 | peer in ascending id, EMPTY padded.
+__global__ __launch_bounds__(TB) void k_extract(MeshArgs a, uint32_t* mesh, uint8_t* mcnt) {
+  const uint32_t u = blockIdx.x * TB + threadIdx.x;
+  if (u >= a.N) return;
+  uint32_t c = 0;
+  for (uint64_t e = a.row[u]; e < a.row[u + 1]; e++)
+    if (a.flags[e] & F_MESH) {
+      if (c == MESH_W) { atomicOr((unsigned*)&a.counters[C_ERR], ERR_MESH); break; }
+      const uint32_t w = a.col[e];
+      mesh[(size_t)u * MESH_W + c++] = ((uint32_t)a.stage[w] << STAGE_SHIFT) | w;
+    }
+  mcnt[u] = (uint8_t)c;
+  for (uint32_t q = c; q < MESH_W; q++) mesh[(size_t)u * MESH_W + q] = EMPTY;
+}
+
+inline unsigned blocks(uint64_t n) { return (unsigned)((n + TB - 1) / TB); }
+
+}  // namespace
+
+uint32_t run_mesh(Ctx& c, uint32_t max_hb) {
+  const uint32_t N = c.cfg.peers;
+  hipStream_t s = c.stream;
+  c.d_until.alloc(c.nnz ? c.nnz : 1);
+  c.d_prop.alloc(c.nnz ? c.nnz : 1);
+  DevBuf<uint32_t> lat;
+  lat.alloc((size_t)c.S * c.S);
+  std::vector<uint32_t> lat32(c.lat_ns.begin(), c.lat_ns.end());
+  GS_HIP(hipMemcpyAsync(lat.p, lat32.data(), lat32.size() * 4, hipMemcpyHostToDevice, s));
+  MeshArgs a{};
+  a.row = c.d_row.p; a.col = c.d_col.p; a.rev = c.d_rev.p; a.flags = c.d_flags.p;
+  a.prop = c.d_prop.p; a.until = c.d_until.p; a.stage = c.d_stage.p; a.lat = lat.p;
+  a.counters = c.d_counters.p; a.seed = c.cfg.seed; a.N = N; a.S = c.S;
+  a.bo = (uint32_t)((c.cfg.backoff_ns + c.cfg.heartbeat_ns - 1) / c.cfg.heartbeat_ns);
+  a.d = c.cfg.d; a.d_lo = c.cfg.d_lo; a.d_hi = c.cfg.d_hi; a.d_out = c.cfg.d_out;
+  if (c.nnz) k_clear_mesh<<<blocks(c.nnz), TB, 0, s>>>(c.nnz, c.d_flags.p, c.d_until.p);
+  GS_HIP(hipMemsetAsync(c.d_counters.p + C_ERR, 0, 8, s));
+  uint32_t epoch = 1, last = 0;
+  uint64_t* h = c.h_pinned;
+  while (epoch <= max_hb) {
+    a.epoch = epoch;
+    GS_HIP(hipMemsetAsync(c.d_prop.p, 0, c.nnz ? c.nnz : 1, s));
+    GS_HIP(hipMemsetAsync(c.d_counters.p + C_MESH_CHANGES, 0, 8, s));
+    k_heartbeat<<<blocks(N), TB, 0, s>>>(a);
+    k_handle_graft<<<blocks(N), TB, 0, s>>>(a);
+    k_apply<<<blocks(N), TB, 0, s>>>(a);
+    GS_HIP(hipGetLastError());
+    GS_HIP(hipMemcpyAsync(h, c.d_counters.p + C_MESH_CHANGES, 8, hipMemcpyDeviceToHost, s));
+    GS_HIP(hipStreamSynchronize(s));
+    last = epoch;
+    if (h[0]) { epoch++; continue; }
+    GS_HIP(hipMemsetAsync(c.d_counters.p + C_MESH_WAKE, 0xFF, 8, s));
+    k_wake<<<blocks(N), TB, 0, s>>>(a);
+    GS_HIP(hipMemcpyAsync(h, c.d_counters.p + C_MESH_WAKE, 8, hipMemcpyDeviceToHost, s));
+    GS_HIP(hipStreamSynchronize(s));
+    if (h[0] == INF64 || h[0] > max_hb) break;
+    epoch = (uint32_t)h[0];
+  }
+  c.d_mesh.alloc((size_t)N * MESH_W);
+  c.d_mcnt.alloc(N);
+  k_extract<<<blocks(N), TB, 0, s>>>(a, c.d_mesh.p, c.d_mcnt.p);
+  GS_HIP(hipGetLastError());
+  GS_HIP(hipMemcpyAsync(h, c.d_counters.p + C_ERR, 8, hipMemcpyDeviceToHost, s));
+  GS_HIP(hipStreamSynchronize(s));
+  if (h[0] & ERR_MESH) c.fail(GS_ERANGE, "mesh row exceeds GS_MESH_W entries");
+  return last;
+}
+
+}  // namespace gs

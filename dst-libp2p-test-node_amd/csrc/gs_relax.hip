@@ -1,0 +1,473 @@
+// gs_relax.hip — eager forwarding + seen-cache + uplink FIFO + reassembly as
+// Delta-stepping frontier relaxation over a batch of concurrent messages.
+//
+// Reference behaviour replaced: publish_new_message
+// (rust-test-node/src/main.rs:101-143) flood-publishes F fragments; each peer's
+// first receipt of a fragment is forwarded to mesh \ {src, publisher}
+// (libp2p-gossipsub forward_msg, upstream) through the peer's uplink FIFO;
+// create_message_handler (main.rs:79-99) completes on the F-th fragment.
+//
+// Layout (HBM): keys[u][m][f] (u64, peer-major, f padded to FP = 2^k) holds
+// key = t_rel_ns << (6+sb) | hops << sb | src; min key wins, so the seen-cache
+// IS the key array and ties break on (time, hops, src) deterministically.
+// Every relaxation adds >= Delta = min latency + min serialisation, so all
+// keys inside the current bucket [lo, lo+Delta) are final: one launch per
+// non-empty bucket scans the keys (coalesced), forwards the bucket's arrivals
+// with 64-bit atomicMin pushes into the same (m,f) slot of the targets, and
+// reduces the next pending key to pick the next bucket on the device
+// (triple-buffered ctrl words; no host round trip per bucket).
+#include "gs_internal.h"
+
+namespace gs {
+namespace {
+
+constexpr int TB = 256;
+
+struct RelaxArgs {
+  uint64_t* keys;
+  uint64_t* busy;
+  const uint32_t* mesh;
+  const uint32_t* pub;
+  const uint8_t* stage;
+  const uint32_t* tables;  // lat[S*S] | ser_up[S] | ser_dn[S]
+  uint64_t* ctrl;
+  uint64_t* counters;
+  uint64_t total;          // N * L lanes
+  uint64_t delta;
+  uint64_t tmax;
+  uint32_t N, B, F, L, S, sb, tshift, launch, idw;
+};
+
+__device__ __forceinline__ uint64_t wave_min(uint64_t v) {
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint64_t x = __shfl_xor(v, off);
+    v = x < v ? x : v;
+  }
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+template <int FP>
+__global__ __launch_bounds__(TB) void k_relax(RelaxArgs a) {
+  __shared__ uint32_t s_lat[MAX_STAGES * MAX_STAGES];
+  __shared__ uint32_t s_su[MAX_STAGES], s_sd[MAX_STAGES];
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.ctrl[(a.launch + 2) % 3] = INF64;
+  const uint64_t cur = a.ctrl[a.launch % 3];
+  if (cur == INF64) return;  // grid-uniform: no pending keys left
+  const uint32_t S = a.S;
+  for (uint32_t i = threadIdx.x; i < S * S; i += TB) s_lat[i] = a.tables[i];
+  if (threadIdx.x < S) {
+    s_su[threadIdx.x] = a.tables[S * S + threadIdx.x];
+    s_sd[threadIdx.x] = a.tables[S * S + S + threadIdx.x];
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd((unsigned long long*)&a.counters[C_BUCKETS], 1ull);
+  const uint64_t lo = ((cur >> a.tshift) / a.delta) * a.delta, hi = lo + a.delta;
+  const uint64_t smask = (1ull << a.sb) - 1;
+  const uint32_t L = a.L;
+  uint64_t nmin = INF64, fd = 0, nr = 0;
+  uint32_t err = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * TB;
+  for (uint64_t base = (uint64_t)blockIdx.x * TB; base < a.total; base += stride) {
+    const uint64_t gid = base + threadIdx.x;
+    const bool valid = gid < a.total;
+    const uint64_t key = valid ? a.keys[gid] : INF64;
+    const uint64_t t = key >> a.tshift;
+    const uint32_t u = valid ? (uint32_t)(gid / L) : 0;
+    const uint32_t slot = (uint32_t)(gid - (uint64_t)u * L);
+    const uint32_t m = slot / FP;
+    const uint32_t pm = valid ? a.pub[m] : EMPTY;
+    const bool pending = key != INF64;
+    const bool active = pending && t >= lo && t < hi && u != pm;
+    if (pending && t >= hi && key < nmin) nmin = key;
+    const uint32_t src = (uint32_t)(key & smask);
+    const uint32_t hp = (uint32_t)((key >> a.sb) & ((1u << HOP_BITS) - 1));
+    const uint32_t su = valid ? a.stage[u] : 0;
+    const uint32_t ser = s_su[su];
+    uint32_t row[MESH_W];
+    uint32_t skip = 0, n = 0;
+    if (active) {
+      const uint4* rp = reinterpret_cast<const uint4*>(a.mesh + (size_t)u * MESH_W);
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint4 x = rp[q];
+        row[4 * q] = x.x; row[4 * q + 1] = x.y; row[4 * q + 2] = x.z; row[4 * q + 3] = x.w;
+      }
+#pragma unroll
+      for (int j = 0; j < (int)MESH_W; j++) {
+        const uint32_t e = row[j];
+        if (e == EMPTY) { skip |= 1u << j; continue; }  // rows are EMPTY-padded at the tail
+        const uint32_t w = e & 0xFFFFFFu;
+        bool sk = (w == src) || (w == pm);
+        if (!sk && a.idw) {  // IDONTWANT from w already here
+          const uint64_t kw = a.keys[(size_t)w * L + slot];
+          sk = kw != INF64 && (kw >> a.tshift) + s_lat[(e >> STAGE_SHIFT) * S + su] <= t;
+        }
+        if (sk) skip |= 1u << j; else n++;
+      }
+    }
+    uint64_t start = t;
+    if constexpr (FP > 1) {
+      // Uplink FIFO across this (u, m)'s fragments: the FP lanes of the group
+      // fold max(t_f, busy) + n_f * ser in key order (all lanes shuffle).
+      const int lane = threadIdx.x & 63, gb = lane & ~(FP - 1);
+      const uint64_t ka = active ? key : INF64;
+      uint64_t kk[FP];
+      uint32_t nn[FP];
+#pragma unroll
+      for (int g = 0; g < FP; g++) { kk[g] = __shfl(ka, gb + g); nn[g] = __shfl(n, gb + g); }
+      int first = -1;
+#pragma unroll
+      for (int g = FP - 1; g >= 0; g--) if (kk[g] != INF64) first = g;
+      if (first >= 0) {
+        uint64_t cb = a.busy[(size_t)u * a.B + m];
+        uint64_t prev = 0;
+#pragma unroll
+        for (int it = 0; it < FP; it++) {
+          uint64_t bk = INF64;
+          uint32_t bn = 0;
+#pragma unroll
+          for (int g = 0; g < FP; g++)
+            if (kk[g] > prev && kk[g] < bk) { bk = kk[g]; bn = nn[g]; }
+          if (bk == INF64) continue;  // nothing left (kept unrollable: no break)
+          const uint64_t tb = bk >> a.tshift;
+          const uint64_t s = tb > cb ? tb : cb;
+          if (active && bk == key) start = s;
+          cb = s + (uint64_t)bn * ser;
+          prev = bk;
+        }
+        if (lane - gb == first) a.busy[(size_t)u * a.B + m] = cb;
+      }
+    }
+    if (active) {
+      fd++;
+      nr += n;
+      if (n && hp + 1 >= (1u << HOP_BITS)) err |= ERR_HOPS;
+      const uint64_t hbits = ((uint64_t)(hp + 1) << a.sb) | u;
+      uint32_t pos = 0;
+#pragma unroll
+      for (int j = 0; j < (int)MESH_W; j++) {
+        if (skip & (1u << j)) continue;
+        const uint32_t e = row[j];
+        const uint32_t w = e & 0xFFFFFFu, sw = e >> STAGE_SHIFT;
+        pos++;
+        const uint32_t sd = s_sd[sw];
+        const uint64_t arr = start + (uint64_t)pos * ser + s_lat[su * S + sw] + (sd > ser ? sd - ser : 0);
+        if (arr > a.tmax) err |= ERR_TIME;
+        const uint64_t nk = (arr << a.tshift) | hbits;
+        atomicMin((unsigned long long*)&a.keys[(size_t)w * L + slot], (unsigned long long)nk);
+        nmin = nk < nmin ? nk : nmin;
+      }
+    }
+  }
+  nmin = wave_min(nmin);
+  fd = wave_sum(fd);
+  nr = wave_sum(nr);
+  for (int off = 32; off > 0; off >>= 1) err |= __shfl_xor(err, off);
+  if ((threadIdx.x & 63) == 0) {
+    if (nmin != INF64) atomicMin((unsigned long long*)&a.ctrl[(a.launch + 1) % 3], (unsigned long long)nmin);
+    if (fd) atomicAdd((unsigned long long*)&a.counters[C_FD], (unsigned long long)fd);
+    if (nr) atomicAdd((unsigned long long*)&a.counters[C_R_FWD], (unsigned long long)nr);
+    if (err) atomicOr((unsigned*)&a.counters[C_ERR], err);
+  }
+}
+
+struct SeedArgs {
+  uint64_t* keys;
+  const uint64_t* row;
+  const uint32_t* col;
+  const uint32_t* mesh;
+  const uint32_t* pub;
+  const uint8_t* stage;
+  const uint32_t* tables;
+  uint64_t* ctrl;
+  uint64_t* counters;
+  uint64_t tmax;
+  uint32_t L, FP, Fe, S, sb, tshift, flood;
+};
+
+// publish_new_message (main.rs:101-143): self key at the publisher and the
+// flood (or mesh) sends of every fragment through its uplink FIFO.
+__global__ __launch_bounds__(TB) void k_seed(SeedArgs a) {
+  const uint32_t m = blockIdx.x, p = a.pub[m], sp = a.stage[p], S = a.S;
+  const uint64_t ser = a.tables[S * S + sp];
+  const uint64_t slot0 = (size_t)p * a.L + (size_t)m * a.FP;
+  if (threadIdx.x < a.Fe) a.keys[slot0 + threadIdx.x] = (uint64_t)p;
+  uint32_t deg;
+  const uint32_t* tg;
+  bool packed;
+  if (a.flood) { deg = (uint32_t)(a.row[p + 1] - a.row[p]); tg = a.col + a.row[p]; packed = false; }
+  else {
+    tg = a.mesh + (size_t)p * MESH_W;
+    deg = 0;
+    while (deg < MESH_W && tg[deg] != EMPTY) deg++;
+    packed = true;
+  }
+  uint64_t nmin = INF64;
+  uint32_t err = 0;
+  const uint32_t total = a.Fe * deg;
+  for (uint32_t i = threadIdx.x; i < total; i += TB) {
+    const uint32_t f = i / deg, j = i % deg;
+    const uint32_t w = packed ? (tg[j] & 0xFFFFFFu) : tg[j];
+    const uint32_t sw = a.stage[w];
+    const uint64_t sd = a.tables[S * S + S + sw];
+    const uint64_t arr = ((uint64_t)f * deg + j + 1) * ser + a.tables[sp * S + sw] + (sd > ser ? sd - ser : 0);
+    if (arr > a.tmax) err |= ERR_TIME;
+    const uint64_t nk = (arr << a.tshift) | (1ull << a.sb) | p;
+    atomicMin((unsigned long long*)&a.keys[(size_t)w * a.L + (size_t)m * a.FP + f], (unsigned long long)nk);
+    nmin = nk < nmin ? nk : nmin;
+  }
+  nmin = wave_min(nmin);
+  for (int off = 32; off > 0; off >>= 1) err |= __shfl_xor(err, off);
+  if ((threadIdx.x & 63) == 0) {
+    if (nmin != INF64) atomicMin((unsigned long long*)&a.ctrl[0], (unsigned long long)nmin);
+    if (err) atomicOr((unsigned*)&a.counters[C_ERR], err);
+  }
+  if (threadIdx.x == 0) atomicAdd((unsigned long long*)&a.counters[C_R], (unsigned long long)total);
+}
+
+struct CompArgs {
+  const uint64_t* keys;
+  const uint32_t* pub;
+  const uint64_t* tpub;
+  uint64_t* tc;     // [B][N]
+  uint8_t* hops;    // [B][N]
+  uint64_t* counters;
+  uint32_t N, B, F, FP, L, sb, tshift, collide;
+};
+
+// Reassembly (main.rs:79-99): completion = max over fragments of the first
+// arrival; transposed through LDS so both the key reads (peer-major) and the
+// result writes (message-major) are coalesced.
+__global__ __launch_bounds__(TB) void k_complete(CompArgs a) {
+  __shared__ uint64_t s_tc[64][65];
+  __shared__ uint8_t s_h[64][68];
+  const uint32_t u0 = blockIdx.x * 64, m0 = blockIdx.y * 64;
+  const uint32_t nu = min(64u, a.N - u0), nm = min(64u, a.B - m0);
+  uint64_t deliv = 0, lsum = 0, lmax = 0;
+  for (uint32_t i = threadIdx.x; i < nu * nm; i += TB) {
+    const uint32_t pu = i / nm, qm = i % nm, u = u0 + pu, m = m0 + qm;
+    const uint64_t* kp = a.keys + (size_t)u * a.L + (size_t)m * a.FP;
+    uint64_t tc = INF64;
+    uint8_t h = 0xFF;
+    if (u == a.pub[m]) { tc = a.tpub[m]; h = 0; }
+    else if (!a.collide) {
+      uint64_t mk = 0;
+      bool ok = true;
+      for (uint32_t f = 0; f < a.F; f++) {
+        const uint64_t k = kp[f];
+        ok &= k != INF64;
+        mk = k > mk ? k : mk;
+      }
+      if (ok) {
+        const uint64_t trel = mk >> a.tshift;
+        tc = a.tpub[m] + trel;
+        h = (uint8_t)((mk >> a.sb) & ((1u << HOP_BITS) - 1));
+        const uint64_t ms = trel / 1000000ull;
+        deliv++;
+        lsum += ms;
+        lmax = ms > lmax ? ms : lmax;
+      }
+    }
+    s_tc[qm][pu] = tc;
+    s_h[qm][pu] = h;
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nm * 64; i += TB) {
+    const uint32_t qm = i >> 6, pu = i & 63;
+    if (pu < nu) {
+      a.tc[(size_t)(m0 + qm) * a.N + u0 + pu] = s_tc[qm][pu];
+      a.hops[(size_t)(m0 + qm) * a.N + u0 + pu] = s_h[qm][pu];
+    }
+  }
+  deliv = wave_sum(deliv);
+  lsum = wave_sum(lsum);
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint64_t x = __shfl_xor(lmax, off);
+    lmax = x > lmax ? x : lmax;
+  }
+  if ((threadIdx.x & 63) == 0 && deliv) {
+    atomicAdd((unsigned long long*)&a.counters[C_DELIV], (unsigned long long)deliv);
+    atomicAdd((unsigned long long*)&a.counters[C_LAT_SUM], (unsigned long long)lsum);
+    atomicMax((unsigned long long*)&a.counters[C_LAT_MAX], (unsigned long long)lmax);
+  }
+}
+
+template <int FP>
+void launch_relax(const RelaxArgs& a, unsigned grid, hipStream_t s) {
+  k_relax<FP><<<grid, TB, 0, s>>>(a);
+}
+
+void relax_dispatch(uint32_t FP, const RelaxArgs& a, unsigned grid, hipStream_t s) {
+  switch (FP) {
+    case 1: launch_relax<1>(a, grid, s); break;
+    case 2: launch_relax<2>(a, grid, s); break;
+    case 4: launch_relax<4>(a, grid, s); break;
+    case 8: launch_relax<8>(a, grid, s); break;
+    default: launch_relax<16>(a, grid, s); break;
+  }
+}
+
+uint32_t pow2_at_least(uint32_t x) { uint32_t p = 1; while (p < x) p <<= 1; return p; }
+
+}  // namespace
+
+void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_result_sink* sink) {
+  const uint32_t N = c.cfg.peers, F = c.cfg.fragments, FP = pow2_at_least(F);
+  const uint32_t Bmax = c.cfg.batch, S = c.S;
+  hipStream_t s = c.stream;
+  const uint32_t sb = bits_for(N), tshift = sb + HOP_BITS;
+  const uint64_t tmax = tshift >= 64 ? 0 : (INF64 >> tshift);
+  GS_HIP(hipMemsetAsync(c.d_counters.p + C_ERR, 0, 8, s));
+  for (uint64_t i = 0; i < n_msgs; i++) {
+    if (sched[i].publisher >= N) c.fail(GS_EINVAL, "publisher id out of range");
+    if (sched[i].msg_size / F < 8)  // main.rs:110-111 slices buffer[..8]
+      c.fail(GS_EINVAL, "fragment payload shorter than the 8-byte tx_time stamp");
+  }
+  c.d_keys.alloc((size_t)N * Bmax * FP);
+  if (FP > 1) c.d_busy.alloc((size_t)N * Bmax);
+  c.d_pub.alloc(Bmax);
+  c.d_tpub.alloc(Bmax);
+  c.d_tc.alloc((size_t)N * Bmax);
+  c.d_hops.alloc((size_t)N * Bmax);
+  c.d_tables.alloc((size_t)S * S + 2 * S);
+  std::vector<uint32_t> pub(Bmax), tab((size_t)S * S + 2 * S);
+  std::vector<uint64_t> tpub(Bmax);
+  // Timing events come from a per-context pool: [0] run start, [1] run end,
+  // then one (start, end) pair around every relaxation launch.
+  size_t n_ev = 0;
+  auto ev = [&](size_t i) {
+    while (c.ev_pool.size() <= i) {
+      hipEvent_t e;
+      GS_HIP(hipEventCreate(&e));
+      c.ev_pool.push_back(e);
+    }
+    return c.ev_pool[i];
+  };
+  if (c.timing) {
+    GS_HIP(hipEventRecord(ev(0), s));
+    ev(1);
+    n_ev = 2;
+  }
+  if (c.num_cus == 0) {
+    hipDeviceProp_t prop;
+    c.num_cus = hipGetDeviceProperties(&prop, c.cfg.device) == hipSuccess ? prop.multiProcessorCount : 256;
+  }
+  const int dev_cus = c.num_cus;
+  uint64_t i0 = 0;
+  while (i0 < n_msgs) {
+    // a batch: up to B messages of equal size (serialisation tables are per batch)
+    uint64_t i1 = i0 + 1;
+    while (i1 < n_msgs && i1 - i0 < Bmax && sched[i1].msg_size == sched[i0].msg_size) i1++;
+    const uint32_t B = (uint32_t)(i1 - i0), L = B * FP;
+    const uint64_t payload = sched[i0].msg_size / F;
+    const bool collide = F > 1 && payload <= 10;  // defect D8
+    const uint64_t wire = gs_wire_bytes(payload, c.cfg.muxer, c.cfg.signed_msgs);
+    uint64_t min_lat = INF64, min_ser = INF64;
+    for (uint32_t a = 0; a < S; a++)
+      for (uint32_t b = 0; b < S; b++) {
+        if (c.lat_ns[(size_t)a * S + b] >= (1ull << 32)) c.fail(GS_ERANGE, "latency >= 2^32 ns");
+        tab[(size_t)a * S + b] = (uint32_t)c.lat_ns[(size_t)a * S + b];
+        min_lat = std::min<uint64_t>(min_lat, c.lat_ns[(size_t)a * S + b]);
+      }
+    for (uint32_t a = 0; a < S; a++) {
+      const uint64_t up = ser_ns(wire, c.bw_up[a]), dn = ser_ns(wire, c.bw_dn[a]);
+      if (up >= (1ull << 32) || dn >= (1ull << 32)) c.fail(GS_ERANGE, "serialisation >= 2^32 ns");
+      tab[(size_t)S * S + a] = (uint32_t)up;
+      tab[(size_t)S * S + S + a] = (uint32_t)dn;
+      min_ser = std::min(min_ser, up);
+    }
+    const uint64_t delta = std::max<uint64_t>(1, min_lat + min_ser);
+    for (uint32_t q = 0; q < B; q++) { pub[q] = sched[i0 + q].publisher; tpub[q] = sched[i0 + q].t_pub_ns; }
+    GS_HIP(hipMemcpyAsync(c.d_pub.p, pub.data(), B * 4, hipMemcpyHostToDevice, s));
+    GS_HIP(hipMemcpyAsync(c.d_tpub.p, tpub.data(), B * 8, hipMemcpyHostToDevice, s));
+    GS_HIP(hipMemcpyAsync(c.d_tables.p, tab.data(), tab.size() * 4, hipMemcpyHostToDevice, s));
+    const uint64_t total = (uint64_t)N * L;
+    GS_HIP(hipMemsetAsync(c.d_keys.p, 0xFF, total * 8, s));
+    if (FP > 1) GS_HIP(hipMemsetAsync(c.d_busy.p, 0, (size_t)N * B * 8, s));
+    GS_HIP(hipMemsetAsync(c.d_ctrl.p, 0xFF, 4 * 8, s));
+
+    SeedArgs sa{};
+    sa.keys = c.d_keys.p; sa.row = c.d_row.p; sa.col = c.d_col.p; sa.mesh = c.d_mesh.p;
+    sa.pub = c.d_pub.p; sa.stage = c.d_stage.p; sa.tables = c.d_tables.p; sa.ctrl = c.d_ctrl.p;
+    sa.counters = c.d_counters.p; sa.tmax = tmax; sa.L = L; sa.FP = FP; sa.Fe = collide ? 1 : F;
+    sa.S = S; sa.sb = sb; sa.tshift = tshift; sa.flood = c.cfg.flood_publish;
+    k_seed<<<B, TB, 0, s>>>(sa);
+    GS_HIP(hipGetLastError());
+
+    RelaxArgs ra{};
+    ra.keys = c.d_keys.p; ra.busy = c.d_busy.p; ra.mesh = c.d_mesh.p; ra.pub = c.d_pub.p;
+    ra.stage = c.d_stage.p; ra.tables = c.d_tables.p; ra.ctrl = c.d_ctrl.p;
+    ra.counters = c.d_counters.p; ra.total = total; ra.delta = delta; ra.tmax = tmax;
+    ra.N = N; ra.B = B; ra.F = F; ra.L = L; ra.S = S; ra.sb = sb; ra.tshift = tshift;
+    ra.idw = (c.cfg.idontwant && payload >= c.cfg.idontwant) ? 1 : 0;
+    const uint64_t need = (total + TB - 1) / TB;
+    const unsigned grid = (unsigned)std::min<uint64_t>(need, (uint64_t)dev_cus * 16);
+    uint32_t launch = 0;
+    const uint32_t chunk = 8;
+    for (;;) {
+      for (uint32_t q = 0; q < chunk; q++) {
+        ra.launch = launch++;
+        if (c.timing) {
+          GS_HIP(hipEventRecord(ev(n_ev), s));
+          relax_dispatch(FP, ra, grid, s);
+          GS_HIP(hipEventRecord(ev(n_ev + 1), s));
+          n_ev += 2;
+        } else {
+          relax_dispatch(FP, ra, grid, s);
+        }
+      }
+      GS_HIP(hipGetLastError());
+      GS_HIP(hipMemcpyAsync(c.h_pinned, c.d_ctrl.p, 3 * 8, hipMemcpyDeviceToHost, s));
+      GS_HIP(hipStreamSynchronize(s));
+      if (c.h_pinned[launch % 3] == INF64) break;
+    }
+    c.stats.relax_launches += launch;
+
+    CompArgs ca{};
+    ca.keys = c.d_keys.p; ca.pub = c.d_pub.p; ca.tpub = c.d_tpub.p; ca.tc = c.d_tc.p;
+    ca.hops = c.d_hops.p; ca.counters = c.d_counters.p; ca.N = N; ca.B = B; ca.F = F;
+    ca.FP = FP; ca.L = L; ca.sb = sb; ca.tshift = tshift; ca.collide = collide ? 1 : 0;
+    dim3 cg((N + 63) / 64, (B + 63) / 64);
+    k_complete<<<cg, TB, 0, s>>>(ca);
+    GS_HIP(hipGetLastError());
+    if (sink && sink->t_complete_ns)
+      GS_HIP(hipMemcpyAsync(sink->t_complete_ns + i0 * N, c.d_tc.p, (size_t)B * N * 8,
+                            hipMemcpyDeviceToHost, s));
+    if (sink && sink->hops)
+      GS_HIP(hipMemcpyAsync(sink->hops + i0 * N, c.d_hops.p, (size_t)B * N, hipMemcpyDeviceToHost, s));
+    c.stats.messages += B;
+    i0 = i1;
+  }
+  if (c.timing) GS_HIP(hipEventRecord(ev(1), s));
+  GS_HIP(hipMemcpyAsync(c.h_pinned, c.d_counters.p, C_COUNT * 8, hipMemcpyDeviceToHost, s));
+  GS_HIP(hipStreamSynchronize(s));
+  const uint64_t* h = c.h_pinned;
+  if (h[C_ERR] & ERR_TIME) c.fail(GS_ERANGE, "relative arrival time overflowed the key's time field");
+  if (h[C_ERR] & ERR_HOPS) c.fail(GS_ERANGE, "hop count overflowed the key's 6-bit hop field");
+  c.stats.frag_deliveries = h[C_FD];
+  c.stats.relaxations = h[C_R] + h[C_R_FWD];
+  c.stats.deliveries = h[C_DELIV];
+  c.stats.latency_sum_ms = h[C_LAT_SUM];
+  c.stats.latency_max_ms = h[C_LAT_MAX];
+  c.stats.buckets = h[C_BUCKETS];
+  c.stats.bytes_alg = 16 * h[C_FD] + 12 * c.stats.relaxations + 8 * h[C_DELIV];
+  c.stats.relax_bytes_alg = 16 * h[C_FD] + 12 * h[C_R_FWD];
+  if (c.timing) {
+    double ms = 0;
+    for (size_t q = 2; q + 1 < n_ev; q += 2) {
+      float x = 0;
+      GS_HIP(hipEventElapsedTime(&x, c.ev_pool[q], c.ev_pool[q + 1]));
+      ms += x;
+    }
+    c.stats.relax_ms += ms;
+    float rm = 0;
+    GS_HIP(hipEventElapsedTime(&rm, c.ev_pool[0], c.ev_pool[1]));
+    c.stats.run_ms += rm;
+  }
+}
+
+}  // namespace gs

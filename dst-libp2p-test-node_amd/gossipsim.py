@@ -1,0 +1,320 @@
+"""Python host mirror of the reference's test-node interface over libgossipsim.so.
+
+The reference node (rust-test-node/src/main.rs) reads its knobs from the env
+(env.rs:27-87), dials random peers (main.rs:303-389), accepts
+`POST /publish {"topic","msgSize","version"}` (main.rs:50-56,146-221) and
+prints `<tx_time> milliseconds: <latency>` per completed message (main.rs:93).
+This module keeps those names and error behaviour on top of the C ABI in
+include/gossipsim.h:
+
+    cfg = PeerConfig.from_env()          # env.rs get_peer_details
+    sim = Simulator(cfg)                 # SwarmBuilder + build_behaviour
+    sim.set_topogen_links(...)           # shadow/topogen.py link graph
+    sim.connect_gossipsub_peers()        # main.rs:303-389 -> CSR on the GPU
+    sim.mesh_converge()                  # heartbeat GRAFT/PRUNE fixed point
+    sim.publish(publisher, msg_size, t)  # POST /publish
+    res = sim.run()                      # receive/forward/reassemble on the GPU
+    sim.write_latency_log(path, res)     # awk-parseable arrival lines
+
+Everything here is plumbing; all simulation work runs in the HIP library. The
+library must be present: there is no CPU fallback (a missing .so raises).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GOSSIPSIM_LIB", os.path.join(HERE, "libgossipsim.so"))
+ABI_VERSION = 1
+MESH_W = 16
+UNDELIVERED = np.uint64(0xFFFFFFFFFFFFFFFF)
+MUXERS = {"yamux": 0, "quic": 1, "mplex": 2}
+STATUS = {0: "GS_OK", -1: "GS_EINVAL", -2: "GS_ENOMEM", -3: "GS_EDEVICE", -4: "GS_ESTATE",
+          -5: "GS_ERANGE", -6: "GS_EUNSUPPORTED"}
+
+u32, u64, i32, u8 = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32, ctypes.c_uint8
+P = ctypes.POINTER
+
+
+class GsConfig(ctypes.Structure):
+    _fields_ = [(n, u32) for n in (
+        "abi_version", "peers", "connect_to", "dial_extra", "max_connections", "fragments",
+        "muxer", "signed_msgs", "d", "d_lo", "d_hi", "d_lazy", "d_out", "gossip_factor_milli")] + [
+        ("heartbeat_ns", u64), ("backoff_ns", u64)] + [
+        (n, u32) for n in ("flood_publish", "idontwant", "lazy_gossip", "self_log")] + [
+        ("seed", u64), ("device", i32), ("batch", u32)]
+
+
+class GsPublish(ctypes.Structure):
+    _fields_ = [("t_pub_ns", u64), ("publisher", u32), ("msg_size", u32)]
+
+
+class GsResultSink(ctypes.Structure):
+    _fields_ = [("t_complete_ns", P(u64)), ("hops", P(u8))]
+
+
+class GsStats(ctypes.Structure):
+    _fields_ = [(n, u64) for n in (
+        "messages", "deliveries", "frag_deliveries", "relaxations", "bytes_alg",
+        "latency_sum_ms", "latency_max_ms", "relax_launches", "buckets")] + [
+        ("relax_ms", ctypes.c_double), ("run_ms", ctypes.c_double), ("relax_bytes_alg", u64)]
+
+
+# Every symbol include/gossipsim.h declares, with its ctypes signature.
+SIGNATURES = {
+    "gs_config_default": (None, [P(GsConfig)]),
+    "gs_config_from_env": (i32, [P(GsConfig), ctypes.c_char_p, ctypes.c_size_t]),
+    "gs_wire_bytes": (u64, [u64, u32, u32]),
+    "gs_topogen_links": (i32, [u32, u32, u32, u32, u32, u32, P(u64), P(u64)]),
+    "gs_schedule_runsh": (i32, [u32, u32, u32, u32, u64, u64, u32, P(GsPublish)]),
+    "gs_write_latency_log": (i32, [ctypes.c_char_p, P(GsPublish), u64, u32, P(u64), u32]),
+    "gs_create": (i32, [P(GsConfig), P(ctypes.c_void_p)]),
+    "gs_destroy": (i32, [ctypes.c_void_p]),
+    "gs_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
+    "gs_set_links": (i32, [ctypes.c_void_p, u32, P(u64), P(u64), P(u64), P(u8)]),
+    "gs_build_topology": (i32, [ctypes.c_void_p]),
+    "gs_graph_info": (i32, [ctypes.c_void_p, P(u32), P(u64), P(u32)]),
+    "gs_get_csr": (i32, [ctypes.c_void_p, P(u64), P(u32), P(u8)]),
+    "gs_mesh_converge": (i32, [ctypes.c_void_p, u32, P(u32)]),
+    "gs_get_mesh": (i32, [ctypes.c_void_p, P(u32), P(u8)]),
+    "gs_run": (i32, [ctypes.c_void_p, P(GsPublish), u64, P(GsResultSink)]),
+    "gs_get_stats": (i32, [ctypes.c_void_p, P(GsStats)]),
+    "gs_reset_stats": (i32, [ctypes.c_void_p]),
+    "gs_set_timing": (i32, [ctypes.c_void_p, u32]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libgossipsim.so; raise if it is missing (no fallback path exists)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("libgossipsim.so not built at %s: run __graft_entry__.build() "
+                               "(make -C dst-libp2p-test-node_amd)" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+class GossipSimError(RuntimeError):
+    def __init__(self, status, msg):
+        super().__init__("%s (%d): %s" % (STATUS.get(status, "?"), status, msg))
+        self.status = status
+
+
+def _ptr(a, ct):
+    return a.ctypes.data_as(P(ct))
+
+
+def wire_bytes(payload, muxer="yamux", signed=True):
+    return int(lib().gs_wire_bytes(payload, MUXERS[muxer] if isinstance(muxer, str) else muxer,
+                                   1 if signed else 0))
+
+
+def topogen_links(stages=1, min_bw=50, max_bw=50, min_lat=100, max_lat=100, shortest=False):
+    """shadow/topogen.py:39-71 -> (lat_ns[S,S], bw_bps[S]); defaults = topogen.py:15-20."""
+    lat = np.zeros(stages * stages, np.uint64)
+    bw = np.zeros(stages, np.uint64)
+    rc = lib().gs_topogen_links(stages, min_bw, max_bw, min_lat, max_lat, 1 if shortest else 0,
+                                _ptr(lat, u64), _ptr(bw, u64))
+    if rc:
+        raise GossipSimError(rc, "invalid topogen parameters")
+    return lat.reshape(stages, stages), bw
+
+
+def schedule_runsh(n_msgs, peers, publisher_id, rotation, t0_ns, delay_ns, msg_size):
+    """shadow/run.sh:34-36 publisher/rotation/delay -> structured schedule array."""
+    out = (GsPublish * n_msgs)()
+    rc = lib().gs_schedule_runsh(n_msgs, peers, publisher_id, rotation, t0_ns, delay_ns, msg_size,
+                                 out)
+    if rc:
+        raise GossipSimError(rc, "invalid schedule")
+    return out
+
+
+# Schedule constants of the benchmark workload: Shadow epoch 2000-01-01 plus the
+# injector start (shadow/topogen.py:130), 1000 ms spacing and publisher
+# (6 + i) mod N with rotation (shadow/README.md:57, run.sh:34-36).
+T0_NS = 946684800_000_000_000 + 500_000_000_000
+DELAY_NS = 1_000_000_000
+PUBLISHER0 = 6
+
+
+def shard_messages(step, rank, world, batch, peers, msg_size):
+    """Message-batch sharding across ranks: global message index
+    (step*world + rank)*batch + q; messages are independent given the frozen mesh,
+    so ranks share nothing on the data path."""
+    idx = (np.uint64(step) * np.uint64(world) + np.uint64(rank)) * np.uint64(batch) + \
+        np.arange(batch, dtype=np.uint64)
+    t = np.uint64(T0_NS) + idx * np.uint64(DELAY_NS)
+    pub = ((np.uint64(PUBLISHER0) + idx) % np.uint64(peers)).astype(np.uint32)
+    return t, pub, np.full(batch, msg_size, np.uint32)
+
+
+class PeerConfig:
+    """Knobs of env.rs:14-25 + gossipsub ConfigBuilder (main.rs:223-241)."""
+
+    def __init__(self, **kw):
+        self.c = GsConfig()
+        lib().gs_config_default(ctypes.byref(self.c))
+        for k, v in kw.items():
+            if k == "muxer" and isinstance(v, str):
+                v = MUXERS[v]
+            if not hasattr(self.c, k):
+                raise AttributeError("unknown knob %s" % k)
+            setattr(self.c, k, v)
+
+    @classmethod
+    def from_env(cls):
+        """get_peer_details (env.rs:27-87): same env names and validation errors."""
+        self = cls()
+        err = ctypes.create_string_buffer(256)
+        rc = lib().gs_config_from_env(ctypes.byref(self.c), err, 256)
+        if rc:
+            raise GossipSimError(rc, err.value.decode())
+        return self
+
+    def __getattr__(self, k):
+        if k == "c":
+            raise AttributeError(k)
+        return getattr(self.c, k)
+
+
+class Simulator:
+    """One context = one HIP device (include/gossipsim.h threading rules)."""
+
+    def __init__(self, cfg=None, **kw):
+        self.cfg = cfg if cfg is not None else PeerConfig(**kw)
+        self.ctx = ctypes.c_void_p()
+        rc = lib().gs_create(ctypes.byref(self.cfg.c), ctypes.byref(self.ctx))
+        if rc:
+            raise GossipSimError(rc, "gs_create failed")
+        self.peers = self.cfg.c.peers
+        self._sched = []
+
+    def _check(self, rc):
+        if rc:
+            raise GossipSimError(rc, lib().gs_last_error(self.ctx).decode())
+
+    def close(self):
+        if self.ctx:
+            lib().gs_destroy(self.ctx)
+            self.ctx = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- links / topology / mesh ----
+    def set_links(self, lat_ns, bw_up, bw_down=None, stage_of_peer=None):
+        lat = np.ascontiguousarray(np.asarray(lat_ns, np.uint64).reshape(-1))
+        S = int(round(len(lat) ** 0.5))
+        up = np.ascontiguousarray(bw_up, np.uint64)
+        dn = np.ascontiguousarray(bw_up if bw_down is None else bw_down, np.uint64)
+        st = None if stage_of_peer is None else np.ascontiguousarray(stage_of_peer, np.uint8)
+        self._check(lib().gs_set_links(self.ctx, S, _ptr(lat, u64), _ptr(up, u64), _ptr(dn, u64),
+                                       None if st is None else _ptr(st, u8)))
+        self._links = (lat, up, dn, st)
+
+    def set_topogen_links(self, stages=1, min_bw=50, max_bw=50, min_lat=100, max_lat=100,
+                          shortest=False):
+        lat, bw = topogen_links(stages, min_bw, max_bw, min_lat, max_lat, shortest)
+        self.set_links(lat, bw, bw)
+        return lat, bw
+
+    def connect_gossipsub_peers(self):
+        """main.rs:303-389: random ID dialing -> CSR (device resident)."""
+        self._check(lib().gs_build_topology(self.ctx))
+
+    build_topology = connect_gossipsub_peers
+
+    def graph_info(self):
+        n, nnz, md = u32(), u64(), u32()
+        self._check(lib().gs_graph_info(self.ctx, ctypes.byref(n), ctypes.byref(nnz),
+                                        ctypes.byref(md)))
+        return n.value, nnz.value, md.value
+
+    def csr(self):
+        _, nnz, _ = self.graph_info()
+        row = np.zeros(self.peers + 1, np.uint64)
+        col = np.zeros(max(nnz, 1), np.uint32)
+        flags = np.zeros(max(nnz, 1), np.uint8)
+        self._check(lib().gs_get_csr(self.ctx, _ptr(row, u64), _ptr(col, u32), _ptr(flags, u8)))
+        return row, col[:nnz], flags[:nnz]
+
+    def mesh_converge(self, max_heartbeats=400):
+        ep = u32()
+        self._check(lib().gs_mesh_converge(self.ctx, max_heartbeats, ctypes.byref(ep)))
+        return ep.value
+
+    def mesh(self):
+        m = np.zeros(self.peers * MESH_W, np.uint32)
+        c = np.zeros(self.peers, np.uint8)
+        self._check(lib().gs_get_mesh(self.ctx, _ptr(m, u32), _ptr(c, u8)))
+        return m.reshape(self.peers, MESH_W), c
+
+    # ---- publish / run ----
+    def publish(self, publisher, msg_size, t_pub_ns):
+        """POST /publish (main.rs:152-168): queue one injection."""
+        if not 0 <= publisher < self.peers:
+            raise GossipSimError(-1, "publisher out of range")
+        self._sched.append((int(t_pub_ns), int(publisher), int(msg_size)))
+
+    def run(self, schedule=None, collect=True):
+        """Simulate the queued publishes (or `schedule`); returns t_complete/hops [M, N]."""
+        if schedule is None:
+            schedule = (GsPublish * len(self._sched))(*[GsPublish(*r) for r in self._sched])
+            self._sched = []
+        elif not isinstance(schedule, ctypes.Array):
+            t, p, s = schedule
+            arr = (GsPublish * len(t))()
+            for i in range(len(t)):
+                arr[i] = GsPublish(int(t[i]), int(p[i]), int(s[i]))
+            schedule = arr
+        M = len(schedule)
+        res = {"schedule": schedule}
+        if collect:
+            tc = np.zeros(M * self.peers, np.uint64)
+            hops = np.zeros(M * self.peers, np.uint8)
+            sink = GsResultSink(_ptr(tc, u64), _ptr(hops, u8))
+            self._check(lib().gs_run(self.ctx, schedule, M, ctypes.byref(sink)))
+            res["t_complete"] = tc.reshape(M, self.peers)
+            res["hops"] = hops.reshape(M, self.peers)
+        else:
+            self._check(lib().gs_run(self.ctx, schedule, M, None))
+        return res
+
+    def stats(self):
+        st = GsStats()
+        self._check(lib().gs_get_stats(self.ctx, ctypes.byref(st)))
+        return {n: getattr(st, n) for n, _ in GsStats._fields_}
+
+    def reset_stats(self):
+        self._check(lib().gs_reset_stats(self.ctx))
+
+    def set_timing(self, on=True):
+        self._check(lib().gs_set_timing(self.ctx, 1 if on else 0))
+
+    def write_latency_log(self, path, res):
+        """Arrival lines as `grep -rne 'milliseconds\\|BW' shadow.data/` prints them."""
+        sched = res["schedule"]
+        tc = np.ascontiguousarray(res["t_complete"], np.uint64)
+        rc = lib().gs_write_latency_log(path.encode(), sched, len(sched), self.peers,
+                                        _ptr(tc, u64), self.cfg.c.self_log)
+        if rc:
+            raise GossipSimError(rc, "gs_write_latency_log failed")

@@ -1,0 +1,115 @@
+// gossipsim-node — C++ host CLI standing in for the reference experiment:
+// the env surface of rust-test-node (src/env.rs:27-87), topogen.py's link
+// graph parameters (shadow/topogen.py:13-36), run.sh's publish schedule
+// (shadow/run.sh:23-36) in place of the HTTP injector, and the arrival log
+// that shadow/summary_latency*.awk parse (main.rs:93, run.sh:61).
+//
+//   PEERS=1000 CONNECTTO=10 FRAGMENTS=1 MUXER=yamux \
+//   ./gossipsim-node -bl 50 -bh 150 -ll 40 -lh 130 -st 5 -s 15000 -m 10 \
+//       --publisher 6 --rotation 1 --delay-ms 1000 --latencies latencies1
+//   awk -f summary_latency_large.awk latencies1
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/gossipsim.h"
+
+namespace {
+
+void usage() {
+  fprintf(stderr,
+          "usage: gossipsim-node [-bl MBIT] [-bh MBIT] [-ll MS] [-lh MS] [-st STAGES] [--shortest]\n"
+          "         [-s MSG_BYTES] [-m MESSAGES] [--publisher ID] [--rotation 0|1]\n"
+          "         [--delay-ms MS] [--t0-s SECONDS] [--max-heartbeats H] [--latencies PATH]\n"
+          "env: PEERS CONNECTTO FRAGMENTS MUXER MAXCONNECTIONS GOSSIPSUB_* SELFTRIGGER GS_SEED GS_BATCH GS_DEVICE\n");
+}
+
+int die(gs_ctx* ctx, gs_status st, const char* what) {
+  fprintf(stderr, "%s failed (%d): %s\n", what, st, ctx ? gs_last_error(ctx) : "");
+  if (ctx) gs_destroy(ctx);
+  return 1;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  // topogen.py defaults (topogen.py:15-26) and run.sh's fixed publisher knobs
+  uint32_t bl = 50, bh = 50, ll = 100, lh = 100, stages = 1, mode = GS_LINKS_DIRECT;
+  uint32_t msg_size = 1500, n_msgs = 10, publisher = 6, rotation = 1, max_hb = 400;
+  uint64_t delay_ms = 1000, t0_s = 946684800ull + 500ull;  // Shadow epoch + injector start
+  std::string latencies;
+  for (int i = 1; i < argc; i++) {
+    std::string a = argv[i];
+    auto next = [&](void) -> const char* {
+      if (i + 1 >= argc) { usage(); exit(2); }
+      return argv[++i];
+    };
+    if (a == "-bl") bl = (uint32_t)atoi(next());
+    else if (a == "-bh") bh = (uint32_t)atoi(next());
+    else if (a == "-ll") ll = (uint32_t)atoi(next());
+    else if (a == "-lh") lh = (uint32_t)atoi(next());
+    else if (a == "-st") stages = (uint32_t)atoi(next());
+    else if (a == "--shortest") mode = GS_LINKS_SHORTEST;
+    else if (a == "-s") msg_size = (uint32_t)atoi(next());
+    else if (a == "-m") n_msgs = (uint32_t)atoi(next());
+    else if (a == "--publisher") publisher = (uint32_t)atoi(next());
+    else if (a == "--rotation") rotation = (uint32_t)atoi(next());
+    else if (a == "--delay-ms") delay_ms = strtoull(next(), nullptr, 10);
+    else if (a == "--t0-s") t0_s = strtoull(next(), nullptr, 10);
+    else if (a == "--max-heartbeats") max_hb = (uint32_t)atoi(next());
+    else if (a == "--latencies") latencies = next();
+    else { usage(); return 2; }
+  }
+  gs_config cfg;
+  gs_config_default(&cfg);
+  char err[256] = {0};
+  gs_status st = gs_config_from_env(&cfg, err, sizeof(err));
+  if (st != GS_OK) { fprintf(stderr, "Error reading peer settings: %s\n", err); return 1; }
+
+  std::vector<uint64_t> lat((size_t)stages * stages), bw(stages);
+  st = gs_topogen_links(stages, bl, bh, ll, lh, mode, lat.data(), bw.data());
+  if (st != GS_OK) { fprintf(stderr, "invalid topogen parameters\n"); return 1; }
+
+  gs_ctx* ctx = nullptr;
+  if ((st = gs_create(&cfg, &ctx)) != GS_OK) return die(nullptr, st, "gs_create");
+  if ((st = gs_set_links(ctx, stages, lat.data(), bw.data(), bw.data(), nullptr)) != GS_OK)
+    return die(ctx, st, "gs_set_links");
+  if ((st = gs_build_topology(ctx)) != GS_OK) return die(ctx, st, "gs_build_topology");
+  uint32_t epochs = 0;
+  if ((st = gs_mesh_converge(ctx, max_hb, &epochs)) != GS_OK) return die(ctx, st, "gs_mesh_converge");
+
+  std::vector<gs_publish> sched(n_msgs);
+  gs_schedule_runsh(n_msgs, cfg.peers, publisher, rotation, t0_s * 1000000000ull,
+                    delay_ms * 1000000ull, msg_size, sched.data());
+  std::vector<uint64_t> tc((size_t)n_msgs * cfg.peers);
+  gs_result_sink sink{tc.data(), nullptr};
+  if ((st = gs_run(ctx, sched.data(), n_msgs, &sink)) != GS_OK) return die(ctx, st, "gs_run");
+  gs_stats s;
+  gs_get_stats(ctx, &s);
+
+  std::vector<uint64_t> ms;
+  ms.reserve(s.deliveries);
+  for (uint32_t m = 0; m < n_msgs; m++)
+    for (uint32_t u = 0; u < cfg.peers; u++) {
+      const uint64_t t = tc[(size_t)m * cfg.peers + u];
+      if (t != GS_UNDELIVERED && u != sched[m].publisher) ms.push_back((t - sched[m].t_pub_ns) / 1000000ull);
+    }
+  std::sort(ms.begin(), ms.end());
+  auto pct = [&](double q) { return ms.empty() ? 0 : ms[std::min(ms.size() - 1, (size_t)(q * (ms.size() - 1)))]; };
+  fprintf(stderr,
+          "peers=%u mesh_epochs=%u messages=%llu deliveries=%llu frag_deliveries=%llu "
+          "relaxations=%llu latency_ms p50=%llu p95=%llu max=%llu\n",
+          cfg.peers, epochs, (unsigned long long)s.messages, (unsigned long long)s.deliveries,
+          (unsigned long long)s.frag_deliveries, (unsigned long long)s.relaxations,
+          (unsigned long long)pct(0.5), (unsigned long long)pct(0.95), (unsigned long long)pct(1.0));
+  if (!latencies.empty() &&
+      (st = gs_write_latency_log(latencies.c_str(), sched.data(), n_msgs, cfg.peers, tc.data(),
+                                 cfg.self_log)) != GS_OK)
+    return die(ctx, st, "gs_write_latency_log");
+  gs_destroy(ctx);
+  return 0;
+}

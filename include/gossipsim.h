@@ -1,0 +1,204 @@
+/*
+ * gossipsim.h — C ABI of the MI355X-native GossipSub dissemination simulator.
+ *
+ * This is the drop-in boundary for the reference's hot path: message
+ * dissemination across the GossipSub peer mesh of vacp2p/dst-libp2p-test-node.
+ * In the reference that path sits behind rust-libp2p's NetworkBehaviour
+ * (libp2p-gossipsub 0.49.2, not vendored; pinned at
+ * rust-test-node/Cargo.lock:1640) and is driven by rust-test-node/src/main.rs.
+ * Every entry point below names the reference interface it replaces.
+ *
+ * Conventions
+ *  - Plain C: fixed-width integers, plain pointers and sizes, no C++ types.
+ *  - Every call returns gs_status (0 = OK, negative = error); the message of the
+ *    last failure is available from gs_last_error(ctx). No exception crosses
+ *    the ABI.
+ *  - The caller owns every host array it passes in; the library owns the
+ *    device buffers of a context.
+ *  - A context is bound to ONE HIP device and is not thread-safe: use one host
+ *    thread per context. Multi-GPU = one context per GPU, each simulating its
+ *    own message shard (message batches are independent).
+ *  - All simulated times are integer nanoseconds.
+ */
+#ifndef GOSSIPSIM_H
+#define GOSSIPSIM_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GS_ABI_VERSION 1u
+
+/* Sentinel for "never delivered" in t_complete_ns. */
+#define GS_UNDELIVERED UINT64_MAX
+
+typedef int32_t gs_status;
+enum {
+    GS_OK = 0,
+    GS_EINVAL = -1,       /* bad argument / knob combination               */
+    GS_ENOMEM = -2,       /* host or device allocation failed              */
+    GS_EDEVICE = -3,      /* HIP runtime error or no usable device         */
+    GS_ESTATE = -4,       /* call out of order (e.g. run before topology)  */
+    GS_ERANGE = -5,       /* a packed field overflowed (time, hops, mesh)  */
+    GS_EUNSUPPORTED = -6  /* knob recognised but not implemented yet       */
+};
+
+/* MUXER (rust-test-node/src/env.rs:48-50,69-71; nim adds mplex,
+ * nim-test-node/gossipsub-queues/main.nim:433-441). */
+enum { GS_MUX_YAMUX = 0, GS_MUX_QUIC = 1, GS_MUX_MPLEX = 2 };
+
+/* Link-table mode for gs_topogen_links. */
+enum {
+    GS_LINKS_DIRECT = 0,   /* latency of the direct GML edge (topogen intent)       */
+    GS_LINKS_SHORTEST = 1  /* shortest path over the GML graph incl. injector hub  */
+};
+
+/* Simulator configuration. Field meaning follows the reference's knobs:
+ * rust-test-node/src/env.rs:27-87 (PEERS, CONNECTTO, FRAGMENTS, MUXER) and
+ * rust-test-node/src/main.rs:223-241 (gossipsub ConfigBuilder). */
+typedef struct gs_config {
+    uint32_t abi_version;        /* must be GS_ABI_VERSION                         */
+    uint32_t peers;              /* PEERS (env.rs:38-41)                           */
+    uint32_t connect_to;         /* CONNECTTO (env.rs:43-46)                       */
+    uint32_t dial_extra;         /* 1: rust/go dial CONNECTTO+1 (main.rs:337); 0: nim */
+    uint32_t max_connections;    /* MAXCONNECTIONS inbound cap (nim main.nim:429); 0 = none */
+    uint32_t fragments;          /* FRAGMENTS (env.rs:64-67)                       */
+    uint32_t muxer;              /* GS_MUX_*                                       */
+    uint32_t signed_msgs;        /* 1: MessageAuthenticity::Signed (main.rs:397)   */
+    uint32_t d;                  /* mesh_n      (main.rs:231)                       */
+    uint32_t d_lo;               /* mesh_n_low  (main.rs:232)                       */
+    uint32_t d_hi;               /* mesh_n_high (main.rs:233)                       */
+    uint32_t d_lazy;             /* gossip_lazy (main.rs:235)                       */
+    uint32_t d_out;              /* mesh_outbound_min (main.rs:234)                 */
+    uint32_t gossip_factor_milli;/* gossip_factor x 1000 (main.rs:230)              */
+    uint64_t heartbeat_ns;       /* heartbeat_interval (main.rs:228)                */
+    uint64_t backoff_ns;         /* prune_backoff (main.rs:229)                     */
+    uint32_t flood_publish;      /* flood_publish (main.rs:227)                     */
+    uint32_t idontwant;          /* IDONTWANT suppression (go main.go:165); 0 = off */
+    uint32_t lazy_gossip;        /* IHAVE/IWANT gossip relaxations; 0 = off         */
+    uint32_t self_log;           /* publisher logs its own message (nim SELFTRIGGER)*/
+    uint64_t seed;               /* counter-RNG key (reference RNG is unseeded, main.rs:308) */
+    int32_t  device;             /* HIP device ordinal                              */
+    uint32_t batch;              /* messages simulated together per device batch    */
+} gs_config;
+
+/* One publish injection (replaces POST /publish, main.rs:50-56,152-168). */
+typedef struct gs_publish {
+    uint64_t t_pub_ns;    /* absolute publish time = tx_time stamped at main.rs:105-111 */
+    uint32_t publisher;   /* peer id that publishes                                     */
+    uint32_t msg_size;    /* msgSize of the request; fragment payload = msg_size/F      */
+} gs_publish;
+
+/* Caller-allocated result arrays, message-major: element [m*peers + u].
+ * Either pointer may be NULL (that output is then not copied back). */
+typedef struct gs_result_sink {
+    uint64_t* t_complete_ns;  /* completion time of message m at peer u (GS_UNDELIVERED if never) */
+    uint8_t*  hops;           /* hop count of the completing fragment (0 at the publisher)        */
+} gs_result_sink;
+
+/* Counters accumulated since gs_create / gs_reset_stats. */
+typedef struct gs_stats {
+    uint64_t messages;          /* messages simulated                                  */
+    uint64_t deliveries;        /* (peer,msg) completions at non-publishers = log lines */
+    uint64_t frag_deliveries;   /* FD: fragment first arrivals at non-publishers       */
+    uint64_t relaxations;       /* R: flood-publish sends + forward sends (dups incl.) */
+    uint64_t bytes_alg;         /* 16*FD + 12*R + 8*deliveries           */
+    uint64_t latency_sum_ms;    /* sum of per-delivery latency in ms (truncated)       */
+    uint64_t latency_max_ms;    /* max per-delivery latency in ms                      */
+    uint64_t relax_launches;    /* bucket-relaxation kernel launches                   */
+    uint64_t buckets;           /* non-empty Delta-buckets processed                   */
+    double   relax_ms;          /* device time of relaxation launches (timing on)      */
+    double   run_ms;            /* device time of whole gs_run calls (timing on)       */
+    uint64_t relax_bytes_alg;   /* 16*FD + 12*R_forward: algorithmic bytes of relax    */
+} gs_stats;
+
+/* ---- host-only helpers (no device work) ---------------------------------- */
+
+/* Defaults of the rust preset (main.rs:36-38,223-241; env.rs:38-67). */
+void gs_config_default(gs_config* cfg);
+
+/* Read the reference's env surface into cfg: PEERS, CONNECTTO, FRAGMENTS,
+ * MUXER (env.rs:38-67), MAXCONNECTIONS (nim main.nim:429), GOSSIPSUB_D,
+ * _D_LOW, _D_HIGH, _D_LAZY, _D_OUT, _HEARTBEAT_MS, _PRUNE_BACKOFF_SEC,
+ * _GOSSIP_FACTOR, _FLOOD_PUBLISH (nim main.nim:252-284), SELFTRIGGER, plus
+ * GS_SEED / GS_BATCH / GS_DEVICE. Validation mirrors env.rs:69-75:
+ * unknown muxer and CONNECTTO >= PEERS are errors (message in err). */
+gs_status gs_config_from_env(gs_config* cfg, char* err, size_t err_len);
+
+/* Wire bytes of one fragment of `payload` bytes on one hop. */
+uint64_t gs_wire_bytes(uint64_t payload, uint32_t muxer, uint32_t signed_msgs);
+
+/* Stage link tables from topogen.py's parameters (shadow/topogen.py:39-71):
+ * lat_ns[S*S] (row = sender stage), bw_bps[S] (up == down). */
+gs_status gs_topogen_links(uint32_t stages, uint32_t min_bw_mbit, uint32_t max_bw_mbit,
+                           uint32_t min_lat_ms, uint32_t max_lat_ms, uint32_t mode,
+                           uint64_t* lat_ns, uint64_t* bw_bps);
+
+/* Publish schedule of shadow/run.sh:34-36 (publisher_id, publisher_rotation,
+ * inter_message_delay): row i = {t0 + i*delay, (pub0 + i*rotation) mod N, size}. */
+gs_status gs_schedule_runsh(uint32_t n_msgs, uint32_t peers, uint32_t publisher_id,
+                            uint32_t rotation, uint64_t t0_ns, uint64_t delay_ns,
+                            uint32_t msg_size, gs_publish* out);
+
+/* Write arrival lines exactly as `grep -rne 'milliseconds\|BW' shadow.data/`
+ * would print them for rust nodes (main.rs:93; shadow/run.sh:61):
+ *   shadow.data/hosts/peer<u>/main.1000.stdout:<line>:<tx_time> milliseconds: <ms>
+ * grouped by peer in ascending id, line numbers counted per peer. */
+gs_status gs_write_latency_log(const char* path, const gs_publish* sched, uint64_t n_msgs,
+                               uint32_t peers, const uint64_t* t_complete_ns,
+                               uint32_t self_log);
+
+/* ---- context lifecycle (replaces SwarmBuilder + build_behaviour, main.rs:391-440) ---- */
+
+gs_status gs_create(const gs_config* cfg, struct gs_ctx** out);
+gs_status gs_destroy(struct gs_ctx* ctx);
+const char* gs_last_error(const struct gs_ctx* ctx);
+
+/* Per-stage link model. lat_ns is S x S (sender stage row), bw arrays have S
+ * entries in bit/s; stage_of_peer has `peers` entries or is NULL (= u % S,
+ * topogen.py:121-122). */
+gs_status gs_set_links(struct gs_ctx* ctx, uint32_t stages, const uint64_t* lat_ns,
+                       const uint64_t* bw_up_bps, const uint64_t* bw_down_bps,
+                       const uint8_t* stage_of_peer);
+
+/* Random ID dialing -> symmetric CSR peer graph, on the device
+ * (replaces connect_gossipsub_peers, main.rs:303-389). */
+gs_status gs_build_topology(struct gs_ctx* ctx);
+
+/* Graph size after gs_build_topology. */
+gs_status gs_graph_info(const struct gs_ctx* ctx, uint32_t* peers, uint64_t* nnz,
+                        uint32_t* max_degree);
+
+/* Copy the CSR out: row_ptr[peers+1], col[nnz], flags[nnz] (bit0 = outbound,
+ * bit1 = in mesh). Any pointer may be NULL. */
+gs_status gs_get_csr(struct gs_ctx* ctx, uint64_t* row_ptr, uint32_t* col, uint8_t* flags);
+
+/* Heartbeat GRAFT/PRUNE to a fixed point or max_heartbeats epochs
+ * (libp2p-gossipsub heartbeat, configured at main.rs:228-236). */
+gs_status gs_mesh_converge(struct gs_ctx* ctx, uint32_t max_heartbeats, uint32_t* out_epochs);
+
+/* Mesh width of gs_get_mesh rows. */
+#define GS_MESH_W 16u
+/* Copy the mesh out: mesh[peers*GS_MESH_W] (ascending ids, UINT32_MAX padding),
+ * count[peers]. Either pointer may be NULL. */
+gs_status gs_get_mesh(struct gs_ctx* ctx, uint32_t* mesh, uint8_t* count);
+
+/* Simulate n_msgs publishes (replaces publish_new_message + the receive /
+ * forward / reassembly loop, main.rs:79-143,519-528). Results go to `sink`
+ * (may be NULL: device-resident run, counters only). */
+gs_status gs_run(struct gs_ctx* ctx, const gs_publish* sched, uint64_t n_msgs,
+                 const gs_result_sink* sink);
+
+gs_status gs_get_stats(const struct gs_ctx* ctx, gs_stats* out);
+gs_status gs_reset_stats(struct gs_ctx* ctx);
+
+/* 1: record HIP events around every relaxation launch and around gs_run. */
+gs_status gs_set_timing(struct gs_ctx* ctx, uint32_t enable);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GOSSIPSIM_H */

@@ -1,0 +1,561 @@
+/*
+ * gs_oracle.c — single-threaded CPU restatement of the dissemination rules.
+ *
+ * TEST INFRASTRUCTURE ONLY (see gs_oracle.h). It is the parity checker for
+ * libgossipsim.so and the `cpu_baseline` of bench.py; nothing in the product
+ * links or calls it.
+ *
+ * Every function cites the reference file:line it follows. The gossipsub
+ * router itself (libp2p-gossipsub 0.49.2) is not vendored: its rules are the
+ * spec choices of DESIGN.md §2, written here with a binary-heap event
+ * simulation (Dijkstra order) so that the GPU's Delta-stepping is checked by a
+ * structurally different algorithm.
+ */
+#include "gs_oracle.h"
+#include <stdlib.h>
+#include <string.h>
+
+#define INF64 UINT64_MAX
+#define HOP_BITS 6u
+#define MESH_W 16u
+#define BIT_OUT 1u
+#define BIT_MESH 2u
+
+enum { P_DIAL = 1, P_DIAL_ORDER = 2, P_GRAFT = 3, P_PRUNE = 4, P_OUT_GRAFT = 5 };
+
+/* ---------------------------------------------------------------- RNG ---- */
+/* Counter-based RNG keyed by (seed, purpose, a, b, c). The reference draws
+ * from an unseeded thread RNG (rust-test-node/src/main.rs:308); go seeds it
+ * with the node id (go-test-node/main.go:280-281). Here every draw is a pure
+ * function of its coordinates so CPU and GPU agree bit for bit. */
+static uint64_t mix64(uint64_t z) {
+    z ^= z >> 30; z *= 0xBF58476D1CE4E5B9ULL;
+    z ^= z >> 27; z *= 0x94D049BB133111EBULL;
+    z ^= z >> 31; return z;
+}
+uint64_t or_rng(uint64_t seed, uint32_t purpose, uint32_t a, uint32_t b, uint32_t c) {
+    uint64_t h = mix64(seed + 0x9E3779B97F4A7C15ULL * (uint64_t)(purpose + 1u));
+    h = mix64(h ^ ((uint64_t)a + 0x9E3779B97F4A7C15ULL));
+    h = mix64(h ^ ((((uint64_t)b) << 32) | c) ^ 0xD6E8FEB86659FD93ULL);
+    return h;
+}
+static uint64_t rand_below(uint64_t x, uint64_t n) {
+    return (uint64_t)(((unsigned __int128)x * n) >> 64);
+}
+
+/* --------------------------------------------------------- wire bytes ---- */
+static uint64_t varint_len(uint64_t x) { uint64_t n = 1; while (x >= 128) { x >>= 7; n++; } return n; }
+static uint64_t pb_field(uint64_t len) { return 1 + varint_len(len) + len; }
+static uint64_t cdiv(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+
+/* Bytes on the wire for one fragment of `payload` bytes (model
+ * constants). Signed gossipsub Message (main.rs:397): from
+ * (38 B peer id), data, seqno (8 B), topic "test" (main.rs:443), signature
+ * (64 B); unsigned (nim anonymize, gossipsub-queues/main.nim:447): data+topic.
+ * RPC{publish} is length-prefixed on its stream. Then the MUXER stack of
+ * main.rs:418-440: yamux 12 B per <=16 KiB frame, noise 18 B per <=65519 B,
+ * TCP/IPv4 40 B per 1460 B segment; QUIC 65 B per 1415 B of stream data;
+ * mplex 4 B per <=1 MiB frame. */
+uint64_t or_wire_bytes(uint64_t payload, uint32_t muxer, uint32_t signed_msgs) {
+    uint64_t msg = pb_field(payload) + pb_field(4);
+    if (signed_msgs) msg += pb_field(38) + pb_field(8) + pb_field(64);
+    uint64_t rpc = pb_field(msg);
+    uint64_t frame = varint_len(rpc) + rpc;
+    if (muxer == 1) /* quic */
+        return frame + cdiv(frame, 1415) * 65;
+    uint64_t a = (muxer == 2) ? frame + cdiv(frame, 1048576) * 4 : frame + cdiv(frame, 16384) * 12;
+    uint64_t b = a + cdiv(a, 65519) * 18;
+    return b + cdiv(b, 1460) * 40;
+}
+
+/* ---------------------------------------------------------- link model ---- */
+/* shadow/topogen.py:39-71: stage bandwidth ceil(i*bj + bl) Mbit (49-51),
+ * self-loop max((S-i)*lj, ll) ms (55), edge i<j min(ceil((S-j)*lj+ll), lh) ms
+ * (60), injector node S at 1 ms from everything (64-69). mode 0 = the direct
+ * GML edge; mode 1 = shortest non-empty path over the GML graph incl. the
+ * injector hub (Shadow's use_shortest_path; upstream, not vendored). */
+int or_topogen_links(uint32_t S, uint32_t bl, uint32_t bh, uint32_t ll, uint32_t lh,
+                     uint32_t mode, uint64_t* lat_ns, uint64_t* bw_bps) {
+    if (S == 0 || S > 255 || bl > bh || ll > lh || mode > 1) return -1;
+    uint64_t bj = (bh - bl) / S, lj = (lh - ll) / S;
+    uint32_t V = S + 1;
+    uint64_t* g = (uint64_t*)malloc(sizeof(uint64_t) * V * V);
+    if (!g) return -2;
+    for (uint32_t i = 0; i < S; i++) {
+        bw_bps[i] = ((uint64_t)i * bj + bl) * 1000000ULL;
+        uint64_t self = (uint64_t)(S - i) * lj; if (self < ll) self = ll;
+        g[i * V + i] = self;
+        for (uint32_t j = i + 1; j < S; j++) {
+            uint64_t e = (uint64_t)(S - j) * lj + ll; if (e > lh) e = lh;
+            g[i * V + j] = g[j * V + i] = e;
+        }
+    }
+    for (uint32_t i = 0; i <= S; i++) g[i * V + S] = g[S * V + i] = 1;
+    if (mode == 0) {
+        for (uint32_t i = 0; i < S; i++)
+            for (uint32_t j = 0; j < S; j++) lat_ns[i * S + j] = g[i * V + j] * 1000000ULL;
+    } else {
+        uint64_t* d = (uint64_t*)malloc(sizeof(uint64_t) * V * V);
+        if (!d) { free(g); return -2; }
+        for (uint32_t i = 0; i < V; i++)
+            for (uint32_t j = 0; j < V; j++) d[i * V + j] = (i == j) ? 0 : g[i * V + j];
+        for (uint32_t k = 0; k < V; k++)
+            for (uint32_t i = 0; i < V; i++)
+                for (uint32_t j = 0; j < V; j++)
+                    if (d[i * V + k] + d[k * V + j] < d[i * V + j]) d[i * V + j] = d[i * V + k] + d[k * V + j];
+        for (uint32_t i = 0; i < S; i++)
+            for (uint32_t j = 0; j < S; j++) {
+                uint64_t v = d[i * V + j];
+                if (i == j) {
+                    v = g[i * V + i];
+                    for (uint32_t k = 0; k < V; k++)
+                        if (k != i && d[i * V + k] + d[k * V + i] < v) v = d[i * V + k] + d[k * V + i];
+                }
+                lat_ns[i * S + j] = v * 1000000ULL;
+            }
+        free(d);
+    }
+    free(g);
+    return 0;
+}
+
+/* ---------------------------------------------------------- topology ---- */
+/* Dials per peer: rust takes min(2*CONNECTTO, N-1) shuffled candidates
+ * (main.rs:311-320) and dials until connected > CONNECTTO (main.rs:336-354),
+ * i.e. CONNECTTO+1 dials (defect D4); nim stops at CONNECTTO
+ * (gossipsub-queues/main.nim:396). */
+uint32_t or_dials_per_peer(const or_params* p) {
+    uint64_t lim = 2ull * p->connect_to;
+    if (lim > (uint64_t)p->peers - 1) lim = p->peers - 1;
+    uint64_t k = (uint64_t)p->connect_to + p->dial_extra;
+    return (uint32_t)(k < lim ? k : lim);
+}
+
+/* Peer v's dial list: a uniform k-subset of the other N-1 ids (Floyd's
+ * sampling), put in dial order by a per-(v,id) random key. */
+static void gen_dials(const or_params* p, uint32_t v, uint32_t k, uint32_t* out) {
+    uint64_t n = p->peers - 1;
+    uint32_t m = 0;
+    for (uint32_t i = 0; i < k; i++) {
+        uint64_t j = n - k + i;
+        uint64_t r = rand_below(or_rng(p->seed, P_DIAL, v, i, 0), j + 1);
+        int dup = 0;
+        for (uint32_t q = 0; q < m; q++) if (out[q] == (uint32_t)r) { dup = 1; break; }
+        out[m++] = dup ? (uint32_t)j : (uint32_t)r;
+    }
+    for (uint32_t i = 0; i < k; i++) out[i] = out[i] < v ? out[i] : out[i] + 1;
+    /* insertion sort by (rng key, id) */
+    for (uint32_t i = 1; i < k; i++) {
+        uint32_t x = out[i]; uint64_t kx = or_rng(p->seed, P_DIAL_ORDER, v, x, 0);
+        int32_t j = (int32_t)i - 1;
+        while (j >= 0) {
+            uint64_t kj = or_rng(p->seed, P_DIAL_ORDER, v, out[j], 0);
+            if (kj < kx || (kj == kx && out[j] < x)) break;
+            out[j + 1] = out[j]; j--;
+        }
+        out[j + 1] = x;
+    }
+}
+
+static int cmp_u64(const void* a, const void* b) {
+    uint64_t x = *(const uint64_t*)a, y = *(const uint64_t*)b;
+    return x < y ? -1 : x > y;
+}
+
+/* Symmetric CSR of accepted dials. Entry (u,w) gets bit0 when u dialed w.
+ * MAXCONNECTIONS (nim gossipsub-queues/main.nim:429): acceptor t takes its
+ * non-mutual inbound dials in (dial index, dialer) order up to cap - k. */
+int or_build_topology(const or_params* p, uint64_t* row_ptr, uint32_t* col, uint8_t* flags,
+                      uint64_t* nnz_out) {
+    uint32_t N = p->peers;
+    if (N < 2) return -1;
+    uint32_t k = or_dials_per_peer(p);
+    if (k == 0) return -1; /* "Failed to connect any peers" (main.rs:381-382) */
+    uint32_t* dial = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)N * k);
+    uint8_t* acc = (uint8_t*)malloc((size_t)N * k);
+    if (!dial || !acc) { free(dial); free(acc); return -2; }
+    for (uint32_t v = 0; v < N; v++) gen_dials(p, v, k, dial + (size_t)v * k);
+    memset(acc, 1, (size_t)N * k);
+    if (p->max_connections) {
+        uint32_t quota = p->max_connections > k ? p->max_connections - k : 0;
+        /* inbound lists: key = (j << 32) | v, bucketed by acceptor */
+        uint64_t* cnt = (uint64_t*)calloc((size_t)N + 1, sizeof(uint64_t));
+        uint64_t* in = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)N * k);
+        uint64_t* fill = (uint64_t*)calloc((size_t)N, sizeof(uint64_t));
+        if (!cnt || !in || !fill) { free(cnt); free(in); free(fill); free(dial); free(acc); return -2; }
+        for (uint64_t e = 0; e < (uint64_t)N * k; e++) cnt[dial[e] + 1]++;
+        for (uint32_t t = 0; t < N; t++) cnt[t + 1] += cnt[t];
+        for (uint32_t v = 0; v < N; v++)
+            for (uint32_t j = 0; j < k; j++) {
+                uint32_t t = dial[(size_t)v * k + j];
+                in[cnt[t] + fill[t]++] = ((uint64_t)j << 32) | v;
+            }
+        for (uint32_t t = 0; t < N; t++) {
+            uint64_t b = cnt[t], e = cnt[t + 1];
+            qsort(in + b, e - b, sizeof(uint64_t), cmp_u64);
+            uint32_t taken = 0;
+            for (uint64_t q = b; q < e; q++) {
+                uint32_t v = (uint32_t)in[q], j = (uint32_t)(in[q] >> 32);
+                int mutual = 0;
+                for (uint32_t jj = 0; jj < k; jj++) if (dial[(size_t)t * k + jj] == v) { mutual = 1; break; }
+                if (mutual) continue;
+                if (taken < quota) taken++; else acc[(size_t)v * k + j] = 0;
+            }
+        }
+        free(cnt); free(in); free(fill);
+    }
+    /* half-edges (row, col<<1 | out), then per-row sort + dedupe */
+    uint64_t* deg = (uint64_t*)calloc((size_t)N + 1, sizeof(uint64_t));
+    uint64_t* he = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)N * k * 2);
+    uint64_t* fill = (uint64_t*)calloc((size_t)N, sizeof(uint64_t));
+    if (!deg || !he || !fill) { free(deg); free(he); free(fill); free(dial); free(acc); return -2; }
+    for (uint32_t v = 0; v < N; v++)
+        for (uint32_t j = 0; j < k; j++)
+            if (acc[(size_t)v * k + j]) { deg[v + 1]++; deg[dial[(size_t)v * k + j] + 1]++; }
+    for (uint32_t v = 0; v < N; v++) deg[v + 1] += deg[v];
+    for (uint32_t v = 0; v < N; v++)
+        for (uint32_t j = 0; j < k; j++) {
+            if (!acc[(size_t)v * k + j]) continue;
+            uint32_t t = dial[(size_t)v * k + j];
+            he[deg[v] + fill[v]++] = ((uint64_t)t << 1) | 1u;
+            he[deg[t] + fill[t]++] = ((uint64_t)v << 1);
+        }
+    uint64_t nnz = 0;
+    row_ptr[0] = 0;
+    for (uint32_t v = 0; v < N; v++) {
+        uint64_t b = deg[v], e = deg[v + 1];
+        qsort(he + b, e - b, sizeof(uint64_t), cmp_u64);
+        for (uint64_t q = b; q < e; q++) {
+            uint32_t c = (uint32_t)(he[q] >> 1); uint8_t o = (uint8_t)(he[q] & 1u);
+            if (nnz > row_ptr[v] && col[nnz - 1] == c) { flags[nnz - 1] |= o; continue; }
+            col[nnz] = c; flags[nnz] = o; nnz++;
+        }
+        row_ptr[v + 1] = nnz;
+    }
+    *nnz_out = nnz;
+    free(deg); free(he); free(fill); free(dial); free(acc);
+    return 0;
+}
+
+/* -------------------------------------------------------------- mesh ---- */
+/* Heartbeat GRAFT/PRUNE (libp2p-gossipsub heartbeat/handle_graft/handle_prune,
+ * upstream, not vendored; parameters main.rs:228-236), synchronous epochs of
+ * A) every peer decides grafts/prunes from the start-of-epoch
+ * state; B) every receiver handles incoming GRAFTs in (latency, id) order;
+ * C) PRUNEs and rejections are applied, both ends back off. */
+static uint64_t find_entry(const uint64_t* row_ptr, const uint32_t* col, uint32_t u, uint32_t w) {
+    uint64_t lo = row_ptr[u], hi = row_ptr[u + 1];
+    while (lo < hi) { uint64_t mid = (lo + hi) / 2; if (col[mid] < w) lo = mid + 1; else hi = mid; }
+    return lo;
+}
+
+typedef struct { uint64_t key; uint64_t e; } sel_t;
+static int cmp_sel(const void* a, const void* b) {
+    const sel_t *x = (const sel_t*)a, *y = (const sel_t*)b;
+    if (x->key != y->key) return x->key < y->key ? -1 : 1;
+    return x->e < y->e ? -1 : x->e > y->e;
+}
+
+int or_mesh_converge(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
+                     uint8_t* flags, const uint8_t* stage, uint32_t S, const uint64_t* lat_ns,
+                     uint32_t max_hb, uint32_t* mesh, uint8_t* cnt, uint32_t* epochs_out) {
+    uint32_t N = p->peers;
+    uint64_t nnz = row_ptr[N];
+    uint64_t bo = (p->backoff_ns + p->heartbeat_ns - 1) / p->heartbeat_ns;
+    uint32_t* until = (uint32_t*)calloc(nnz ? nnz : 1, sizeof(uint32_t));
+    uint8_t* prop = (uint8_t*)calloc(nnz ? nnz : 1, 1); /* 1 graft, 2 prune, 4 accepted */
+    uint64_t* rev = (uint64_t*)malloc(sizeof(uint64_t) * (nnz ? nnz : 1));
+    uint32_t maxdeg = 0;
+    for (uint32_t u = 0; u < N; u++) {
+        uint32_t dg = (uint32_t)(row_ptr[u + 1] - row_ptr[u]); if (dg > maxdeg) maxdeg = dg;
+    }
+    sel_t* sel = (sel_t*)malloc(sizeof(sel_t) * (maxdeg + 1));
+    if (!until || !prop || !rev || !sel) { free(until); free(prop); free(rev); free(sel); return -2; }
+    for (uint32_t u = 0; u < N; u++)
+        for (uint64_t e = row_ptr[u]; e < row_ptr[u + 1]; e++) rev[e] = find_entry(row_ptr, col, col[e], u);
+    for (uint64_t e = 0; e < nnz; e++) flags[e] &= (uint8_t)~BIT_MESH;
+
+    uint32_t epoch = 1, last = 0;
+    while (epoch <= max_hb) {
+        uint64_t changes = 0;
+        memset(prop, 0, nnz);
+        /* ---- A: heartbeat decisions ---- */
+        for (uint32_t u = 0; u < N; u++) {
+            uint64_t b = row_ptr[u], en = row_ptr[u + 1];
+            uint32_t m = 0, o = 0;
+            for (uint64_t e = b; e < en; e++) if (flags[e] & BIT_MESH) { m++; if (flags[e] & BIT_OUT) o++; }
+            uint32_t mm = m, oo = o;
+            if (m < p->d_lo) { /* graft mesh_n - len random eligible peers */
+                uint32_t nc = 0;
+                for (uint64_t e = b; e < en; e++)
+                    if (!(flags[e] & BIT_MESH) && epoch > until[e]) {
+                        sel[nc].key = or_rng(p->seed, P_GRAFT, u, epoch, col[e]); sel[nc].e = e; nc++;
+                    }
+                qsort(sel, nc, sizeof(sel_t), cmp_sel);
+                uint32_t want = p->d - m; if (want > nc) want = nc;
+                for (uint32_t q = 0; q < want; q++) {
+                    prop[sel[q].e] |= 1; mm++; if (flags[sel[q].e] & BIT_OUT) oo++;
+                }
+            }
+            if (mm > p->d_hi) { /* prune down to mesh_n keeping mesh_outbound_min outbound */
+                uint32_t nc = 0;
+                for (uint64_t e = b; e < en; e++)
+                    if (flags[e] & BIT_MESH) { sel[nc].key = or_rng(p->seed, P_PRUNE, u, epoch, col[e]); sel[nc].e = e; nc++; }
+                qsort(sel, nc, sizeof(sel_t), cmp_sel);
+                uint32_t excess = mm - p->d, removed = 0;
+                for (uint32_t q = 0; q < nc && removed < excess; q++) {
+                    uint64_t e = sel[q].e;
+                    if (flags[e] & BIT_OUT) { if (oo <= p->d_out) continue; oo--; }
+                    prop[e] |= 2; removed++; mm--;
+                }
+            }
+            if (mm >= p->d_lo && oo < p->d_out) { /* graft outbound peers */
+                uint32_t nc = 0;
+                for (uint64_t e = b; e < en; e++)
+                    if ((flags[e] & BIT_OUT) && !(flags[e] & BIT_MESH) && !(prop[e] & 1) && epoch > until[e]) {
+                        sel[nc].key = or_rng(p->seed, P_OUT_GRAFT, u, epoch, col[e]); sel[nc].e = e; nc++;
+                    }
+                qsort(sel, nc, sizeof(sel_t), cmp_sel);
+                uint32_t want = p->d_out - oo; if (want > nc) want = nc;
+                for (uint32_t q = 0; q < want; q++) { prop[sel[q].e] |= 1; mm++; }
+            }
+        }
+        /* ---- B: receivers handle GRAFTs ---- */
+        for (uint32_t w = 0; w < N; w++) {
+            uint64_t b = row_ptr[w], en = row_ptr[w + 1];
+            uint32_t c = 0, nin = 0;
+            for (uint64_t e = b; e < en; e++)
+                if (((flags[e] & BIT_MESH) && !(prop[e] & 2)) || (prop[e] & 1)) c++;
+            for (uint64_t e = b; e < en; e++)
+                if (prop[rev[e]] & 1) {
+                    sel[nin].key = lat_ns[(uint32_t)stage[col[e]] * S + stage[w]]; sel[nin].e = e; nin++;
+                }
+            /* order by (latency u->w, u): stable wrt ascending ids */
+            for (uint32_t i = 1; i < nin; i++) {
+                sel_t x = sel[i]; int32_t j = (int32_t)i - 1;
+                while (j >= 0 && sel[j].key > x.key) { sel[j + 1] = sel[j]; j--; }
+                sel[j + 1] = x;
+            }
+            for (uint32_t q = 0; q < nin; q++) {
+                uint64_t e = sel[q].e;               /* entry (w -> u) */
+                int in_mesh = ((flags[e] & BIT_MESH) && !(prop[e] & 2)) || (prop[e] & 1);
+                if (in_mesh) { prop[rev[e]] |= 4; continue; }
+                if (epoch < until[e]) { until[e] = epoch + (uint32_t)bo; continue; }
+                if (c >= p->d_hi && !(flags[e] & BIT_OUT)) { until[e] = epoch + (uint32_t)bo; continue; }
+                prop[rev[e]] |= 4; flags[e] |= BIT_MESH; c++;
+            }
+        }
+        /* ---- C: apply prunes and rejections ---- */
+        for (uint32_t u = 0; u < N; u++) {
+            for (uint64_t e = row_ptr[u]; e < row_ptr[u + 1]; e++) {
+                uint8_t pr = prop[e];
+                if (pr & 1) {
+                    changes++;
+                    if (pr & 4) flags[e] |= BIT_MESH;
+                    else { flags[e] &= (uint8_t)~BIT_MESH; until[e] = epoch + (uint32_t)bo; }
+                }
+                if (pr & 2) { changes++; flags[e] &= (uint8_t)~BIT_MESH; until[e] = epoch + (uint32_t)bo; }
+                if (prop[rev[e]] & 2) { flags[e] &= (uint8_t)~BIT_MESH; until[e] = epoch + (uint32_t)bo; }
+            }
+        }
+        last = epoch;
+        if (changes) { epoch++; continue; }
+        /* quiescent: next epoch at which a back-off expiry can wake a peer */
+        uint64_t wake = UINT64_MAX;
+        for (uint32_t u = 0; u < N; u++) {
+            uint64_t b = row_ptr[u], en = row_ptr[u + 1];
+            uint32_t m = 0, o = 0;
+            for (uint64_t e = b; e < en; e++) if (flags[e] & BIT_MESH) { m++; if (flags[e] & BIT_OUT) o++; }
+            int need_any = m < p->d_lo;
+            int need_out = !need_any && m <= p->d_hi && o < p->d_out;
+            if (!need_any && !need_out) continue;
+            for (uint64_t e = b; e < en; e++) {
+                if (flags[e] & BIT_MESH) continue;
+                if (need_out && !(flags[e] & BIT_OUT)) continue;
+                if (until[e] >= epoch + 1 && (uint64_t)until[e] + 1 < wake) wake = (uint64_t)until[e] + 1;
+            }
+        }
+        if (wake == UINT64_MAX || wake > max_hb) break;
+        epoch = (uint32_t)wake;
+    }
+    for (uint32_t u = 0; u < N; u++) {
+        uint32_t c = 0;
+        for (uint64_t e = row_ptr[u]; e < row_ptr[u + 1]; e++)
+            if (flags[e] & BIT_MESH) {
+                if (c >= MESH_W) { free(until); free(prop); free(rev); free(sel); return -5; }
+                mesh[(size_t)u * MESH_W + c++] = col[e];
+            }
+        cnt[u] = (uint8_t)c;
+        for (uint32_t q = c; q < MESH_W; q++) mesh[(size_t)u * MESH_W + q] = UINT32_MAX;
+    }
+    *epochs_out = last;
+    free(until); free(prop); free(rev); free(sel);
+    return 0;
+}
+
+/* ------------------------------------------------------ dissemination ---- */
+typedef struct { uint64_t key; uint32_t dst; uint32_t frag; } ev_t;
+typedef struct { ev_t* a; size_t n, cap; } heap_t;
+
+static int ev_less(const ev_t* x, const ev_t* y) {
+    if (x->key != y->key) return x->key < y->key;
+    if (x->dst != y->dst) return x->dst < y->dst;
+    return x->frag < y->frag;
+}
+static int heap_push(heap_t* h, ev_t v) {
+    if (h->n == h->cap) {
+        size_t nc = h->cap ? h->cap * 2 : 1024;
+        ev_t* na = (ev_t*)realloc(h->a, nc * sizeof(ev_t));
+        if (!na) return -2;
+        h->a = na; h->cap = nc;
+    }
+    size_t i = h->n++;
+    while (i > 0) {
+        size_t pa = (i - 1) / 2;
+        if (!ev_less(&v, &h->a[pa])) break;
+        h->a[i] = h->a[pa]; i = pa;
+    }
+    h->a[i] = v;
+    return 0;
+}
+static ev_t heap_pop(heap_t* h) {
+    ev_t top = h->a[0], last = h->a[--h->n];
+    size_t i = 0;
+    for (;;) {
+        size_t l = 2 * i + 1, r = l + 1, s = i;
+        const ev_t* cur = &last;
+        if (l < h->n && ev_less(&h->a[l], cur)) { s = l; cur = &h->a[l]; }
+        if (r < h->n && ev_less(&h->a[r], cur)) { s = r; }
+        if (s == i) break;
+        h->a[i] = h->a[s]; i = s;
+    }
+    if (h->n) h->a[i] = last;
+    return top;
+}
+
+static uint32_t bits_for(uint32_t n) { uint32_t b = 1; while ((1ull << b) < n) b++; return b; }
+
+/* One publish -> receive -> forward -> reassemble pass per message:
+ *  publish_new_message (main.rs:101-143): F fragments of msg_size/F bytes,
+ *    byte 10 = chunk (fragments distinct only if payload > 10: defect D8),
+ *    flood-published (main.rs:227) to every connection in ascending id,
+ *    fragment after fragment, through the publisher's uplink FIFO.
+ *  first receipt of (peer, fragment) wins by key (time, hops, src); it is
+ *    forwarded to mesh \ {src, publisher} in ascending id through the peer's
+ *    uplink FIFO (busy carried across that message's fragments).
+ *  create_message_handler (main.rs:79-99): completion = arrival of the F-th
+ *    distinct fragment; latency ms = (t_complete - tx_time)/1e6 truncated. */
+int or_run(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
+           const uint32_t* mesh, const uint8_t* cnt, const uint8_t* stage, uint32_t S,
+           const uint64_t* lat_ns, const uint64_t* bw_up, const uint64_t* bw_dn,
+           const uint64_t* sched_t, const uint32_t* sched_pub, const uint32_t* sched_size,
+           uint64_t n_msgs, uint64_t* t_complete, uint8_t* hops, or_stats* st) {
+    uint32_t N = p->peers, F = p->fragments;
+    if (F == 0 || F > 16 || p->lazy_gossip) return -6;
+    uint32_t sb = bits_for(N), tshift = sb + HOP_BITS;
+    uint64_t tmax = (tshift >= 64) ? 0 : (UINT64_MAX >> tshift);
+    uint64_t hmask = (1ull << HOP_BITS) - 1, smask = (1ull << sb) - 1;
+    size_t NF = (size_t)N * F;
+    uint64_t* best = (uint64_t*)malloc(sizeof(uint64_t) * NF);
+    uint8_t* fin = (uint8_t*)malloc(NF);
+    uint64_t* busy = (uint64_t*)malloc(sizeof(uint64_t) * N);
+    uint64_t *su = (uint64_t*)malloc(8 * S), *sd = (uint64_t*)malloc(8 * S);
+    heap_t h = {0, 0, 0};
+    int rc = 0;
+    if (!best || !fin || !busy || !su || !sd) { rc = -2; goto out; }
+    for (uint64_t mi = 0; mi < n_msgs; mi++) {
+        uint32_t pub = sched_pub[mi];
+        uint64_t payload = sched_size[mi] / F;
+        if (pub >= N || payload < 8) { rc = -1; goto out; } /* main.rs:110 panics below 8 B */
+        int collide = (F > 1 && payload <= 10);             /* defect D8 */
+        uint32_t Fe = collide ? 1 : F;
+        uint64_t wire = or_wire_bytes(payload, p->muxer, p->signed_msgs);
+        for (uint32_t s = 0; s < S; s++) {
+            su[s] = (wire * 8000000000ULL + bw_up[s] - 1) / bw_up[s];
+            sd[s] = (wire * 8000000000ULL + bw_dn[s] - 1) / bw_dn[s];
+        }
+        for (size_t i = 0; i < NF; i++) { best[i] = INF64; fin[i] = 0; }
+        for (uint32_t u = 0; u < N; u++) busy[u] = 0;
+        h.n = 0;
+        /* publisher: self key, flood through the uplink FIFO */
+        uint32_t sp = stage[pub];
+        for (uint32_t f = 0; f < Fe; f++) { best[(size_t)pub * F + f] = (uint64_t)pub; fin[(size_t)pub * F + f] = 1; }
+        const uint32_t* tgt; uint32_t deg;
+        uint32_t meshrow[MESH_W];
+        if (p->flood_publish) { tgt = col + row_ptr[pub]; deg = (uint32_t)(row_ptr[pub + 1] - row_ptr[pub]); }
+        else { deg = cnt[pub]; for (uint32_t q = 0; q < deg; q++) meshrow[q] = mesh[(size_t)pub * MESH_W + q]; tgt = meshrow; }
+        for (uint32_t f = 0; f < Fe; f++)
+            for (uint32_t j = 0; j < deg; j++) {
+                uint32_t w = tgt[j], sw = stage[w];
+                uint64_t dn = sd[sw] > su[sp] ? sd[sw] - su[sp] : 0;
+                uint64_t arr = ((uint64_t)f * deg + j + 1) * su[sp] + lat_ns[sp * S + sw] + dn;
+                if (arr > tmax) { rc = -5; goto out; }
+                uint64_t key = (arr << tshift) | (1ull << sb) | pub;
+                st->relaxations++;
+                if (key < best[(size_t)w * F + f]) best[(size_t)w * F + f] = key;
+                ev_t ev = {key, w, f};
+                if (heap_push(&h, ev)) { rc = -2; goto out; }
+            }
+        while (h.n) {
+            ev_t ev = heap_pop(&h);
+            size_t idx = (size_t)ev.dst * F + ev.frag;
+            if (fin[idx]) continue;
+            fin[idx] = 1;
+            uint32_t u = ev.dst, su_ = stage[u];
+            uint64_t t = ev.key >> tshift;
+            uint64_t hp = (ev.key >> sb) & hmask;
+            uint32_t src = (uint32_t)(ev.key & smask);
+            st->frag_deliveries++;
+            uint32_t tg[MESH_W], n = 0;
+            for (uint32_t q = 0; q < cnt[u]; q++) {
+                uint32_t w = mesh[(size_t)u * MESH_W + q];
+                if (w == src || w == pub) continue;
+                if (p->idontwant && payload >= p->idontwant) {
+                    uint64_t bw_ = best[(size_t)w * F + ev.frag];
+                    if (bw_ != INF64 && (bw_ >> tshift) + lat_ns[stage[w] * S + su_] <= t) continue;
+                }
+                tg[n++] = w;
+            }
+            uint64_t start = (Fe > 1 && busy[u] > t) ? busy[u] : t;
+            busy[u] = start + (uint64_t)n * su[su_];
+            if (n && hp + 1 > hmask) { rc = -5; goto out; }
+            for (uint32_t j = 0; j < n; j++) {
+                uint32_t w = tg[j], sw = stage[w];
+                uint64_t dn = sd[sw] > su[su_] ? sd[sw] - su[su_] : 0;
+                uint64_t arr = start + (uint64_t)(j + 1) * su[su_] + lat_ns[su_ * S + sw] + dn;
+                if (arr > tmax) { rc = -5; goto out; }
+                uint64_t key = (arr << tshift) | ((hp + 1) << sb) | u;
+                st->relaxations++;
+                size_t wi = (size_t)w * F + ev.frag;
+                if (key < best[wi]) {
+                    best[wi] = key;
+                    ev_t ne = {key, w, ev.frag};
+                    if (heap_push(&h, ne)) { rc = -2; goto out; }
+                }
+            }
+        }
+        /* reassembly: F-th distinct fragment completes the message */
+        for (uint32_t u = 0; u < N; u++) {
+            size_t o = (size_t)mi * N + u;
+            if (u == pub) { t_complete[o] = sched_t[mi]; hops[o] = 0; continue; }
+            uint64_t mk = 0; int ok = !collide;
+            for (uint32_t f = 0; f < F && ok; f++) {
+                uint64_t k = best[(size_t)u * F + f];
+                if (k == INF64) ok = 0; else if (k > mk) mk = k;
+            }
+            if (!ok) { t_complete[o] = INF64; hops[o] = 0xFF; continue; }
+            uint64_t trel = mk >> tshift;
+            t_complete[o] = sched_t[mi] + trel;
+            hops[o] = (uint8_t)((mk >> sb) & hmask);
+            uint64_t ms = trel / 1000000ULL;
+            st->deliveries++;
+            st->latency_sum_ms += ms;
+            if (ms > st->latency_max_ms) st->latency_max_ms = ms;
+        }
+        st->messages++;
+    }
+out:
+    st->bytes_alg = 16 * st->frag_deliveries + 12 * st->relaxations + 8 * st->deliveries;
+    free(best); free(fin); free(busy); free(su); free(sd); free(h.a);
+    return rc;
+}

@@ -1,0 +1,178 @@
+"""ctypes wrapper of the CPU oracle (oracle/gs_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, as the checker. The product path
+(dst-libp2p-test-node_amd/) never imports this module.
+
+Parity status: link tables pinned against shadow/topogen.py outputs and the
+log format pinned against shadow/summary_latency*.awk (tests/golden/); the
+gossipsub dissemination and mesh rules are a restatement of the
+third-party libp2p-gossipsub 0.49.2 behaviour (not vendored, no reference
+tests) — parity unpinned for those, see DESIGN.md §3.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "gs_oracle.c")
+LIB = os.path.join(HERE, "_build", "libgs_oracle.so")
+MESH_W = 16
+
+
+class OrParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint32) for n in (
+        "peers", "connect_to", "dial_extra", "max_connections", "fragments",
+        "muxer", "signed_msgs", "d", "d_lo", "d_hi", "d_lazy", "d_out",
+        "gossip_factor_milli")] + [
+        ("heartbeat_ns", ctypes.c_uint64), ("backoff_ns", ctypes.c_uint64)] + [
+        (n, ctypes.c_uint32) for n in ("flood_publish", "idontwant", "lazy_gossip", "self_log")] + [
+        ("seed", ctypes.c_uint64)]
+
+
+class OrStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in (
+        "messages", "deliveries", "frag_deliveries", "relaxations", "bytes_alg",
+        "latency_sum_ms", "latency_max_ms")]
+
+
+def build(force=False):
+    """Compile the oracle with gcc into oracle/_build (git-ignored)."""
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(SRC):
+        subprocess.check_call(["gcc", "-O2", "-shared", "-fPIC", "-o", LIB, SRC])
+    return LIB
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(LIB)
+        P = ctypes.POINTER
+        u32, u64, u8 = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint8
+        L.or_rng.restype = u64
+        L.or_rng.argtypes = [u64, u32, u32, u32, u32]
+        L.or_wire_bytes.restype = u64
+        L.or_wire_bytes.argtypes = [u64, u32, u32]
+        L.or_topogen_links.argtypes = [u32, u32, u32, u32, u32, u32, P(u64), P(u64)]
+        L.or_dials_per_peer.restype = u32
+        L.or_dials_per_peer.argtypes = [P(OrParams)]
+        L.or_build_topology.argtypes = [P(OrParams), P(u64), P(u32), P(u8), P(u64)]
+        L.or_mesh_converge.argtypes = [P(OrParams), P(u64), P(u32), P(u8), P(u8), u32, P(u64),
+                                       u32, P(u32), P(u8), P(u32)]
+        L.or_run.argtypes = [P(OrParams), P(u64), P(u32), P(u32), P(u8), P(u8), u32, P(u64),
+                             P(u64), P(u64), P(u64), P(u32), P(u32), u64, P(u64), P(u8),
+                             P(OrStats)]
+        _lib = L
+    return _lib
+
+
+def _p(a, ct):
+    return a.ctypes.data_as(ctypes.POINTER(ct))
+
+
+def params(**kw):
+    """Rust preset defaults (rust-test-node/src/main.rs:36-38,223-241; env.rs:38-67)."""
+    d = dict(peers=100, connect_to=10, dial_extra=1, max_connections=0, fragments=1,
+             muxer=0, signed_msgs=1, d=6, d_lo=4, d_hi=8, d_lazy=6, d_out=3,
+             gossip_factor_milli=250, heartbeat_ns=1_000_000_000, backoff_ns=60_000_000_000,
+             flood_publish=1, idontwant=0, lazy_gossip=0, self_log=0, seed=1)
+    d.update(kw)
+    return OrParams(**d)
+
+
+def wire_bytes(payload, muxer=0, signed=1):
+    return int(lib().or_wire_bytes(payload, muxer, signed))
+
+
+def rng(seed, purpose, a, b, c):
+    return int(lib().or_rng(seed, purpose, a, b, c))
+
+
+def topogen_links(stages, bl, bh, ll, lh, mode=0):
+    lat = np.zeros(stages * stages, np.uint64)
+    bw = np.zeros(stages, np.uint64)
+    rc = lib().or_topogen_links(stages, bl, bh, ll, lh, mode, _p(lat, ctypes.c_uint64),
+                                _p(bw, ctypes.c_uint64))
+    if rc:
+        raise ValueError("or_topogen_links rc=%d" % rc)
+    return lat.reshape(stages, stages), bw
+
+
+def build_topology(p):
+    N = p.peers
+    k = lib().or_dials_per_peer(ctypes.byref(p))
+    row_ptr = np.zeros(N + 1, np.uint64)
+    col = np.zeros(max(1, 2 * k * N), np.uint32)
+    flags = np.zeros(max(1, 2 * k * N), np.uint8)
+    nnz = ctypes.c_uint64(0)
+    rc = lib().or_build_topology(ctypes.byref(p), _p(row_ptr, ctypes.c_uint64),
+                                 _p(col, ctypes.c_uint32), _p(flags, ctypes.c_uint8),
+                                 ctypes.byref(nnz))
+    if rc:
+        raise ValueError("or_build_topology rc=%d" % rc)
+    n = nnz.value
+    return row_ptr, col[:n].copy(), flags[:n].copy()
+
+
+def mesh_converge(p, row_ptr, col, flags, stage, lat, max_hb=400):
+    N = p.peers
+    S = lat.shape[0]
+    flags = flags.copy()
+    mesh = np.zeros(N * MESH_W, np.uint32)
+    cnt = np.zeros(N, np.uint8)
+    ep = ctypes.c_uint32(0)
+    lat = np.ascontiguousarray(lat.reshape(-1), np.uint64)
+    stage = np.ascontiguousarray(stage, np.uint8)
+    rc = lib().or_mesh_converge(ctypes.byref(p), _p(row_ptr, ctypes.c_uint64),
+                                _p(col, ctypes.c_uint32), _p(flags, ctypes.c_uint8),
+                                _p(stage, ctypes.c_uint8), S, _p(lat, ctypes.c_uint64), max_hb,
+                                _p(mesh, ctypes.c_uint32), _p(cnt, ctypes.c_uint8),
+                                ctypes.byref(ep))
+    if rc:
+        raise ValueError("or_mesh_converge rc=%d" % rc)
+    return flags, mesh.reshape(N, MESH_W), cnt, ep.value
+
+
+def run(p, row_ptr, col, mesh, cnt, stage, lat, bw_up, bw_dn, sched_t, sched_pub, sched_size):
+    N = p.peers
+    S = lat.shape[0]
+    M = len(sched_t)
+    tc = np.zeros(M * N, np.uint64)
+    hops = np.zeros(M * N, np.uint8)
+    st = OrStats()
+    a64 = lambda x: np.ascontiguousarray(x, np.uint64)
+    a32 = lambda x: np.ascontiguousarray(x, np.uint32)
+    lat, bw_up, bw_dn, sched_t = a64(lat.reshape(-1)), a64(bw_up), a64(bw_dn), a64(sched_t)
+    sched_pub, sched_size = a32(sched_pub), a32(sched_size)
+    mesh = a32(mesh.reshape(-1))
+    stage = np.ascontiguousarray(stage, np.uint8)
+    rc = lib().or_run(ctypes.byref(p), _p(row_ptr, ctypes.c_uint64), _p(col, ctypes.c_uint32),
+                      _p(mesh, ctypes.c_uint32), _p(cnt, ctypes.c_uint8), _p(stage, ctypes.c_uint8),
+                      S, _p(lat, ctypes.c_uint64), _p(bw_up, ctypes.c_uint64),
+                      _p(bw_dn, ctypes.c_uint64), _p(sched_t, ctypes.c_uint64),
+                      _p(sched_pub, ctypes.c_uint32), _p(sched_size, ctypes.c_uint32), M,
+                      _p(tc, ctypes.c_uint64), _p(hops, ctypes.c_uint8), ctypes.byref(st))
+    if rc:
+        raise ValueError("or_run rc=%d" % rc)
+    stats = {n: getattr(st, n) for n, _ in OrStats._fields_}
+    return tc.reshape(M, N), hops.reshape(M, N), stats
+
+
+def simulate(p, stages=1, links=(50, 50, 50, 50), mode=0, sched=None, max_hb=400):
+    """Whole pipeline on the CPU: links -> topology -> mesh -> run."""
+    bl, bh, ll, lh = links
+    lat, bw = topogen_links(stages, bl, bh, ll, lh, mode)
+    stage = (np.arange(p.peers) % stages).astype(np.uint8)
+    row_ptr, col, flags = build_topology(p)
+    flags, mesh, cnt, epochs = mesh_converge(p, row_ptr, col, flags, stage, lat, max_hb)
+    t, pub, size = sched
+    tc, hops, stats = run(p, row_ptr, col, mesh, cnt, stage, lat, bw, bw, t, pub, size)
+    return dict(lat=lat, bw=bw, stage=stage, row_ptr=row_ptr, col=col, flags=flags, mesh=mesh,
+                cnt=cnt, epochs=epochs, t_complete=tc, hops=hops, stats=stats)

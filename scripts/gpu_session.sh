@@ -1,0 +1,29 @@
+#!/bin/bash
+# One gpurun session: GPU tests -> smoke -> bench -> rocprofv3 kernel trace.
+# Every GPU step has its own time limit; a fault/abort/timeout ends the session
+# (exit codes 124, 134, 137, 139), an ordinary test failure does not.
+set -u
+OUT=${OUT:-gpurun_out}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+step() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc" | tee -a "$OUT/rc.txt"
+  tail -5 "$OUT/$name.log"
+  case $rc in 124|134|137|139) echo "fatal rc=$rc in $name: stopping"; exit $rc;; esac
+  return 0
+}
+for s in ${STEPS:-tests smoke bench prof}; do
+  case $s in
+    tests) step gpu_tests 900 python -m pytest tests -m gpu -x -q ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 600 python bench.py --steps ${BENCH_STEPS:-20} --warmup 3 ;;
+    prof) step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --cpu-seconds 0 ;;
+    pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_relax -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --cpu-seconds 0 ;
+         step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_relax -d "$OUT/pmc_write" -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --cpu-seconds 0 ;;
+  esac
+done
+echo "session done"

@@ -1,0 +1,155 @@
+"""GPU parity: libgossipsim (HIP, through the C ABI) vs the CPU oracle.
+
+Bit-exact on every integer output: CSR (row_ptr, col, outbound bits), mesh,
+per-(message, peer) completion time in ns, hop count, and the counters
+(FD, R, deliveries, latency sums). Small sizes compare against the committed
+fixtures and fresh oracle runs; large sizes check size-independent properties
+plus a sample of messages against the oracle."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import gossipsim
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+T0 = gossipsim.T0_NS
+UND = np.iinfo(np.uint64).max
+
+
+def _knobs(p):
+    return {n: getattr(p, n) for n, _ in oracle.OrParams._fields_}
+
+
+def gpu_sim(p, S, links, mode=0, batch=64, max_hb=400):
+    kw = _knobs(p)
+    kw["batch"] = batch
+    sim = gossipsim.Simulator(**kw)
+    sim.set_topogen_links(S, *links, shortest=bool(mode))
+    sim.connect_gossipsub_peers()
+    ep = sim.mesh_converge(max_hb)
+    return sim, ep
+
+
+def compare(p, S, links, sched, mode=0, batch=64, ref=None):
+    sim, ep = gpu_sim(p, S, links, mode, batch)
+    if ref is None:
+        ref = oracle.simulate(p, S, links, mode=mode, sched=sched)
+    row, col, flags = sim.csr()
+    np.testing.assert_array_equal(row, ref["row_ptr"], err_msg="row_ptr")
+    np.testing.assert_array_equal(col, ref["col"], err_msg="col")
+    mesh, cnt = sim.mesh()
+    np.testing.assert_array_equal(cnt, ref["cnt"], err_msg="mesh count")
+    np.testing.assert_array_equal(mesh, ref["mesh"], err_msg="mesh")
+    np.testing.assert_array_equal(flags, ref["flags"], err_msg="flags")
+    assert ep == ref["epochs"]
+    res = sim.run(sched)
+    np.testing.assert_array_equal(res["t_complete"], ref["t_complete"], err_msg="t_complete")
+    np.testing.assert_array_equal(res["hops"], ref["hops"], err_msg="hops")
+    st = sim.stats()
+    for k in ("deliveries", "frag_deliveries", "relaxations", "bytes_alg", "latency_sum_ms",
+              "latency_max_ms", "messages"):
+        assert st[k] == ref["stats"][k], k
+    return sim, res
+
+
+def _sched(M, N, size=15000, pub0=6):
+    t = T0 + np.arange(M, dtype=np.uint64) * np.uint64(1_000_000_000)
+    return t, (pub0 + np.arange(M)) % N, np.full(M, size)
+
+
+@pytest.mark.parametrize("name", ["uniform_n300", "hetero_n400_f4", "nim_n200_cap"])
+def test_against_committed_oracle_fixtures(name):
+    meta = json.load(open(os.path.join(GOLDEN, "oracle_%s.json" % name)))
+    fx = np.load(os.path.join(GOLDEN, "oracle_%s.npz" % name))
+    p = oracle.params(**meta["params"])
+    ref = dict(row_ptr=fx["row_ptr"], col=fx["col"], flags=fx["flags"], mesh=fx["mesh"], cnt=fx["cnt"],
+               t_complete=fx["t_complete"], hops=fx["hops"], epochs=int(fx["epochs"][0]), stats=meta["stats"])
+    sched = (fx["sched_t"], fx["sched_pub"], np.full(meta["n_msgs"], meta["msg_size"]))
+    compare(p, meta["stages"], tuple(meta["links"]), sched, ref=ref)
+
+
+def test_config1_1k_peers_100_publishes():
+    """Config #1: 1k peers, D=6, 100 publishes (publisher 6+i), uniform 50 ms / 50 Mbit."""
+    for seed in (1, 2, 3):
+        p = oracle.params(peers=1000, seed=seed)
+        compare(p, 1, (50, 50, 50, 50), _sched(100, 1000), batch=100)
+
+
+@pytest.mark.parametrize("frags", [2, 3, 8])
+def test_fragments_uplink_fifo(frags):
+    p = oracle.params(peers=700, seed=11, fragments=frags)
+    compare(p, 5, (50, 150, 40, 130), _sched(12, 700), batch=5)
+
+
+def test_multi_batch_uneven_and_varying_sizes():
+    p = oracle.params(peers=900, seed=5)
+    t, pub, size = _sched(23, 900)
+    size = size.copy()
+    size[7:15] = 3000  # size change splits batches
+    compare(p, 3, (20, 200, 10, 90), (t, pub, size), batch=6)
+
+
+def test_knob_variants():
+    cases = [
+        (dict(peers=500, seed=3, muxer=1, signed_msgs=0), 2, (10, 100, 5, 50), 0),
+        (dict(peers=500, seed=4, flood_publish=0), 1, (50, 50, 50, 50), 0),
+        (dict(peers=500, seed=6, idontwant=1000), 5, (50, 150, 40, 130), 0),
+        (dict(peers=400, seed=8, dial_extra=0, max_connections=13, connect_to=8), 4, (50, 150, 40, 130), 0),
+        (dict(peers=400, seed=9, d=8, d_lo=6, d_hi=12, d_out=2), 1, (100, 100, 30, 30), 0),
+        (dict(peers=300, seed=10), 5, (50, 150, 40, 130), 1),  # Shadow shortest-path links
+        (dict(peers=64, seed=12, connect_to=3), 1, (50, 50, 50, 50), 0),
+    ]
+    for kw, S, links, mode in cases:
+        p = oracle.params(**kw)
+        compare(p, S, links, _sched(9, p.peers), mode=mode, batch=4)
+
+
+def test_fragment_collision_defect_d8():
+    p = oracle.params(peers=100, fragments=4)
+    sim, res = compare(p, 1, (50, 50, 50, 50), _sched(2, 100, size=40))
+    assert sim.stats()["deliveries"] == 0
+
+
+def test_errors_are_reported_not_hidden():
+    sim = gossipsim.Simulator(peers=100)
+    with pytest.raises(gossipsim.GossipSimError, match="GS_ESTATE"):
+        sim.run(_sched(1, 100))
+    sim.set_topogen_links()
+    sim.connect_gossipsub_peers()
+    sim.mesh_converge()
+    with pytest.raises(gossipsim.GossipSimError, match="GS_EINVAL"):
+        sim.run((np.array([T0], np.uint64), np.array([100]), np.array([15000])))
+    with pytest.raises(gossipsim.GossipSimError, match="8-byte"):
+        sim.run((np.array([T0], np.uint64), np.array([1]), np.array([7])))
+    with pytest.raises(gossipsim.GossipSimError):
+        gossipsim.Simulator(peers=10, connect_to=10)  # env.rs:73-75
+
+
+def test_large_graph_properties_and_sampled_parity():
+    """100k peers, one 64-message batch: structure invariants + 2 messages vs the oracle."""
+    N = 100_000
+    p = oracle.params(peers=N, seed=21)
+    sim, ep = gpu_sim(p, 5, (50, 150, 40, 130), batch=64)
+    row, col, flags = sim.csr()
+    mesh, cnt = sim.mesh()
+    deg = np.diff(row.astype(np.int64))
+    assert deg.min() >= 11 and (flags & 1).reshape(-1).sum() == 11 * N
+    assert cnt.min() >= p.d_lo and cnt.max() <= p.d_hi
+    sched = _sched(64, N)
+    res = sim.run(sched)
+    st = sim.stats()
+    assert st["deliveries"] == 64 * (N - 1)  # connected mesh: everyone completes
+    assert (res["hops"][res["t_complete"] != UND] < 63).all()
+    # oracle on the GPU's own graph for 2 of the 64 messages
+    lat, bw = oracle.topogen_links(5, 50, 150, 40, 130)
+    stage = (np.arange(N) % 5).astype(np.uint8)
+    for m in (0, 37):
+        tc, hp, _ = oracle.run(p, row, col, mesh, cnt, stage, lat, bw, bw, sched[0][m:m + 1],
+                               sched[1][m:m + 1], sched[2][m:m + 1])
+        np.testing.assert_array_equal(res["t_complete"][m], tc[0])
+        np.testing.assert_array_equal(res["hops"][m], hp[0])

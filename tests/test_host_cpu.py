@@ -1,0 +1,159 @@
+"""CPU tests of the product's host side: the C-ABI library loads and exports every
+symbol include/gossipsim.h declares, and its host-only helpers (wire bytes,
+topogen links, run.sh schedule, env surface, arrival-log writer) agree with the
+oracle and the reference's golden artefacts. No device compute is called."""
+import ctypes
+import glob
+import json
+import os
+import re
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+import gossipsim
+import oracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+HEADER = os.path.join(ROOT, "include", "gossipsim.h")
+REF_SHADOW = "/root/reference/shadow"
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(gs_[a-z_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = gossipsim.lib()
+    syms = declared_symbols()
+    assert len(syms) >= 19
+    for s in syms:
+        assert hasattr(L, s), s
+    assert set(syms) == set(gossipsim.SIGNATURES)
+
+
+def test_no_gpu_means_loud_failure():
+    """Without a device the product raises; there is no CPU fallback path."""
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("GPU present")
+    except ImportError:
+        pass
+    with pytest.raises(gossipsim.GossipSimError) as e:
+        gossipsim.Simulator(peers=50)
+    assert e.value.status == -3  # GS_EDEVICE
+
+
+@pytest.mark.parametrize("muxer", [0, 1, 2])
+@pytest.mark.parametrize("signed", [0, 1])
+def test_wire_bytes_match_oracle(muxer, signed):
+    for payload in [8, 11, 100, 1000, 1460, 1875, 15000, 16380, 65519, 70000, 1 << 20]:
+        assert gossipsim.wire_bytes(payload, muxer, signed) == oracle.wire_bytes(payload, muxer, signed)
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "topogen_*.json"))))
+@pytest.mark.parametrize("shortest", [False, True])
+def test_topogen_links_match_oracle_and_fixture(path, shortest):
+    fx = json.load(open(path))
+    a = {"-bl": 50, "-bh": 50, "-ll": 100, "-lh": 100, "-st": 1}
+    for i in range(0, len(fx["flags"]), 2):
+        if fx["flags"][i] in a:
+            a[fx["flags"][i]] = int(fx["flags"][i + 1])
+    S = a["-st"]
+    lat, bw = gossipsim.topogen_links(S, a["-bl"], a["-bh"], a["-ll"], a["-lh"], shortest)
+    olat, obw = oracle.topogen_links(S, a["-bl"], a["-bh"], a["-ll"], a["-lh"], 1 if shortest else 0)
+    np.testing.assert_array_equal(lat, olat)
+    np.testing.assert_array_equal(bw, obw)
+    if not shortest:
+        for s, t, l, _ in fx["edges"]:
+            if s < S and t < S:
+                assert lat[s, t] == l * 1_000_000
+
+
+def test_schedule_runsh():
+    # run.sh:34-36: publisher_id, rotation, inter_message_delay (ms)
+    sch = gossipsim.schedule_runsh(5, 100, 98, 1, 10, 1_000_000_000, 15000)
+    assert [s.publisher for s in sch] == [98, 99, 0, 1, 2]
+    assert [s.t_pub_ns for s in sch] == [10 + i * 1_000_000_000 for i in range(5)]
+    sch = gossipsim.schedule_runsh(3, 100, 4, 0, 0, 4_000_000_000, 15000)
+    assert [s.publisher for s in sch] == [4, 4, 4] and sch[2].t_pub_ns == 8_000_000_000
+
+
+def _emit_awk_fixture(tmp_path):
+    arrivals = json.load(open(os.path.join(GOLDEN, "awk_arrivals.json")))
+    txs = sorted(set(a[1] for a in arrivals))
+    peers = 13
+    sched = (gossipsim.GsPublish * len(txs))()
+    tc = np.full((len(txs), peers), np.iinfo(np.uint64).max, np.uint64)
+    for i, tx in enumerate(txs):
+        sched[i] = gossipsim.GsPublish(tx, 0, 15000)  # publisher 0 never logs (rust preset)
+        tc[i, 0] = tx
+    for peer, tx, ms in arrivals:
+        tc[txs.index(tx), peer] = tx + ms * 1_000_000 + 123_456  # sub-ms part is truncated
+    out = str(tmp_path / "latencies")
+    rc = gossipsim.lib().gs_write_latency_log(out.encode(), sched, len(txs), peers,
+                                              tc.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), 0)
+    assert rc == 0
+    return out
+
+
+def test_latency_log_matches_reference_grep_format(tmp_path):
+    out = _emit_awk_fixture(tmp_path)
+    assert open(out).read() == open(os.path.join(GOLDEN, "awk_latencies.txt")).read()
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_SHADOW) or not shutil.which("awk"),
+                    reason="reference awk scripts only in the build container")
+@pytest.mark.parametrize("script", ["summary_latency", "summary_latency_large"])
+def test_latency_log_round_trips_through_reference_awk(tmp_path, script):
+    out = _emit_awk_fixture(tmp_path)
+    got = subprocess.check_output(["awk", "-f", os.path.join(REF_SHADOW, script + ".awk"), out]).decode()
+    want = open(os.path.join(GOLDEN, "awk_latencies__%s.txt" % script)).read()
+    assert got == want
+
+
+def test_config_from_env_defaults_and_errors(monkeypatch):
+    for k in ("PEERS", "CONNECTTO", "FRAGMENTS", "MUXER", "MAXCONNECTIONS", "GOSSIPSUB_D"):
+        monkeypatch.delenv(k, raising=False)
+    c = gossipsim.PeerConfig.from_env()
+    assert (c.peers, c.connect_to, c.fragments, c.muxer) == (100, 10, 1, 0)  # env.rs:38-67
+    assert (c.d, c.d_lo, c.d_hi, c.d_out, c.d_lazy) == (6, 4, 8, 3, 6)      # main.rs:36-38,234-235
+    monkeypatch.setenv("PEERS", "2000")
+    monkeypatch.setenv("MUXER", "QUIC")
+    monkeypatch.setenv("FRAGMENTS", "8")
+    monkeypatch.setenv("GOSSIPSUB_D_HIGH", "12")
+    monkeypatch.setenv("GOSSIPSUB_GOSSIP_FACTOR", "0.5")
+    c = gossipsim.PeerConfig.from_env()
+    assert (c.peers, c.muxer, c.fragments, c.d_hi, c.gossip_factor_milli) == (2000, 1, 8, 12, 500)
+    monkeypatch.setenv("PEERS", "notanumber")  # parse().unwrap_or(100) (env.rs:38-41)
+    assert gossipsim.PeerConfig.from_env().peers == 100
+    monkeypatch.setenv("MUXER", "tcp")
+    with pytest.raises(gossipsim.GossipSimError, match="Unknown muxer type: tcp"):
+        gossipsim.PeerConfig.from_env()
+    monkeypatch.setenv("MUXER", "yamux")
+    monkeypatch.setenv("PEERS", "10")
+    monkeypatch.setenv("CONNECTTO", "10")
+    with pytest.raises(gossipsim.GossipSimError, match="Not enough peers"):
+        gossipsim.PeerConfig.from_env()
+
+
+def test_shard_messages_partition():
+    """Message sharding used by bench.py: disjoint, covering, publisher rule of run.sh."""
+    N, B, world, steps = 1000, 8, 4, 3
+    seen = []
+    for step in range(steps):
+        for rank in range(world):
+            t, pub, size = gossipsim.shard_messages(step, rank, world, B, N, 15000)
+            assert len(t) == B
+            seen.extend(zip(t.tolist(), pub.tolist()))
+    assert len(set(seen)) == steps * world * B
+    idx = sorted((t - gossipsim.T0_NS) // gossipsim.DELAY_NS for t, _ in seen)
+    assert idx == list(range(steps * world * B))
+    for t, p in seen:
+        assert p == (6 + (t - gossipsim.T0_NS) // gossipsim.DELAY_NS) % N

@@ -1,0 +1,204 @@
+"""CPU tests of the oracle (oracle/gs_oracle.c) against the reference's own
+artefacts (topogen.py outputs, committed as tests/golden/topogen_*.json) and a
+pure-Python restatement of the dissemination rules for small cases."""
+import glob
+import heapq
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+T0 = 946684800_000_000_000 + 500_000_000_000  # Shadow epoch + injector start (topogen.py:130)
+
+
+def _topogen_args(flags):
+    d = {"-n": 100, "-bl": 50, "-bh": 50, "-ll": 100, "-lh": 100, "-st": 1}  # topogen.py:15-20
+    for i in range(0, len(flags), 2):
+        if flags[i] in d:
+            d[flags[i]] = int(flags[i + 1])
+    return d
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "topogen_*.json"))))
+def test_links_match_topogen_gml(path):
+    fx = json.load(open(path))
+    a = _topogen_args(fx["flags"])
+    S = a["-st"]
+    lat, bw = oracle.topogen_links(S, a["-bl"], a["-bh"], a["-ll"], a["-lh"], mode=0)
+    for i in range(S):
+        up, dn = fx["nodes"][str(i)]
+        assert bw[i] == up * 1_000_000 == dn * 1_000_000
+    assert fx["nodes"][str(S)] == [100, 100]  # injector node (topogen.py:65)
+    seen = 0
+    for s, t, l, loss in fx["edges"]:
+        assert loss == 0.0
+        if s < S and t < S:
+            assert lat[s, t] == lat[t, s] == l * 1_000_000
+            seen += 1
+        else:
+            assert l == 1  # injector hub edges (topogen.py:66-69)
+    assert seen == S * (S + 1) // 2
+    # host -> stage (topogen.py:121-122) and the controller on the hub node
+    assert fx["host_stage"] == [i % S for i in range(a["-n"])]
+    assert fx["controller"] == S
+
+
+def test_shortest_path_mode_uses_injector_hub():
+    lat, _ = oracle.topogen_links(5, 50, 150, 40, 130, mode=1)
+    assert (lat == 2_000_000).all()  # every pair is 1 ms + 1 ms through the hub
+
+
+def test_wire_bytes_known_answers():
+    # signed RPC: from(40) + data(1+2+15000) + seqno(10) + topic(6) + sig(66) = 15125;
+    # RPC field 1+2+15125 = 15128; length prefix 2 -> frame 15130; yamux +12 -> 15142;
+    # noise +18 -> 15160; TCP/IP 11 segments x 40 -> 15600
+    assert oracle.wire_bytes(15000, 0, 1) == 15600
+    # fragment of config #2: 1875 B payload
+    frame = 1875 + 2 + 1 + 40 + 10 + 6 + 66  # data field + other fields
+    frame = 1 + 2 + frame  # RPC publish field
+    frame = 2 + frame  # length prefix
+    assert oracle.wire_bytes(1875, 0, 1) == frame + 12 + 18 + 2 * 40
+    # QUIC: 65 B per 1415 B packet
+    assert oracle.wire_bytes(15000, 1, 1) == 15130 + 11 * 65
+    # unsigned (nim anonymize): data + topic only
+    assert oracle.wire_bytes(100, 0, 0) == (1 + 1 + (1 + 1 + 100) + 6) + 1 + 12 + 18 + 40
+
+
+@pytest.mark.parametrize("name", ["uniform_n300", "hetero_n400_f4", "nim_n200_cap"])
+def test_oracle_regression_fixture(name):
+    """The oracle still reproduces its committed outputs bit for bit."""
+    meta = json.load(open(os.path.join(GOLDEN, "oracle_%s.json" % name)))
+    fx = np.load(os.path.join(GOLDEN, "oracle_%s.npz" % name))
+    p = oracle.params(**meta["params"])
+    r = oracle.simulate(p, meta["stages"], tuple(meta["links"]),
+                        sched=(fx["sched_t"], fx["sched_pub"], np.full(meta["n_msgs"], meta["msg_size"])))
+    for k in ("row_ptr", "col", "flags", "mesh", "cnt", "t_complete", "hops"):
+        np.testing.assert_array_equal(r[k], fx[k], err_msg=k)
+    assert r["stats"] == meta["stats"]
+    assert r["epochs"] == meta["epochs"]
+
+
+def _sim(N=300, seed=7, S=3, links=(30, 90, 20, 80), **kw):
+    p = oracle.params(peers=N, seed=seed, **kw)
+    M = 4
+    t = T0 + np.arange(M, dtype=np.uint64) * 1_000_000_000
+    pub = (np.arange(M) * 37 + 5) % N
+    return p, oracle.simulate(p, S, links, sched=(t, pub, np.full(M, 15000))), (t, pub)
+
+
+def test_topology_invariants():
+    p, r, _ = _sim(N=500, max_connections=0)
+    row, col, flags = r["row_ptr"].astype(np.int64), r["col"], r["flags"]
+    N = p.peers
+    k = oracle.lib().or_dials_per_peer(p)
+    assert k == 11  # CONNECTTO + 1 (main.rs:337, defect D4)
+    edges = set()
+    for u in range(N):
+        c = col[row[u]:row[u + 1]]
+        assert (np.diff(c.astype(np.int64)) > 0).all() and u not in c
+        assert (flags[row[u]:row[u + 1]] & 1).sum() == k  # u dialed exactly k peers
+        edges.update((u, int(w)) for w in c)
+    assert all((w, u) in edges for (u, w) in edges)
+
+
+def test_mesh_invariants():
+    p, r, _ = _sim(N=600)
+    row, col, flags, mesh, cnt = r["row_ptr"].astype(np.int64), r["col"], r["flags"], r["mesh"], r["cnt"]
+    N = p.peers
+    ms = [set(int(x) for x in mesh[u, :cnt[u]]) for u in range(N)]
+    for u in range(N):
+        nb = set(int(w) for w in col[row[u]:row[u + 1]])
+        assert ms[u] <= nb
+        assert p.d_lo <= len(ms[u]) <= p.d_hi
+        for w in ms[u]:
+            assert u in ms[w]  # GRAFT/PRUNE keep the mesh symmetric
+        in_mesh = set(int(col[e]) for e in range(row[u], row[u + 1]) if flags[e] & 2)
+        assert in_mesh == ms[u]
+    assert r["epochs"] < 400
+
+
+def _py_disseminate(p, r, t_pub, pub, size):
+    """Pure-Python event simulation of DESIGN.md §2.5 (small N only)."""
+    N, F = p.peers, p.fragments
+    row, col = r["row_ptr"].astype(np.int64), r["col"]
+    mesh, cnt, stage, lat, bw = r["mesh"], r["cnt"], r["stage"], r["lat"], r["bw"]
+    payload = size // F
+    wire = oracle.wire_bytes(payload, p.muxer, p.signed_msgs)
+    ser = [(-(-wire * 8_000_000_000 // int(b))) for b in bw]
+    sb = max(1, int(np.ceil(np.log2(N))))
+    best = {}
+    busy = [0] * N
+    heap = []
+    for f in range(F):
+        best[(pub, f)] = (0, 0, pub)
+    tg = [int(x) for x in col[row[pub]:row[pub + 1]]]
+    sp = stage[pub]
+    for f in range(F):
+        for j, w in enumerate(tg):
+            arr = (f * len(tg) + j + 1) * ser[sp] + int(lat[sp, stage[w]]) + max(0, ser[stage[w]] - ser[sp])
+            k = (arr, 1, pub)
+            if k < best.get((w, f), (1 << 80,)):
+                best[(w, f)] = k
+                heapq.heappush(heap, (k, w, f))
+    done = set([(pub, f) for f in range(F)])
+    while heap:
+        k, u, f = heapq.heappop(heap)
+        if (u, f) in done or best[(u, f)] != k:
+            continue
+        done.add((u, f))
+        t, h, src = k
+        su = stage[u]
+        targets = [int(w) for w in mesh[u, :cnt[u]] if w != src and w != pub]
+        start = max(t, busy[u]) if F > 1 else t
+        busy[u] = start + len(targets) * ser[su]
+        for j, w in enumerate(targets):
+            arr = start + (j + 1) * ser[su] + int(lat[su, stage[w]]) + max(0, ser[stage[w]] - ser[su])
+            nk = (arr, h + 1, u)
+            if nk < best.get((w, f), (1 << 80,)):
+                best[(w, f)] = nk
+                heapq.heappush(heap, (nk, w, f))
+    tc = np.full(N, np.iinfo(np.uint64).max, np.uint64)
+    hops = np.full(N, 255, np.uint8)
+    for u in range(N):
+        if u == pub:
+            tc[u], hops[u] = t_pub, 0
+            continue
+        ks = [best.get((u, f)) for f in range(F)]
+        if any(x is None for x in ks):
+            continue
+        mk = max(ks)
+        tc[u] = t_pub + mk[0]
+        hops[u] = mk[1]
+    return tc, hops
+
+
+@pytest.mark.parametrize("frags", [1, 3])
+def test_oracle_matches_pure_python_restatement(frags):
+    p, r, (t, pub) = _sim(N=150, fragments=frags)
+    for m in range(len(t)):
+        tc, hops = _py_disseminate(p, r, int(t[m]), int(pub[m]), 15000)
+        np.testing.assert_array_equal(r["t_complete"][m], tc)
+        np.testing.assert_array_equal(r["hops"][m], hops)
+
+
+def test_fragment_collision_defect_d8():
+    # payload 10 B with 4 fragments: fragments identical -> dedup -> never complete
+    p = oracle.params(peers=60, fragments=4)
+    r = oracle.simulate(p, 1, (50, 50, 50, 50), sched=(np.array([T0], np.uint64), np.array([3]), np.array([40])))
+    assert r["stats"]["deliveries"] == 0
+    assert r["stats"]["frag_deliveries"] == 59  # fragment 0 still spreads
+    with pytest.raises(ValueError):  # payload < 8 B: main.rs:110 would panic
+        oracle.simulate(p, 1, (50, 50, 50, 50), sched=(np.array([T0], np.uint64), np.array([3]), np.array([28])))
+
+
+def test_stats_identities():
+    p, r, _ = _sim(N=400, fragments=2)
+    st = r["stats"]
+    assert st["bytes_alg"] == 16 * st["frag_deliveries"] + 12 * st["relaxations"] + 8 * st["deliveries"]
+    delivered = (r["t_complete"] != np.iinfo(np.uint64).max).sum() - st["messages"]
+    assert st["deliveries"] == delivered
+    assert st["frag_deliveries"] == st["deliveries"] * 2
