@@ -85,6 +85,7 @@ struct Ctx {
   // dissemination (per batch)
   DevBuf<uint64_t> d_keys;   // [N * B * FP] peer-major (u, m, f)
   DevBuf<uint64_t> d_busy;   // [N * B] uplink FIFO end per (u, m) (F > 1)
+  DevBuf<uint64_t> d_meta;   // per-64-lane tile metadata (TileMeta, 16 B)
   DevBuf<uint32_t> d_pub;    // [B]
   DevBuf<uint64_t> d_tpub;   // [B]
   DevBuf<uint64_t> d_tc;     // [B * N] message-major completion times

@@ -23,157 +23,8 @@ namespace {
 
 constexpr int TB = 256;
 
-struct RelaxArgs {
-  uint64_t* keys;
-  uint64_t* busy;
-  const uint32_t* mesh;
-  const uint32_t* pub;
-  const uint8_t* stage;
-  const uint32_t* tables;  // lat[S*S] | ser_up[S] | ser_dn[S]
-  uint64_t* ctrl;
-  uint64_t* counters;
-  uint64_t total;          // N * L lanes
-  uint64_t delta;
-  uint64_t tmax;
-  uint32_t N, B, F, L, S, sb, tshift, launch, idw;
-};
+#include "gs_relax_kernel.h"
 
-__device__ __forceinline__ uint64_t wave_min(uint64_t v) {
-  for (int off = 32; off > 0; off >>= 1) {
-    const uint64_t x = __shfl_xor(v, off);
-    v = x < v ? x : v;
-  }
-  return v;
-}
-__device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-  return v;
-}
-
-template <int FP>
-__global__ __launch_bounds__(TB) void k_relax(RelaxArgs a) {
-  __shared__ uint32_t s_lat[MAX_STAGES * MAX_STAGES];
-  __shared__ uint32_t s_su[MAX_STAGES], s_sd[MAX_STAGES];
-  if (blockIdx.x == 0 && threadIdx.x == 0) a.ctrl[(a.launch + 2) % 3] = INF64;
-  const uint64_t cur = a.ctrl[a.launch % 3];
-  if (cur == INF64) return;  // grid-uniform: no pending keys left
-  const uint32_t S = a.S;
-  for (uint32_t i = threadIdx.x; i < S * S; i += TB) s_lat[i] = a.tables[i];
-  if (threadIdx.x < S) {
-    s_su[threadIdx.x] = a.tables[S * S + threadIdx.x];
-    s_sd[threadIdx.x] = a.tables[S * S + S + threadIdx.x];
-  }
-  __syncthreads();
-  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd((unsigned long long*)&a.counters[C_BUCKETS], 1ull);
-  const uint64_t lo = ((cur >> a.tshift) / a.delta) * a.delta, hi = lo + a.delta;
-  const uint64_t smask = (1ull << a.sb) - 1;
-  const uint32_t L = a.L;
-  uint64_t nmin = INF64, fd = 0, nr = 0;
-  uint32_t err = 0;
-  const uint64_t stride = (uint64_t)gridDim.x * TB;
-  for (uint64_t base = (uint64_t)blockIdx.x * TB; base < a.total; base += stride) {
-    const uint64_t gid = base + threadIdx.x;
-    const bool valid = gid < a.total;
-    const uint64_t key = valid ? a.keys[gid] : INF64;
-    const uint64_t t = key >> a.tshift;
-    const uint32_t u = valid ? (uint32_t)(gid / L) : 0;
-    const uint32_t slot = (uint32_t)(gid - (uint64_t)u * L);
-    const uint32_t m = slot / FP;
-    const uint32_t pm = valid ? a.pub[m] : EMPTY;
-    const bool pending = key != INF64;
-    const bool active = pending && t >= lo && t < hi && u != pm;
-    if (pending && t >= hi && key < nmin) nmin = key;
-    const uint32_t src = (uint32_t)(key & smask);
-    const uint32_t hp = (uint32_t)((key >> a.sb) & ((1u << HOP_BITS) - 1));
-    const uint32_t su = valid ? a.stage[u] : 0;
-    const uint32_t ser = s_su[su];
-    uint32_t row[MESH_W];
-    uint32_t skip = 0, n = 0;
-    if (active) {
-      const uint4* rp = reinterpret_cast<const uint4*>(a.mesh + (size_t)u * MESH_W);
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const uint4 x = rp[q];
-        row[4 * q] = x.x; row[4 * q + 1] = x.y; row[4 * q + 2] = x.z; row[4 * q + 3] = x.w;
-      }
-#pragma unroll
-      for (int j = 0; j < (int)MESH_W; j++) {
-        const uint32_t e = row[j];
-        if (e == EMPTY) { skip |= 1u << j; continue; }  // rows are EMPTY-padded at the tail
-        const uint32_t w = e & 0xFFFFFFu;
-        bool sk = (w == src) || (w == pm);
-        if (!sk && a.idw) {  // IDONTWANT from w already here
-          const uint64_t kw = a.keys[(size_t)w * L + slot];
-          sk = kw != INF64 && (kw >> a.tshift) + s_lat[(e >> STAGE_SHIFT) * S + su] <= t;
-        }
-        if (sk) skip |= 1u << j; else n++;
-      }
-    }
-    uint64_t start = t;
-    if constexpr (FP > 1) {
-      // Uplink FIFO across this (u, m)'s fragments: the FP lanes of the group
-      // fold max(t_f, busy) + n_f * ser in key order (all lanes shuffle).
-      const int lane = threadIdx.x & 63, gb = lane & ~(FP - 1);
-      const uint64_t ka = active ? key : INF64;
-      uint64_t kk[FP];
-      uint32_t nn[FP];
-#pragma unroll
-      for (int g = 0; g < FP; g++) { kk[g] = __shfl(ka, gb + g); nn[g] = __shfl(n, gb + g); }
-      int first = -1;
-#pragma unroll
-      for (int g = FP - 1; g >= 0; g--) if (kk[g] != INF64) first = g;
-      if (first >= 0) {
-        uint64_t cb = a.busy[(size_t)u * a.B + m];
-        uint64_t prev = 0;
-#pragma unroll
-        for (int it = 0; it < FP; it++) {
-          uint64_t bk = INF64;
-          uint32_t bn = 0;
-#pragma unroll
-          for (int g = 0; g < FP; g++)
-            if (kk[g] > prev && kk[g] < bk) { bk = kk[g]; bn = nn[g]; }
-          if (bk == INF64) continue;  // nothing left (kept unrollable: no break)
-          const uint64_t tb = bk >> a.tshift;
-          const uint64_t s = tb > cb ? tb : cb;
-          if (active && bk == key) start = s;
-          cb = s + (uint64_t)bn * ser;
-          prev = bk;
-        }
-        if (lane - gb == first) a.busy[(size_t)u * a.B + m] = cb;
-      }
-    }
-    if (active) {
-      fd++;
-      nr += n;
-      if (n && hp + 1 >= (1u << HOP_BITS)) err |= ERR_HOPS;
-      const uint64_t hbits = ((uint64_t)(hp + 1) << a.sb) | u;
-      uint32_t pos = 0;
-#pragma unroll
-      for (int j = 0; j < (int)MESH_W; j++) {
-        if (skip & (1u << j)) continue;
-        const uint32_t e = row[j];
-        const uint32_t w = e & 0xFFFFFFu, sw = e >> STAGE_SHIFT;
-        pos++;
-        const uint32_t sd = s_sd[sw];
-        const uint64_t arr = start + (uint64_t)pos * ser + s_lat[su * S + sw] + (sd > ser ? sd - ser : 0);
-        if (arr > a.tmax) err |= ERR_TIME;
-        const uint64_t nk = (arr << a.tshift) | hbits;
-        atomicMin((unsigned long long*)&a.keys[(size_t)w * L + slot], (unsigned long long)nk);
-        nmin = nk < nmin ? nk : nmin;
-      }
-    }
-  }
-  nmin = wave_min(nmin);
-  fd = wave_sum(fd);
-  nr = wave_sum(nr);
-  for (int off = 32; off > 0; off >>= 1) err |= __shfl_xor(err, off);
-  if ((threadIdx.x & 63) == 0) {
-    if (nmin != INF64) atomicMin((unsigned long long*)&a.ctrl[(a.launch + 1) % 3], (unsigned long long)nmin);
-    if (fd) atomicAdd((unsigned long long*)&a.counters[C_FD], (unsigned long long)fd);
-    if (nr) atomicAdd((unsigned long long*)&a.counters[C_R_FWD], (unsigned long long)nr);
-    if (err) atomicOr((unsigned*)&a.counters[C_ERR], err);
-  }
-}
 
 struct SeedArgs {
   uint64_t* keys;
@@ -296,20 +147,6 @@ __global__ __launch_bounds__(TB) void k_complete(CompArgs a) {
   }
 }
 
-template <int FP>
-void launch_relax(const RelaxArgs& a, unsigned grid, hipStream_t s) {
-  k_relax<FP><<<grid, TB, 0, s>>>(a);
-}
-
-void relax_dispatch(uint32_t FP, const RelaxArgs& a, unsigned grid, hipStream_t s) {
-  switch (FP) {
-    case 1: launch_relax<1>(a, grid, s); break;
-    case 2: launch_relax<2>(a, grid, s); break;
-    case 4: launch_relax<4>(a, grid, s); break;
-    case 8: launch_relax<8>(a, grid, s); break;
-    default: launch_relax<16>(a, grid, s); break;
-  }
-}
 
 uint32_t pow2_at_least(uint32_t x) { uint32_t p = 1; while (p < x) p <<= 1; return p; }
 
@@ -327,7 +164,10 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     if (sched[i].msg_size / F < 8)  // main.rs:110-111 slices buffer[..8]
       c.fail(GS_EINVAL, "fragment payload shorter than the 8-byte tx_time stamp");
   }
+  const char* var_env = getenv("GS_RELAX_VARIANT");
+  const uint32_t variant = var_env && *var_env ? (uint32_t)atoi(var_env) : 3u;
   c.d_keys.alloc((size_t)N * Bmax * FP);
+  c.d_meta.alloc(((size_t)N * Bmax * FP + 63) / 64 * sizeof(TileMeta) / 8);
   if (FP > 1) c.d_busy.alloc((size_t)N * Bmax);
   c.d_pub.alloc(Bmax);
   c.d_tpub.alloc(Bmax);
@@ -388,6 +228,7 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     const uint64_t total = (uint64_t)N * L;
     GS_HIP(hipMemsetAsync(c.d_keys.p, 0xFF, total * 8, s));
     if (FP > 1) GS_HIP(hipMemsetAsync(c.d_busy.p, 0, (size_t)N * B * 8, s));
+    if (variant & 2) GS_HIP(hipMemsetAsync(c.d_meta.p, 0, (total + 63) / 64 * sizeof(TileMeta), s));
     GS_HIP(hipMemsetAsync(c.d_ctrl.p, 0xFF, 4 * 8, s));
 
     SeedArgs sa{};
@@ -400,6 +241,7 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
 
     RelaxArgs ra{};
     ra.keys = c.d_keys.p; ra.busy = c.d_busy.p; ra.mesh = c.d_mesh.p; ra.pub = c.d_pub.p;
+    ra.meta = reinterpret_cast<TileMeta*>(c.d_meta.p);
     ra.stage = c.d_stage.p; ra.tables = c.d_tables.p; ra.ctrl = c.d_ctrl.p;
     ra.counters = c.d_counters.p; ra.total = total; ra.delta = delta; ra.tmax = tmax;
     ra.N = N; ra.B = B; ra.F = F; ra.L = L; ra.S = S; ra.sb = sb; ra.tshift = tshift;
@@ -413,11 +255,11 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
         ra.launch = launch++;
         if (c.timing) {
           GS_HIP(hipEventRecord(ev(n_ev), s));
-          relax_dispatch(FP, ra, grid, s);
+          relax_dispatch(FP, variant, ra, grid, s);
           GS_HIP(hipEventRecord(ev(n_ev + 1), s));
           n_ev += 2;
         } else {
-          relax_dispatch(FP, ra, grid, s);
+          relax_dispatch(FP, variant, ra, grid, s);
         }
       }
       GS_HIP(hipGetLastError());

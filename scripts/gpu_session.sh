@@ -22,6 +22,7 @@ for s in ${STEPS:-tests smoke bench prof}; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --steps ${BENCH_STEPS:-20} --warmup 3 ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --cpu-seconds 0 ;;
+    ab) step ab_relax 600 python scripts/ab_relax.py ;;
     pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_relax -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --cpu-seconds 0 ;
          step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_relax -d "$OUT/pmc_write" -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --cpu-seconds 0 ;;
   esac

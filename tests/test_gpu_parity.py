@@ -153,3 +153,13 @@ def test_large_graph_properties_and_sampled_parity():
                                sched[1][m:m + 1], sched[2][m:m + 1])
         np.testing.assert_array_equal(res["t_complete"][m], tc[0])
         np.testing.assert_array_equal(res["hops"][m], hp[0])
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+def test_relax_kernel_variants_exact(variant, monkeypatch):
+    """Every k_relax variant (read-filter / tile-skip on/off) is bit-exact."""
+    monkeypatch.setenv("GS_RELAX_VARIANT", str(variant))
+    p = oracle.params(peers=2000, seed=31, fragments=2)
+    compare(p, 5, (50, 150, 40, 130), _sched(40, 2000), batch=16)
+    p = oracle.params(peers=3000, seed=32)
+    compare(p, 3, (20, 200, 10, 90), _sched(70, 3000), batch=64)
