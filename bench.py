@@ -33,7 +33,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--peers", type=int, default=1_000_000)
-    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--fragments", type=int, default=1)
     ap.add_argument("--msg-size", type=int, default=15000)
     ap.add_argument("--links", default="5,50,150,40,130", help="stages,bl,bh,ll,lh (topogen.py)")
@@ -147,7 +147,7 @@ def main():
                                          st["bytes_alg"]], SUM)
     deliveries = tot[0]
 
-    launches = max(1, st["relax_launches"])
+    launches = max(1, st["relax_launches"])  # one launch = one bucket = k_scan + k_frontier
     achieved = st["relax_bytes_alg"] / (st["relax_ms"] / 1e3) / 1e9 if st["relax_ms"] > 0 else None
     traffic = None
     if os.path.exists(args.traffic_json):
@@ -159,9 +159,14 @@ def main():
             traffic = None
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
-            "kernel": "k_relax<1> (Delta-bucket relaxation)",
+            "kernel": "Delta-bucket relaxation = k_scan<1,false> + k_frontier<1,true,false>",
             "alg_bytes_per_launch": st["relax_bytes_alg"] / launches,
-            "avg_launch_us": st["relax_ms"] * 1e3 / launches, "launches": st["relax_launches"]}
+            "avg_launch_us": st["relax_ms"] * 1e3 / launches,
+            "avg_scan_us": st["scan_ms"] * 1e3 / launches,
+            "avg_frontier_us": st["frontier_ms"] * 1e3 / launches,
+            "launches": st["relax_launches"],
+            "timing": "HIP events on the library stream around every bucket's two launches",
+            "pushes_per_relaxation": st["pushes"] / max(1, st["relaxations"])}
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:

@@ -50,7 +50,7 @@ struct DevBuf {
 // Counters written by kernels: index constants into Ctx::d_counters.
 enum : uint32_t {
   C_FD = 0, C_R = 1, C_DELIV = 2, C_LAT_SUM = 3, C_LAT_MAX = 4, C_BUCKETS = 5,
-  C_R_FWD = 6, C_MESH_CHANGES = 7, C_MESH_WAKE = 8, C_ERR = 9, C_COUNT = 16
+  C_R_FWD = 6, C_MESH_CHANGES = 7, C_MESH_WAKE = 8, C_ERR = 9, C_PUSH = 10, C_COUNT = 16
 };
 
 struct Ctx {
@@ -86,10 +86,18 @@ struct Ctx {
   DevBuf<uint64_t> d_keys;   // [N * B * FP] peer-major (u, m, f)
   DevBuf<uint64_t> d_busy;   // [N * B] uplink FIFO end per (u, m) (F > 1)
   DevBuf<uint64_t> d_meta;   // per-64-lane tile metadata (TileMeta, 16 B)
+  DevBuf<uint64_t> d_fbits;  // final bitset, one u64 per 64-lane tile
+  DevBuf<uint32_t> d_fr_idx; // bucket frontier (per-scan-wave segments)
+  DevBuf<uint64_t> d_fr_key;
+  DevBuf<uint32_t> d_fr_cnt;
+  DevBuf<uint64_t> d_tmin;   // split tile skip: min pending key per tile
+  DevBuf<uint8_t> d_touched; // split tile skip: pushed since last scan
   DevBuf<uint32_t> d_pub;    // [B]
   DevBuf<uint64_t> d_tpub;   // [B]
-  DevBuf<uint64_t> d_tc;     // [B * N] message-major completion times
-  DevBuf<uint8_t> d_hops;    // [B * N]
+  DevBuf<uint64_t> d_tc;     // [N * B] peer-major completion times (device result)
+  DevBuf<uint8_t> d_hops;    // [N * B]
+  DevBuf<uint64_t> d_tc_t;   // [B * N] message-major staging for the caller's sink
+  DevBuf<uint8_t> d_hops_t;
   DevBuf<uint32_t> d_tables; // lat[S*S] | ser_up[S] | ser_dn[S] (u32 ns)
   DevBuf<uint64_t> d_ctrl;   // [4] triple-buffered next-min keys + spare
   DevBuf<uint64_t> d_counters;  // [C_COUNT]

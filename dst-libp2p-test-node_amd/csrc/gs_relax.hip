@@ -84,55 +84,46 @@ struct CompArgs {
   const uint64_t* keys;
   const uint32_t* pub;
   const uint64_t* tpub;
-  uint64_t* tc;     // [B][N]
-  uint8_t* hops;    // [B][N]
+  uint64_t* tc;     // [N][B] peer-major, like the keys
+  uint8_t* hops;    // [N][B]
   uint64_t* counters;
   uint32_t N, B, F, FP, L, sb, tshift, collide;
 };
 
 // Reassembly (main.rs:79-99): completion = max over fragments of the first
-// arrival; transposed through LDS so both the key reads (peer-major) and the
-// result writes (message-major) are coalesced.
+// arrival. keys[(u*B + m)*FP + f] -> tc[u*B + m]: one coalesced stream (a
+// message-major write would put ~1000 resident blocks on 64 rows 8 MB apart
+// each and thrash the TLB; the transpose runs only when results are copied out).
+template <int FP>
 __global__ __launch_bounds__(TB) void k_complete(CompArgs a) {
-  __shared__ uint64_t s_tc[64][65];
-  __shared__ uint8_t s_h[64][68];
-  const uint32_t u0 = blockIdx.x * 64, m0 = blockIdx.y * 64;
-  const uint32_t nu = min(64u, a.N - u0), nm = min(64u, a.B - m0);
+  const uint64_t total = (uint64_t)a.N * a.B;
   uint64_t deliv = 0, lsum = 0, lmax = 0;
-  for (uint32_t i = threadIdx.x; i < nu * nm; i += TB) {
-    const uint32_t pu = i / nm, qm = i % nm, u = u0 + pu, m = m0 + qm;
-    const uint64_t* kp = a.keys + (size_t)u * a.L + (size_t)m * a.FP;
+  for (uint64_t i = (uint64_t)blockIdx.x * TB + threadIdx.x; i < total; i += (uint64_t)gridDim.x * TB) {
+    const uint32_t u = (uint32_t)(i / a.B), m = (uint32_t)(i - (uint64_t)u * a.B);
+    const uint64_t* kp = a.keys + i * FP;
+    uint64_t mk = 0;
+    bool ok = true;
+#pragma unroll
+    for (int f = 0; f < FP; f++) {  // padded fragments are INF: only f < F count
+      const uint64_t x = f < (int)a.F ? kp[f] : 0;
+      ok &= x != INF64;
+      mk = x > mk ? x : mk;
+    }
     uint64_t tc = INF64;
     uint8_t h = 0xFF;
-    if (u == a.pub[m]) { tc = a.tpub[m]; h = 0; }
-    else if (!a.collide) {
-      uint64_t mk = 0;
-      bool ok = true;
-      for (uint32_t f = 0; f < a.F; f++) {
-        const uint64_t k = kp[f];
-        ok &= k != INF64;
-        mk = k > mk ? k : mk;
-      }
-      if (ok) {
-        const uint64_t trel = mk >> a.tshift;
-        tc = a.tpub[m] + trel;
-        h = (uint8_t)((mk >> a.sb) & ((1u << HOP_BITS) - 1));
-        const uint64_t ms = trel / 1000000ull;
-        deliv++;
-        lsum += ms;
-        lmax = ms > lmax ? ms : lmax;
-      }
+    const uint64_t tp = a.tpub[m];
+    if (u == a.pub[m]) { tc = tp; h = 0; }
+    else if (!a.collide && ok) {
+      const uint64_t trel = mk >> a.tshift;
+      tc = tp + trel;
+      h = (uint8_t)((mk >> a.sb) & ((1u << HOP_BITS) - 1));
+      const uint64_t ms = trel / 1000000ull;
+      deliv++;
+      lsum += ms;
+      lmax = ms > lmax ? ms : lmax;
     }
-    s_tc[qm][pu] = tc;
-    s_h[qm][pu] = h;
-  }
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < nm * 64; i += TB) {
-    const uint32_t qm = i >> 6, pu = i & 63;
-    if (pu < nu) {
-      a.tc[(size_t)(m0 + qm) * a.N + u0 + pu] = s_tc[qm][pu];
-      a.hops[(size_t)(m0 + qm) * a.N + u0 + pu] = s_h[qm][pu];
-    }
+    a.tc[i] = tc;
+    a.hops[i] = h;
   }
   deliv = wave_sum(deliv);
   lsum = wave_sum(lsum);
@@ -147,6 +138,34 @@ __global__ __launch_bounds__(TB) void k_complete(CompArgs a) {
   }
 }
 
+
+// [N][B] -> [B][N] through a 64x64 LDS tile, for the caller's message-major
+// sink (include/gossipsim.h); not on the device-resident path.
+__global__ __launch_bounds__(TB) void k_transpose(const uint64_t* __restrict__ tc, const uint8_t* __restrict__ hp,
+                                                  uint64_t* __restrict__ tc_t, uint8_t* __restrict__ hp_t,
+                                                  uint32_t N, uint32_t B) {
+  __shared__ uint64_t s_tc[64][65];
+  __shared__ uint8_t s_h[64][68];
+  const uint32_t u0 = blockIdx.x * 64, m0 = blockIdx.y * 64;
+  const uint32_t nu = min(64u, N - u0), nm = min(64u, B - m0);
+  for (uint32_t i = threadIdx.x; i < 64 * 64; i += TB) {
+    const uint32_t pu = i >> 6, qm = i & 63;
+    if (pu < nu && qm < nm) {
+      const size_t src = (size_t)(u0 + pu) * B + m0 + qm;
+      s_tc[qm][pu] = tc[src];
+      s_h[qm][pu] = hp[src];
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < 64 * 64; i += TB) {
+    const uint32_t qm = i >> 6, pu = i & 63;
+    if (pu < nu && qm < nm) {
+      const size_t dst = (size_t)(m0 + qm) * N + u0 + pu;
+      tc_t[dst] = s_tc[qm][pu];
+      hp_t[dst] = s_h[qm][pu];
+    }
+  }
+}
 
 uint32_t pow2_at_least(uint32_t x) { uint32_t p = 1; while (p < x) p <<= 1; return p; }
 
@@ -165,9 +184,12 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       c.fail(GS_EINVAL, "fragment payload shorter than the 8-byte tx_time stamp");
   }
   const char* var_env = getenv("GS_RELAX_VARIANT");
-  const uint32_t variant = var_env && *var_env ? (uint32_t)atoi(var_env) : 3u;
+  uint32_t variant = var_env && *var_env ? (uint32_t)atoi(var_env) : 13u;  // split + final bitset + read filter
+  if ((uint64_t)N * Bmax * FP >= (1ull << 32)) variant &= ~8u;  // frontier indices are u32
+  const size_t max_tiles = ((size_t)N * Bmax * FP + 63) / 64;
   c.d_keys.alloc((size_t)N * Bmax * FP);
-  c.d_meta.alloc(((size_t)N * Bmax * FP + 63) / 64 * sizeof(TileMeta) / 8);
+  c.d_meta.alloc(max_tiles * sizeof(TileMeta) / 8);
+  c.d_fbits.alloc(max_tiles);
   if (FP > 1) c.d_busy.alloc((size_t)N * Bmax);
   c.d_pub.alloc(Bmax);
   c.d_tpub.alloc(Bmax);
@@ -229,6 +251,13 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     GS_HIP(hipMemsetAsync(c.d_keys.p, 0xFF, total * 8, s));
     if (FP > 1) GS_HIP(hipMemsetAsync(c.d_busy.p, 0, (size_t)N * B * 8, s));
     if (variant & 2) GS_HIP(hipMemsetAsync(c.d_meta.p, 0, (total + 63) / 64 * sizeof(TileMeta), s));
+    if (variant & 12) GS_HIP(hipMemsetAsync(c.d_fbits.p, 0, (total + 63) / 64 * 8, s));
+    if ((variant & 10) == 10) {  // split + tile skip: tmin 0 forces every tile's first scan
+      c.d_tmin.alloc(max_tiles);
+      c.d_touched.alloc(max_tiles);
+      GS_HIP(hipMemsetAsync(c.d_tmin.p, 0, (total + 63) / 64 * 8, s));
+      GS_HIP(hipMemsetAsync(c.d_touched.p, 0, (total + 63) / 64, s));
+    }
     GS_HIP(hipMemsetAsync(c.d_ctrl.p, 0xFF, 4 * 8, s));
 
     SeedArgs sa{};
@@ -242,22 +271,40 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     RelaxArgs ra{};
     ra.keys = c.d_keys.p; ra.busy = c.d_busy.p; ra.mesh = c.d_mesh.p; ra.pub = c.d_pub.p;
     ra.meta = reinterpret_cast<TileMeta*>(c.d_meta.p);
+    ra.fbits = c.d_fbits.p;
+    ra.tmin = c.d_tmin.p;
+    ra.touched = c.d_touched.p;
     ra.stage = c.d_stage.p; ra.tables = c.d_tables.p; ra.ctrl = c.d_ctrl.p;
     ra.counters = c.d_counters.p; ra.total = total; ra.delta = delta; ra.tmax = tmax;
     ra.N = N; ra.B = B; ra.F = F; ra.L = L; ra.S = S; ra.sb = sb; ra.tshift = tshift;
     ra.idw = (c.cfg.idontwant && payload >= c.cfg.idontwant) ? 1 : 0;
     const uint64_t need = (total + TB - 1) / TB;
     const unsigned grid = (unsigned)std::min<uint64_t>(need, (uint64_t)dev_cus * 16);
+    if (variant & 8) {  // frontier segments: one per scan wave
+      const uint64_t nwaves = (uint64_t)grid * (TB / 64), ntiles = (total + 63) / 64;
+      ra.seg_cap = (uint32_t)(((ntiles + nwaves - 1) / nwaves) * (64 / FP));
+      c.d_fr_idx.alloc(nwaves * ra.seg_cap);
+      if (FP == 1) c.d_fr_key.alloc(nwaves * ra.seg_cap);
+      c.d_fr_cnt.alloc(nwaves);
+      ra.fr_idx = c.d_fr_idx.p;
+      ra.fr_key = c.d_fr_key.p;
+      ra.fr_cnt = c.d_fr_cnt.p;
+    }
     uint32_t launch = 0;
     const uint32_t chunk = 8;
     for (;;) {
       for (uint32_t q = 0; q < chunk; q++) {
         ra.launch = launch++;
-        if (c.timing) {
+        if (c.timing) {  // (start, scan end, end) per bucket
           GS_HIP(hipEventRecord(ev(n_ev), s));
-          relax_dispatch(FP, variant, ra, grid, s);
-          GS_HIP(hipEventRecord(ev(n_ev + 1), s));
-          n_ev += 2;
+          const hipEvent_t mid = ev(n_ev + 1);
+          if (variant & 8) relax_dispatch(FP, variant, ra, grid, s, mid);
+          else {
+            relax_dispatch(FP, variant, ra, grid, s);
+            GS_HIP(hipEventRecord(mid, s));
+          }
+          GS_HIP(hipEventRecord(ev(n_ev + 2), s));
+          n_ev += 3;
         } else {
           relax_dispatch(FP, variant, ra, grid, s);
         }
@@ -273,14 +320,27 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     ca.keys = c.d_keys.p; ca.pub = c.d_pub.p; ca.tpub = c.d_tpub.p; ca.tc = c.d_tc.p;
     ca.hops = c.d_hops.p; ca.counters = c.d_counters.p; ca.N = N; ca.B = B; ca.F = F;
     ca.FP = FP; ca.L = L; ca.sb = sb; ca.tshift = tshift; ca.collide = collide ? 1 : 0;
-    dim3 cg((N + 63) / 64, (B + 63) / 64);
-    k_complete<<<cg, TB, 0, s>>>(ca);
+    const unsigned cgrid = (unsigned)std::min<uint64_t>(((uint64_t)N * B + TB - 1) / TB, (uint64_t)dev_cus * 16);
+    switch (FP) {
+      case 1: k_complete<1><<<cgrid, TB, 0, s>>>(ca); break;
+      case 2: k_complete<2><<<cgrid, TB, 0, s>>>(ca); break;
+      case 4: k_complete<4><<<cgrid, TB, 0, s>>>(ca); break;
+      case 8: k_complete<8><<<cgrid, TB, 0, s>>>(ca); break;
+      default: k_complete<16><<<cgrid, TB, 0, s>>>(ca); break;
+    }
     GS_HIP(hipGetLastError());
-    if (sink && sink->t_complete_ns)
-      GS_HIP(hipMemcpyAsync(sink->t_complete_ns + i0 * N, c.d_tc.p, (size_t)B * N * 8,
-                            hipMemcpyDeviceToHost, s));
-    if (sink && sink->hops)
-      GS_HIP(hipMemcpyAsync(sink->hops + i0 * N, c.d_hops.p, (size_t)B * N, hipMemcpyDeviceToHost, s));
+    if (sink && (sink->t_complete_ns || sink->hops)) {  // message-major copy-out
+      c.d_tc_t.alloc((size_t)N * Bmax);
+      c.d_hops_t.alloc((size_t)N * Bmax);
+      dim3 tg((N + 63) / 64, (B + 63) / 64);
+      k_transpose<<<tg, TB, 0, s>>>(c.d_tc.p, c.d_hops.p, c.d_tc_t.p, c.d_hops_t.p, N, B);
+      GS_HIP(hipGetLastError());
+      if (sink->t_complete_ns)
+        GS_HIP(hipMemcpyAsync(sink->t_complete_ns + i0 * N, c.d_tc_t.p, (size_t)B * N * 8,
+                              hipMemcpyDeviceToHost, s));
+      if (sink->hops)
+        GS_HIP(hipMemcpyAsync(sink->hops + i0 * N, c.d_hops_t.p, (size_t)B * N, hipMemcpyDeviceToHost, s));
+    }
     c.stats.messages += B;
     i0 = i1;
   }
@@ -298,14 +358,19 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
   c.stats.buckets = h[C_BUCKETS];
   c.stats.bytes_alg = 16 * h[C_FD] + 12 * c.stats.relaxations + 8 * h[C_DELIV];
   c.stats.relax_bytes_alg = 16 * h[C_FD] + 12 * h[C_R_FWD];
+  c.stats.pushes = h[C_PUSH];
   if (c.timing) {
-    double ms = 0;
-    for (size_t q = 2; q + 1 < n_ev; q += 2) {
-      float x = 0;
+    double scan = 0, front = 0;
+    for (size_t q = 2; q + 2 < n_ev; q += 3) {
+      float x = 0, y = 0;
       GS_HIP(hipEventElapsedTime(&x, c.ev_pool[q], c.ev_pool[q + 1]));
-      ms += x;
+      GS_HIP(hipEventElapsedTime(&y, c.ev_pool[q + 1], c.ev_pool[q + 2]));
+      scan += x;
+      front += y;
     }
-    c.stats.relax_ms += ms;
+    c.stats.relax_ms += scan + front;
+    c.stats.scan_ms += scan;
+    c.stats.frontier_ms += front;
     float rm = 0;
     GS_HIP(hipEventElapsedTime(&rm, c.ev_pool[0], c.ev_pool[1]));
     c.stats.run_ms += rm;

@@ -58,7 +58,8 @@ class GsStats(ctypes.Structure):
     _fields_ = [(n, u64) for n in (
         "messages", "deliveries", "frag_deliveries", "relaxations", "bytes_alg",
         "latency_sum_ms", "latency_max_ms", "relax_launches", "buckets")] + [
-        ("relax_ms", ctypes.c_double), ("run_ms", ctypes.c_double), ("relax_bytes_alg", u64)]
+        ("relax_ms", ctypes.c_double), ("run_ms", ctypes.c_double), ("relax_bytes_alg", u64),
+        ("pushes", u64), ("scan_ms", ctypes.c_double), ("frontier_ms", ctypes.c_double)]
 
 
 # Every symbol include/gossipsim.h declares, with its ctypes signature.

@@ -113,6 +113,10 @@ typedef struct gs_stats {
     double   relax_ms;          /* device time of relaxation launches (timing on)      */
     double   run_ms;            /* device time of whole gs_run calls (timing on)       */
     uint64_t relax_bytes_alg;   /* 16*FD + 12*R_forward: algorithmic bytes of relax    */
+    uint64_t pushes;            /* atomicMin pushes issued (forward sends not dropped  */
+                                /* because the target was already final)              */
+    double   scan_ms;           /* relax_ms split: bucket scan + compaction kernel     */
+    double   frontier_ms;       /* relax_ms split: frontier forwarding kernel          */
 } gs_stats;
 
 /* ---- host-only helpers (no device work) ---------------------------------- */

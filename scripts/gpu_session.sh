@@ -1,7 +1,9 @@
 #!/bin/bash
-# One gpurun session: GPU tests -> smoke -> bench -> rocprofv3 kernel trace.
+# One gpurun session: GPU tests -> smoke -> bench -> rocprofv3 kernel trace -> PMC.
 # Every GPU step has its own time limit; a fault/abort/timeout ends the session
 # (exit codes 124, 134, 137, 139), an ordinary test failure does not.
+# PMC counters run in their own passes (FETCH_SIZE and WRITE_SIZE cannot share
+# one pass on gfx950) and never together with tracing.
 set -u
 OUT=${OUT:-gpurun_out}
 mkdir -p "$OUT"
@@ -16,15 +18,17 @@ step() {  # name seconds cmd...
   case $rc in 124|134|137|139) echo "fatal rc=$rc in $name: stopping"; exit $rc;; esac
   return 0
 }
+PROFARGS="--steps ${PROF_STEPS:-6} --warmup 2 --cpu-seconds 0"
+KRE="k_scan|k_frontier|k_complete"
 for s in ${STEPS:-tests smoke bench prof}; do
   case $s in
     tests) step gpu_tests 900 python -m pytest tests -m gpu -x -q ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --steps ${BENCH_STEPS:-20} --warmup 3 ;;
-    prof) step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --cpu-seconds 0 ;;
-    ab) step ab_relax 600 python scripts/ab_relax.py ;;
-    pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_relax -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --cpu-seconds 0 ;
-         step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_relax -d "$OUT/pmc_write" -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --cpu-seconds 0 ;;
+    prof) step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py $PROFARGS ;;
+    ab) step ab_relax 600 python scripts/ab_relax.py ${AB_ARGS:-} ;;
+    pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KRE" -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py $PROFARGS ;
+         step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KRE" -d "$OUT/pmc_write" -o run --output-format csv -- python bench.py $PROFARGS ;;
   esac
 done
 echo "session done"
