@@ -22,7 +22,7 @@ constexpr uint32_t MAX_DEG = 256;     // per-row working sets of the mesh kernel
 constexpr uint32_t MAX_FRAGS = 16;    // FRAGMENTS (topogen allows 1..9)
 constexpr uint32_t STAGE_SHIFT = 24;  // packed mesh entry: stage << 24 | peer
 
-enum : uint32_t { P_DIAL = 1, P_DIAL_ORDER = 2, P_GRAFT = 3, P_PRUNE = 4, P_OUT_GRAFT = 5 };
+enum : uint32_t { P_DIAL = 1, P_DIAL_ORDER = 2, P_GRAFT = 3, P_PRUNE = 4, P_OUT_GRAFT = 5, P_GOSSIP = 6 };
 enum : uint8_t { F_OUT = 1, F_MESH = 2 };
 enum : uint8_t { PR_GRAFT = 1, PR_PRUNE = 2, PR_ACCEPT = 4 };
 

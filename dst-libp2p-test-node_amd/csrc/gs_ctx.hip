@@ -203,7 +203,6 @@ extern "C" gs_status gs_run(gs_ctx* ctx, const gs_publish* sched, uint64_t n_msg
   GS_API_BEGIN(ctx)
   if (!ctx->mesh_built) ctx->fail(GS_ESTATE, "gs_mesh_converge first");
   if (!sched && n_msgs) ctx->fail(GS_EINVAL, "null schedule");
-  if (ctx->cfg.lazy_gossip) ctx->fail(GS_EUNSUPPORTED, "lazy IHAVE/IWANT gossip not implemented yet");
   GS_HIP(hipSetDevice(ctx->cfg.device));
   if (n_msgs) run_messages(*ctx, sched, n_msgs, sink);
   GS_API_END(ctx)

@@ -36,7 +36,9 @@ extern "C" void gs_config_default(gs_config* c) {
   c->self_log = 0;                // rust: no self delivery
   c->seed = 1;
   c->device = 0;
-  c->batch = 64;
+  c->batch = 1024;
+  c->history_gossip = 3;          // libp2p-gossipsub default (not overridden, main.rs:223-241)
+  c->hb_phase_ns = 0;
 }
 
 namespace {

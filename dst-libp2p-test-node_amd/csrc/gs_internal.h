@@ -50,7 +50,8 @@ struct DevBuf {
 // Counters written by kernels: index constants into Ctx::d_counters.
 enum : uint32_t {
   C_FD = 0, C_R = 1, C_DELIV = 2, C_LAT_SUM = 3, C_LAT_MAX = 4, C_BUCKETS = 5,
-  C_R_FWD = 6, C_MESH_CHANGES = 7, C_MESH_WAKE = 8, C_ERR = 9, C_PUSH = 10, C_COUNT = 16
+  C_R_FWD = 6, C_MESH_CHANGES = 7, C_MESH_WAKE = 8, C_ERR = 9, C_PUSH = 10, C_GOSSIP = 11,
+  C_COUNT = 16
 };
 
 struct Ctx {
@@ -92,6 +93,11 @@ struct Ctx {
   DevBuf<uint32_t> d_fr_cnt;
   DevBuf<uint64_t> d_tmin;   // split tile skip: min pending key per tile
   DevBuf<uint8_t> d_touched; // split tile skip: pushed since last scan
+  DevBuf<uint32_t> d_gl_idx; // lazy gossip: lanes with an IHAVE arrival in the bucket
+  DevBuf<uint32_t> d_gl_cnt;
+  DevBuf<uint64_t> d_nonfinal;  // [3]
+  DevBuf<uint64_t> d_rel0;   // [B] first heartbeat >= t_pub (relative ns)
+  DevBuf<uint64_t> d_habs0;  // [B] its absolute heartbeat index
   DevBuf<uint32_t> d_pub;    // [B]
   DevBuf<uint64_t> d_tpub;   // [B]
   DevBuf<uint64_t> d_tc;     // [N * B] peer-major completion times (device result)

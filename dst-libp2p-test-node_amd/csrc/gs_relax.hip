@@ -185,7 +185,16 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
   }
   const char* var_env = getenv("GS_RELAX_VARIANT");
   uint32_t variant = var_env && *var_env ? (uint32_t)atoi(var_env) : 13u;  // split + final bitset + read filter
-  if ((uint64_t)N * Bmax * FP >= (1ull << 32)) variant &= ~8u;  // frontier indices are u32
+  if ((uint64_t)N * Bmax * FP >= (1ull << 32)) {  // frontier indices are u32
+    if (c.cfg.lazy_gossip) c.fail(GS_EUNSUPPORTED, "lazy gossip needs peers*batch*FP < 2^32");
+    variant &= ~8u;
+  }
+  const bool gossip = c.cfg.lazy_gossip != 0;
+  if (gossip) {  // gossip runs on the split path only, without tile skip
+    variant = (variant | 8u) & ~2u;
+    const uint64_t rmax = std::max<uint64_t>(c.cfg.d_lazy, (uint64_t)c.max_degree * c.cfg.gossip_factor_milli / 1000);
+    if (rmax > GOSSIP_R_MAX) c.fail(GS_EUNSUPPORTED, "gossip fan-out above 32 targets");
+  }
   const size_t max_tiles = ((size_t)N * Bmax * FP + 63) / 64;
   c.d_keys.alloc((size_t)N * Bmax * FP);
   c.d_meta.alloc(max_tiles * sizeof(TileMeta) / 8);
@@ -197,7 +206,7 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
   c.d_hops.alloc((size_t)N * Bmax);
   c.d_tables.alloc((size_t)S * S + 2 * S);
   std::vector<uint32_t> pub(Bmax), tab((size_t)S * S + 2 * S);
-  std::vector<uint64_t> tpub(Bmax);
+  std::vector<uint64_t> tpub(Bmax), rel0(Bmax), habs0(Bmax);
   // Timing events come from a per-context pool: [0] run start, [1] run end,
   // then one (start, end) pair around every relaxation launch.
   size_t n_ev = 0;
@@ -246,6 +255,19 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     for (uint32_t q = 0; q < B; q++) { pub[q] = sched[i0 + q].publisher; tpub[q] = sched[i0 + q].t_pub_ns; }
     GS_HIP(hipMemcpyAsync(c.d_pub.p, pub.data(), B * 4, hipMemcpyHostToDevice, s));
     GS_HIP(hipMemcpyAsync(c.d_tpub.p, tpub.data(), B * 8, hipMemcpyHostToDevice, s));
+    if (gossip) {  // heartbeats at hb_phase + h*hb: first one at or after each t_pub
+      const uint64_t hb = c.cfg.heartbeat_ns, ph = c.cfg.hb_phase_ns;
+      for (uint32_t q = 0; q < B; q++) {
+        const uint64_t tp = tpub[q];
+        const uint64_t h0 = tp <= ph ? 0 : (tp - ph + hb - 1) / hb;
+        rel0[q] = ph + h0 * hb - tp;
+        habs0[q] = h0;
+      }
+      c.d_rel0.alloc(Bmax);
+      c.d_habs0.alloc(Bmax);
+      GS_HIP(hipMemcpyAsync(c.d_rel0.p, rel0.data(), B * 8, hipMemcpyHostToDevice, s));
+      GS_HIP(hipMemcpyAsync(c.d_habs0.p, habs0.data(), B * 8, hipMemcpyHostToDevice, s));
+    }
     GS_HIP(hipMemcpyAsync(c.d_tables.p, tab.data(), tab.size() * 4, hipMemcpyHostToDevice, s));
     const uint64_t total = (uint64_t)N * L;
     GS_HIP(hipMemsetAsync(c.d_keys.p, 0xFF, total * 8, s));
@@ -259,6 +281,9 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       GS_HIP(hipMemsetAsync(c.d_touched.p, 0, (total + 63) / 64, s));
     }
     GS_HIP(hipMemsetAsync(c.d_ctrl.p, 0xFF, 4 * 8, s));
+    // with gossip the first bucket is [0, Delta): the publisher's own IHAVEs
+    // can land before the first eager arrival
+    if (gossip) GS_HIP(hipMemsetAsync(c.d_ctrl.p, 0, 8, s));
 
     SeedArgs sa{};
     sa.keys = c.d_keys.p; sa.row = c.d_row.p; sa.col = c.d_col.p; sa.mesh = c.d_mesh.p;
@@ -289,6 +314,26 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       ra.fr_idx = c.d_fr_idx.p;
       ra.fr_key = c.d_fr_key.p;
       ra.fr_cnt = c.d_fr_cnt.p;
+      if (gossip) {  // gossip list: per-lane entries, one segment per scan wave
+        ra.gl_cap = (uint32_t)(((ntiles + nwaves - 1) / nwaves) * 64);
+        c.d_gl_idx.alloc(nwaves * ra.gl_cap);
+        c.d_gl_cnt.alloc(nwaves);
+        c.d_nonfinal.alloc(3);
+        GS_HIP(hipMemsetAsync(c.d_nonfinal.p, 0, 3 * 8, s));
+        ra.gl_idx = c.d_gl_idx.p;
+        ra.gl_cnt = c.d_gl_cnt.p;
+        ra.nonfinal = c.d_nonfinal.p;
+        ra.rel0 = c.d_rel0.p;
+        ra.habs0 = c.d_habs0.p;
+        ra.row = c.d_row.p;
+        ra.col = c.d_col.p;
+        ra.hb_ns = c.cfg.heartbeat_ns;
+        ra.seed = c.cfg.seed;
+        ra.gossip = 1;
+        ra.hist = c.cfg.history_gossip;
+        ra.d_lazy = c.cfg.d_lazy;
+        ra.gf_milli = c.cfg.gossip_factor_milli;
+      }
     }
     uint32_t launch = 0;
     const uint32_t chunk = 8;
@@ -351,7 +396,8 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
   if (h[C_ERR] & ERR_TIME) c.fail(GS_ERANGE, "relative arrival time overflowed the key's time field");
   if (h[C_ERR] & ERR_HOPS) c.fail(GS_ERANGE, "hop count overflowed the key's 6-bit hop field");
   c.stats.frag_deliveries = h[C_FD];
-  c.stats.relaxations = h[C_R] + h[C_R_FWD];
+  c.stats.relaxations = h[C_R] + h[C_R_FWD] + h[C_GOSSIP];
+  c.stats.gossip_iwant = h[C_GOSSIP];
   c.stats.deliveries = h[C_DELIV];
   c.stats.latency_sum_ms = h[C_LAT_SUM];
   c.stats.latency_max_ms = h[C_LAT_MAX];

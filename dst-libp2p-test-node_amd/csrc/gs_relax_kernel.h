@@ -40,6 +40,16 @@ struct RelaxArgs {
   uint32_t* fr_cnt;   // frontier: items per wave segment
   uint64_t* tmin;     // split SKIP: min pending key per tile at its last scan
   uint8_t* touched;   // split SKIP: tile received a push since its last scan
+  // lazy gossip
+  uint32_t* gl_idx;   // gossip list: lane gid with an IHAVE arrival in this bucket
+  uint32_t* gl_cnt;   // per scan wave
+  uint64_t* nonfinal; // [3] lanes not final after scan k (slot k % 3)
+  const uint64_t* rel0;   // per message: first heartbeat >= t_pub, relative ns
+  const uint64_t* habs0;  // per message: its absolute heartbeat index
+  const uint64_t* row;    // CSR (gossip targets are non-mesh connections)
+  const uint32_t* col;
+  uint64_t hb_ns, seed;
+  uint32_t gl_cap, gossip, hist, d_lazy, gf_milli;
   const uint32_t* mesh;
   const uint32_t* pub;
   const uint8_t* stage;
@@ -74,6 +84,7 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
 struct BucketLds {
   uint32_t lat[MAX_STAGES * MAX_STAGES];
   uint32_t su[MAX_STAGES], sd[MAX_STAGES];
+  uint32_t lmin[MAX_STAGES], lmax[MAX_STAGES];  // min/max latency out of each stage
 };
 
 __device__ __forceinline__ void load_tables(BucketLds& L, const RelaxArgs& a) {
@@ -82,7 +93,27 @@ __device__ __forceinline__ void load_tables(BucketLds& L, const RelaxArgs& a) {
   if (threadIdx.x < S) {
     L.su[threadIdx.x] = a.tables[S * S + threadIdx.x];
     L.sd[threadIdx.x] = a.tables[S * S + S + threadIdx.x];
+    uint32_t mn = ~0u, mx = 0;
+    for (uint32_t s = 0; s < S; s++) {
+      const uint32_t l = a.tables[threadIdx.x * S + s];
+      mn = l < mn ? l : mn;
+      mx = l > mx ? l : mx;
+    }
+    L.lmin[threadIdx.x] = mn;
+    L.lmax[threadIdx.x] = mx;
   }
+}
+
+// With gossip on, launch k+1 has nothing to do once scan k left no lane
+// non-final: every later IHAVE finds its target served.
+__device__ __forceinline__ bool gossip_done(const RelaxArgs& a) {
+  return a.gossip && a.launch > 0 && a.nonfinal[(a.launch + 2) % 3] == 0;
+}
+
+// First gossip heartbeat index j0 (relative to the message's first heartbeat
+// rel0) with T_j0 >= t: heartbeats at rel0 + j*hb.
+__device__ __forceinline__ uint64_t first_hb(uint64_t t, uint64_t rel0, uint64_t hb) {
+  return t <= rel0 ? 0 : (t - rel0 + hb - 1) / hb;
 }
 
 // Forward one lane's first arrival (key at lane gid = u*L + slot). `active`
@@ -137,21 +168,29 @@ __device__ __forceinline__ void relax_lane(const RelaxArgs& a, const BucketLds& 
 #pragma unroll
     for (int g = FP - 1; g >= 0; g--) if (kk[g] != INF64) first = g;
     if (first >= 0) {
+      // (key, fragment) order: gossip answers bypass the FIFO, so two
+      // fragments can carry equal keys; the fragment index breaks the tie
       uint64_t cb = a.busy[(size_t)u * a.B + m];
-      uint64_t prev = 0;
+      uint64_t pk = 0;
+      int pg = -1;
 #pragma unroll
       for (int it = 0; it < FP; it++) {
         uint64_t bk = INF64;
+        int bg = FP;
         uint32_t bn = 0;
 #pragma unroll
-        for (int g = 0; g < FP; g++)
-          if (kk[g] > prev && kk[g] < bk) { bk = kk[g]; bn = nn[g]; }
-        if (bk == INF64) continue;  // nothing left (kept unrollable: no break)
+        for (int g = 0; g < FP; g++) {
+          const bool after = kk[g] > pk || (kk[g] == pk && g > pg);
+          const bool better = kk[g] < bk || (kk[g] == bk && g < bg);
+          if (kk[g] != INF64 && after && better) { bk = kk[g]; bg = g; bn = nn[g]; }
+        }
+        if (bg == FP) continue;  // nothing left (kept unrollable: no break)
         const uint64_t tb = bk >> a.tshift;
         const uint64_t s = tb > cb ? tb : cb;
-        if (active && bk == key) start = s;
+        if (active && bg == lane - gb) start = s;
         cb = s + (uint64_t)bn * ser;
-        prev = bk;
+        pk = bk;
+        pg = bg;
       }
       if (lane - gb == first) a.busy[(size_t)u * a.B + m] = cb;
     }
@@ -275,21 +314,31 @@ __global__ __launch_bounds__(TB) void k_relax(RelaxArgs a) {
 // Scan: stream the keys, compact the bucket's arrivals (FP-lane groups with
 // any active lane) into this wave's frontier segment, store the final bitset,
 // reduce the next pending key.
-template <int FP, bool SKIP>
+template <int FP, bool SKIP, bool GOSSIP>
 __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
+  __shared__ BucketLds L;
   const uint32_t wave = blockIdx.x * (TB / 64) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (blockIdx.x == 0 && threadIdx.x == 0) a.ctrl[(a.launch + 2) % 3] = INF64;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    a.ctrl[(a.launch + 2) % 3] = INF64;
+    if (GOSSIP) a.nonfinal[(a.launch + 1) % 3] = 0;
+  }
   const uint64_t cur = a.ctrl[a.launch % 3];
   if (cur == INF64) return;  // the frontier kernel exits on the same word
+  if (GOSSIP && gossip_done(a)) return;
+  if constexpr (GOSSIP) {
+    load_tables(L, a);
+    __syncthreads();
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd((unsigned long long*)&a.counters[C_BUCKETS], 1ull);
   const uint64_t lo = ((cur >> a.tshift) / a.delta) * a.delta, hi = lo + a.delta;
   const uint32_t LL = a.L;
   const uint64_t ntiles = (a.total + 63) >> 6;
   const uint64_t nwaves = (uint64_t)gridDim.x * (TB / 64);
   const size_t seg = (size_t)wave * a.seg_cap;
-  uint64_t nmin = INF64;
-  uint32_t cnt = 0;
+  const size_t gseg = (size_t)wave * a.gl_cap;
+  uint64_t nmin = INF64, nonfin = 0;
+  uint32_t cnt = 0, gcnt = 0, err = 0;
   for (uint64_t tile = uniform64(wave); tile < ntiles; tile += nwaves) {
     if constexpr (SKIP) {
       // untouched since its last scan and nothing due in this bucket: the
@@ -321,6 +370,40 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
         a.touched[tile] = 0;
       }
     }
+    if constexpr (GOSSIP) {
+      // final lanes gossip at the history_gossip heartbeats T >= t; their
+      // IHAVEs reach targets at T + lat(s_v, s): list the lane if one of
+      // those can fall in [lo, hi), fold the next one >= hi into nmin
+      const bool fin = pending && t < hi;
+      nonfin += (valid && !fin && slot % FP < a.F) ? 1u : 0u;  // padded fragments never arrive
+      bool gwork = false;
+      uint64_t gnext = INF64;
+      if (fin) {
+        const uint32_t m = slot / FP, sv = a.stage[u];
+        const uint64_t r0 = a.rel0[m], lmn = L.lmin[sv], lmx = L.lmax[sv];
+        const uint64_t j0 = first_hb(t, r0, a.hb_ns);
+        const uint64_t tlast = r0 + (j0 + a.hist - 1) * a.hb_ns;
+        if (a.hist && tlast + lmx >= lo) {
+          for (uint32_t k = 0; k < a.hist; k++) {
+            const uint64_t T = r0 + (j0 + k) * a.hb_ns;
+            gwork |= (T + lmx >= lo && T + lmn < hi);
+            if (T + lmx >= hi)
+              for (uint32_t s = 0; s < a.S; s++) {
+                const uint64_t x = T + L.lat[sv * a.S + s];
+                if (x >= hi && x < gnext) gnext = x;
+              }
+          }
+        }
+      }
+      if (gnext != INF64) {
+        if (gnext > a.tmax) err |= ERR_TIME;
+        const uint64_t gk = gnext << a.tshift;
+        nmin = gk < nmin ? gk : nmin;
+      }
+      const uint64_t gm = __ballot(gwork);
+      if (gwork) a.gl_idx[gseg + gcnt + (uint32_t)__popcll(gm & ((1ull << lane) - 1))] = (uint32_t)gid;
+      gcnt += (uint32_t)__popcll(gm);
+    }
     const uint64_t am = __ballot(active);
     if (am == 0) continue;
     if constexpr (FP == 1) {
@@ -342,6 +425,116 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
   nmin = wave_min(nmin);
   if (lane == 0 && nmin != INF64)
     atomicMin((unsigned long long*)&a.ctrl[(a.launch + 1) % 3], (unsigned long long)nmin);
+  if constexpr (GOSSIP) {
+    nonfin = wave_sum(nonfin);
+    for (int off = 32; off > 0; off >>= 1) err |= __shfl_xor(err, off);
+    if (lane == 0) {
+      a.gl_cnt[wave] = gcnt;
+      if (nonfin) atomicAdd((unsigned long long*)&a.nonfinal[a.launch % 3], (unsigned long long)nonfin);
+      if (err) atomicOr((unsigned*)&a.counters[C_ERR], err);
+    }
+  }
+}
+
+// Lazy gossip of one bucket: for every listed final lane
+// (v, m, f) and each of its gossip heartbeats with an IHAVE arrival in
+// [lo, hi): recompute gossip_targets(v, h); a target w that has not seen
+// (m, f) by the IHAVE's arrival t_i sends IWANT, and v's answer is pushed with
+// key (t_i + lat(w,v) + ser_up(v) + lat(v,w) + dn, hops_v + 1, v). Deciding
+// here is exact: every key below hi is final, and every answer lands >= hi.
+constexpr uint32_t GOSSIP_R_MAX = 32;
+
+template <int FP>
+__global__ __launch_bounds__(TB) void k_gossip(RelaxArgs a) {
+  __shared__ BucketLds L;
+  const uint64_t cur = a.ctrl[a.launch % 3];
+  if (cur == INF64 || gossip_done(a)) return;
+  load_tables(L, a);
+  __syncthreads();
+  const uint64_t lo = ((cur >> a.tshift) / a.delta) * a.delta, hi = lo + a.delta;
+  const uint32_t LL = a.L, S = a.S;
+  const uint32_t wave = blockIdx.x * (TB / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const uint32_t n = __builtin_amdgcn_readfirstlane(a.gl_cnt[wave]);
+  const size_t seg = (size_t)wave * a.gl_cap;
+  const uint64_t smask = (1ull << a.sb) - 1;
+  uint64_t nmin = INF64, iw = 0;
+  uint32_t err = 0;
+  for (uint32_t i = lane; i < n; i += 64) {
+    const uint64_t gid = a.gl_idx[seg + i];
+    const uint64_t key = a.keys[gid];
+    const uint64_t t = key >> a.tshift;
+    const uint32_t u = (uint32_t)(gid / LL), slot = (uint32_t)(gid - (uint64_t)u * LL);
+    const uint32_t m = slot / FP, sv = a.stage[u];
+    const uint32_t hp = (uint32_t)((key >> a.sb) & ((1u << HOP_BITS) - 1));
+    const uint64_t ser = L.su[sv];
+    const uint64_t r0 = a.rel0[m];
+    const uint64_t j0 = first_hb(t, r0, a.hb_ns);
+    uint32_t mrow[MESH_W];
+    const uint4* rp = reinterpret_cast<const uint4*>(a.mesh + (size_t)u * MESH_W);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint4 x = rp[q];
+      mrow[4 * q] = x.x & 0xFFFFFFu; mrow[4 * q + 1] = x.y & 0xFFFFFFu;
+      mrow[4 * q + 2] = x.z & 0xFFFFFFu; mrow[4 * q + 3] = x.w & 0xFFFFFFu;
+    }
+    for (uint32_t k = 0; k < a.hist; k++) {
+      const uint64_t T = r0 + (j0 + k) * a.hb_ns;
+      if (T + L.lmax[sv] < lo || T + L.lmin[sv] >= hi) continue;
+      const uint32_t h = (uint32_t)(a.habs0[m] + j0 + k);
+      uint64_t kk[GOSSIP_R_MAX];
+      uint32_t ww[GOSSIP_R_MAX];
+      uint32_t nsel = 0, nonmesh = 0;
+      // r smallest rng(GOSSIP, u, h, w) among non-mesh connections; r depends
+      // on |non-mesh|, so keep GOSSIP_R_MAX and cut after counting
+      for (uint64_t e = a.row[u]; e < a.row[u + 1]; e++) {
+        const uint32_t w = a.col[e];
+        bool inm = false;
+#pragma unroll
+        for (int q = 0; q < (int)MESH_W; q++) inm |= mrow[q] == w;
+        if (inm) continue;
+        nonmesh++;
+        const uint64_t rk = rng(a.seed, P_GOSSIP, u, h, w);
+        if (nsel == GOSSIP_R_MAX && (kk[nsel - 1] < rk || (kk[nsel - 1] == rk && ww[nsel - 1] < w))) continue;
+        if (nsel == GOSSIP_R_MAX) nsel--;
+        int32_t j = (int32_t)nsel - 1;
+        while (j >= 0 && (kk[j] > rk || (kk[j] == rk && ww[j] > w))) { kk[j + 1] = kk[j]; ww[j + 1] = ww[j]; j--; }
+        kk[j + 1] = rk;
+        ww[j + 1] = w;
+        nsel++;
+      }
+      uint32_t r = (uint32_t)(((uint64_t)nonmesh * a.gf_milli) / 1000);
+      if (r < a.d_lazy) r = a.d_lazy;
+      if (r > nonmesh) r = nonmesh;
+      for (uint32_t q = 0; q < r; q++) {
+        const uint32_t w = ww[q], sw = a.stage[w];
+        const uint64_t ti = T + L.lat[sv * S + sw];
+        if (ti < lo || ti >= hi) continue;
+        const size_t dst = (size_t)w * LL + slot;
+        const uint64_t kw = a.keys[dst];
+        if (kw != INF64 && (kw >> a.tshift) <= ti) continue;  // already seen: no IWANT
+        iw++;
+        const uint64_t sd = L.sd[sw];
+        const uint64_t A = ti + L.lat[sw * S + sv] + ser + L.lat[sv * S + sw] + (sd > ser ? sd - ser : 0);
+        if (A > a.tmax) err |= ERR_TIME;
+        if (hp + 1 >= (1u << HOP_BITS)) err |= ERR_HOPS;
+        const uint64_t nk = (A << a.tshift) | ((uint64_t)(hp + 1) << a.sb) | u;
+        if (nk < kw) {
+          atomicMin((unsigned long long*)&a.keys[dst], (unsigned long long)nk);
+          nmin = nk < nmin ? nk : nmin;
+        }
+      }
+    }
+    (void)smask;
+  }
+  nmin = wave_min(nmin);
+  iw = wave_sum(iw);
+  for (int off = 32; off > 0; off >>= 1) err |= __shfl_xor(err, off);
+  if (lane == 0) {
+    if (nmin != INF64) atomicMin((unsigned long long*)&a.ctrl[(a.launch + 1) % 3], (unsigned long long)nmin);
+    if (iw) atomicAdd((unsigned long long*)&a.counters[C_GOSSIP], (unsigned long long)iw);
+    if (err) atomicOr((unsigned*)&a.counters[C_ERR], err);
+  }
 }
 
 // Frontier: every lane carries one compacted arrival (FP lanes per group).
@@ -349,7 +542,7 @@ template <int FP, bool FILTER, bool TOUCH>
 __global__ __launch_bounds__(TB) void k_frontier(RelaxArgs a) {
   __shared__ BucketLds L;
   const uint64_t cur = a.ctrl[a.launch % 3];
-  if (cur == INF64) return;
+  if (cur == INF64 || gossip_done(a)) return;
   load_tables(L, a);
   __syncthreads();
   const uint64_t lo = ((cur >> a.tshift) / a.delta) * a.delta, hi = lo + a.delta;
@@ -386,8 +579,9 @@ __global__ __launch_bounds__(TB) void k_frontier(RelaxArgs a) {
 template <int FP>
 void relax_fp(uint32_t variant, const RelaxArgs& a, unsigned grid, hipStream_t s, hipEvent_t mid) {
   if (variant & 8) {
-    if (variant & 2) k_scan<FP, true><<<grid, TB, 0, s>>>(a);
-    else k_scan<FP, false><<<grid, TB, 0, s>>>(a);
+    if (a.gossip) k_scan<FP, false, true><<<grid, TB, 0, s>>>(a);
+    else if (variant & 2) k_scan<FP, true, false><<<grid, TB, 0, s>>>(a);
+    else k_scan<FP, false, false><<<grid, TB, 0, s>>>(a);
     if (mid) (void)hipEventRecord(mid, s);  // splits scan / frontier time when timing
     switch (variant & 3) {
       case 0: k_frontier<FP, false, false><<<grid, TB, 0, s>>>(a); break;
@@ -395,6 +589,7 @@ void relax_fp(uint32_t variant, const RelaxArgs& a, unsigned grid, hipStream_t s
       case 2: k_frontier<FP, false, true><<<grid, TB, 0, s>>>(a); break;
       default: k_frontier<FP, true, true><<<grid, TB, 0, s>>>(a); break;
     }
+    if (a.gossip) k_gossip<FP><<<grid, TB, 0, s>>>(a);
     return;
   }
   switch (variant & 7) {

@@ -43,7 +43,7 @@ class GsConfig(ctypes.Structure):
         "muxer", "signed_msgs", "d", "d_lo", "d_hi", "d_lazy", "d_out", "gossip_factor_milli")] + [
         ("heartbeat_ns", u64), ("backoff_ns", u64)] + [
         (n, u32) for n in ("flood_publish", "idontwant", "lazy_gossip", "self_log")] + [
-        ("seed", u64), ("device", i32), ("batch", u32)]
+        ("seed", u64), ("device", i32), ("batch", u32), ("history_gossip", u32), ("hb_phase_ns", u64)]
 
 
 class GsPublish(ctypes.Structure):
@@ -59,7 +59,8 @@ class GsStats(ctypes.Structure):
         "messages", "deliveries", "frag_deliveries", "relaxations", "bytes_alg",
         "latency_sum_ms", "latency_max_ms", "relax_launches", "buckets")] + [
         ("relax_ms", ctypes.c_double), ("run_ms", ctypes.c_double), ("relax_bytes_alg", u64),
-        ("pushes", u64), ("scan_ms", ctypes.c_double), ("frontier_ms", ctypes.c_double)]
+        ("pushes", u64), ("scan_ms", ctypes.c_double), ("frontier_ms", ctypes.c_double),
+        ("gossip_iwant", u64)]
 
 
 # Every symbol include/gossipsim.h declares, with its ctypes signature.

@@ -83,6 +83,8 @@ typedef struct gs_config {
     uint64_t seed;               /* counter-RNG key (reference RNG is unseeded, main.rs:308) */
     int32_t  device;             /* HIP device ordinal                              */
     uint32_t batch;              /* messages simulated together per device batch    */
+    uint32_t history_gossip;     /* mcache windows gossiped (upstream default 3)    */
+    uint64_t hb_phase_ns;        /* heartbeats at hb_phase + h*heartbeat (absolute) */
 } gs_config;
 
 /* One publish injection (replaces POST /publish, main.rs:50-56,152-168). */
@@ -117,6 +119,7 @@ typedef struct gs_stats {
                                 /* because the target was already final)              */
     double   scan_ms;           /* relax_ms split: bucket scan + compaction kernel     */
     double   frontier_ms;       /* relax_ms split: frontier forwarding kernel          */
+    uint64_t gossip_iwant;      /* IWANT responses sent (counted in relaxations too)   */
 } gs_stats;
 
 /* ---- host-only helpers (no device work) ---------------------------------- */

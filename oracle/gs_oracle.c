@@ -394,10 +394,14 @@ int or_mesh_converge(const or_params* p, const uint64_t* row_ptr, const uint32_t
 }
 
 /* ------------------------------------------------------ dissemination ---- */
-typedef struct { uint64_t key; uint32_t dst; uint32_t frag; } ev_t;
+/* Events in time order; at equal time arrivals (type 0) precede IHAVE
+ * arrivals (type 1), so "w has seen m by t" reads w's finality at the IHAVE. */
+typedef struct { uint64_t t; uint64_t key; uint32_t dst; uint32_t frag; uint32_t type; } ev_t;
 typedef struct { ev_t* a; size_t n, cap; } heap_t;
 
 static int ev_less(const ev_t* x, const ev_t* y) {
+    if (x->t != y->t) return x->t < y->t;
+    if (x->type != y->type) return x->type < y->type;
     if (x->key != y->key) return x->key < y->key;
     if (x->dst != y->dst) return x->dst < y->dst;
     return x->frag < y->frag;
@@ -435,6 +439,32 @@ static ev_t heap_pop(heap_t* h) {
 
 static uint32_t bits_for(uint32_t n) { uint32_t b = 1; while ((1ull << b) < n) b++; return b; }
 
+enum { P_GOSSIP = 6 };
+
+/* Lazy-gossip targets of peer v at heartbeat h (libp2p-gossipsub emit_gossip,
+ * upstream, not vendored; gossip_lazy/gossip_factor at main.rs:230,235):
+ * r = max(D_lazy, floor(factor*|non-mesh|)) non-mesh peers, capped at
+ * |non-mesh|, the r smallest rng(GOSSIP, v, h, w) (ties by id). */
+static uint32_t gossip_targets(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
+                               const uint32_t* mesh, const uint8_t* cnt, uint32_t v, uint64_t h,
+                               sel_t* sel, uint32_t* out) {
+    uint32_t nc = 0;
+    for (uint64_t e = row_ptr[v]; e < row_ptr[v + 1]; e++) {
+        uint32_t w = col[e], in = 0;
+        for (uint32_t q = 0; q < cnt[v]; q++) in |= mesh[(size_t)v * MESH_W + q] == w;
+        if (in) continue;
+        sel[nc].key = or_rng(p->seed, P_GOSSIP, v, (uint32_t)h, w);
+        sel[nc].e = w;
+        nc++;
+    }
+    qsort(sel, nc, sizeof(sel_t), cmp_sel);
+    uint32_t r = (uint32_t)(((uint64_t)nc * p->gossip_factor_milli) / 1000);
+    if (r < p->d_lazy) r = p->d_lazy;
+    if (r > nc) r = nc;
+    for (uint32_t q = 0; q < r; q++) out[q] = (uint32_t)sel[q].e;
+    return r;
+}
+
 /* One publish -> receive -> forward -> reassemble pass per message:
  *  publish_new_message (main.rs:101-143): F fragments of msg_size/F bytes,
  *    byte 10 = chunk (fragments distinct only if payload > 10: defect D8),
@@ -451,18 +481,23 @@ int or_run(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
            const uint64_t* sched_t, const uint32_t* sched_pub, const uint32_t* sched_size,
            uint64_t n_msgs, uint64_t* t_complete, uint8_t* hops, or_stats* st) {
     uint32_t N = p->peers, F = p->fragments;
-    if (F == 0 || F > 16 || p->lazy_gossip) return -6;
+    if (F == 0 || F > 16) return -6;
     uint32_t sb = bits_for(N), tshift = sb + HOP_BITS;
     uint64_t tmax = (tshift >= 64) ? 0 : (UINT64_MAX >> tshift);
     uint64_t hmask = (1ull << HOP_BITS) - 1, smask = (1ull << sb) - 1;
     size_t NF = (size_t)N * F;
+    uint32_t maxdeg = 0;
+    for (uint32_t u = 0; u < N; u++)
+        if (row_ptr[u + 1] - row_ptr[u] > maxdeg) maxdeg = (uint32_t)(row_ptr[u + 1] - row_ptr[u]);
     uint64_t* best = (uint64_t*)malloc(sizeof(uint64_t) * NF);
     uint8_t* fin = (uint8_t*)malloc(NF);
     uint64_t* busy = (uint64_t*)malloc(sizeof(uint64_t) * N);
     uint64_t *su = (uint64_t*)malloc(8 * S), *sd = (uint64_t*)malloc(8 * S);
+    sel_t* gsel = (sel_t*)malloc(sizeof(sel_t) * (maxdeg + 1));
+    uint32_t* gtg = (uint32_t*)malloc(sizeof(uint32_t) * (maxdeg + 1));
     heap_t h = {0, 0, 0};
     int rc = 0;
-    if (!best || !fin || !busy || !su || !sd) { rc = -2; goto out; }
+    if (!best || !fin || !busy || !su || !sd || !gsel || !gtg) { rc = -2; goto out; }
     for (uint64_t mi = 0; mi < n_msgs; mi++) {
         uint32_t pub = sched_pub[mi];
         uint64_t payload = sched_size[mi] / F;
@@ -477,9 +512,37 @@ int or_run(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
         for (size_t i = 0; i < NF; i++) { best[i] = INF64; fin[i] = 0; }
         for (uint32_t u = 0; u < N; u++) busy[u] = 0;
         h.n = 0;
+        /* Lazy gossip of (v, f) first received at t_v (relative): IHAVE at the
+         * history_gossip heartbeats T >= t_v to gossip_targets(v, h); the
+         * IHAVE reaches w at T + lat(v,w); an IWANT comes back and v's answer
+         * lands at T + 2 lat(v,w) + lat(w,v) + ser_up(v) + dn. */
+#define SCHED_GOSSIP(v_, f_, tv_, hp_)                                                          \
+        do {                                                                                    \
+            const uint64_t tabs_ = sched_t[mi] + (tv_);                                        \
+            uint64_t h0_ = tabs_ <= p->hb_phase_ns ? 0                                          \
+                         : (tabs_ - p->hb_phase_ns + p->heartbeat_ns - 1) / p->heartbeat_ns;    \
+            const uint32_t sv_ = stage[v_];                                                     \
+            for (uint32_t k_ = 0; k_ < p->history_gossip; k_++) {                              \
+                const uint64_t hh_ = h0_ + k_;                                                  \
+                const uint64_t T_ = p->hb_phase_ns + hh_ * p->heartbeat_ns - sched_t[mi];       \
+                const uint32_t r_ = gossip_targets(p, row_ptr, col, mesh, cnt, v_, hh_, gsel, gtg); \
+                if (r_ && (hp_) + 1 > hmask) { rc = -5; goto out; }                            \
+                for (uint32_t q_ = 0; q_ < r_; q_++) {                                          \
+                    const uint32_t w_ = gtg[q_], sw_ = stage[w_];                               \
+                    const uint64_t ti_ = T_ + lat_ns[sv_ * S + sw_];                            \
+                    const uint64_t dn_ = sd[sw_] > su[sv_] ? sd[sw_] - su[sv_] : 0;             \
+                    const uint64_t A_ = ti_ + lat_ns[sw_ * S + sv_] + su[sv_] + lat_ns[sv_ * S + sw_] + dn_; \
+                    if (A_ > tmax) { rc = -5; goto out; }                                       \
+                    ev_t ge_ = {ti_, (A_ << tshift) | (((uint64_t)(hp_) + 1) << sb) | (v_), w_, (f_), 1}; \
+                    if (heap_push(&h, ge_)) { rc = -2; goto out; }                             \
+                }                                                                               \
+            }                                                                                   \
+        } while (0)
         /* publisher: self key, flood through the uplink FIFO */
         uint32_t sp = stage[pub];
         for (uint32_t f = 0; f < Fe; f++) { best[(size_t)pub * F + f] = (uint64_t)pub; fin[(size_t)pub * F + f] = 1; }
+        if (p->lazy_gossip)
+            for (uint32_t f = 0; f < Fe; f++) SCHED_GOSSIP(pub, f, 0, 0);
         const uint32_t* tgt; uint32_t deg;
         uint32_t meshrow[MESH_W];
         if (p->flood_publish) { tgt = col + row_ptr[pub]; deg = (uint32_t)(row_ptr[pub + 1] - row_ptr[pub]); }
@@ -493,12 +556,23 @@ int or_run(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
                 uint64_t key = (arr << tshift) | (1ull << sb) | pub;
                 st->relaxations++;
                 if (key < best[(size_t)w * F + f]) best[(size_t)w * F + f] = key;
-                ev_t ev = {key, w, f};
+                ev_t ev = {arr, key, w, f, 0};
                 if (heap_push(&h, ev)) { rc = -2; goto out; }
             }
         while (h.n) {
             ev_t ev = heap_pop(&h);
             size_t idx = (size_t)ev.dst * F + ev.frag;
+            if (ev.type == 1) { /* IHAVE arrives at w: IWANT unless w already has it */
+                if (fin[idx]) continue;
+                st->gossip_iwant++;
+                st->relaxations++;
+                if (ev.key < best[idx]) {
+                    best[idx] = ev.key;
+                    ev_t ne = {ev.key >> tshift, ev.key, ev.dst, ev.frag, 0};
+                    if (heap_push(&h, ne)) { rc = -2; goto out; }
+                }
+                continue;
+            }
             if (fin[idx]) continue;
             fin[idx] = 1;
             uint32_t u = ev.dst, su_ = stage[u];
@@ -516,6 +590,7 @@ int or_run(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
                 }
                 tg[n++] = w;
             }
+            if (p->lazy_gossip) SCHED_GOSSIP(u, ev.frag, t, hp);
             uint64_t start = (Fe > 1 && busy[u] > t) ? busy[u] : t;
             busy[u] = start + (uint64_t)n * su[su_];
             if (n && hp + 1 > hmask) { rc = -5; goto out; }
@@ -529,7 +604,7 @@ int or_run(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
                 size_t wi = (size_t)w * F + ev.frag;
                 if (key < best[wi]) {
                     best[wi] = key;
-                    ev_t ne = {key, w, ev.frag};
+                    ev_t ne = {arr, key, w, ev.frag, 0};
                     if (heap_push(&h, ne)) { rc = -2; goto out; }
                 }
             }
@@ -556,6 +631,7 @@ int or_run(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
     }
 out:
     st->bytes_alg = 16 * st->frag_deliveries + 12 * st->relaxations + 8 * st->deliveries;
-    free(best); free(fin); free(busy); free(su); free(sd); free(h.a);
+#undef SCHED_GOSSIP
+    free(best); free(fin); free(busy); free(su); free(sd); free(gsel); free(gtg); free(h.a);
     return rc;
 }

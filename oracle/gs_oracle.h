@@ -27,11 +27,14 @@ typedef struct or_params {
     uint64_t heartbeat_ns, backoff_ns;
     uint32_t flood_publish, idontwant, lazy_gossip, self_log;
     uint64_t seed;
+    uint32_t history_gossip;
+    uint64_t hb_phase_ns;
 } or_params;
 
 typedef struct or_stats {
     uint64_t messages, deliveries, frag_deliveries, relaxations, bytes_alg;
     uint64_t latency_sum_ms, latency_max_ms;
+    uint64_t gossip_iwant;
 } or_stats;
 
 uint64_t or_rng(uint64_t seed, uint32_t purpose, uint32_t a, uint32_t b, uint32_t c);

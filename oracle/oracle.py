@@ -29,13 +29,13 @@ class OrParams(ctypes.Structure):
         "gossip_factor_milli")] + [
         ("heartbeat_ns", ctypes.c_uint64), ("backoff_ns", ctypes.c_uint64)] + [
         (n, ctypes.c_uint32) for n in ("flood_publish", "idontwant", "lazy_gossip", "self_log")] + [
-        ("seed", ctypes.c_uint64)]
+        ("seed", ctypes.c_uint64), ("history_gossip", ctypes.c_uint32), ("hb_phase_ns", ctypes.c_uint64)]
 
 
 class OrStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in (
         "messages", "deliveries", "frag_deliveries", "relaxations", "bytes_alg",
-        "latency_sum_ms", "latency_max_ms")]
+        "latency_sum_ms", "latency_max_ms", "gossip_iwant")]
 
 
 def build(force=False):
@@ -82,7 +82,8 @@ def params(**kw):
     d = dict(peers=100, connect_to=10, dial_extra=1, max_connections=0, fragments=1,
              muxer=0, signed_msgs=1, d=6, d_lo=4, d_hi=8, d_lazy=6, d_out=3,
              gossip_factor_milli=250, heartbeat_ns=1_000_000_000, backoff_ns=60_000_000_000,
-             flood_publish=1, idontwant=0, lazy_gossip=0, self_log=0, seed=1)
+             flood_publish=1, idontwant=0, lazy_gossip=0, self_log=0, seed=1, history_gossip=3,
+             hb_phase_ns=0)
     d.update(kw)
     return OrParams(**d)
 

@@ -109,6 +109,23 @@ def test_knob_variants():
         compare(p, S, links, _sched(9, p.peers), mode=mode, batch=4)
 
 
+@pytest.mark.parametrize("frags", [1, 2, 3])
+def test_lazy_gossip_ihave_iwant(frags):
+    """A6: IHAVE/IWANT relaxations, heartbeats landing inside the dissemination
+    window (fast heartbeat + phase) so that IWANTs actually happen."""
+    p = oracle.params(peers=1500, seed=41, fragments=frags, lazy_gossip=1,
+                      heartbeat_ns=100_000_000, hb_phase_ns=37_000_000)
+    sim, res = compare(p, 3, (5, 20, 20, 80), _sched(20, 1500), batch=8)
+    st = sim.stats()
+    ref = oracle.simulate(p, 3, (5, 20, 20, 80), sched=_sched(20, 1500))
+    assert st["gossip_iwant"] == ref["stats"]["gossip_iwant"] > 0
+
+
+def test_lazy_gossip_default_heartbeat():
+    p = oracle.params(peers=3000, seed=42, lazy_gossip=1)
+    compare(p, 5, (50, 150, 40, 130), _sched(30, 3000), batch=16)
+
+
 def test_fragment_collision_defect_d8():
     p = oracle.params(peers=100, fragments=4)
     sim, res = compare(p, 1, (50, 50, 50, 50), _sched(2, 100, size=40))

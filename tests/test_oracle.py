@@ -121,20 +121,44 @@ def test_mesh_invariants():
     assert r["epochs"] < 400
 
 
+def _py_gossip_targets(p, r, v, h):
+    row, col, mesh, cnt = r["row_ptr"].astype(np.int64), r["col"], r["mesh"], r["cnt"]
+    ms = set(int(x) for x in mesh[v, :cnt[v]])
+    cand = sorted((oracle.rng(p.seed, 6, v, h & 0xFFFFFFFF, int(w)), int(w))
+                  for w in col[row[v]:row[v + 1]] if int(w) not in ms)
+    rr = max(p.d_lazy, len(cand) * p.gossip_factor_milli // 1000)
+    return [w for _, w in cand[:min(rr, len(cand))]]
+
+
 def _py_disseminate(p, r, t_pub, pub, size):
-    """Pure-Python event simulation of DESIGN.md §2.5 (small N only)."""
+    """Pure-Python event simulation of DESIGN.md §2.5-2.7 (small N only)."""
     N, F = p.peers, p.fragments
     row, col = r["row_ptr"].astype(np.int64), r["col"]
     mesh, cnt, stage, lat, bw = r["mesh"], r["cnt"], r["stage"], r["lat"], r["bw"]
     payload = size // F
     wire = oracle.wire_bytes(payload, p.muxer, p.signed_msgs)
     ser = [(-(-wire * 8_000_000_000 // int(b))) for b in bw]
-    sb = max(1, int(np.ceil(np.log2(N))))
     best = {}
     busy = [0] * N
-    heap = []
+    heap = []  # (time, type, key, dst, frag): arrivals (0) before IHAVEs (1) at equal time
+    iwant = [0]
+
+    def gossip(v, f, tv, hv):
+        tabs = t_pub + tv
+        h0 = 0 if tabs <= p.hb_phase_ns else -(-(tabs - p.hb_phase_ns) // p.heartbeat_ns)
+        sv = stage[v]
+        for k in range(p.history_gossip):
+            T = p.hb_phase_ns + (h0 + k) * p.heartbeat_ns - t_pub
+            for w in _py_gossip_targets(p, r, v, h0 + k):
+                sw = stage[w]
+                ti = T + int(lat[sv, sw])
+                A = ti + int(lat[sw, sv]) + ser[sv] + int(lat[sv, sw]) + max(0, ser[sw] - ser[sv])
+                heapq.heappush(heap, (ti, 1, (A, hv + 1, v), w, f))
+
     for f in range(F):
         best[(pub, f)] = (0, 0, pub)
+        if p.lazy_gossip:
+            gossip(pub, f, 0, 0)
     tg = [int(x) for x in col[row[pub]:row[pub + 1]]]
     sp = stage[pub]
     for f in range(F):
@@ -143,15 +167,25 @@ def _py_disseminate(p, r, t_pub, pub, size):
             k = (arr, 1, pub)
             if k < best.get((w, f), (1 << 80,)):
                 best[(w, f)] = k
-                heapq.heappush(heap, (k, w, f))
+                heapq.heappush(heap, (arr, 0, k, w, f))
     done = set([(pub, f) for f in range(F)])
     while heap:
-        k, u, f = heapq.heappop(heap)
+        _, typ, k, u, f = heapq.heappop(heap)
+        if typ == 1:
+            if (u, f) in done:
+                continue
+            iwant[0] += 1
+            if k < best.get((u, f), (1 << 80,)):
+                best[(u, f)] = k
+                heapq.heappush(heap, (k[0], 0, k, u, f))
+            continue
         if (u, f) in done or best[(u, f)] != k:
             continue
         done.add((u, f))
         t, h, src = k
         su = stage[u]
+        if p.lazy_gossip:
+            gossip(u, f, t, h)
         targets = [int(w) for w in mesh[u, :cnt[u]] if w != src and w != pub]
         start = max(t, busy[u]) if F > 1 else t
         busy[u] = start + len(targets) * ser[su]
@@ -160,7 +194,7 @@ def _py_disseminate(p, r, t_pub, pub, size):
             nk = (arr, h + 1, u)
             if nk < best.get((w, f), (1 << 80,)):
                 best[(w, f)] = nk
-                heapq.heappush(heap, (nk, w, f))
+                heapq.heappush(heap, (arr, 0, nk, w, f))
     tc = np.full(N, np.iinfo(np.uint64).max, np.uint64)
     hops = np.full(N, 255, np.uint8)
     for u in range(N):
@@ -173,16 +207,23 @@ def _py_disseminate(p, r, t_pub, pub, size):
         mk = max(ks)
         tc[u] = t_pub + mk[0]
         hops[u] = mk[1]
-    return tc, hops
+    return tc, hops, iwant[0]
 
 
-@pytest.mark.parametrize("frags", [1, 3])
-def test_oracle_matches_pure_python_restatement(frags):
-    p, r, (t, pub) = _sim(N=150, fragments=frags)
+@pytest.mark.parametrize("frags,gossip", [(1, 0), (3, 0), (1, 1), (2, 1)])
+def test_oracle_matches_pure_python_restatement(frags, gossip):
+    # slow links + a heartbeat phase inside the dissemination window so IWANTs happen
+    kw = dict(lazy_gossip=gossip, hb_phase_ns=37_000_000, heartbeat_ns=100_000_000) if gossip else {}
+    p, r, (t, pub) = _sim(N=150, fragments=frags, links=(5, 20, 20, 80), **kw)
+    iw = 0
     for m in range(len(t)):
-        tc, hops = _py_disseminate(p, r, int(t[m]), int(pub[m]), 15000)
+        tc, hops, nw = _py_disseminate(p, r, int(t[m]), int(pub[m]), 15000)
+        iw += nw
         np.testing.assert_array_equal(r["t_complete"][m], tc)
         np.testing.assert_array_equal(r["hops"][m], hops)
+    assert r["stats"]["gossip_iwant"] == iw
+    if gossip:
+        assert iw > 0
 
 
 def test_fragment_collision_defect_d8():
