@@ -6,7 +6,9 @@ roofline fraction and the CPU oracle's rate on a bounded sample.
 One step = one batch of B messages disseminated over a frozen 1M-peer mesh
 (publish -> flood -> mesh forwarding -> reassembly), inputs resident in HBM.
 Multi-GPU: one process per GPU (torchrun), each simulating its own message
-shard (weak scaling; no data-path collective).
+shard (weak scaling; no data-path collective). `--mode peer`
+instead partitions the peers across ranks and exchanges each bucket's records
+over RCCL (strong scaling of one batch, config #4).
 
     python bench.py --gpus 1 --steps 20 --warmup 3
 """
@@ -40,6 +42,10 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--max-heartbeats", type=int, default=400)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU oracle sample budget (0=off)")
+    ap.add_argument("--mode", choices=("msg", "peer"), default="msg",
+                    help="msg: message-sharded ranks (default); peer: peer-partitioned ranks")
+    ap.add_argument("--also-peers", type=int, default=100_000,
+                    help="second graph size reported beside the headline (metric names 100k & 1M; 0=off)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="per-launch HBM bytes of the relax kernel from a rocprofv3 --pmc pass")
     return ap.parse_args()
@@ -111,22 +117,31 @@ def cpu_baseline(sim, args, S, links, budget_s):
             "parity_with_gpu_on_sample": same}
 
 
-def main():
-    args = parse()
-    world, rank, local, torch, dist = dist_setup()
-    S, bl, bh, ll, lh = [int(x) for x in args.links.split(",")]
-    links = (bl, bh, ll, lh)
-    sim = gossipsim.Simulator(peers=args.peers, batch=args.batch, fragments=args.fragments,
+def make_sim(args, peers, S, links, local):
+    sim = gossipsim.Simulator(peers=peers, batch=args.batch, fragments=args.fragments,
                               seed=args.seed, device=local)
     t_setup = time.perf_counter()
-    sim.set_topogen_links(S, bl, bh, ll, lh)
+    sim.set_topogen_links(S, *links)
     sim.connect_gossipsub_peers()
     epochs = sim.mesh_converge(args.max_heartbeats)
-    t_setup = time.perf_counter() - t_setup
+    return sim, epochs, time.perf_counter() - t_setup
 
-    def step(i):
-        sim.run(gossipsim.shard_messages(i, rank, world, args.batch, args.peers, args.msg_size),
-                collect=False)
+
+def measure(args, sim, peers, world, rank, torch, dist):
+    """W untimed + K timed steps between barrier+synchronize; -> (max elapsed, stats, sums)."""
+    if args.mode == "peer":
+        import partition
+        exch = partition.DistExchange(device=torch.device("cuda", torch.cuda.current_device())) \
+            if world > 1 else partition.LoopbackExchange()
+        bufs = [partition.RecordBuffer(torch.device("cuda", sim.cfg.c.device), capacity=1 << 22)]
+
+        def step(i):  # every rank works on the same batch, each over its own peers
+            partition.run_partitioned([sim], gossipsim.shard_messages(i, 0, 1, args.batch, peers, args.msg_size),
+                                      exch, bufs=bufs, collect=False)
+    else:
+        def step(i):
+            sim.run(gossipsim.shard_messages(i, rank, world, args.batch, peers, args.msg_size),
+                    collect=False)
 
     for i in range(args.warmup):
         step(i)
@@ -145,7 +160,26 @@ def main():
     (max_elapsed,) = allreduce(torch, dist, world, [elapsed], MAX)
     tot = allreduce(torch, dist, world, [st["deliveries"], st["frag_deliveries"], st["relaxations"],
                                          st["bytes_alg"]], SUM)
+    return max_elapsed, st, tot
+
+
+def main():
+    args = parse()
+    world, rank, local, torch, dist = dist_setup()
+    S, bl, bh, ll, lh = [int(x) for x in args.links.split(",")]
+    links = (bl, bh, ll, lh)
+    sim, epochs, t_setup = make_sim(args, args.peers, S, links, local)
+    if args.mode == "peer":
+        sim.set_partition(world, rank)
+    steps = measure(args, sim, args.peers, world, rank, torch, dist)
+    max_elapsed, st, tot = steps
     deliveries = tot[0]
+    extra = None
+    if args.also_peers and args.also_peers != args.peers and args.mode == "msg":
+        sim2, _, _ = make_sim(args, args.also_peers, S, links, local)
+        e2, _, tot2 = measure(args, sim2, args.also_peers, world, rank, torch, dist)
+        extra = {"peers": args.also_peers, "value": tot2[0] / e2, "ms_per_step": e2 * 1e3 / args.steps}
+        sim2.close()
 
     launches = max(1, st["relax_launches"])  # one launch = one bucket = k_scan + k_frontier
     achieved = st["relax_bytes_alg"] / (st["relax_ms"] / 1e3) / 1e9 if st["relax_ms"] > 0 else None
@@ -169,7 +203,7 @@ def main():
             "pushes_per_relaxation": st["pushes"] / max(1, st["relaxations"])}
 
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+    if rank == 0 and world == 1 and args.cpu_seconds > 0 and args.mode == "msg":
         cpu = cpu_baseline(sim, args, S, links, args.cpu_seconds)
 
     if rank == 0:
@@ -182,16 +216,17 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": max_elapsed * 1e3 / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if args.mode == "msg" else "strong",
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic (random-ID dial graph + converged mesh, run.sh publish schedule)",
             "config": {
                 "workload": "%d peers, %d-stage topogen links (%d-%d Mbit, %d-%d ms), CONNECTTO=10, "
-                            "D=6/4/8, F=%d, %d B msgs, %d msgs/step/GPU, message-sharded"
-                            % (args.peers, S, bl, bh, ll, lh, args.fragments, args.msg_size, args.batch),
+                            "D=6/4/8, F=%d, %d B msgs, %d msgs/step%s"
+                            % (args.peers, S, bl, bh, ll, lh, args.fragments, args.msg_size, args.batch,
+                               "/GPU, message-sharded" if args.mode == "msg" else ", peer-partitioned"),
                 "peers": args.peers, "batch": args.batch, "fragments": args.fragments,
-                "msg_size": args.msg_size, "links": args.links, "parallelism": "msg-shard%d" % world,
+                "msg_size": args.msg_size, "links": args.links, "parallelism": ("msg-shard%d" if args.mode == "msg" else "peer-part%d") % world,
             },
             "deliveries": int(deliveries),
             "frag_deliveries": int(tot[1]),
@@ -200,6 +235,7 @@ def main():
             "setup_s": t_setup,
             "mesh_epochs": epochs,
             "buckets_per_step": st["buckets"] / max(1, args.steps),
+            "at_%dk_peers" % (args.also_peers // 1000) if extra else "at_second_size": extra,
             "roofline": roof,
             "cpu_baseline": cpu,
         }

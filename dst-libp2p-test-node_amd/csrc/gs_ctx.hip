@@ -228,3 +228,46 @@ extern "C" gs_status gs_set_timing(gs_ctx* ctx, uint32_t enable) {
   ctx->timing = enable != 0;
   return GS_OK;
 }
+
+// ---- peer-partitioned mode (gs_part.h) ----
+extern "C" gs_status gs_set_partition(gs_ctx* ctx, uint32_t parts, uint32_t part) {
+  GS_API_BEGIN(ctx)
+  part_set(*ctx, parts, part);
+  GS_API_END(ctx)
+}
+
+extern "C" gs_status gs_part_begin(gs_ctx* ctx, const gs_publish* sched, uint64_t n_msgs,
+                                   uint64_t* out_min_key) {
+  GS_API_BEGIN(ctx)
+  if (!ctx->mesh_built) ctx->fail(GS_ESTATE, "gs_mesh_converge first");
+  if (!sched || !out_min_key) ctx->fail(GS_EINVAL, "null schedule or output");
+  GS_HIP(hipSetDevice(ctx->cfg.device));
+  *out_min_key = part_begin(*ctx, sched, n_msgs);
+  GS_API_END(ctx)
+}
+
+extern "C" gs_status gs_part_scan(gs_ctx* ctx, uint64_t bucket_key, gs_part_record* dev_records,
+                                  uint64_t capacity, uint64_t* out_n, uint64_t* out_min_key) {
+  GS_API_BEGIN(ctx)
+  if (!out_n || !out_min_key) ctx->fail(GS_EINVAL, "null output");
+  GS_HIP(hipSetDevice(ctx->cfg.device));
+  if (!part_scan(*ctx, bucket_key, dev_records, capacity, out_n, out_min_key))
+    ctx->fail(GS_ERANGE, "record buffer too small: need " + std::to_string(*out_n) + " records");
+  GS_API_END(ctx)
+}
+
+extern "C" gs_status gs_part_relax(gs_ctx* ctx, uint64_t bucket_key, const gs_part_record* dev_records,
+                                   uint64_t n, uint64_t* out_min_key) {
+  GS_API_BEGIN(ctx)
+  if (!out_min_key) ctx->fail(GS_EINVAL, "null output");
+  GS_HIP(hipSetDevice(ctx->cfg.device));
+  *out_min_key = part_relax(*ctx, bucket_key, dev_records, n);
+  GS_API_END(ctx)
+}
+
+extern "C" gs_status gs_part_finish(gs_ctx* ctx, const gs_result_sink* sink) {
+  GS_API_BEGIN(ctx)
+  GS_HIP(hipSetDevice(ctx->cfg.device));
+  part_finish(*ctx, sink);
+  GS_API_END(ctx)
+}

@@ -54,6 +54,14 @@ enum : uint32_t {
   C_COUNT = 16
 };
 
+// Per-batch geometry (gs_relax.hip setup_batch).
+struct Batch {
+  uint32_t B = 0, L = 0, F = 0, FP = 1, sb = 0, tshift = 0, Fe = 1;
+  bool collide = false;
+  uint64_t payload = 0, tmax = 0, delta = 1;
+  std::vector<uint64_t> tpub;
+};
+
 struct Ctx {
   gs_config cfg{};
   std::string last_error;
@@ -109,6 +117,14 @@ struct Ctx {
   DevBuf<uint64_t> d_counters;  // [C_COUNT]
   uint64_t* h_pinned = nullptr; // pinned host mirror of ctrl + counters
 
+  // peer-partitioned mode (gs_part.h): this context holds keys of peers [u0, u0 + un)
+  uint32_t part_parts = 1, part_idx = 0, part_u0 = 0, part_un = 0;
+  bool part_open = false;       // between gs_part_begin and gs_part_finish
+  Batch part_b;
+  unsigned part_grid = 0;
+  uint32_t part_seg_cap = 0;
+  DevBuf<uint64_t> d_pcnt;      // [4] frontier groups, records, relax min key, spare
+
   // stats
   gs_stats stats{};
   std::vector<hipEvent_t> ev_pool;
@@ -122,6 +138,11 @@ struct Ctx {
 void launch_topology(Ctx& c);
 uint32_t run_mesh(Ctx& c, uint32_t max_heartbeats);
 void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_result_sink* sink);
+void part_set(Ctx& c, uint32_t parts, uint32_t part);
+uint64_t part_begin(Ctx& c, const gs_publish* sched, uint64_t n_msgs);
+bool part_scan(Ctx& c, uint64_t bucket_key, gs_part_record* rec, uint64_t cap, uint64_t* n, uint64_t* m1);
+uint64_t part_relax(Ctx& c, uint64_t bucket_key, const gs_part_record* rec, uint64_t n);
+void part_finish(Ctx& c, const gs_result_sink* sink);
 
 // small device helpers
 void device_exclusive_scan(Ctx& c, const uint64_t* in, uint64_t* out, uint32_t n);

@@ -1,0 +1,345 @@
+// gs_part.h — peer-partitioned dissemination.
+// Included by gs_relax.hip inside namespace gs (after the batch helpers).
+//
+// Partition `part` of P owns the keys rows of peers [u0, u0 + un); the CSR and
+// the mesh are replicated (every partition builds them identically from the
+// same seed). A Delta-bucket is split at the one place where data crosses
+// partitions — the mesh edge u -> w with u and w owned by different parts:
+//
+//   scan    (owner of u)  k_scan (shared with gs_run) streams the own keys,
+//                         compacts the bucket's arrivals and writes the final
+//                         bitset; k_pexport folds each arrival's uplink FIFO
+//                         (busy is owner-local: the FIFO is u's own uplink)
+//                         and emits one 24-B record {key, start, u, slot} per
+//                         arrival with at least one forward target.
+//   exchange (caller)     all-gather of every part's records (RCCL / loopback).
+//   relax   (owner of w)  k_precv re-walks u's mesh row from the record (same
+//                         target order and position counter as relax_lane, so
+//                         arrival = start + pos*ser + lat + max(0, dn - ser)),
+//                         pushing only into own targets, with the same final
+//                         bitset + read filter as the single-device frontier.
+//
+// The next bucket is min over parts of (scan's next pending key, relax's min
+// pushed key): exactly the single-device ctrl word. Results are bit-identical
+// to gs_run; the exchange volume per bucket is 24 B x (arrivals with targets).
+
+namespace {
+
+__global__ void k_pbucket(uint64_t* ctrl, uint64_t* pcnt, uint64_t key) {
+  if (threadIdx.x == 0) {
+    ctrl[0] = key;      // the bucket k_scan reads (launch 0)
+    ctrl[1] = INF64;    // k_scan's next pending key
+    ctrl[2] = INF64;
+    pcnt[0] = 0;        // frontier groups
+    pcnt[1] = 0;        // records emitted
+  }
+}
+
+__global__ __launch_bounds__(TB) void k_pcount(const uint32_t* __restrict__ fr_cnt, uint32_t nwaves,
+                                                uint64_t* pcnt) {
+  uint64_t s = 0;
+  for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < nwaves; i += gridDim.x * TB) s += fr_cnt[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0 && s) atomicAdd((unsigned long long*)&pcnt[0], (unsigned long long)s);
+}
+
+__device__ __forceinline__ void load_mesh_row(const uint32_t* mesh, uint32_t u, uint32_t (&row)[MESH_W]) {
+  const uint4* rp = reinterpret_cast<const uint4*>(mesh + (size_t)u * MESH_W);
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const uint4 x = rp[q];
+    row[4 * q] = x.x; row[4 * q + 1] = x.y; row[4 * q + 2] = x.z; row[4 * q + 3] = x.w;
+  }
+}
+
+// Owner side of a bucket: the frontier segments written by k_scan -> records.
+template <int FP>
+__global__ __launch_bounds__(TB) void k_pexport(RelaxArgs a, gs_part_record* __restrict__ rec, uint64_t cap,
+                                                uint64_t* pcnt) {
+  __shared__ BucketLds L;
+  load_tables(L, a);
+  __syncthreads();
+  const uint64_t cur = a.ctrl[0];
+  const uint64_t lo = ((cur >> a.tshift) / a.delta) * a.delta, hi = lo + a.delta;
+  const uint32_t LL = a.L;
+  const uint32_t wave = blockIdx.x * (TB / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const uint32_t n = __builtin_amdgcn_readfirstlane(a.fr_cnt[wave]);
+  const size_t seg = (size_t)wave * a.seg_cap;
+  constexpr uint32_t GPW = 64 / FP;
+  const uint64_t smask = (1ull << a.sb) - 1;
+  uint64_t fd = 0, nr = 0;
+  uint32_t err = 0;
+  for (uint32_t base = 0; base < n; base += GPW) {
+    const uint32_t gi = base + (uint32_t)lane / FP;
+    const bool valid = gi < n;
+    uint64_t gid, key;
+    if constexpr (FP == 1) {
+      gid = valid ? a.fr_idx[seg + gi] : 0;
+      key = valid ? a.fr_key[seg + gi] : INF64;
+    } else {
+      gid = valid ? (uint64_t)a.fr_idx[seg + gi] * FP + (lane & (FP - 1)) : 0;
+      key = valid ? a.keys[gid] : INF64;
+    }
+    const uint64_t t = key >> a.tshift;
+    const uint32_t u = (uint32_t)(gid / LL);
+    const uint32_t slot = (uint32_t)(gid - (uint64_t)u * LL);
+    const uint32_t ug = u + a.u0;
+    const uint32_t pm = valid ? a.pub[slot / FP] : EMPTY;
+    const bool active = valid && key != INF64 && t >= lo && t < hi && ug != pm;
+    const uint32_t src = (uint32_t)(key & smask);
+    uint32_t cnt = 0;
+    if (active) {
+      uint32_t row[MESH_W];
+      load_mesh_row(a.mesh, ug, row);
+#pragma unroll
+      for (int j = 0; j < (int)MESH_W; j++) {
+        const uint32_t w = row[j] & 0xFFFFFFu;
+        cnt += (row[j] != EMPTY && w != src && w != pm) ? 1u : 0u;
+      }
+    }
+    const uint32_t ser = L.su[a.stage[valid ? ug : a.u0]];
+    const uint64_t start = uplink_start<FP>(a.busy, (size_t)u * a.B + slot / FP, active, key, cnt, ser, a.tshift);
+    if (active) {
+      fd++;
+      nr += cnt;
+      const uint32_t hp = (uint32_t)((key >> a.sb) & ((1u << HOP_BITS) - 1));
+      if (cnt && hp + 1 >= (1u << HOP_BITS)) err |= ERR_HOPS;
+    }
+    const bool want = active && cnt != 0;
+    const uint64_t wm = __ballot(want);
+    if (wm == 0) continue;
+    uint64_t wbase = 0;
+    if (lane == 0) wbase = atomicAdd((unsigned long long*)&pcnt[1], (unsigned long long)__popcll(wm));
+    wbase = uniform64(wbase);
+    if (want) {
+      const uint64_t pos = wbase + (uint64_t)__popcll(wm & ((1ull << lane) - 1));
+      if (pos < cap) {
+        gs_part_record r;
+        r.key = key;
+        r.start = start;
+        r.peer = ug;
+        r.slot = slot;
+        rec[pos] = r;
+      }
+    }
+  }
+  fd = wave_sum(fd);
+  nr = wave_sum(nr);
+  for (int off = 32; off > 0; off >>= 1) err |= __shfl_xor(err, off);
+  if (lane == 0) {
+    if (fd) atomicAdd((unsigned long long*)&a.counters[C_FD], (unsigned long long)fd);
+    if (nr) atomicAdd((unsigned long long*)&a.counters[C_R_FWD], (unsigned long long)nr);
+    if (err) atomicOr((unsigned*)&a.counters[C_ERR], err);
+  }
+}
+
+// Target side: every gathered record pushes into this partition's own peers.
+template <int FP>
+__global__ __launch_bounds__(TB) void k_precv(RelaxArgs a, const gs_part_record* __restrict__ rec, uint64_t n,
+                                              uint64_t* pcnt) {
+  __shared__ BucketLds L;
+  load_tables(L, a);
+  __syncthreads();
+  const uint32_t S = a.S, LL = a.L;
+  const uint64_t smask = (1ull << a.sb) - 1;
+  uint64_t nmin = INF64, np = 0;
+  uint32_t err = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * TB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * TB) {
+    const gs_part_record r = rec[i];
+    const uint32_t ug = r.peer, slot = r.slot;
+    const uint32_t src = (uint32_t)(r.key & smask);
+    const uint32_t hp = (uint32_t)((r.key >> a.sb) & ((1u << HOP_BITS) - 1));
+    const uint32_t pm = a.pub[slot / FP];
+    const uint32_t su = a.stage[ug];
+    const uint32_t ser = L.su[su];
+    const uint64_t hbits = ((uint64_t)(hp + 1) << a.sb) | ug;
+    uint32_t row[MESH_W];
+    load_mesh_row(a.mesh, ug, row);
+    uint32_t pos = 0;
+#pragma unroll
+    for (int j = 0; j < (int)MESH_W; j++) {
+      const uint32_t e = row[j];
+      const uint32_t w = e & 0xFFFFFFu;
+      if (e == EMPTY || w == src || w == pm) continue;
+      pos++;
+      if (w - a.u0 >= a.N) continue;  // another partition's peer
+      const size_t dst = (size_t)(w - a.u0) * LL + slot;
+      if ((a.fbits[dst >> 6] >> (dst & 63)) & 1) continue;  // final: cannot improve
+      const uint32_t sw = e >> STAGE_SHIFT, sd = L.sd[sw];
+      const uint64_t arr = r.start + (uint64_t)pos * ser + L.lat[su * S + sw] + (sd > ser ? sd - ser : 0);
+      if (arr > a.tmax) err |= ERR_TIME;
+      const uint64_t nk = (arr << a.tshift) | hbits;
+      if (!(nk < a.keys[dst])) continue;
+      atomicMin((unsigned long long*)&a.keys[dst], (unsigned long long)nk);
+      np++;
+      nmin = nk < nmin ? nk : nmin;
+    }
+  }
+  nmin = wave_min(nmin);
+  np = wave_sum(np);
+  for (int off = 32; off > 0; off >>= 1) err |= __shfl_xor(err, off);
+  if ((threadIdx.x & 63) == 0) {
+    if (nmin != INF64) atomicMin((unsigned long long*)&pcnt[2], (unsigned long long)nmin);
+    if (np) atomicAdd((unsigned long long*)&a.counters[C_PUSH], (unsigned long long)np);
+    if (err) atomicOr((unsigned*)&a.counters[C_ERR], err);
+  }
+}
+
+template <int FP>
+void part_export_fp(const RelaxArgs& a, unsigned grid, hipStream_t s, gs_part_record* rec, uint64_t cap,
+                    uint64_t* pcnt) {
+  k_pexport<FP><<<grid, TB, 0, s>>>(a, rec, cap, pcnt);
+}
+template <int FP>
+void part_recv_fp(const RelaxArgs& a, unsigned grid, hipStream_t s, const gs_part_record* rec, uint64_t n,
+                  uint64_t* pcnt) {
+  k_precv<FP><<<grid, TB, 0, s>>>(a, rec, n, pcnt);
+}
+
+RelaxArgs part_args(Ctx& c) {
+  const Batch& b = c.part_b;
+  RelaxArgs ra{};
+  ra.keys = c.d_keys.p; ra.busy = c.d_busy.p; ra.mesh = c.d_mesh.p; ra.pub = c.d_pub.p;
+  ra.fbits = c.d_fbits.p;
+  ra.fr_idx = c.d_fr_idx.p; ra.fr_key = c.d_fr_key.p; ra.fr_cnt = c.d_fr_cnt.p;
+  ra.stage = c.d_stage.p; ra.tables = c.d_tables.p; ra.ctrl = c.d_ctrl.p;
+  ra.counters = c.d_counters.p;
+  ra.total = (uint64_t)c.part_un * b.L;
+  ra.delta = b.delta; ra.tmax = b.tmax; ra.seg_cap = c.part_seg_cap;
+  ra.N = c.part_un; ra.B = b.B; ra.F = b.F; ra.L = b.L; ra.S = c.S; ra.sb = b.sb; ra.tshift = b.tshift;
+  ra.launch = 0;
+  ra.u0 = c.part_u0;
+  return ra;
+}
+
+}  // namespace
+
+void part_set(Ctx& c, uint32_t parts, uint32_t part) {
+  const uint32_t N = c.cfg.peers;
+  if (c.part_open) c.fail(GS_ESTATE, "a partitioned batch is in flight (gs_part_finish first)");
+  if (parts < 1 || part >= parts || parts > N) c.fail(GS_EINVAL, "need 1 <= parts <= peers and part < parts");
+  c.part_parts = parts;
+  c.part_idx = part;
+  c.part_u0 = (uint32_t)((uint64_t)part * N / parts);
+  c.part_un = (uint32_t)((uint64_t)(part + 1) * N / parts) - c.part_u0;
+}
+
+uint64_t part_begin(Ctx& c, const gs_publish* sched, uint64_t n_msgs) {
+  if (c.part_un == 0) part_set(c, 1, 0);
+  if (c.part_open) c.fail(GS_ESTATE, "a partitioned batch is in flight (gs_part_finish first)");
+  if (n_msgs < 1 || n_msgs > c.cfg.batch) c.fail(GS_EINVAL, "partitioned batch needs 1..cfg.batch messages");
+  check_schedule(c, sched, n_msgs);
+  for (uint64_t i = 1; i < n_msgs; i++)
+    if (sched[i].msg_size != sched[0].msg_size) c.fail(GS_EINVAL, "partitioned batch needs equal msg_size");
+  if (c.cfg.lazy_gossip) c.fail(GS_EUNSUPPORTED, "lazy gossip is not supported in partitioned mode");
+  const uint32_t F = c.cfg.fragments;
+  if (c.cfg.idontwant && sched[0].msg_size / F >= c.cfg.idontwant)
+    c.fail(GS_EUNSUPPORTED, "IDONTWANT is not supported in partitioned mode");
+  const uint32_t FP = pow2_at_least(F), Bmax = c.cfg.batch, un = c.part_un;
+  if ((uint64_t)un * Bmax * FP >= (1ull << 32)) c.fail(GS_EUNSUPPORTED, "partition needs own peers*batch*FP < 2^32");
+  hipStream_t s = c.stream;
+  GS_HIP(hipMemsetAsync(c.d_counters.p + C_ERR, 0, 8, s));
+  ensure_cus(c);
+  const size_t lanes = (size_t)un * Bmax * FP, max_tiles = (lanes + 63) / 64;
+  c.d_keys.alloc(lanes);
+  c.d_fbits.alloc(max_tiles);
+  if (FP > 1) c.d_busy.alloc((size_t)un * Bmax);
+  c.d_tc.alloc((size_t)un * Bmax);
+  c.d_hops.alloc((size_t)un * Bmax);
+  c.d_pcnt.alloc(4);
+  c.part_b = setup_batch(c, sched, 0, n_msgs);
+  const Batch& b = c.part_b;
+  const uint64_t total = (uint64_t)un * b.L;
+  GS_HIP(hipMemsetAsync(c.d_keys.p, 0xFF, total * 8, s));
+  if (FP > 1) GS_HIP(hipMemsetAsync(c.d_busy.p, 0, (size_t)un * b.B * 8, s));
+  GS_HIP(hipMemsetAsync(c.d_fbits.p, 0, (total + 63) / 64 * 8, s));
+  GS_HIP(hipMemsetAsync(c.d_ctrl.p, 0xFF, 4 * 8, s));
+  c.part_grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((total + TB - 1) / TB, (uint64_t)c.num_cus * 16));
+  const uint64_t nwaves = (uint64_t)c.part_grid * (TB / 64), ntiles = (total + 63) / 64;
+  c.part_seg_cap = (uint32_t)(((ntiles + nwaves - 1) / nwaves) * (64 / FP));
+  c.d_fr_idx.alloc(nwaves * c.part_seg_cap);
+  if (FP == 1) c.d_fr_key.alloc(nwaves * c.part_seg_cap);
+  c.d_fr_cnt.alloc(nwaves);
+  launch_seed(c, b, c.part_u0, un);
+  GS_HIP(hipMemcpyAsync(c.h_pinned, c.d_ctrl.p, 8, hipMemcpyDeviceToHost, s));
+  GS_HIP(hipStreamSynchronize(s));
+  c.part_open = true;
+  return c.h_pinned[0];
+}
+
+bool part_scan(Ctx& c, uint64_t bucket_key, gs_part_record* rec, uint64_t cap, uint64_t* n, uint64_t* m1) {
+  if (!c.part_open) c.fail(GS_ESTATE, "gs_part_begin first");
+  if (bucket_key == INF64) c.fail(GS_EINVAL, "bucket key is the empty marker");
+  hipStream_t s = c.stream;
+  const Batch& b = c.part_b;
+  const RelaxArgs ra = part_args(c);
+  const unsigned grid = c.part_grid;
+  const uint32_t nwaves = grid * (TB / 64);
+  k_pbucket<<<1, 64, 0, s>>>(c.d_ctrl.p, c.d_pcnt.p, bucket_key);
+  switch (b.FP) {
+    case 1: k_scan<1, false, false><<<grid, TB, 0, s>>>(ra); break;
+    case 2: k_scan<2, false, false><<<grid, TB, 0, s>>>(ra); break;
+    case 4: k_scan<4, false, false><<<grid, TB, 0, s>>>(ra); break;
+    case 8: k_scan<8, false, false><<<grid, TB, 0, s>>>(ra); break;
+    default: k_scan<16, false, false><<<grid, TB, 0, s>>>(ra); break;
+  }
+  k_pcount<<<std::min<uint32_t>(64, (nwaves + TB - 1) / TB), TB, 0, s>>>(c.d_fr_cnt.p, nwaves, c.d_pcnt.p);
+  GS_HIP(hipGetLastError());
+  GS_HIP(hipMemcpyAsync(c.h_pinned, c.d_ctrl.p + 1, 8, hipMemcpyDeviceToHost, s));
+  GS_HIP(hipMemcpyAsync(c.h_pinned + 1, c.d_pcnt.p, 8, hipMemcpyDeviceToHost, s));
+  GS_HIP(hipStreamSynchronize(s));
+  *m1 = c.h_pinned[0];
+  const uint64_t need = c.h_pinned[1] * b.FP;  // lanes of the compacted groups bound the records
+  c.stats.relax_launches++;
+  if (need > cap) {
+    *n = need;
+    return false;
+  }
+  if (need) {
+    if (!rec) c.fail(GS_EINVAL, "null record buffer");
+    switch (b.FP) {
+      case 1: part_export_fp<1>(ra, grid, s, rec, cap, c.d_pcnt.p); break;
+      case 2: part_export_fp<2>(ra, grid, s, rec, cap, c.d_pcnt.p); break;
+      case 4: part_export_fp<4>(ra, grid, s, rec, cap, c.d_pcnt.p); break;
+      case 8: part_export_fp<8>(ra, grid, s, rec, cap, c.d_pcnt.p); break;
+      default: part_export_fp<16>(ra, grid, s, rec, cap, c.d_pcnt.p); break;
+    }
+    GS_HIP(hipGetLastError());
+  }
+  GS_HIP(hipMemcpyAsync(c.h_pinned, c.d_pcnt.p + 1, 8, hipMemcpyDeviceToHost, s));
+  GS_HIP(hipStreamSynchronize(s));
+  *n = c.h_pinned[0];
+  return true;
+}
+
+uint64_t part_relax(Ctx& c, uint64_t bucket_key, const gs_part_record* rec, uint64_t n) {
+  if (!c.part_open) c.fail(GS_ESTATE, "gs_part_begin first");
+  (void)bucket_key;  // records carry their own keys; the argument documents the protocol step
+  if (n == 0) return INF64;
+  if (!rec) c.fail(GS_EINVAL, "null record buffer");
+  hipStream_t s = c.stream;
+  const Batch& b = c.part_b;
+  const RelaxArgs ra = part_args(c);
+  GS_HIP(hipMemsetAsync(c.d_pcnt.p + 2, 0xFF, 8, s));
+  const unsigned grid = (unsigned)std::min<uint64_t>((n + TB - 1) / TB, (uint64_t)c.num_cus * 16);
+  switch (b.FP) {
+    case 1: part_recv_fp<1>(ra, grid, s, rec, n, c.d_pcnt.p); break;
+    case 2: part_recv_fp<2>(ra, grid, s, rec, n, c.d_pcnt.p); break;
+    case 4: part_recv_fp<4>(ra, grid, s, rec, n, c.d_pcnt.p); break;
+    case 8: part_recv_fp<8>(ra, grid, s, rec, n, c.d_pcnt.p); break;
+    default: part_recv_fp<16>(ra, grid, s, rec, n, c.d_pcnt.p); break;
+  }
+  GS_HIP(hipGetLastError());
+  GS_HIP(hipMemcpyAsync(c.h_pinned, c.d_pcnt.p + 2, 8, hipMemcpyDeviceToHost, s));
+  GS_HIP(hipStreamSynchronize(s));
+  return c.h_pinned[0];
+}
+
+void part_finish(Ctx& c, const gs_result_sink* sink) {
+  if (!c.part_open) c.fail(GS_ESTATE, "gs_part_begin first");
+  c.part_open = false;
+  launch_complete(c, c.part_b, c.part_u0, c.part_un, sink, 0);
+  c.stats.messages += c.part_b.B;
+  collect_stats(c);
+}

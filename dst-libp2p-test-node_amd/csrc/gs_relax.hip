@@ -38,15 +38,17 @@ struct SeedArgs {
   uint64_t* counters;
   uint64_t tmax;
   uint32_t L, FP, Fe, S, sb, tshift, flood;
+  uint32_t u0, un;  // keys held for peers [u0, u0 + un) (the whole graph unless partitioned)
 };
 
 // publish_new_message (main.rs:101-143): self key at the publisher and the
-// flood (or mesh) sends of every fragment through its uplink FIFO.
+// flood (or mesh) sends of every fragment through its uplink FIFO. Only
+// targets inside [u0, u0 + un) are written; the publisher's owner counts R.
 __global__ __launch_bounds__(TB) void k_seed(SeedArgs a) {
   const uint32_t m = blockIdx.x, p = a.pub[m], sp = a.stage[p], S = a.S;
   const uint64_t ser = a.tables[S * S + sp];
-  const uint64_t slot0 = (size_t)p * a.L + (size_t)m * a.FP;
-  if (threadIdx.x < a.Fe) a.keys[slot0 + threadIdx.x] = (uint64_t)p;
+  const bool own_pub = p - a.u0 < a.un;
+  if (own_pub && threadIdx.x < a.Fe) a.keys[(size_t)(p - a.u0) * a.L + (size_t)m * a.FP + threadIdx.x] = (uint64_t)p;
   uint32_t deg;
   const uint32_t* tg;
   bool packed;
@@ -68,7 +70,8 @@ __global__ __launch_bounds__(TB) void k_seed(SeedArgs a) {
     const uint64_t arr = ((uint64_t)f * deg + j + 1) * ser + a.tables[sp * S + sw] + (sd > ser ? sd - ser : 0);
     if (arr > a.tmax) err |= ERR_TIME;
     const uint64_t nk = (arr << a.tshift) | (1ull << a.sb) | p;
-    atomicMin((unsigned long long*)&a.keys[(size_t)w * a.L + (size_t)m * a.FP + f], (unsigned long long)nk);
+    if (w - a.u0 >= a.un) continue;
+    atomicMin((unsigned long long*)&a.keys[(size_t)(w - a.u0) * a.L + (size_t)m * a.FP + f], (unsigned long long)nk);
     nmin = nk < nmin ? nk : nmin;
   }
   nmin = wave_min(nmin);
@@ -77,7 +80,7 @@ __global__ __launch_bounds__(TB) void k_seed(SeedArgs a) {
     if (nmin != INF64) atomicMin((unsigned long long*)&a.ctrl[0], (unsigned long long)nmin);
     if (err) atomicOr((unsigned*)&a.counters[C_ERR], err);
   }
-  if (threadIdx.x == 0) atomicAdd((unsigned long long*)&a.counters[C_R], (unsigned long long)total);
+  if (threadIdx.x == 0 && own_pub) atomicAdd((unsigned long long*)&a.counters[C_R], (unsigned long long)total);
 }
 
 struct CompArgs {
@@ -88,6 +91,7 @@ struct CompArgs {
   uint8_t* hops;    // [N][B]
   uint64_t* counters;
   uint32_t N, B, F, FP, L, sb, tshift, collide;
+  uint32_t u0;  // global id of keys row 0
 };
 
 // Reassembly (main.rs:79-99): completion = max over fragments of the first
@@ -112,7 +116,7 @@ __global__ __launch_bounds__(TB) void k_complete(CompArgs a) {
     uint64_t tc = INF64;
     uint8_t h = 0xFF;
     const uint64_t tp = a.tpub[m];
-    if (u == a.pub[m]) { tc = tp; h = 0; }
+    if (u + a.u0 == a.pub[m]) { tc = tp; h = 0; }
     else if (!a.collide && ok) {
       const uint64_t trel = mk >> a.tshift;
       tc = tp + trel;
@@ -171,18 +175,138 @@ uint32_t pow2_at_least(uint32_t x) { uint32_t p = 1; while (p < x) p <<= 1; retu
 
 }  // namespace
 
-void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_result_sink* sink) {
-  const uint32_t N = c.cfg.peers, F = c.cfg.fragments, FP = pow2_at_least(F);
-  const uint32_t Bmax = c.cfg.batch, S = c.S;
-  hipStream_t s = c.stream;
-  const uint32_t sb = bits_for(N), tshift = sb + HOP_BITS;
-  const uint64_t tmax = tshift >= 64 ? 0 : (INF64 >> tshift);
-  GS_HIP(hipMemsetAsync(c.d_counters.p + C_ERR, 0, 8, s));
+static void check_schedule(Ctx& c, const gs_publish* sched, uint64_t n_msgs) {
   for (uint64_t i = 0; i < n_msgs; i++) {
-    if (sched[i].publisher >= N) c.fail(GS_EINVAL, "publisher id out of range");
-    if (sched[i].msg_size / F < 8)  // main.rs:110-111 slices buffer[..8]
+    if (sched[i].publisher >= c.cfg.peers) c.fail(GS_EINVAL, "publisher id out of range");
+    if (sched[i].msg_size / c.cfg.fragments < 8)  // main.rs:110-111 slices buffer[..8]
       c.fail(GS_EINVAL, "fragment payload shorter than the 8-byte tx_time stamp");
   }
+}
+
+// Upload pub/tpub/link tables for messages [i0, i1) (equal msg_size) and
+// compute the bucket width Delta = min latency + min serialisation.
+static Batch setup_batch(Ctx& c, const gs_publish* sched, uint64_t i0, uint64_t i1) {
+  Batch b;
+  const uint32_t N = c.cfg.peers, S = c.S;
+  b.F = c.cfg.fragments;
+  b.FP = pow2_at_least(b.F);
+  b.B = (uint32_t)(i1 - i0);
+  b.L = b.B * b.FP;
+  b.sb = bits_for(N);
+  b.tshift = b.sb + HOP_BITS;
+  b.tmax = b.tshift >= 64 ? 0 : (INF64 >> b.tshift);
+  b.payload = sched[i0].msg_size / b.F;
+  b.collide = b.F > 1 && b.payload <= 10;  // defect D8
+  b.Fe = b.collide ? 1 : b.F;
+  hipStream_t s = c.stream;
+  const uint64_t wire = gs_wire_bytes(b.payload, c.cfg.muxer, c.cfg.signed_msgs);
+  std::vector<uint32_t> tab((size_t)S * S + 2 * S), pub(b.B);
+  uint64_t min_lat = INF64, min_ser = INF64;
+  for (uint32_t x = 0; x < S; x++)
+    for (uint32_t y = 0; y < S; y++) {
+      if (c.lat_ns[(size_t)x * S + y] >= (1ull << 32)) c.fail(GS_ERANGE, "latency >= 2^32 ns");
+      tab[(size_t)x * S + y] = (uint32_t)c.lat_ns[(size_t)x * S + y];
+      min_lat = std::min<uint64_t>(min_lat, c.lat_ns[(size_t)x * S + y]);
+    }
+  for (uint32_t x = 0; x < S; x++) {
+    const uint64_t up = ser_ns(wire, c.bw_up[x]), dn = ser_ns(wire, c.bw_dn[x]);
+    if (up >= (1ull << 32) || dn >= (1ull << 32)) c.fail(GS_ERANGE, "serialisation >= 2^32 ns");
+    tab[(size_t)S * S + x] = (uint32_t)up;
+    tab[(size_t)S * S + S + x] = (uint32_t)dn;
+    min_ser = std::min(min_ser, up);
+  }
+  b.delta = std::max<uint64_t>(1, min_lat + min_ser);
+  b.tpub.resize(b.B);
+  for (uint32_t q = 0; q < b.B; q++) { pub[q] = sched[i0 + q].publisher; b.tpub[q] = sched[i0 + q].t_pub_ns; }
+  c.d_pub.alloc(c.cfg.batch);
+  c.d_tpub.alloc(c.cfg.batch);
+  c.d_tables.alloc((size_t)S * S + 2 * S);
+  GS_HIP(hipMemcpyAsync(c.d_pub.p, pub.data(), b.B * 4, hipMemcpyHostToDevice, s));
+  GS_HIP(hipMemcpyAsync(c.d_tpub.p, b.tpub.data(), b.B * 8, hipMemcpyHostToDevice, s));
+  GS_HIP(hipMemcpyAsync(c.d_tables.p, tab.data(), tab.size() * 4, hipMemcpyHostToDevice, s));
+  // the host vectors die here: make the copies complete first
+  GS_HIP(hipStreamSynchronize(s));
+  return b;
+}
+
+static void launch_seed(Ctx& c, const Batch& b, uint32_t u0, uint32_t un) {
+  SeedArgs sa{};
+  sa.keys = c.d_keys.p; sa.row = c.d_row.p; sa.col = c.d_col.p; sa.mesh = c.d_mesh.p;
+  sa.pub = c.d_pub.p; sa.stage = c.d_stage.p; sa.tables = c.d_tables.p; sa.ctrl = c.d_ctrl.p;
+  sa.counters = c.d_counters.p; sa.tmax = b.tmax; sa.L = b.L; sa.FP = b.FP; sa.Fe = b.Fe;
+  sa.S = c.S; sa.sb = b.sb; sa.tshift = b.tshift; sa.flood = c.cfg.flood_publish;
+  sa.u0 = u0; sa.un = un;
+  k_seed<<<b.B, TB, 0, c.stream>>>(sa);
+  GS_HIP(hipGetLastError());
+}
+
+// Completion of the keys rows [0, un) (global ids u0 + row) into d_tc/d_hops,
+// then the message-major copy into sink[q * un + row] for q < B.
+static void launch_complete(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, const gs_result_sink* sink,
+                            uint64_t sink_row0) {
+  hipStream_t s = c.stream;
+  CompArgs ca{};
+  ca.keys = c.d_keys.p; ca.pub = c.d_pub.p; ca.tpub = c.d_tpub.p; ca.tc = c.d_tc.p;
+  ca.hops = c.d_hops.p; ca.counters = c.d_counters.p; ca.N = un; ca.B = b.B; ca.F = b.F;
+  ca.FP = b.FP; ca.L = b.L; ca.sb = b.sb; ca.tshift = b.tshift; ca.collide = b.collide ? 1 : 0;
+  ca.u0 = u0;
+  const unsigned cgrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(((uint64_t)un * b.B + TB - 1) / TB,
+                                                                            (uint64_t)c.num_cus * 16));
+  switch (b.FP) {
+    case 1: k_complete<1><<<cgrid, TB, 0, s>>>(ca); break;
+    case 2: k_complete<2><<<cgrid, TB, 0, s>>>(ca); break;
+    case 4: k_complete<4><<<cgrid, TB, 0, s>>>(ca); break;
+    case 8: k_complete<8><<<cgrid, TB, 0, s>>>(ca); break;
+    default: k_complete<16><<<cgrid, TB, 0, s>>>(ca); break;
+  }
+  GS_HIP(hipGetLastError());
+  if (sink && (sink->t_complete_ns || sink->hops)) {  // message-major copy-out
+    c.d_tc_t.alloc((size_t)un * c.cfg.batch);
+    c.d_hops_t.alloc((size_t)un * c.cfg.batch);
+    dim3 tg((un + 63) / 64, (b.B + 63) / 64);
+    k_transpose<<<tg, TB, 0, s>>>(c.d_tc.p, c.d_hops.p, c.d_tc_t.p, c.d_hops_t.p, un, b.B);
+    GS_HIP(hipGetLastError());
+    if (sink->t_complete_ns)
+      GS_HIP(hipMemcpyAsync(sink->t_complete_ns + sink_row0 * un, c.d_tc_t.p, (size_t)b.B * un * 8,
+                            hipMemcpyDeviceToHost, s));
+    if (sink->hops)
+      GS_HIP(hipMemcpyAsync(sink->hops + sink_row0 * un, c.d_hops_t.p, (size_t)b.B * un, hipMemcpyDeviceToHost, s));
+  }
+}
+
+// Read the device counters into ctx->stats (and raise the device error word).
+static void collect_stats(Ctx& c) {
+  hipStream_t s = c.stream;
+  GS_HIP(hipMemcpyAsync(c.h_pinned, c.d_counters.p, C_COUNT * 8, hipMemcpyDeviceToHost, s));
+  GS_HIP(hipStreamSynchronize(s));
+  const uint64_t* h = c.h_pinned;
+  if (h[C_ERR] & ERR_TIME) c.fail(GS_ERANGE, "relative arrival time overflowed the key's time field");
+  if (h[C_ERR] & ERR_HOPS) c.fail(GS_ERANGE, "hop count overflowed the key's 6-bit hop field");
+  c.stats.frag_deliveries = h[C_FD];
+  c.stats.relaxations = h[C_R] + h[C_R_FWD] + h[C_GOSSIP];
+  c.stats.gossip_iwant = h[C_GOSSIP];
+  c.stats.deliveries = h[C_DELIV];
+  c.stats.latency_sum_ms = h[C_LAT_SUM];
+  c.stats.latency_max_ms = h[C_LAT_MAX];
+  c.stats.buckets = h[C_BUCKETS];
+  c.stats.bytes_alg = 16 * h[C_FD] + 12 * c.stats.relaxations + 8 * h[C_DELIV];
+  c.stats.relax_bytes_alg = 16 * h[C_FD] + 12 * h[C_R_FWD];
+  c.stats.pushes = h[C_PUSH];
+}
+
+static void ensure_cus(Ctx& c) {
+  if (c.num_cus == 0) {
+    hipDeviceProp_t prop;
+    c.num_cus = hipGetDeviceProperties(&prop, c.cfg.device) == hipSuccess ? prop.multiProcessorCount : 256;
+  }
+}
+
+void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_result_sink* sink) {
+  const uint32_t N = c.cfg.peers, F = c.cfg.fragments, FP = pow2_at_least(F);
+  const uint32_t Bmax = c.cfg.batch;
+  hipStream_t s = c.stream;
+  GS_HIP(hipMemsetAsync(c.d_counters.p + C_ERR, 0, 8, s));
+  check_schedule(c, sched, n_msgs);
   const char* var_env = getenv("GS_RELAX_VARIANT");
   uint32_t variant = var_env && *var_env ? (uint32_t)atoi(var_env) : 13u;  // split + final bitset + read filter
   if ((uint64_t)N * Bmax * FP >= (1ull << 32)) {  // frontier indices are u32
@@ -200,15 +324,11 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
   c.d_meta.alloc(max_tiles * sizeof(TileMeta) / 8);
   c.d_fbits.alloc(max_tiles);
   if (FP > 1) c.d_busy.alloc((size_t)N * Bmax);
-  c.d_pub.alloc(Bmax);
-  c.d_tpub.alloc(Bmax);
   c.d_tc.alloc((size_t)N * Bmax);
   c.d_hops.alloc((size_t)N * Bmax);
-  c.d_tables.alloc((size_t)S * S + 2 * S);
-  std::vector<uint32_t> pub(Bmax), tab((size_t)S * S + 2 * S);
-  std::vector<uint64_t> tpub(Bmax), rel0(Bmax), habs0(Bmax);
+  std::vector<uint64_t> rel0(Bmax), habs0(Bmax);
   // Timing events come from a per-context pool: [0] run start, [1] run end,
-  // then one (start, end) pair around every relaxation launch.
+  // then one (start, scan end, end) triple around every relaxation launch.
   size_t n_ev = 0;
   auto ev = [&](size_t i) {
     while (c.ev_pool.size() <= i) {
@@ -223,42 +343,19 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     ev(1);
     n_ev = 2;
   }
-  if (c.num_cus == 0) {
-    hipDeviceProp_t prop;
-    c.num_cus = hipGetDeviceProperties(&prop, c.cfg.device) == hipSuccess ? prop.multiProcessorCount : 256;
-  }
+  ensure_cus(c);
   const int dev_cus = c.num_cus;
   uint64_t i0 = 0;
   while (i0 < n_msgs) {
     // a batch: up to B messages of equal size (serialisation tables are per batch)
     uint64_t i1 = i0 + 1;
     while (i1 < n_msgs && i1 - i0 < Bmax && sched[i1].msg_size == sched[i0].msg_size) i1++;
-    const uint32_t B = (uint32_t)(i1 - i0), L = B * FP;
-    const uint64_t payload = sched[i0].msg_size / F;
-    const bool collide = F > 1 && payload <= 10;  // defect D8
-    const uint64_t wire = gs_wire_bytes(payload, c.cfg.muxer, c.cfg.signed_msgs);
-    uint64_t min_lat = INF64, min_ser = INF64;
-    for (uint32_t a = 0; a < S; a++)
-      for (uint32_t b = 0; b < S; b++) {
-        if (c.lat_ns[(size_t)a * S + b] >= (1ull << 32)) c.fail(GS_ERANGE, "latency >= 2^32 ns");
-        tab[(size_t)a * S + b] = (uint32_t)c.lat_ns[(size_t)a * S + b];
-        min_lat = std::min<uint64_t>(min_lat, c.lat_ns[(size_t)a * S + b]);
-      }
-    for (uint32_t a = 0; a < S; a++) {
-      const uint64_t up = ser_ns(wire, c.bw_up[a]), dn = ser_ns(wire, c.bw_dn[a]);
-      if (up >= (1ull << 32) || dn >= (1ull << 32)) c.fail(GS_ERANGE, "serialisation >= 2^32 ns");
-      tab[(size_t)S * S + a] = (uint32_t)up;
-      tab[(size_t)S * S + S + a] = (uint32_t)dn;
-      min_ser = std::min(min_ser, up);
-    }
-    const uint64_t delta = std::max<uint64_t>(1, min_lat + min_ser);
-    for (uint32_t q = 0; q < B; q++) { pub[q] = sched[i0 + q].publisher; tpub[q] = sched[i0 + q].t_pub_ns; }
-    GS_HIP(hipMemcpyAsync(c.d_pub.p, pub.data(), B * 4, hipMemcpyHostToDevice, s));
-    GS_HIP(hipMemcpyAsync(c.d_tpub.p, tpub.data(), B * 8, hipMemcpyHostToDevice, s));
+    const Batch b = setup_batch(c, sched, i0, i1);
+    const uint32_t B = b.B, L = b.L;
     if (gossip) {  // heartbeats at hb_phase + h*hb: first one at or after each t_pub
       const uint64_t hb = c.cfg.heartbeat_ns, ph = c.cfg.hb_phase_ns;
       for (uint32_t q = 0; q < B; q++) {
-        const uint64_t tp = tpub[q];
+        const uint64_t tp = b.tpub[q];
         const uint64_t h0 = tp <= ph ? 0 : (tp - ph + hb - 1) / hb;
         rel0[q] = ph + h0 * hb - tp;
         habs0[q] = h0;
@@ -268,7 +365,6 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       GS_HIP(hipMemcpyAsync(c.d_rel0.p, rel0.data(), B * 8, hipMemcpyHostToDevice, s));
       GS_HIP(hipMemcpyAsync(c.d_habs0.p, habs0.data(), B * 8, hipMemcpyHostToDevice, s));
     }
-    GS_HIP(hipMemcpyAsync(c.d_tables.p, tab.data(), tab.size() * 4, hipMemcpyHostToDevice, s));
     const uint64_t total = (uint64_t)N * L;
     GS_HIP(hipMemsetAsync(c.d_keys.p, 0xFF, total * 8, s));
     if (FP > 1) GS_HIP(hipMemsetAsync(c.d_busy.p, 0, (size_t)N * B * 8, s));
@@ -284,14 +380,7 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     // with gossip the first bucket is [0, Delta): the publisher's own IHAVEs
     // can land before the first eager arrival
     if (gossip) GS_HIP(hipMemsetAsync(c.d_ctrl.p, 0, 8, s));
-
-    SeedArgs sa{};
-    sa.keys = c.d_keys.p; sa.row = c.d_row.p; sa.col = c.d_col.p; sa.mesh = c.d_mesh.p;
-    sa.pub = c.d_pub.p; sa.stage = c.d_stage.p; sa.tables = c.d_tables.p; sa.ctrl = c.d_ctrl.p;
-    sa.counters = c.d_counters.p; sa.tmax = tmax; sa.L = L; sa.FP = FP; sa.Fe = collide ? 1 : F;
-    sa.S = S; sa.sb = sb; sa.tshift = tshift; sa.flood = c.cfg.flood_publish;
-    k_seed<<<B, TB, 0, s>>>(sa);
-    GS_HIP(hipGetLastError());
+    launch_seed(c, b, 0, N);
 
     RelaxArgs ra{};
     ra.keys = c.d_keys.p; ra.busy = c.d_busy.p; ra.mesh = c.d_mesh.p; ra.pub = c.d_pub.p;
@@ -300,9 +389,9 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     ra.tmin = c.d_tmin.p;
     ra.touched = c.d_touched.p;
     ra.stage = c.d_stage.p; ra.tables = c.d_tables.p; ra.ctrl = c.d_ctrl.p;
-    ra.counters = c.d_counters.p; ra.total = total; ra.delta = delta; ra.tmax = tmax;
-    ra.N = N; ra.B = B; ra.F = F; ra.L = L; ra.S = S; ra.sb = sb; ra.tshift = tshift;
-    ra.idw = (c.cfg.idontwant && payload >= c.cfg.idontwant) ? 1 : 0;
+    ra.counters = c.d_counters.p; ra.total = total; ra.delta = b.delta; ra.tmax = b.tmax;
+    ra.N = N; ra.B = B; ra.F = F; ra.L = L; ra.S = c.S; ra.sb = b.sb; ra.tshift = b.tshift;
+    ra.idw = (c.cfg.idontwant && b.payload >= c.cfg.idontwant) ? 1 : 0;
     const uint64_t need = (total + TB - 1) / TB;
     const unsigned grid = (unsigned)std::min<uint64_t>(need, (uint64_t)dev_cus * 16);
     if (variant & 8) {  // frontier segments: one per scan wave
@@ -360,51 +449,12 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       if (c.h_pinned[launch % 3] == INF64) break;
     }
     c.stats.relax_launches += launch;
-
-    CompArgs ca{};
-    ca.keys = c.d_keys.p; ca.pub = c.d_pub.p; ca.tpub = c.d_tpub.p; ca.tc = c.d_tc.p;
-    ca.hops = c.d_hops.p; ca.counters = c.d_counters.p; ca.N = N; ca.B = B; ca.F = F;
-    ca.FP = FP; ca.L = L; ca.sb = sb; ca.tshift = tshift; ca.collide = collide ? 1 : 0;
-    const unsigned cgrid = (unsigned)std::min<uint64_t>(((uint64_t)N * B + TB - 1) / TB, (uint64_t)dev_cus * 16);
-    switch (FP) {
-      case 1: k_complete<1><<<cgrid, TB, 0, s>>>(ca); break;
-      case 2: k_complete<2><<<cgrid, TB, 0, s>>>(ca); break;
-      case 4: k_complete<4><<<cgrid, TB, 0, s>>>(ca); break;
-      case 8: k_complete<8><<<cgrid, TB, 0, s>>>(ca); break;
-      default: k_complete<16><<<cgrid, TB, 0, s>>>(ca); break;
-    }
-    GS_HIP(hipGetLastError());
-    if (sink && (sink->t_complete_ns || sink->hops)) {  // message-major copy-out
-      c.d_tc_t.alloc((size_t)N * Bmax);
-      c.d_hops_t.alloc((size_t)N * Bmax);
-      dim3 tg((N + 63) / 64, (B + 63) / 64);
-      k_transpose<<<tg, TB, 0, s>>>(c.d_tc.p, c.d_hops.p, c.d_tc_t.p, c.d_hops_t.p, N, B);
-      GS_HIP(hipGetLastError());
-      if (sink->t_complete_ns)
-        GS_HIP(hipMemcpyAsync(sink->t_complete_ns + i0 * N, c.d_tc_t.p, (size_t)B * N * 8,
-                              hipMemcpyDeviceToHost, s));
-      if (sink->hops)
-        GS_HIP(hipMemcpyAsync(sink->hops + i0 * N, c.d_hops_t.p, (size_t)B * N, hipMemcpyDeviceToHost, s));
-    }
+    launch_complete(c, b, 0, N, sink, i0);
     c.stats.messages += B;
     i0 = i1;
   }
   if (c.timing) GS_HIP(hipEventRecord(ev(1), s));
-  GS_HIP(hipMemcpyAsync(c.h_pinned, c.d_counters.p, C_COUNT * 8, hipMemcpyDeviceToHost, s));
-  GS_HIP(hipStreamSynchronize(s));
-  const uint64_t* h = c.h_pinned;
-  if (h[C_ERR] & ERR_TIME) c.fail(GS_ERANGE, "relative arrival time overflowed the key's time field");
-  if (h[C_ERR] & ERR_HOPS) c.fail(GS_ERANGE, "hop count overflowed the key's 6-bit hop field");
-  c.stats.frag_deliveries = h[C_FD];
-  c.stats.relaxations = h[C_R] + h[C_R_FWD] + h[C_GOSSIP];
-  c.stats.gossip_iwant = h[C_GOSSIP];
-  c.stats.deliveries = h[C_DELIV];
-  c.stats.latency_sum_ms = h[C_LAT_SUM];
-  c.stats.latency_max_ms = h[C_LAT_MAX];
-  c.stats.buckets = h[C_BUCKETS];
-  c.stats.bytes_alg = 16 * h[C_FD] + 12 * c.stats.relaxations + 8 * h[C_DELIV];
-  c.stats.relax_bytes_alg = 16 * h[C_FD] + 12 * h[C_R_FWD];
-  c.stats.pushes = h[C_PUSH];
+  collect_stats(c);
   if (c.timing) {
     double scan = 0, front = 0;
     for (size_t q = 2; q + 2 < n_ev; q += 3) {
@@ -422,5 +472,7 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     c.stats.run_ms += rm;
   }
 }
+
+#include "gs_part.h"
 
 }  // namespace gs

@@ -50,6 +50,7 @@ struct RelaxArgs {
   const uint32_t* col;
   uint64_t hb_ns, seed;
   uint32_t gl_cap, gossip, hist, d_lazy, gf_milli;
+  uint32_t u0;        // global id of the first peer whose keys this context holds
   const uint32_t* mesh;
   const uint32_t* pub;
   const uint8_t* stage;
@@ -116,6 +117,55 @@ __device__ __forceinline__ uint64_t first_hb(uint64_t t, uint64_t rel0, uint64_t
   return t <= rel0 ? 0 : (t - rel0 + hb - 1) / hb;
 }
 
+// Uplink FIFO across one (u, m)'s fragments: the FP-aligned lane group folds
+// max(t_f, busy) + n_f * ser in (key, fragment) order (gossip answers bypass
+// the FIFO, so two fragments can carry equal keys; the index breaks the tie)
+// and stores the new FIFO end in busy[bi]. Returns the lane's uplink start.
+// Every lane of the wave must call this.
+template <int FP>
+__device__ __forceinline__ uint64_t uplink_start(uint64_t* busy, size_t bi, bool active, uint64_t key,
+                                                 uint32_t n, uint32_t ser, uint32_t tshift) {
+  uint64_t start = key >> tshift;
+  if constexpr (FP > 1) {
+    const int lane = threadIdx.x & 63;
+    const int gb = lane & ~(FP - 1);
+    const uint64_t ka = active ? key : INF64;
+    uint64_t kk[FP];
+    uint32_t nn[FP];
+#pragma unroll
+    for (int g = 0; g < FP; g++) { kk[g] = __shfl(ka, gb + g); nn[g] = __shfl(n, gb + g); }
+    int first = -1;
+#pragma unroll
+    for (int g = FP - 1; g >= 0; g--) if (kk[g] != INF64) first = g;
+    if (first >= 0) {
+      uint64_t cb = busy[bi];
+      uint64_t pk = 0;
+      int pg = -1;
+#pragma unroll
+      for (int it = 0; it < FP; it++) {
+        uint64_t bk = INF64;
+        int bg = FP;
+        uint32_t bn = 0;
+#pragma unroll
+        for (int g = 0; g < FP; g++) {
+          const bool after = kk[g] > pk || (kk[g] == pk && g > pg);
+          const bool better = kk[g] < bk || (kk[g] == bk && g < bg);
+          if (kk[g] != INF64 && after && better) { bk = kk[g]; bg = g; bn = nn[g]; }
+        }
+        if (bg == FP) continue;  // nothing left (kept unrollable: no break)
+        const uint64_t tb = bk >> tshift;
+        const uint64_t s = tb > cb ? tb : cb;
+        if (active && bg == lane - gb) start = s;
+        cb = s + (uint64_t)bn * ser;
+        pk = bk;
+        pg = bg;
+      }
+      if (lane - gb == first) busy[bi] = cb;
+    }
+  }
+  return start;
+}
+
 // Forward one lane's first arrival (key at lane gid = u*L + slot). `active`
 // must be true only for lanes finalised in this bucket; every lane of the wave
 // must call this (FP > 1 shuffles across the FP-aligned lane group).
@@ -124,7 +174,6 @@ __device__ __forceinline__ void relax_lane(const RelaxArgs& a, const BucketLds& 
                                            uint64_t key, uint32_t u, uint32_t slot, uint32_t pm,
                                            uint64_t& nmin, uint64_t& fd, uint64_t& nr, uint64_t& np, uint32_t& err) {
   const uint32_t S = a.S, LL = a.L;
-  const int lane = threadIdx.x & 63;
   const uint64_t t = key >> a.tshift;
   const uint64_t smask = (1ull << a.sb) - 1;
   const uint32_t src = (uint32_t)(key & smask);
@@ -153,48 +202,7 @@ __device__ __forceinline__ void relax_lane(const RelaxArgs& a, const BucketLds& 
       if (sk) skip |= 1u << j; else n++;
     }
   }
-  uint64_t start = t;
-  if constexpr (FP > 1) {
-    // Uplink FIFO across this (u, m)'s fragments: the FP lanes of the group
-    // fold max(t_f, busy) + n_f * ser in key order (all lanes shuffle).
-    const int gb = lane & ~(FP - 1);
-    const uint64_t ka = active ? key : INF64;
-    const uint32_t m = slot / FP;
-    uint64_t kk[FP];
-    uint32_t nn[FP];
-#pragma unroll
-    for (int g = 0; g < FP; g++) { kk[g] = __shfl(ka, gb + g); nn[g] = __shfl(n, gb + g); }
-    int first = -1;
-#pragma unroll
-    for (int g = FP - 1; g >= 0; g--) if (kk[g] != INF64) first = g;
-    if (first >= 0) {
-      // (key, fragment) order: gossip answers bypass the FIFO, so two
-      // fragments can carry equal keys; the fragment index breaks the tie
-      uint64_t cb = a.busy[(size_t)u * a.B + m];
-      uint64_t pk = 0;
-      int pg = -1;
-#pragma unroll
-      for (int it = 0; it < FP; it++) {
-        uint64_t bk = INF64;
-        int bg = FP;
-        uint32_t bn = 0;
-#pragma unroll
-        for (int g = 0; g < FP; g++) {
-          const bool after = kk[g] > pk || (kk[g] == pk && g > pg);
-          const bool better = kk[g] < bk || (kk[g] == bk && g < bg);
-          if (kk[g] != INF64 && after && better) { bk = kk[g]; bg = g; bn = nn[g]; }
-        }
-        if (bg == FP) continue;  // nothing left (kept unrollable: no break)
-        const uint64_t tb = bk >> a.tshift;
-        const uint64_t s = tb > cb ? tb : cb;
-        if (active && bg == lane - gb) start = s;
-        cb = s + (uint64_t)bn * ser;
-        pk = bk;
-        pg = bg;
-      }
-      if (lane - gb == first) a.busy[(size_t)u * a.B + m] = cb;
-    }
-  }
+  const uint64_t start = uplink_start<FP>(a.busy, (size_t)u * a.B + slot / FP, active, key, n, ser, a.tshift);
   if (!active) return;
   fd++;
   nr += n;
@@ -358,7 +366,7 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
     const uint32_t slot = (uint32_t)(gid - (uint64_t)u * LL);
     const uint32_t pm = valid ? a.pub[slot / FP] : EMPTY;
     const bool pending = key != INF64;
-    const bool active = pending && t >= lo && t < hi && u != pm;
+    const bool active = pending && t >= lo && t < hi && u + a.u0 != pm;
     const uint64_t later = (pending && t >= hi) ? key : INF64;
     nmin = later < nmin ? later : nmin;
     const uint64_t fw = __ballot(pending && t < hi);

@@ -63,6 +63,10 @@ class GsStats(ctypes.Structure):
         ("gossip_iwant", u64)]
 
 
+class GsPartRecord(ctypes.Structure):
+    _fields_ = [("key", u64), ("start", u64), ("peer", u32), ("slot", u32)]
+
+
 # Every symbol include/gossipsim.h declares, with its ctypes signature.
 SIGNATURES = {
     "gs_config_default": (None, [P(GsConfig)]),
@@ -84,7 +88,14 @@ SIGNATURES = {
     "gs_get_stats": (i32, [ctypes.c_void_p, P(GsStats)]),
     "gs_reset_stats": (i32, [ctypes.c_void_p]),
     "gs_set_timing": (i32, [ctypes.c_void_p, u32]),
+    "gs_set_partition": (i32, [ctypes.c_void_p, u32, u32]),
+    "gs_part_begin": (i32, [ctypes.c_void_p, P(GsPublish), u64, P(u64)]),
+    "gs_part_scan": (i32, [ctypes.c_void_p, u64, ctypes.c_void_p, u64, P(u64), P(u64)]),
+    "gs_part_relax": (i32, [ctypes.c_void_p, u64, ctypes.c_void_p, u64, P(u64)]),
+    "gs_part_finish": (i32, [ctypes.c_void_p, P(GsResultSink)]),
 }
+GS_ERANGE = -5
+KEY_NONE = (1 << 64) - 1  # empty-bucket marker of the partitioned protocol
 
 _lib = None
 
@@ -277,8 +288,7 @@ class Simulator:
             raise GossipSimError(-1, "publisher out of range")
         self._sched.append((int(t_pub_ns), int(publisher), int(msg_size)))
 
-    def run(self, schedule=None, collect=True):
-        """Simulate the queued publishes (or `schedule`); returns t_complete/hops [M, N]."""
+    def _schedule(self, schedule):
         if schedule is None:
             schedule = (GsPublish * len(self._sched))(*[GsPublish(*r) for r in self._sched])
             self._sched = []
@@ -288,6 +298,11 @@ class Simulator:
             for i in range(len(t)):
                 arr[i] = GsPublish(int(t[i]), int(p[i]), int(s[i]))
             schedule = arr
+        return schedule
+
+    def run(self, schedule=None, collect=True):
+        """Simulate the queued publishes (or `schedule`); returns t_complete/hops [M, N]."""
+        schedule = self._schedule(schedule)
         M = len(schedule)
         res = {"schedule": schedule}
         if collect:
@@ -320,3 +335,47 @@ class Simulator:
                                         _ptr(tc, u64), self.cfg.c.self_log)
         if rc:
             raise GossipSimError(rc, "gs_write_latency_log failed")
+
+    # ---- peer-partitioned mode (include/gossipsim.h gs_part_*; driver in partition.py) ----
+    def set_partition(self, parts, part):
+        self._check(lib().gs_set_partition(self.ctx, parts, part))
+        self.part_range = (part * self.peers // parts, (part + 1) * self.peers // parts)
+
+    def part_begin(self, schedule):
+        schedule = self._schedule(schedule)
+        if not hasattr(self, "part_range"):
+            self.part_range = (0, self.peers)
+        k = u64()
+        self._check(lib().gs_part_begin(self.ctx, schedule, len(schedule), ctypes.byref(k)))
+        self._part_sched = schedule
+        return k.value
+
+    def part_scan(self, bucket_key, dev_ptr, capacity):
+        """-> (ok, n, next_key): ok False means `capacity` < n records (state unchanged)."""
+        n, m = u64(), u64()
+        rc = lib().gs_part_scan(self.ctx, bucket_key, dev_ptr, capacity, ctypes.byref(n), ctypes.byref(m))
+        if rc == GS_ERANGE and n.value > capacity:
+            return False, n.value, m.value
+        self._check(rc)
+        return True, n.value, m.value
+
+    def part_relax(self, bucket_key, dev_ptr, n):
+        m = u64()
+        self._check(lib().gs_part_relax(self.ctx, bucket_key, dev_ptr, n, ctypes.byref(m)))
+        return m.value
+
+    def part_finish(self, collect=True):
+        """-> {"t_complete", "hops"} [M, own peers] (message-major over this part's peers)."""
+        M = len(self._part_sched)
+        u0, u1 = self.part_range
+        res = {"schedule": self._part_sched, "peer_range": (u0, u1)}
+        if collect:
+            tc = np.zeros(M * (u1 - u0), np.uint64)
+            hops = np.zeros(M * (u1 - u0), np.uint8)
+            sink = GsResultSink(_ptr(tc, u64), _ptr(hops, u8))
+            self._check(lib().gs_part_finish(self.ctx, ctypes.byref(sink)))
+            res["t_complete"] = tc.reshape(M, u1 - u0)
+            res["hops"] = hops.reshape(M, u1 - u0)
+        else:
+            self._check(lib().gs_part_finish(self.ctx, None))
+        return res

@@ -205,6 +205,41 @@ gs_status gs_reset_stats(struct gs_ctx* ctx);
 /* 1: record HIP events around every relaxation launch and around gs_run. */
 gs_status gs_set_timing(struct gs_ctx* ctx, uint32_t enable);
 
+/* ---- peer-partitioned mode -------------------------
+ * Context `part` of `parts` owns the keys of peers [part*N/parts,
+ * (part+1)*N/parts); topology and mesh are built identically (replicated) in
+ * every partition. One batch (<= cfg.batch messages of equal size) is driven
+ * bucket by bucket by the caller, who performs the exchange:
+ *   k = min over parts of gs_part_begin(...)
+ *   while k != UINT64_MAX:
+ *     gs_part_scan(ctx, k, recs, cap, &n, &m1)        -- own arrivals of k's bucket
+ *     all-gather the n records of every part           -- RCCL / loop-back
+ *     gs_part_relax(ctx, k, all_recs, n_all, &m2)      -- edges into own peers
+ *     k = min over parts of min(m1, m2)
+ *   gs_part_finish(ctx, sink)                         -- sink rows hold own peers
+ * Record pointers are DEVICE pointers on the context's device; the records
+ * passed to gs_part_relax must be complete when it is called (synchronise the
+ * stream that gathered them). A scan whose records exceed `capacity` returns
+ * GS_ERANGE with *out_n = the capacity needed and changes no state: call it
+ * again with a larger buffer. IDONTWANT and lazy gossip are not supported in
+ * this mode (GS_EUNSUPPORTED). Results are bit-identical to gs_run. */
+typedef struct gs_part_record {
+    uint64_t key;      /* packed first-arrival key (t_rel | hops | src)          */
+    uint64_t start;    /* uplink start of its forward (FIFO fold by the owner)   */
+    uint32_t peer;     /* global id of the forwarding peer                        */
+    uint32_t slot;     /* message * FP + fragment within the batch               */
+} gs_part_record;
+
+gs_status gs_set_partition(struct gs_ctx* ctx, uint32_t parts, uint32_t part);
+gs_status gs_part_begin(struct gs_ctx* ctx, const gs_publish* sched, uint64_t n_msgs,
+                        uint64_t* out_min_key);
+gs_status gs_part_scan(struct gs_ctx* ctx, uint64_t bucket_key, gs_part_record* dev_records,
+                       uint64_t capacity, uint64_t* out_n, uint64_t* out_min_key);
+gs_status gs_part_relax(struct gs_ctx* ctx, uint64_t bucket_key, const gs_part_record* dev_records,
+                        uint64_t n, uint64_t* out_min_key);
+/* sink arrays are [n_msgs][own peers] (message-major over this part's peers) */
+gs_status gs_part_finish(struct gs_ctx* ctx, const gs_result_sink* sink);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,85 @@
+"""GPU parity of the peer-partitioned mode.
+
+P partitions live as P contexts on the one GPU and exchange records through
+partition.LoopbackExchange; the per-partition results, concatenated over the
+peer ranges, must equal the oracle (and gs_run) bit for bit, and the counters
+summed over partitions must equal the single-device counters."""
+import numpy as np
+import pytest
+
+import gossipsim
+import oracle
+import partition
+
+pytestmark = pytest.mark.gpu
+T0 = gossipsim.T0_NS
+
+
+def _sched(M, N, size=15000, pub0=6):
+    t = T0 + np.arange(M, dtype=np.uint64) * np.uint64(1_000_000_000)
+    return t, (pub0 + np.arange(M)) % N, np.full(M, size)
+
+
+def _parts(p, S, links, parts, batch):
+    kw = {n: getattr(p, n) for n, _ in oracle.OrParams._fields_}
+    kw["batch"] = batch
+    sims = []
+    for i in range(parts):
+        s = gossipsim.Simulator(**kw)
+        s.set_topogen_links(S, *links)
+        s.connect_gossipsub_peers()
+        s.mesh_converge()
+        s.set_partition(parts, i)
+        sims.append(s)
+    return sims
+
+
+def _check(p, S, links, parts, sched, small_buffers=False):
+    import torch
+    sims = _parts(p, S, links, parts, len(sched[0]))
+    bufs = [partition.RecordBuffer(torch.device("cuda", 0), capacity=16 if small_buffers else 1 << 16)
+            for _ in sims]
+    res, info = partition.run_partitioned(sims, sched, partition.LoopbackExchange(), bufs=bufs)
+    ref = oracle.simulate(p, S, links, sched=sched)
+    tc = np.concatenate([r["t_complete"] for r in res], axis=1)
+    hops = np.concatenate([r["hops"] for r in res], axis=1)
+    np.testing.assert_array_equal(tc, ref["t_complete"])
+    np.testing.assert_array_equal(hops, ref["hops"])
+    st = [s.stats() for s in sims]
+    for k in ("deliveries", "frag_deliveries", "relaxations", "bytes_alg", "latency_sum_ms"):
+        assert sum(x[k] for x in st) == ref["stats"][k], k
+    assert max(x["latency_max_ms"] for x in st) == ref["stats"]["latency_max_ms"]
+    assert all(x["messages"] == len(sched[0]) for x in st)
+    return info
+
+
+@pytest.mark.parametrize("parts,frags", [(1, 1), (2, 1), (3, 2), (4, 4), (2, 3)])
+def test_partitioned_matches_oracle(parts, frags):
+    p = oracle.params(peers=1200, seed=51, fragments=frags)
+    info = _check(p, 5, (50, 150, 40, 130), parts, _sched(16, 1200))
+    assert info["buckets"] > 0 and info["records"] > 0
+
+
+def test_partitioned_grows_record_buffer_and_uneven_ranges():
+    p = oracle.params(peers=1001, seed=52)  # 1001 / 3: uneven peer ranges
+    _check(p, 3, (20, 200, 10, 90), 3, _sched(9, 1001), small_buffers=True)
+
+
+def test_partitioned_knobs():
+    for kw, S, links in [(dict(peers=600, seed=53, flood_publish=0), 1, (50, 50, 50, 50)),
+                         (dict(peers=500, seed=54, muxer=1, signed_msgs=0, d=8, d_lo=6, d_hi=12), 2,
+                          (10, 100, 5, 50))]:
+        _check(oracle.params(**kw), S, links, 2, _sched(7, kw["peers"]))
+
+
+def test_partitioned_unsupported_modes_fail_loudly():
+    p = oracle.params(peers=300, seed=55, lazy_gossip=1)
+    (s,) = _parts(p, 1, (50, 50, 50, 50), 1, 4)
+    with pytest.raises(gossipsim.GossipSimError, match="GS_EUNSUPPORTED"):
+        s.part_begin(_sched(4, 300))
+    p = oracle.params(peers=300, seed=56, idontwant=1000)
+    (s,) = _parts(p, 1, (50, 50, 50, 50), 1, 4)
+    with pytest.raises(gossipsim.GossipSimError, match="GS_EUNSUPPORTED"):
+        s.part_begin(_sched(4, 300))
+    with pytest.raises(gossipsim.GossipSimError, match="GS_ESTATE"):
+        s.part_relax(1, 0, 0)
