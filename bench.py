@@ -193,7 +193,7 @@ def main():
             traffic = None
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
-            "kernel": "Delta-bucket relaxation = k_scan<1,false> + k_frontier<1,true,false>",
+            "kernel": "Delta-bucket relaxation = k_scan<1,false,false> + k_frontier<1,true,false>",
             "alg_bytes_per_launch": st["relax_bytes_alg"] / launches,
             "avg_launch_us": st["relax_ms"] * 1e3 / launches,
             "avg_scan_us": st["scan_ms"] * 1e3 / launches,
