@@ -50,7 +50,7 @@ struct DevBuf {
 // Counters written by kernels: index constants into Ctx::d_counters.
 enum : uint32_t {
   C_FD = 0, C_R = 1, C_DELIV = 2, C_LAT_SUM = 3, C_LAT_MAX = 4, C_BUCKETS = 5,
-  C_R_FWD = 6, C_MESH_CHANGES = 7, C_MESH_WAKE = 8, C_ERR = 9, C_PUSH = 10, C_GOSSIP = 11,
+  C_R_FWD = 6, C_MESH_CHANGES = 7, C_MESH_WAKE = 8, C_ERR = 9, C_PUSH = 10, C_GOSSIP = 11, C_PASSES = 12,
   C_COUNT = 16
 };
 
@@ -114,6 +114,13 @@ struct Ctx {
   DevBuf<uint8_t> d_hops_t;
   DevBuf<uint32_t> d_tables; // lat[S*S] | ser_up[S] | ser_dn[S] (u32 ns)
   DevBuf<uint64_t> d_ctrl;   // [4] triple-buffered next-min keys + spare
+  // owner-computes pull path (gs_pull_kernel.h)
+  DevBuf<uint64_t> d_rowmin; // [N] min pending key beyond the last emitted window
+  DevBuf<uint64_t> d_lrec;   // [2][N][L] per-row arrival records (gs_pull_kernel.h)
+  DevBuf<uint32_t> d_lcnt;   // [2][N]
+  DevBuf<uint8_t> d_rpos;    // [N][MESH_W] index of w in mesh(mesh[w][j])
+  bool rpos_valid = false;
+  DevBuf<uint64_t> d_pctrl;  // [3][4] pass control slots
   DevBuf<uint64_t> d_counters;  // [C_COUNT]
   uint64_t* h_pinned = nullptr; // pinned host mirror of ctrl + counters
 

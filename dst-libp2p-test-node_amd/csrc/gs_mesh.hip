@@ -271,6 +271,7 @@ uint32_t run_mesh(Ctx& c, uint32_t max_hb) {
     epoch = (uint32_t)h[0];
   }
   c.d_mesh.alloc((size_t)N * MESH_W);
+  c.rpos_valid = false;
   c.d_mcnt.alloc(N);
   k_extract<<<blocks(N), TB, 0, s>>>(a, c.d_mesh.p, c.d_mcnt.p);
   GS_HIP(hipGetLastError());

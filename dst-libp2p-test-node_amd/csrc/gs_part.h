@@ -43,15 +43,6 @@ __global__ __launch_bounds__(TB) void k_pcount(const uint32_t* __restrict__ fr_c
   if ((threadIdx.x & 63) == 0 && s) atomicAdd((unsigned long long*)&pcnt[0], (unsigned long long)s);
 }
 
-__device__ __forceinline__ void load_mesh_row(const uint32_t* mesh, uint32_t u, uint32_t (&row)[MESH_W]) {
-  const uint4* rp = reinterpret_cast<const uint4*>(mesh + (size_t)u * MESH_W);
-#pragma unroll
-  for (int q = 0; q < 4; q++) {
-    const uint4 x = rp[q];
-    row[4 * q] = x.x; row[4 * q + 1] = x.y; row[4 * q + 2] = x.z; row[4 * q + 3] = x.w;
-  }
-}
-
 // Owner side of a bucket: the frontier segments written by k_scan -> records.
 template <int FP>
 __global__ __launch_bounds__(TB) void k_pexport(RelaxArgs a, gs_part_record* __restrict__ rec, uint64_t cap,

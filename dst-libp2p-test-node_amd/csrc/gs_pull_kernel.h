@@ -1,0 +1,319 @@
+// gs_pull_kernel.h — owner-computes Delta-window pass, the default eager
+// forwarding path. Included by gs_relax.hip after
+// gs_relax_kernel.h (inside namespace gs::{anon}).
+//
+// Why: the push path (k_scan + k_frontier) issues one random 64-bit atomicMin
+// per improving send. On gfx950 a random 8-byte atomic into an HBM-sized table
+// runs at ~18 G/s chip-wide (scripts/ubench_mem.hip), and k_frontier sat on
+// that floor. Here every key row is written by its owner only:
+//
+//   one wave owns peer w's row keys[w][0..L) for the pass; it
+//    1. loads the row into registers (L <= 1024: 16 lanes-chunks of 64),
+//    2. PULL passes: reads the arrival records its mesh neighbours u emitted
+//       for window [lo, lo+D) in the previous pass — all neighbours' records
+//       in one flattened loop — and re-derives each forward u -> w exactly as
+//       relax_lane/k_precv do (w's position in mesh(u) \ {src, publisher},
+//       u's uplink start, link latency), min-reducing them in an LDS buffer,
+//    3. merges, writes changed lanes back, and emits its own arrivals of the
+//       next window as 8-byte records for the pass after,
+//    4. keeps rowmin[w] = min pending key beyond that window, so rows with
+//       nothing to apply and nothing due cost one 8-B read.
+//
+// Record (u64): start - window_lo (32) | hops (6) | j_src (5) | j_pub (5) |
+// slot (16), where j_src / j_pub are the indices of the sender's source and of
+// the message's publisher in the sender's mesh row (31 = not in the mesh). A
+// receiver w at index r = rpos[w][j] of mesh(u) is skipped if r is j_src or
+// j_pub, else its position is r + 1 - [j_src < r] - [j_pub < r, j_pub != j_src]
+// (mesh rows are sorted by id, so index order is id order).
+//
+// Exactness is the Delta-stepping argument of the push path: every send adds
+// >= D, so after applying window b's candidates all keys below the end of
+// window b+1 are final. Candidates are the same keys the push path atomically
+// min-reduces, so the result is bit-identical.
+//
+// Control (device side, no host round trip per pass): ctrl holds three slots
+// of {lo, mode, records emitted, min pending}. Pass k decides from slot k-1:
+//   records > 0  -> PULL the window whose records were just emitted;
+//   else min < INF -> EMIT the window holding the min pending key (a gap);
+//   else DONE.
+
+enum : uint64_t { PM_DONE = 0, PM_EMIT = 1, PM_PULL = 2 };
+constexpr uint32_t PULL_WAVES = TB / 64;  // rows in flight per block
+constexpr uint32_t PULL_LMAX = 1024;       // row lanes held in registers (16 chunks)
+constexpr uint32_t PULL_CH = PULL_LMAX / 64;
+constexpr uint32_t J_NONE = 31;
+
+struct PullArgs {
+  uint64_t* keys;       // [N][L]
+  uint64_t* busy;       // [N][B] uplink FIFO end per (peer, message), FP > 1
+  uint64_t* rowmin;     // [N]
+  uint64_t* lrec;       // [2][N][L] per-row arrival records
+  uint32_t* lcnt;       // [2][N]
+  const uint32_t* mesh;
+  const uint8_t* rpos;  // [N][MESH_W] index of w in mesh(mesh[w][j])
+  const uint32_t* pub;
+  const uint8_t* stage;
+  const uint32_t* tables;  // lat[S*S] | ser_up[S] | ser_dn[S] (read with scalar loads)
+  uint64_t* ctrl;          // [3][4]
+  uint64_t* counters;
+  uint64_t delta, tmax;
+  uint32_t N, B, L, S, sb, tshift, pass;
+};
+
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Per wave: CW = the row's candidate minima, then (in place) the compacted
+// arrivals; LST = their group indices. 10 KB per wave, 4 blocks per CU.
+struct PullLds {
+  uint64_t cw[PULL_WAVES][PULL_LMAX];
+  uint16_t lst[PULL_WAVES][PULL_LMAX];
+};
+
+template <int FP>
+__global__ __launch_bounds__(TB, 4) void k_pull(PullArgs a) {
+  __shared__ PullLds Ls;
+  // ---- decide this pass from the previous slot (grid-uniform) ----
+  const uint64_t* pv = a.ctrl + ((a.pass + 2) % 3) * 4;
+  uint64_t lo, mode;
+  if (pv[1] != PM_DONE && pv[2]) { mode = PM_PULL; lo = pv[1] == PM_PULL ? pv[0] + a.delta : pv[0]; }
+  else if (pv[3] != INF64) { mode = PM_EMIT; lo = ((pv[3] >> a.tshift) / a.delta) * a.delta; }
+  else { mode = PM_DONE; lo = pv[0]; }
+  uint64_t* me = a.ctrl + (a.pass % 3) * 4;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    me[0] = lo;
+    me[1] = mode;
+    uint64_t* nx = a.ctrl + ((a.pass + 1) % 3) * 4;
+    nx[2] = 0;
+    nx[3] = INF64;
+    if (mode != PM_DONE) atomicAdd((unsigned long long*)&a.counters[C_PASSES], 1ull);
+    if (mode == PM_PULL) atomicAdd((unsigned long long*)&a.counters[C_BUCKETS], 1ull);
+  }
+  if (mode == PM_DONE) return;
+
+  const bool pull = mode == PM_PULL;
+  const uint64_t wlo = pull ? lo + a.delta : lo;  // the window this pass emits
+  const uint64_t whi = wlo + a.delta;
+  // the window in key space (times above tmax cannot occur: clamp to INF)
+  const uint64_t lok = wlo > a.tmax ? INF64 : wlo << a.tshift;
+  const uint64_t hik = whi > a.tmax ? INF64 : whi << a.tshift;
+  const uint32_t LL = a.L, S = a.S;
+  const size_t NL = (size_t)a.N * LL;
+  const uint32_t pb = (a.pass + 1) & 1, nb = a.pass & 1;  // records read / written
+  const uint64_t* rrec = a.lrec + pb * NL;
+  const uint32_t* rcnt = a.lcnt + (size_t)pb * a.N;
+  uint64_t* wrec = a.lrec + nb * NL;
+  uint32_t* wcnt = a.lcnt + (size_t)nb * a.N;
+  const uint32_t* lat = a.tables;
+  const uint32_t* sup = a.tables + S * S;
+  const uint32_t* sdn = a.tables + S * S + S;
+
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint64_t* CW = Ls.cw[wv];
+  uint16_t* LST = Ls.lst[wv];
+  const uint64_t smask = (1ull << a.sb) - 1;
+  const uint32_t hmask = (1u << HOP_BITS) - 1;
+  const uint64_t lanelt = (1ull << lane) - 1;
+  uint64_t nmin = INF64, fd = 0, nr = 0, np = 0, nrec = 0;
+  uint32_t err = 0;
+
+  for (uint32_t w = blockIdx.x * PULL_WAVES + wv; w < a.N; w += gridDim.x * PULL_WAVES) {
+    // header: lane j < 16 holds mesh entry j of w, w's index in that
+    // neighbour's row, and the length of the neighbour's record list
+    uint32_t ej = EMPTY, cj = 0, rj = 0;
+    if (lane < (int)MESH_W) {
+      ej = a.mesh[(size_t)w * MESH_W + lane];
+      rj = a.rpos[(size_t)w * MESH_W + lane];
+      if (pull && ej != EMPTY) cj = rcnt[ej & 0xFFFFFFu];
+    }
+    const uint64_t rm = a.rowmin[w];
+    const uint64_t cand = __ballot(cj != 0);
+    if (cand == 0 && rm >= hik) {  // nothing to apply, nothing due in [wlo, whi)
+      if (lane == 0) wcnt[w] = 0;
+      nmin = rm < nmin ? rm : nmin;
+      continue;
+    }
+    // 1. the row into registers (16 loads in flight per lane)
+    const uint64_t* grow = a.keys + (size_t)w * LL;
+    uint64_t v[PULL_CH];
+#pragma unroll
+    for (int q = 0; q < (int)PULL_CH; q++) {
+      const uint32_t i = q * 64 + lane;
+      v[q] = i < LL ? grow[i] : INF64;
+    }
+    const uint32_t sw = a.stage[w];
+    if (pull) {
+#pragma unroll
+      for (int q = 0; q < (int)PULL_CH; q++) CW[q * 64 + lane] = INF64;
+      wave_lds_sync();
+      // 2. each neighbour's records (wave-uniform loop over the lists)
+      const uint32_t sd = sdn[sw];
+      uint64_t cm = cand;
+      while (cm) {
+        const int j = __builtin_ctzll(cm);
+        cm &= cm - 1;
+        const uint32_t e = __builtin_amdgcn_readlane(ej, j), r = __builtin_amdgcn_readlane(rj, j);
+        const uint32_t n = __builtin_amdgcn_readlane(cj, j);
+        const uint32_t u = e & 0xFFFFFFu, su = e >> STAGE_SHIFT;
+        const uint32_t ser = sup[su];
+        const uint64_t base = lo + lat[su * S + sw] + (sd > ser ? sd - ser : 0);
+        const uint64_t ubits = u;
+        const uint64_t* lr = rrec + (size_t)u * LL;
+        for (uint32_t i = lane; i < n; i += 64) {
+          const uint64_t rec = lr[i];
+          const uint32_t lo32 = (uint32_t)rec;
+          const uint32_t js = (lo32 >> 21) & 31u, jp = (lo32 >> 16) & 31u;
+          if (js == r || jp == r) continue;  // w is the source or the publisher
+          const uint32_t pos = r + 1 - (js < r ? 1u : 0u) - ((jp < r && jp != js) ? 1u : 0u);
+          const uint64_t arr = base + (rec >> 32) + (uint64_t)(pos * ser);
+          if (arr > a.tmax) err |= ERR_TIME;
+          const uint64_t hp1 = ((lo32 >> 26) & hmask) + 1;
+          const uint64_t nk = (arr << a.tshift) | (hp1 << a.sb) | ubits;
+          atomicMin((unsigned long long*)&CW[lo32 & 0xFFFFu], (unsigned long long)nk);
+        }
+      }
+      wave_lds_sync();
+    }
+    // 3. dense: merge, write back changed lanes, compact the arrivals of
+    //    [wlo, whi) in place (groups of FP lanes), min of what lies beyond
+    const bool chk_pub = wlo == 0;  // only window 0 can hold a publisher's own key
+    uint32_t cnt = 0;               // compacted groups
+    uint64_t rmin = INF64;
+#pragma unroll
+    for (int q = 0; q < (int)PULL_CH; q++) {
+      if (q * 64 < (int)LL) {  // wave-uniform
+        const uint32_t i = q * 64 + lane;
+        const bool valid = i < LL;
+        uint64_t x = v[q];
+        if (pull && valid) {
+          const uint64_t c = CW[i];
+          if (c < x) {
+            x = c;
+            a.keys[(size_t)w * LL + i] = x;
+            np++;
+          }
+        }
+        bool act = valid && (x - lok) < (hik - lok);
+        if (chk_pub && act) act = a.pub[i / FP] != w;
+        const uint64_t later = (x >= hik) ? x : INF64;
+        rmin = later < rmin ? later : rmin;
+        const uint64_t am = __ballot(act);
+        if (am) {  // wave-uniform
+          if constexpr (FP == 1) {
+            if (act) {
+              const uint32_t k = cnt + (uint32_t)__popcll(am & lanelt);
+              CW[k] = x;
+              LST[k] = (uint16_t)i;
+            }
+            cnt += (uint32_t)__popcll(am);
+          } else {
+            constexpr uint64_t gmask = (FP == 64) ? ~0ull : ((1ull << FP) - 1);
+            const int gb = lane & ~(FP - 1);
+            const bool gact = ((am >> gb) & gmask) != 0;
+            const uint64_t lm = __ballot(gact && (lane & (FP - 1)) == 0);  // group leaders
+            const uint32_t k = cnt + (uint32_t)__popcll(lm & ((1ull << gb) - 1));
+            if (gact) {
+              CW[k * FP + (lane & (FP - 1))] = x;
+              if ((lane & (FP - 1)) == 0) LST[k] = (uint16_t)(i / FP);
+            }
+            cnt += (uint32_t)__popcll(lm);
+          }
+        }
+      }
+    }
+    wave_lds_sync();
+    // 4. sparse: forward targets, uplink FIFO and one record per arrival
+    uint32_t ecnt = 0;
+    if (cnt) {
+      uint32_t mrow[MESH_W];
+      load_mesh_row(a.mesh, w, mrow);
+      const uint32_t serw = sup[sw];
+      constexpr uint32_t GPW = 64 / FP;
+      for (uint32_t g0 = 0; g0 < cnt; g0 += GPW) {
+        const uint32_t gi = g0 + (uint32_t)lane / FP;
+        const bool gv = gi < cnt;
+        const uint32_t grp = gv ? LST[gi] : 0;
+        const uint32_t i = grp * FP + (lane & (FP - 1));
+        const uint64_t x = gv ? CW[gi * FP + (lane & (FP - 1))] : INF64;
+        const uint32_t pm = gv ? a.pub[grp] : EMPTY;
+        const bool act = gv && (x - lok) < (hik - lok) && w != pm;
+        const uint32_t src = (uint32_t)(x & smask);
+        uint32_t n = 0, js = J_NONE, jp = J_NONE;  // targets: mesh(w) \ {src, publisher}
+        if (act) {
+#pragma unroll
+          for (int k = 0; k < (int)MESH_W; k++) {
+            const uint32_t y = mrow[k] & 0xFFFFFFu;
+            const bool in = mrow[k] != EMPTY;
+            js = (in && y == src) ? k : js;
+            jp = (in && y == pm) ? k : jp;
+            n += (in && y != src && y != pm) ? 1u : 0u;
+          }
+        }
+        const uint64_t start = uplink_start<FP>(a.busy, (size_t)w * a.B + grp, act, x, n, serw, a.tshift);
+        const uint32_t hp = (uint32_t)(x >> a.sb) & hmask;
+        if (act) {
+          fd++;
+          nr += n;
+          if (n && hp + 1 >= (1u << HOP_BITS)) err |= ERR_HOPS;
+          if (start - wlo >= (1ull << 32)) err |= ERR_TIME;
+        }
+        const bool want = act && n != 0;
+        const uint64_t wm = __ballot(want);
+        if (want)
+          wrec[(size_t)w * LL + ecnt + (uint32_t)__popcll(wm & lanelt)] =
+              ((start - wlo) << 32) | ((uint64_t)hp << 26) | ((uint64_t)js << 21) | ((uint64_t)jp << 16) | i;
+        ecnt += (uint32_t)__popcll(wm);
+      }
+    }
+    rmin = wave_min(rmin);
+    if (lane == 0) {
+      wcnt[w] = ecnt;
+      a.rowmin[w] = rmin;
+    }
+    nrec += ecnt;
+    nmin = rmin < nmin ? rmin : nmin;
+  }
+  nmin = wave_min(nmin);
+  fd = wave_sum(fd);
+  nr = wave_sum(nr);
+  np = wave_sum(np);
+  for (int off = 32; off > 0; off >>= 1) err |= __shfl_xor(err, off);
+  if (lane == 0) {
+    if (nrec) atomicAdd((unsigned long long*)&me[2], (unsigned long long)nrec);
+    if (nmin != INF64) atomicMin((unsigned long long*)&me[3], (unsigned long long)nmin);
+    if (fd) atomicAdd((unsigned long long*)&a.counters[C_FD], (unsigned long long)fd);
+    if (nr) atomicAdd((unsigned long long*)&a.counters[C_R_FWD], (unsigned long long)nr);
+    if (np) atomicAdd((unsigned long long*)&a.counters[C_PUSH], (unsigned long long)np);
+    if (err) atomicOr((unsigned*)&a.counters[C_ERR], err);
+  }
+}
+
+// rpos[w][j] = index of w in mesh(mesh[w][j]) (the mesh is symmetric, so it
+// exists); 0 for EMPTY entries. Once per mesh.
+__global__ __launch_bounds__(TB) void k_rpos(const uint32_t* __restrict__ mesh, uint8_t* __restrict__ rpos,
+                                             uint32_t N, uint64_t* counters) {
+  const uint64_t g = (uint64_t)blockIdx.x * TB + threadIdx.x;
+  if (g >= (uint64_t)N * MESH_W) return;
+  const uint32_t w = (uint32_t)(g / MESH_W);
+  const uint32_t e = mesh[g];
+  uint8_t r = 0;
+  if (e != EMPTY) {
+    const uint32_t* ur = mesh + (size_t)(e & 0xFFFFFFu) * MESH_W;
+    uint32_t k = 0;
+    while (k < MESH_W && ur[k] != EMPTY && (ur[k] & 0xFFFFFFu) != w) k++;
+    if (k == MESH_W || ur[k] == EMPTY) atomicOr((unsigned*)&counters[C_ERR], ERR_MESH);  // asymmetric
+    r = (uint8_t)k;
+  }
+  rpos[g] = r;
+}
+
+inline bool pull_fits(uint32_t L) { return L <= PULL_LMAX; }
+
+void pull_dispatch(uint32_t FP, const PullArgs& a, unsigned grid, hipStream_t s) {
+  switch (FP) {
+    case 1: k_pull<1><<<grid, TB, 0, s>>>(a); break;
+    case 2: k_pull<2><<<grid, TB, 0, s>>>(a); break;
+    case 4: k_pull<4><<<grid, TB, 0, s>>>(a); break;
+    case 8: k_pull<8><<<grid, TB, 0, s>>>(a); break;
+    default: k_pull<16><<<grid, TB, 0, s>>>(a); break;
+  }
+}

@@ -24,6 +24,7 @@ namespace {
 constexpr int TB = 256;
 
 #include "gs_relax_kernel.h"
+#include "gs_pull_kernel.h"
 
 
 struct SeedArgs {
@@ -34,7 +35,8 @@ struct SeedArgs {
   const uint32_t* pub;
   const uint8_t* stage;
   const uint32_t* tables;
-  uint64_t* ctrl;
+  uint64_t* ctrl;      // min seeded key (push: the first bucket; pull: slot 2's min)
+  uint64_t* rowmin;    // pull path: per-row min pending key (nullptr on the push path)
   uint64_t* counters;
   uint64_t tmax;
   uint32_t L, FP, Fe, S, sb, tshift, flood;
@@ -72,12 +74,13 @@ __global__ __launch_bounds__(TB) void k_seed(SeedArgs a) {
     const uint64_t nk = (arr << a.tshift) | (1ull << a.sb) | p;
     if (w - a.u0 >= a.un) continue;
     atomicMin((unsigned long long*)&a.keys[(size_t)(w - a.u0) * a.L + (size_t)m * a.FP + f], (unsigned long long)nk);
+    if (a.rowmin) atomicMin((unsigned long long*)&a.rowmin[w - a.u0], (unsigned long long)nk);
     nmin = nk < nmin ? nk : nmin;
   }
   nmin = wave_min(nmin);
   for (int off = 32; off > 0; off >>= 1) err |= __shfl_xor(err, off);
   if ((threadIdx.x & 63) == 0) {
-    if (nmin != INF64) atomicMin((unsigned long long*)&a.ctrl[0], (unsigned long long)nmin);
+    if (nmin != INF64) atomicMin((unsigned long long*)a.ctrl, (unsigned long long)nmin);
     if (err) atomicOr((unsigned*)&a.counters[C_ERR], err);
   }
   if (threadIdx.x == 0 && own_pub) atomicAdd((unsigned long long*)&a.counters[C_R], (unsigned long long)total);
@@ -229,10 +232,12 @@ static Batch setup_batch(Ctx& c, const gs_publish* sched, uint64_t i0, uint64_t 
   return b;
 }
 
-static void launch_seed(Ctx& c, const Batch& b, uint32_t u0, uint32_t un) {
+static void launch_seed(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, uint64_t* seed_min = nullptr,
+                        uint64_t* rowmin = nullptr) {
   SeedArgs sa{};
   sa.keys = c.d_keys.p; sa.row = c.d_row.p; sa.col = c.d_col.p; sa.mesh = c.d_mesh.p;
-  sa.pub = c.d_pub.p; sa.stage = c.d_stage.p; sa.tables = c.d_tables.p; sa.ctrl = c.d_ctrl.p;
+  sa.pub = c.d_pub.p; sa.stage = c.d_stage.p; sa.tables = c.d_tables.p;
+  sa.ctrl = seed_min ? seed_min : c.d_ctrl.p; sa.rowmin = rowmin;
   sa.counters = c.d_counters.p; sa.tmax = b.tmax; sa.L = b.L; sa.FP = b.FP; sa.Fe = b.Fe;
   sa.S = c.S; sa.sb = b.sb; sa.tshift = b.tshift; sa.flood = c.cfg.flood_publish;
   sa.u0 = u0; sa.un = un;
@@ -301,6 +306,60 @@ static void ensure_cus(Ctx& c) {
   }
 }
 
+// One batch on the owner-computes path (gs_pull_kernel.h): seed, then passes in
+// chunks of 8 until a pass decides DONE (one host read of the ctrl slots per chunk).
+template <class EvFn>
+static void run_pull_batch(Ctx& c, const Batch& b, EvFn& ev, size_t& n_ev, int dev_cus) {
+  const uint32_t N = c.cfg.peers, L = b.L;
+  hipStream_t s = c.stream;
+  const size_t NL = (size_t)N * L;
+  c.d_rowmin.alloc(N);
+  c.d_lrec.alloc(2 * NL);
+  c.d_lcnt.alloc(2 * (size_t)N);
+  c.d_pctrl.alloc(12);
+  if (!c.rpos_valid) {
+    c.d_rpos.alloc((size_t)N * MESH_W);
+    GS_HIP(hipMemsetAsync(c.d_counters.p + C_ERR, 0, 8, s));
+    k_rpos<<<(unsigned)(((uint64_t)N * MESH_W + TB - 1) / TB), TB, 0, s>>>(c.d_mesh.p, c.d_rpos.p, N, c.d_counters.p);
+    GS_HIP(hipGetLastError());
+    if (read_counter(c, C_ERR) & ERR_MESH) c.fail(GS_ERANGE, "mesh is not symmetric");
+    c.rpos_valid = true;
+  }
+  GS_HIP(hipMemsetAsync(c.d_rowmin.p, 0xFF, (size_t)N * 8, s));
+  GS_HIP(hipMemsetAsync(c.d_pctrl.p, 0, 12 * 8, s));  // every slot {lo 0, DONE, 0 records, min INF}
+  for (int q = 0; q < 3; q++) GS_HIP(hipMemsetAsync(c.d_pctrl.p + q * 4 + 3, 0xFF, 8, s));
+  launch_seed(c, b, 0, N, c.d_pctrl.p + 2 * 4 + 3, c.d_rowmin.p);
+  PullArgs pa{};
+  pa.keys = c.d_keys.p; pa.busy = c.d_busy.p; pa.rowmin = c.d_rowmin.p;
+  pa.lrec = c.d_lrec.p; pa.lcnt = c.d_lcnt.p; pa.rpos = c.d_rpos.p;
+  pa.mesh = c.d_mesh.p; pa.pub = c.d_pub.p; pa.stage = c.d_stage.p; pa.tables = c.d_tables.p;
+  pa.ctrl = c.d_pctrl.p; pa.counters = c.d_counters.p; pa.delta = b.delta; pa.tmax = b.tmax;
+  pa.N = N; pa.B = b.B; pa.L = L; pa.S = c.S; pa.sb = b.sb; pa.tshift = b.tshift;
+  // 33 KB of LDS per block: 4 blocks (16 waves, 16 rows in flight) per CU
+  const unsigned grid = (unsigned)std::max<uint64_t>(
+      1, std::min<uint64_t>(((uint64_t)N + PULL_WAVES - 1) / PULL_WAVES, (uint64_t)dev_cus * 4));
+  uint32_t pass = 0;
+  for (;;) {
+    for (uint32_t q = 0; q < 8; q++) {
+      pa.pass = pass++;
+      if (c.timing) {  // (start, mid, end): the whole pass is frontier time
+        GS_HIP(hipEventRecord(ev(n_ev), s));
+        GS_HIP(hipEventRecord(ev(n_ev + 1), s));
+        pull_dispatch(b.FP, pa, grid, s);
+        GS_HIP(hipEventRecord(ev(n_ev + 2), s));
+        n_ev += 3;
+      } else {
+        pull_dispatch(b.FP, pa, grid, s);
+      }
+    }
+    GS_HIP(hipGetLastError());
+    GS_HIP(hipMemcpyAsync(c.h_pinned, c.d_pctrl.p, 12 * 8, hipMemcpyDeviceToHost, s));
+    GS_HIP(hipStreamSynchronize(s));
+    if (c.h_pinned[((pass - 1) % 3) * 4 + 1] == PM_DONE) break;
+  }
+  c.stats.relax_launches += pass;
+}
+
 void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_result_sink* sink) {
   const uint32_t N = c.cfg.peers, F = c.cfg.fragments, FP = pow2_at_least(F);
   const uint32_t Bmax = c.cfg.batch;
@@ -308,12 +367,19 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
   GS_HIP(hipMemsetAsync(c.d_counters.p + C_ERR, 0, 8, s));
   check_schedule(c, sched, n_msgs);
   const char* var_env = getenv("GS_RELAX_VARIANT");
-  uint32_t variant = var_env && *var_env ? (uint32_t)atoi(var_env) : 13u;  // split + final bitset + read filter
+  // default: owner-computes pull (32); without it the push path: split (8) + final bitset (4) + read filter (1)
+  uint32_t variant = var_env && *var_env ? (uint32_t)atoi(var_env) : 45u;
   if ((uint64_t)N * Bmax * FP >= (1ull << 32)) {  // frontier indices are u32
     if (c.cfg.lazy_gossip) c.fail(GS_EUNSUPPORTED, "lazy gossip needs peers*batch*FP < 2^32");
     variant &= ~8u;
   }
   const bool gossip = c.cfg.lazy_gossip != 0;
+  // the pull path needs rows in LDS and no cross-row reads (IDONTWANT reads the
+  // target's key, lazy gossip pushes from heartbeats): those stay on the push path
+  const bool idw_any = c.cfg.idontwant != 0;
+  const bool pull = (variant & 32) && !gossip && !idw_any;
+  // pull rows live in registers: cap the batch at PULL_LMAX / FP messages
+  const uint32_t Bcap = pull ? std::max<uint32_t>(1, std::min<uint32_t>(Bmax, PULL_LMAX / FP)) : Bmax;
   if (gossip) {  // gossip runs on the split path only, without tile skip
     variant = (variant | 8u) & ~2u;
     const uint64_t rmax = std::max<uint64_t>(c.cfg.d_lazy, (uint64_t)c.max_degree * c.cfg.gossip_factor_milli / 1000);
@@ -349,7 +415,7 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
   while (i0 < n_msgs) {
     // a batch: up to B messages of equal size (serialisation tables are per batch)
     uint64_t i1 = i0 + 1;
-    while (i1 < n_msgs && i1 - i0 < Bmax && sched[i1].msg_size == sched[i0].msg_size) i1++;
+    while (i1 < n_msgs && i1 - i0 < Bcap && sched[i1].msg_size == sched[i0].msg_size) i1++;
     const Batch b = setup_batch(c, sched, i0, i1);
     const uint32_t B = b.B, L = b.L;
     if (gossip) {  // heartbeats at hb_phase + h*hb: first one at or after each t_pub
@@ -369,7 +435,7 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     GS_HIP(hipMemsetAsync(c.d_keys.p, 0xFF, total * 8, s));
     if (FP > 1) GS_HIP(hipMemsetAsync(c.d_busy.p, 0, (size_t)N * B * 8, s));
     if (variant & 2) GS_HIP(hipMemsetAsync(c.d_meta.p, 0, (total + 63) / 64 * sizeof(TileMeta), s));
-    if (variant & 12) GS_HIP(hipMemsetAsync(c.d_fbits.p, 0, (total + 63) / 64 * 8, s));
+    if ((variant & 12) && !pull) GS_HIP(hipMemsetAsync(c.d_fbits.p, 0, (total + 63) / 64 * 8, s));
     if ((variant & 10) == 10) {  // split + tile skip: tmin 0 forces every tile's first scan
       c.d_tmin.alloc(max_tiles);
       c.d_touched.alloc(max_tiles);
@@ -380,6 +446,14 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     // with gossip the first bucket is [0, Delta): the publisher's own IHAVEs
     // can land before the first eager arrival
     if (gossip) GS_HIP(hipMemsetAsync(c.d_ctrl.p, 0, 8, s));
+    if (pull) {
+      if (c.cfg.idontwant && b.payload >= c.cfg.idontwant) c.fail(GS_EINVAL, "internal: IDONTWANT on the pull path");
+      run_pull_batch(c, b, ev, n_ev, dev_cus);
+      c.stats.messages += B;
+      launch_complete(c, b, 0, N, sink, i0);
+      i0 = i1;
+      continue;
+    }
     launch_seed(c, b, 0, N);
 
     RelaxArgs ra{};

@@ -81,6 +81,15 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+__device__ __forceinline__ void load_mesh_row(const uint32_t* mesh, uint32_t u, uint32_t (&row)[MESH_W]) {
+  const uint4* rp = reinterpret_cast<const uint4*>(mesh + (size_t)u * MESH_W);
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const uint4 x = rp[q];
+    row[4 * q] = x.x; row[4 * q + 1] = x.y; row[4 * q + 2] = x.z; row[4 * q + 3] = x.w;
+  }
+}
+
 // Shared per-bucket constants in LDS.
 struct BucketLds {
   uint32_t lat[MAX_STAGES * MAX_STAGES];

@@ -27,6 +27,7 @@ for s in ${STEPS:-tests smoke bench prof}; do
     bench) step bench 600 python bench.py --steps ${BENCH_STEPS:-20} --warmup 3 ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py $PROFARGS ;;
     ab) step ab_relax 600 python scripts/ab_relax.py ${AB_ARGS:-} ;;
+    ubench) step ubench_mem 300 ./build_tools/ubench_mem ;;
     pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KRE" -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py $PROFARGS ;
          step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KRE" -d "$OUT/pmc_write" -o run --output-format csv -- python bench.py $PROFARGS ;;
   esac

@@ -172,10 +172,10 @@ def test_large_graph_properties_and_sampled_parity():
         np.testing.assert_array_equal(res["hops"][m], hp[0])
 
 
-@pytest.mark.parametrize("variant", list(range(8)) + [8, 9, 10, 11, 13, 15])
+@pytest.mark.parametrize("variant", list(range(8)) + [8, 9, 10, 11, 13, 15, 45])
 def test_relax_kernel_variants_exact(variant, monkeypatch):
     """Every bucket implementation (fused with read-filter / tile-skip / final-bitset,
-    split scan+frontier) is bit-exact."""
+    split scan+frontier, owner-computes pull = 45, the default) is bit-exact."""
     monkeypatch.setenv("GS_RELAX_VARIANT", str(variant))
     p = oracle.params(peers=2000, seed=31, fragments=2)
     compare(p, 5, (50, 150, 40, 130), _sched(40, 2000), batch=16)
