@@ -93,9 +93,13 @@ __global__ __launch_bounds__(TB, 4) void k_pull(PullArgs a) {
   const bool pull = mode == PM_PULL;
   const uint64_t wlo = pull ? lo + a.delta : lo;  // the window this pass emits
   const uint64_t whi = wlo + a.delta;
-  // the window in key space (times above tmax cannot occur: clamp to INF)
+  // The window in key space. Window bounds are multiples of 2^(32 - tshift) ns
+  // (the host rounds D down to that grain), so a key's position relative to
+  // them is decided by its high 32 bits alone; keys stay below hi word
+  // 0xFFFFFFFF (tmax is lowered by one grain), which is kept for INF.
   const uint64_t lok = wlo > a.tmax ? INF64 : wlo << a.tshift;
   const uint64_t hik = whi > a.tmax ? INF64 : whi << a.tshift;
+  const uint32_t hlo = (uint32_t)(lok >> 32), hhi = (uint32_t)(hik >> 32), hspan = hhi - hlo;
   const uint32_t LL = a.L, S = a.S;
   const size_t NL = (size_t)a.N * LL;
   const uint32_t pb = (a.pass + 1) & 1, nb = a.pass & 1;  // records read / written
@@ -116,20 +120,39 @@ __global__ __launch_bounds__(TB, 4) void k_pull(PullArgs a) {
   uint64_t nmin = INF64, fd = 0, nr = 0, np = 0, nrec = 0;
   uint32_t err = 0;
 
-  for (uint32_t w = blockIdx.x * PULL_WAVES + wv; w < a.N; w += gridDim.x * PULL_WAVES) {
-    // header: lane j < 16 holds mesh entry j of w, w's index in that
-    // neighbour's row, and the length of the neighbour's record list
-    uint32_t ej = EMPTY, cj = 0, rj = 0;
+  // Row headers are software-pipelined one row ahead: lane j < 16 holds mesh
+  // entry j of the row, w's index in that neighbour's row, and the length of
+  // the neighbour's record list; plus rowmin. The next row's entries are
+  // loaded while this row is processed, its list lengths after step 2.
+  const uint32_t stride = gridDim.x * PULL_WAVES;
+  uint32_t w = blockIdx.x * PULL_WAVES + wv;
+  uint32_t ej = EMPTY, cj = 0, rj = 0;
+  uint64_t rm = INF64;
+  if (w < a.N) {
     if (lane < (int)MESH_W) {
       ej = a.mesh[(size_t)w * MESH_W + lane];
       rj = a.rpos[(size_t)w * MESH_W + lane];
       if (pull && ej != EMPTY) cj = rcnt[ej & 0xFFFFFFu];
     }
-    const uint64_t rm = a.rowmin[w];
+    rm = a.rowmin[w];
+  }
+  for (; w < a.N; w += stride) {
+    const uint32_t w2 = w + stride;
+    uint32_t ej2 = EMPTY, rj2 = 0, cj2 = 0;
+    uint64_t rm2 = INF64;
+    if (w2 < a.N) {  // wave-uniform
+      if (lane < (int)MESH_W) {
+        ej2 = a.mesh[(size_t)w2 * MESH_W + lane];
+        rj2 = a.rpos[(size_t)w2 * MESH_W + lane];
+      }
+      rm2 = a.rowmin[w2];
+    }
     const uint64_t cand = __ballot(cj != 0);
     if (cand == 0 && rm >= hik) {  // nothing to apply, nothing due in [wlo, whi)
       if (lane == 0) wcnt[w] = 0;
       nmin = rm < nmin ? rm : nmin;
+      if (pull && lane < (int)MESH_W && ej2 != EMPTY) cj2 = rcnt[ej2 & 0xFFFFFFu];
+      ej = ej2; rj = rj2; cj = cj2; rm = rm2;
       continue;
     }
     // 1. the row into registers (16 loads in flight per lane)
@@ -145,39 +168,65 @@ __global__ __launch_bounds__(TB, 4) void k_pull(PullArgs a) {
 #pragma unroll
       for (int q = 0; q < (int)PULL_CH; q++) CW[q * 64 + lane] = INF64;
       wave_lds_sync();
-      // 2. each neighbour's records (wave-uniform loop over the lists)
+      // 2. the neighbours' records: lists in groups of 4, two 64-record chunks
+      //    each, so up to 8 independent record loads per lane are in flight
       const uint32_t sd = sdn[sw];
       uint64_t cm = cand;
       while (cm) {
-        const int j = __builtin_ctzll(cm);
-        cm &= cm - 1;
-        const uint32_t e = __builtin_amdgcn_readlane(ej, j), r = __builtin_amdgcn_readlane(rj, j);
-        const uint32_t n = __builtin_amdgcn_readlane(cj, j);
-        const uint32_t u = e & 0xFFFFFFu, su = e >> STAGE_SHIFT;
-        const uint32_t ser = sup[su];
-        const uint64_t base = lo + lat[su * S + sw] + (sd > ser ? sd - ser : 0);
-        const uint64_t ubits = u;
-        const uint64_t* lr = rrec + (size_t)u * LL;
-        for (uint32_t i = lane; i < n; i += 64) {
-          const uint64_t rec = lr[i];
-          const uint32_t lo32 = (uint32_t)rec;
-          const uint32_t js = (lo32 >> 21) & 31u, jp = (lo32 >> 16) & 31u;
-          if (js == r || jp == r) continue;  // w is the source or the publisher
-          const uint32_t pos = r + 1 - (js < r ? 1u : 0u) - ((jp < r && jp != js) ? 1u : 0u);
-          const uint64_t arr = base + (rec >> 32) + (uint64_t)(pos * ser);
-          if (arr > a.tmax) err |= ERR_TIME;
-          const uint64_t hp1 = ((lo32 >> 26) & hmask) + 1;
-          const uint64_t nk = (arr << a.tshift) | (hp1 << a.sb) | ubits;
-          atomicMin((unsigned long long*)&CW[lo32 & 0xFFFFu], (unsigned long long)nk);
+        uint32_t U[4], R4[4], NN[4], SER[4];
+        uint64_t BASE[4];
+        uint32_t maxn = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          U[k] = 0; R4[k] = 0; NN[k] = 0; SER[k] = 0; BASE[k] = 0;
+          if (cm) {  // wave-uniform
+            const int j = __builtin_ctzll(cm);
+            cm &= cm - 1;
+            const uint32_t e = __builtin_amdgcn_readlane(ej, j);
+            U[k] = e & 0xFFFFFFu;
+            R4[k] = __builtin_amdgcn_readlane(rj, j);
+            NN[k] = __builtin_amdgcn_readlane(cj, j);
+            const uint32_t su = e >> STAGE_SHIFT;
+            SER[k] = sup[su];
+            BASE[k] = lo + lat[su * S + sw] + (sd > SER[k] ? sd - SER[k] : 0);
+            maxn = NN[k] > maxn ? NN[k] : maxn;
+          }
+        }
+        for (uint32_t i0 = 0; i0 < maxn; i0 += 128) {
+          uint64_t rec[4][2];
+#pragma unroll
+          for (int k = 0; k < 4; k++)
+#pragma unroll
+            for (int c = 0; c < 2; c++) {
+              const uint32_t i = i0 + c * 64 + lane;
+              rec[k][c] = i < NN[k] ? rrec[(size_t)U[k] * LL + i] : ~0ull;
+            }
+#pragma unroll
+          for (int k = 0; k < 4; k++)
+#pragma unroll
+            for (int c = 0; c < 2; c++) {
+              const uint64_t rc = rec[k][c];
+              if (rc == ~0ull) continue;  // no record (records never have all bits set)
+              const uint32_t lo32 = (uint32_t)rc, r = R4[k];
+              const uint32_t js = (lo32 >> 21) & 31u, jp = (lo32 >> 16) & 31u;
+              if (js == r || jp == r) continue;  // w is the source or the publisher
+              const uint32_t pos = r + 1 - (js < r ? 1u : 0u) - ((jp < r && jp != js) ? 1u : 0u);
+              const uint64_t arr = BASE[k] + (rc >> 32) + (uint64_t)(pos * SER[k]);
+              if (arr > a.tmax) err |= ERR_TIME;
+              const uint64_t hp1 = ((lo32 >> 26) & hmask) + 1;
+              const uint64_t nk = (arr << a.tshift) | (hp1 << a.sb) | U[k];
+              atomicMin((unsigned long long*)&CW[lo32 & 0xFFFFu], (unsigned long long)nk);
+            }
         }
       }
       wave_lds_sync();
     }
+    if (pull && lane < (int)MESH_W && ej2 != EMPTY) cj2 = rcnt[ej2 & 0xFFFFFFu];  // next row's lists
     // 3. dense: merge, write back changed lanes, compact the arrivals of
     //    [wlo, whi) in place (groups of FP lanes), min of what lies beyond
     const bool chk_pub = wlo == 0;  // only window 0 can hold a publisher's own key
     uint32_t cnt = 0;               // compacted groups
-    uint64_t rmin = INF64;
+    uint32_t rmin = ~0u;            // high word of the min key beyond the window
 #pragma unroll
     for (int q = 0; q < (int)PULL_CH; q++) {
       if (q * 64 < (int)LL) {  // wave-uniform
@@ -192,9 +241,10 @@ __global__ __launch_bounds__(TB, 4) void k_pull(PullArgs a) {
             np++;
           }
         }
-        bool act = valid && (x - lok) < (hik - lok);
+        const uint32_t hx = (uint32_t)(x >> 32);
+        bool act = valid && (hx - hlo) < hspan;
         if (chk_pub && act) act = a.pub[i / FP] != w;
-        const uint64_t later = (x >= hik) ? x : INF64;
+        const uint32_t later = hx >= hhi ? hx : ~0u;
         rmin = later < rmin ? later : rmin;
         const uint64_t am = __ballot(act);
         if (am) {  // wave-uniform
@@ -224,8 +274,7 @@ __global__ __launch_bounds__(TB, 4) void k_pull(PullArgs a) {
     // 4. sparse: forward targets, uplink FIFO and one record per arrival
     uint32_t ecnt = 0;
     if (cnt) {
-      uint32_t mrow[MESH_W];
-      load_mesh_row(a.mesh, w, mrow);
+      const uint32_t deg = (uint32_t)__popcll(__ballot(ej != EMPTY));  // rows are packed
       const uint32_t serw = sup[sw];
       constexpr uint32_t GPW = 64 / FP;
       for (uint32_t g0 = 0; g0 < cnt; g0 += GPW) {
@@ -235,19 +284,16 @@ __global__ __launch_bounds__(TB, 4) void k_pull(PullArgs a) {
         const uint32_t i = grp * FP + (lane & (FP - 1));
         const uint64_t x = gv ? CW[gi * FP + (lane & (FP - 1))] : INF64;
         const uint32_t pm = gv ? a.pub[grp] : EMPTY;
-        const bool act = gv && (x - lok) < (hik - lok) && w != pm;
+        const bool act = gv && ((uint32_t)(x >> 32) - hlo) < hspan && w != pm;
         const uint32_t src = (uint32_t)(x & smask);
-        uint32_t n = 0, js = J_NONE, jp = J_NONE;  // targets: mesh(w) \ {src, publisher}
-        if (act) {
-#pragma unroll
-          for (int k = 0; k < (int)MESH_W; k++) {
-            const uint32_t y = mrow[k] & 0xFFFFFFu;
-            const bool in = mrow[k] != EMPTY;
-            js = (in && y == src) ? k : js;
-            jp = (in && y == pm) ? k : jp;
-            n += (in && y != src && y != pm) ? 1u : 0u;
-          }
+        uint32_t js = J_NONE, jp = J_NONE;  // indices of src / publisher in mesh(w)
+        for (uint32_t k = 0; k < deg; k++) {  // wave-uniform: entry k from lane k
+          const uint32_t y = __builtin_amdgcn_readlane(ej, k) & 0xFFFFFFu;
+          js = y == src ? k : js;
+          jp = y == pm ? k : jp;
         }
+        // targets: mesh(w) \ {src, publisher}
+        const uint32_t n = act ? deg - (js != J_NONE ? 1u : 0u) - ((jp != J_NONE && jp != js) ? 1u : 0u) : 0u;
         const uint64_t start = uplink_start<FP>(a.busy, (size_t)w * a.B + grp, act, x, n, serw, a.tshift);
         const uint32_t hp = (uint32_t)(x >> a.sb) & hmask;
         if (act) {
@@ -264,13 +310,18 @@ __global__ __launch_bounds__(TB, 4) void k_pull(PullArgs a) {
         ecnt += (uint32_t)__popcll(wm);
       }
     }
-    rmin = wave_min(rmin);
+    for (int off = 32; off > 0; off >>= 1) {
+      const uint32_t y = __shfl_xor(rmin, off);
+      rmin = y < rmin ? y : rmin;
+    }
+    const uint64_t rmk = rmin == ~0u ? INF64 : (uint64_t)rmin << 32;
     if (lane == 0) {
       wcnt[w] = ecnt;
-      a.rowmin[w] = rmin;
+      a.rowmin[w] = rmk;
     }
     nrec += ecnt;
-    nmin = rmin < nmin ? rmin : nmin;
+    nmin = rmk < nmin ? rmk : nmin;
+    ej = ej2; rj = rj2; cj = cj2; rm = rm2;
   }
   nmin = wave_min(nmin);
   fd = wave_sum(fd);
@@ -306,7 +357,8 @@ __global__ __launch_bounds__(TB) void k_rpos(const uint32_t* __restrict__ mesh, 
   rpos[g] = r;
 }
 
-inline bool pull_fits(uint32_t L) { return L <= PULL_LMAX; }
+// Window grain of the pull path: one unit of the key's high 32-bit word.
+inline uint64_t pull_grain(uint32_t tshift) { return tshift >= 32 ? 1ull : 1ull << (32 - tshift); }
 
 void pull_dispatch(uint32_t FP, const PullArgs& a, unsigned grid, hipStream_t s) {
   switch (FP) {

@@ -333,7 +333,10 @@ static void run_pull_batch(Ctx& c, const Batch& b, EvFn& ev, size_t& n_ev, int d
   pa.keys = c.d_keys.p; pa.busy = c.d_busy.p; pa.rowmin = c.d_rowmin.p;
   pa.lrec = c.d_lrec.p; pa.lcnt = c.d_lcnt.p; pa.rpos = c.d_rpos.p;
   pa.mesh = c.d_mesh.p; pa.pub = c.d_pub.p; pa.stage = c.d_stage.p; pa.tables = c.d_tables.p;
-  pa.ctrl = c.d_pctrl.p; pa.counters = c.d_counters.p; pa.delta = b.delta; pa.tmax = b.tmax;
+  // windows on the key's high-word grain (gs_pull_kernel.h); the caller checked delta >= grain
+  const uint64_t grain = pull_grain(b.tshift);
+  pa.ctrl = c.d_pctrl.p; pa.counters = c.d_counters.p; pa.delta = b.delta / grain * grain;
+  pa.tmax = b.tmax - grain;
   pa.N = N; pa.B = b.B; pa.L = L; pa.S = c.S; pa.sb = b.sb; pa.tshift = b.tshift;
   // 33 KB of LDS per block: 4 blocks (16 waves, 16 rows in flight) per CU
   const unsigned grid = (unsigned)std::max<uint64_t>(
@@ -446,8 +449,7 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     // with gossip the first bucket is [0, Delta): the publisher's own IHAVEs
     // can land before the first eager arrival
     if (gossip) GS_HIP(hipMemsetAsync(c.d_ctrl.p, 0, 8, s));
-    if (pull) {
-      if (c.cfg.idontwant && b.payload >= c.cfg.idontwant) c.fail(GS_EINVAL, "internal: IDONTWANT on the pull path");
+    if (pull && b.delta >= pull_grain(b.tshift)) {
       run_pull_batch(c, b, ev, n_ev, dev_cus);
       c.stats.messages += B;
       launch_complete(c, b, 0, N, sink, i0);
