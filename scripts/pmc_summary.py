@@ -5,12 +5,13 @@ python scripts/pmc_summary.py <fetch_counter_collection.csv> <write_counter_coll
 
 FETCH_SIZE / WRITE_SIZE are in KB per dispatch. On gfx950 FETCH_SIZE reports
 half the bytes of a coalesced streaming read (MI355X_MICROARCH.md, HBM
-section); we calibrate that factor on our own k_scan, whose reads are known
-exactly: it streams every key once per non-empty bucket (8 B x peers x
-batch), so read_factor = 8*N*B*buckets / sum(FETCH_SIZE of k_scan). The same
-factor is applied to every kernel's FETCH_SIZE ("corrected"); WRITE_SIZE is
-taken as is. The traffic json carries the relaxation (k_scan + k_frontier)
-bytes per launch for bench.py's roofline.traffic.
+section); we calibrate that factor on a kernel of our own whose reads are
+known exactly: k_complete streams every key once per batch (8 B x peers x
+batch x FP, 8-byte lanes, the same access width as the pull pass's row reads),
+or, on the push path, k_scan per non-empty bucket. The same factor is applied
+to every kernel's FETCH_SIZE ("corrected"); WRITE_SIZE is taken as is. The
+traffic json carries the relaxation kernel's bytes per launch (k_pull, or
+k_scan + k_frontier) for bench.py's roofline.traffic.
 """
 import argparse
 import csv
@@ -43,12 +44,19 @@ def main():
     ap.add_argument("--traffic-json")
     ap.add_argument("--peers", type=int)
     ap.add_argument("--batch", type=int)
-    ap.add_argument("--buckets", type=int, help="non-empty buckets in the profiled run (calibration)")
+    ap.add_argument("--buckets", type=int, help="non-empty buckets in the profiled run (k_scan calibration)")
+    ap.add_argument("--fp", type=int, default=1, help="fragment lanes per message (k_complete calibration)")
     a = ap.parse_args()
     fe, wr = load(a.fetch, "FETCH_SIZE"), load(a.write, "WRITE_SIZE")
     factor, calib = 2.0, "guide value (x2 on streaming reads)"
     scan = [k for k in fe if k.startswith("k_scan<")]
-    if scan and a.peers and a.batch and a.buckets:
+    comp = [k for k in fe if k.startswith("k_complete<")]
+    if comp and a.peers and a.batch:
+        known = 8.0 * a.peers * a.batch * a.fp * len(fe[comp[0]])
+        got = sum(fe[comp[0]]) * 1024.0
+        factor, calib = known / got, "k_complete: %d launches x %d peers x %d msgs x %d lanes x 8 B / FETCH_SIZE" % (
+            len(fe[comp[0]]), a.peers, a.batch, a.fp)
+    elif scan and a.peers and a.batch and a.buckets:
         known = 8.0 * a.peers * a.batch * a.buckets
         got = sum(fe[scan[0]]) * 1024.0
         factor, calib = known / got, "k_scan: %d buckets x %d peers x %d msgs x 8 B / FETCH_SIZE" % (
@@ -63,7 +71,8 @@ def main():
                              "hbm_bytes_per_launch_corrected": fm * factor + wm}
     json.dump(out, open(a.out, "w"), indent=1)
     if a.traffic_json:
-        rel = [k for k in out["kernels"] if k.startswith("k_scan<") or k.startswith("k_frontier<")]
+        rel = [k for k in out["kernels"] if k.startswith("k_pull<")] or \
+            [k for k in out["kernels"] if k.startswith("k_scan<") or k.startswith("k_frontier<")]
         launches = max(out["kernels"][k]["launches"] for k in rel)
         per_launch = sum(out["kernels"][k]["hbm_bytes_per_launch_corrected"] for k in rel)
         json.dump({"peers": a.peers, "batch": a.batch, "kernels": rel, "launches": launches,

@@ -1,5 +1,5 @@
 // ubench_mem.hip — random 8-byte access rates on gfx950, to size the relax
-// kernels (DESIGN.md §4.1). Standalone: hipcc -O3 --offload-arch=gfx950.
+// kernels (DESIGN.md §4.1-4.2). Standalone: hipcc -O3 --offload-arch=gfx950.
 //
 // Every lane makes ITERS accesses at hashed indices into a u64 table of T
 // bytes; a "cluster" of C consecutive lanes shares one 64-B sector (C = 1:
