@@ -22,7 +22,7 @@ constexpr uint32_t MAX_DEG = 256;     // per-row working sets of the mesh kernel
 constexpr uint32_t MAX_FRAGS = 16;    // FRAGMENTS (topogen allows 1..9)
 constexpr uint32_t STAGE_SHIFT = 24;  // packed mesh entry: stage << 24 | peer
 
-enum : uint32_t { P_DIAL = 1, P_DIAL_ORDER = 2, P_GRAFT = 3, P_PRUNE = 4, P_OUT_GRAFT = 5, P_GOSSIP = 6 };
+enum : uint32_t { P_DIAL = 1, P_DIAL_ORDER = 2, P_GRAFT = 3, P_PRUNE = 4, P_OUT_GRAFT = 5, P_GOSSIP = 6, P_CHURN = 7 };
 enum : uint8_t { F_OUT = 1, F_MESH = 2 };
 enum : uint8_t { PR_GRAFT = 1, PR_PRUNE = 2, PR_ACCEPT = 4 };
 
@@ -49,6 +49,15 @@ GS_HD uint64_t mulhi64(uint64_t a, uint64_t b) {
 }
 // Uniform draw in [0, n) (multiply-high; bias <= n / 2^64).
 GS_HD uint64_t rand_below(uint64_t x, uint64_t n) { return mulhi64(x, n); }
+
+// Churn: peer u is offline during heartbeat epoch h >= 1 iff
+// a departure was drawn at one of the epochs h-down+1..h.
+GS_HD bool offline_draw(uint64_t seed, uint32_t ppm, uint32_t down, uint32_t u, uint64_t h) {
+  if (!ppm || h == 0) return false;
+  for (uint64_t k = 0; k < down && k < h; k++)
+    if (rand_below(rng(seed, P_CHURN, u, (uint32_t)(h - k), 0), 1000000) < ppm) return true;
+  return false;
+}
 
 GS_HD uint32_t bits_for(uint32_t n) { uint32_t b = 1; while ((1ull << b) < n) b++; return b; }
 

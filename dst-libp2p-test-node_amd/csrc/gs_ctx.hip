@@ -41,6 +41,8 @@ static void validate(const gs_config& c) {
   if (c.d_out > c.d) bad("need D_out <= D");
   if (c.heartbeat_ns == 0) bad("heartbeat interval must be > 0");
   if (c.batch < 1 || c.batch > 65536) bad("batch must be in 1..65536");
+  if (c.churn_ppm > 1000000) bad("churn_ppm must be <= 1000000");
+  if (c.churn_ppm && (c.churn_down < 1 || c.churn_horizon < 1)) bad("churn needs churn_down >= 1 and churn_horizon >= 1");
 }
 
 }  // namespace gs

@@ -39,6 +39,9 @@ extern "C" void gs_config_default(gs_config* c) {
   c->batch = 1024;
   c->history_gossip = 3;          // libp2p-gossipsub default (not overridden, main.rs:223-241)
   c->hb_phase_ns = 0;
+  c->churn_ppm = 0;               // frozen mesh (the reference has no churn)
+  c->churn_down = 10;             // rejoin after 10 epochs
+  c->churn_horizon = 16;
 }
 
 namespace {
@@ -92,6 +95,10 @@ extern "C" gs_status gs_config_from_env(gs_config* c, char* err, size_t err_len)
   if (env_u64("GS_BATCH", &x, err, err_len, &bad)) c->batch = (uint32_t)x;
   if (env_u64("GS_DEVICE", &x, err, err_len, &bad)) c->device = (int32_t)x;
   if (env_u64("GS_IDONTWANT", &x, err, err_len, &bad)) c->idontwant = (uint32_t)x;
+  if (env_u64("GS_CHURN_PPM", &x, err, err_len, &bad)) c->churn_ppm = (uint32_t)x;
+  if (env_u64("GS_CHURN_DOWN", &x, err, err_len, &bad)) c->churn_down = (uint32_t)x;
+  if (env_u64("GS_CHURN_HORIZON", &x, err, err_len, &bad)) c->churn_horizon = (uint32_t)x;
+  if (env_u64("GS_HB_PHASE_NS", &x, err, err_len, &bad)) c->hb_phase_ns = x;
   const char* gf = getenv("GOSSIPSUB_GOSSIP_FACTOR");
   if (gf && *gf) {
     char* end = nullptr;

@@ -89,6 +89,14 @@ struct Ctx {
   DevBuf<uint32_t> d_until;  // [nnz] back-off: graft refused while epoch < until
   DevBuf<uint8_t> d_prop;    // [nnz] per-epoch GRAFT/PRUNE/ACCEPT bits
   DevBuf<uint32_t> d_mesh;   // [N*MESH_W] packed stage<<24|peer, EMPTY padded
+  DevBuf<uint32_t> d_lat32;  // [S*S] u32 latency for the mesh kernels
+  // churn: ring of per-epoch snapshots, slot = epoch % ring_R
+  DevBuf<uint64_t> d_off;       // offline bitset scratch (gs_mesh_converge)
+  DevBuf<uint32_t> d_ring_mesh; // [R][N][MESH_W]
+  DevBuf<uint64_t> d_ring_off;  // [R][(N+63)/64]
+  DevBuf<uint64_t> d_q0, d_r0;  // [B] epoch of t_pub, t_pub - start of that epoch
+  uint32_t ring_R = 0;
+  uint64_t churn_state = 0, ring_lo = 1, ring_hi = 0;  // mesh state epoch; valid ring epochs
   DevBuf<uint8_t> d_mcnt;    // [N]
 
   // dissemination (per batch)
@@ -144,6 +152,7 @@ struct Ctx {
 // ---- launchers (gs_topology.hip / gs_mesh.hip / gs_relax.hip) ----
 void launch_topology(Ctx& c);
 uint32_t run_mesh(Ctx& c, uint32_t max_heartbeats);
+void churn_ring(Ctx& c, uint64_t h_lo, uint64_t h_hi);
 void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_result_sink* sink);
 void part_set(Ctx& c, uint32_t parts, uint32_t part);
 uint64_t part_begin(Ctx& c, const gs_publish* sched, uint64_t n_msgs);

@@ -11,6 +11,12 @@
 //      D_hi-unless-outbound rejections),
 //   C  PRUNEs and rejections applied, both ends back off.
 // Random choices use per-(peer, epoch, candidate) keys: take the r smallest.
+//
+// Churn: each epoch first draws the offline set (k_offline),
+// drops mesh links of offline peers without back-off (k_disconnect), and the
+// heartbeat grafts online candidates only. gs_run keeps a ring of per-epoch
+// snapshots {mesh ELL, offline bitset} (slot = epoch mod R) that the
+// relaxation kernels index by the epoch each event falls in.
 #include "gs_internal.h"
 
 namespace gs {
@@ -28,6 +34,7 @@ struct MeshArgs {
   uint32_t* until;
   const uint8_t* stage;
   const uint32_t* lat;  // S*S ns
+  const uint64_t* off;  // offline bitset of this epoch (churn), nullptr: everyone online
   uint64_t* counters;
   uint64_t seed;
   uint32_t N, S, epoch, bo, d, d_lo, d_hi, d_out;
@@ -52,9 +59,30 @@ __device__ __forceinline__ void top_insert(uint64_t* kk, uint32_t* ee, uint32_t&
   n++;
 }
 
-__global__ __launch_bounds__(TB) void k_heartbeat(MeshArgs a) {
+__device__ __forceinline__ bool is_off(const uint64_t* off, uint32_t u) {
+  return off && ((off[u >> 6] >> (u & 63)) & 1);
+}
+
+// Offline set of epoch h: one bit per peer, one u64 word per wave.
+__global__ __launch_bounds__(TB) void k_offline(uint32_t N, uint64_t seed, uint32_t ppm, uint32_t down, uint64_t h,
+                                                uint64_t* off) {
+  const uint32_t u = blockIdx.x * TB + threadIdx.x;
+  const uint64_t m = __ballot(u < N && offline_draw(seed, ppm, down, u, h));
+  if ((threadIdx.x & 63) == 0 && u < N) off[u >> 6] = m;
+}
+
+// Links to offline peers leave the mesh (a disconnect, not a PRUNE: no back-off).
+__global__ __launch_bounds__(TB) void k_disconnect(MeshArgs a) {
   const uint32_t u = blockIdx.x * TB + threadIdx.x;
   if (u >= a.N) return;
+  const bool ou = is_off(a.off, u);
+  for (uint64_t e = a.row[u]; e < a.row[u + 1]; e++)
+    if (ou || is_off(a.off, a.col[e])) a.flags[e] &= (uint8_t)~F_MESH;
+}
+
+__global__ __launch_bounds__(TB) void k_heartbeat(MeshArgs a) {
+  const uint32_t u = blockIdx.x * TB + threadIdx.x;
+  if (u >= a.N || is_off(a.off, u)) return;
   const uint64_t b = a.row[u], en = a.row[u + 1];
   uint32_t m = 0, o = 0;
   for (uint64_t e = b; e < en; e++) {
@@ -68,7 +96,7 @@ __global__ __launch_bounds__(TB) void k_heartbeat(MeshArgs a) {
   if (m < a.d_lo) {  // graft mesh_n - |mesh| random eligible peers
     const uint32_t want = a.d - m;
     for (uint64_t e = b; e < en; e++)
-      if (!(a.flags[e] & F_MESH) && a.epoch > a.until[e])
+      if (!(a.flags[e] & F_MESH) && a.epoch > a.until[e] && !is_off(a.off, a.col[e]))
         top_insert(kk, ee, n, want, rng(a.seed, P_GRAFT, u, a.epoch, a.col[e]), (uint32_t)(e - b));
     for (uint32_t q = 0; q < n; q++) {
       a.prop[b + ee[q]] |= PR_GRAFT;
@@ -110,7 +138,8 @@ __global__ __launch_bounds__(TB) void k_heartbeat(MeshArgs a) {
     const uint32_t want = a.d_out - oo;
     for (uint64_t e = b; e < en; e++) {
       const uint8_t f = a.flags[e];
-      if ((f & F_OUT) && !(f & F_MESH) && !(a.prop[e] & PR_GRAFT) && a.epoch > a.until[e])
+      if ((f & F_OUT) && !(f & F_MESH) && !(a.prop[e] & PR_GRAFT) && a.epoch > a.until[e] &&
+          !is_off(a.off, a.col[e]))
         top_insert(kk, ee, n, want, rng(a.seed, P_OUT_GRAFT, u, a.epoch, a.col[e]),
                    (uint32_t)(e - b));
     }
@@ -224,33 +253,99 @@ __global__ __launch_bounds__(TB) void k_extract(MeshArgs a, uint32_t* mesh, uint
       const uint32_t w = a.col[e];
       mesh[(size_t)u * MESH_W + c++] = ((uint32_t)a.stage[w] << STAGE_SHIFT) | w;
     }
-  mcnt[u] = (uint8_t)c;
+  if (mcnt) mcnt[u] = (uint8_t)c;
   for (uint32_t q = c; q < MESH_W; q++) mesh[(size_t)u * MESH_W + q] = EMPTY;
 }
 
 inline unsigned blocks(uint64_t n) { return (unsigned)((n + TB - 1) / TB); }
 
+MeshArgs mesh_args(Ctx& c) {
+  const uint32_t N = c.cfg.peers;
+  c.d_until.alloc(c.nnz ? c.nnz : 1);
+  c.d_prop.alloc(c.nnz ? c.nnz : 1);
+  c.d_lat32.alloc((size_t)c.S * c.S);
+  std::vector<uint32_t> lat32(c.lat_ns.begin(), c.lat_ns.end());
+  GS_HIP(hipMemcpyAsync(c.d_lat32.p, lat32.data(), lat32.size() * 4, hipMemcpyHostToDevice, c.stream));
+  GS_HIP(hipStreamSynchronize(c.stream));  // lat32 dies here
+  MeshArgs a{};
+  a.row = c.d_row.p; a.col = c.d_col.p; a.rev = c.d_rev.p; a.flags = c.d_flags.p;
+  a.prop = c.d_prop.p; a.until = c.d_until.p; a.stage = c.d_stage.p; a.lat = c.d_lat32.p;
+  a.counters = c.d_counters.p; a.seed = c.cfg.seed; a.N = N; a.S = c.S;
+  a.bo = (uint32_t)((c.cfg.backoff_ns + c.cfg.heartbeat_ns - 1) / c.cfg.heartbeat_ns);
+  a.d = c.cfg.d; a.d_lo = c.cfg.d_lo; a.d_hi = c.cfg.d_hi; a.d_out = c.cfg.d_out;
+  return a;
+}
+
+// One heartbeat epoch h >= 1 under churn: the offline set into `off`, the
+// disconnects, then A/B/C as without churn.
+void churn_epoch(Ctx& c, MeshArgs& a, uint64_t h, uint64_t* off) {
+  const uint32_t N = c.cfg.peers;
+  hipStream_t s = c.stream;
+  k_offline<<<blocks(N), TB, 0, s>>>(N, c.cfg.seed, c.cfg.churn_ppm, c.cfg.churn_down, h, off);
+  a.off = off;
+  a.epoch = (uint32_t)h;
+  GS_HIP(hipMemsetAsync(c.d_prop.p, 0, c.nnz ? c.nnz : 1, s));
+  k_disconnect<<<blocks(N), TB, 0, s>>>(a);
+  k_heartbeat<<<blocks(N), TB, 0, s>>>(a);
+  k_handle_graft<<<blocks(N), TB, 0, s>>>(a);
+  k_apply<<<blocks(N), TB, 0, s>>>(a);
+  GS_HIP(hipGetLastError());
+}
+
 }  // namespace
+
+// Make the churn ring hold the snapshots of epochs [h_lo, h_hi] (h_hi - h_lo
+// < ring_R): replay from the empty mesh when h_lo has left the ring, else run
+// the epochs after the current mesh state. Snapshot h = mesh after heartbeat h
+// with the offline bits of epoch h; epoch 0 is the empty mesh, all online.
+void churn_ring(Ctx& c, uint64_t h_lo, uint64_t h_hi) {
+  const uint32_t N = c.cfg.peers, R = c.ring_R;
+  const size_t w64 = ((size_t)N + 63) / 64;
+  hipStream_t s = c.stream;
+  if (h_hi - h_lo >= R) c.fail(GS_EINVAL, "internal: batch spans more epochs than the churn ring");
+  MeshArgs a = mesh_args(c);
+  if (h_lo < c.ring_lo) {  // replay from epoch 0
+    if (c.nnz) k_clear_mesh<<<blocks(c.nnz), TB, 0, s>>>(c.nnz, c.d_flags.p, c.d_until.p);
+    GS_HIP(hipMemsetAsync(c.d_ring_mesh.p, 0xFF, (size_t)N * MESH_W * 4, s));  // slot 0: empty
+    GS_HIP(hipMemsetAsync(c.d_ring_off.p, 0, w64 * 8, s));
+    c.churn_state = 0;
+    c.ring_lo = 0;
+    c.ring_hi = 0;
+  }
+  for (uint64_t h = c.churn_state + 1; h <= h_hi; h++) {
+    const size_t slot = (size_t)(h % R);
+    uint64_t* off = c.d_ring_off.p + slot * w64;
+    churn_epoch(c, a, h, off);
+    k_extract<<<blocks(N), TB, 0, s>>>(a, c.d_ring_mesh.p + slot * N * MESH_W, nullptr);
+  }
+  GS_HIP(hipGetLastError());
+  if (h_hi > c.churn_state) {
+    c.churn_state = h_hi;
+    c.ring_hi = h_hi;
+    c.ring_lo = std::max<uint64_t>(c.ring_lo, h_hi + 1 >= R ? h_hi + 1 - R : 0);
+  }
+  GS_HIP(hipMemcpyAsync(c.h_pinned, c.d_counters.p + C_ERR, 8, hipMemcpyDeviceToHost, s));
+  GS_HIP(hipStreamSynchronize(s));
+  if (c.h_pinned[0] & ERR_MESH) c.fail(GS_ERANGE, "mesh row exceeds GS_MESH_W entries");
+}
 
 uint32_t run_mesh(Ctx& c, uint32_t max_hb) {
   const uint32_t N = c.cfg.peers;
   hipStream_t s = c.stream;
-  c.d_until.alloc(c.nnz ? c.nnz : 1);
-  c.d_prop.alloc(c.nnz ? c.nnz : 1);
-  DevBuf<uint32_t> lat;
-  lat.alloc((size_t)c.S * c.S);
-  std::vector<uint32_t> lat32(c.lat_ns.begin(), c.lat_ns.end());
-  GS_HIP(hipMemcpyAsync(lat.p, lat32.data(), lat32.size() * 4, hipMemcpyHostToDevice, s));
-  MeshArgs a{};
-  a.row = c.d_row.p; a.col = c.d_col.p; a.rev = c.d_rev.p; a.flags = c.d_flags.p;
-  a.prop = c.d_prop.p; a.until = c.d_until.p; a.stage = c.d_stage.p; a.lat = lat.p;
-  a.counters = c.d_counters.p; a.seed = c.cfg.seed; a.N = N; a.S = c.S;
-  a.bo = (uint32_t)((c.cfg.backoff_ns + c.cfg.heartbeat_ns - 1) / c.cfg.heartbeat_ns);
-  a.d = c.cfg.d; a.d_lo = c.cfg.d_lo; a.d_hi = c.cfg.d_hi; a.d_out = c.cfg.d_out;
+  MeshArgs a = mesh_args(c);
   if (c.nnz) k_clear_mesh<<<blocks(c.nnz), TB, 0, s>>>(c.nnz, c.d_flags.p, c.d_until.p);
   GS_HIP(hipMemsetAsync(c.d_counters.p + C_ERR, 0, 8, s));
   uint32_t epoch = 1, last = 0;
   uint64_t* h = c.h_pinned;
+  if (c.cfg.churn_ppm) {  // no fixed point under churn: exactly max_hb epochs
+    c.d_off.alloc(((size_t)N + 63) / 64);
+    for (; epoch <= max_hb; epoch++) churn_epoch(c, a, epoch, c.d_off.p);
+    last = max_hb;
+    c.churn_state = max_hb;  // the ring restarts after this state
+    c.ring_lo = (uint64_t)max_hb + 1;
+    c.ring_hi = max_hb;
+    epoch = max_hb + 1;
+  }
   while (epoch <= max_hb) {
     a.epoch = epoch;
     GS_HIP(hipMemsetAsync(c.d_prop.p, 0, c.nnz ? c.nnz : 1, s));

@@ -224,6 +224,7 @@ uint64_t part_begin(Ctx& c, const gs_publish* sched, uint64_t n_msgs) {
   for (uint64_t i = 1; i < n_msgs; i++)
     if (sched[i].msg_size != sched[0].msg_size) c.fail(GS_EINVAL, "partitioned batch needs equal msg_size");
   if (c.cfg.lazy_gossip) c.fail(GS_EUNSUPPORTED, "lazy gossip is not supported in partitioned mode");
+  if (c.cfg.churn_ppm) c.fail(GS_EUNSUPPORTED, "churn is not supported in partitioned mode");
   const uint32_t F = c.cfg.fragments;
   if (c.cfg.idontwant && sched[0].msg_size / F >= c.cfg.idontwant)
     c.fail(GS_EUNSUPPORTED, "IDONTWANT is not supported in partitioned mode");

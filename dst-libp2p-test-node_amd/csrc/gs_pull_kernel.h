@@ -1,5 +1,5 @@
 // gs_pull_kernel.h — owner-computes Delta-window pass, the default eager
-// forwarding path (DESIGN.md §4.2). Included by gs_relax.hip after
+// forwarding path (DESIGN.md §4.1). Included by gs_relax.hip after
 // gs_relax_kernel.h (inside namespace gs::{anon}).
 //
 // Why: the push path (k_scan + k_frontier) issues one random 64-bit atomicMin

@@ -41,14 +41,25 @@ struct SeedArgs {
   uint64_t tmax;
   uint32_t L, FP, Fe, S, sb, tshift, flood;
   uint32_t u0, un;  // keys held for peers [u0, u0 + un) (the whole graph unless partitioned)
+  // churn: see RelaxArgs
+  const uint32_t* ring_mesh;
+  const uint64_t* ring_off;
+  const uint64_t* q0;
+  const uint64_t* r0;
+  uint64_t hb_ns;
+  uint32_t churn, ring_R, w64, horizon, N;
 };
 
 // publish_new_message (main.rs:101-143): self key at the publisher and the
 // flood (or mesh) sends of every fragment through its uplink FIFO. Only
 // targets inside [u0, u0 + un) are written; the publisher's owner counts R.
 __global__ __launch_bounds__(TB) void k_seed(SeedArgs a) {
+  __shared__ uint32_t live[MAX_DEG];  // churn: the connections online at t_pub, ascending
+  __shared__ uint32_t wcnt[TB / 64];
   const uint32_t m = blockIdx.x, p = a.pub[m], sp = a.stage[p], S = a.S;
   const uint64_t ser = a.tables[S * S + sp];
+  // churn: an offline publisher publishes nothing (the injector's POST finds no node)
+  if (a.churn && ep_off(a, a.q0[m], p)) return;
   const bool own_pub = p - a.u0 < a.un;
   if (own_pub && threadIdx.x < a.Fe) a.keys[(size_t)(p - a.u0) * a.L + (size_t)m * a.FP + threadIdx.x] = (uint64_t)p;
   uint32_t deg;
@@ -56,10 +67,25 @@ __global__ __launch_bounds__(TB) void k_seed(SeedArgs a) {
   bool packed;
   if (a.flood) { deg = (uint32_t)(a.row[p + 1] - a.row[p]); tg = a.col + a.row[p]; packed = false; }
   else {
-    tg = a.mesh + (size_t)p * MESH_W;
+    tg = a.churn ? ep_mesh(a, a.q0[m], p) : a.mesh + (size_t)p * MESH_W;
     deg = 0;
     while (deg < MESH_W && tg[deg] != EMPTY) deg++;
     packed = true;
+  }
+  if (a.churn && a.flood) {  // compact the online connections in id order (deg <= MAX_DEG = TB)
+    const uint32_t j = threadIdx.x;
+    const bool on = j < deg && !ep_off(a, a.q0[m], tg[j]);
+    const uint64_t bm = __ballot(on);
+    if ((threadIdx.x & 63) == 0) wcnt[threadIdx.x >> 6] = (uint32_t)__popcll(bm);
+    __syncthreads();
+    uint32_t base = 0;
+    for (uint32_t q = 0; q < (threadIdx.x >> 6); q++) base += wcnt[q];
+    if (on) live[base + (uint32_t)__popcll(bm & ((1ull << (threadIdx.x & 63)) - 1))] = tg[j];
+    uint32_t tot = 0;
+    for (uint32_t q = 0; q < TB / 64; q++) tot += wcnt[q];
+    __syncthreads();
+    deg = tot;
+    tg = live;
   }
   uint64_t nmin = INF64;
   uint32_t err = 0;
@@ -73,6 +99,7 @@ __global__ __launch_bounds__(TB) void k_seed(SeedArgs a) {
     if (arr > a.tmax) err |= ERR_TIME;
     const uint64_t nk = (arr << a.tshift) | (1ull << a.sb) | p;
     if (w - a.u0 >= a.un) continue;
+    if (a.churn && ev_lost(a, m, arr, w)) continue;
     atomicMin((unsigned long long*)&a.keys[(size_t)(w - a.u0) * a.L + (size_t)m * a.FP + f], (unsigned long long)nk);
     if (a.rowmin) atomicMin((unsigned long long*)&a.rowmin[w - a.u0], (unsigned long long)nk);
     nmin = nk < nmin ? nk : nmin;
@@ -119,7 +146,9 @@ __global__ __launch_bounds__(TB) void k_complete(CompArgs a) {
     uint64_t tc = INF64;
     uint8_t h = 0xFF;
     const uint64_t tp = a.tpub[m];
-    if (u + a.u0 == a.pub[m]) { tc = tp; h = 0; }
+    if (u + a.u0 == a.pub[m]) {  // its own key is set unless it published nothing (churn)
+      if (kp[0] != INF64) { tc = tp; h = 0; }
+    }
     else if (!a.collide && ok) {
       const uint64_t trel = mk >> a.tshift;
       tc = tp + trel;
@@ -232,9 +261,26 @@ static Batch setup_batch(Ctx& c, const gs_publish* sched, uint64_t i0, uint64_t 
   return b;
 }
 
+// churn fields shared by SeedArgs and RelaxArgs (the ring and per-message epochs of gs_run)
+template <class A>
+static void set_churn_args(Ctx& c, A& a) {
+  if (!c.cfg.churn_ppm) return;
+  a.churn = 1;
+  a.ring_mesh = c.d_ring_mesh.p;
+  a.ring_off = c.d_ring_off.p;
+  a.q0 = c.d_q0.p;
+  a.r0 = c.d_r0.p;
+  a.hb_ns = c.cfg.heartbeat_ns;
+  a.ring_R = c.ring_R;
+  a.w64 = (c.cfg.peers + 63) / 64;
+  a.horizon = c.cfg.churn_horizon;
+  a.N = c.cfg.peers;
+}
+
 static void launch_seed(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, uint64_t* seed_min = nullptr,
                         uint64_t* rowmin = nullptr) {
   SeedArgs sa{};
+  set_churn_args(c, sa);
   sa.keys = c.d_keys.p; sa.row = c.d_row.p; sa.col = c.d_col.p; sa.mesh = c.d_mesh.p;
   sa.pub = c.d_pub.p; sa.stage = c.d_stage.p; sa.tables = c.d_tables.p;
   sa.ctrl = seed_min ? seed_min : c.d_ctrl.p; sa.rowmin = rowmin;
@@ -380,11 +426,31 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
   // the pull path needs rows in LDS and no cross-row reads (IDONTWANT reads the
   // target's key, lazy gossip pushes from heartbeats): those stay on the push path
   const bool idw_any = c.cfg.idontwant != 0;
-  const bool pull = (variant & 32) && !gossip && !idw_any;
+  const bool churn = c.cfg.churn_ppm != 0;  // per-epoch mesh lookups live on the push path
+  const bool pull = (variant & 32) && !gossip && !idw_any && !churn;
   // pull rows live in registers: cap the batch at PULL_LMAX / FP messages
   const uint32_t Bcap = pull ? std::max<uint32_t>(1, std::min<uint32_t>(Bmax, PULL_LMAX / FP)) : Bmax;
-  if (gossip) {  // gossip runs on the split path only, without tile skip
+  if (gossip || churn) {  // gossip and churn run on the split path only, without tile skip
     variant = (variant | 8u) & ~2u;
+  }
+  std::vector<uint64_t> q0v(Bmax), r0v(Bmax), ep(churn ? n_msgs : 0);
+  if (churn) {  // epoch of every publish; the snapshot ring
+    const uint64_t hb = c.cfg.heartbeat_ns, ph = c.cfg.hb_phase_ns;
+    for (uint64_t i = 0; i < n_msgs; i++) {
+      if (sched[i].t_pub_ns < ph || (sched[i].t_pub_ns - ph) / hb >= (1ull << 20))
+        c.fail(GS_EINVAL, "churn needs every publish within 2^20 heartbeats after hb_phase_ns");
+      ep[i] = (sched[i].t_pub_ns - ph) / hb;
+    }
+    if (!c.ring_R) {
+      const uint64_t w64 = ((uint64_t)N + 63) / 64, per_slot = (uint64_t)N * MESH_W * 4 + w64 * 8;
+      const uint64_t budget = 8ull << 30;
+      const uint64_t want = (uint64_t)Bmax + c.cfg.churn_horizon + 1;
+      c.ring_R = (uint32_t)std::min<uint64_t>(want, std::max<uint64_t>(c.cfg.churn_horizon + 2, budget / per_slot));
+      c.d_ring_mesh.alloc((size_t)c.ring_R * N * MESH_W);
+      c.d_ring_off.alloc((size_t)c.ring_R * w64);
+    }
+  }
+  if (gossip) {
     const uint64_t rmax = std::max<uint64_t>(c.cfg.d_lazy, (uint64_t)c.max_degree * c.cfg.gossip_factor_milli / 1000);
     if (rmax > GOSSIP_R_MAX) c.fail(GS_EUNSUPPORTED, "gossip fan-out above 32 targets");
   }
@@ -418,8 +484,30 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
   while (i0 < n_msgs) {
     // a batch: up to B messages of equal size (serialisation tables are per batch)
     uint64_t i1 = i0 + 1;
-    while (i1 < n_msgs && i1 - i0 < Bcap && sched[i1].msg_size == sched[i0].msg_size) i1++;
+    uint64_t h_lo = churn ? ep[i0] : 0, h_hi = churn ? ep[i0] : 0;  // churn: publish epochs of the batch
+    while (i1 < n_msgs && i1 - i0 < Bcap && sched[i1].msg_size == sched[i0].msg_size) {
+      if (churn) {  // the batch's epochs (+ lifetime) must fit the ring
+        const uint64_t lo2 = std::min(h_lo, ep[i1]), hi2 = std::max(h_hi, ep[i1]);
+        if (hi2 + c.cfg.churn_horizon - lo2 + 1 > c.ring_R) break;
+        h_lo = lo2;
+        h_hi = hi2;
+      }
+      i1++;
+    }
     const Batch b = setup_batch(c, sched, i0, i1);
+    if (churn) {
+      churn_ring(c, h_lo, h_hi + c.cfg.churn_horizon);
+      const uint64_t hb = c.cfg.heartbeat_ns, ph = c.cfg.hb_phase_ns;
+      for (uint32_t q = 0; q < b.B; q++) {
+        q0v[q] = ep[i0 + q];
+        r0v[q] = b.tpub[q] - ph - q0v[q] * hb;
+      }
+      c.d_q0.alloc(Bmax);
+      c.d_r0.alloc(Bmax);
+      GS_HIP(hipMemcpyAsync(c.d_q0.p, q0v.data(), b.B * 8, hipMemcpyHostToDevice, s));
+      GS_HIP(hipMemcpyAsync(c.d_r0.p, r0v.data(), b.B * 8, hipMemcpyHostToDevice, s));
+      GS_HIP(hipStreamSynchronize(s));
+    }
     const uint32_t B = b.B, L = b.L;
     if (gossip) {  // heartbeats at hb_phase + h*hb: first one at or after each t_pub
       const uint64_t hb = c.cfg.heartbeat_ns, ph = c.cfg.hb_phase_ns;
@@ -459,6 +547,7 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     launch_seed(c, b, 0, N);
 
     RelaxArgs ra{};
+    set_churn_args(c, ra);
     ra.keys = c.d_keys.p; ra.busy = c.d_busy.p; ra.mesh = c.d_mesh.p; ra.pub = c.d_pub.p;
     ra.meta = reinterpret_cast<TileMeta*>(c.d_meta.p);
     ra.fbits = c.d_fbits.p;

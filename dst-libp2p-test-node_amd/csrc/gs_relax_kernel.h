@@ -51,6 +51,12 @@ struct RelaxArgs {
   uint64_t hb_ns, seed;
   uint32_t gl_cap, gossip, hist, d_lazy, gf_milli;
   uint32_t u0;        // global id of the first peer whose keys this context holds
+  // churn: mesh / offline set of the epoch an event falls in
+  const uint32_t* ring_mesh;  // [R][N][MESH_W]
+  const uint64_t* ring_off;   // [R][w64]
+  const uint64_t* q0;         // [B] epoch of t_pub
+  const uint64_t* r0;         // [B] t_pub - start of that epoch
+  uint32_t churn, ring_R, w64, horizon;
   const uint32_t* mesh;
   const uint32_t* pub;
   const uint8_t* stage;
@@ -63,6 +69,26 @@ struct RelaxArgs {
   uint32_t seg_cap;        // frontier groups per wave segment
   uint32_t N, B, F, L, S, sb, tshift, launch, idw;
 };
+
+// ---- churn helpers; m = message index within the batch ----
+template <class A>
+__device__ __forceinline__ uint64_t ev_epoch(const A& a, uint32_t m, uint64_t t) {  // t relative to t_pub
+  return a.q0[m] + (a.r0[m] + t) / a.hb_ns;
+}
+template <class A>
+__device__ __forceinline__ bool ep_off(const A& a, uint64_t h, uint32_t w) {
+  return (a.ring_off[(size_t)(h % a.ring_R) * a.w64 + (w >> 6)] >> (w & 63)) & 1;
+}
+template <class A>
+__device__ __forceinline__ const uint32_t* ep_mesh(const A& a, uint64_t h, uint32_t u) {
+  return a.ring_mesh + ((size_t)(h % a.ring_R) * a.N + u) * MESH_W;
+}
+// a delivery to w at relative time t is lost: past the message's lifetime or w offline
+template <class A>
+__device__ __forceinline__ bool ev_lost(const A& a, uint32_t m, uint64_t t, uint32_t w) {
+  const uint64_t h = ev_epoch(a, m, t);
+  return h > a.q0[m] + a.horizon || ep_off(a, h, w);
+}
 
 __device__ __forceinline__ uint64_t wave_min(uint64_t v) {
   for (int off = 32; off > 0; off >>= 1) {
@@ -191,8 +217,15 @@ __device__ __forceinline__ void relax_lane(const RelaxArgs& a, const BucketLds& 
   const uint32_t ser = L.su[su];
   uint32_t row[MESH_W];
   uint32_t skip = 0, n = 0;
+  const uint32_t* mrp = a.mesh + (size_t)u * MESH_W;
+  bool dead = false;  // churn: received past the message's lifetime -> not forwarded
+  if (active && a.churn) {
+    const uint64_t h = ev_epoch(a, slot / FP, t);
+    dead = h > a.q0[slot / FP] + a.horizon;
+    mrp = ep_mesh(a, dead ? a.q0[slot / FP] : h, u);
+  }
   if (active) {
-    const uint4* rp = reinterpret_cast<const uint4*>(a.mesh + (size_t)u * MESH_W);
+    const uint4* rp = reinterpret_cast<const uint4*>(mrp);
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       const uint4 x = rp[q];
@@ -201,7 +234,7 @@ __device__ __forceinline__ void relax_lane(const RelaxArgs& a, const BucketLds& 
 #pragma unroll
     for (int j = 0; j < (int)MESH_W; j++) {
       const uint32_t e = row[j];
-      if (e == EMPTY) { skip |= 1u << j; continue; }  // rows are EMPTY-padded at the tail
+      if (e == EMPTY || dead) { skip |= 1u << j; continue; }  // rows are EMPTY-padded at the tail
       const uint32_t w = e & 0xFFFFFFu;
       bool sk = (w == src) || (w == pm);
       if (!sk && a.idw) {  // IDONTWANT from w already here
@@ -244,6 +277,7 @@ __device__ __forceinline__ void relax_lane(const RelaxArgs& a, const BucketLds& 
     const uint32_t sd = L.sd[sw];
     const uint64_t arr = start + (uint64_t)pos * ser + L.lat[su * S + sw] + (sd > ser ? sd - ser : 0);
     if (arr > a.tmax) err |= ERR_TIME;
+    if (a.churn && ev_lost(a, slot / FP, arr, w)) continue;  // the send still took its uplink slot
     const uint64_t nk = (arr << a.tshift) | hbits;
     if (FILTER && !(nk < old[j])) continue;
     const size_t dst = (size_t)w * LL + slot;
@@ -488,17 +522,23 @@ __global__ __launch_bounds__(TB) void k_gossip(RelaxArgs a) {
     const uint64_t r0 = a.rel0[m];
     const uint64_t j0 = first_hb(t, r0, a.hb_ns);
     uint32_t mrow[MESH_W];
-    const uint4* rp = reinterpret_cast<const uint4*>(a.mesh + (size_t)u * MESH_W);
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const uint4 x = rp[q];
-      mrow[4 * q] = x.x & 0xFFFFFFu; mrow[4 * q + 1] = x.y & 0xFFFFFFu;
-      mrow[4 * q + 2] = x.z & 0xFFFFFFu; mrow[4 * q + 3] = x.w & 0xFFFFFFu;
-    }
     for (uint32_t k = 0; k < a.hist; k++) {
       const uint64_t T = r0 + (j0 + k) * a.hb_ns;
       if (T + L.lmax[sv] < lo || T + L.lmin[sv] >= hi) continue;
-      const uint32_t h = (uint32_t)(a.habs0[m] + j0 + k);
+      const uint64_t hab = a.habs0[m] + j0 + k;
+      const uint32_t h = (uint32_t)hab;
+      const uint32_t* mrp = a.mesh + (size_t)u * MESH_W;
+      if (a.churn) {  // v gossips only while online, within the message's lifetime, over its epoch's mesh
+        if (hab > a.q0[m] + a.horizon || ep_off(a, hab, u)) continue;
+        mrp = ep_mesh(a, hab, u);
+      }
+      const uint4* rp = reinterpret_cast<const uint4*>(mrp);
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint4 x = rp[q];
+        mrow[4 * q] = x.x & 0xFFFFFFu; mrow[4 * q + 1] = x.y & 0xFFFFFFu;
+        mrow[4 * q + 2] = x.z & 0xFFFFFFu; mrow[4 * q + 3] = x.w & 0xFFFFFFu;
+      }
       uint64_t kk[GOSSIP_R_MAX];
       uint32_t ww[GOSSIP_R_MAX];
       uint32_t nsel = 0, nonmesh = 0;
@@ -509,7 +549,7 @@ __global__ __launch_bounds__(TB) void k_gossip(RelaxArgs a) {
         bool inm = false;
 #pragma unroll
         for (int q = 0; q < (int)MESH_W; q++) inm |= mrow[q] == w;
-        if (inm) continue;
+        if (inm || (a.churn && ep_off(a, hab, w))) continue;
         nonmesh++;
         const uint64_t rk = rng(a.seed, P_GOSSIP, u, h, w);
         if (nsel == GOSSIP_R_MAX && (kk[nsel - 1] < rk || (kk[nsel - 1] == rk && ww[nsel - 1] < w))) continue;
@@ -527,12 +567,13 @@ __global__ __launch_bounds__(TB) void k_gossip(RelaxArgs a) {
         const uint32_t w = ww[q], sw = a.stage[w];
         const uint64_t ti = T + L.lat[sv * S + sw];
         if (ti < lo || ti >= hi) continue;
+        const uint64_t sd = L.sd[sw];
+        const uint64_t A = ti + L.lat[sw * S + sv] + ser + L.lat[sv * S + sw] + (sd > ser ? sd - ser : 0);
+        if (a.churn && (ev_lost(a, m, ti, w) || ev_lost(a, m, A, w))) continue;  // IHAVE or answer lost
         const size_t dst = (size_t)w * LL + slot;
         const uint64_t kw = a.keys[dst];
         if (kw != INF64 && (kw >> a.tshift) <= ti) continue;  // already seen: no IWANT
         iw++;
-        const uint64_t sd = L.sd[sw];
-        const uint64_t A = ti + L.lat[sw * S + sv] + ser + L.lat[sv * S + sw] + (sd > ser ? sd - ser : 0);
         if (A > a.tmax) err |= ERR_TIME;
         if (hp + 1 >= (1u << HOP_BITS)) err |= ERR_HOPS;
         const uint64_t nk = (A << a.tshift) | ((uint64_t)(hp + 1) << a.sb) | u;

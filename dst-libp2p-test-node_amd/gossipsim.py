@@ -26,7 +26,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GOSSIPSIM_LIB", os.path.join(HERE, "libgossipsim.so"))
-ABI_VERSION = 1
+ABI_VERSION = 2
 MESH_W = 16
 UNDELIVERED = np.uint64(0xFFFFFFFFFFFFFFFF)
 MUXERS = {"yamux": 0, "quic": 1, "mplex": 2}
@@ -43,7 +43,8 @@ class GsConfig(ctypes.Structure):
         "muxer", "signed_msgs", "d", "d_lo", "d_hi", "d_lazy", "d_out", "gossip_factor_milli")] + [
         ("heartbeat_ns", u64), ("backoff_ns", u64)] + [
         (n, u32) for n in ("flood_publish", "idontwant", "lazy_gossip", "self_log")] + [
-        ("seed", u64), ("device", i32), ("batch", u32), ("history_gossip", u32), ("hb_phase_ns", u64)]
+        ("seed", u64), ("device", i32), ("batch", u32), ("history_gossip", u32), ("hb_phase_ns", u64)] + [
+        (n, u32) for n in ("churn_ppm", "churn_down", "churn_horizon")]
 
 
 class GsPublish(ctypes.Structure):
@@ -156,6 +157,9 @@ def schedule_runsh(n_msgs, peers, publisher_id, rotation, t0_ns, delay_ns, msg_s
 # injector start (shadow/topogen.py:130), 1000 ms spacing and publisher
 # (6 + i) mod N with rotation (shadow/README.md:57, run.sh:34-36).
 T0_NS = 946684800_000_000_000 + 500_000_000_000
+# Heartbeat 0 when every node starts (Shadow starts processes at 5 s,
+# shadow/topogen.py:106): the phase churn runs need.
+SHADOW_START_NS = 946684800_000_000_000 + 5_000_000_000
 DELAY_NS = 1_000_000_000
 PUBLISHER0 = 6
 

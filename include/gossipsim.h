@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 1u
+#define GS_ABI_VERSION 2u
 
 /* Sentinel for "never delivered" in t_complete_ns. */
 #define GS_UNDELIVERED UINT64_MAX
@@ -85,6 +85,15 @@ typedef struct gs_config {
     uint32_t batch;              /* messages simulated together per device batch    */
     uint32_t history_gossip;     /* mcache windows gossiped (upstream default 3)    */
     uint64_t hb_phase_ns;        /* heartbeats at hb_phase + h*heartbeat (absolute) */
+    /* churn (BASELINE config #3; build-defined): each heartbeat
+     * epoch every peer starts a churn_down-epoch outage with probability
+     * churn_ppm / 1e6; the mesh evolves epoch by epoch and every send uses the
+     * mesh of its epoch. 0 = frozen converged mesh. Needs hb_phase_ns within
+     * 2^20 heartbeats of every publish. */
+    uint32_t churn_ppm;
+    uint32_t churn_down;         /* outage length in heartbeats (default 10)        */
+    uint32_t churn_horizon;      /* message lifetime in heartbeats under churn: no  */
+                                 /* event past epoch(t_pub) + horizon (default 16)  */
 } gs_config;
 
 /* One publish injection (replaces POST /publish, main.rs:50-56,152-168). */
@@ -184,7 +193,9 @@ gs_status gs_graph_info(const struct gs_ctx* ctx, uint32_t* peers, uint64_t* nnz
 gs_status gs_get_csr(struct gs_ctx* ctx, uint64_t* row_ptr, uint32_t* col, uint8_t* flags);
 
 /* Heartbeat GRAFT/PRUNE to a fixed point or max_heartbeats epochs
- * (libp2p-gossipsub heartbeat, configured at main.rs:228-236). */
+ * (libp2p-gossipsub heartbeat, configured at main.rs:228-236). With churn
+ * there is no fixed point: exactly max_heartbeats epochs run, and gs_run then
+ * advances the mesh to the epochs its schedule needs. */
 gs_status gs_mesh_converge(struct gs_ctx* ctx, uint32_t max_heartbeats, uint32_t* out_epochs);
 
 /* Mesh width of gs_get_mesh rows. */

@@ -240,9 +240,7 @@ int or_build_topology(const or_params* p, uint64_t* row_ptr, uint32_t* col, uint
 /* -------------------------------------------------------------- mesh ---- */
 /* Heartbeat GRAFT/PRUNE (libp2p-gossipsub heartbeat/handle_graft/handle_prune,
  * upstream, not vendored; parameters main.rs:228-236), synchronous epochs of
- * A) every peer decides grafts/prunes from the start-of-epoch
- * state; B) every receiver handles incoming GRAFTs in (latency, id) order;
- * C) PRUNEs and rejections are applied, both ends back off. */
+ * DESIGN.md §2.3 (mesh_epoch below). */
 static uint64_t find_entry(const uint64_t* row_ptr, const uint32_t* col, uint32_t u, uint32_t w) {
     uint64_t lo = row_ptr[u], hi = row_ptr[u + 1];
     while (lo < hi) { uint64_t mid = (lo + hi) / 2; if (col[mid] < w) lo = mid + 1; else hi = mid; }
@@ -256,108 +254,180 @@ static int cmp_sel(const void* a, const void* b) {
     return x->e < y->e ? -1 : x->e > y->e;
 }
 
-int or_mesh_converge(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
-                     uint8_t* flags, const uint8_t* stage, uint32_t S, const uint64_t* lat_ns,
-                     uint32_t max_hb, uint32_t* mesh, uint8_t* cnt, uint32_t* epochs_out) {
+/* Churn (config #3 of BASELINE.json, build-defined, parity
+ * unpinned: the reference has no churn). Peer u is offline during heartbeat
+ * epoch h >= 1 iff a departure was drawn at one of the epochs h-down+1..h:
+ * rng(CHURN, u, h') below churn_ppm per million. Epoch 0 (before the first
+ * heartbeat) has everyone online. */
+enum { P_CHURN = 7 };
+int or_offline(const or_params* p, uint32_t u, uint64_t h) {
+    if (!p->churn_ppm || h == 0) return 0;
+    for (uint64_t k = 0; k < p->churn_down && k < h; k++)
+        if (rand_below(or_rng(p->seed, P_CHURN, u, (uint32_t)(h - k), 0), 1000000) < p->churn_ppm) return 1;
+    return 0;
+}
+
+typedef struct {
+    uint32_t* until; uint8_t* prop; uint64_t* rev; sel_t* sel; uint64_t bo;
+} mesh_ws;
+
+static void mesh_ws_free(mesh_ws* w) { free(w->until); free(w->prop); free(w->rev); free(w->sel); }
+
+static int mesh_ws_init(const or_params* p, const uint64_t* row_ptr, const uint32_t* col, uint8_t* flags,
+                        mesh_ws* w) {
     uint32_t N = p->peers;
     uint64_t nnz = row_ptr[N];
-    uint64_t bo = (p->backoff_ns + p->heartbeat_ns - 1) / p->heartbeat_ns;
-    uint32_t* until = (uint32_t*)calloc(nnz ? nnz : 1, sizeof(uint32_t));
-    uint8_t* prop = (uint8_t*)calloc(nnz ? nnz : 1, 1); /* 1 graft, 2 prune, 4 accepted */
-    uint64_t* rev = (uint64_t*)malloc(sizeof(uint64_t) * (nnz ? nnz : 1));
+    w->bo = (p->backoff_ns + p->heartbeat_ns - 1) / p->heartbeat_ns;
+    w->until = (uint32_t*)calloc(nnz ? nnz : 1, sizeof(uint32_t));
+    w->prop = (uint8_t*)calloc(nnz ? nnz : 1, 1); /* 1 graft, 2 prune, 4 accepted */
+    w->rev = (uint64_t*)malloc(sizeof(uint64_t) * (nnz ? nnz : 1));
     uint32_t maxdeg = 0;
     for (uint32_t u = 0; u < N; u++) {
         uint32_t dg = (uint32_t)(row_ptr[u + 1] - row_ptr[u]); if (dg > maxdeg) maxdeg = dg;
     }
-    sel_t* sel = (sel_t*)malloc(sizeof(sel_t) * (maxdeg + 1));
-    if (!until || !prop || !rev || !sel) { free(until); free(prop); free(rev); free(sel); return -2; }
+    w->sel = (sel_t*)malloc(sizeof(sel_t) * (maxdeg + 1));
+    if (!w->until || !w->prop || !w->rev || !w->sel) { mesh_ws_free(w); return -2; }
     for (uint32_t u = 0; u < N; u++)
-        for (uint64_t e = row_ptr[u]; e < row_ptr[u + 1]; e++) rev[e] = find_entry(row_ptr, col, col[e], u);
+        for (uint64_t e = row_ptr[u]; e < row_ptr[u + 1]; e++) w->rev[e] = find_entry(row_ptr, col, col[e], u);
     for (uint64_t e = 0; e < nnz; e++) flags[e] &= (uint8_t)~BIT_MESH;
+    return 0;
+}
 
+/* One synchronous heartbeat epoch: A) every peer decides
+ * grafts/prunes from the start-of-epoch state; B) every receiver handles
+ * incoming GRAFTs in (latency, id) order; C) PRUNEs and rejections are
+ * applied, both ends back off. off = offline flags of the epoch (NULL: no
+ * churn; §2.8). Returns the number of GRAFT/PRUNE changes. */
+static uint64_t mesh_epoch(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
+                           uint8_t* flags, const uint8_t* stage, uint32_t S, const uint64_t* lat_ns,
+                           mesh_ws* ws, uint32_t epoch, const uint8_t* off) {
+    uint32_t N = p->peers;
+    uint64_t nnz = row_ptr[N], changes = 0;
+    uint32_t* until = ws->until; uint8_t* prop = ws->prop; const uint64_t* rev = ws->rev; sel_t* sel = ws->sel;
+    const uint32_t bo = (uint32_t)ws->bo;
+    memset(prop, 0, nnz);
+    /* ---- 0: links to offline peers leave the mesh (disconnect: no back-off) ---- */
+    if (off)
+        for (uint32_t u = 0; u < N; u++)
+            for (uint64_t e = row_ptr[u]; e < row_ptr[u + 1]; e++)
+                if (off[u] || off[col[e]]) flags[e] &= (uint8_t)~BIT_MESH;
+    /* ---- A: heartbeat decisions ---- */
+    for (uint32_t u = 0; u < N; u++) {
+        if (off && off[u]) continue;
+        uint64_t b = row_ptr[u], en = row_ptr[u + 1];
+        uint32_t m = 0, o = 0;
+        for (uint64_t e = b; e < en; e++) if (flags[e] & BIT_MESH) { m++; if (flags[e] & BIT_OUT) o++; }
+        uint32_t mm = m, oo = o;
+        if (m < p->d_lo) { /* graft mesh_n - len random eligible peers */
+            uint32_t nc = 0;
+            for (uint64_t e = b; e < en; e++)
+                if (!(flags[e] & BIT_MESH) && epoch > until[e] && !(off && off[col[e]])) {
+                    sel[nc].key = or_rng(p->seed, P_GRAFT, u, epoch, col[e]); sel[nc].e = e; nc++;
+                }
+            qsort(sel, nc, sizeof(sel_t), cmp_sel);
+            uint32_t want = p->d - m; if (want > nc) want = nc;
+            for (uint32_t q = 0; q < want; q++) {
+                prop[sel[q].e] |= 1; mm++; if (flags[sel[q].e] & BIT_OUT) oo++;
+            }
+        }
+        if (mm > p->d_hi) { /* prune down to mesh_n keeping mesh_outbound_min outbound */
+            uint32_t nc = 0;
+            for (uint64_t e = b; e < en; e++)
+                if (flags[e] & BIT_MESH) { sel[nc].key = or_rng(p->seed, P_PRUNE, u, epoch, col[e]); sel[nc].e = e; nc++; }
+            qsort(sel, nc, sizeof(sel_t), cmp_sel);
+            uint32_t excess = mm - p->d, removed = 0;
+            for (uint32_t q = 0; q < nc && removed < excess; q++) {
+                uint64_t e = sel[q].e;
+                if (flags[e] & BIT_OUT) { if (oo <= p->d_out) continue; oo--; }
+                prop[e] |= 2; removed++; mm--;
+            }
+        }
+        if (mm >= p->d_lo && oo < p->d_out) { /* graft outbound peers */
+            uint32_t nc = 0;
+            for (uint64_t e = b; e < en; e++)
+                if ((flags[e] & BIT_OUT) && !(flags[e] & BIT_MESH) && !(prop[e] & 1) && epoch > until[e] &&
+                    !(off && off[col[e]])) {
+                    sel[nc].key = or_rng(p->seed, P_OUT_GRAFT, u, epoch, col[e]); sel[nc].e = e; nc++;
+                }
+            qsort(sel, nc, sizeof(sel_t), cmp_sel);
+            uint32_t want = p->d_out - oo; if (want > nc) want = nc;
+            for (uint32_t q = 0; q < want; q++) { prop[sel[q].e] |= 1; mm++; }
+        }
+    }
+    /* ---- B: receivers handle GRAFTs ---- */
+    for (uint32_t w = 0; w < N; w++) {
+        uint64_t b = row_ptr[w], en = row_ptr[w + 1];
+        uint32_t c = 0, nin = 0;
+        for (uint64_t e = b; e < en; e++)
+            if (((flags[e] & BIT_MESH) && !(prop[e] & 2)) || (prop[e] & 1)) c++;
+        for (uint64_t e = b; e < en; e++)
+            if (prop[rev[e]] & 1) {
+                sel[nin].key = lat_ns[(uint32_t)stage[col[e]] * S + stage[w]]; sel[nin].e = e; nin++;
+            }
+        /* order by (latency u->w, u): stable wrt ascending ids */
+        for (uint32_t i = 1; i < nin; i++) {
+            sel_t x = sel[i]; int32_t j = (int32_t)i - 1;
+            while (j >= 0 && sel[j].key > x.key) { sel[j + 1] = sel[j]; j--; }
+            sel[j + 1] = x;
+        }
+        for (uint32_t q = 0; q < nin; q++) {
+            uint64_t e = sel[q].e;               /* entry (w -> u) */
+            int in_mesh = ((flags[e] & BIT_MESH) && !(prop[e] & 2)) || (prop[e] & 1);
+            if (in_mesh) { prop[rev[e]] |= 4; continue; }
+            if (epoch < until[e]) { until[e] = epoch + bo; continue; }
+            if (c >= p->d_hi && !(flags[e] & BIT_OUT)) { until[e] = epoch + bo; continue; }
+            prop[rev[e]] |= 4; flags[e] |= BIT_MESH; c++;
+        }
+    }
+    /* ---- C: apply prunes and rejections ---- */
+    for (uint32_t u = 0; u < N; u++) {
+        for (uint64_t e = row_ptr[u]; e < row_ptr[u + 1]; e++) {
+            uint8_t pr = prop[e];
+            if (pr & 1) {
+                changes++;
+                if (pr & 4) flags[e] |= BIT_MESH;
+                else { flags[e] &= (uint8_t)~BIT_MESH; until[e] = epoch + bo; }
+            }
+            if (pr & 2) { changes++; flags[e] &= (uint8_t)~BIT_MESH; until[e] = epoch + bo; }
+            if (prop[rev[e]] & 2) { flags[e] &= (uint8_t)~BIT_MESH; until[e] = epoch + bo; }
+        }
+    }
+    return changes;
+}
+
+/* mesh ELL rows (ascending ids, UINT32_MAX padded) from the CSR flags */
+static int mesh_extract(const or_params* p, const uint64_t* row_ptr, const uint32_t* col, const uint8_t* flags,
+                        uint32_t* mesh, uint8_t* cnt) {
+    for (uint32_t u = 0; u < p->peers; u++) {
+        uint32_t c = 0;
+        for (uint64_t e = row_ptr[u]; e < row_ptr[u + 1]; e++)
+            if (flags[e] & BIT_MESH) {
+                if (c >= MESH_W) return -5;
+                mesh[(size_t)u * MESH_W + c++] = col[e];
+            }
+        cnt[u] = (uint8_t)c;
+        for (uint32_t q = c; q < MESH_W; q++) mesh[(size_t)u * MESH_W + q] = UINT32_MAX;
+    }
+    return 0;
+}
+
+int or_mesh_converge(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
+                     uint8_t* flags, const uint8_t* stage, uint32_t S, const uint64_t* lat_ns,
+                     uint32_t max_hb, uint32_t* mesh, uint8_t* cnt, uint32_t* epochs_out) {
+    uint32_t N = p->peers;
+    mesh_ws ws;
+    if (mesh_ws_init(p, row_ptr, col, flags, &ws)) return -2;
+    uint8_t* off = p->churn_ppm ? (uint8_t*)malloc(N ? N : 1) : NULL;
+    if (p->churn_ppm && !off) { mesh_ws_free(&ws); return -2; }
     uint32_t epoch = 1, last = 0;
     while (epoch <= max_hb) {
-        uint64_t changes = 0;
-        memset(prop, 0, nnz);
-        /* ---- A: heartbeat decisions ---- */
-        for (uint32_t u = 0; u < N; u++) {
-            uint64_t b = row_ptr[u], en = row_ptr[u + 1];
-            uint32_t m = 0, o = 0;
-            for (uint64_t e = b; e < en; e++) if (flags[e] & BIT_MESH) { m++; if (flags[e] & BIT_OUT) o++; }
-            uint32_t mm = m, oo = o;
-            if (m < p->d_lo) { /* graft mesh_n - len random eligible peers */
-                uint32_t nc = 0;
-                for (uint64_t e = b; e < en; e++)
-                    if (!(flags[e] & BIT_MESH) && epoch > until[e]) {
-                        sel[nc].key = or_rng(p->seed, P_GRAFT, u, epoch, col[e]); sel[nc].e = e; nc++;
-                    }
-                qsort(sel, nc, sizeof(sel_t), cmp_sel);
-                uint32_t want = p->d - m; if (want > nc) want = nc;
-                for (uint32_t q = 0; q < want; q++) {
-                    prop[sel[q].e] |= 1; mm++; if (flags[sel[q].e] & BIT_OUT) oo++;
-                }
-            }
-            if (mm > p->d_hi) { /* prune down to mesh_n keeping mesh_outbound_min outbound */
-                uint32_t nc = 0;
-                for (uint64_t e = b; e < en; e++)
-                    if (flags[e] & BIT_MESH) { sel[nc].key = or_rng(p->seed, P_PRUNE, u, epoch, col[e]); sel[nc].e = e; nc++; }
-                qsort(sel, nc, sizeof(sel_t), cmp_sel);
-                uint32_t excess = mm - p->d, removed = 0;
-                for (uint32_t q = 0; q < nc && removed < excess; q++) {
-                    uint64_t e = sel[q].e;
-                    if (flags[e] & BIT_OUT) { if (oo <= p->d_out) continue; oo--; }
-                    prop[e] |= 2; removed++; mm--;
-                }
-            }
-            if (mm >= p->d_lo && oo < p->d_out) { /* graft outbound peers */
-                uint32_t nc = 0;
-                for (uint64_t e = b; e < en; e++)
-                    if ((flags[e] & BIT_OUT) && !(flags[e] & BIT_MESH) && !(prop[e] & 1) && epoch > until[e]) {
-                        sel[nc].key = or_rng(p->seed, P_OUT_GRAFT, u, epoch, col[e]); sel[nc].e = e; nc++;
-                    }
-                qsort(sel, nc, sizeof(sel_t), cmp_sel);
-                uint32_t want = p->d_out - oo; if (want > nc) want = nc;
-                for (uint32_t q = 0; q < want; q++) { prop[sel[q].e] |= 1; mm++; }
-            }
+        if (off) { /* churn: no fixed point, every epoch runs */
+            for (uint32_t u = 0; u < N; u++) off[u] = (uint8_t)or_offline(p, u, epoch);
+            mesh_epoch(p, row_ptr, col, flags, stage, S, lat_ns, &ws, epoch, off);
+            last = epoch++;
+            continue;
         }
-        /* ---- B: receivers handle GRAFTs ---- */
-        for (uint32_t w = 0; w < N; w++) {
-            uint64_t b = row_ptr[w], en = row_ptr[w + 1];
-            uint32_t c = 0, nin = 0;
-            for (uint64_t e = b; e < en; e++)
-                if (((flags[e] & BIT_MESH) && !(prop[e] & 2)) || (prop[e] & 1)) c++;
-            for (uint64_t e = b; e < en; e++)
-                if (prop[rev[e]] & 1) {
-                    sel[nin].key = lat_ns[(uint32_t)stage[col[e]] * S + stage[w]]; sel[nin].e = e; nin++;
-                }
-            /* order by (latency u->w, u): stable wrt ascending ids */
-            for (uint32_t i = 1; i < nin; i++) {
-                sel_t x = sel[i]; int32_t j = (int32_t)i - 1;
-                while (j >= 0 && sel[j].key > x.key) { sel[j + 1] = sel[j]; j--; }
-                sel[j + 1] = x;
-            }
-            for (uint32_t q = 0; q < nin; q++) {
-                uint64_t e = sel[q].e;               /* entry (w -> u) */
-                int in_mesh = ((flags[e] & BIT_MESH) && !(prop[e] & 2)) || (prop[e] & 1);
-                if (in_mesh) { prop[rev[e]] |= 4; continue; }
-                if (epoch < until[e]) { until[e] = epoch + (uint32_t)bo; continue; }
-                if (c >= p->d_hi && !(flags[e] & BIT_OUT)) { until[e] = epoch + (uint32_t)bo; continue; }
-                prop[rev[e]] |= 4; flags[e] |= BIT_MESH; c++;
-            }
-        }
-        /* ---- C: apply prunes and rejections ---- */
-        for (uint32_t u = 0; u < N; u++) {
-            for (uint64_t e = row_ptr[u]; e < row_ptr[u + 1]; e++) {
-                uint8_t pr = prop[e];
-                if (pr & 1) {
-                    changes++;
-                    if (pr & 4) flags[e] |= BIT_MESH;
-                    else { flags[e] &= (uint8_t)~BIT_MESH; until[e] = epoch + (uint32_t)bo; }
-                }
-                if (pr & 2) { changes++; flags[e] &= (uint8_t)~BIT_MESH; until[e] = epoch + (uint32_t)bo; }
-                if (prop[rev[e]] & 2) { flags[e] &= (uint8_t)~BIT_MESH; until[e] = epoch + (uint32_t)bo; }
-            }
-        }
+        uint64_t changes = mesh_epoch(p, row_ptr, col, flags, stage, S, lat_ns, &ws, epoch, NULL);
         last = epoch;
         if (changes) { epoch++; continue; }
         /* quiescent: next epoch at which a back-off expiry can wake a peer */
@@ -372,25 +442,49 @@ int or_mesh_converge(const or_params* p, const uint64_t* row_ptr, const uint32_t
             for (uint64_t e = b; e < en; e++) {
                 if (flags[e] & BIT_MESH) continue;
                 if (need_out && !(flags[e] & BIT_OUT)) continue;
-                if (until[e] >= epoch + 1 && (uint64_t)until[e] + 1 < wake) wake = (uint64_t)until[e] + 1;
+                if (ws.until[e] >= epoch + 1 && (uint64_t)ws.until[e] + 1 < wake) wake = (uint64_t)ws.until[e] + 1;
             }
         }
         if (wake == UINT64_MAX || wake > max_hb) break;
         epoch = (uint32_t)wake;
     }
-    for (uint32_t u = 0; u < N; u++) {
-        uint32_t c = 0;
-        for (uint64_t e = row_ptr[u]; e < row_ptr[u + 1]; e++)
-            if (flags[e] & BIT_MESH) {
-                if (c >= MESH_W) { free(until); free(prop); free(rev); free(sel); return -5; }
-                mesh[(size_t)u * MESH_W + c++] = col[e];
-            }
-        cnt[u] = (uint8_t)c;
-        for (uint32_t q = c; q < MESH_W; q++) mesh[(size_t)u * MESH_W + q] = UINT32_MAX;
-    }
+    int rc = mesh_extract(p, row_ptr, col, flags, mesh, cnt);
     *epochs_out = last;
-    free(until); free(prop); free(rev); free(sel);
-    return 0;
+    free(off);
+    mesh_ws_free(&ws);
+    return rc;
+}
+
+/* Mesh snapshots under churn: heartbeats 1..h_hi from the empty mesh; slot
+ * h - h_lo holds the mesh after heartbeat h (h = 0: the empty initial mesh)
+ * and the offline flags of epoch h, for h in [h_lo, h_hi]. */
+int or_mesh_churn(const or_params* p, const uint64_t* row_ptr, const uint32_t* col, const uint8_t* flags_in,
+                  const uint8_t* stage, uint32_t S, const uint64_t* lat_ns, uint32_t h_lo, uint32_t h_hi,
+                  uint32_t* snap_mesh, uint8_t* snap_cnt, uint8_t* snap_off) {
+    uint32_t N = p->peers;
+    uint64_t nnz = row_ptr[N];
+    if (h_hi < h_lo) return -1;
+    uint8_t* flags = (uint8_t*)malloc(nnz ? nnz : 1);
+    uint8_t* off = (uint8_t*)calloc(N ? N : 1, 1);
+    if (!flags || !off) { free(flags); free(off); return -2; }
+    memcpy(flags, flags_in, nnz);
+    mesh_ws ws;
+    if (mesh_ws_init(p, row_ptr, col, flags, &ws)) { free(flags); free(off); return -2; }
+    int rc = 0;
+    for (uint32_t h = 0; h <= h_hi && !rc; h++) {
+        if (h > 0) {
+            for (uint32_t u = 0; u < N; u++) off[u] = (uint8_t)or_offline(p, u, h);
+            mesh_epoch(p, row_ptr, col, flags, stage, S, lat_ns, &ws, h, off);
+        }
+        if (h >= h_lo) {
+            size_t o = (size_t)(h - h_lo);
+            rc = mesh_extract(p, row_ptr, col, flags, snap_mesh + o * N * MESH_W, snap_cnt + o * N);
+            memcpy(snap_off + o * N, off, N);
+        }
+    }
+    mesh_ws_free(&ws);
+    free(flags); free(off);
+    return rc;
 }
 
 /* ------------------------------------------------------ dissemination ---- */
@@ -441,18 +535,49 @@ static uint32_t bits_for(uint32_t n) { uint32_t b = 1; while ((1ull << b) < n) b
 
 enum { P_GOSSIP = 6 };
 
+/* Where a send reads the mesh: the frozen converged mesh, or under churn the
+ * snapshot of the heartbeat epoch the send falls in. */
+typedef struct {
+    const uint32_t* mesh; const uint8_t* cnt;                               /* frozen */
+    const uint32_t* snap_mesh; const uint8_t* snap_cnt; const uint8_t* snap_off; /* churn */
+    uint64_t h_lo, n_snap;
+    uint64_t h_cap;  /* last epoch the current message may use: epoch(t_pub) + churn_horizon */
+} mesh_src;
+
+/* heartbeat epoch containing absolute time tabs: heartbeats at hb_phase + h*hb */
+static uint64_t epoch_at(const or_params* p, uint64_t tabs) {
+    return tabs < p->hb_phase_ns ? 0 : (tabs - p->hb_phase_ns) / p->heartbeat_ns;
+}
+/* snapshot slot of epoch h; -1 past the message's lifetime h_cap (its event is
+ * not made / not delivered) or outside the snapshots */
+static int64_t slot_of(const mesh_src* ms, uint64_t h) {
+    if (!ms->snap_mesh) return 0;
+    return (h < ms->h_lo || h - ms->h_lo >= ms->n_snap || h > ms->h_cap) ? -1 : (int64_t)(h - ms->h_lo);
+}
+static const uint32_t* mesh_row(const mesh_src* ms, uint32_t N, int64_t slot, uint32_t u, uint32_t* cnt) {
+    if (!ms->snap_mesh) { *cnt = ms->cnt[u]; return ms->mesh + (size_t)u * MESH_W; }
+    *cnt = ms->snap_cnt[(size_t)slot * N + u];
+    return ms->snap_mesh + ((size_t)slot * N + u) * MESH_W;
+}
+static int offline_at(const mesh_src* ms, uint32_t N, int64_t slot, uint32_t u) {
+    return ms->snap_off ? ms->snap_off[(size_t)slot * N + u] : 0;
+}
+
 /* Lazy-gossip targets of peer v at heartbeat h (libp2p-gossipsub emit_gossip,
  * upstream, not vendored; gossip_lazy/gossip_factor at main.rs:230,235):
  * r = max(D_lazy, floor(factor*|non-mesh|)) non-mesh peers, capped at
- * |non-mesh|, the r smallest rng(GOSSIP, v, h, w) (ties by id). */
+ * |non-mesh|, the r smallest rng(GOSSIP, v, h, w) (ties by id). Under churn
+ * the mesh is the epoch-h snapshot and offline peers are not candidates. */
 static uint32_t gossip_targets(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
-                               const uint32_t* mesh, const uint8_t* cnt, uint32_t v, uint64_t h,
+                               const mesh_src* ms, int64_t slot, uint32_t v, uint64_t h,
                                sel_t* sel, uint32_t* out) {
+    uint32_t N = p->peers, mc;
+    const uint32_t* mr = mesh_row(ms, N, slot, v, &mc);
     uint32_t nc = 0;
     for (uint64_t e = row_ptr[v]; e < row_ptr[v + 1]; e++) {
         uint32_t w = col[e], in = 0;
-        for (uint32_t q = 0; q < cnt[v]; q++) in |= mesh[(size_t)v * MESH_W + q] == w;
-        if (in) continue;
+        for (uint32_t q = 0; q < mc; q++) in |= mr[q] == w;
+        if (in || offline_at(ms, N, slot, w)) continue;
         sel[nc].key = or_rng(p->seed, P_GOSSIP, v, (uint32_t)h, w);
         sel[nc].e = w;
         nc++;
@@ -465,6 +590,48 @@ static uint32_t gossip_targets(const or_params* p, const uint64_t* row_ptr, cons
     return r;
 }
 
+/* Events in time order; at equal time arrivals (type 0) precede IHAVE
+ * arrivals (type 1), so "w has seen m by t" reads w's finality at the IHAVE. */
+
+/* Lazy gossip of (v, f) first received at t_v (relative to t_pub): IHAVE at
+ * the history_gossip heartbeats T >= t_v to gossip_targets(v, h); the IHAVE
+ * reaches w at T + lat(v,w); an IWANT comes back and v's answer lands at
+ * T + 2 lat(v,w) + lat(w,v) + ser_up(v) + dn. Under churn v
+ * gossips only while online, and an IHAVE or answer reaching an offline w is
+ * lost (§2.8). */
+static int sched_gossip(const or_params* p, const uint64_t* row_ptr, const uint32_t* col, const mesh_src* ms,
+                        const uint8_t* stage, uint32_t S, const uint64_t* lat_ns, const uint64_t* su,
+                        const uint64_t* sd, uint64_t t_pub, uint32_t v, uint32_t f, uint64_t tv, uint64_t hp,
+                        uint32_t tshift, uint32_t sb, uint64_t tmax, sel_t* gsel, uint32_t* gtg, heap_t* h) {
+    const uint32_t N = p->peers;
+    const uint64_t hmask = (1ull << HOP_BITS) - 1;
+    const uint64_t tabs = t_pub + tv;
+    uint64_t h0 = tabs <= p->hb_phase_ns ? 0 : (tabs - p->hb_phase_ns + p->heartbeat_ns - 1) / p->heartbeat_ns;
+    const uint32_t sv = stage[v];
+    for (uint32_t k = 0; k < p->history_gossip; k++) {
+        const uint64_t hh = h0 + k;
+        const uint64_t T = p->hb_phase_ns + hh * p->heartbeat_ns - t_pub;
+        const int64_t sl = slot_of(ms, hh);
+        if (sl < 0 || offline_at(ms, N, sl, v)) continue;  /* expired, or v is offline */
+        const uint32_t r = gossip_targets(p, row_ptr, col, ms, sl, v, hh, gsel, gtg);
+        if (r && hp + 1 > hmask) return -5;
+        for (uint32_t q = 0; q < r; q++) {
+            const uint32_t w = gtg[q], sw = stage[w];
+            const uint64_t ti = T + lat_ns[sv * S + sw];
+            const uint64_t dn = sd[sw] > su[sv] ? sd[sw] - su[sv] : 0;
+            const uint64_t A = ti + lat_ns[sw * S + sv] + su[sv] + lat_ns[sv * S + sw] + dn;
+            if (A > tmax) return -5;
+            if (ms->snap_off) {
+                const int64_t si = slot_of(ms, epoch_at(p, t_pub + ti)), sa = slot_of(ms, epoch_at(p, t_pub + A));
+                if (si < 0 || sa < 0 || offline_at(ms, N, si, w) || offline_at(ms, N, sa, w)) continue;
+            }
+            ev_t ge = {ti, (A << tshift) | ((hp + 1) << sb) | v, w, f, 1};
+            if (heap_push(h, ge)) return -2;
+        }
+    }
+    return 0;
+}
+
 /* One publish -> receive -> forward -> reassemble pass per message:
  *  publish_new_message (main.rs:101-143): F fragments of msg_size/F bytes,
  *    byte 10 = chunk (fragments distinct only if payload > 10: defect D8),
@@ -474,12 +641,17 @@ static uint32_t gossip_targets(const or_params* p, const uint64_t* row_ptr, cons
  *    forwarded to mesh \ {src, publisher} in ascending id through the peer's
  *    uplink FIFO (busy carried across that message's fragments).
  *  create_message_handler (main.rs:79-99): completion = arrival of the F-th
- *    distinct fragment; latency ms = (t_complete - tx_time)/1e6 truncated. */
-int or_run(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
-           const uint32_t* mesh, const uint8_t* cnt, const uint8_t* stage, uint32_t S,
-           const uint64_t* lat_ns, const uint64_t* bw_up, const uint64_t* bw_dn,
-           const uint64_t* sched_t, const uint32_t* sched_pub, const uint32_t* sched_size,
-           uint64_t n_msgs, uint64_t* t_complete, uint8_t* hops, or_stats* st) {
+ *    distinct fragment; latency ms = (t_complete - tx_time)/1e6 truncated.
+ *  churn: a publisher offline at t_pub publishes nothing;
+ *    the flood goes to the connections online at t_pub; a forward uses the
+ *    mesh snapshot of the epoch it is sent in; a delivery to a peer offline
+ *    at its arrival is lost (the send still occupies the uplink); nothing
+ *    happens past epoch(t_pub) + churn_horizon (the message's lifetime). */
+static int run_impl(const or_params* p, const uint64_t* row_ptr, const uint32_t* col, const mesh_src* ms0,
+                    const uint8_t* stage, uint32_t S, const uint64_t* lat_ns, const uint64_t* bw_up,
+                    const uint64_t* bw_dn, const uint64_t* sched_t, const uint32_t* sched_pub,
+                    const uint32_t* sched_size, uint64_t n_msgs, uint64_t* t_complete, uint8_t* hops,
+                    or_stats* st) {
     uint32_t N = p->peers, F = p->fragments;
     if (F == 0 || F > 16) return -6;
     uint32_t sb = bits_for(N), tshift = sb + HOP_BITS;
@@ -495,9 +667,10 @@ int or_run(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
     uint64_t *su = (uint64_t*)malloc(8 * S), *sd = (uint64_t*)malloc(8 * S);
     sel_t* gsel = (sel_t*)malloc(sizeof(sel_t) * (maxdeg + 1));
     uint32_t* gtg = (uint32_t*)malloc(sizeof(uint32_t) * (maxdeg + 1));
+    uint32_t* ftg = (uint32_t*)malloc(sizeof(uint32_t) * (maxdeg + 1));
     heap_t h = {0, 0, 0};
     int rc = 0;
-    if (!best || !fin || !busy || !su || !sd || !gsel || !gtg) { rc = -2; goto out; }
+    if (!best || !fin || !busy || !su || !sd || !gsel || !gtg || !ftg) { rc = -2; goto out; }
     for (uint64_t mi = 0; mi < n_msgs; mi++) {
         uint32_t pub = sched_pub[mi];
         uint64_t payload = sched_size[mi] / F;
@@ -505,6 +678,10 @@ int or_run(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
         int collide = (F > 1 && payload <= 10);             /* defect D8 */
         uint32_t Fe = collide ? 1 : F;
         uint64_t wire = or_wire_bytes(payload, p->muxer, p->signed_msgs);
+        const uint64_t tp = sched_t[mi];
+        mesh_src msg_ms = *ms0;
+        msg_ms.h_cap = epoch_at(p, tp) + p->churn_horizon;
+        const mesh_src* ms = &msg_ms;
         for (uint32_t s = 0; s < S; s++) {
             su[s] = (wire * 8000000000ULL + bw_up[s] - 1) / bw_up[s];
             sd[s] = (wire * 8000000000ULL + bw_dn[s] - 1) / bw_dn[s];
@@ -512,49 +689,42 @@ int or_run(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
         for (size_t i = 0; i < NF; i++) { best[i] = INF64; fin[i] = 0; }
         for (uint32_t u = 0; u < N; u++) busy[u] = 0;
         h.n = 0;
-        /* Lazy gossip of (v, f) first received at t_v (relative): IHAVE at the
-         * history_gossip heartbeats T >= t_v to gossip_targets(v, h); the
-         * IHAVE reaches w at T + lat(v,w); an IWANT comes back and v's answer
-         * lands at T + 2 lat(v,w) + lat(w,v) + ser_up(v) + dn. */
-#define SCHED_GOSSIP(v_, f_, tv_, hp_)                                                          \
-        do {                                                                                    \
-            const uint64_t tabs_ = sched_t[mi] + (tv_);                                        \
-            uint64_t h0_ = tabs_ <= p->hb_phase_ns ? 0                                          \
-                         : (tabs_ - p->hb_phase_ns + p->heartbeat_ns - 1) / p->heartbeat_ns;    \
-            const uint32_t sv_ = stage[v_];                                                     \
-            for (uint32_t k_ = 0; k_ < p->history_gossip; k_++) {                              \
-                const uint64_t hh_ = h0_ + k_;                                                  \
-                const uint64_t T_ = p->hb_phase_ns + hh_ * p->heartbeat_ns - sched_t[mi];       \
-                const uint32_t r_ = gossip_targets(p, row_ptr, col, mesh, cnt, v_, hh_, gsel, gtg); \
-                if (r_ && (hp_) + 1 > hmask) { rc = -5; goto out; }                            \
-                for (uint32_t q_ = 0; q_ < r_; q_++) {                                          \
-                    const uint32_t w_ = gtg[q_], sw_ = stage[w_];                               \
-                    const uint64_t ti_ = T_ + lat_ns[sv_ * S + sw_];                            \
-                    const uint64_t dn_ = sd[sw_] > su[sv_] ? sd[sw_] - su[sv_] : 0;             \
-                    const uint64_t A_ = ti_ + lat_ns[sw_ * S + sv_] + su[sv_] + lat_ns[sv_ * S + sw_] + dn_; \
-                    if (A_ > tmax) { rc = -5; goto out; }                                       \
-                    ev_t ge_ = {ti_, (A_ << tshift) | (((uint64_t)(hp_) + 1) << sb) | (v_), w_, (f_), 1}; \
-                    if (heap_push(&h, ge_)) { rc = -2; goto out; }                             \
-                }                                                                               \
-            }                                                                                   \
-        } while (0)
+        st->messages++;
+        const int64_t sp0 = slot_of(ms, epoch_at(p, tp));
+        if (sp0 < 0) { rc = -7; goto out; }
+        if (offline_at(ms, N, sp0, pub)) { /* the injector's POST finds no node: nothing is published */
+            for (uint32_t u = 0; u < N; u++) { t_complete[(size_t)mi * N + u] = INF64; hops[(size_t)mi * N + u] = 0xFF; }
+            continue;
+        }
         /* publisher: self key, flood through the uplink FIFO */
         uint32_t sp = stage[pub];
         for (uint32_t f = 0; f < Fe; f++) { best[(size_t)pub * F + f] = (uint64_t)pub; fin[(size_t)pub * F + f] = 1; }
         if (p->lazy_gossip)
-            for (uint32_t f = 0; f < Fe; f++) SCHED_GOSSIP(pub, f, 0, 0);
-        const uint32_t* tgt; uint32_t deg;
-        uint32_t meshrow[MESH_W];
-        if (p->flood_publish) { tgt = col + row_ptr[pub]; deg = (uint32_t)(row_ptr[pub + 1] - row_ptr[pub]); }
-        else { deg = cnt[pub]; for (uint32_t q = 0; q < deg; q++) meshrow[q] = mesh[(size_t)pub * MESH_W + q]; tgt = meshrow; }
+            for (uint32_t f = 0; f < Fe; f++)
+                if ((rc = sched_gossip(p, row_ptr, col, ms, stage, S, lat_ns, su, sd, tp, pub, f, 0, 0, tshift, sb,
+                                       tmax, gsel, gtg, &h)))
+                    goto out;
+        uint32_t deg = 0;
+        if (p->flood_publish) {
+            for (uint64_t e = row_ptr[pub]; e < row_ptr[pub + 1]; e++)
+                if (!offline_at(ms, N, sp0, col[e])) ftg[deg++] = col[e];
+        } else {
+            uint32_t mc;
+            const uint32_t* mr = mesh_row(ms, N, sp0, pub, &mc);
+            for (uint32_t q = 0; q < mc; q++) ftg[deg++] = mr[q];
+        }
         for (uint32_t f = 0; f < Fe; f++)
             for (uint32_t j = 0; j < deg; j++) {
-                uint32_t w = tgt[j], sw = stage[w];
+                uint32_t w = ftg[j], sw = stage[w];
                 uint64_t dn = sd[sw] > su[sp] ? sd[sw] - su[sp] : 0;
                 uint64_t arr = ((uint64_t)f * deg + j + 1) * su[sp] + lat_ns[sp * S + sw] + dn;
                 if (arr > tmax) { rc = -5; goto out; }
                 uint64_t key = (arr << tshift) | (1ull << sb) | pub;
                 st->relaxations++;
+                if (ms->snap_off) {  /* lost: past the lifetime, or w offline at the arrival */
+                    const int64_t sl = slot_of(ms, epoch_at(p, tp + arr));
+                    if (sl < 0 || offline_at(ms, N, sl, w)) continue;
+                }
                 if (key < best[(size_t)w * F + f]) best[(size_t)w * F + f] = key;
                 ev_t ev = {arr, key, w, f, 0};
                 if (heap_push(&h, ev)) { rc = -2; goto out; }
@@ -580,9 +750,13 @@ int or_run(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
             uint64_t hp = (ev.key >> sb) & hmask;
             uint32_t src = (uint32_t)(ev.key & smask);
             st->frag_deliveries++;
+            const int64_t sl = slot_of(ms, epoch_at(p, tp + t));
+            if (sl < 0) continue;  /* received past the message's lifetime: delivered, not forwarded */
+            uint32_t mc;
+            const uint32_t* mr = mesh_row(ms, N, sl, u, &mc);
             uint32_t tg[MESH_W], n = 0;
-            for (uint32_t q = 0; q < cnt[u]; q++) {
-                uint32_t w = mesh[(size_t)u * MESH_W + q];
+            for (uint32_t q = 0; q < mc; q++) {
+                uint32_t w = mr[q];
                 if (w == src || w == pub) continue;
                 if (p->idontwant && payload >= p->idontwant) {
                     uint64_t bw_ = best[(size_t)w * F + ev.frag];
@@ -590,7 +764,10 @@ int or_run(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
                 }
                 tg[n++] = w;
             }
-            if (p->lazy_gossip) SCHED_GOSSIP(u, ev.frag, t, hp);
+            if (p->lazy_gossip &&
+                (rc = sched_gossip(p, row_ptr, col, ms, stage, S, lat_ns, su, sd, tp, u, ev.frag, t, hp, tshift, sb,
+                                   tmax, gsel, gtg, &h)))
+                goto out;
             uint64_t start = (Fe > 1 && busy[u] > t) ? busy[u] : t;
             busy[u] = start + (uint64_t)n * su[su_];
             if (n && hp + 1 > hmask) { rc = -5; goto out; }
@@ -601,6 +778,10 @@ int or_run(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
                 if (arr > tmax) { rc = -5; goto out; }
                 uint64_t key = (arr << tshift) | ((hp + 1) << sb) | u;
                 st->relaxations++;
+                if (ms->snap_off) {
+                    const int64_t sa = slot_of(ms, epoch_at(p, tp + arr));
+                    if (sa < 0 || offline_at(ms, N, sa, w)) continue;
+                }
                 size_t wi = (size_t)w * F + ev.frag;
                 if (key < best[wi]) {
                     best[wi] = key;
@@ -612,7 +793,7 @@ int or_run(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
         /* reassembly: F-th distinct fragment completes the message */
         for (uint32_t u = 0; u < N; u++) {
             size_t o = (size_t)mi * N + u;
-            if (u == pub) { t_complete[o] = sched_t[mi]; hops[o] = 0; continue; }
+            if (u == pub) { t_complete[o] = tp; hops[o] = 0; continue; }
             uint64_t mk = 0; int ok = !collide;
             for (uint32_t f = 0; f < F && ok; f++) {
                 uint64_t k = best[(size_t)u * F + f];
@@ -620,18 +801,37 @@ int or_run(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
             }
             if (!ok) { t_complete[o] = INF64; hops[o] = 0xFF; continue; }
             uint64_t trel = mk >> tshift;
-            t_complete[o] = sched_t[mi] + trel;
+            t_complete[o] = tp + trel;
             hops[o] = (uint8_t)((mk >> sb) & hmask);
-            uint64_t ms = trel / 1000000ULL;
+            uint64_t ms_ = trel / 1000000ULL;
             st->deliveries++;
-            st->latency_sum_ms += ms;
-            if (ms > st->latency_max_ms) st->latency_max_ms = ms;
+            st->latency_sum_ms += ms_;
+            if (ms_ > st->latency_max_ms) st->latency_max_ms = ms_;
         }
-        st->messages++;
     }
 out:
     st->bytes_alg = 16 * st->frag_deliveries + 12 * st->relaxations + 8 * st->deliveries;
-#undef SCHED_GOSSIP
-    free(best); free(fin); free(busy); free(su); free(sd); free(gsel); free(gtg); free(h.a);
+    free(best); free(fin); free(busy); free(su); free(sd); free(gsel); free(gtg); free(ftg); free(h.a);
     return rc;
+}
+
+int or_run(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
+           const uint32_t* mesh, const uint8_t* cnt, const uint8_t* stage, uint32_t S,
+           const uint64_t* lat_ns, const uint64_t* bw_up, const uint64_t* bw_dn,
+           const uint64_t* sched_t, const uint32_t* sched_pub, const uint32_t* sched_size,
+           uint64_t n_msgs, uint64_t* t_complete, uint8_t* hops, or_stats* st) {
+    mesh_src ms = {mesh, cnt, NULL, NULL, NULL, 0, 0, 0};
+    return run_impl(p, row_ptr, col, &ms, stage, S, lat_ns, bw_up, bw_dn, sched_t, sched_pub, sched_size,
+                    n_msgs, t_complete, hops, st);
+}
+
+int or_run_churn(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
+                 const uint32_t* snap_mesh, const uint8_t* snap_cnt, const uint8_t* snap_off,
+                 uint32_t h_lo, uint32_t n_snap, const uint8_t* stage, uint32_t S,
+                 const uint64_t* lat_ns, const uint64_t* bw_up, const uint64_t* bw_dn,
+                 const uint64_t* sched_t, const uint32_t* sched_pub, const uint32_t* sched_size,
+                 uint64_t n_msgs, uint64_t* t_complete, uint8_t* hops, or_stats* st) {
+    mesh_src ms = {NULL, NULL, snap_mesh, snap_cnt, snap_off, h_lo, n_snap, 0};
+    return run_impl(p, row_ptr, col, &ms, stage, S, lat_ns, bw_up, bw_dn, sched_t, sched_pub, sched_size,
+                    n_msgs, t_complete, hops, st);
 }

@@ -29,6 +29,7 @@ typedef struct or_params {
     uint64_t seed;
     uint32_t history_gossip;
     uint64_t hb_phase_ns;
+    uint32_t churn_ppm, churn_down, churn_horizon; /* DESIGN.md §2.8; 0 ppm = no churn */
 } or_params;
 
 typedef struct or_stats {
@@ -49,6 +50,21 @@ int or_build_topology(const or_params* p, uint64_t* row_ptr, uint32_t* col, uint
 int or_mesh_converge(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
                      uint8_t* flags, const uint8_t* stage, uint32_t S, const uint64_t* lat_ns,
                      uint32_t max_hb, uint32_t* mesh, uint8_t* cnt, uint32_t* epochs_out);
+/* 1 if peer u is offline during heartbeat epoch h (churn). */
+int or_offline(const or_params* p, uint32_t u, uint64_t h);
+/* Mesh snapshots for heartbeat epochs [h_lo, h_hi] under churn: snap_mesh
+ * [(h_hi-h_lo+1)][N*16], snap_cnt / snap_off [(h_hi-h_lo+1)][N]. */
+int or_mesh_churn(const or_params* p, const uint64_t* row_ptr, const uint32_t* col, const uint8_t* flags,
+                  const uint8_t* stage, uint32_t S, const uint64_t* lat_ns, uint32_t h_lo, uint32_t h_hi,
+                  uint32_t* snap_mesh, uint8_t* snap_cnt, uint8_t* snap_off);
+/* or_run over a time-varying mesh: the snapshot of the epoch each send falls
+ * in; events past epoch(t_pub) + churn_horizon are dropped. */
+int or_run_churn(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
+                 const uint32_t* snap_mesh, const uint8_t* snap_cnt, const uint8_t* snap_off,
+                 uint32_t h_lo, uint32_t n_snap, const uint8_t* stage, uint32_t S,
+                 const uint64_t* lat_ns, const uint64_t* bw_up, const uint64_t* bw_dn,
+                 const uint64_t* sched_t, const uint32_t* sched_pub, const uint32_t* sched_size,
+                 uint64_t n_msgs, uint64_t* t_complete, uint8_t* hops, or_stats* st);
 int or_run(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
            const uint32_t* mesh, const uint8_t* cnt, const uint8_t* stage, uint32_t S,
            const uint64_t* lat_ns, const uint64_t* bw_up, const uint64_t* bw_dn,

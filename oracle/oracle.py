@@ -29,7 +29,8 @@ class OrParams(ctypes.Structure):
         "gossip_factor_milli")] + [
         ("heartbeat_ns", ctypes.c_uint64), ("backoff_ns", ctypes.c_uint64)] + [
         (n, ctypes.c_uint32) for n in ("flood_publish", "idontwant", "lazy_gossip", "self_log")] + [
-        ("seed", ctypes.c_uint64), ("history_gossip", ctypes.c_uint32), ("hb_phase_ns", ctypes.c_uint64)]
+        ("seed", ctypes.c_uint64), ("history_gossip", ctypes.c_uint32), ("hb_phase_ns", ctypes.c_uint64)] + [
+        (n, ctypes.c_uint32) for n in ("churn_ppm", "churn_down", "churn_horizon")]
 
 
 class OrStats(ctypes.Structure):
@@ -69,6 +70,12 @@ def lib():
         L.or_run.argtypes = [P(OrParams), P(u64), P(u32), P(u32), P(u8), P(u8), u32, P(u64),
                              P(u64), P(u64), P(u64), P(u32), P(u32), u64, P(u64), P(u8),
                              P(OrStats)]
+        L.or_offline.argtypes = [P(OrParams), u32, u64]
+        L.or_mesh_churn.argtypes = [P(OrParams), P(u64), P(u32), P(u8), P(u8), u32, P(u64), u32, u32,
+                                    P(u32), P(u8), P(u8)]
+        L.or_run_churn.argtypes = [P(OrParams), P(u64), P(u32), P(u32), P(u8), P(u8), u32, u32, P(u8), u32,
+                                   P(u64), P(u64), P(u64), P(u64), P(u32), P(u32), u64, P(u64), P(u8),
+                                   P(OrStats)]
         _lib = L
     return _lib
 
@@ -83,7 +90,7 @@ def params(**kw):
              muxer=0, signed_msgs=1, d=6, d_lo=4, d_hi=8, d_lazy=6, d_out=3,
              gossip_factor_milli=250, heartbeat_ns=1_000_000_000, backoff_ns=60_000_000_000,
              flood_publish=1, idontwant=0, lazy_gossip=0, self_log=0, seed=1, history_gossip=3,
-             hb_phase_ns=0)
+             hb_phase_ns=0, churn_ppm=0, churn_down=10, churn_horizon=16)
     d.update(kw)
     return OrParams(**d)
 
@@ -141,6 +148,62 @@ def mesh_converge(p, row_ptr, col, flags, stage, lat, max_hb=400):
     return flags, mesh.reshape(N, MESH_W), cnt, ep.value
 
 
+def offline(p, u, h):
+    return bool(lib().or_offline(ctypes.byref(p), u, h))
+
+
+def epoch_at(p, t_abs):
+    """Heartbeat epoch containing absolute time t (heartbeats at hb_phase + h*hb)."""
+    t_abs = int(t_abs)
+    return 0 if t_abs < p.hb_phase_ns else (t_abs - p.hb_phase_ns) // p.heartbeat_ns
+
+
+def mesh_churn(p, row_ptr, col, flags, stage, lat, h_lo, h_hi):
+    """Churn snapshots for epochs [h_lo, h_hi]: mesh [E, N, 16], cnt [E, N], offline [E, N]."""
+    N, E = p.peers, h_hi - h_lo + 1
+    S = lat.shape[0]
+    mesh = np.zeros(E * N * MESH_W, np.uint32)
+    cnt = np.zeros(E * N, np.uint8)
+    off = np.zeros(E * N, np.uint8)
+    lat = np.ascontiguousarray(lat.reshape(-1), np.uint64)
+    stage = np.ascontiguousarray(stage, np.uint8)
+    flags = np.ascontiguousarray(flags, np.uint8)
+    rc = lib().or_mesh_churn(ctypes.byref(p), _p(row_ptr, ctypes.c_uint64), _p(col, ctypes.c_uint32),
+                             _p(flags, ctypes.c_uint8), _p(stage, ctypes.c_uint8), S, _p(lat, ctypes.c_uint64),
+                             h_lo, h_hi, _p(mesh, ctypes.c_uint32), _p(cnt, ctypes.c_uint8),
+                             _p(off, ctypes.c_uint8))
+    if rc:
+        raise ValueError("or_mesh_churn rc=%d" % rc)
+    return mesh.reshape(E, N, MESH_W), cnt.reshape(E, N), off.reshape(E, N)
+
+
+def run_churn(p, row_ptr, col, snaps, h_lo, stage, lat, bw_up, bw_dn, sched_t, sched_pub, sched_size):
+    N = p.peers
+    S = lat.shape[0]
+    M = len(sched_t)
+    smesh, scnt, soff = snaps
+    tc = np.zeros(M * N, np.uint64)
+    hops = np.zeros(M * N, np.uint8)
+    st = OrStats()
+    a64 = lambda x: np.ascontiguousarray(x, np.uint64)
+    a32 = lambda x: np.ascontiguousarray(x, np.uint32)
+    lat, bw_up, bw_dn, sched_t = a64(lat.reshape(-1)), a64(bw_up), a64(bw_dn), a64(sched_t)
+    sched_pub, sched_size = a32(sched_pub), a32(sched_size)
+    smesh, scnt, soff = a32(smesh.reshape(-1)), np.ascontiguousarray(scnt.reshape(-1), np.uint8), \
+        np.ascontiguousarray(soff.reshape(-1), np.uint8)
+    stage = np.ascontiguousarray(stage, np.uint8)
+    rc = lib().or_run_churn(ctypes.byref(p), _p(row_ptr, ctypes.c_uint64), _p(col, ctypes.c_uint32),
+                            _p(smesh, ctypes.c_uint32), _p(scnt, ctypes.c_uint8), _p(soff, ctypes.c_uint8),
+                            h_lo, len(scnt) // N, _p(stage, ctypes.c_uint8), S, _p(lat, ctypes.c_uint64),
+                            _p(bw_up, ctypes.c_uint64), _p(bw_dn, ctypes.c_uint64), _p(sched_t, ctypes.c_uint64),
+                            _p(sched_pub, ctypes.c_uint32), _p(sched_size, ctypes.c_uint32), M,
+                            _p(tc, ctypes.c_uint64), _p(hops, ctypes.c_uint8), ctypes.byref(st))
+    if rc:
+        raise ValueError("or_run_churn rc=%d" % rc)
+    stats = {n: getattr(st, n) for n, _ in OrStats._fields_}
+    return tc.reshape(M, N), hops.reshape(M, N), stats
+
+
 def run(p, row_ptr, col, mesh, cnt, stage, lat, bw_up, bw_dn, sched_t, sched_pub, sched_size):
     N = p.peers
     S = lat.shape[0]
@@ -171,9 +234,18 @@ def simulate(p, stages=1, links=(50, 50, 50, 50), mode=0, sched=None, max_hb=400
     bl, bh, ll, lh = links
     lat, bw = topogen_links(stages, bl, bh, ll, lh, mode)
     stage = (np.arange(p.peers) % stages).astype(np.uint8)
-    row_ptr, col, flags = build_topology(p)
-    flags, mesh, cnt, epochs = mesh_converge(p, row_ptr, col, flags, stage, lat, max_hb)
+    row_ptr, col, flags0 = build_topology(p)
+    flags, mesh, cnt, epochs = mesh_converge(p, row_ptr, col, flags0, stage, lat, max_hb)
     t, pub, size = sched
-    tc, hops, stats = run(p, row_ptr, col, mesh, cnt, stage, lat, bw, bw, t, pub, size)
-    return dict(lat=lat, bw=bw, stage=stage, row_ptr=row_ptr, col=col, flags=flags, mesh=mesh,
-                cnt=cnt, epochs=epochs, t_complete=tc, hops=hops, stats=stats)
+    out = dict(lat=lat, bw=bw, stage=stage, row_ptr=row_ptr, col=col, flags=flags, mesh=mesh,
+               cnt=cnt, epochs=epochs)
+    if p.churn_ppm:  # time-varying mesh: snapshots of every epoch the schedule can use
+        h_lo = min(epoch_at(p, x) for x in t)
+        h_hi = max(epoch_at(p, x) for x in t) + p.churn_horizon
+        snaps = mesh_churn(p, row_ptr, col, flags0, stage, lat, h_lo, h_hi)
+        tc, hops, stats = run_churn(p, row_ptr, col, snaps, h_lo, stage, lat, bw, bw, t, pub, size)
+        out.update(snaps=snaps, h_lo=h_lo)
+    else:
+        tc, hops, stats = run(p, row_ptr, col, mesh, cnt, stage, lat, bw, bw, t, pub, size)
+    out.update(t_complete=tc, hops=hops, stats=stats)
+    return out

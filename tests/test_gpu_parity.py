@@ -52,7 +52,7 @@ def compare(p, S, links, sched, mode=0, batch=64, ref=None):
     np.testing.assert_array_equal(res["hops"], ref["hops"], err_msg="hops")
     st = sim.stats()
     for k in ("deliveries", "frag_deliveries", "relaxations", "bytes_alg", "latency_sum_ms",
-              "latency_max_ms", "messages"):
+              "latency_max_ms", "messages", "gossip_iwant"):
         assert st[k] == ref["stats"][k], k
     return sim, res
 
@@ -181,3 +181,31 @@ def test_relax_kernel_variants_exact(variant, monkeypatch):
     compare(p, 5, (50, 150, 40, 130), _sched(40, 2000), batch=16)
     p = oracle.params(peers=3000, seed=32)
     compare(p, 3, (20, 200, 10, 90), _sched(70, 3000), batch=64)
+
+
+@pytest.mark.parametrize("frags,gossip,fast,idw", [(1, 0, 0, 0), (2, 0, 0, 0), (1, 1, 0, 0), (1, 0, 1, 0),
+                                                   (1, 1, 1, 0), (2, 1, 1, 0), (1, 0, 1, 1)])
+def test_churn_time_varying_mesh(frags, gossip, fast, idw):
+    """Churn (config #3 semantics) at small size: the device's
+    per-epoch snapshot ring (advanced from the converged state, or replayed from
+    epoch 0), offline peers, lost deliveries and the message lifetime, with and
+    without lazy gossip / IDONTWANT; bit-exact against the oracle."""
+    kw = dict(churn_ppm=20000, lazy_gossip=gossip, fragments=frags, idontwant=1000 if idw else 0)
+    if fast:  # 100 ms heartbeats from T0 - 2 s: several epochs per dissemination, replay from epoch 0
+        kw.update(heartbeat_ns=100_000_000, hb_phase_ns=T0 - 2_000_000_000 + 37_000_000, churn_down=8,
+                  churn_horizon=12)
+    else:  # heartbeat 0 at the Shadow process start: publishes at epoch ~495, ring advanced from epoch 400
+        kw.update(hb_phase_ns=gossipsim.SHADOW_START_NS)
+    p = oracle.params(peers=700, seed=51, **kw)
+    sim, res = compare(p, 5, (50, 150, 40, 130), _sched(24, 700), batch=8)
+    st = sim.stats()
+    assert 0 < st["deliveries"] < 24 * 699  # churn loses deliveries
+    if gossip:
+        assert st["gossip_iwant"] > 0
+
+
+def test_churn_errors():
+    p = oracle.params(peers=200, seed=3, churn_ppm=10000)  # hb_phase 0: publishes ~1e9 heartbeats later
+    sim, _ = gpu_sim(p, 1, (50, 50, 50, 50))
+    with pytest.raises(gossipsim.GossipSimError, match="2\\^20 heartbeats"):
+        sim.run(_sched(2, 200))

@@ -121,20 +121,49 @@ def test_mesh_invariants():
     assert r["epochs"] < 400
 
 
-def _py_gossip_targets(p, r, v, h):
-    row, col, mesh, cnt = r["row_ptr"].astype(np.int64), r["col"], r["mesh"], r["cnt"]
+def _py_gossip_targets(p, r, v, h, ch=None):
+    row, col = r["row_ptr"].astype(np.int64), r["col"]
+    mesh, cnt = (r["mesh"], r["cnt"]) if ch is None else ch.snap(h)
     ms = set(int(x) for x in mesh[v, :cnt[v]])
     cand = sorted((oracle.rng(p.seed, 6, v, h & 0xFFFFFFFF, int(w)), int(w))
-                  for w in col[row[v]:row[v + 1]] if int(w) not in ms)
+                  for w in col[row[v]:row[v + 1]] if int(w) not in ms and not (ch and ch.off(h, int(w))))
     rr = max(p.d_lazy, len(cand) * p.gossip_factor_milli // 1000)
     return [w for _, w in cand[:min(rr, len(cand))]]
 
 
+class _Churn:
+    """Epoch lookups over the oracle's snapshots for one message."""
+
+    def __init__(self, p, r, t_pub):
+        self.p, self.mesh, self.cnt, self.offl = p, *r["snaps"]
+        self.h_lo = r["h_lo"]
+        self.cap = self.epoch(t_pub) + p.churn_horizon
+
+    def epoch(self, tabs):
+        return 0 if tabs < self.p.hb_phase_ns else (tabs - self.p.hb_phase_ns) // self.p.heartbeat_ns
+
+    def dead(self, h):
+        return h > self.cap
+
+    def snap(self, h):
+        return self.mesh[h - self.h_lo], self.cnt[h - self.h_lo]
+
+    def off(self, h, u):
+        return bool(self.offl[h - self.h_lo, u])
+
+    def lost(self, tabs, w):  # delivery at absolute time tabs
+        h = self.epoch(tabs)
+        return self.dead(h) or self.off(h, w)
+
+
 def _py_disseminate(p, r, t_pub, pub, size):
-    """Pure-Python event simulation of DESIGN.md §2.5-2.7 (small N only)."""
+    """Pure-Python event simulation of DESIGN.md §2.5-2.8 (small N only)."""
     N, F = p.peers, p.fragments
     row, col = r["row_ptr"].astype(np.int64), r["col"]
     mesh, cnt, stage, lat, bw = r["mesh"], r["cnt"], r["stage"], r["lat"], r["bw"]
+    ch = _Churn(p, r, t_pub) if p.churn_ppm else None
+    if ch and ch.off(ch.epoch(t_pub), pub):  # an offline publisher publishes nothing
+        return np.full(N, np.iinfo(np.uint64).max, np.uint64), np.full(N, 255, np.uint8), 0
     payload = size // F
     wire = oracle.wire_bytes(payload, p.muxer, p.signed_msgs)
     ser = [(-(-wire * 8_000_000_000 // int(b))) for b in bw]
@@ -149,21 +178,27 @@ def _py_disseminate(p, r, t_pub, pub, size):
         sv = stage[v]
         for k in range(p.history_gossip):
             T = p.hb_phase_ns + (h0 + k) * p.heartbeat_ns - t_pub
-            for w in _py_gossip_targets(p, r, v, h0 + k):
+            if ch and (ch.dead(h0 + k) or ch.off(h0 + k, v)):
+                continue
+            for w in _py_gossip_targets(p, r, v, h0 + k, ch):
                 sw = stage[w]
                 ti = T + int(lat[sv, sw])
                 A = ti + int(lat[sw, sv]) + ser[sv] + int(lat[sv, sw]) + max(0, ser[sw] - ser[sv])
+                if ch and (ch.lost(t_pub + ti, w) or ch.lost(t_pub + A, w)):
+                    continue
                 heapq.heappush(heap, (ti, 1, (A, hv + 1, v), w, f))
 
     for f in range(F):
         best[(pub, f)] = (0, 0, pub)
         if p.lazy_gossip:
             gossip(pub, f, 0, 0)
-    tg = [int(x) for x in col[row[pub]:row[pub + 1]]]
+    tg = [int(x) for x in col[row[pub]:row[pub + 1]] if not (ch and ch.off(ch.epoch(t_pub), int(x)))]
     sp = stage[pub]
     for f in range(F):
         for j, w in enumerate(tg):
             arr = (f * len(tg) + j + 1) * ser[sp] + int(lat[sp, stage[w]]) + max(0, ser[stage[w]] - ser[sp])
+            if ch and ch.lost(t_pub + arr, w):
+                continue
             k = (arr, 1, pub)
             if k < best.get((w, f), (1 << 80,)):
                 best[(w, f)] = k
@@ -184,13 +219,20 @@ def _py_disseminate(p, r, t_pub, pub, size):
         done.add((u, f))
         t, h, src = k
         su = stage[u]
+        mrow, mcnt = mesh, cnt
+        if ch:
+            if ch.dead(ch.epoch(t_pub + t)):
+                continue  # received past the message's lifetime: not forwarded
+            mrow, mcnt = ch.snap(ch.epoch(t_pub + t))
         if p.lazy_gossip:
             gossip(u, f, t, h)
-        targets = [int(w) for w in mesh[u, :cnt[u]] if w != src and w != pub]
+        targets = [int(w) for w in mrow[u, :mcnt[u]] if w != src and w != pub]
         start = max(t, busy[u]) if F > 1 else t
         busy[u] = start + len(targets) * ser[su]
         for j, w in enumerate(targets):
             arr = start + (j + 1) * ser[su] + int(lat[su, stage[w]]) + max(0, ser[stage[w]] - ser[su])
+            if ch and ch.lost(t_pub + arr, w):
+                continue
             nk = (arr, h + 1, u)
             if nk < best.get((w, f), (1 << 80,)):
                 best[(w, f)] = nk
@@ -210,10 +252,13 @@ def _py_disseminate(p, r, t_pub, pub, size):
     return tc, hops, iwant[0]
 
 
-@pytest.mark.parametrize("frags,gossip", [(1, 0), (3, 0), (1, 1), (2, 1)])
-def test_oracle_matches_pure_python_restatement(frags, gossip):
+@pytest.mark.parametrize("frags,gossip,churn", [(1, 0, 0), (3, 0, 0), (1, 1, 0), (2, 1, 0), (1, 0, 1), (2, 1, 1)])
+def test_oracle_matches_pure_python_restatement(frags, gossip, churn):
     # slow links + a heartbeat phase inside the dissemination window so IWANTs happen
     kw = dict(lazy_gossip=gossip, hb_phase_ns=37_000_000, heartbeat_ns=100_000_000) if gossip else {}
+    if churn:  # 3 % departures per 100 ms heartbeat, 8-heartbeat outages, heartbeats from T0 - 2 s
+        kw.update(churn_ppm=30000, churn_down=8, churn_horizon=12, heartbeat_ns=100_000_000,
+                  hb_phase_ns=T0 - 2_000_000_000 + 37_000_000)
     p, r, (t, pub) = _sim(N=150, fragments=frags, links=(5, 20, 20, 80), **kw)
     iw = 0
     for m in range(len(t)):
@@ -243,3 +288,39 @@ def test_stats_identities():
     delivered = (r["t_complete"] != np.iinfo(np.uint64).max).sum() - st["messages"]
     assert st["deliveries"] == delivered
     assert st["frag_deliveries"] == st["deliveries"] * 2
+
+
+def _py_offline(p, u, h):
+    """a departure drawn at one of the epochs h-down+1..h."""
+    return h > 0 and any((oracle.rng(p.seed, 7, u, h - k, 0) * 1_000_000) >> 64 < p.churn_ppm
+                         for k in range(min(p.churn_down, h)))
+
+
+def test_churn_snapshots_invariants():
+    """Churn (config #3 semantics): the offline draw, empty rows for offline
+    peers, no offline peer in any row, a symmetric mesh in every epoch, the
+    expected offline fraction, and offline publishers publishing nothing."""
+    ph = T0 - 3_000_000_000
+    p, r, (t, pub) = _sim(N=400, seed=9, churn_ppm=20000, churn_down=10, churn_horizon=6,
+                          heartbeat_ns=100_000_000, hb_phase_ns=ph)
+    sm, sc, so = r["snaps"]
+    h_lo = r["h_lo"]
+    N = p.peers
+    for e in range(0, len(sc), 7):
+        for u in range(0, N, 13):
+            assert bool(so[e, u]) == _py_offline(p, u, h_lo + e)
+    for e in range(len(sc)):
+        rows = [set(int(x) for x in sm[e, u, :sc[e, u]]) for u in range(N)]
+        off = so[e].astype(bool)
+        assert all(len(rows[u]) == 0 for u in np.flatnonzero(off))
+        for u in range(N):
+            assert not any(off[w] for w in rows[u])
+            assert all(u in rows[w] for w in rows[u])
+    q = 1 - (1 - p.churn_ppm / 1e6) ** p.churn_down
+    assert abs(so[1:].mean() - q) < 0.05
+    for m in range(len(t)):
+        e = (int(t[m]) - ph) // p.heartbeat_ns - h_lo
+        if so[e, pub[m]]:
+            assert (r["t_complete"][m] == np.iinfo(np.uint64).max).all()
+        else:
+            assert r["t_complete"][m, pub[m]] == t[m]
