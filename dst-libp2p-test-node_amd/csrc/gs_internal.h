@@ -123,7 +123,7 @@ struct Ctx {
   DevBuf<uint32_t> d_tables; // lat[S*S] | ser_up[S] | ser_dn[S] (u32 ns)
   DevBuf<uint64_t> d_ctrl;   // [4] triple-buffered next-min keys + spare
   // owner-computes pull path (gs_pull_kernel.h)
-  DevBuf<uint64_t> d_rowmin; // [N] min pending key beyond the last emitted window
+  DevBuf<uint32_t> d_chunkmin; // [N][16] per 64-lane chunk: hi word of the min key beyond the last emitted window
   DevBuf<uint64_t> d_lrec;   // [2][N][L] per-row arrival records (gs_pull_kernel.h)
   DevBuf<uint32_t> d_lcnt;   // [2][N]
   DevBuf<uint8_t> d_rpos;    // [N][MESH_W] index of w in mesh(mesh[w][j])

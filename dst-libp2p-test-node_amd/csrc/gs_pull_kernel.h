@@ -8,7 +8,8 @@
 // that floor. Here every key row is written by its owner only:
 //
 //   one wave owns peer w's row keys[w][0..L) for the pass; it
-//    1. loads the row into registers (L <= 1024: 16 lanes-chunks of 64),
+//    1. loads the row's live 64-lane chunks into registers (L <= 1024: up to
+//       16 chunks of 64 lanes),
 //    2. PULL passes: reads the arrival records its mesh neighbours u emitted
 //       for window [lo, lo+D) in the previous pass — all neighbours' records
 //       in one flattened loop — and re-derives each forward u -> w exactly as
@@ -16,8 +17,12 @@
 //       u's uplink start, link latency), min-reducing them in an LDS buffer,
 //    3. merges, writes changed lanes back, and emits its own arrivals of the
 //       next window as 8-byte records for the pass after,
-//    4. keeps rowmin[w] = min pending key beyond that window, so rows with
-//       nothing to apply and nothing due cost one 8-B read.
+//    4. keeps chunkmin[w][q] = hi word of the min pending key of chunk q
+//       beyond that window. A chunk is live in a pass (read from HBM) only if
+//       it holds a key due in the emitted window or receives a candidate; rows
+//       with neither cost one 64-B read. Windows on the rising and falling
+//       edge of a batch touch a few of a row's 16 chunks, the peak windows
+//       all of them.
 //
 // Record (u64): start - window_lo (32) | hops (6) | j_src (5) | j_pub (5) |
 // slot (16), where j_src / j_pub are the indices of the sender's source and of
@@ -29,7 +34,8 @@
 // Exactness is the Delta-stepping argument of the push path: every send adds
 // >= D, so after applying window b's candidates all keys below the end of
 // window b+1 are final. Candidates are the same keys the push path atomically
-// min-reduces, so the result is bit-identical.
+// min-reduces, so the result is bit-identical. A chunk that is not live keeps
+// its keys and its chunkmin (>= the window end, so still the min beyond it).
 //
 // Control (device side, no host round trip per pass): ctrl holds three slots
 // of {lo, mode, records emitted, min pending}. Pass k decides from slot k-1:
@@ -42,11 +48,12 @@ constexpr uint32_t PULL_WAVES = TB / 64;  // rows in flight per block
 constexpr uint32_t PULL_LMAX = 1024;       // row lanes held in registers (16 chunks)
 constexpr uint32_t PULL_CH = PULL_LMAX / 64;
 constexpr uint32_t J_NONE = 31;
+static_assert(PULL_CH == MESH_W, "row header lane j carries mesh entry j and chunk j");
 
 struct PullArgs {
   uint64_t* keys;       // [N][L]
   uint64_t* busy;       // [N][B] uplink FIFO end per (peer, message), FP > 1
-  uint64_t* rowmin;     // [N]
+  uint32_t* chunkmin;   // [N][PULL_CH] hi word of the min pending key per chunk (~0 = none)
   uint64_t* lrec;       // [2][N][L] per-row arrival records
   uint32_t* lcnt;       // [2][N]
   const uint32_t* mesh;
@@ -61,6 +68,23 @@ struct PullArgs {
 };
 
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ uint32_t umin32(uint32_t x, uint32_t y) { return x < y ? x : y; }
+
+// Lane l receives the wave-wide min of x[l >> 2]: recursive halving over the
+// 16 chunk values (17 shuffles instead of 16 full 6-step reductions).
+__device__ __forceinline__ uint32_t chunk_min_scatter(const uint32_t (&x)[PULL_CH], int lane) {
+  const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8, b2 = lane & 4;
+  uint32_t a8[8], a4[4], a2[2];
+#pragma unroll
+  for (int i = 0; i < 8; i++) a8[i] = umin32(b5 ? x[i + 8] : x[i], __shfl_xor(b5 ? x[i] : x[i + 8], 32));
+#pragma unroll
+  for (int i = 0; i < 4; i++) a4[i] = umin32(b4 ? a8[i + 4] : a8[i], __shfl_xor(b4 ? a8[i] : a8[i + 4], 16));
+#pragma unroll
+  for (int i = 0; i < 2; i++) a2[i] = umin32(b3 ? a4[i + 2] : a4[i], __shfl_xor(b3 ? a4[i] : a4[i + 2], 8));
+  uint32_t a1 = umin32(b2 ? a2[1] : a2[0], __shfl_xor(b2 ? a2[0] : a2[1], 4));
+  a1 = umin32(a1, __shfl_xor(a1, 2));
+  return umin32(a1, __shfl_xor(a1, 1));
+}
 
 // Per wave: CW = the row's candidate minima, then (in place) the compacted
 // arrivals; LST = their group indices. 10 KB per wave, 4 blocks per CU.
@@ -117,51 +141,49 @@ __global__ __launch_bounds__(TB, 4) void k_pull(PullArgs a) {
   const uint64_t smask = (1ull << a.sb) - 1;
   const uint32_t hmask = (1u << HOP_BITS) - 1;
   const uint64_t lanelt = (1ull << lane) - 1;
-  uint64_t nmin = INF64, fd = 0, nr = 0, np = 0, nrec = 0;
+  uint64_t fd = 0, nr = 0, np = 0, nrec = 0;
+  uint32_t nmh = ~0u;  // hi word of the min pending key over this wave's rows
   uint32_t err = 0;
 
   // Row headers are software-pipelined one row ahead: lane j < 16 holds mesh
-  // entry j of the row, w's index in that neighbour's row, and the length of
-  // the neighbour's record list; plus rowmin. The next row's entries are
-  // loaded while this row is processed, its list lengths after step 2.
+  // entry j of the row, w's index in that neighbour's row, the length of the
+  // neighbour's record list, and chunk j's pending min. The next row's entries
+  // are loaded while this row is processed, its list lengths after step 2.
   const uint32_t stride = gridDim.x * PULL_WAVES;
   uint32_t w = blockIdx.x * PULL_WAVES + wv;
-  uint32_t ej = EMPTY, cj = 0, rj = 0;
-  uint64_t rm = INF64;
-  if (w < a.N) {
-    if (lane < (int)MESH_W) {
-      ej = a.mesh[(size_t)w * MESH_W + lane];
-      rj = a.rpos[(size_t)w * MESH_W + lane];
-      if (pull && ej != EMPTY) cj = rcnt[ej & 0xFFFFFFu];
-    }
-    rm = a.rowmin[w];
+  uint32_t ej = EMPTY, cj = 0, rj = 0, cm = ~0u;
+  if (w < a.N && lane < (int)MESH_W) {
+    ej = a.mesh[(size_t)w * MESH_W + lane];
+    rj = a.rpos[(size_t)w * MESH_W + lane];
+    if (pull && ej != EMPTY) cj = rcnt[ej & 0xFFFFFFu];
+    cm = a.chunkmin[(size_t)w * PULL_CH + lane];
   }
   for (; w < a.N; w += stride) {
     const uint32_t w2 = w + stride;
-    uint32_t ej2 = EMPTY, rj2 = 0, cj2 = 0;
-    uint64_t rm2 = INF64;
-    if (w2 < a.N) {  // wave-uniform
-      if (lane < (int)MESH_W) {
-        ej2 = a.mesh[(size_t)w2 * MESH_W + lane];
-        rj2 = a.rpos[(size_t)w2 * MESH_W + lane];
-      }
-      rm2 = a.rowmin[w2];
+    uint32_t ej2 = EMPTY, rj2 = 0, cj2 = 0, cm2 = ~0u;
+    if (w2 < a.N && lane < (int)MESH_W) {  // w2 < N is wave-uniform
+      ej2 = a.mesh[(size_t)w2 * MESH_W + lane];
+      rj2 = a.rpos[(size_t)w2 * MESH_W + lane];
+      cm2 = a.chunkmin[(size_t)w2 * PULL_CH + lane];
     }
     const uint64_t cand = __ballot(cj != 0);
-    if (cand == 0 && rm >= hik) {  // nothing to apply, nothing due in [wlo, whi)
+    // chunks holding a key due in [wlo, whi) (chunkmin never drops below the
+    // emitted windows: keys below wlo are final and were emitted earlier)
+    uint32_t live = (uint32_t)__ballot(cm < hhi);
+    if (cand == 0 && live == 0) {  // nothing to apply, nothing due
       if (lane == 0) wcnt[w] = 0;
-      nmin = rm < nmin ? rm : nmin;
+      nmh = umin32(nmh, cm);
       if (pull && lane < (int)MESH_W && ej2 != EMPTY) cj2 = rcnt[ej2 & 0xFFFFFFu];
-      ej = ej2; rj = rj2; cj = cj2; rm = rm2;
+      ej = ej2; rj = rj2; cj = cj2; cm = cm2;
       continue;
     }
-    // 1. the row into registers (16 loads in flight per lane)
+    // 1. the due chunks into registers (up to 16 loads in flight per lane)
     const uint64_t* grow = a.keys + (size_t)w * LL;
     uint64_t v[PULL_CH];
 #pragma unroll
     for (int q = 0; q < (int)PULL_CH; q++) {
       const uint32_t i = q * 64 + lane;
-      v[q] = i < LL ? grow[i] : INF64;
+      v[q] = ((live >> q) & 1u) && i < LL ? grow[i] : INF64;
     }
     const uint32_t sw = a.stage[w];
     if (pull) {
@@ -171,17 +193,18 @@ __global__ __launch_bounds__(TB, 4) void k_pull(PullArgs a) {
       // 2. the neighbours' records: lists in groups of 4, two 64-record chunks
       //    each, so up to 8 independent record loads per lane are in flight
       const uint32_t sd = sdn[sw];
-      uint64_t cm = cand;
-      while (cm) {
+      uint64_t cmk = cand;
+      uint32_t cb = 0;  // chunks that receive a candidate
+      while (cmk) {
         uint32_t U[4], R4[4], NN[4], SER[4];
         uint64_t BASE[4];
         uint32_t maxn = 0;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
           U[k] = 0; R4[k] = 0; NN[k] = 0; SER[k] = 0; BASE[k] = 0;
-          if (cm) {  // wave-uniform
-            const int j = __builtin_ctzll(cm);
-            cm &= cm - 1;
+          if (cmk) {  // wave-uniform
+            const int j = __builtin_ctzll(cmk);
+            cmk &= cmk - 1;
             const uint32_t e = __builtin_amdgcn_readlane(ej, j);
             U[k] = e & 0xFFFFFFu;
             R4[k] = __builtin_amdgcn_readlane(rj, j);
@@ -215,37 +238,55 @@ __global__ __launch_bounds__(TB, 4) void k_pull(PullArgs a) {
               if (arr > a.tmax) err |= ERR_TIME;
               const uint64_t hp1 = ((lo32 >> 26) & hmask) + 1;
               const uint64_t nk = (arr << a.tshift) | (hp1 << a.sb) | U[k];
-              atomicMin((unsigned long long*)&CW[lo32 & 0xFFFFu], (unsigned long long)nk);
+              const uint32_t slot = lo32 & 0xFFFFu;
+              atomicMin((unsigned long long*)&CW[slot], (unsigned long long)nk);
+              cb |= 1u << (slot >> 6);
             }
         }
+      }
+      for (int off = 32; off > 0; off >>= 1) cb |= __shfl_xor(cb, off);
+      cb = __builtin_amdgcn_readfirstlane(cb);
+      // 1b. chunks live only through candidates
+      const uint32_t extra = cb & ~live;
+      live |= cb;
+#pragma unroll
+      for (int q = 0; q < (int)PULL_CH; q++) {
+        const uint32_t i = q * 64 + lane;
+        if ((extra >> q) & 1u) v[q] = i < LL ? grow[i] : INF64;
       }
       wave_lds_sync();
     }
     if (pull && lane < (int)MESH_W && ej2 != EMPTY) cj2 = rcnt[ej2 & 0xFFFFFFu];  // next row's lists
     // 3. dense: merge, write back changed lanes, compact the arrivals of
-    //    [wlo, whi) in place (groups of FP lanes), min of what lies beyond
+    //    [wlo, whi) in place (groups of FP lanes), per-chunk min beyond it
     const bool chk_pub = wlo == 0;  // only window 0 can hold a publisher's own key
     uint32_t cnt = 0;               // compacted groups
-    uint32_t rmin = ~0u;            // high word of the min key beyond the window
+    uint32_t lq[PULL_CH];           // this lane's key beyond the window, per chunk
 #pragma unroll
     for (int q = 0; q < (int)PULL_CH; q++) {
-      if (q * 64 < (int)LL) {  // wave-uniform
+      lq[q] = ~0u;
+      if (q * 64 < (int)LL && ((live >> q) & 1u)) {  // wave-uniform
         const uint32_t i = q * 64 + lane;
         const bool valid = i < LL;
         uint64_t x = v[q];
-        if (pull && valid) {
-          const uint64_t c = CW[i];
-          if (c < x) {
+        if (pull) {
+          const uint64_t c = valid ? CW[i] : INF64;
+          const bool chg = c < x;
+          if (chg) {
             x = c;
-            a.keys[(size_t)w * LL + i] = x;
             np++;
           }
+          // write back whole 64-B sectors that hold a changed lane: a partial
+          // sector store costs a read-modify-write (random single-lane stores
+          // into an 8 GB table run at 22 G/s, full sectors at 383 G/s,
+          // profiles/r01_v6/ubench_mem.json)
+          const uint64_t cm8 = __ballot(chg);
+          if (valid && ((cm8 >> (lane & 56)) & 0xFFull)) a.keys[(size_t)w * LL + i] = x;
         }
         const uint32_t hx = (uint32_t)(x >> 32);
         bool act = valid && (hx - hlo) < hspan;
         if (chk_pub && act) act = a.pub[i / FP] != w;
-        const uint32_t later = hx >= hhi ? hx : ~0u;
-        rmin = later < rmin ? later : rmin;
+        lq[q] = hx >= hhi ? hx : ~0u;
         const uint64_t am = __ballot(act);
         if (am) {  // wave-uniform
           if constexpr (FP == 1) {
@@ -310,20 +351,23 @@ __global__ __launch_bounds__(TB, 4) void k_pull(PullArgs a) {
         ecnt += (uint32_t)__popcll(wm);
       }
     }
-    for (int off = 32; off > 0; off >>= 1) {
-      const uint32_t y = __shfl_xor(rmin, off);
-      rmin = y < rmin ? y : rmin;
+    // 5. new chunk minima: lanes 4c..4c+3 hold chunk c's; chunks that were not
+    //    live keep theirs (their keys did not change and lie beyond the window)
+    {
+      const uint32_t red = chunk_min_scatter(lq, lane);
+      const uint32_t c = (uint32_t)lane >> 2;
+      const uint32_t oldc = (uint32_t)__shfl((int)cm, (int)c);
+      const bool lc = (live >> c) & 1u;
+      const uint32_t ncm = lc ? red : oldc;
+      if ((lane & 3) == 0) a.chunkmin[(size_t)w * PULL_CH + c] = ncm;  // the whole 64-B sector
+      nmh = umin32(nmh, ncm);
     }
-    const uint64_t rmk = rmin == ~0u ? INF64 : (uint64_t)rmin << 32;
-    if (lane == 0) {
-      wcnt[w] = ecnt;
-      a.rowmin[w] = rmk;
-    }
+    if (lane == 0) wcnt[w] = ecnt;
     nrec += ecnt;
-    nmin = rmk < nmin ? rmk : nmin;
-    ej = ej2; rj = rj2; cj = cj2; rm = rm2;
+    ej = ej2; rj = rj2; cj = cj2; cm = cm2;
   }
-  nmin = wave_min(nmin);
+  for (int off = 32; off > 0; off >>= 1) nmh = umin32(nmh, __shfl_xor(nmh, off));
+  const uint64_t nmin = nmh == ~0u ? INF64 : (uint64_t)nmh << 32;
   fd = wave_sum(fd);
   nr = wave_sum(nr);
   np = wave_sum(np);

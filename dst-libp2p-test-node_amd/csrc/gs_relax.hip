@@ -36,7 +36,7 @@ struct SeedArgs {
   const uint8_t* stage;
   const uint32_t* tables;
   uint64_t* ctrl;      // min seeded key (push: the first bucket; pull: slot 2's min)
-  uint64_t* rowmin;    // pull path: per-row min pending key (nullptr on the push path)
+  uint32_t* chunkmin;  // pull path: [N][16] min pending key hi-word per 64-lane chunk (push path: nullptr)
   uint64_t* counters;
   uint64_t tmax;
   uint32_t L, FP, Fe, S, sb, tshift, flood;
@@ -101,7 +101,8 @@ __global__ __launch_bounds__(TB) void k_seed(SeedArgs a) {
     if (w - a.u0 >= a.un) continue;
     if (a.churn && ev_lost(a, m, arr, w)) continue;
     atomicMin((unsigned long long*)&a.keys[(size_t)(w - a.u0) * a.L + (size_t)m * a.FP + f], (unsigned long long)nk);
-    if (a.rowmin) atomicMin((unsigned long long*)&a.rowmin[w - a.u0], (unsigned long long)nk);
+    if (a.chunkmin)
+      atomicMin(&a.chunkmin[(size_t)(w - a.u0) * PULL_CH + ((m * a.FP + f) >> 6)], (uint32_t)(nk >> 32));
     nmin = nk < nmin ? nk : nmin;
   }
   nmin = wave_min(nmin);
@@ -278,12 +279,12 @@ static void set_churn_args(Ctx& c, A& a) {
 }
 
 static void launch_seed(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, uint64_t* seed_min = nullptr,
-                        uint64_t* rowmin = nullptr) {
+                        uint32_t* chunkmin = nullptr) {
   SeedArgs sa{};
   set_churn_args(c, sa);
   sa.keys = c.d_keys.p; sa.row = c.d_row.p; sa.col = c.d_col.p; sa.mesh = c.d_mesh.p;
   sa.pub = c.d_pub.p; sa.stage = c.d_stage.p; sa.tables = c.d_tables.p;
-  sa.ctrl = seed_min ? seed_min : c.d_ctrl.p; sa.rowmin = rowmin;
+  sa.ctrl = seed_min ? seed_min : c.d_ctrl.p; sa.chunkmin = chunkmin;
   sa.counters = c.d_counters.p; sa.tmax = b.tmax; sa.L = b.L; sa.FP = b.FP; sa.Fe = b.Fe;
   sa.S = c.S; sa.sb = b.sb; sa.tshift = b.tshift; sa.flood = c.cfg.flood_publish;
   sa.u0 = u0; sa.un = un;
@@ -359,7 +360,7 @@ static void run_pull_batch(Ctx& c, const Batch& b, EvFn& ev, size_t& n_ev, int d
   const uint32_t N = c.cfg.peers, L = b.L;
   hipStream_t s = c.stream;
   const size_t NL = (size_t)N * L;
-  c.d_rowmin.alloc(N);
+  c.d_chunkmin.alloc((size_t)N * PULL_CH);
   c.d_lrec.alloc(2 * NL);
   c.d_lcnt.alloc(2 * (size_t)N);
   c.d_pctrl.alloc(12);
@@ -371,12 +372,12 @@ static void run_pull_batch(Ctx& c, const Batch& b, EvFn& ev, size_t& n_ev, int d
     if (read_counter(c, C_ERR) & ERR_MESH) c.fail(GS_ERANGE, "mesh is not symmetric");
     c.rpos_valid = true;
   }
-  GS_HIP(hipMemsetAsync(c.d_rowmin.p, 0xFF, (size_t)N * 8, s));
+  GS_HIP(hipMemsetAsync(c.d_chunkmin.p, 0xFF, (size_t)N * PULL_CH * 4, s));
   GS_HIP(hipMemsetAsync(c.d_pctrl.p, 0, 12 * 8, s));  // every slot {lo 0, DONE, 0 records, min INF}
   for (int q = 0; q < 3; q++) GS_HIP(hipMemsetAsync(c.d_pctrl.p + q * 4 + 3, 0xFF, 8, s));
-  launch_seed(c, b, 0, N, c.d_pctrl.p + 2 * 4 + 3, c.d_rowmin.p);
+  launch_seed(c, b, 0, N, c.d_pctrl.p + 2 * 4 + 3, c.d_chunkmin.p);
   PullArgs pa{};
-  pa.keys = c.d_keys.p; pa.busy = c.d_busy.p; pa.rowmin = c.d_rowmin.p;
+  pa.keys = c.d_keys.p; pa.busy = c.d_busy.p; pa.chunkmin = c.d_chunkmin.p;
   pa.lrec = c.d_lrec.p; pa.lcnt = c.d_lcnt.p; pa.rpos = c.d_rpos.p;
   pa.mesh = c.d_mesh.p; pa.pub = c.d_pub.p; pa.stage = c.d_stage.p; pa.tables = c.d_tables.p;
   // windows on the key's high-word grain (gs_pull_kernel.h); the caller checked delta >= grain
