@@ -1,0 +1,143 @@
+"""GPU runs at BASELINE.json's full config sizes (configs #2, #3, #4; config #1
+is tests/test_gpu_parity.py::test_config1_1k_peers_100_publishes).
+
+At these sizes the whole oracle run would take minutes, so each test checks
+size-independent properties (every peer completes on a connected mesh, the
+publisher's own row, hop bounds, message sharding = the whole run, peer
+partition = one device) and a sample of messages bit-exact against the CPU
+oracle run on the GPU's own graph and mesh."""
+import numpy as np
+import pytest
+
+import gossipsim
+import oracle
+import partition
+
+pytestmark = pytest.mark.gpu
+T0 = gossipsim.T0_NS
+UND = np.iinfo(np.uint64).max
+LINKS = (50, 150, 40, 130)  # run.sh / shadow/README.md example: 5 stages, 50-150 Mbit, 40-130 ms
+
+
+def _sched(M, N, size=15000, pub0=6):
+    t = T0 + np.arange(M, dtype=np.uint64) * np.uint64(1_000_000_000)
+    return t, (pub0 + np.arange(M)) % N, np.full(M, size)
+
+
+def _sim(p, S, links, batch):
+    kw = {n: getattr(p, n) for n, _ in oracle.OrParams._fields_}
+    kw["batch"] = batch
+    sim = gossipsim.Simulator(**kw)
+    sim.set_topogen_links(S, *links)
+    sim.connect_gossipsub_peers()
+    sim.mesh_converge()
+    return sim
+
+
+def _links(p, S, links):
+    lat, bw = oracle.topogen_links(S, *links)
+    return lat, bw, (np.arange(p.peers) % S).astype(np.uint8)
+
+
+def _sub(sched, idx):
+    return tuple(np.asarray(x)[idx] for x in sched)
+
+
+def _publisher_rows(res, sched):
+    M = len(sched[0])
+    np.testing.assert_array_equal(res["t_complete"][np.arange(M), sched[1]], sched[0])
+    assert (res["hops"][np.arange(M), sched[1]] == 0).all()
+
+
+def test_config2_10k_peers_f8_1000_msgs():
+    """Config #2: 10k peers, FRAGMENTS=8 (1875 B fragments), 1000 messages, 5-stage links."""
+    N, M, S = 10_000, 1000, 5
+    p = oracle.params(peers=N, seed=2, fragments=8)
+    sched = _sched(M, N)
+    sim = _sim(p, S, LINKS, batch=128)
+    res = sim.run(sched)
+    st = sim.stats()
+    assert st["deliveries"] == M * (N - 1) and st["frag_deliveries"] == 8 * M * (N - 1)
+    tc, hp = res["t_complete"], res["hops"]
+    assert (tc >= sched[0][:, None]).all() and (hp < 63).all()
+    _publisher_rows(res, sched)
+    lat_ms = (tc - sched[0][:, None]) // 1_000_000
+    assert st["latency_sum_ms"] == int(lat_ms.sum()) and st["latency_max_ms"] == int(lat_ms.max())
+    # sampled parity against the oracle on the GPU's graph and mesh
+    row, col, _ = sim.csr()
+    mesh, cnt = sim.mesh()
+    lat, bw, stage = _links(p, S, LINKS)
+    idx = np.array([0, 517, 999])
+    otc, ohp, _ = oracle.run(p, row, col, mesh, cnt, stage, lat, bw, bw, *_sub(sched, idx))
+    np.testing.assert_array_equal(tc[idx], otc)
+    np.testing.assert_array_equal(hp[idx], ohp)
+    # message sharding (bench.py --gpus N): shards on fresh contexts == the whole run
+    for lo, hi in ((0, 384), (384, M)):
+        r2 = _sim(p, S, LINKS, batch=128).run(_sub(sched, slice(lo, hi)))
+        np.testing.assert_array_equal(r2["t_complete"], tc[lo:hi])
+        np.testing.assert_array_equal(r2["hops"], hp[lo:hi])
+
+
+def test_config3_100k_hetero_gossip_churn():
+    """Config #3: 100k peers, heterogeneous topogen links, lazy IHAVE/IWANT and
+    churn (1 % of peers start a 10-heartbeat outage every heartbeat), 1000 msgs."""
+    N, M, S = 100_000, 1000, 5
+    hb = 1_000_000_000
+    p = oracle.params(peers=N, seed=3, lazy_gossip=1, churn_ppm=10_000, churn_down=10, churn_horizon=16,
+                      heartbeat_ns=hb, hb_phase_ns=T0 - 20 * hb + 370_000_000)
+    sched = _sched(M, N)
+    sim = _sim(p, S, LINKS, batch=64)
+    res = sim.run(sched)
+    st = sim.stats()
+    tc, hp = res["t_complete"], res["hops"]
+    got = tc != UND
+    assert 0.5 * M * (N - 1) < st["deliveries"] < M * (N - 1)  # churn loses deliveries, most still arrive
+    assert st["gossip_iwant"] > 0
+    assert (hp[got] < 63).all() and ((tc >= sched[0][:, None]) | ~got).all()
+    # nothing arrives past the message lifetime (epoch of t_pub + horizon)
+    ep_pub = (sched[0] - np.uint64(p.hb_phase_ns)) // np.uint64(hb)
+    limit = np.uint64(p.hb_phase_ns) + (ep_pub + np.uint64(p.churn_horizon + 1)) * np.uint64(hb)
+    assert (tc[got] < np.broadcast_to(limit[:, None], tc.shape)[got]).all()
+    # sampled parity: the oracle replays churn from epoch 0 on the GPU's graph
+    row, col, flags = sim.csr()
+    lat, bw, stage = _links(p, S, LINKS)
+    idx = np.array([0, 1])
+    t, pub, size = _sub(sched, idx)
+    h_lo = min(oracle.epoch_at(p, x) for x in t)
+    h_hi = max(oracle.epoch_at(p, x) for x in t) + p.churn_horizon
+    snaps = oracle.mesh_churn(p, row, col, (flags & 1).astype(np.uint8), stage, lat, h_lo, h_hi)
+    otc, ohp, ost = oracle.run_churn(p, row, col, snaps, h_lo, stage, lat, bw, bw, t, pub, size)
+    np.testing.assert_array_equal(tc[idx], otc)
+    np.testing.assert_array_equal(hp[idx], ohp)
+    # message sharding under churn: a fresh context on a later shard reproduces it
+    r2 = _sim(p, S, LINKS, batch=64).run(_sub(sched, slice(600, 700)))
+    np.testing.assert_array_equal(r2["t_complete"], tc[600:700])
+    np.testing.assert_array_equal(r2["hops"], hp[600:700])
+
+
+def test_config4_1m_peers_peer_partitioned():
+    """Config #4 at 1M peers: peers partitioned over 2 contexts exchanging each
+    window's records (loop-back all-gather, the same protocol as RCCL across
+    GPUs) == one device == the oracle on a sampled message."""
+    import torch
+    N, S, M = 1_000_000, 5, 8
+    p = oracle.params(peers=N, seed=4)
+    sched = _sched(M, N)
+    whole = _sim(p, S, LINKS, batch=M)
+    ref = whole.run(sched)
+    _publisher_rows(ref, sched)
+    assert whole.stats()["deliveries"] == M * (N - 1)
+    sims = [_sim(p, S, LINKS, batch=M) for _ in range(2)]
+    for i, s in enumerate(sims):
+        s.set_partition(2, i)
+    bufs = [partition.RecordBuffer(torch.device("cuda", 0), capacity=1 << 22) for _ in sims]
+    res, info = partition.run_partitioned(sims, sched, partition.LoopbackExchange(), bufs=bufs)
+    np.testing.assert_array_equal(np.concatenate([r["t_complete"] for r in res], axis=1), ref["t_complete"])
+    np.testing.assert_array_equal(np.concatenate([r["hops"] for r in res], axis=1), ref["hops"])
+    assert sum(s.stats()["deliveries"] for s in sims) == M * (N - 1)
+    row, col, _ = whole.csr()
+    mesh, cnt = whole.mesh()
+    lat, bw, stage = _links(p, S, LINKS)
+    otc, ohp, _ = oracle.run(p, row, col, mesh, cnt, stage, lat, bw, bw, *_sub(sched, np.array([5])))
+    np.testing.assert_array_equal(ref["t_complete"][5:6], otc)
+    np.testing.assert_array_equal(ref["hops"][5:6], ohp)
