@@ -22,7 +22,9 @@ constexpr uint32_t MAX_DEG = 256;     // per-row working sets of the mesh kernel
 constexpr uint32_t MAX_FRAGS = 16;    // FRAGMENTS (topogen allows 1..9)
 constexpr uint32_t STAGE_SHIFT = 24;  // packed mesh entry: stage << 24 | peer
 
-enum : uint32_t { P_DIAL = 1, P_DIAL_ORDER = 2, P_GRAFT = 3, P_PRUNE = 4, P_OUT_GRAFT = 5, P_GOSSIP = 6, P_CHURN = 7 };
+enum : uint32_t { P_DIAL = 1, P_DIAL_ORDER = 2, P_GRAFT = 3, P_PRUNE = 4, P_OUT_GRAFT = 5, P_GOSSIP = 6, P_CHURN = 7,
+                  P_MSGID = 8 };
+enum : uint32_t { NODE_RUST = 0, NODE_GO = 1, NODE_NIM = 2 };  // GS_NODE_*
 enum : uint8_t { F_OUT = 1, F_MESH = 2 };
 enum : uint8_t { PR_GRAFT = 1, PR_PRUNE = 2, PR_ACCEPT = 4 };
 
@@ -68,6 +70,26 @@ GS_HD uint32_t dials_per_peer(uint32_t peers, uint32_t connect_to, uint32_t dial
   if (lim > (uint64_t)peers - 1) lim = peers - 1;
   uint64_t k = (uint64_t)connect_to + dial_extra;
   return (uint32_t)(k < lim ? k : lim);
+}
+
+// Fragment layout per node flavour:
+//  rust publish_new_message (main.rs:109-121): msg_size/F bytes, i64 stamp in
+//    [0..8) (panics below 8 B), byte 10 = chunk only when the buffer is > 10 B
+//    (else every fragment is identical: one msg-id, defect D8);
+//  go publishNewMessage (go-test-node/main.go:63-74): 8-byte stamp + msg_size/F
+//    bytes, payload[10] = chunk (index out of range when msg_size/F <= 2);
+//  nim publishNewMessage (nim gossipsub-queues/main.nim:158-175): 16-byte
+//    header + msg_size div F - 16 bytes, nowBytes[16] = chunk (IndexDefect
+//    when msg_size div F <= 16).
+GS_HD uint64_t frag_payload(uint32_t node, uint64_t msg_size, uint32_t F) {
+  return msg_size / F + (node == NODE_GO ? 8 : 0);
+}
+GS_HD bool frag_invalid(uint32_t node, uint64_t msg_size, uint32_t F) {
+  const uint64_t q = msg_size / F;
+  return node == NODE_GO ? q <= 2 : node == NODE_NIM ? q <= 16 : q < 8;
+}
+GS_HD bool frag_collide(uint32_t node, uint64_t msg_size, uint32_t F) {
+  return node == NODE_RUST && F > 1 && msg_size / F <= 10;
 }
 
 // Serialisation time in ns of `bytes` at `bps` (ceil).

@@ -43,6 +43,7 @@ static void validate(const gs_config& c) {
   if (c.batch < 1 || c.batch > 65536) bad("batch must be in 1..65536");
   if (c.churn_ppm > 1000000) bad("churn_ppm must be <= 1000000");
   if (c.churn_ppm && (c.churn_down < 1 || c.churn_horizon < 1)) bad("churn needs churn_down >= 1 and churn_horizon >= 1");
+  if (c.node > GS_NODE_NIM) bad("unknown node flavour (GS_NODE_RUST / _GO / _NIM)");
 }
 
 }  // namespace gs

@@ -42,6 +42,27 @@ extern "C" void gs_config_default(gs_config* c) {
   c->churn_ppm = 0;               // frozen mesh (the reference has no churn)
   c->churn_down = 10;             // rejoin after 10 epochs
   c->churn_horizon = 16;
+  c->node = GS_NODE_RUST;
+}
+
+extern "C" gs_status gs_config_preset(gs_config* c, uint32_t node) {
+  if (!c || node > GS_NODE_NIM) return GS_EINVAL;
+  gs_config_default(c);
+  c->node = node;
+  if (node == GS_NODE_GO) {       // go-test-node/main.go:153-175,374-385
+    c->d_out = 2;                 // gsParams.Dout = 2 (main.go:160)
+    c->idontwant = 1000;          // IDontWantMessageThreshold = 1000 (main.go:165)
+    c->signed_msgs = 0;           // WithMessageSignaturePolicy(StrictNoSign) (main.go:383)
+    c->self_log = 1;              // the node's own subscription delivers its publish (readLoop, main.go:52-60)
+  } else if (node == GS_NODE_NIM) {  // nim-test-node/gossipsub-queues/main.nim
+    c->dial_extra = 0;            // dials CONNECTTO peers (main.nim:396)
+    c->max_connections = 250;     // withMaxConnections(MAXCONNECTIONS, default 250) (main.nim:429)
+    c->d_out = c->d / 2;          // GOSSIPSUB_D_OUT default d div 2 (main.nim:258)
+    c->d_lazy = c->d;             // GOSSIPSUB_D_LAZY default d (main.nim:259)
+    c->signed_msgs = 0;           // initializeGossipsub(switch, anonymize = true) (main.nim:447)
+    c->self_log = 1;              // triggerSelf = SELFTRIGGER, default true (main.nim:245)
+  }
+  return GS_OK;
 }
 
 namespace {
@@ -80,6 +101,16 @@ extern "C" gs_status gs_config_from_env(gs_config* c, char* err, size_t err_len)
   if (!c) return GS_EINVAL;
   bool bad = false;
   uint64_t x;
+  const char* nd = getenv("GS_NODE");  // which test node's defaults (rust | go | nim)
+  if (nd && *nd) {
+    const uint32_t keep_dev = (uint32_t)c->device, keep_batch = c->batch;
+    if (!strcasecmp(nd, "rust")) gs_config_preset(c, GS_NODE_RUST);
+    else if (!strcasecmp(nd, "go")) gs_config_preset(c, GS_NODE_GO);
+    else if (!strcasecmp(nd, "nim")) gs_config_preset(c, GS_NODE_NIM);
+    else { set_err(err, err_len, std::string("Unknown node type: ") + nd); return GS_EINVAL; }
+    c->device = (int32_t)keep_dev;
+    c->batch = keep_batch;
+  }
   if (env_u64("PEERS", &x, err, err_len, &bad)) c->peers = (uint32_t)x;
   if (env_u64("CONNECTTO", &x, err, err_len, &bad)) c->connect_to = (uint32_t)x;
   if (env_u64("FRAGMENTS", &x, err, err_len, &bad)) c->fragments = (uint32_t)x;
@@ -232,6 +263,35 @@ extern "C" gs_status gs_write_latency_log(const char* path, const gs_publish* sc
       const int64_t ms = ((int64_t)t - (int64_t)tx) / 1000000;  // i64 division, main.rs:91-93
       fprintf(f, "shadow.data/hosts/peer%u/main.1000.stdout:%llu:%lld milliseconds: %lld\n", u,
               (unsigned long long)++line, (long long)tx, (long long)ms);
+    }
+  }
+  if (fclose(f)) return GS_EINVAL;
+  return GS_OK;
+}
+
+extern "C" gs_status gs_write_node_log(const gs_config* cfg, const char* path, const gs_publish* sched,
+                                       uint64_t n_msgs, const uint64_t* t_complete_ns) {
+  if (!cfg || cfg->node > GS_NODE_NIM) return GS_EINVAL;
+  if (cfg->node != GS_NODE_NIM)  // rust main.rs:93 and go main.go:49 print the same line
+    return gs_write_latency_log(path, sched, n_msgs, cfg->peers, t_complete_ns, cfg->self_log);
+  if (!path || !sched || !t_complete_ns) return GS_EINVAL;
+  FILE* f = fopen(path, "w");
+  if (!f) return GS_EINVAL;
+  std::vector<char> buf(1 << 20);
+  setvbuf(f, buf.data(), _IOFBF, buf.size());
+  std::vector<uint64_t> ids(n_msgs);  // msgId = uint64(rand(high(int64))) (main.nim:162), drawn per message
+  for (uint64_t m = 0; m < n_msgs; m++)
+    ids[m] = gs::rng(cfg->seed, gs::P_MSGID, sched[m].publisher, (uint32_t)(sched[m].t_pub_ns >> 32),
+                     (uint32_t)sched[m].t_pub_ns) >> 1;
+  for (uint32_t u = 0; u < cfg->peers; u++) {
+    uint64_t line = 0;
+    for (uint64_t m = 0; m < n_msgs; m++) {
+      const uint64_t t = t_complete_ns[m * cfg->peers + u];
+      if (t == GS_UNDELIVERED) continue;
+      if (u == sched[m].publisher && !cfg->self_log) continue;
+      const int64_t ms = ((int64_t)t - (int64_t)sched[m].t_pub_ns) / 1000000;  // delay.inMilliseconds()
+      fprintf(f, "shadow.data/hosts/peer%u/main.1000.stdout:%llu:%llu milliseconds: %lld\n", u,
+              (unsigned long long)++line, (unsigned long long)ids[m], (long long)ms);
     }
   }
   if (fclose(f)) return GS_EINVAL;

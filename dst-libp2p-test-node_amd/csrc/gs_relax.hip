@@ -211,8 +211,10 @@ uint32_t pow2_at_least(uint32_t x) { uint32_t p = 1; while (p < x) p <<= 1; retu
 static void check_schedule(Ctx& c, const gs_publish* sched, uint64_t n_msgs) {
   for (uint64_t i = 0; i < n_msgs; i++) {
     if (sched[i].publisher >= c.cfg.peers) c.fail(GS_EINVAL, "publisher id out of range");
-    if (sched[i].msg_size / c.cfg.fragments < 8)  // main.rs:110-111 slices buffer[..8]
-      c.fail(GS_EINVAL, "fragment payload shorter than the 8-byte tx_time stamp");
+    if (frag_invalid(c.cfg.node, sched[i].msg_size, c.cfg.fragments))  // the node's publish fails
+      c.fail(GS_EINVAL, c.cfg.node == NODE_RUST ? "fragment payload shorter than the 8-byte tx_time stamp"
+                        : c.cfg.node == NODE_GO ? "fragment too short for its chunk byte (payload[10])"
+                                                : "fragment shorter than the 16-byte nim header + chunk byte");
   }
 }
 
@@ -228,8 +230,8 @@ static Batch setup_batch(Ctx& c, const gs_publish* sched, uint64_t i0, uint64_t 
   b.sb = bits_for(N);
   b.tshift = b.sb + HOP_BITS;
   b.tmax = b.tshift >= 64 ? 0 : (INF64 >> b.tshift);
-  b.payload = sched[i0].msg_size / b.F;
-  b.collide = b.F > 1 && b.payload <= 10;  // defect D8
+  b.payload = frag_payload(c.cfg.node, sched[i0].msg_size, b.F);
+  b.collide = frag_collide(c.cfg.node, sched[i0].msg_size, b.F);  // defect D8 (rust layout)
   b.Fe = b.collide ? 1 : b.F;
   hipStream_t s = c.stream;
   const uint64_t wire = gs_wire_bytes(b.payload, c.cfg.muxer, c.cfg.signed_msgs);

@@ -26,10 +26,11 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GOSSIPSIM_LIB", os.path.join(HERE, "libgossipsim.so"))
-ABI_VERSION = 2
+ABI_VERSION = 3
 MESH_W = 16
 UNDELIVERED = np.uint64(0xFFFFFFFFFFFFFFFF)
 MUXERS = {"yamux": 0, "quic": 1, "mplex": 2}
+NODES = {"rust": 0, "go": 1, "nim": 2}  # GS_NODE_*: rust-test-node, go-test-node, nim gossipsub-queues
 STATUS = {0: "GS_OK", -1: "GS_EINVAL", -2: "GS_ENOMEM", -3: "GS_EDEVICE", -4: "GS_ESTATE",
           -5: "GS_ERANGE", -6: "GS_EUNSUPPORTED"}
 
@@ -44,7 +45,7 @@ class GsConfig(ctypes.Structure):
         ("heartbeat_ns", u64), ("backoff_ns", u64)] + [
         (n, u32) for n in ("flood_publish", "idontwant", "lazy_gossip", "self_log")] + [
         ("seed", u64), ("device", i32), ("batch", u32), ("history_gossip", u32), ("hb_phase_ns", u64)] + [
-        (n, u32) for n in ("churn_ppm", "churn_down", "churn_horizon")]
+        (n, u32) for n in ("churn_ppm", "churn_down", "churn_horizon", "node")]
 
 
 class GsPublish(ctypes.Structure):
@@ -71,6 +72,8 @@ class GsPartRecord(ctypes.Structure):
 # Every symbol include/gossipsim.h declares, with its ctypes signature.
 SIGNATURES = {
     "gs_config_default": (None, [P(GsConfig)]),
+    "gs_config_preset": (i32, [P(GsConfig), u32]),
+    "gs_write_node_log": (i32, [P(GsConfig), ctypes.c_char_p, P(GsPublish), u64, P(u64)]),
     "gs_config_from_env": (i32, [P(GsConfig), ctypes.c_char_p, ctypes.c_size_t]),
     "gs_wire_bytes": (u64, [u64, u32, u32]),
     "gs_topogen_links": (i32, [u32, u32, u32, u32, u32, u32, P(u64), P(u64)]),
@@ -179,8 +182,13 @@ class PeerConfig:
     """Knobs of env.rs:14-25 + gossipsub ConfigBuilder (main.rs:223-241)."""
 
     def __init__(self, **kw):
+        """Knobs over the defaults of `node` (rust | go | nim, gs_config_preset; default rust)."""
         self.c = GsConfig()
-        lib().gs_config_default(ctypes.byref(self.c))
+        node = kw.pop("node", 0)
+        node = NODES[node] if isinstance(node, str) else int(node)
+        rc = lib().gs_config_preset(ctypes.byref(self.c), node)
+        if rc:
+            raise GossipSimError(rc, "unknown node flavour %r" % node)
         for k, v in kw.items():
             if k == "muxer" and isinstance(v, str):
                 v = MUXERS[v]
@@ -335,8 +343,7 @@ class Simulator:
         """Arrival lines as `grep -rne 'milliseconds\\|BW' shadow.data/` prints them."""
         sched = res["schedule"]
         tc = np.ascontiguousarray(res["t_complete"], np.uint64)
-        rc = lib().gs_write_latency_log(path.encode(), sched, len(sched), self.peers,
-                                        _ptr(tc, u64), self.cfg.c.self_log)
+        rc = lib().gs_write_node_log(ctypes.byref(self.cfg.c), path.encode(), sched, len(sched), _ptr(tc, u64))
         if rc:
             raise GossipSimError(rc, "gs_write_latency_log failed")
 

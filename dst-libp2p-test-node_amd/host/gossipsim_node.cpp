@@ -107,9 +107,8 @@ int main(int argc, char** argv) {
           (unsigned long long)s.frag_deliveries, (unsigned long long)s.relaxations,
           (unsigned long long)pct(0.5), (unsigned long long)pct(0.95), (unsigned long long)pct(1.0));
   if (!latencies.empty() &&
-      (st = gs_write_latency_log(latencies.c_str(), sched.data(), n_msgs, cfg.peers, tc.data(),
-                                 cfg.self_log)) != GS_OK)
-    return die(ctx, st, "gs_write_latency_log");
+      (st = gs_write_node_log(&cfg, latencies.c_str(), sched.data(), n_msgs, tc.data())) != GS_OK)
+    return die(ctx, st, "gs_write_node_log");
   gs_destroy(ctx);
   return 0;
 }

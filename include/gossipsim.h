@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 2u
+#define GS_ABI_VERSION 3u
 
 /* Sentinel for "never delivered" in t_complete_ns. */
 #define GS_UNDELIVERED UINT64_MAX
@@ -49,6 +49,11 @@ enum {
 /* MUXER (rust-test-node/src/env.rs:48-50,69-71; nim adds mplex,
  * nim-test-node/gossipsub-queues/main.nim:433-441). */
 enum { GS_MUX_YAMUX = 0, GS_MUX_QUIC = 1, GS_MUX_MPLEX = 2 };
+
+/* Node flavour whose gossipsub settings, payload layout and log line the
+ * simulator reproduces (gs_config_preset): rust-test-node (the north star),
+ * go-test-node, nim-test-node/gossipsub-queues. */
+enum { GS_NODE_RUST = 0, GS_NODE_GO = 1, GS_NODE_NIM = 2 };
 
 /* Link-table mode for gs_topogen_links. */
 enum {
@@ -94,6 +99,7 @@ typedef struct gs_config {
     uint32_t churn_down;         /* outage length in heartbeats (default 10)        */
     uint32_t churn_horizon;      /* message lifetime in heartbeats under churn: no  */
                                  /* event past epoch(t_pub) + horizon (default 16)  */
+    uint32_t node;               /* GS_NODE_*: fragment layout + log line */
 } gs_config;
 
 /* One publish injection (replaces POST /publish, main.rs:50-56,152-168). */
@@ -136,11 +142,25 @@ typedef struct gs_stats {
 /* Defaults of the rust preset (main.rs:36-38,223-241; env.rs:38-67). */
 void gs_config_default(gs_config* cfg);
 
+/* Overwrite cfg with the defaults of one node flavour (gs_config_default +
+ * the node's own settings):
+ *  GS_NODE_RUST  rust-test-node/src/main.rs:223-241 (= gs_config_default);
+ *  GS_NODE_GO    go-test-node/main.go:153-175,374-385: Dout 2, IDONTWANT
+ *                threshold 1000 B, StrictNoSign (unsigned), local delivery of
+ *                own messages (self log), 8-byte stamp + msg_size/F payload;
+ *  GS_NODE_NIM   nim-test-node/gossipsub-queues/main.nim:242-332,396,429:
+ *                CONNECTTO dials (no +1), MAXCONNECTIONS 250, Dout = D/2,
+ *                anonymize (unsigned), SELFTRIGGER, 16-byte header, log line
+ *                keyed by msgId.
+ * Returns GS_EINVAL for an unknown node. */
+gs_status gs_config_preset(gs_config* cfg, uint32_t node);
+
 /* Read the reference's env surface into cfg: PEERS, CONNECTTO, FRAGMENTS,
  * MUXER (env.rs:38-67), MAXCONNECTIONS (nim main.nim:429), GOSSIPSUB_D,
  * _D_LOW, _D_HIGH, _D_LAZY, _D_OUT, _HEARTBEAT_MS, _PRUNE_BACKOFF_SEC,
  * _GOSSIP_FACTOR, _FLOOD_PUBLISH (nim main.nim:252-284), SELFTRIGGER, plus
- * GS_SEED / GS_BATCH / GS_DEVICE. Validation mirrors env.rs:69-75:
+ * GS_SEED / GS_BATCH / GS_DEVICE. GS_NODE=rust|go|nim first applies that
+ * node's preset (gs_config_preset). Validation mirrors env.rs:69-75:
  * unknown muxer and CONNECTTO >= PEERS are errors (message in err). */
 gs_status gs_config_from_env(gs_config* cfg, char* err, size_t err_len);
 
@@ -166,6 +186,14 @@ gs_status gs_schedule_runsh(uint32_t n_msgs, uint32_t peers, uint32_t publisher_
 gs_status gs_write_latency_log(const char* path, const gs_publish* sched, uint64_t n_msgs,
                                uint32_t peers, const uint64_t* t_complete_ns,
                                uint32_t self_log);
+
+/* The same arrival log for the node flavour of cfg (peers, self_log, node,
+ * seed): rust and go print "<tx_time> milliseconds: <ms>" (main.rs:93,
+ * go-test-node/main.go:49); nim prints "<msgId> milliseconds: <ms>"
+ * (nim gossipsub-queues/main.nim:150) with msgId a 63-bit id drawn from
+ * (seed, publisher, t_pub) in place of the node's rand(high(int64)). */
+gs_status gs_write_node_log(const gs_config* cfg, const char* path, const gs_publish* sched,
+                            uint64_t n_msgs, const uint64_t* t_complete_ns);
 
 /* ---- context lifecycle (replaces SwarmBuilder + build_behaviour, main.rs:391-440) ---- */
 

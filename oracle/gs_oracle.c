@@ -632,9 +632,30 @@ static int sched_gossip(const or_params* p, const uint64_t* row_ptr, const uint3
     return 0;
 }
 
+/* Fragment layout per node flavour: the data field's size,
+ * whether the node's own publish code fails (the run is rejected), and whether
+ * all fragments are byte-identical (one msg-id, defect D8).
+ *  rust publish_new_message (main.rs:109-121): msg_size/F bytes, i64 stamp in
+ *    [0..8) (panics below 8 B), byte 10 = chunk only if the buffer is longer
+ *    than 10 B;
+ *  go publishNewMessage (go-test-node/main.go:63-74): 8-byte stamp + msg_size/F
+ *    zero bytes, payload[10] = chunk (index out of range when msg_size/F <= 2);
+ *  nim publishNewMessage (nim-test-node/gossipsub-queues/main.nim:158-175):
+ *    16-byte header (stamp, random msgId) + msg_size div F - 16 bytes,
+ *    nowBytes[16] = chunk (IndexDefect when msg_size div F <= 16). */
+static uint64_t frag_payload(const or_params* p, uint64_t msg_size) {
+    return msg_size / p->fragments + (p->node == 1 ? 8 : 0);
+}
+static int frag_invalid(const or_params* p, uint64_t msg_size) {
+    uint64_t q = msg_size / p->fragments;
+    return p->node == 1 ? q <= 2 : p->node == 2 ? q <= 16 : q < 8;
+}
+static int frag_collide(const or_params* p, uint64_t msg_size) {
+    return p->node == 0 && p->fragments > 1 && msg_size / p->fragments <= 10;
+}
+
 /* One publish -> receive -> forward -> reassemble pass per message:
- *  publish_new_message (main.rs:101-143): F fragments of msg_size/F bytes,
- *    byte 10 = chunk (fragments distinct only if payload > 10: defect D8),
+ *  publish_new_message (main.rs:101-143): F fragments (layout above),
  *    flood-published (main.rs:227) to every connection in ascending id,
  *    fragment after fragment, through the publisher's uplink FIFO.
  *  first receipt of (peer, fragment) wins by key (time, hops, src); it is
@@ -673,9 +694,9 @@ static int run_impl(const or_params* p, const uint64_t* row_ptr, const uint32_t*
     if (!best || !fin || !busy || !su || !sd || !gsel || !gtg || !ftg) { rc = -2; goto out; }
     for (uint64_t mi = 0; mi < n_msgs; mi++) {
         uint32_t pub = sched_pub[mi];
-        uint64_t payload = sched_size[mi] / F;
-        if (pub >= N || payload < 8) { rc = -1; goto out; } /* main.rs:110 panics below 8 B */
-        int collide = (F > 1 && payload <= 10);             /* defect D8 */
+        uint64_t payload = frag_payload(p, sched_size[mi]);
+        if (pub >= N || frag_invalid(p, sched_size[mi])) { rc = -1; goto out; } /* the node's publish fails */
+        int collide = frag_collide(p, sched_size[mi]);                      /* defect D8 */
         uint32_t Fe = collide ? 1 : F;
         uint64_t wire = or_wire_bytes(payload, p->muxer, p->signed_msgs);
         const uint64_t tp = sched_t[mi];

@@ -30,6 +30,7 @@ typedef struct or_params {
     uint32_t history_gossip;
     uint64_t hb_phase_ns;
     uint32_t churn_ppm, churn_down, churn_horizon; /* DESIGN.md §2.8; 0 ppm = no churn */
+    uint32_t node; /* payload layout of the node flavour: 0 rust, 1 go, 2 nim */
 } or_params;
 
 typedef struct or_stats {

@@ -30,7 +30,7 @@ class OrParams(ctypes.Structure):
         ("heartbeat_ns", ctypes.c_uint64), ("backoff_ns", ctypes.c_uint64)] + [
         (n, ctypes.c_uint32) for n in ("flood_publish", "idontwant", "lazy_gossip", "self_log")] + [
         ("seed", ctypes.c_uint64), ("history_gossip", ctypes.c_uint32), ("hb_phase_ns", ctypes.c_uint64)] + [
-        (n, ctypes.c_uint32) for n in ("churn_ppm", "churn_down", "churn_horizon")]
+        (n, ctypes.c_uint32) for n in ("churn_ppm", "churn_down", "churn_horizon", "node")]
 
 
 class OrStats(ctypes.Structure):
@@ -90,9 +90,26 @@ def params(**kw):
              muxer=0, signed_msgs=1, d=6, d_lo=4, d_hi=8, d_lazy=6, d_out=3,
              gossip_factor_milli=250, heartbeat_ns=1_000_000_000, backoff_ns=60_000_000_000,
              flood_publish=1, idontwant=0, lazy_gossip=0, self_log=0, seed=1, history_gossip=3,
-             hb_phase_ns=0, churn_ppm=0, churn_down=10, churn_horizon=16)
+             hb_phase_ns=0, churn_ppm=0, churn_down=10, churn_horizon=16, node=0)
     d.update(kw)
     return OrParams(**d)
+
+
+def params_for(node, **kw):
+    """The oracle's restatement of each test node's own settings:
+    go-test-node/main.go:153-175,374-385 (Dout 2, IDONTWANT 1000 B, StrictNoSign,
+    own publish delivered locally) and nim gossipsub-queues/main.nim:242-332,
+    396, 429 (CONNECTTO dials, MAXCONNECTIONS 250, Dout = D div 2, Dlazy = D,
+    anonymize, SELFTRIGGER)."""
+    node = {"rust": 0, "go": 1, "nim": 2}.get(node, node)
+    d = dict(node=node)
+    if node == 1:
+        d.update(d_out=2, idontwant=1000, signed_msgs=0, self_log=1)
+    elif node == 2:
+        D = kw.get("d", 6)
+        d.update(dial_extra=0, max_connections=250, d_out=D // 2, d_lazy=D, signed_msgs=0, self_log=1)
+    d.update(kw)
+    return params(**d)
 
 
 def wire_bytes(payload, muxer=0, signed=1):

@@ -126,6 +126,21 @@ def test_lazy_gossip_default_heartbeat():
     compare(p, 5, (50, 150, 40, 130), _sched(30, 3000), batch=16)
 
 
+@pytest.mark.parametrize("node", ["go", "nim"])
+def test_node_presets(node):
+    """go-test-node / nim gossipsub-queues settings and fragment layouts
+    (gs_config_preset; go's IDONTWANT threshold puts 15 KB messages on the
+    IDONTWANT path) bit-exact against the oracle, incl. the smallest valid
+    fragments and the node's own publish failure."""
+    p = oracle.params_for(node, peers=800, seed=61, fragments=3)
+    compare(p, 5, (50, 150, 40, 130), _sched(10, 800), batch=4)
+    small = 9 if node == "go" else 51  # msg_size / F = 3 (go) or 17 (nim): the first valid size
+    compare(p, 5, (50, 150, 40, 130), _sched(6, 800, size=small), batch=3)
+    sim, _ = gpu_sim(p, 5, (50, 150, 40, 130))
+    with pytest.raises(gossipsim.GossipSimError, match="GS_EINVAL"):
+        sim.run(_sched(1, 800, size=small - 3))
+
+
 def test_fragment_collision_defect_d8():
     p = oracle.params(peers=100, fragments=4)
     sim, res = compare(p, 1, (50, 50, 50, 50), _sched(2, 100, size=40))

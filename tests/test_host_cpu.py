@@ -143,6 +143,72 @@ def test_config_from_env_defaults_and_errors(monkeypatch):
         gossipsim.PeerConfig.from_env()
 
 
+@pytest.mark.parametrize("node", ["rust", "go", "nim"])
+def test_node_presets_match_oracle_restatement(node):
+    """gs_config_preset == the oracle's own reading of each node's settings."""
+    c = gossipsim.PeerConfig(node=node)
+    p = oracle.params_for(node)
+    for name, _ in oracle.OrParams._fields_:
+        assert getattr(c, name) == getattr(p, name), name
+
+
+def test_gs_node_env_selects_preset(monkeypatch):
+    for k in ("PEERS", "CONNECTTO", "MAXCONNECTIONS", "SELFTRIGGER", "MUXER", "GOSSIPSUB_D_OUT"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("GS_NODE", "nim")
+    c = gossipsim.PeerConfig.from_env()
+    assert (c.node, c.dial_extra, c.max_connections, c.d_out, c.self_log, c.signed_msgs) == (2, 0, 250, 3, 1, 0)
+    monkeypatch.setenv("MAXCONNECTIONS", "40")  # env still overrides the preset (main.nim:429)
+    monkeypatch.setenv("SELFTRIGGER", "false")  # main.nim:245
+    c = gossipsim.PeerConfig.from_env()
+    assert (c.max_connections, c.self_log) == (40, 0)
+    monkeypatch.setenv("GS_NODE", "GO")
+    c = gossipsim.PeerConfig.from_env()
+    assert (c.node, c.d_out, c.idontwant, c.signed_msgs) == (1, 2, 1000, 0)
+    monkeypatch.setenv("GS_NODE", "java")
+    with pytest.raises(gossipsim.GossipSimError, match="Unknown node type: java"):
+        gossipsim.PeerConfig.from_env()
+
+
+def _node_log(tmp_path, node, self_log):
+    cfg = gossipsim.PeerConfig(node=node, peers=4, self_log=self_log, seed=9)
+    tx = [1_700_000_000_000_000_000, 1_700_000_001_000_000_000]
+    sched = (gossipsim.GsPublish * 2)(gossipsim.GsPublish(tx[0], 0, 15000), gossipsim.GsPublish(tx[1], 2, 15000))
+    tc = np.array([[tx[0], tx[0] + 120_400_000, gossipsim.UNDELIVERED, tx[0] + 95_000_001],
+                   [tx[1] + 310_999_999, tx[1] + 5_000_000, tx[1], tx[1] + 230_000_000]], np.uint64)
+    out = str(tmp_path / ("latencies_" + node))
+    rc = gossipsim.lib().gs_write_node_log(ctypes.byref(cfg.c), out.encode(), sched, 2,
+                                           tc.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)))
+    assert rc == 0
+    return [l.split(":", 2) for l in open(out).read().splitlines()], tx
+
+
+def test_node_log_lines(tmp_path):
+    rows, tx = _node_log(tmp_path, "rust", 0)
+    assert [r[2] for r in rows] == ["%d milliseconds: 310" % tx[1], "%d milliseconds: 120" % tx[0],
+                                    "%d milliseconds: 5" % tx[1], "%d milliseconds: 95" % tx[0],
+                                    "%d milliseconds: 230" % tx[1]]
+    rows_go, _ = _node_log(tmp_path, "go", 1)  # go: same line, own publish delivered locally
+    assert len(rows_go) == len(rows) + 2
+    nim, _ = _node_log(tmp_path, "nim", 1)     # nim: "<msgId> milliseconds: <ms>" (main.nim:150)
+    ids = {}
+    for path, _, text in nim:
+        mid, rest = text.split(" ", 1)
+        assert int(mid) < 2 ** 63 and int(mid) not in tx
+        ids.setdefault(rest.split()[-1], set()).add(mid)
+    assert len({m for s in ids.values() for m in s}) == 2  # one id per message
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_SHADOW) or not shutil.which("awk"),
+                    reason="reference awk scripts only in the build container")
+def test_nim_log_round_trips_through_reference_awk(tmp_path):
+    _node_log(tmp_path, "nim", 1)
+    got = subprocess.check_output(["awk", "-f", os.path.join(REF_SHADOW, "summary_latency.awk"),
+                                   str(tmp_path / "latencies_nim")]).decode()
+    assert re.search(r"Total Messages Published :\s+2\b", got) and re.search(r"Total Nodes :\s+3\b", got)
+    assert re.search(r"MAX :\s+310\b", got)
+
+
 def test_shard_messages_partition():
     """Message sharding used by bench.py: disjoint, covering, publisher rule of run.sh."""
     N, B, world, steps = 1000, 8, 4, 3

@@ -281,6 +281,22 @@ def test_fragment_collision_defect_d8():
         oracle.simulate(p, 1, (50, 50, 50, 50), sched=(np.array([T0], np.uint64), np.array([3]), np.array([28])))
 
 
+@pytest.mark.parametrize("node,bad,good", [("rust", 28, 40), ("go", 8, 12), ("nim", 64, 68)])
+def test_fragment_layout_per_node(node, bad, good):
+    """F=4: rust rejects payloads under 8 B and merges fragments of <= 10 B
+    (D8); go's 8-byte stamp + msg_size/F layout fails only below 3 B of body
+    (payload[10], main.go:70-74); nim's 16-byte header needs msg_size/F >= 17
+    (nowBytes[16], main.nim:165-175). Layouts that accept a size never merge."""
+    p = oracle.params_for(node, peers=60, fragments=4)
+    one = lambda size: oracle.simulate(p, 1, (50, 50, 50, 50),
+                                       sched=(np.array([T0], np.uint64), np.array([3]), np.array([size])))
+    with pytest.raises(ValueError):
+        one(bad)
+    r = one(good)
+    assert r["stats"]["deliveries"] == (0 if node == "rust" else 59)  # the publisher is not counted
+    assert r["stats"]["frag_deliveries"] == (59 if node == "rust" else 4 * 59)
+
+
 def test_stats_identities():
     p, r, _ = _sim(N=400, fragments=2)
     st = r["stats"]
