@@ -221,6 +221,8 @@ extern "C" gs_status gs_reset_stats(gs_ctx* ctx) {
   GS_API_BEGIN(ctx)
   GS_HIP(hipSetDevice(ctx->cfg.device));
   GS_HIP(hipMemsetAsync(ctx->d_counters.p, 0, C_COUNT * 8, ctx->stream));
+  if (ctx->traffic)
+    GS_HIP(hipMemsetAsync(ctx->d_traffic.p, 0, (size_t)ctx->cfg.peers * GS_TRAFFIC_COLS * 8, ctx->stream));
   GS_HIP(hipStreamSynchronize(ctx->stream));
   memset(&ctx->stats, 0, sizeof(ctx->stats));
   GS_API_END(ctx)
@@ -230,6 +232,29 @@ extern "C" gs_status gs_set_timing(gs_ctx* ctx, uint32_t enable) {
   if (!ctx) return GS_EINVAL;
   ctx->timing = enable != 0;
   return GS_OK;
+}
+
+extern "C" gs_status gs_set_traffic(gs_ctx* ctx, uint32_t enable) {
+  GS_API_BEGIN(ctx)
+  GS_HIP(hipSetDevice(ctx->cfg.device));
+  ctx->traffic = enable != 0;
+  if (ctx->traffic) {
+    ctx->d_traffic.alloc((size_t)ctx->cfg.peers * GS_TRAFFIC_COLS);
+    GS_HIP(hipMemsetAsync(ctx->d_traffic.p, 0, (size_t)ctx->cfg.peers * GS_TRAFFIC_COLS * 8, ctx->stream));
+    GS_HIP(hipStreamSynchronize(ctx->stream));
+  }
+  GS_API_END(ctx)
+}
+
+extern "C" gs_status gs_get_traffic(gs_ctx* ctx, uint64_t* traffic) {
+  GS_API_BEGIN(ctx)
+  if (!traffic) ctx->fail(GS_EINVAL, "null traffic array");
+  if (!ctx->traffic) ctx->fail(GS_ESTATE, "gs_set_traffic(ctx, 1) first");
+  GS_HIP(hipSetDevice(ctx->cfg.device));
+  GS_HIP(hipMemcpyAsync(traffic, ctx->d_traffic.p, (size_t)ctx->cfg.peers * GS_TRAFFIC_COLS * 8,
+                        hipMemcpyDeviceToHost, ctx->stream));
+  GS_HIP(hipStreamSynchronize(ctx->stream));
+  GS_API_END(ctx)
 }
 
 // ---- peer-partitioned mode (gs_part.h) ----

@@ -67,6 +67,8 @@ struct Ctx {
   std::string last_error;
   hipStream_t stream = nullptr;
   bool timing = false;
+  bool traffic = false;        // gs_set_traffic: per-peer send/receive counters
+  DevBuf<uint64_t> d_traffic;  // [N][GS_TRAFFIC_COLS]
 
   // links
   uint32_t S = 0;

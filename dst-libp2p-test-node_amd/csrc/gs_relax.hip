@@ -204,6 +204,95 @@ __global__ __launch_bounds__(TB) void k_transpose(const uint64_t* __restrict__ t
   }
 }
 
+struct TrafficArgs {
+  const uint64_t* keys;
+  const uint32_t* mesh;
+  const uint32_t* pub;
+  const uint8_t* stage;
+  const uint32_t* tables;  // lat[S*S] | ...
+  const uint64_t* row;
+  const uint32_t* col;
+  uint64_t* traffic;       // [N][GS_TRAFFIC_COLS]
+  uint64_t W, pk, hdr;     // wire bytes, packets, header bytes of one fragment send
+  uint32_t N, L, FP, Fe, S, sb, tshift, idw, flood;
+};
+
+// Per-peer traffic of a finished batch (gs_set_traffic), from the final keys:
+// the first receipt of (m, f) at u != publisher sent one copy to each of
+// mesh(u) \ {src, publisher} minus the IDONTWANT skips — exactly the forward
+// sends the relaxation counted (R). One wave per row u; lane k < deg ends with
+// the number of copies u sent to its mesh entry k. The sender's tx columns are
+// written by its own wave only; rx columns take atomics.
+template <int FP>
+__global__ __launch_bounds__(TB) void k_traffic(TrafficArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t nw = gridDim.x * (TB / 64);
+  const uint64_t smask = (1ull << a.sb) - 1;
+  for (uint32_t u = (blockIdx.x * TB + threadIdx.x) >> 6; u < a.N; u += nw) {
+    const uint32_t e = lane < (int)MESH_W ? a.mesh[(size_t)u * MESH_W + lane] : EMPTY;
+    const uint32_t deg = (uint32_t)__popcll(__ballot(e != EMPTY));
+    const uint32_t su = a.stage[u];
+    uint32_t cnt = 0;
+    for (uint32_t i0 = 0; i0 < a.L; i0 += 64) {
+      const uint32_t i = i0 + lane;
+      const bool in = i < a.L && (i & (FP - 1)) < a.Fe;
+      const uint64_t key = in ? a.keys[(size_t)u * a.L + i] : INF64;
+      const uint32_t pm = in ? a.pub[i / FP] : EMPTY;
+      const bool got = key != INF64 && pm != u;
+      const uint32_t src = (uint32_t)(key & smask);
+      const uint64_t t = key >> a.tshift;
+      for (uint32_t k = 0; k < deg; k++) {  // wave-uniform
+        const uint32_t y = __builtin_amdgcn_readlane(e, k), w = y & 0xFFFFFFu;
+        bool send = got && w != src && w != pm;
+        if (send && a.idw) {  // go's IDONTWANT (main.go:165): w announced it before u's receipt
+          const uint64_t kw = a.keys[(size_t)w * a.L + i];
+          if (kw != INF64 && (kw >> a.tshift) + a.tables[(y >> STAGE_SHIFT) * a.S + su] <= t) send = false;
+        }
+        const uint32_t c = (uint32_t)__popcll(__ballot(send));
+        cnt += lane == (int)k ? c : 0u;
+      }
+    }
+    const uint64_t tot = wave_sum((uint64_t)cnt);
+    if (lane == 0 && tot) {
+      uint64_t* r = a.traffic + (size_t)u * GS_TRAFFIC_COLS;
+      r[GS_TR_TX_BYTES] += tot * a.W;
+      r[GS_TR_TX_PKTS] += tot * a.pk;
+      r[GS_TR_TX_HDR] += tot * a.hdr;
+    }
+    if (cnt) {
+      uint64_t* r = a.traffic + (size_t)(e & 0xFFFFFFu) * GS_TRAFFIC_COLS;
+      atomicAdd((unsigned long long*)&r[GS_TR_RX_BYTES], (unsigned long long)cnt * a.W);
+      atomicAdd((unsigned long long*)&r[GS_TR_RX_PKTS], (unsigned long long)cnt * a.pk);
+      atomicAdd((unsigned long long*)&r[GS_TR_RX_HDR], (unsigned long long)cnt * a.hdr);
+    }
+  }
+}
+
+// The publishers' own sends (main.rs:123 with flood_publish, main.rs:227):
+// every fragment to every connection (or to the mesh without flood publish).
+// One block per message; runs after k_traffic (same stream), so the atomics
+// on the publisher's tx do not race its row's plain updates.
+__global__ __launch_bounds__(TB) void k_traffic_pub(TrafficArgs a) {
+  const uint32_t p = a.pub[blockIdx.x];
+  uint32_t deg = 0;
+  const uint32_t* tg;
+  if (a.flood) { deg = (uint32_t)(a.row[p + 1] - a.row[p]); tg = a.col + a.row[p]; }
+  else { tg = a.mesh + (size_t)p * MESH_W; while (deg < MESH_W && tg[deg] != EMPTY) deg++; }
+  if (threadIdx.x == 0) {
+    uint64_t* r = a.traffic + (size_t)p * GS_TRAFFIC_COLS;
+    const unsigned long long n = (unsigned long long)a.Fe * deg;
+    atomicAdd((unsigned long long*)&r[GS_TR_TX_BYTES], n * a.W);
+    atomicAdd((unsigned long long*)&r[GS_TR_TX_PKTS], n * a.pk);
+    atomicAdd((unsigned long long*)&r[GS_TR_TX_HDR], n * a.hdr);
+  }
+  for (uint32_t j = threadIdx.x; j < deg; j += TB) {
+    uint64_t* r = a.traffic + (size_t)(tg[j] & 0xFFFFFFu) * GS_TRAFFIC_COLS;
+    atomicAdd((unsigned long long*)&r[GS_TR_RX_BYTES], (unsigned long long)a.Fe * a.W);
+    atomicAdd((unsigned long long*)&r[GS_TR_RX_PKTS], (unsigned long long)a.Fe * a.pk);
+    atomicAdd((unsigned long long*)&r[GS_TR_RX_HDR], (unsigned long long)a.Fe * a.hdr);
+  }
+}
+
 uint32_t pow2_at_least(uint32_t x) { uint32_t p = 1; while (p < x) p <<= 1; return p; }
 
 }  // namespace
@@ -328,6 +417,29 @@ static void launch_complete(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, co
   }
 }
 
+// Per-peer traffic of the batch just finished (keys final, before the next reset).
+static void launch_traffic(Ctx& c, const Batch& b) {
+  TrafficArgs ta{};
+  ta.keys = c.d_keys.p; ta.mesh = c.d_mesh.p; ta.pub = c.d_pub.p; ta.stage = c.d_stage.p;
+  ta.tables = c.d_tables.p; ta.row = c.d_row.p; ta.col = c.d_col.p; ta.traffic = c.d_traffic.p;
+  ta.W = gs_wire_bytes(b.payload, c.cfg.muxer, c.cfg.signed_msgs);
+  gs_wire_packets(b.payload, c.cfg.muxer, c.cfg.signed_msgs, &ta.pk, &ta.hdr);
+  ta.N = c.cfg.peers; ta.L = b.L; ta.FP = b.FP; ta.Fe = b.Fe; ta.S = c.S; ta.sb = b.sb; ta.tshift = b.tshift;
+  ta.idw = (c.cfg.idontwant && b.payload >= c.cfg.idontwant) ? 1 : 0;
+  ta.flood = c.cfg.flood_publish;
+  const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(((uint64_t)ta.N + 3) / 4,
+                                                                           (uint64_t)c.num_cus * 8));
+  switch (b.FP) {
+    case 1: k_traffic<1><<<grid, TB, 0, c.stream>>>(ta); break;
+    case 2: k_traffic<2><<<grid, TB, 0, c.stream>>>(ta); break;
+    case 4: k_traffic<4><<<grid, TB, 0, c.stream>>>(ta); break;
+    case 8: k_traffic<8><<<grid, TB, 0, c.stream>>>(ta); break;
+    default: k_traffic<16><<<grid, TB, 0, c.stream>>>(ta); break;
+  }
+  k_traffic_pub<<<b.B, TB, 0, c.stream>>>(ta);
+  GS_HIP(hipGetLastError());
+}
+
 // Read the device counters into ctx->stats (and raise the device error word).
 static void collect_stats(Ctx& c) {
   hipStream_t s = c.stream;
@@ -430,6 +542,8 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
   // target's key, lazy gossip pushes from heartbeats): those stay on the push path
   const bool idw_any = c.cfg.idontwant != 0;
   const bool churn = c.cfg.churn_ppm != 0;  // per-epoch mesh lookups live on the push path
+  if (c.traffic && (gossip || churn))
+    c.fail(GS_EUNSUPPORTED, "per-peer traffic covers eager forwarding: turn off lazy gossip and churn");
   const bool pull = (variant & 32) && !gossip && !idw_any && !churn;
   // pull rows live in registers: cap the batch at PULL_LMAX / FP messages
   const uint32_t Bcap = pull ? std::max<uint32_t>(1, std::min<uint32_t>(Bmax, PULL_LMAX / FP)) : Bmax;
@@ -543,6 +657,7 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     if (pull && b.delta >= pull_grain(b.tshift)) {
       run_pull_batch(c, b, ev, n_ev, dev_cus);
       c.stats.messages += B;
+      if (c.traffic) launch_traffic(c, b);
       launch_complete(c, b, 0, N, sink, i0);
       i0 = i1;
       continue;
@@ -617,6 +732,7 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       if (c.h_pinned[launch % 3] == INF64) break;
     }
     c.stats.relax_launches += launch;
+    if (c.traffic) launch_traffic(c, b);
     launch_complete(c, b, 0, N, sink, i0);
     c.stats.messages += B;
     i0 = i1;

@@ -76,6 +76,10 @@ SIGNATURES = {
     "gs_write_node_log": (i32, [P(GsConfig), ctypes.c_char_p, P(GsPublish), u64, P(u64)]),
     "gs_config_from_env": (i32, [P(GsConfig), ctypes.c_char_p, ctypes.c_size_t]),
     "gs_wire_bytes": (u64, [u64, u32, u32]),
+    "gs_wire_packets": (None, [u64, u32, u32, P(u64), P(u64)]),
+    "gs_write_shadow_heartbeat": (i32, [ctypes.c_char_p, u32, P(u64), u64]),
+    "gs_set_traffic": (i32, [ctypes.c_void_p, u32]),
+    "gs_get_traffic": (i32, [ctypes.c_void_p, P(u64)]),
     "gs_topogen_links": (i32, [u32, u32, u32, u32, u32, u32, P(u64), P(u64)]),
     "gs_schedule_runsh": (i32, [u32, u32, u32, u32, u64, u64, u32, P(GsPublish)]),
     "gs_write_latency_log": (i32, [ctypes.c_char_p, P(GsPublish), u64, u32, P(u64), u32]),
@@ -133,6 +137,26 @@ def _ptr(a, ct):
 def wire_bytes(payload, muxer="yamux", signed=True):
     return int(lib().gs_wire_bytes(payload, MUXERS[muxer] if isinstance(muxer, str) else muxer,
                                    1 if signed else 0))
+
+
+def wire_packets(payload, muxer="yamux", signed=True):
+    """-> (packets, header bytes) of one fragment send (the model of wire_bytes)."""
+    pk, hd = u64(), u64()
+    lib().gs_wire_packets(payload, MUXERS[muxer] if isinstance(muxer, str) else muxer, 1 if signed else 0,
+                          ctypes.byref(pk), ctypes.byref(hd))
+    return pk.value, hd.value
+
+
+TRAFFIC_COLS = ("tx_bytes", "rx_bytes", "tx_packets", "rx_packets", "tx_header_bytes", "rx_header_bytes")
+
+
+def write_shadow_heartbeat(path, traffic, sim_seconds=900):
+    """Per-peer traffic [N, 6] as Shadow tracker "[node]" lines (shadow/summary_shadowlog.awk);
+    sim_seconds defaults to topogen's 15-minute stop time (shadow/topogen.py:82)."""
+    tr = np.ascontiguousarray(traffic, np.uint64)
+    rc = lib().gs_write_shadow_heartbeat(path.encode(), tr.shape[0], _ptr(tr, u64), sim_seconds)
+    if rc:
+        raise GossipSimError(rc, "gs_write_shadow_heartbeat failed")
 
 
 def topogen_links(stages=1, min_bw=50, max_bw=50, min_lat=100, max_lat=100, shortest=False):
@@ -338,6 +362,16 @@ class Simulator:
 
     def set_timing(self, on=True):
         self._check(lib().gs_set_timing(self.ctx, 1 if on else 0))
+
+    def set_traffic(self, on=True):
+        """Per-peer send/receive counters of later runs (zeroed now)."""
+        self._check(lib().gs_set_traffic(self.ctx, 1 if on else 0))
+
+    def traffic(self):
+        """-> uint64 [N, 6] in TRAFFIC_COLS order."""
+        tr = np.zeros((self.peers, len(TRAFFIC_COLS)), np.uint64)
+        self._check(lib().gs_get_traffic(self.ctx, _ptr(tr, u64)))
+        return tr
 
     def write_latency_log(self, path, res):
         """Arrival lines as `grep -rne 'milliseconds\\|BW' shadow.data/` prints them."""

@@ -195,6 +195,24 @@ gs_status gs_write_latency_log(const char* path, const gs_publish* sched, uint64
 gs_status gs_write_node_log(const gs_config* cfg, const char* path, const gs_publish* sched,
                             uint64_t n_msgs, const uint64_t* t_complete_ns);
 
+/* Packets and header bytes of one fragment send in the same model as
+ * gs_wire_bytes: TCP/IPv4 segments of <= 1460 B carrying 40 B of headers each,
+ * or QUIC packets of <= 1415 B carrying 65 B each. */
+void gs_wire_packets(uint64_t payload, uint32_t muxer, uint32_t signed_msgs, uint64_t* packets,
+                     uint64_t* header_bytes);
+
+/* Columns of a per-peer traffic row (gs_get_traffic). */
+enum { GS_TR_TX_BYTES = 0, GS_TR_RX_BYTES = 1, GS_TR_TX_PKTS = 2, GS_TR_RX_PKTS = 3,
+       GS_TR_TX_HDR = 4, GS_TR_RX_HDR = 5, GS_TRAFFIC_COLS = 6 };
+
+/* Shadow's per-host heartbeat counters for the same runs, one "[node]" line
+ * per peer as Shadow's tracker logs them (recv/send bytes, then inbound and
+ * outbound localhost / remote packet, header and payload counters), so that
+ * shadow/summary_shadowlog.awk:12-143 summarises them unchanged. traffic is
+ * [peers][GS_TRAFFIC_COLS]. Host names are pod-<id> (topogen.py:118). */
+gs_status gs_write_shadow_heartbeat(const char* path, uint32_t peers, const uint64_t* traffic,
+                                    uint64_t sim_seconds);
+
 /* ---- context lifecycle (replaces SwarmBuilder + build_behaviour, main.rs:391-440) ---- */
 
 gs_status gs_create(const gs_config* cfg, struct gs_ctx** out);
@@ -243,6 +261,18 @@ gs_status gs_reset_stats(struct gs_ctx* ctx);
 
 /* 1: record HIP events around every relaxation launch and around gs_run. */
 gs_status gs_set_timing(struct gs_ctx* ctx, uint32_t enable);
+
+/* 1: account every data send of gs_run per peer (the byte counters Shadow's
+ * tracker keeps per host, summary_shadowlog.awk): a flood-publish or forward
+ * send of a fragment adds its wire bytes / packets / header bytes to the
+ * sender's tx and the receiver's rx columns. Counted after each batch from the
+ * final keys (one extra pass over them), so it is off by default. Covers
+ * eager forwarding incl. IDONTWANT; gs_run returns GS_EUNSUPPORTED with lazy
+ * gossip or churn while it is on. Enabling zeroes the counters, as does
+ * gs_reset_stats. */
+gs_status gs_set_traffic(struct gs_ctx* ctx, uint32_t enable);
+/* Copy the per-peer counters out: traffic[peers][GS_TRAFFIC_COLS]. */
+gs_status gs_get_traffic(struct gs_ctx* ctx, uint64_t* traffic);
 
 /* ---- peer-partitioned mode -------------------------
  * Context `part` of `parts` owns the keys of peers [part*N/parts,

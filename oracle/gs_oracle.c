@@ -68,6 +68,16 @@ uint64_t or_wire_bytes(uint64_t payload, uint32_t muxer, uint32_t signed_msgs) {
     return b + cdiv(b, 1460) * 40;
 }
 
+/* The packets of that last layer and their header bytes (the counters Shadow's
+ * tracker keeps per host, shadow/summary_shadowlog.awk:21-63). */
+void or_wire_packets(uint64_t payload, uint32_t muxer, uint32_t signed_msgs, uint64_t* packets,
+                     uint64_t* header_bytes) {
+    uint64_t w = or_wire_bytes(payload, muxer, signed_msgs), per = muxer == 1 ? 1415 + 65 : 1460 + 40;
+    uint64_t n = cdiv(w, per); /* every packet but the last is full: ceil(wire / full packet) */
+    *packets = n;
+    *header_bytes = n * (muxer == 1 ? 65 : 40);
+}
+
 /* ---------------------------------------------------------- link model ---- */
 /* shadow/topogen.py:39-71: stage bandwidth ceil(i*bj + bl) Mbit (49-51),
  * self-loop max((S-i)*lj, ll) ms (55), edge i<j min(ceil((S-j)*lj+ll), lh) ms
@@ -672,7 +682,7 @@ static int run_impl(const or_params* p, const uint64_t* row_ptr, const uint32_t*
                     const uint8_t* stage, uint32_t S, const uint64_t* lat_ns, const uint64_t* bw_up,
                     const uint64_t* bw_dn, const uint64_t* sched_t, const uint32_t* sched_pub,
                     const uint32_t* sched_size, uint64_t n_msgs, uint64_t* t_complete, uint8_t* hops,
-                    or_stats* st) {
+                    or_stats* st, uint64_t* tr) {
     uint32_t N = p->peers, F = p->fragments;
     if (F == 0 || F > 16) return -6;
     uint32_t sb = bits_for(N), tshift = sb + HOP_BITS;
@@ -698,7 +708,11 @@ static int run_impl(const or_params* p, const uint64_t* row_ptr, const uint32_t*
         if (pub >= N || frag_invalid(p, sched_size[mi])) { rc = -1; goto out; } /* the node's publish fails */
         int collide = frag_collide(p, sched_size[mi]);                      /* defect D8 */
         uint32_t Fe = collide ? 1 : F;
-        uint64_t wire = or_wire_bytes(payload, p->muxer, p->signed_msgs);
+        uint64_t wire = or_wire_bytes(payload, p->muxer, p->signed_msgs), wpk = 0, whd = 0;
+        or_wire_packets(payload, p->muxer, p->signed_msgs, &wpk, &whd);
+        /* per-peer traffic: a send adds to the sender's tx, an arrival to the receiver's rx */
+#define TR_SEND(x) if (tr) { tr[(size_t)(x) * 6 + 0] += wire; tr[(size_t)(x) * 6 + 2] += wpk; tr[(size_t)(x) * 6 + 4] += whd; }
+#define TR_RECV(x) if (tr) { tr[(size_t)(x) * 6 + 1] += wire; tr[(size_t)(x) * 6 + 3] += wpk; tr[(size_t)(x) * 6 + 5] += whd; }
         const uint64_t tp = sched_t[mi];
         mesh_src msg_ms = *ms0;
         msg_ms.h_cap = epoch_at(p, tp) + p->churn_horizon;
@@ -742,10 +756,12 @@ static int run_impl(const or_params* p, const uint64_t* row_ptr, const uint32_t*
                 if (arr > tmax) { rc = -5; goto out; }
                 uint64_t key = (arr << tshift) | (1ull << sb) | pub;
                 st->relaxations++;
+                TR_SEND(pub);
                 if (ms->snap_off) {  /* lost: past the lifetime, or w offline at the arrival */
                     const int64_t sl = slot_of(ms, epoch_at(p, tp + arr));
                     if (sl < 0 || offline_at(ms, N, sl, w)) continue;
                 }
+                TR_RECV(w);
                 if (key < best[(size_t)w * F + f]) best[(size_t)w * F + f] = key;
                 ev_t ev = {arr, key, w, f, 0};
                 if (heap_push(&h, ev)) { rc = -2; goto out; }
@@ -757,6 +773,8 @@ static int run_impl(const or_params* p, const uint64_t* row_ptr, const uint32_t*
                 if (fin[idx]) continue;
                 st->gossip_iwant++;
                 st->relaxations++;
+                TR_SEND(ev.key & smask); /* the IWANT answer: src -> w */
+                TR_RECV(ev.dst);
                 if (ev.key < best[idx]) {
                     best[idx] = ev.key;
                     ev_t ne = {ev.key >> tshift, ev.key, ev.dst, ev.frag, 0};
@@ -799,10 +817,12 @@ static int run_impl(const or_params* p, const uint64_t* row_ptr, const uint32_t*
                 if (arr > tmax) { rc = -5; goto out; }
                 uint64_t key = (arr << tshift) | ((hp + 1) << sb) | u;
                 st->relaxations++;
+                TR_SEND(u);
                 if (ms->snap_off) {
                     const int64_t sa = slot_of(ms, epoch_at(p, tp + arr));
                     if (sa < 0 || offline_at(ms, N, sa, w)) continue;
                 }
+                TR_RECV(w);
                 size_t wi = (size_t)w * F + ev.frag;
                 if (key < best[wi]) {
                     best[wi] = key;
@@ -843,7 +863,7 @@ int or_run(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
            uint64_t n_msgs, uint64_t* t_complete, uint8_t* hops, or_stats* st) {
     mesh_src ms = {mesh, cnt, NULL, NULL, NULL, 0, 0, 0};
     return run_impl(p, row_ptr, col, &ms, stage, S, lat_ns, bw_up, bw_dn, sched_t, sched_pub, sched_size,
-                    n_msgs, t_complete, hops, st);
+                    n_msgs, t_complete, hops, st, NULL);
 }
 
 int or_run_churn(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
@@ -854,5 +874,17 @@ int or_run_churn(const or_params* p, const uint64_t* row_ptr, const uint32_t* co
                  uint64_t n_msgs, uint64_t* t_complete, uint8_t* hops, or_stats* st) {
     mesh_src ms = {NULL, NULL, snap_mesh, snap_cnt, snap_off, h_lo, n_snap, 0};
     return run_impl(p, row_ptr, col, &ms, stage, S, lat_ns, bw_up, bw_dn, sched_t, sched_pub, sched_size,
-                    n_msgs, t_complete, hops, st);
+                    n_msgs, t_complete, hops, st, NULL);
+}
+
+/* or_run plus per-peer traffic tr[N][6] (tx bytes, rx bytes, tx packets, rx
+ * packets, tx header bytes, rx header bytes), accumulated (caller zeroes). */
+int or_run_traffic(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
+                   const uint32_t* mesh, const uint8_t* cnt, const uint8_t* stage, uint32_t S,
+                   const uint64_t* lat_ns, const uint64_t* bw_up, const uint64_t* bw_dn,
+                   const uint64_t* sched_t, const uint32_t* sched_pub, const uint32_t* sched_size,
+                   uint64_t n_msgs, uint64_t* t_complete, uint8_t* hops, or_stats* st, uint64_t* tr) {
+    mesh_src ms = {mesh, cnt, NULL, NULL, NULL, 0, 0, 0};
+    return run_impl(p, row_ptr, col, &ms, stage, S, lat_ns, bw_up, bw_dn, sched_t, sched_pub, sched_size,
+                    n_msgs, t_complete, hops, st, tr);
 }

@@ -61,6 +61,10 @@ def lib():
         L.or_rng.argtypes = [u64, u32, u32, u32, u32]
         L.or_wire_bytes.restype = u64
         L.or_wire_bytes.argtypes = [u64, u32, u32]
+        L.or_wire_packets.argtypes = [u64, u32, u32, P(u64), P(u64)]
+        L.or_run_traffic.argtypes = [P(OrParams), P(u64), P(u32), P(u32), P(u8), P(u8), u32, P(u64),
+                                     P(u64), P(u64), P(u64), P(u32), P(u32), u64, P(u64), P(u8),
+                                     P(OrStats), P(u64)]
         L.or_topogen_links.argtypes = [u32, u32, u32, u32, u32, u32, P(u64), P(u64)]
         L.or_dials_per_peer.restype = u32
         L.or_dials_per_peer.argtypes = [P(OrParams)]
@@ -221,7 +225,14 @@ def run_churn(p, row_ptr, col, snaps, h_lo, stage, lat, bw_up, bw_dn, sched_t, s
     return tc.reshape(M, N), hops.reshape(M, N), stats
 
 
-def run(p, row_ptr, col, mesh, cnt, stage, lat, bw_up, bw_dn, sched_t, sched_pub, sched_size):
+def wire_packets(payload, muxer=0, signed=1):
+    pk, hd = ctypes.c_uint64(), ctypes.c_uint64()
+    lib().or_wire_packets(payload, muxer, signed, ctypes.byref(pk), ctypes.byref(hd))
+    return pk.value, hd.value
+
+
+def run(p, row_ptr, col, mesh, cnt, stage, lat, bw_up, bw_dn, sched_t, sched_pub, sched_size, traffic=None):
+    """traffic: optional uint64 [N, 6] accumulated per-peer counters (or_run_traffic)."""
     N = p.peers
     S = lat.shape[0]
     M = len(sched_t)
@@ -234,20 +245,25 @@ def run(p, row_ptr, col, mesh, cnt, stage, lat, bw_up, bw_dn, sched_t, sched_pub
     sched_pub, sched_size = a32(sched_pub), a32(sched_size)
     mesh = a32(mesh.reshape(-1))
     stage = np.ascontiguousarray(stage, np.uint8)
-    rc = lib().or_run(ctypes.byref(p), _p(row_ptr, ctypes.c_uint64), _p(col, ctypes.c_uint32),
-                      _p(mesh, ctypes.c_uint32), _p(cnt, ctypes.c_uint8), _p(stage, ctypes.c_uint8),
-                      S, _p(lat, ctypes.c_uint64), _p(bw_up, ctypes.c_uint64),
-                      _p(bw_dn, ctypes.c_uint64), _p(sched_t, ctypes.c_uint64),
-                      _p(sched_pub, ctypes.c_uint32), _p(sched_size, ctypes.c_uint32), M,
-                      _p(tc, ctypes.c_uint64), _p(hops, ctypes.c_uint8), ctypes.byref(st))
+    args = (ctypes.byref(p), _p(row_ptr, ctypes.c_uint64), _p(col, ctypes.c_uint32),
+            _p(mesh, ctypes.c_uint32), _p(cnt, ctypes.c_uint8), _p(stage, ctypes.c_uint8),
+            S, _p(lat, ctypes.c_uint64), _p(bw_up, ctypes.c_uint64),
+            _p(bw_dn, ctypes.c_uint64), _p(sched_t, ctypes.c_uint64),
+            _p(sched_pub, ctypes.c_uint32), _p(sched_size, ctypes.c_uint32), M,
+            _p(tc, ctypes.c_uint64), _p(hops, ctypes.c_uint8), ctypes.byref(st))
+    if traffic is None:
+        rc = lib().or_run(*args)
+    else:
+        assert traffic.dtype == np.uint64 and traffic.shape == (N, 6) and traffic.flags.c_contiguous
+        rc = lib().or_run_traffic(*args, _p(traffic, ctypes.c_uint64))
     if rc:
         raise ValueError("or_run rc=%d" % rc)
     stats = {n: getattr(st, n) for n, _ in OrStats._fields_}
     return tc.reshape(M, N), hops.reshape(M, N), stats
 
 
-def simulate(p, stages=1, links=(50, 50, 50, 50), mode=0, sched=None, max_hb=400):
-    """Whole pipeline on the CPU: links -> topology -> mesh -> run."""
+def simulate(p, stages=1, links=(50, 50, 50, 50), mode=0, sched=None, max_hb=400, traffic=False):
+    """Whole pipeline on the CPU: links -> topology -> mesh -> run (+ per-peer traffic [N, 6])."""
     bl, bh, ll, lh = links
     lat, bw = topogen_links(stages, bl, bh, ll, lh, mode)
     stage = (np.arange(p.peers) % stages).astype(np.uint8)
@@ -263,6 +279,9 @@ def simulate(p, stages=1, links=(50, 50, 50, 50), mode=0, sched=None, max_hb=400
         tc, hops, stats = run_churn(p, row_ptr, col, snaps, h_lo, stage, lat, bw, bw, t, pub, size)
         out.update(snaps=snaps, h_lo=h_lo)
     else:
-        tc, hops, stats = run(p, row_ptr, col, mesh, cnt, stage, lat, bw, bw, t, pub, size)
+        tr = np.zeros((p.peers, 6), np.uint64) if traffic else None
+        tc, hops, stats = run(p, row_ptr, col, mesh, cnt, stage, lat, bw, bw, t, pub, size, traffic=tr)
+        if traffic:
+            out["traffic"] = tr
     out.update(t_complete=tc, hops=hops, stats=stats)
     return out

@@ -141,6 +141,34 @@ def test_node_presets(node):
         sim.run(_sched(1, 800, size=small - 3))
 
 
+@pytest.mark.parametrize("kw", [dict(), dict(fragments=3), dict(flood_publish=0), dict(node=1, fragments=2),
+                                dict(muxer=1, signed_msgs=0)])
+def test_peer_traffic_counters(kw):
+    """gs_set_traffic: per-peer tx/rx bytes, packets and header bytes (Shadow's
+    tracker counters) bit-exact against the oracle, on the pull path and (go
+    preset: IDONTWANT) the push path, accumulated over two runs."""
+    p = oracle.params_for(kw.pop("node", 0), peers=900, seed=71, **kw)
+    sched = _sched(12, 900)
+    ref = oracle.simulate(p, 5, (50, 150, 40, 130), sched=sched, traffic=True)
+    sim, _ = gpu_sim(p, 5, (50, 150, 40, 130), batch=8)
+    sim.set_traffic(True)
+    sim.run((sched[0][:5], sched[1][:5], sched[2][:5]))
+    sim.run((sched[0][5:], sched[1][5:], sched[2][5:]))
+    np.testing.assert_array_equal(sim.traffic(), ref["traffic"])
+    sim.reset_stats()
+    assert not sim.traffic().any()
+
+
+def test_peer_traffic_unsupported_modes():
+    p = oracle.params(peers=300, seed=72, lazy_gossip=1)
+    sim, _ = gpu_sim(p, 1, (50, 50, 50, 50))
+    with pytest.raises(gossipsim.GossipSimError, match="GS_ESTATE"):
+        sim.traffic()
+    sim.set_traffic(True)
+    with pytest.raises(gossipsim.GossipSimError, match="GS_EUNSUPPORTED"):
+        sim.run(_sched(2, 300))
+
+
 def test_fragment_collision_defect_d8():
     p = oracle.params(peers=100, fragments=4)
     sim, res = compare(p, 1, (50, 50, 50, 50), _sched(2, 100, size=40))

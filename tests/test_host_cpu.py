@@ -57,6 +57,50 @@ def test_wire_bytes_match_oracle(muxer, signed):
         assert gossipsim.wire_bytes(payload, muxer, signed) == oracle.wire_bytes(payload, muxer, signed)
 
 
+@pytest.mark.parametrize("muxer", [0, 1, 2])
+@pytest.mark.parametrize("signed", [0, 1])
+def test_wire_packets_match_oracle(muxer, signed):
+    for payload in [8, 100, 1300, 1460, 1875, 2900, 15000, 65519, 1 << 20]:
+        pk, hd = gossipsim.wire_packets(payload, muxer, signed)
+        assert (pk, hd) == oracle.wire_packets(payload, muxer, signed)
+        assert hd == pk * (65 if muxer == 1 else 40) and pk >= 1
+
+
+def _shadow_log(tmp_path):
+    p = oracle.params(peers=80, seed=5, fragments=2)
+    t = np.uint64(gossipsim.T0_NS) + np.arange(3, dtype=np.uint64) * np.uint64(10 ** 9)
+    r = oracle.simulate(p, 3, (20, 80, 30, 60), sched=(t, np.array([1, 40, 79]), np.full(3, 15000)), traffic=True)
+    out = str(tmp_path / "shadowlog")
+    gossipsim.write_shadow_heartbeat(out, r["traffic"], sim_seconds=900)
+    return r["traffic"], out
+
+
+def test_shadow_heartbeat_lines(tmp_path):
+    tr, out = _shadow_log(tmp_path)
+    lines = open(out).read().splitlines()
+    assert len(lines) == tr.shape[0]
+    for u, ln in enumerate(lines):
+        f = ln.split()
+        assert f[4] == "[pod-%d]" % u and f[8] == "[node]"
+        arr = re.split(",|;", f[9])
+        assert int(arr[1]) == tr[u, 1] and int(arr[2]) == tr[u, 0]
+        assert int(arr[30]) == tr[u, 3] and int(arr[31]) == tr[u, 1] and int(arr[38]) == tr[u, 1] - tr[u, 5]
+        assert int(arr[42]) == tr[u, 2] and int(arr[43]) == tr[u, 0] and int(arr[48]) == tr[u, 2]
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_SHADOW) or not shutil.which("awk"),
+                    reason="reference awk scripts only in the build container")
+def test_shadow_heartbeat_round_trips_through_reference_awk(tmp_path):
+    tr, out = _shadow_log(tmp_path)
+    got = subprocess.check_output(["awk", "-f", os.path.join(REF_SHADOW, "summary_shadowlog.awk"), out]).decode()
+    m = re.search(r"Total Bytes Received :\s+(\d+)\s+Total Bytes Transferred :\s+(\d+)", got)
+    assert m and int(m.group(1)) == int(tr[:, 1].sum()) and int(m.group(2)) == int(tr[:, 0].sum())
+    m = re.search(r"Remote IN pkt:\s+(\d+)\s+Bytes :\s+(\d+).*DataPkt:\s+(\d+)\s+DataHdrBytes:\s+(\d+)\s+DataBytes\s+(\d+)",
+                  got)
+    assert m and [int(x) for x in m.groups()] == [int(tr[:, 3].sum()), int(tr[:, 1].sum()), int(tr[:, 3].sum()),
+                                                  int(tr[:, 5].sum()), int((tr[:, 1] - tr[:, 5]).sum())]
+
+
 @pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "topogen_*.json"))))
 @pytest.mark.parametrize("shortest", [False, True])
 def test_topogen_links_match_oracle_and_fixture(path, shortest):

@@ -297,6 +297,22 @@ def test_fragment_layout_per_node(node, bad, good):
     assert r["stats"]["frag_deliveries"] == (59 if node == "rust" else 4 * 59)
 
 
+@pytest.mark.parametrize("kw", [dict(), dict(fragments=3), dict(flood_publish=0), dict(idontwant=1000)])
+def test_traffic_identities(kw):
+    """Every send is one relaxation and, without churn, one receipt: sum(tx) =
+    sum(rx) = R x wire bytes; a non-publisher's sends = its forwards."""
+    p = oracle.params(peers=300, seed=7, **kw)
+    t = np.uint64(T0) + np.arange(4, dtype=np.uint64) * np.uint64(10 ** 9)
+    r = oracle.simulate(p, 5, (50, 150, 40, 130), sched=(t, np.array([3, 50, 120, 299]), np.full(4, 15000)),
+                        traffic=True)
+    tr, st = r["traffic"], r["stats"]
+    W = oracle.wire_bytes(15000 // p.fragments, p.muxer, p.signed_msgs)
+    pk, hd = oracle.wire_packets(15000 // p.fragments, p.muxer, p.signed_msgs)
+    assert tr[:, 0].sum() == tr[:, 1].sum() == st["relaxations"] * W
+    assert tr[:, 2].sum() == st["relaxations"] * pk and tr[:, 4].sum() == st["relaxations"] * hd
+    assert (tr[:, 0] % W == 0).all() and (tr[:, 1] >= W).all()  # everyone receives at least once
+
+
 def test_stats_identities():
     p, r, _ = _sim(N=400, fragments=2)
     st = r["stats"]
