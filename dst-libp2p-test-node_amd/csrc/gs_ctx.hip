@@ -128,10 +128,12 @@ extern "C" gs_status gs_set_links(gs_ctx* ctx, uint32_t S, const uint64_t* lat_n
   ctx->bw_up.assign(bw_up, bw_up + S);
   ctx->bw_dn.assign(bw_dn, bw_dn + S);
   ctx->stage_host.resize(N);
+  ctx->stage_used.assign(S, 0);
   for (uint32_t u = 0; u < N; u++) {
     const uint8_t st = stage_of_peer ? stage_of_peer[u] : (uint8_t)(u % S);  // topogen.py:121-122
     if (st >= S) ctx->fail(GS_EINVAL, "stage_of_peer entry >= stages");
     ctx->stage_host[u] = st;
+    ctx->stage_used[st] = 1;
   }
   GS_HIP(hipSetDevice(ctx->cfg.device));
   ctx->d_stage.alloc(N);

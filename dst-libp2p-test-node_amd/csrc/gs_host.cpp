@@ -232,6 +232,49 @@ extern "C" gs_status gs_write_shadow_heartbeat(const char* path, uint32_t peers,
   return GS_OK;
 }
 
+namespace {
+constexpr uint64_t NO_EDGE = ~0ull;
+
+// Stage-to-stage latency table of the first S nodes of a V-node network graph
+// g (ns, NO_EDGE = no edge). GS_LINKS_DIRECT: the edge itself (topogen's
+// intent); GS_LINKS_SHORTEST: Shadow's use_shortest_path (upstream, not
+// vendored) — the shortest non-empty path, so a self-loop may be beaten by a
+// round trip through another node.
+gs_status graph_latencies(uint32_t V, const std::vector<uint64_t>& g, uint32_t S, uint32_t mode, uint64_t* lat) {
+  if (mode == GS_LINKS_DIRECT) {
+    for (uint32_t i = 0; i < S; i++)
+      for (uint32_t j = 0; j < S; j++) {
+        if (g[(size_t)i * V + j] == NO_EDGE) return GS_EINVAL;  // direct mode needs every stage pair
+        lat[(size_t)i * S + j] = g[(size_t)i * V + j];
+      }
+    return GS_OK;
+  }
+  std::vector<uint64_t> d((size_t)V * V);
+  for (uint32_t i = 0; i < V; i++)
+    for (uint32_t j = 0; j < V; j++) d[(size_t)i * V + j] = i == j ? 0 : g[(size_t)i * V + j];
+  for (uint32_t k = 0; k < V; k++)
+    for (uint32_t i = 0; i < V; i++)
+      for (uint32_t j = 0; j < V; j++) {
+        const uint64_t a = d[(size_t)i * V + k], b = d[(size_t)k * V + j];
+        if (a != NO_EDGE && b != NO_EDGE && a + b < d[(size_t)i * V + j]) d[(size_t)i * V + j] = a + b;
+      }
+  for (uint32_t i = 0; i < S; i++)
+    for (uint32_t j = 0; j < S; j++) {
+      uint64_t v = d[(size_t)i * V + j];
+      if (i == j) {
+        v = g[(size_t)i * V + i];
+        for (uint32_t k = 0; k < V; k++) {
+          const uint64_t a = d[(size_t)i * V + k], b = d[(size_t)k * V + i];
+          if (k != i && a != NO_EDGE && b != NO_EDGE && a + b < v) v = a + b;
+        }
+      }
+      if (v == NO_EDGE) return GS_EINVAL;  // unreachable stage pair
+      lat[(size_t)i * S + j] = v;
+    }
+  return GS_OK;
+}
+}  // namespace
+
 // shadow/topogen.py:39-71 restated: stage i bandwidth ceil(i*bj + bl) Mbit
 // (44,49-51); self-loop max((S-i)*lj, ll) ms (55); edge i<j
 // min(ceil((S-j)*lj + ll), lh) ms (60); injector node S, 1 ms to all (64-69).
@@ -253,34 +296,178 @@ extern "C" gs_status gs_topogen_links(uint32_t S, uint32_t bl, uint32_t bh, uint
     }
   }
   for (uint32_t i = 0; i <= S; i++) g[(size_t)i * V + S] = g[(size_t)S * V + i] = 1;
-  if (mode == GS_LINKS_DIRECT) {
-    for (uint32_t i = 0; i < S; i++)
-      for (uint32_t j = 0; j < S; j++) lat_ns[(size_t)i * S + j] = g[(size_t)i * V + j] * 1000000ull;
-    return GS_OK;
+  for (auto& x : g) x *= 1000000ull;  // ms -> ns
+  return graph_latencies(V, g, S, mode, lat_ns);
+}
+
+namespace {
+// "<number> <unit>" of Shadow's GML attributes -> value in base units (ns or bit/s).
+bool parse_quantity(const std::string& s, bool time, uint64_t* out) {
+  char* end = nullptr;
+  const double x = strtod(s.c_str(), &end);
+  if (end == s.c_str() || x < 0) return false;
+  std::string u(end);
+  u.erase(0, u.find_first_not_of(' '));
+  double mul;
+  if (time) {
+    if (u == "ns") mul = 1;
+    else if (u == "us" || u == "μs") mul = 1e3;
+    else if (u == "ms") mul = 1e6;
+    else if (u == "s" || u == "sec") mul = 1e9;
+    else return false;
+  } else {
+    if (u == "bit") mul = 1;
+    else if (u == "Kbit" || u == "kbit") mul = 1e3;
+    else if (u == "Mbit") mul = 1e6;
+    else if (u == "Gbit") mul = 1e9;
+    else if (u == "Kibit") mul = 1024.0;
+    else if (u == "Mibit") mul = 1048576.0;
+    else if (u == "Gibit") mul = 1073741824.0;
+    else return false;
   }
-  // Shadow use_shortest_path (upstream, not vendored): shortest non-empty path.
-  std::vector<uint64_t> d((size_t)V * V);
-  for (uint32_t i = 0; i < V; i++)
-    for (uint32_t j = 0; j < V; j++) d[(size_t)i * V + j] = i == j ? 0 : g[(size_t)i * V + j];
-  for (uint32_t k = 0; k < V; k++)
-    for (uint32_t i = 0; i < V; i++)
-      for (uint32_t j = 0; j < V; j++) {
-        uint64_t via = d[(size_t)i * V + k] + d[(size_t)k * V + j];
-        if (via < d[(size_t)i * V + j]) d[(size_t)i * V + j] = via;
-      }
-  for (uint32_t i = 0; i < S; i++)
-    for (uint32_t j = 0; j < S; j++) {
-      uint64_t v = d[(size_t)i * V + j];
-      if (i == j) {
-        v = g[(size_t)i * V + i];
-        for (uint32_t k = 0; k < V; k++) {
-          if (k == i) continue;
-          uint64_t rt = d[(size_t)i * V + k] + d[(size_t)k * V + i];
-          if (rt < v) v = rt;
-        }
-      }
-      lat_ns[(size_t)i * S + j] = v * 1000000ull;
+  *out = (uint64_t)(x * mul + 0.5);
+  return true;
+}
+}  // namespace
+
+// network_topology.gml as topogen.py:39-71 writes it (networkx write_gml):
+// node [ id, host_bandwidth_up/down "<n> Mbit" ] and edge [ source, target,
+// latency "<n> ms", packet_loss ] blocks, undirected. Every node becomes one
+// link class (the injector node of topogen included; no peer maps to it).
+extern "C" gs_status gs_links_from_gml(const char* path, uint32_t mode, uint32_t max_nodes, uint32_t* nodes,
+                                       uint64_t* lat_ns, uint64_t* bw_up_bps, uint64_t* bw_down_bps) {
+  if (!path || !nodes || mode > GS_LINKS_SHORTEST) return GS_EINVAL;
+  FILE* f = fopen(path, "r");
+  if (!f) return GS_EINVAL;
+  std::string text;
+  char buf[4096];
+  size_t n;
+  while ((n = fread(buf, 1, sizeof buf, f)) > 0) text.append(buf, n);
+  fclose(f);
+  // tokens: bare words, numbers, quoted strings, [ and ]
+  std::vector<std::string> tok;
+  for (size_t i = 0; i < text.size();) {
+    const char ch = text[i];
+    if (isspace((unsigned char)ch)) { i++; continue; }
+    if (ch == '[' || ch == ']') { tok.emplace_back(1, ch); i++; continue; }
+    if (ch == '"') {
+      const size_t j = text.find('"', i + 1);
+      if (j == std::string::npos) return GS_EINVAL;
+      tok.push_back(text.substr(i, j - i + 1));
+      i = j + 1;
+      continue;
     }
+    size_t j = i;
+    while (j < text.size() && !isspace((unsigned char)text[j]) && text[j] != '[' && text[j] != ']') j++;
+    tok.push_back(text.substr(i, j - i));
+    i = j;
+  }
+  struct Node { int64_t id = -1; uint64_t up = 0, dn = 0; };
+  struct Edge { int64_t s = -1, t = -1; uint64_t lat = 0; double loss = 0; };
+  std::vector<Node> nv;
+  std::vector<Edge> ev;
+  auto unq = [](const std::string& s) { return s.size() >= 2 && s[0] == '"' ? s.substr(1, s.size() - 2) : s; };
+  for (size_t i = 0; i + 1 < tok.size(); i++) {
+    if ((tok[i] != "node" && tok[i] != "edge") || tok[i + 1] != "[") continue;
+    const bool is_node = tok[i] == "node";
+    Node nd;
+    Edge ed;
+    size_t j = i + 2;
+    for (; j + 1 < tok.size() && tok[j] != "]"; j += 2) {
+      const std::string& k = tok[j];
+      const std::string v = unq(tok[j + 1]);
+      if (tok[j + 1] == "[") return GS_EINVAL;  // no nested blocks in topogen's GML
+      if (is_node && k == "id") nd.id = strtoll(v.c_str(), nullptr, 10);
+      else if (is_node && k == "host_bandwidth_up") { if (!parse_quantity(v, false, &nd.up)) return GS_EINVAL; }
+      else if (is_node && k == "host_bandwidth_down") { if (!parse_quantity(v, false, &nd.dn)) return GS_EINVAL; }
+      else if (!is_node && k == "source") ed.s = strtoll(v.c_str(), nullptr, 10);
+      else if (!is_node && k == "target") ed.t = strtoll(v.c_str(), nullptr, 10);
+      else if (!is_node && k == "latency") { if (!parse_quantity(v, true, &ed.lat)) return GS_EINVAL; }
+      else if (!is_node && k == "packet_loss") ed.loss = strtod(v.c_str(), nullptr);
+    }
+    if (is_node) nv.push_back(nd); else ev.push_back(ed);
+    i = j;
+  }
+  const uint32_t V = (uint32_t)nv.size();
+  *nodes = V;
+  if (V == 0) return GS_EINVAL;
+  if (V > max_nodes) return GS_ERANGE;  // *nodes tells the caller the size needed
+  if (!lat_ns || !bw_up_bps || !bw_down_bps) return GS_EINVAL;
+  std::vector<uint64_t> g((size_t)V * V, NO_EDGE);
+  std::vector<bool> seen(V, false);
+  for (const Node& nd : nv) {
+    if (nd.id < 0 || nd.id >= (int64_t)V || seen[nd.id] || nd.up == 0 || nd.dn == 0) return GS_EINVAL;
+    seen[nd.id] = true;
+    bw_up_bps[nd.id] = nd.up;
+    bw_down_bps[nd.id] = nd.dn;
+  }
+  for (const Edge& ed : ev) {
+    if (ed.s < 0 || ed.t < 0 || ed.s >= (int64_t)V || ed.t >= (int64_t)V || ed.lat == 0) return GS_EINVAL;
+    if (ed.loss != 0.0) return GS_EUNSUPPORTED;  // packet loss is not modelled (run.sh:33: "not yet tested")
+    g[(size_t)ed.s * V + ed.t] = g[(size_t)ed.t * V + ed.s] = ed.lat;
+  }
+  return graph_latencies(V, g, V, mode, lat_ns);
+}
+
+// shadow.yaml as topogen.py:73-139 writes it (PyYAML): under "hosts:", blocks
+// "  pod-<i>: &idN" with "    network_node_id: <k>", repeated hosts as
+// aliases "  pod-<j>: *idN". The peer id is the number after the '-' of the
+// host name (rust env.rs:34-36); hosts with ids >= peers (the injector) are
+// skipped.
+extern "C" gs_status gs_shadow_hosts(const char* path, uint32_t peers, uint8_t* stage_of_peer) {
+  if (!path || !stage_of_peer) return GS_EINVAL;
+  FILE* f = fopen(path, "r");
+  if (!f) return GS_EINVAL;
+  std::vector<int> stage(peers, -1);
+  std::vector<std::pair<std::string, int>> anchors;
+  auto anchor_get = [&](const std::string& a) {
+    for (auto& kv : anchors) if (kv.first == a) return kv.second;
+    return -1;
+  };
+  bool in_hosts = false;
+  int64_t cur = -1;
+  std::string cur_anchor;
+  char line[4096];
+  while (fgets(line, sizeof line, f)) {
+    std::string s(line);
+    while (!s.empty() && (s.back() == '\n' || s.back() == '\r')) s.pop_back();
+    if (s.empty()) continue;
+    const size_t ind = s.find_first_not_of(' ');
+    if (ind == std::string::npos) continue;
+    if (ind == 0) { in_hosts = s == "hosts:"; cur = -1; continue; }
+    if (!in_hosts) continue;
+    if (ind == 2) {  // a host
+      const size_t colon = s.find(':');
+      if (colon == std::string::npos) continue;
+      const std::string name = s.substr(2, colon - 2);
+      const size_t dash = name.find('-');
+      char* end = nullptr;
+      const int64_t id = dash == std::string::npos ? -1 : strtoll(name.c_str() + dash + 1, &end, 10);
+      cur = (dash != std::string::npos && end && *end == '\0') ? id : -1;
+      std::string rest = s.substr(colon + 1);
+      rest.erase(0, rest.find_first_not_of(' '));
+      cur_anchor.clear();
+      if (!rest.empty() && rest[0] == '&') cur_anchor = rest.substr(1);
+      else if (!rest.empty() && rest[0] == '*') {  // alias of an earlier host block
+        const int st = anchor_get(rest.substr(1));
+        if (st < 0) { fclose(f); return GS_EINVAL; }
+        if (cur >= 0 && cur < (int64_t)peers) stage[cur] = st;
+        cur = -1;
+      }
+      continue;
+    }
+    if (ind == 4 && s.compare(4, 16, "network_node_id:") == 0) {
+      const long k = strtol(s.c_str() + 20, nullptr, 10);
+      if (k < 0 || k > 255) { fclose(f); return GS_ERANGE; }
+      if (!cur_anchor.empty()) anchors.emplace_back(cur_anchor, (int)k);
+      if (cur >= 0 && cur < (int64_t)peers) stage[cur] = (int)k;
+    }
+  }
+  fclose(f);
+  for (uint32_t u = 0; u < peers; u++) {
+    if (stage[u] < 0) return GS_EINVAL;  // every peer needs a host entry
+    stage_of_peer[u] = (uint8_t)stage[u];
+  }
   return GS_OK;
 }
 

@@ -74,6 +74,7 @@ struct Ctx {
   uint32_t S = 0;
   std::vector<uint64_t> lat_ns, bw_up, bw_dn;
   std::vector<uint8_t> stage_host;
+  std::vector<uint8_t> stage_used;  // [S] 1 if some peer sits on that link class
   bool links_set = false;
 
   // graph (device resident)

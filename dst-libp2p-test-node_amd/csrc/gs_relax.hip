@@ -326,18 +326,20 @@ static Batch setup_batch(Ctx& c, const gs_publish* sched, uint64_t i0, uint64_t 
   const uint64_t wire = gs_wire_bytes(b.payload, c.cfg.muxer, c.cfg.signed_msgs);
   std::vector<uint32_t> tab((size_t)S * S + 2 * S), pub(b.B);
   uint64_t min_lat = INF64, min_ser = INF64;
+  // Delta from the link classes peers actually sit on (a Shadow graph may
+  // carry nodes no peer uses, e.g. topogen's 1 ms injector hub)
   for (uint32_t x = 0; x < S; x++)
     for (uint32_t y = 0; y < S; y++) {
       if (c.lat_ns[(size_t)x * S + y] >= (1ull << 32)) c.fail(GS_ERANGE, "latency >= 2^32 ns");
       tab[(size_t)x * S + y] = (uint32_t)c.lat_ns[(size_t)x * S + y];
-      min_lat = std::min<uint64_t>(min_lat, c.lat_ns[(size_t)x * S + y]);
+      if (c.stage_used[x] && c.stage_used[y]) min_lat = std::min<uint64_t>(min_lat, c.lat_ns[(size_t)x * S + y]);
     }
   for (uint32_t x = 0; x < S; x++) {
     const uint64_t up = ser_ns(wire, c.bw_up[x]), dn = ser_ns(wire, c.bw_dn[x]);
     if (up >= (1ull << 32) || dn >= (1ull << 32)) c.fail(GS_ERANGE, "serialisation >= 2^32 ns");
     tab[(size_t)S * S + x] = (uint32_t)up;
     tab[(size_t)S * S + S + x] = (uint32_t)dn;
-    min_ser = std::min(min_ser, up);
+    if (c.stage_used[x]) min_ser = std::min(min_ser, up);
   }
   b.delta = std::max<uint64_t>(1, min_lat + min_ser);
   b.tpub.resize(b.B);

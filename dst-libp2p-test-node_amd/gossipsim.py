@@ -78,6 +78,8 @@ SIGNATURES = {
     "gs_wire_bytes": (u64, [u64, u32, u32]),
     "gs_wire_packets": (None, [u64, u32, u32, P(u64), P(u64)]),
     "gs_write_shadow_heartbeat": (i32, [ctypes.c_char_p, u32, P(u64), u64]),
+    "gs_links_from_gml": (i32, [ctypes.c_char_p, u32, u32, P(u32), P(u64), P(u64), P(u64)]),
+    "gs_shadow_hosts": (i32, [ctypes.c_char_p, u32, P(u8)]),
     "gs_set_traffic": (i32, [ctypes.c_void_p, u32]),
     "gs_get_traffic": (i32, [ctypes.c_void_p, P(u64)]),
     "gs_topogen_links": (i32, [u32, u32, u32, u32, u32, u32, P(u64), P(u64)]),
@@ -157,6 +159,32 @@ def write_shadow_heartbeat(path, traffic, sim_seconds=900):
     rc = lib().gs_write_shadow_heartbeat(path.encode(), tr.shape[0], _ptr(tr, u64), sim_seconds)
     if rc:
         raise GossipSimError(rc, "gs_write_shadow_heartbeat failed")
+
+
+def links_from_gml(path, shortest=False):
+    """Shadow network graph (network_topology.gml) -> (lat_ns[V,V], bw_up[V], bw_down[V])."""
+    V = u32()
+    cap = 16
+    while True:
+        lat, up, dn = np.zeros(cap * cap, np.uint64), np.zeros(cap, np.uint64), np.zeros(cap, np.uint64)
+        rc = lib().gs_links_from_gml(path.encode(), 1 if shortest else 0, cap, ctypes.byref(V), _ptr(lat, u64),
+                                     _ptr(up, u64), _ptr(dn, u64))
+        if rc == GS_ERANGE and V.value > cap:
+            cap = V.value
+            continue
+        if rc:
+            raise GossipSimError(rc, "cannot ingest %s" % path)
+        n = V.value
+        return lat[:n * n].reshape(n, n), up[:n], dn[:n]
+
+
+def shadow_hosts(path, peers):
+    """shadow.yaml hosts pod-<i> -> network_node_id, as the stage_of_peer array of set_links."""
+    st = np.zeros(peers, np.uint8)
+    rc = lib().gs_shadow_hosts(path.encode(), peers, _ptr(st, u8))
+    if rc:
+        raise GossipSimError(rc, "cannot map the %d peers of %s" % (peers, path))
+    return st
 
 
 def topogen_links(stages=1, min_bw=50, max_bw=50, min_lat=100, max_lat=100, shortest=False):
@@ -285,6 +313,12 @@ class Simulator:
         lat, bw = topogen_links(stages, min_bw, max_bw, min_lat, max_lat, shortest)
         self.set_links(lat, bw, bw)
         return lat, bw
+
+    def set_shadow_links(self, gml_path, yaml_path, shortest=False):
+        """Links straight from a Shadow experiment: the GML graph + shadow.yaml's host placement."""
+        lat, up, dn = links_from_gml(gml_path, shortest)
+        self.set_links(lat, up, dn, shadow_hosts(yaml_path, self.peers))
+        return lat, up, dn
 
     def connect_gossipsub_peers(self):
         """main.rs:303-389: random ID dialing -> CSR (device resident)."""

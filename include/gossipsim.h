@@ -173,6 +173,22 @@ gs_status gs_topogen_links(uint32_t stages, uint32_t min_bw_mbit, uint32_t max_b
                            uint32_t min_lat_ms, uint32_t max_lat_ms, uint32_t mode,
                            uint64_t* lat_ns, uint64_t* bw_bps);
 
+/* Link tables from a Shadow network graph file (network_topology.gml as
+ * shadow/topogen.py:39-71 writes it: node host_bandwidth_up/down, edge latency;
+ * units bit/Kbit/Mbit/Gbit, ns/us/ms/s). Every GML node becomes one link class,
+ * so V = *nodes classes: lat_ns[V*V], bw_up_bps[V], bw_down_bps[V]. mode as
+ * gs_topogen_links (GS_LINKS_DIRECT needs an edge for every pair). Returns
+ * GS_ERANGE with *nodes = V when V > max_nodes (call again with room), and
+ * GS_EUNSUPPORTED for a non-zero packet_loss (not modelled). */
+gs_status gs_links_from_gml(const char* gml_path, uint32_t mode, uint32_t max_nodes, uint32_t* nodes,
+                            uint64_t* lat_ns, uint64_t* bw_up_bps, uint64_t* bw_down_bps);
+
+/* Peer -> link class from a Shadow config (shadow.yaml as topogen.py:73-139
+ * writes it): host "pod-<id>" (the id parse of rust env.rs:34-36) ->
+ * network_node_id, incl. YAML anchors/aliases; hosts with id >= peers (the
+ * injector) are skipped; a peer without a host is GS_EINVAL. */
+gs_status gs_shadow_hosts(const char* yaml_path, uint32_t peers, uint8_t* stage_of_peer);
+
 /* Publish schedule of shadow/run.sh:34-36 (publisher_id, publisher_rotation,
  * inter_message_delay): row i = {t0 + i*delay, (pub0 + i*rotation) mod N, size}. */
 gs_status gs_schedule_runsh(uint32_t n_msgs, uint32_t peers, uint32_t publisher_id,

@@ -37,6 +37,9 @@ TOPOGEN_CASES = {
 }
 
 
+RAW_CASES = ("runsh_example", "seven_stages")
+
+
 def parse_gml(path):
     """Minimal GML reader for topogen's output (nodes with bandwidth, edges with latency)."""
     text = open(path).read()
@@ -64,6 +67,11 @@ def topogen_fixtures():
             subprocess.check_call([sys.executable, os.path.join(REF, "topogen.py")] + flags, cwd=d)
             nodes, edges = parse_gml(os.path.join(d, "network_topology.gml"))
             cfg = yaml.safe_load(open(os.path.join(d, "shadow.yaml")))
+            if name in RAW_CASES:  # the generated files themselves, for the GML / shadow.yaml ingest tests
+                for src, dst in (("network_topology.gml", "gml"), ("shadow.yaml", "yaml")):
+                    with open(os.path.join(d, src)) as fi, open(os.path.join(HERE, "topogen_%s.%s" % (name, dst)),
+                                                                "w") as fo:
+                        fo.write(fi.read())
         hosts = cfg["hosts"]
         peers = [h for h in hosts if h != "pod-%d" % (len(hosts) - 1)]
         fx = {

@@ -169,6 +169,24 @@ def test_peer_traffic_unsupported_modes():
         sim.run(_sched(2, 300))
 
 
+def test_shadow_experiment_files_drive_the_run():
+    """set_shadow_links(network_topology.gml, shadow.yaml) of topogen's run.sh
+    example == the same links from topogen's parameters (the injector node is
+    an extra link class no peer uses)."""
+    p = oracle.params(peers=100, seed=81)
+    sched = _sched(6, 100)
+    ref = oracle.simulate(p, 5, (50, 150, 40, 130), sched=sched)
+    kw = _knobs(p)
+    sim = gossipsim.Simulator(batch=8, **kw)
+    sim.set_shadow_links(os.path.join(GOLDEN, "topogen_runsh_example.gml"),
+                         os.path.join(GOLDEN, "topogen_runsh_example.yaml"))
+    sim.connect_gossipsub_peers()
+    sim.mesh_converge()
+    res = sim.run(sched)
+    np.testing.assert_array_equal(res["t_complete"], ref["t_complete"])
+    np.testing.assert_array_equal(res["hops"], ref["hops"])
+
+
 def test_fragment_collision_defect_d8():
     p = oracle.params(peers=100, fragments=4)
     sim, res = compare(p, 1, (50, 50, 50, 50), _sched(2, 100, size=40))

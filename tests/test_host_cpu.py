@@ -120,6 +120,36 @@ def test_topogen_links_match_oracle_and_fixture(path, shortest):
                 assert lat[s, t] == l * 1_000_000
 
 
+@pytest.mark.parametrize("name,S,links", [("runsh_example", 5, (50, 150, 40, 130)),
+                                          ("seven_stages", 7, (10, 1000, 5, 300))])
+@pytest.mark.parametrize("shortest", [False, True])
+def test_gml_and_shadow_yaml_ingest(name, S, links, shortest):
+    """topogen's own GML / shadow.yaml (tests/golden, made by running shadow/topogen.py)
+    read back == the topogen arithmetic restated in gs_topogen_links."""
+    lat, up, dn = gossipsim.links_from_gml(os.path.join(GOLDEN, "topogen_%s.gml" % name), shortest)
+    tlat, tbw = gossipsim.topogen_links(S, *links, shortest)
+    assert lat.shape == (S + 1, S + 1)  # + topogen's injector node
+    np.testing.assert_array_equal(lat[:S, :S], tlat)
+    np.testing.assert_array_equal(up[:S], tbw)
+    np.testing.assert_array_equal(dn[:S], tbw)
+    assert up[S] == dn[S] == 100_000_000  # the injector node: 100 Mbit (topogen.py:64-69)
+    if not shortest:
+        assert (lat[S, :S] == 1_000_000).all()
+    fx = json.load(open(os.path.join(GOLDEN, "topogen_%s.json" % name)))
+    st = gossipsim.shadow_hosts(os.path.join(GOLDEN, "topogen_%s.yaml" % name), len(fx["host_stage"]))
+    np.testing.assert_array_equal(st, fx["host_stage"])
+    np.testing.assert_array_equal(st, np.arange(len(st)) % S)  # topogen.py:121-122
+    with pytest.raises(gossipsim.GossipSimError, match="GS_EINVAL"):  # more peers than hosts
+        gossipsim.shadow_hosts(os.path.join(GOLDEN, "topogen_%s.yaml" % name), len(st) + 5)
+
+
+def test_gml_rejects_packet_loss(tmp_path):
+    g = open(os.path.join(GOLDEN, "topogen_runsh_example.gml")).read().replace("packet_loss 0.0", "packet_loss 0.01", 1)
+    (tmp_path / "lossy.gml").write_text(g)
+    with pytest.raises(gossipsim.GossipSimError, match="GS_EUNSUPPORTED"):
+        gossipsim.links_from_gml(str(tmp_path / "lossy.gml"))
+
+
 def test_schedule_runsh():
     # run.sh:34-36: publisher_id, rotation, inter_message_delay (ms)
     sch = gossipsim.schedule_runsh(5, 100, 98, 1, 10, 1_000_000_000, 15000)
