@@ -471,6 +471,57 @@ extern "C" gs_status gs_shadow_hosts(const char* path, uint32_t peers, uint8_t* 
   return GS_OK;
 }
 
+// The node's custom metrics (rust-test-node/src/metrics.rs:60-132, names shared
+// with go metrics.go and nim gossipsub-queues/main.nim:25-78) for every peer,
+// in prometheus-client's OpenMetrics text encoding (the format store_metrics
+// dumps, env.rs:114-152): gauges as is, counters with the _total suffix,
+// topic families labelled topic="test" (main.rs:248), "# EOF" at the end.
+extern "C" gs_status gs_write_node_metrics(const gs_config* cfg, const char* path, const uint64_t* row_ptr,
+                                           const uint8_t* mesh_count, const uint64_t* traffic) {
+  if (!cfg || !path || !row_ptr || !mesh_count || !traffic) return GS_EINVAL;
+  FILE* f = fopen(path, "w");
+  if (!f) return GS_EINVAL;
+  std::vector<char> buf(1 << 20);
+  setvbuf(f, buf.data(), _IOFBF, buf.size());
+  const uint32_t N = cfg->peers;
+  auto deg = [&](uint32_t u) { return (unsigned long long)(row_ptr[u + 1] - row_ptr[u]); };
+  auto family = [&](const char* name, const char* type, const char* help, bool topic, auto value) {
+    fprintf(f, "# HELP %s %s.\n# TYPE %s %s\n", name, help, name, type);
+    const char* suffix = strcmp(type, "counter") == 0 ? "_total" : "";
+    for (uint32_t u = 0; u < N; u++)
+      fprintf(f, "%s%s{%speer=\"pod-%u\"} %llu\n", name, suffix, topic ? "topic=\"test\"," : "", u,
+              (unsigned long long)value(u));
+  };
+  const uint64_t* tr = traffic;
+  auto mc = [&](uint32_t u) { return (uint64_t)mesh_count[u]; };
+  family("libp2p_peers", "gauge", "total connected peers", false, deg);
+  family("libp2p_pubsub_peers", "gauge", "pubsub peer instances", false, deg);
+  family("libp2p_pubsub_topics", "gauge", "pubsub subscribed topics", false, [](uint32_t) { return 1ull; });
+  family("libp2p_gossipsub_peers_per_topic_mesh", "gauge", "gossipsub peers per topic in mesh", true, mc);
+  family("libp2p_gossipsub_peers_per_topic_gossipsub", "gauge", "gossipsub peers per topic in gossipsub", true, deg);
+  // update_health (metrics.rs:158-176) over the one topic
+  family("libp2p_gossipsub_no_peers_topics", "gauge", "number of topics in mesh with no peers", false,
+         [&](uint32_t u) { return mc(u) == 0 ? 1ull : 0ull; });
+  family("libp2p_gossipsub_low_peers_topics", "gauge",
+         "number of topics in mesh with at least one but below dlow peers", false,
+         [&](uint32_t u) { return mc(u) > 0 && mc(u) < cfg->d_lo ? 1ull : 0ull; });
+  family("libp2p_gossipsub_healthy_peers_topics", "gauge", "number of topics in mesh with at least dlow peers",
+         false, [&](uint32_t u) { return mc(u) >= cfg->d_lo ? 1ull : 0ull; });
+  auto rcv = [&](uint32_t u) { return tr[(size_t)u * GS_TRAFFIC_COLS + GS_TR_RECEIVED]; };
+  family("libp2p_gossipsub_received", "counter", "number of messages received (deduplicated)", false, rcv);
+  family("libp2p_pubsub_messages_published", "counter", "published messages", true,
+         [&](uint32_t u) { return tr[(size_t)u * GS_TRAFFIC_COLS + GS_TR_PUBLISHED]; });
+  family("libp2p_pubsub_validation_success", "counter", "pubsub successfully validated messages", false, rcv);
+  family("libp2p_pubsub_validation_failure", "counter", "pubsub failed validated messages", false,
+         [](uint32_t) { return 0ull; });
+  family("libp2p_pubsub_received_subscriptions", "counter", "pubsub received subscriptions", true, deg);
+  family("libp2p_pubsub_received_unsubscriptions", "counter", "pubsub received unsubscriptions", true,
+         [](uint32_t) { return 0ull; });
+  fprintf(f, "# EOF\n");
+  if (fclose(f)) return GS_EINVAL;
+  return GS_OK;
+}
+
 // shadow/run.sh:34-36 + shadow/README.md:76-78: publisher_id, rotation 0/1,
 // inter_message_delay. tx_time is the publish instant (main.rs:105-111).
 extern "C" gs_status gs_schedule_runsh(uint32_t n_msgs, uint32_t peers, uint32_t publisher_id,

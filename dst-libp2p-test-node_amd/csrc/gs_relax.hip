@@ -214,7 +214,7 @@ struct TrafficArgs {
   const uint32_t* col;
   uint64_t* traffic;       // [N][GS_TRAFFIC_COLS]
   uint64_t W, pk, hdr;     // wire bytes, packets, header bytes of one fragment send
-  uint32_t N, L, FP, Fe, S, sb, tshift, idw, flood;
+  uint32_t N, L, FP, Fe, S, sb, tshift, idw, flood, collide;
 };
 
 // Per-peer traffic of a finished batch (gs_set_traffic), from the final keys:
@@ -232,13 +232,20 @@ __global__ __launch_bounds__(TB) void k_traffic(TrafficArgs a) {
     const uint32_t e = lane < (int)MESH_W ? a.mesh[(size_t)u * MESH_W + lane] : EMPTY;
     const uint32_t deg = (uint32_t)__popcll(__ballot(e != EMPTY));
     const uint32_t su = a.stage[u];
-    uint32_t cnt = 0;
+    uint32_t cnt = 0, done = 0;
     for (uint32_t i0 = 0; i0 < a.L; i0 += 64) {
       const uint32_t i = i0 + lane;
       const bool in = i < a.L && (i & (FP - 1)) < a.Fe;
       const uint64_t key = in ? a.keys[(size_t)u * a.L + i] : INF64;
       const uint32_t pm = in ? a.pub[i / FP] : EMPTY;
       const bool got = key != INF64 && pm != u;
+      {  // completed messages (reassembly, main.rs:79-99): every fragment of the group received
+        constexpr uint64_t gmask = (FP == 64) ? ~0ull : ((1ull << FP) - 1);
+        const uint64_t ok = __ballot(i < a.L && ((i & (FP - 1)) >= a.Fe || got));
+        const bool lead = (lane & (FP - 1)) == 0 && i < a.L && got && !a.collide &&
+                          ((ok >> (lane & ~(FP - 1))) & gmask) == gmask;
+        done += (uint32_t)__popcll(__ballot(lead));
+      }
       const uint32_t src = (uint32_t)(key & smask);
       const uint64_t t = key >> a.tshift;
       for (uint32_t k = 0; k < deg; k++) {  // wave-uniform
@@ -253,11 +260,12 @@ __global__ __launch_bounds__(TB) void k_traffic(TrafficArgs a) {
       }
     }
     const uint64_t tot = wave_sum((uint64_t)cnt);
-    if (lane == 0 && tot) {
+    if (lane == 0 && (tot || done)) {
       uint64_t* r = a.traffic + (size_t)u * GS_TRAFFIC_COLS;
       r[GS_TR_TX_BYTES] += tot * a.W;
       r[GS_TR_TX_PKTS] += tot * a.pk;
       r[GS_TR_TX_HDR] += tot * a.hdr;
+      r[GS_TR_RECEIVED] += done;
     }
     if (cnt) {
       uint64_t* r = a.traffic + (size_t)(e & 0xFFFFFFu) * GS_TRAFFIC_COLS;
@@ -284,6 +292,7 @@ __global__ __launch_bounds__(TB) void k_traffic_pub(TrafficArgs a) {
     atomicAdd((unsigned long long*)&r[GS_TR_TX_BYTES], n * a.W);
     atomicAdd((unsigned long long*)&r[GS_TR_TX_PKTS], n * a.pk);
     atomicAdd((unsigned long long*)&r[GS_TR_TX_HDR], n * a.hdr);
+    atomicAdd((unsigned long long*)&r[GS_TR_PUBLISHED], 1ull);
   }
   for (uint32_t j = threadIdx.x; j < deg; j += TB) {
     uint64_t* r = a.traffic + (size_t)(tg[j] & 0xFFFFFFu) * GS_TRAFFIC_COLS;
@@ -429,6 +438,7 @@ static void launch_traffic(Ctx& c, const Batch& b) {
   ta.N = c.cfg.peers; ta.L = b.L; ta.FP = b.FP; ta.Fe = b.Fe; ta.S = c.S; ta.sb = b.sb; ta.tshift = b.tshift;
   ta.idw = (c.cfg.idontwant && b.payload >= c.cfg.idontwant) ? 1 : 0;
   ta.flood = c.cfg.flood_publish;
+  ta.collide = b.collide ? 1 : 0;
   const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(((uint64_t)ta.N + 3) / 4,
                                                                            (uint64_t)c.num_cus * 8));
   switch (b.FP) {

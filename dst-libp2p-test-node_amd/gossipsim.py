@@ -80,6 +80,7 @@ SIGNATURES = {
     "gs_write_shadow_heartbeat": (i32, [ctypes.c_char_p, u32, P(u64), u64]),
     "gs_links_from_gml": (i32, [ctypes.c_char_p, u32, u32, P(u32), P(u64), P(u64), P(u64)]),
     "gs_shadow_hosts": (i32, [ctypes.c_char_p, u32, P(u8)]),
+    "gs_write_node_metrics": (i32, [P(GsConfig), ctypes.c_char_p, P(u64), P(u8), P(u64)]),
     "gs_set_traffic": (i32, [ctypes.c_void_p, u32]),
     "gs_get_traffic": (i32, [ctypes.c_void_p, P(u64)]),
     "gs_topogen_links": (i32, [u32, u32, u32, u32, u32, u32, P(u64), P(u64)]),
@@ -149,16 +150,27 @@ def wire_packets(payload, muxer="yamux", signed=True):
     return pk.value, hd.value
 
 
-TRAFFIC_COLS = ("tx_bytes", "rx_bytes", "tx_packets", "rx_packets", "tx_header_bytes", "rx_header_bytes")
+TRAFFIC_COLS = ("tx_bytes", "rx_bytes", "tx_packets", "rx_packets", "tx_header_bytes", "rx_header_bytes",
+                "received", "published")
 
 
 def write_shadow_heartbeat(path, traffic, sim_seconds=900):
-    """Per-peer traffic [N, 6] as Shadow tracker "[node]" lines (shadow/summary_shadowlog.awk);
+    """Per-peer traffic [N, 8] as Shadow tracker "[node]" lines (shadow/summary_shadowlog.awk);
     sim_seconds defaults to topogen's 15-minute stop time (shadow/topogen.py:82)."""
     tr = np.ascontiguousarray(traffic, np.uint64)
     rc = lib().gs_write_shadow_heartbeat(path.encode(), tr.shape[0], _ptr(tr, u64), sim_seconds)
     if rc:
         raise GossipSimError(rc, "gs_write_shadow_heartbeat failed")
+
+
+def write_node_metrics(cfg, path, row_ptr, mesh_count, traffic):
+    """OpenMetrics text of the test node's metrics for every peer (gs_write_node_metrics)."""
+    row = np.ascontiguousarray(row_ptr, np.uint64)
+    mc = np.ascontiguousarray(mesh_count, np.uint8)
+    tr = np.ascontiguousarray(traffic, np.uint64)
+    rc = lib().gs_write_node_metrics(ctypes.byref(cfg.c), path.encode(), _ptr(row, u64), _ptr(mc, u8), _ptr(tr, u64))
+    if rc:
+        raise GossipSimError(rc, "gs_write_node_metrics failed")
 
 
 def links_from_gml(path, shortest=False):
@@ -402,10 +414,14 @@ class Simulator:
         self._check(lib().gs_set_traffic(self.ctx, 1 if on else 0))
 
     def traffic(self):
-        """-> uint64 [N, 6] in TRAFFIC_COLS order."""
+        """-> uint64 [N, 8] in TRAFFIC_COLS order."""
         tr = np.zeros((self.peers, len(TRAFFIC_COLS)), np.uint64)
         self._check(lib().gs_get_traffic(self.ctx, _ptr(tr, u64)))
         return tr
+
+    def write_node_metrics(self, path):
+        """Every peer's Prometheus metrics (rust-test-node/src/metrics.rs names) after traffic runs."""
+        write_node_metrics(self.cfg, path, self.csr()[0], self.mesh()[1], self.traffic())
 
     def write_latency_log(self, path, res):
         """Arrival lines as `grep -rne 'milliseconds\\|BW' shadow.data/` prints them."""

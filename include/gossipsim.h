@@ -219,7 +219,10 @@ void gs_wire_packets(uint64_t payload, uint32_t muxer, uint32_t signed_msgs, uin
 
 /* Columns of a per-peer traffic row (gs_get_traffic). */
 enum { GS_TR_TX_BYTES = 0, GS_TR_RX_BYTES = 1, GS_TR_TX_PKTS = 2, GS_TR_RX_PKTS = 3,
-       GS_TR_TX_HDR = 4, GS_TR_RX_HDR = 5, GS_TRAFFIC_COLS = 6 };
+       GS_TR_TX_HDR = 4, GS_TR_RX_HDR = 5,
+       GS_TR_RECEIVED = 6,   /* completed messages (main.rs:94 inc_received_message)   */
+       GS_TR_PUBLISHED = 7,  /* messages published (main.rs:515 inc_messages_published) */
+       GS_TRAFFIC_COLS = 8 };
 
 /* Shadow's per-host heartbeat counters for the same runs, one "[node]" line
  * per peer as Shadow's tracker logs them (recv/send bytes, then inbound and
@@ -228,6 +231,18 @@ enum { GS_TR_TX_BYTES = 0, GS_TR_RX_BYTES = 1, GS_TR_TX_PKTS = 2, GS_TR_RX_PKTS 
  * [peers][GS_TRAFFIC_COLS]. Host names are pod-<id> (topogen.py:118). */
 gs_status gs_write_shadow_heartbeat(const char* path, uint32_t peers, const uint64_t* traffic,
                                     uint64_t sim_seconds);
+
+/* The test node's Prometheus metrics (rust-test-node/src/metrics.rs:13-199,
+ * names shared with the go and nim nodes) for every peer, in the OpenMetrics
+ * text format prometheus-client encodes (counters with _total, "# EOF"), one
+ * series per peer labelled peer="pod-<id>": connected / pubsub peers and
+ * subscriptions = CSR degree, topics = 1, mesh peers = mesh_count, topic
+ * health buckets against cfg->d_lo (metrics.rs:158-176), received / validated
+ * and published messages from the traffic columns. Arrays are host copies:
+ * row_ptr[peers+1] (gs_get_csr), mesh_count[peers] (gs_get_mesh),
+ * traffic[peers][GS_TRAFFIC_COLS] (gs_get_traffic). */
+gs_status gs_write_node_metrics(const gs_config* cfg, const char* path, const uint64_t* row_ptr,
+                                const uint8_t* mesh_count, const uint64_t* traffic);
 
 /* ---- context lifecycle (replaces SwarmBuilder + build_behaviour, main.rs:391-440) ---- */
 

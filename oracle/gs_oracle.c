@@ -711,8 +711,8 @@ static int run_impl(const or_params* p, const uint64_t* row_ptr, const uint32_t*
         uint64_t wire = or_wire_bytes(payload, p->muxer, p->signed_msgs), wpk = 0, whd = 0;
         or_wire_packets(payload, p->muxer, p->signed_msgs, &wpk, &whd);
         /* per-peer traffic: a send adds to the sender's tx, an arrival to the receiver's rx */
-#define TR_SEND(x) if (tr) { tr[(size_t)(x) * 6 + 0] += wire; tr[(size_t)(x) * 6 + 2] += wpk; tr[(size_t)(x) * 6 + 4] += whd; }
-#define TR_RECV(x) if (tr) { tr[(size_t)(x) * 6 + 1] += wire; tr[(size_t)(x) * 6 + 3] += wpk; tr[(size_t)(x) * 6 + 5] += whd; }
+#define TR_SEND(x) if (tr) { tr[(size_t)(x) * 8 + 0] += wire; tr[(size_t)(x) * 8 + 2] += wpk; tr[(size_t)(x) * 8 + 4] += whd; }
+#define TR_RECV(x) if (tr) { tr[(size_t)(x) * 8 + 1] += wire; tr[(size_t)(x) * 8 + 3] += wpk; tr[(size_t)(x) * 8 + 5] += whd; }
         const uint64_t tp = sched_t[mi];
         mesh_src msg_ms = *ms0;
         msg_ms.h_cap = epoch_at(p, tp) + p->churn_horizon;
@@ -732,6 +732,7 @@ static int run_impl(const or_params* p, const uint64_t* row_ptr, const uint32_t*
             continue;
         }
         /* publisher: self key, flood through the uplink FIFO */
+        if (tr) tr[(size_t)pub * 8 + 7] += 1; /* published (main.rs:515) */
         uint32_t sp = stage[pub];
         for (uint32_t f = 0; f < Fe; f++) { best[(size_t)pub * F + f] = (uint64_t)pub; fin[(size_t)pub * F + f] = 1; }
         if (p->lazy_gossip)
@@ -846,6 +847,7 @@ static int run_impl(const or_params* p, const uint64_t* row_ptr, const uint32_t*
             hops[o] = (uint8_t)((mk >> sb) & hmask);
             uint64_t ms_ = trel / 1000000ULL;
             st->deliveries++;
+            if (tr) tr[(size_t)u * 8 + 6] += 1; /* received (main.rs:94) */
             st->latency_sum_ms += ms_;
             if (ms_ > st->latency_max_ms) st->latency_max_ms = ms_;
         }
@@ -877,8 +879,9 @@ int or_run_churn(const or_params* p, const uint64_t* row_ptr, const uint32_t* co
                     n_msgs, t_complete, hops, st, NULL);
 }
 
-/* or_run plus per-peer traffic tr[N][6] (tx bytes, rx bytes, tx packets, rx
- * packets, tx header bytes, rx header bytes), accumulated (caller zeroes). */
+/* or_run plus per-peer traffic tr[N][8] (tx bytes, rx bytes, tx packets, rx
+ * packets, tx header bytes, rx header bytes, completed messages, published
+ * messages), accumulated (caller zeroes). */
 int or_run_traffic(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
                    const uint32_t* mesh, const uint8_t* cnt, const uint8_t* stage, uint32_t S,
                    const uint64_t* lat_ns, const uint64_t* bw_up, const uint64_t* bw_dn,

@@ -232,7 +232,7 @@ def wire_packets(payload, muxer=0, signed=1):
 
 
 def run(p, row_ptr, col, mesh, cnt, stage, lat, bw_up, bw_dn, sched_t, sched_pub, sched_size, traffic=None):
-    """traffic: optional uint64 [N, 6] accumulated per-peer counters (or_run_traffic)."""
+    """traffic: optional uint64 [N, 8] accumulated per-peer counters (or_run_traffic)."""
     N = p.peers
     S = lat.shape[0]
     M = len(sched_t)
@@ -254,7 +254,7 @@ def run(p, row_ptr, col, mesh, cnt, stage, lat, bw_up, bw_dn, sched_t, sched_pub
     if traffic is None:
         rc = lib().or_run(*args)
     else:
-        assert traffic.dtype == np.uint64 and traffic.shape == (N, 6) and traffic.flags.c_contiguous
+        assert traffic.dtype == np.uint64 and traffic.shape == (N, 8) and traffic.flags.c_contiguous
         rc = lib().or_run_traffic(*args, _p(traffic, ctypes.c_uint64))
     if rc:
         raise ValueError("or_run rc=%d" % rc)
@@ -263,7 +263,7 @@ def run(p, row_ptr, col, mesh, cnt, stage, lat, bw_up, bw_dn, sched_t, sched_pub
 
 
 def simulate(p, stages=1, links=(50, 50, 50, 50), mode=0, sched=None, max_hb=400, traffic=False):
-    """Whole pipeline on the CPU: links -> topology -> mesh -> run (+ per-peer traffic [N, 6])."""
+    """Whole pipeline on the CPU: links -> topology -> mesh -> run (+ per-peer traffic [N, 8])."""
     bl, bh, ll, lh = links
     lat, bw = topogen_links(stages, bl, bh, ll, lh, mode)
     stage = (np.arange(p.peers) % stages).astype(np.uint8)
@@ -279,7 +279,7 @@ def simulate(p, stages=1, links=(50, 50, 50, 50), mode=0, sched=None, max_hb=400
         tc, hops, stats = run_churn(p, row_ptr, col, snaps, h_lo, stage, lat, bw, bw, t, pub, size)
         out.update(snaps=snaps, h_lo=h_lo)
     else:
-        tr = np.zeros((p.peers, 6), np.uint64) if traffic else None
+        tr = np.zeros((p.peers, 8), np.uint64) if traffic else None
         tc, hops, stats = run(p, row_ptr, col, mesh, cnt, stage, lat, bw, bw, t, pub, size, traffic=tr)
         if traffic:
             out["traffic"] = tr

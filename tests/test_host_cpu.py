@@ -101,6 +101,33 @@ def test_shadow_heartbeat_round_trips_through_reference_awk(tmp_path):
                                                   int(tr[:, 5].sum()), int((tr[:, 1] - tr[:, 5]).sum())]
 
 
+def test_node_metrics_openmetrics(tmp_path):
+    """rust-test-node's metric names (metrics.rs:60-129) per peer from the simulator's counters."""
+    p = oracle.params(peers=120, seed=6)
+    t = np.uint64(gossipsim.T0_NS) + np.arange(5, dtype=np.uint64) * np.uint64(10 ** 9)
+    pubs = np.array([0, 7, 7, 60, 119])
+    r = oracle.simulate(p, 5, (50, 150, 40, 130), sched=(t, pubs, np.full(5, 15000)), traffic=True)
+    cfg = gossipsim.PeerConfig(peers=120)
+    out = str(tmp_path / "metrics.txt")
+    gossipsim.write_node_metrics(cfg, out, r["row_ptr"], r["cnt"], r["traffic"])
+    text = open(out).read()
+    assert text.endswith("# EOF\n")
+    vals = {}
+    for ln in text.splitlines():
+        m = re.match(r'(\w+)\{(?:topic="test",)?peer="pod-(\d+)"\} (\d+)$', ln)
+        if m:
+            vals.setdefault(m.group(1), {})[int(m.group(2))] = int(m.group(3))
+    deg = np.diff(r["row_ptr"].astype(np.int64))
+    assert [vals["libp2p_peers"][u] for u in range(120)] == deg.tolist()
+    assert [vals["libp2p_gossipsub_peers_per_topic_mesh"][u] for u in range(120)] == r["cnt"].tolist()
+    recv = (r["t_complete"] != np.iinfo(np.uint64).max).sum(axis=0) - np.bincount(pubs, minlength=120)
+    assert [vals["libp2p_gossipsub_received_total"][u] for u in range(120)] == recv.tolist()
+    assert vals["libp2p_pubsub_messages_published_total"][7] == 2 and sum(
+        vals["libp2p_pubsub_messages_published_total"].values()) == 5
+    assert all(vals["libp2p_gossipsub_healthy_peers_topics"][u] == (r["cnt"][u] >= 4) for u in range(120))
+    assert "# TYPE libp2p_gossipsub_received counter" in text
+
+
 @pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "topogen_*.json"))))
 @pytest.mark.parametrize("shortest", [False, True])
 def test_topogen_links_match_oracle_and_fixture(path, shortest):

@@ -311,6 +311,9 @@ def test_traffic_identities(kw):
     assert tr[:, 0].sum() == tr[:, 1].sum() == st["relaxations"] * W
     assert tr[:, 2].sum() == st["relaxations"] * pk and tr[:, 4].sum() == st["relaxations"] * hd
     assert (tr[:, 0] % W == 0).all() and (tr[:, 1] >= W).all()  # everyone receives at least once
+    assert tr[:, 6].sum() == st["deliveries"] and tr[:, 7].sum() == st["messages"] == 4
+    got = (r["t_complete"] != np.iinfo(np.uint64).max).sum(axis=0) - np.bincount([3, 50, 120, 299], minlength=300)
+    np.testing.assert_array_equal(tr[:, 6], got)
 
 
 def test_stats_identities():
