@@ -25,7 +25,9 @@ void usage() {
           "usage: gossipsim-node [-bl MBIT] [-bh MBIT] [-ll MS] [-lh MS] [-st STAGES] [--shortest]\n"
           "         [-s MSG_BYTES] [-m MESSAGES] [--publisher ID] [--rotation 0|1]\n"
           "         [--delay-ms MS] [--t0-s SECONDS] [--max-heartbeats H] [--latencies PATH]\n"
-          "env: PEERS CONNECTTO FRAGMENTS MUXER MAXCONNECTIONS GOSSIPSUB_* SELFTRIGGER GS_SEED GS_BATCH GS_DEVICE\n");
+          "         [--gml network_topology.gml --yaml shadow.yaml] [--shadowlog PATH] [--metrics PATH]\n"
+          "env: PEERS CONNECTTO FRAGMENTS MUXER MAXCONNECTIONS GOSSIPSUB_* SELFTRIGGER GS_NODE GS_SEED GS_BATCH\n"
+          "     GS_DEVICE\n");
 }
 
 int die(gs_ctx* ctx, gs_status st, const char* what) {
@@ -41,7 +43,7 @@ int main(int argc, char** argv) {
   uint32_t bl = 50, bh = 50, ll = 100, lh = 100, stages = 1, mode = GS_LINKS_DIRECT;
   uint32_t msg_size = 1500, n_msgs = 10, publisher = 6, rotation = 1, max_hb = 400;
   uint64_t delay_ms = 1000, t0_s = 946684800ull + 500ull;  // Shadow epoch + injector start
-  std::string latencies;
+  std::string latencies, gml, yaml, shadowlog, metrics;
   for (int i = 1; i < argc; i++) {
     std::string a = argv[i];
     auto next = [&](void) -> const char* {
@@ -62,6 +64,10 @@ int main(int argc, char** argv) {
     else if (a == "--t0-s") t0_s = strtoull(next(), nullptr, 10);
     else if (a == "--max-heartbeats") max_hb = (uint32_t)atoi(next());
     else if (a == "--latencies") latencies = next();
+    else if (a == "--gml") gml = next();            // a Shadow experiment's network graph ...
+    else if (a == "--yaml") yaml = next();          // ... and its host placement (topogen.py output)
+    else if (a == "--shadowlog") shadowlog = next(); // tracker counters for summary_shadowlog.awk
+    else if (a == "--metrics") metrics = next();    // the node metrics (rust-test-node/src/metrics.rs)
     else { usage(); return 2; }
   }
   gs_config cfg;
@@ -70,14 +76,38 @@ int main(int argc, char** argv) {
   gs_status st = gs_config_from_env(&cfg, err, sizeof(err));
   if (st != GS_OK) { fprintf(stderr, "Error reading peer settings: %s\n", err); return 1; }
 
-  std::vector<uint64_t> lat((size_t)stages * stages), bw(stages);
-  st = gs_topogen_links(stages, bl, bh, ll, lh, mode, lat.data(), bw.data());
-  if (st != GS_OK) { fprintf(stderr, "invalid topogen parameters\n"); return 1; }
+  std::vector<uint64_t> lat((size_t)stages * stages), bw(stages), bw_dn;
+  std::vector<uint8_t> stage_of_peer;
+  if (!gml.empty()) {  // links straight from the Shadow experiment files
+    if (yaml.empty()) { fprintf(stderr, "--gml needs --yaml (host placement)\n"); return 2; }
+    uint32_t V = 0;
+    gs_links_from_gml(gml.c_str(), mode, 0, &V, nullptr, nullptr, nullptr);
+    lat.assign((size_t)V * V, 0);
+    bw.assign(V, 0);
+    bw_dn.assign(V, 0);
+    if ((st = gs_links_from_gml(gml.c_str(), mode, V, &V, lat.data(), bw.data(), bw_dn.data())) != GS_OK) {
+      fprintf(stderr, "cannot read %s (%d)\n", gml.c_str(), st);
+      return 1;
+    }
+    stages = V;
+    stage_of_peer.assign(cfg.peers, 0);
+    if ((st = gs_shadow_hosts(yaml.c_str(), cfg.peers, stage_of_peer.data())) != GS_OK) {
+      fprintf(stderr, "cannot place the %u peers with %s (%d)\n", cfg.peers, yaml.c_str(), st);
+      return 1;
+    }
+  } else {
+    st = gs_topogen_links(stages, bl, bh, ll, lh, mode, lat.data(), bw.data());
+    if (st != GS_OK) { fprintf(stderr, "invalid topogen parameters\n"); return 1; }
+    bw_dn = bw;
+  }
 
   gs_ctx* ctx = nullptr;
   if ((st = gs_create(&cfg, &ctx)) != GS_OK) return die(nullptr, st, "gs_create");
-  if ((st = gs_set_links(ctx, stages, lat.data(), bw.data(), bw.data(), nullptr)) != GS_OK)
+  if ((st = gs_set_links(ctx, stages, lat.data(), bw.data(), bw_dn.data(),
+                         stage_of_peer.empty() ? nullptr : stage_of_peer.data())) != GS_OK)
     return die(ctx, st, "gs_set_links");
+  const bool counters = !shadowlog.empty() || !metrics.empty();
+  if (counters && (st = gs_set_traffic(ctx, 1)) != GS_OK) return die(ctx, st, "gs_set_traffic");
   if ((st = gs_build_topology(ctx)) != GS_OK) return die(ctx, st, "gs_build_topology");
   uint32_t epochs = 0;
   if ((st = gs_mesh_converge(ctx, max_hb, &epochs)) != GS_OK) return die(ctx, st, "gs_mesh_converge");
@@ -109,6 +139,18 @@ int main(int argc, char** argv) {
   if (!latencies.empty() &&
       (st = gs_write_node_log(&cfg, latencies.c_str(), sched.data(), n_msgs, tc.data())) != GS_OK)
     return die(ctx, st, "gs_write_node_log");
+  if (counters) {
+    std::vector<uint64_t> tr((size_t)cfg.peers * GS_TRAFFIC_COLS), row((size_t)cfg.peers + 1);
+    std::vector<uint8_t> mc(cfg.peers);
+    if ((st = gs_get_traffic(ctx, tr.data())) != GS_OK) return die(ctx, st, "gs_get_traffic");
+    if ((st = gs_get_csr(ctx, row.data(), nullptr, nullptr)) != GS_OK) return die(ctx, st, "gs_get_csr");
+    if ((st = gs_get_mesh(ctx, nullptr, mc.data())) != GS_OK) return die(ctx, st, "gs_get_mesh");
+    const uint64_t end_s = sched.empty() ? 0 : (sched.back().t_pub_ns / 1000000000ull) - 946684800ull + 1;
+    if (!shadowlog.empty() && (st = gs_write_shadow_heartbeat(shadowlog.c_str(), cfg.peers, tr.data(), end_s)) != GS_OK)
+      return die(ctx, st, "gs_write_shadow_heartbeat");
+    if (!metrics.empty() && (st = gs_write_node_metrics(&cfg, metrics.c_str(), row.data(), mc.data(), tr.data())) != GS_OK)
+      return die(ctx, st, "gs_write_node_metrics");
+  }
   gs_destroy(ctx);
   return 0;
 }

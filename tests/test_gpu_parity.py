@@ -187,6 +187,33 @@ def test_shadow_experiment_files_drive_the_run():
     np.testing.assert_array_equal(res["hops"], ref["hops"])
 
 
+def test_cli_runs_a_shadow_experiment(tmp_path):
+    """gossipsim-node (the C++ host) on topogen's GML + shadow.yaml with the
+    reference's env knobs: its arrival log equals the Python host's for the
+    same run, and it writes the tracker heartbeat and metrics files."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(gossipsim.LIB_PATH), "gossipsim-node")
+    env = dict(os.environ, PEERS="100", CONNECTTO="10", FRAGMENTS="2", MUXER="yamux", GS_SEED="5")
+    out = {k: str(tmp_path / k) for k in ("lat", "shadowlog", "metrics")}
+    subprocess.run([exe, "--gml", os.path.join(GOLDEN, "topogen_runsh_example.gml"), "--yaml",
+                    os.path.join(GOLDEN, "topogen_runsh_example.yaml"), "-s", "15000", "-m", "4",
+                    "--publisher", "6", "--rotation", "1", "--delay-ms", "1000", "--latencies", out["lat"],
+                    "--shadowlog", out["shadowlog"], "--metrics", out["metrics"]],
+                   env=env, check=True, timeout=60)
+    p = oracle.params(peers=100, seed=5, fragments=2)
+    sim = gossipsim.Simulator(**_knobs(p))
+    sim.set_shadow_links(os.path.join(GOLDEN, "topogen_runsh_example.gml"),
+                         os.path.join(GOLDEN, "topogen_runsh_example.yaml"))
+    sim.connect_gossipsub_peers()
+    sim.mesh_converge()
+    sched = gossipsim.schedule_runsh(4, 100, 6, 1, gossipsim.T0_NS, gossipsim.DELAY_NS, 15000)
+    res = sim.run(sched)
+    sim.write_latency_log(str(tmp_path / "py_lat"), res)
+    assert open(out["lat"]).read() == open(str(tmp_path / "py_lat")).read()
+    assert len(open(out["shadowlog"]).read().splitlines()) == 100
+    assert open(out["metrics"]).read().endswith("# EOF\n")
+
+
 def test_fragment_collision_defect_d8():
     p = oracle.params(peers=100, fragments=4)
     sim, res = compare(p, 1, (50, 50, 50, 50), _sched(2, 100, size=40))
