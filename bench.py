@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--max-heartbeats", type=int, default=400)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU oracle sample budget (0=off)")
+    ap.add_argument("--configs", type=int, default=1, help="also time BASELINE configs #1-#3 (1 GPU runs)")
     ap.add_argument("--mode", choices=("msg", "peer"), default="msg",
                     help="msg: message-sharded ranks (default); peer: peer-partitioned ranks")
     ap.add_argument("--also-peers", type=int, default=100_000,
@@ -170,6 +171,42 @@ def measure(args, sim, peers, world, rank, torch, dist):
     return max_elapsed, st, tot
 
 
+# BASELINE.json configs #1-#3 on one GPU, timed like the headline (inputs in HBM,
+# results left on the device): each is one Simulator with that config's knobs,
+# a short untimed warm-up run, then `msgs` messages timed. The peer-partitioned
+# config #4 is bench.py --mode peer.
+CONFIGS = {
+    "c1_1k_uniform_F1": dict(peers=1000, knobs={}, links=(1, 50, 50, 50, 50), fragments=1, batch=1024, msgs=1024),
+    "c2_10k_F8": dict(peers=10_000, knobs={}, links=(5, 50, 150, 40, 130), fragments=8, batch=128, msgs=1024),
+    "c3_100k_gossip_churn": dict(
+        peers=100_000, links=(5, 50, 150, 40, 130), fragments=1, batch=64, msgs=256,
+        knobs=dict(lazy_gossip=1, churn_ppm=10_000, churn_down=10, churn_horizon=16,
+                   heartbeat_ns=1_000_000_000, hb_phase_ns=gossipsim.T0_NS - 20 * 1_000_000_000 + 370_000_000)),
+}
+
+
+def config_rates(args, local):
+    out = {}
+    for name, c in CONFIGS.items():
+        sim = gossipsim.Simulator(peers=c["peers"], batch=c["batch"], fragments=c["fragments"], seed=args.seed,
+                                  device=local, **c["knobs"])
+        sim.set_topogen_links(c["links"][0], *c["links"][1:])
+        sim.connect_gossipsub_peers()
+        sim.mesh_converge(args.max_heartbeats)
+        sim.run(gossipsim.shard_messages(0, 0, 1, c["batch"], c["peers"], args.msg_size), collect=False)
+        sim.reset_stats()
+        sched = gossipsim.shard_messages(1, 0, 1, c["msgs"], c["peers"], args.msg_size)  # after the warm-up's
+        t0 = time.perf_counter()
+        sim.run(sched, collect=False)
+        dt = time.perf_counter() - t0
+        st = sim.stats()
+        out[name] = {"value": st["deliveries"] / dt, "unit": "deliveries/s", "msgs": c["msgs"],
+                     "ms": dt * 1e3, "deliveries": int(st["deliveries"]),
+                     "kernel_path": "push (k_scan+k_frontier+k_gossip)" if c["knobs"] else "pull (k_pull)"}
+        sim.close()
+    return out
+
+
 def main():
     args = parse()
     world, rank, local, torch, dist = dist_setup()
@@ -215,6 +252,10 @@ def main():
             "timing": "HIP events on the library stream around every window pass",
             "pushes_per_relaxation": st["pushes"] / max(1, st["relaxations"])}
 
+    cfg_rates = None
+    if world == 1 and args.configs and args.mode == "msg":
+        cfg_rates = config_rates(args, local)
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0 and args.mode == "msg":
         cpu = cpu_baseline(sim, args, S, links, args.cpu_seconds)
@@ -251,6 +292,7 @@ def main():
             "at_%dk_peers" % (args.also_peers // 1000) if extra else "at_second_size": extra,
             "roofline": roof,
             "cpu_baseline": cpu,
+            "configs_1gpu": cfg_rates,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

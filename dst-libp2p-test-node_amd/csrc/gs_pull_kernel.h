@@ -93,6 +93,17 @@ struct PullLds {
   uint16_t lst[PULL_WAVES][PULL_LMAX];
 };
 
+#ifdef GS_PULL_PROF
+// Diagnostic build only (scripts/pull_prof.py): per pass, summed over waves,
+// the shader clocks spent in each step of the row loop.
+__device__ unsigned long long g_pull_prof[32][8];
+#define PP_T(v) const uint64_t v = clock64()
+#define PP_ADD(k, x) pp[k] += (x)
+#else
+#define PP_T(v)
+#define PP_ADD(k, x)
+#endif
+
 template <int FP>
 __global__ __launch_bounds__(TB, 4) void k_pull(PullArgs a) {
   __shared__ PullLds Ls;
@@ -144,6 +155,9 @@ __global__ __launch_bounds__(TB, 4) void k_pull(PullArgs a) {
   uint64_t fd = 0, nr = 0, np = 0, nrec = 0;
   uint32_t nmh = ~0u;  // hi word of the min pending key over this wave's rows
   uint32_t err = 0;
+#ifdef GS_PULL_PROF
+  uint64_t pp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
 
   // Row headers are software-pipelined one row ahead: lane j < 16 holds mesh
   // entry j of the row, w's index in that neighbour's row, the length of the
@@ -159,6 +173,7 @@ __global__ __launch_bounds__(TB, 4) void k_pull(PullArgs a) {
     cm = a.chunkmin[(size_t)w * PULL_CH + lane];
   }
   for (; w < a.N; w += stride) {
+    PP_T(tA);
     const uint32_t w2 = w + stride;
     uint32_t ej2 = EMPTY, rj2 = 0, cj2 = 0, cm2 = ~0u;
     if (w2 < a.N && lane < (int)MESH_W) {  // w2 < N is wave-uniform
@@ -175,8 +190,11 @@ __global__ __launch_bounds__(TB, 4) void k_pull(PullArgs a) {
       nmh = umin32(nmh, cm);
       if (pull && lane < (int)MESH_W && ej2 != EMPTY) cj2 = rcnt[ej2 & 0xFFFFFFu];
       ej = ej2; rj = rj2; cj = cj2; cm = cm2;
+      PP_T(tS);
+      PP_ADD(0, tS - tA);
       continue;
     }
+    PP_ADD(5, 1);
     // 1. the due chunks into registers (up to 16 loads in flight per lane)
     const uint64_t* grow = a.keys + (size_t)w * LL;
     uint64_t v[PULL_CH];
@@ -257,6 +275,8 @@ __global__ __launch_bounds__(TB, 4) void k_pull(PullArgs a) {
       wave_lds_sync();
     }
     if (pull && lane < (int)MESH_W && ej2 != EMPTY) cj2 = rcnt[ej2 & 0xFFFFFFu];  // next row's lists
+    PP_T(tB);
+    PP_ADD(1, tB - tA);
     // 3. dense: merge, write back changed lanes, compact the arrivals of
     //    [wlo, whi) in place (groups of FP lanes), per-chunk min beyond it
     const bool chk_pub = wlo == 0;  // only window 0 can hold a publisher's own key
@@ -312,6 +332,8 @@ __global__ __launch_bounds__(TB, 4) void k_pull(PullArgs a) {
       }
     }
     wave_lds_sync();
+    PP_T(tC);
+    PP_ADD(2, tC - tB);
     // 4. sparse: forward targets, uplink FIFO and one record per arrival
     uint32_t ecnt = 0;
     if (cnt) {
@@ -351,6 +373,8 @@ __global__ __launch_bounds__(TB, 4) void k_pull(PullArgs a) {
         ecnt += (uint32_t)__popcll(wm);
       }
     }
+    PP_T(tD);
+    PP_ADD(3, tD - tC);
     // 5. new chunk minima: lanes 4c..4c+3 hold chunk c's; chunks that were not
     //    live keep theirs (their keys did not change and lie beyond the window)
     {
@@ -365,7 +389,13 @@ __global__ __launch_bounds__(TB, 4) void k_pull(PullArgs a) {
     if (lane == 0) wcnt[w] = ecnt;
     nrec += ecnt;
     ej = ej2; rj = rj2; cj = cj2; cm = cm2;
+    PP_T(tE);
+    PP_ADD(4, tE - tD);
   }
+#ifdef GS_PULL_PROF
+  if (lane == 0 && a.pass < 32)
+    for (int k = 0; k < 6; k++) atomicAdd(&g_pull_prof[a.pass][k], (unsigned long long)pp[k]);
+#endif
   for (int off = 32; off > 0; off >>= 1) nmh = umin32(nmh, __shfl_xor(nmh, off));
   const uint64_t nmin = nmh == ~0u ? INF64 : (uint64_t)nmh << 32;
   fd = wave_sum(fd);

@@ -536,6 +536,14 @@ static void run_pull_batch(Ctx& c, const Batch& b, EvFn& ev, size_t& n_ev, int d
   c.stats.relax_launches += pass;
 }
 
+#ifdef GS_PULL_PROF
+extern "C" int gs_debug_pull_prof(uint64_t* out) {  // 32 passes x 8 slots; read and clear
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pull_prof), sizeof(g_pull_prof)) != hipSuccess) return -1;
+  static const uint64_t zero[32 * 8] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_pull_prof), zero, sizeof(g_pull_prof)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_result_sink* sink) {
   const uint32_t N = c.cfg.peers, F = c.cfg.fragments, FP = pow2_at_least(F);
   const uint32_t Bmax = c.cfg.batch;
@@ -578,10 +586,6 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       c.d_ring_mesh.alloc((size_t)c.ring_R * N * MESH_W);
       c.d_ring_off.alloc((size_t)c.ring_R * w64);
     }
-  }
-  if (gossip) {
-    const uint64_t rmax = std::max<uint64_t>(c.cfg.d_lazy, (uint64_t)c.max_degree * c.cfg.gossip_factor_milli / 1000);
-    if (rmax > GOSSIP_R_MAX) c.fail(GS_EUNSUPPORTED, "gossip fan-out above 32 targets");
   }
   const size_t max_tiles = ((size_t)N * Bmax * FP + 63) / 64;
   c.d_keys.alloc((size_t)N * Bmax * FP);

@@ -493,7 +493,10 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
 // (m, f) by the IHAVE's arrival t_i sends IWANT, and v's answer is pushed with
 // key (t_i + lat(w,v) + ser_up(v) + lat(v,w) + dn, hops_v + 1, v). Deciding
 // here is exact: every key below hi is final, and every answer lands >= hi.
-constexpr uint32_t GOSSIP_R_MAX = 32;
+constexpr uint32_t GOSSIP_R_REG = 8;
+__device__ __forceinline__ bool pair_lt(uint64_t k1, uint32_t w1, uint64_t k2, uint32_t w2) {
+  return k1 < k2 || (k1 == k2 && w1 < w2);
+}
 
 template <int FP>
 __global__ __launch_bounds__(TB) void k_gossip(RelaxArgs a) {
@@ -539,40 +542,49 @@ __global__ __launch_bounds__(TB) void k_gossip(RelaxArgs a) {
         mrow[4 * q] = x.x & 0xFFFFFFu; mrow[4 * q + 1] = x.y & 0xFFFFFFu;
         mrow[4 * q + 2] = x.z & 0xFFFFFFu; mrow[4 * q + 3] = x.w & 0xFFFFFFu;
       }
-      uint64_t kk[GOSSIP_R_MAX];
-      uint32_t ww[GOSSIP_R_MAX];
-      uint32_t nsel = 0, nonmesh = 0;
-      // r smallest rng(GOSSIP, u, h, w) among non-mesh connections; r depends
-      // on |non-mesh|, so keep GOSSIP_R_MAX and cut after counting
-      for (uint64_t e = a.row[u]; e < a.row[u + 1]; e++) {
-        const uint32_t w = a.col[e];
+      // r smallest (rng(GOSSIP, u, h, w), w) among non-mesh connections. The
+      // first GOSSIP_R_REG stay sorted in registers (static indices: no
+      // scratch); r depends on |non-mesh|, so it is cut after counting, and
+      // the rare targets beyond GOSSIP_R_REG are found by rescanning for the
+      // next smallest pair.
+      uint64_t kk[GOSSIP_R_REG];
+      uint32_t ww[GOSSIP_R_REG];
+#pragma unroll
+      for (int q = 0; q < (int)GOSSIP_R_REG; q++) { kk[q] = ~0ull; ww[q] = ~0u; }
+      uint32_t nonmesh = 0;
+      const uint64_t e0 = a.row[u], e1 = a.row[u + 1];
+      auto eligible = [&](uint32_t w) {
         bool inm = false;
 #pragma unroll
         for (int q = 0; q < (int)MESH_W; q++) inm |= mrow[q] == w;
-        if (inm || (a.churn && ep_off(a, hab, w))) continue;
+        return !inm && !(a.churn && ep_off(a, hab, w));
+      };
+      for (uint64_t e = e0; e < e1; e++) {
+        const uint32_t w = a.col[e];
+        if (!eligible(w)) continue;
         nonmesh++;
         const uint64_t rk = rng(a.seed, P_GOSSIP, u, h, w);
-        if (nsel == GOSSIP_R_MAX && (kk[nsel - 1] < rk || (kk[nsel - 1] == rk && ww[nsel - 1] < w))) continue;
-        if (nsel == GOSSIP_R_MAX) nsel--;
-        int32_t j = (int32_t)nsel - 1;
-        while (j >= 0 && (kk[j] > rk || (kk[j] == rk && ww[j] > w))) { kk[j + 1] = kk[j]; ww[j + 1] = ww[j]; j--; }
-        kk[j + 1] = rk;
-        ww[j + 1] = w;
-        nsel++;
+        if (!pair_lt(rk, w, kk[GOSSIP_R_REG - 1], ww[GOSSIP_R_REG - 1])) continue;
+#pragma unroll
+        for (int q = (int)GOSSIP_R_REG - 1; q > 0; q--) {  // insert, shifting the larger pairs up
+          if (pair_lt(rk, w, kk[q - 1], ww[q - 1])) { kk[q] = kk[q - 1]; ww[q] = ww[q - 1]; }
+          else if (pair_lt(rk, w, kk[q], ww[q])) { kk[q] = rk; ww[q] = w; }
+        }
+        if (pair_lt(rk, w, kk[0], ww[0])) { kk[0] = rk; ww[0] = w; }
       }
       uint32_t r = (uint32_t)(((uint64_t)nonmesh * a.gf_milli) / 1000);
       if (r < a.d_lazy) r = a.d_lazy;
       if (r > nonmesh) r = nonmesh;
-      for (uint32_t q = 0; q < r; q++) {
-        const uint32_t w = ww[q], sw = a.stage[w];
+      auto ihave = [&](uint32_t w) {  // v's IHAVE to w; IWANT + answer if w has not seen it
+        const uint32_t sw = a.stage[w];
         const uint64_t ti = T + L.lat[sv * S + sw];
-        if (ti < lo || ti >= hi) continue;
+        if (ti < lo || ti >= hi) return;
         const uint64_t sd = L.sd[sw];
         const uint64_t A = ti + L.lat[sw * S + sv] + ser + L.lat[sv * S + sw] + (sd > ser ? sd - ser : 0);
-        if (a.churn && (ev_lost(a, m, ti, w) || ev_lost(a, m, A, w))) continue;  // IHAVE or answer lost
+        if (a.churn && (ev_lost(a, m, ti, w) || ev_lost(a, m, A, w))) return;  // IHAVE or answer lost
         const size_t dst = (size_t)w * LL + slot;
         const uint64_t kw = a.keys[dst];
-        if (kw != INF64 && (kw >> a.tshift) <= ti) continue;  // already seen: no IWANT
+        if (kw != INF64 && (kw >> a.tshift) <= ti) return;  // already seen: no IWANT
         iw++;
         if (A > a.tmax) err |= ERR_TIME;
         if (hp + 1 >= (1u << HOP_BITS)) err |= ERR_HOPS;
@@ -581,6 +593,24 @@ __global__ __launch_bounds__(TB) void k_gossip(RelaxArgs a) {
           atomicMin((unsigned long long*)&a.keys[dst], (unsigned long long)nk);
           nmin = nk < nmin ? nk : nmin;
         }
+      };
+#pragma unroll
+      for (int q = 0; q < (int)GOSSIP_R_REG; q++)
+        if ((uint32_t)q < r) ihave(ww[q]);
+      uint64_t pk = kk[GOSSIP_R_REG - 1];
+      uint32_t pw = ww[GOSSIP_R_REG - 1];
+      for (uint32_t q = GOSSIP_R_REG; q < r; q++) {  // rare: more than GOSSIP_R_REG targets
+        uint64_t bk = ~0ull;
+        uint32_t bw = ~0u;
+        for (uint64_t e = e0; e < e1; e++) {
+          const uint32_t w = a.col[e];
+          if (!eligible(w)) continue;
+          const uint64_t rk = rng(a.seed, P_GOSSIP, u, h, w);
+          if (pair_lt(pk, pw, rk, w) && pair_lt(rk, w, bk, bw)) { bk = rk; bw = w; }
+        }
+        ihave(bw);
+        pk = bk;
+        pw = bw;
       }
     }
     (void)smask;

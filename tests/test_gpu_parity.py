@@ -121,6 +121,17 @@ def test_lazy_gossip_ihave_iwant(frags):
     assert st["gossip_iwant"] == ref["stats"]["gossip_iwant"] > 0
 
 
+@pytest.mark.parametrize("factor,d_lazy", [(1000, 6), (500, 12)])
+def test_lazy_gossip_wide_fanout(factor, d_lazy):
+    """Gossip fan-out beyond the 8 targets k_gossip keeps in registers: the
+    rescan path for the next smallest (rng, id) pair must pick the oracle's
+    targets (gossip_factor 1.0 sends IHAVE to every non-mesh connection)."""
+    p = oracle.params(peers=1200, seed=43, lazy_gossip=1, gossip_factor_milli=factor, d_lazy=d_lazy,
+                      heartbeat_ns=100_000_000, hb_phase_ns=37_000_000)
+    sim, _ = compare(p, 3, (5, 20, 20, 80), _sched(16, 1200), batch=8)
+    assert sim.stats()["gossip_iwant"] > 0
+
+
 def test_lazy_gossip_default_heartbeat():
     p = oracle.params(peers=3000, seed=42, lazy_gossip=1)
     compare(p, 5, (50, 150, 40, 130), _sched(30, 3000), batch=16)
