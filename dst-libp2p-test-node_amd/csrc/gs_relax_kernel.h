@@ -70,18 +70,34 @@ struct RelaxArgs {
   uint32_t N, B, F, L, S, sb, tshift, launch, idw;
 };
 
+// n / d for n, d < 2^53: the correctly rounded double quotient is off by at
+// most one, fixed exactly in integers (a 64-bit integer division is a long
+// software sequence on gfx950)
+// row of lane index gid (32-bit division whenever the index fits)
+__device__ __forceinline__ uint32_t row_of(uint64_t gid, uint32_t LL) {
+  return gid < (1ull << 32) ? (uint32_t)gid / LL : (uint32_t)(gid / LL);
+}
+__device__ __forceinline__ uint64_t udiv53(uint64_t n, uint64_t d) {
+  uint64_t q = (uint64_t)((double)n / (double)d);
+  if (q * d > n) q--;
+  else if ((q + 1) * d <= n) q++;
+  return q;
+}
+
 // ---- churn helpers; m = message index within the batch ----
+// Epochs stay below 2^20 + horizon (gs_run checks the schedule), so the ring
+// index is a 32-bit remainder.
 template <class A>
 __device__ __forceinline__ uint64_t ev_epoch(const A& a, uint32_t m, uint64_t t) {  // t relative to t_pub
-  return a.q0[m] + (a.r0[m] + t) / a.hb_ns;
+  return a.q0[m] + udiv53(a.r0[m] + t, a.hb_ns);
 }
 template <class A>
 __device__ __forceinline__ bool ep_off(const A& a, uint64_t h, uint32_t w) {
-  return (a.ring_off[(size_t)(h % a.ring_R) * a.w64 + (w >> 6)] >> (w & 63)) & 1;
+  return (a.ring_off[(size_t)((uint32_t)h % a.ring_R) * a.w64 + (w >> 6)] >> (w & 63)) & 1;
 }
 template <class A>
 __device__ __forceinline__ const uint32_t* ep_mesh(const A& a, uint64_t h, uint32_t u) {
-  return a.ring_mesh + ((size_t)(h % a.ring_R) * a.N + u) * MESH_W;
+  return a.ring_mesh + ((size_t)((uint32_t)h % a.ring_R) * a.N + u) * MESH_W;
 }
 // a delivery to w at relative time t is lost: past the message's lifetime or w offline
 template <class A>
@@ -97,6 +113,38 @@ __device__ __forceinline__ uint64_t wave_min(uint64_t v) {
   }
   return v;
 }
+// Block-level flush of wave-reduced values: one device-scope atomic per block
+// instead of one per wave (same-address atomics serialize at the memory side,
+// and a grid-wide counter sees thousands of waves per launch). Every thread of
+// the block calls it. Wave wv stages its values at lds[wv * stride + k] (a
+// block-shared area the caller owns; with stride >= the values per wave each
+// wave touches only its own slot range). Slot 0 holds the min, slots
+// 1..NS the sums.
+template <int NW, int NS>
+__device__ __forceinline__ void block_flush(uint64_t wmin, const uint64_t (&ws)[NS], unsigned long long* pmin,
+                                            unsigned long long* const (&ps)[NS], uint64_t* lds, uint32_t stride) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) {
+    lds[wv * stride] = wmin;
+#pragma unroll
+    for (int k = 0; k < NS; k++) lds[wv * stride + 1 + k] = ws[k];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && pmin) {
+    uint64_t m = ~0ull;
+#pragma unroll
+    for (int i = 0; i < NW; i++) m = lds[i * stride] < m ? lds[i * stride] : m;
+    if (m != ~0ull) atomicMin(pmin, (unsigned long long)m);
+  }
+  if (threadIdx.x >= 64 && threadIdx.x < 64 + NS) {  // another wave does the sums
+    const int k = (int)threadIdx.x - 64;
+    uint64_t t = 0;
+#pragma unroll
+    for (int i = 0; i < NW; i++) t += lds[i * stride + 1 + k];
+    if (t && ps[k]) atomicAdd(ps[k], (unsigned long long)t);
+  }
+}
+
 __device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
   return v;
@@ -149,7 +197,7 @@ __device__ __forceinline__ bool gossip_done(const RelaxArgs& a) {
 // First gossip heartbeat index j0 (relative to the message's first heartbeat
 // rel0) with T_j0 >= t: heartbeats at rel0 + j*hb.
 __device__ __forceinline__ uint64_t first_hb(uint64_t t, uint64_t rel0, uint64_t hb) {
-  return t <= rel0 ? 0 : (t - rel0 + hb - 1) / hb;
+  return t <= rel0 ? 0 : udiv53(t - rel0 + hb - 1, hb);
 }
 
 // Uplink FIFO across one (u, m)'s fragments: the FP-aligned lane group folds
@@ -405,7 +453,7 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
     const bool valid = gid < a.total;
     const uint64_t key = valid ? a.keys[gid] : INF64;
     const uint64_t t = key >> a.tshift;
-    const uint32_t u = valid ? (uint32_t)(gid / LL) : 0;
+    const uint32_t u = valid ? row_of(gid, LL) : 0;
     const uint32_t slot = (uint32_t)(gid - (uint64_t)u * LL);
     const uint32_t pm = valid ? a.pub[slot / FP] : EMPTY;
     const bool pending = key != INF64;
@@ -474,17 +522,18 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
   }
   if (lane == 0) a.fr_cnt[wave] = cnt;
   nmin = wave_min(nmin);
-  if (lane == 0 && nmin != INF64)
-    atomicMin((unsigned long long*)&a.ctrl[(a.launch + 1) % 3], (unsigned long long)nmin);
   if constexpr (GOSSIP) {
     nonfin = wave_sum(nonfin);
     for (int off = 32; off > 0; off >>= 1) err |= __shfl_xor(err, off);
     if (lane == 0) {
       a.gl_cnt[wave] = gcnt;
-      if (nonfin) atomicAdd((unsigned long long*)&a.nonfinal[a.launch % 3], (unsigned long long)nonfin);
       if (err) atomicOr((unsigned*)&a.counters[C_ERR], err);
     }
   }
+  __shared__ uint64_t s_red[TB / 64 * 2];
+  const uint64_t ws[1] = {nonfin};
+  unsigned long long* const ps[1] = {GOSSIP ? (unsigned long long*)&a.nonfinal[a.launch % 3] : nullptr};
+  block_flush<TB / 64, 1>(nmin, ws, (unsigned long long*)&a.ctrl[(a.launch + 1) % 3], ps, s_red, 2);
 }
 
 // Lazy gossip of one bucket: for every listed final lane
@@ -518,7 +567,7 @@ __global__ __launch_bounds__(TB) void k_gossip(RelaxArgs a) {
     const uint64_t gid = a.gl_idx[seg + i];
     const uint64_t key = a.keys[gid];
     const uint64_t t = key >> a.tshift;
-    const uint32_t u = (uint32_t)(gid / LL), slot = (uint32_t)(gid - (uint64_t)u * LL);
+    const uint32_t u = row_of(gid, LL), slot = (uint32_t)(gid - (uint64_t)u * LL);
     const uint32_t m = slot / FP, sv = a.stage[u];
     const uint32_t hp = (uint32_t)((key >> a.sb) & ((1u << HOP_BITS) - 1));
     const uint64_t ser = L.su[sv];
@@ -654,7 +703,7 @@ __global__ __launch_bounds__(TB) void k_frontier(RelaxArgs a) {
       key = valid ? a.keys[gid] : INF64;
     }
     const uint64_t t = key >> a.tshift;
-    const uint32_t u = (uint32_t)(gid / LL);
+    const uint32_t u = row_of(gid, LL);
     const uint32_t slot = (uint32_t)(gid - (uint64_t)u * LL);
     const uint32_t pm = valid ? a.pub[slot / FP] : EMPTY;
     const bool active = valid && key != INF64 && t >= lo && t < hi && u != pm;

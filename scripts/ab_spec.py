@@ -10,6 +10,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "dst-libp2p-test-node_amd"))
 import gossipsim  # noqa: E402
 
+if os.environ.get("GS_LIB_PATH"):
+    gossipsim.LIB_PATH = os.environ["GS_LIB_PATH"]
+
 ap = argparse.ArgumentParser()
 ap.add_argument("--peers", type=int, default=1_000_000)
 ap.add_argument("--rounds", type=int, default=4)
