@@ -23,7 +23,6 @@ namespace gs {
 namespace {
 
 constexpr int TB = 256;
-constexpr uint32_t SEL_MAX = 16;   // r <= D <= 16 picks per heartbeat
 
 struct MeshArgs {
   const uint64_t* row;
@@ -39,25 +38,6 @@ struct MeshArgs {
   uint64_t seed;
   uint32_t N, S, epoch, bo, d, d_lo, d_hi, d_out;
 };
-
-// Insert (key, e) into a bounded ascending list of length <= r.
-__device__ __forceinline__ void top_insert(uint64_t* kk, uint32_t* ee, uint32_t& n, uint32_t r,
-                                           uint64_t key, uint32_t e) {
-  if (r == 0) return;
-  if (n == r) {
-    if (kk[n - 1] < key || (kk[n - 1] == key && ee[n - 1] < e)) return;
-    n--;
-  }
-  int32_t j = (int32_t)n - 1;
-  while (j >= 0 && (kk[j] > key || (kk[j] == key && ee[j] > e))) {
-    kk[j + 1] = kk[j];
-    ee[j + 1] = ee[j];
-    j--;
-  }
-  kk[j + 1] = key;
-  ee[j + 1] = e;
-  n++;
-}
 
 __device__ __forceinline__ bool is_off(const uint64_t* off, uint32_t u) {
   return off && ((off[u >> 6] >> (u & 63)) & 1);
@@ -80,70 +60,126 @@ __global__ __launch_bounds__(TB) void k_disconnect(MeshArgs a) {
     if (ou || is_off(a.off, a.col[e])) a.flags[e] &= (uint8_t)~F_MESH;
 }
 
-__global__ __launch_bounds__(TB) void k_heartbeat(MeshArgs a) {
-  const uint32_t u = blockIdx.x * TB + threadIdx.x;
-  if (u >= a.N || is_off(a.off, u)) return;
-  const uint64_t b = a.row[u], en = a.row[u + 1];
-  uint32_t m = 0, o = 0;
-  for (uint64_t e = b; e < en; e++) {
-    const uint8_t f = a.flags[e];
-    if (f & F_MESH) { m++; o += f & F_OUT; }
+// Heartbeat decisions of one peer per wave (lane l holds CSR entries l, l+64,
+// l+128, l+192 of the row; MAX_DEG = 256). Every choice is a wave-wide argmin
+// of (rng key, entry index), so the graft picks, the prune walk and the
+// outbound grafts are exactly the sequential rules of DESIGN.md §2.3: the r
+// smallest pairs, and the mesh visited in ascending pair order. (Thread per
+// peer left 1.5 waves per SIMD at 100k peers and walked the row serially.)
+constexpr int HB_PER_LANE = (int)(MAX_DEG / 64);
+static_assert(MAX_DEG % 64 == 0 && HB_PER_LANE <= 4, "k_heartbeat covers MAX_DEG entries with 64 lanes");
+
+// wave argmin over (key, idx); ~0u if every key is INF64
+__device__ __forceinline__ uint32_t wave_argmin(uint64_t key, uint32_t idx) {
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint64_t k2 = __shfl_xor(key, off);
+    const uint32_t i2 = (uint32_t)__shfl_xor((int)idx, off);
+    if (k2 < key || (k2 == key && i2 < idx)) { key = k2; idx = i2; }
   }
+  return key == INF64 ? ~0u : (uint32_t)__builtin_amdgcn_readfirstlane(idx);
+}
+
+// This lane's smallest (key, entry) among its entries k*64 + lane.
+__device__ __forceinline__ void lane_min(const uint64_t (&key)[HB_PER_LANE], int lane, uint64_t& bk, uint32_t& bi) {
+  bk = INF64;
+  bi = ~0u;
+#pragma unroll
+  for (int k = 0; k < HB_PER_LANE; k++)  // ascending k: a tie keeps the lower entry
+    if (key[k] < bk) { bk = key[k]; bi = (uint32_t)(k * 64 + lane); }
+}
+
+__device__ __forceinline__ void drop_key(uint64_t (&key)[HB_PER_LANE], uint32_t sel) {
+#pragma unroll
+  for (int k = 0; k < HB_PER_LANE; k++)
+    if ((uint32_t)k == (sel >> 6)) key[k] = INF64;
+}
+
+__global__ __launch_bounds__(TB) void k_heartbeat(MeshArgs a) {
+  const uint32_t u = blockIdx.x * (TB / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (u >= a.N || is_off(a.off, u)) return;  // wave-uniform
+  const uint64_t b = a.row[u], en = a.row[u + 1];
+  const uint32_t deg = (uint32_t)(en - b);
+  uint32_t f[HB_PER_LANE], w[HB_PER_LANE];
+  bool elig[HB_PER_LANE];  // not in mesh, back-off over, neighbour online
+  uint32_t m = 0, o = 0;
+#pragma unroll
+  for (int k = 0; k < HB_PER_LANE; k++) {
+    const uint32_t i = (uint32_t)(k * 64 + lane);
+    f[k] = 0;
+    w[k] = 0;
+    elig[k] = false;
+    if (i < deg) {
+      f[k] = a.flags[b + i];
+      w[k] = a.col[b + i];
+      elig[k] = !(f[k] & F_MESH) && a.epoch > a.until[b + i] && !is_off(a.off, w[k]);
+    }
+    m += (uint32_t)__popcll(__ballot(f[k] & F_MESH));
+    o += (uint32_t)__popcll(__ballot((f[k] & F_MESH) && (f[k] & F_OUT)));
+  }
+  const int fpack = (int)(f[0] | (f[1] << 8) | (f[2] << 16) | (f[3] << 24));
+  auto flag_of = [&](uint32_t sel) {  // flags of entry sel, from the lane holding it
+    return ((uint32_t)__shfl(fpack, (int)(sel & 63)) >> (8 * (sel >> 6))) & 0xFFu;
+  };
   uint32_t mm = m, oo = o;
-  uint64_t kk[SEL_MAX];
-  uint32_t ee[SEL_MAX];
-  uint32_t n = 0;
+  uint32_t graft = 0;  // bit k: entry k*64 + lane grafted this epoch
+  uint64_t key[HB_PER_LANE];
   if (m < a.d_lo) {  // graft mesh_n - |mesh| random eligible peers
-    const uint32_t want = a.d - m;
-    for (uint64_t e = b; e < en; e++)
-      if (!(a.flags[e] & F_MESH) && a.epoch > a.until[e] && !is_off(a.off, a.col[e]))
-        top_insert(kk, ee, n, want, rng(a.seed, P_GRAFT, u, a.epoch, a.col[e]), (uint32_t)(e - b));
-    for (uint32_t q = 0; q < n; q++) {
-      a.prop[b + ee[q]] |= PR_GRAFT;
+#pragma unroll
+    for (int k = 0; k < HB_PER_LANE; k++) key[k] = elig[k] ? rng(a.seed, P_GRAFT, u, a.epoch, w[k]) : INF64;
+    for (uint32_t q = 0; q < a.d - m; q++) {
+      uint64_t bk;
+      uint32_t bi;
+      lane_min(key, lane, bk, bi);
+      const uint32_t sel = wave_argmin(bk, bi);
+      if (sel == ~0u) break;
+      if ((int)(sel & 63) == lane) {
+        drop_key(key, sel);
+        graft |= 1u << (sel >> 6);
+        a.prop[b + sel] |= PR_GRAFT;
+      }
       mm++;
-      oo += a.flags[b + ee[q]] & F_OUT;
+      oo += flag_of(sel) & F_OUT;
     }
   }
   if (mm > a.d_hi) {  // prune down to mesh_n, keep mesh_outbound_min outbound
-    // walk the mesh in ascending (key, entry) order by repeated selection
+    // walk the (start-of-epoch) mesh in ascending (key, entry) order
     const uint32_t excess = mm - a.d;
     uint32_t removed = 0;
-    uint64_t pk = 0;
-    int64_t pe = -1;
+#pragma unroll
+    for (int k = 0; k < HB_PER_LANE; k++) key[k] = (f[k] & F_MESH) ? rng(a.seed, P_PRUNE, u, a.epoch, w[k]) : INF64;
     for (uint32_t q = 0; q < m && removed < excess; q++) {
-      uint64_t bk = INF64;
-      int64_t be = -1;
-      for (uint64_t e = b; e < en; e++) {
-        if (!(a.flags[e] & F_MESH)) continue;
-        const uint64_t k = rng(a.seed, P_PRUNE, u, a.epoch, a.col[e]);
-        const int64_t le = (int64_t)(e - b);
-        const bool after = k > pk || (k == pk && le > pe);
-        const bool better = be < 0 || k < bk || (k == bk && le < be);
-        if (after && better) { bk = k; be = le; }
-      }
-      pk = bk;
-      pe = be;
-      const uint64_t e = b + (uint64_t)be;
-      if (a.flags[e] & F_OUT) {
+      uint64_t bk;
+      uint32_t bi;
+      lane_min(key, lane, bk, bi);
+      const uint32_t sel = wave_argmin(bk, bi);
+      if (sel == ~0u) break;
+      if ((int)(sel & 63) == lane) drop_key(key, sel);
+      if (flag_of(sel) & F_OUT) {
         if (oo <= a.d_out) continue;
         oo--;
       }
-      a.prop[e] |= PR_PRUNE;
+      if ((int)(sel & 63) == lane) a.prop[b + sel] |= PR_PRUNE;
       removed++;
       mm--;
     }
   }
   if (mm >= a.d_lo && oo < a.d_out) {  // graft outbound peers
-    n = 0;
-    const uint32_t want = a.d_out - oo;
-    for (uint64_t e = b; e < en; e++) {
-      const uint8_t f = a.flags[e];
-      if ((f & F_OUT) && !(f & F_MESH) && !(a.prop[e] & PR_GRAFT) && a.epoch > a.until[e] &&
-          !is_off(a.off, a.col[e]))
-        top_insert(kk, ee, n, want, rng(a.seed, P_OUT_GRAFT, u, a.epoch, a.col[e]),
-                   (uint32_t)(e - b));
+#pragma unroll
+    for (int k = 0; k < HB_PER_LANE; k++)
+      key[k] = (elig[k] && (f[k] & F_OUT) && !((graft >> k) & 1u)) ? rng(a.seed, P_OUT_GRAFT, u, a.epoch, w[k])
+                                                                    : INF64;
+    for (uint32_t q = 0; q < a.d_out - oo; q++) {
+      uint64_t bk;
+      uint32_t bi;
+      lane_min(key, lane, bk, bi);
+      const uint32_t sel = wave_argmin(bk, bi);
+      if (sel == ~0u) break;
+      if ((int)(sel & 63) == lane) {
+        drop_key(key, sel);
+        a.prop[b + sel] |= PR_GRAFT;
+      }
     }
-    for (uint32_t q = 0; q < n; q++) a.prop[b + ee[q]] |= PR_GRAFT;
   }
 }
 
@@ -286,7 +322,7 @@ void churn_epoch(Ctx& c, MeshArgs& a, uint64_t h, uint64_t* off) {
   a.epoch = (uint32_t)h;
   GS_HIP(hipMemsetAsync(c.d_prop.p, 0, c.nnz ? c.nnz : 1, s));
   k_disconnect<<<blocks(N), TB, 0, s>>>(a);
-  k_heartbeat<<<blocks(N), TB, 0, s>>>(a);
+  k_heartbeat<<<(N + TB / 64 - 1) / (TB / 64), TB, 0, s>>>(a);
   k_handle_graft<<<blocks(N), TB, 0, s>>>(a);
   k_apply<<<blocks(N), TB, 0, s>>>(a);
   GS_HIP(hipGetLastError());
@@ -350,7 +386,7 @@ uint32_t run_mesh(Ctx& c, uint32_t max_hb) {
     a.epoch = epoch;
     GS_HIP(hipMemsetAsync(c.d_prop.p, 0, c.nnz ? c.nnz : 1, s));
     GS_HIP(hipMemsetAsync(c.d_counters.p + C_MESH_CHANGES, 0, 8, s));
-    k_heartbeat<<<blocks(N), TB, 0, s>>>(a);
+    k_heartbeat<<<(N + TB / 64 - 1) / (TB / 64), TB, 0, s>>>(a);
     k_handle_graft<<<blocks(N), TB, 0, s>>>(a);
     k_apply<<<blocks(N), TB, 0, s>>>(a);
     GS_HIP(hipGetLastError());
