@@ -52,11 +52,13 @@ __global__ __launch_bounds__(TB) void k_offline(uint32_t N, uint64_t seed, uint3
 }
 
 // Links to offline peers leave the mesh (a disconnect, not a PRUNE: no back-off).
+// One peer per wave, lane per CSR entry.
 __global__ __launch_bounds__(TB) void k_disconnect(MeshArgs a) {
-  const uint32_t u = blockIdx.x * TB + threadIdx.x;
-  if (u >= a.N) return;
+  const uint32_t u = blockIdx.x * (TB / 64) + (threadIdx.x >> 6);
+  if (u >= a.N) return;  // wave-uniform
   const bool ou = is_off(a.off, u);
-  for (uint64_t e = a.row[u]; e < a.row[u + 1]; e++)
+  const uint64_t b = a.row[u], en = a.row[u + 1];
+  for (uint64_t e = b + (threadIdx.x & 63); e < en; e += 64)
     if (ou || is_off(a.off, a.col[e])) a.flags[e] &= (uint8_t)~F_MESH;
 }
 
@@ -183,66 +185,86 @@ __global__ __launch_bounds__(TB) void k_heartbeat(MeshArgs a) {
   }
 }
 
+// GRAFT handling at receiver w, one peer per wave: the proposals of w's
+// neighbours are found in parallel (lane per entry), then taken in arrival
+// order — (latency u->w, id), by wave argmin — with the running mesh size c.
 __global__ __launch_bounds__(TB) void k_handle_graft(MeshArgs a) {
-  const uint32_t w = blockIdx.x * TB + threadIdx.x;
-  if (w >= a.N) return;
+  const uint32_t w = blockIdx.x * (TB / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (w >= a.N) return;  // wave-uniform
   const uint64_t b = a.row[w], en = a.row[w + 1];
-  uint32_t c = 0;
+  const uint32_t deg = (uint32_t)(en - b);
   const uint32_t sw = a.stage[w];
-  for (uint64_t e = b; e < en; e++) {
-    const uint8_t f = a.flags[e], p = a.prop[e];
-    c += (((f & F_MESH) && !(p & PR_PRUNE)) || (p & PR_GRAFT)) ? 1u : 0u;
-  }
-  // GRAFTs arrive in (latency u->w, id) order: one pass per distinct latency
-  // level (<= S levels), each pass in ascending id.
-  int64_t prev = -1;
-  for (;;) {
-    int64_t level = -1;
-    for (uint64_t e = b; e < en; e++)
-      if (a.prop[a.rev[e]] & PR_GRAFT) {
-        const int64_t l = a.lat[a.stage[a.col[e]] * a.S + sw];
-        if (l > prev && (level < 0 || l < level)) level = l;
-      }
-    if (level < 0) break;
-    for (uint64_t e = b; e < en; e++) {  // entry (w -> u)
-      if (!(a.prop[a.rev[e]] & PR_GRAFT) || (int64_t)a.lat[a.stage[a.col[e]] * a.S + sw] != level)
-        continue;
-      const uint8_t f = a.flags[e], p = a.prop[e];
-      const bool in_mesh = ((f & F_MESH) && !(p & PR_PRUNE)) || (p & PR_GRAFT);
-      if (in_mesh) { a.prop[a.rev[e]] |= PR_ACCEPT; continue; }
-      if (a.epoch < a.until[e] || (c >= a.d_hi && !(f & F_OUT))) {
-        a.until[e] = a.epoch + a.bo;  // PRUNE back, both ends back off
-        continue;
-      }
-      a.prop[a.rev[e]] |= PR_ACCEPT;
-      a.flags[e] = f | F_MESH;
-      c++;
+  uint32_t f[HB_PER_LANE], p[HB_PER_LANE], r[HB_PER_LANE];
+  uint64_t lvl[HB_PER_LANE];  // latency u->w of a proposing neighbour u, else INF64
+  uint32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < HB_PER_LANE; k++) {
+    const uint32_t i = (uint32_t)(k * 64 + lane);
+    f[k] = 0;
+    p[k] = 0;
+    r[k] = 0;
+    lvl[k] = INF64;
+    if (i < deg) {
+      f[k] = a.flags[b + i];
+      p[k] = a.prop[b + i];
+      r[k] = a.rev[b + i];
+      if (a.prop[r[k]] & PR_GRAFT) lvl[k] = a.lat[a.stage[a.col[b + i]] * a.S + sw];
     }
-    prev = level;
+    c += (uint32_t)__popcll(__ballot(((f[k] & F_MESH) && !(p[k] & PR_PRUNE)) || (p[k] & PR_GRAFT)));
+  }
+  const int fpack = (int)(f[0] | (f[1] << 8) | (f[2] << 16) | (f[3] << 24));
+  const int ppack = (int)(p[0] | (p[1] << 8) | (p[2] << 16) | (p[3] << 24));
+  for (;;) {
+    uint64_t bk;
+    uint32_t bi;
+    lane_min(lvl, lane, bk, bi);
+    const uint32_t sel = wave_argmin(bk, bi);  // entry (w -> u) of the next GRAFT to arrive
+    if (sel == ~0u) break;
+    const int src = (int)(sel & 63), sh = (int)(8 * (sel >> 6));
+    const uint32_t fs = ((uint32_t)__shfl(fpack, src) >> sh) & 0xFFu, ps = ((uint32_t)__shfl(ppack, src) >> sh) & 0xFFu;
+    const bool in_mesh = ((fs & F_MESH) && !(ps & PR_PRUNE)) || (ps & PR_GRAFT);
+    const uint64_t e = b + sel;
+    const uint32_t us = a.until[e];  // every lane, before the owner writes
+    const bool rej = !in_mesh && (a.epoch < us || (c >= a.d_hi && !(fs & F_OUT)));
+    if (lane == src) {
+      drop_key(lvl, sel);
+      uint32_t rs = 0;
+#pragma unroll
+      for (int k = 0; k < HB_PER_LANE; k++)
+        if ((uint32_t)k == (sel >> 6)) rs = r[k];
+      if (rej) a.until[e] = a.epoch + a.bo;  // PRUNE back, both ends back off
+      else a.prop[rs] |= PR_ACCEPT;
+      if (!in_mesh && !rej) a.flags[e] = (uint8_t)(fs | F_MESH);
+    }
+    if (!in_mesh && !rej) c++;
   }
 }
 
+// Apply the epoch's decisions, one peer per wave (lane per entry). The change
+// flag only has to be non-zero when anything changed (run_mesh's fixed-point
+// test), so every wave with a change stores 1: no atomics.
 __global__ __launch_bounds__(TB) void k_apply(MeshArgs a) {
-  const uint32_t u = blockIdx.x * TB + threadIdx.x;
-  uint64_t changes = 0;
-  if (u < a.N) {
-    for (uint64_t e = a.row[u]; e < a.row[u + 1]; e++) {
-      const uint8_t p = a.prop[e];
-      uint8_t f = a.flags[e];
-      if (p & PR_GRAFT) {
-        changes++;
-        if (p & PR_ACCEPT) f |= F_MESH;
-        else { f &= (uint8_t)~F_MESH; a.until[e] = a.epoch + a.bo; }
-      }
-      if (p & PR_PRUNE) { changes++; f &= (uint8_t)~F_MESH; a.until[e] = a.epoch + a.bo; }
-      if (a.prop[a.rev[e]] & PR_PRUNE) { f &= (uint8_t)~F_MESH; a.until[e] = a.epoch + a.bo; }
-      a.flags[e] = f;
+  const uint32_t u = blockIdx.x * (TB / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (u >= a.N) return;  // wave-uniform
+  const uint64_t b = a.row[u];
+  const uint32_t deg = (uint32_t)(a.row[u + 1] - b);
+  bool changed = false;
+  for (uint32_t i = (uint32_t)lane; i < deg; i += 64) {
+    const uint64_t e = b + i;
+    const uint8_t p = a.prop[e];
+    uint8_t f = a.flags[e];
+    if (p & PR_GRAFT) {
+      changed = true;
+      if (p & PR_ACCEPT) f |= F_MESH;
+      else { f &= (uint8_t)~F_MESH; a.until[e] = a.epoch + a.bo; }
     }
+    if (p & PR_PRUNE) { changed = true; f &= (uint8_t)~F_MESH; a.until[e] = a.epoch + a.bo; }
+    if (a.prop[a.rev[e]] & PR_PRUNE) { f &= (uint8_t)~F_MESH; a.until[e] = a.epoch + a.bo; }
+    a.flags[e] = f;
   }
-  // one atomic per wave
-  for (int off = 32; off > 0; off >>= 1) changes += __shfl_xor(changes, off);
-  if ((threadIdx.x & 63) == 0 && changes)
-    atomicAdd((unsigned long long*)&a.counters[C_MESH_CHANGES], (unsigned long long)changes);
+  if (__ballot(changed) && lane == 0) a.counters[C_MESH_CHANGES] = 1;
 }
 
 // Quiescent epoch: earliest back-off expiry that can wake a hungry peer.
@@ -321,10 +343,10 @@ void churn_epoch(Ctx& c, MeshArgs& a, uint64_t h, uint64_t* off) {
   a.off = off;
   a.epoch = (uint32_t)h;
   GS_HIP(hipMemsetAsync(c.d_prop.p, 0, c.nnz ? c.nnz : 1, s));
-  k_disconnect<<<blocks(N), TB, 0, s>>>(a);
+  k_disconnect<<<(N + TB / 64 - 1) / (TB / 64), TB, 0, s>>>(a);
   k_heartbeat<<<(N + TB / 64 - 1) / (TB / 64), TB, 0, s>>>(a);
-  k_handle_graft<<<blocks(N), TB, 0, s>>>(a);
-  k_apply<<<blocks(N), TB, 0, s>>>(a);
+  k_handle_graft<<<(N + TB / 64 - 1) / (TB / 64), TB, 0, s>>>(a);
+  k_apply<<<(N + TB / 64 - 1) / (TB / 64), TB, 0, s>>>(a);
   GS_HIP(hipGetLastError());
 }
 
@@ -387,8 +409,8 @@ uint32_t run_mesh(Ctx& c, uint32_t max_hb) {
     GS_HIP(hipMemsetAsync(c.d_prop.p, 0, c.nnz ? c.nnz : 1, s));
     GS_HIP(hipMemsetAsync(c.d_counters.p + C_MESH_CHANGES, 0, 8, s));
     k_heartbeat<<<(N + TB / 64 - 1) / (TB / 64), TB, 0, s>>>(a);
-    k_handle_graft<<<blocks(N), TB, 0, s>>>(a);
-    k_apply<<<blocks(N), TB, 0, s>>>(a);
+    k_handle_graft<<<(N + TB / 64 - 1) / (TB / 64), TB, 0, s>>>(a);
+    k_apply<<<(N + TB / 64 - 1) / (TB / 64), TB, 0, s>>>(a);
     GS_HIP(hipGetLastError());
     GS_HIP(hipMemcpyAsync(h, c.d_counters.p + C_MESH_CHANGES, 8, hipMemcpyDeviceToHost, s));
     GS_HIP(hipStreamSynchronize(s));
