@@ -111,6 +111,7 @@ __global__ __launch_bounds__(TB) void k_heartbeat(MeshArgs a) {
     f[k] = 0;
     w[k] = 0;
     elig[k] = false;
+    if (k * 64 >= (int)deg) continue;  // wave-uniform
     if (i < deg) {
       f[k] = a.flags[b + i];
       w[k] = a.col[b + i];
@@ -128,7 +129,10 @@ __global__ __launch_bounds__(TB) void k_heartbeat(MeshArgs a) {
   uint64_t key[HB_PER_LANE];
   if (m < a.d_lo) {  // graft mesh_n - |mesh| random eligible peers
 #pragma unroll
-    for (int k = 0; k < HB_PER_LANE; k++) key[k] = elig[k] ? rng(a.seed, P_GRAFT, u, a.epoch, w[k]) : INF64;
+    for (int k = 0; k < HB_PER_LANE; k++) {
+      key[k] = INF64;
+      if (k * 64 < (int)deg && elig[k]) key[k] = rng(a.seed, P_GRAFT, u, a.epoch, w[k]);
+    }
     for (uint32_t q = 0; q < a.d - m; q++) {
       uint64_t bk;
       uint32_t bi;
@@ -149,7 +153,10 @@ __global__ __launch_bounds__(TB) void k_heartbeat(MeshArgs a) {
     const uint32_t excess = mm - a.d;
     uint32_t removed = 0;
 #pragma unroll
-    for (int k = 0; k < HB_PER_LANE; k++) key[k] = (f[k] & F_MESH) ? rng(a.seed, P_PRUNE, u, a.epoch, w[k]) : INF64;
+    for (int k = 0; k < HB_PER_LANE; k++) {
+      key[k] = INF64;
+      if (k * 64 < (int)deg && (f[k] & F_MESH)) key[k] = rng(a.seed, P_PRUNE, u, a.epoch, w[k]);
+    }
     for (uint32_t q = 0; q < m && removed < excess; q++) {
       uint64_t bk;
       uint32_t bi;
@@ -169,8 +176,11 @@ __global__ __launch_bounds__(TB) void k_heartbeat(MeshArgs a) {
   if (mm >= a.d_lo && oo < a.d_out) {  // graft outbound peers
 #pragma unroll
     for (int k = 0; k < HB_PER_LANE; k++)
-      key[k] = (elig[k] && (f[k] & F_OUT) && !((graft >> k) & 1u)) ? rng(a.seed, P_OUT_GRAFT, u, a.epoch, w[k])
-                                                                    : INF64;
+    {
+      key[k] = INF64;
+      if (k * 64 < (int)deg && elig[k] && (f[k] & F_OUT) && !((graft >> k) & 1u))
+        key[k] = rng(a.seed, P_OUT_GRAFT, u, a.epoch, w[k]);
+    }
     for (uint32_t q = 0; q < a.d_out - oo; q++) {
       uint64_t bk;
       uint32_t bi;
@@ -315,7 +325,79 @@ __global__ __launch_bounds__(TB) void k_extract(MeshArgs a, uint32_t* mesh, uint
   for (uint32_t q = c; q < MESH_W; q++) mesh[(size_t)u * MESH_W + q] = EMPTY;
 }
 
+// Lazy gossip under churn: the IHAVE targets of every peer u at epoch h
+// (DESIGN.md §2.7 — the r smallest (rng(GOSSIP, u, h, w), w) among u's online
+// connections outside its epoch-h mesh, r = max(D_lazy, factor·|non-mesh|)
+// capped at |non-mesh|), computed once per epoch snapshot instead of by every
+// (lane, bucket) of k_gossip that needs them. One peer per thread: the
+// selection is serial compute (one rng per connection, an 8-deep sorted
+// insert in registers with static indices), which a wave per peer would
+// leave mostly idle.
+__global__ __launch_bounds__(TB) void k_gossip_targets(const uint64_t* __restrict__ row, const uint32_t* __restrict__ col,
+                                                       const uint32_t* __restrict__ mesh, const uint64_t* __restrict__ off,
+                                                       uint32_t N, uint64_t seed, uint32_t h, uint32_t d_lazy,
+                                                       uint32_t gf_milli, uint32_t* __restrict__ tgt,
+                                                       uint8_t* __restrict__ tcnt) {
+  const uint32_t u = blockIdx.x * TB + threadIdx.x;
+  if (u >= N) return;
+  if (is_off(off, u)) {  // offline peers gossip nothing (k_gossip skips them first)
+    tcnt[u] = 0;
+    return;
+  }
+  uint32_t mrow[MESH_W];
+  const uint4* rp = reinterpret_cast<const uint4*>(mesh + (size_t)u * MESH_W);
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const uint4 x = rp[q];
+    mrow[4 * q] = x.x & 0xFFFFFFu; mrow[4 * q + 1] = x.y & 0xFFFFFFu;
+    mrow[4 * q + 2] = x.z & 0xFFFFFFu; mrow[4 * q + 3] = x.w & 0xFFFFFFu;
+  }
+  uint64_t kk[GT_W];
+  uint32_t ww[GT_W];
+#pragma unroll
+  for (int q = 0; q < (int)GT_W; q++) { kk[q] = INF64; ww[q] = ~0u; }
+  uint32_t nonmesh = 0;
+  for (uint64_t e = row[u]; e < row[u + 1]; e++) {
+    const uint32_t w = col[e];
+    bool inm = false;
+#pragma unroll
+    for (int q = 0; q < (int)MESH_W; q++) inm |= mrow[q] == w;
+    if (inm || is_off(off, w)) continue;
+    nonmesh++;
+    const uint64_t rk = rng(seed, P_GOSSIP, u, h, w);
+    if (!(rk < kk[GT_W - 1] || (rk == kk[GT_W - 1] && w < ww[GT_W - 1]))) continue;
+#pragma unroll
+    for (int q = (int)GT_W - 1; q > 0; q--) {  // insert, shifting the larger pairs up
+      if (rk < kk[q - 1] || (rk == kk[q - 1] && w < ww[q - 1])) { kk[q] = kk[q - 1]; ww[q] = ww[q - 1]; }
+      else if (rk < kk[q] || (rk == kk[q] && w < ww[q])) { kk[q] = rk; ww[q] = w; }
+    }
+    if (rk < kk[0] || (rk == kk[0] && w < ww[0])) { kk[0] = rk; ww[0] = w; }
+  }
+  uint32_t r = (uint32_t)(((uint64_t)nonmesh * gf_milli) / 1000);
+  if (r < d_lazy) r = d_lazy;
+  if (r > nonmesh) r = nonmesh;
+  if (r > GT_W) {
+    tcnt[u] = GT_NONE;
+    return;
+  }
+#pragma unroll
+  for (int q = 0; q < (int)GT_W; q++)
+    if ((uint32_t)q < r) tgt[(size_t)u * GT_W + q] = ww[q];
+  tcnt[u] = (uint8_t)r;
+}
+
 inline unsigned blocks(uint64_t n) { return (unsigned)((n + TB - 1) / TB); }
+
+// Targets of the snapshot in ring slot `slot` (epoch h), when lazy gossip is on.
+void ring_targets(Ctx& c, uint64_t h, size_t slot) {
+  if (!c.cfg.lazy_gossip || !c.d_ring_tcnt.p) return;
+  const uint32_t N = c.cfg.peers;
+  const size_t w64 = ((size_t)N + 63) / 64;
+  k_gossip_targets<<<blocks(N), TB, 0, c.stream>>>(
+      c.d_row.p, c.d_col.p, c.d_ring_mesh.p + slot * N * MESH_W, c.d_ring_off.p + slot * w64, N, c.cfg.seed,
+      (uint32_t)h, c.cfg.d_lazy, c.cfg.gossip_factor_milli, c.d_ring_tgt.p + slot * N * GT_W,
+      c.d_ring_tcnt.p + slot * N);
+}
 
 MeshArgs mesh_args(Ctx& c) {
   const uint32_t N = c.cfg.peers;
@@ -369,12 +451,14 @@ void churn_ring(Ctx& c, uint64_t h_lo, uint64_t h_hi) {
     c.churn_state = 0;
     c.ring_lo = 0;
     c.ring_hi = 0;
+    ring_targets(c, 0, 0);
   }
   for (uint64_t h = c.churn_state + 1; h <= h_hi; h++) {
     const size_t slot = (size_t)(h % R);
     uint64_t* off = c.d_ring_off.p + slot * w64;
     churn_epoch(c, a, h, off);
     k_extract<<<blocks(N), TB, 0, s>>>(a, c.d_ring_mesh.p + slot * N * MESH_W, nullptr);
+    ring_targets(c, h, slot);
   }
   GS_HIP(hipGetLastError());
   if (h_hi > c.churn_state) {

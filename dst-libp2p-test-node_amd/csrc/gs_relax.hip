@@ -579,12 +579,17 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       ep[i] = (sched[i].t_pub_ns - ph) / hb;
     }
     if (!c.ring_R) {
-      const uint64_t w64 = ((uint64_t)N + 63) / 64, per_slot = (uint64_t)N * MESH_W * 4 + w64 * 8;
+      const uint64_t w64 = ((uint64_t)N + 63) / 64;
+      const uint64_t per_slot = (uint64_t)N * MESH_W * 4 + w64 * 8 + (gossip ? (uint64_t)N * (GT_W * 4 + 1) : 0);
       const uint64_t budget = 8ull << 30;
       const uint64_t want = (uint64_t)Bmax + c.cfg.churn_horizon + 1;
       c.ring_R = (uint32_t)std::min<uint64_t>(want, std::max<uint64_t>(c.cfg.churn_horizon + 2, budget / per_slot));
       c.d_ring_mesh.alloc((size_t)c.ring_R * N * MESH_W);
       c.d_ring_off.alloc((size_t)c.ring_R * w64);
+      if (gossip) {  // IHAVE targets per (peer, epoch) beside the snapshots (k_gossip_targets)
+        c.d_ring_tgt.alloc((size_t)c.ring_R * N * GT_W);
+        c.d_ring_tcnt.alloc((size_t)c.ring_R * N);
+      }
     }
   }
   const size_t max_tiles = ((size_t)N * Bmax * FP + 63) / 64;
@@ -718,6 +723,10 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
         ra.hb_ns = c.cfg.heartbeat_ns;
         ra.seed = c.cfg.seed;
         ra.gossip = 1;
+        if (churn) {
+          ra.ring_tgt = c.d_ring_tgt.p;
+          ra.ring_tcnt = c.d_ring_tcnt.p;
+        }
         ra.hist = c.cfg.history_gossip;
         ra.d_lazy = c.cfg.d_lazy;
         ra.gf_milli = c.cfg.gossip_factor_milli;

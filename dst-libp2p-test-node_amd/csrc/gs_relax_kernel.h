@@ -57,6 +57,8 @@ struct RelaxArgs {
   const uint64_t* q0;         // [B] epoch of t_pub
   const uint64_t* r0;         // [B] t_pub - start of that epoch
   uint32_t churn, ring_R, w64, horizon;
+  const uint32_t* ring_tgt;   // churn + gossip: [R][N][GT_W] IHAVE targets of (peer, epoch)
+  const uint8_t* ring_tcnt;   // [R][N] their count, GT_NONE = more than GT_W (recompute)
   const uint32_t* mesh;
   const uint32_t* pub;
   const uint8_t* stage;
@@ -579,10 +581,37 @@ __global__ __launch_bounds__(TB) void k_gossip(RelaxArgs a) {
       if (T + L.lmax[sv] < lo || T + L.lmin[sv] >= hi) continue;
       const uint64_t hab = a.habs0[m] + j0 + k;
       const uint32_t h = (uint32_t)hab;
+      auto ihave = [&](uint32_t w) {  // v's IHAVE to w; IWANT + answer if w has not seen it
+        const uint32_t sw = a.stage[w];
+        const uint64_t ti = T + L.lat[sv * S + sw];
+        if (ti < lo || ti >= hi) return;
+        const uint64_t sd = L.sd[sw];
+        const uint64_t A = ti + L.lat[sw * S + sv] + ser + L.lat[sv * S + sw] + (sd > ser ? sd - ser : 0);
+        if (a.churn && (ev_lost(a, m, ti, w) || ev_lost(a, m, A, w))) return;  // IHAVE or answer lost
+        const size_t dst = (size_t)w * LL + slot;
+        const uint64_t kw = a.keys[dst];
+        if (kw != INF64 && (kw >> a.tshift) <= ti) return;  // already seen: no IWANT
+        iw++;
+        if (A > a.tmax) err |= ERR_TIME;
+        if (hp + 1 >= (1u << HOP_BITS)) err |= ERR_HOPS;
+        const uint64_t nk = (A << a.tshift) | ((uint64_t)(hp + 1) << a.sb) | u;
+        if (nk < kw) {
+          atomicMin((unsigned long long*)&a.keys[dst], (unsigned long long)nk);
+          nmin = nk < nmin ? nk : nmin;
+        }
+      };
       const uint32_t* mrp = a.mesh + (size_t)u * MESH_W;
       if (a.churn) {  // v gossips only while online, within the message's lifetime, over its epoch's mesh
         if (hab > a.q0[m] + a.horizon || ep_off(a, hab, u)) continue;
         mrp = ep_mesh(a, hab, u);
+        if (a.ring_tcnt) {  // targets of (u, h) precomputed with the epoch's snapshot (k_gossip_targets)
+          const size_t ti = (size_t)((uint32_t)hab % a.ring_R) * a.N + u;
+          const uint32_t rc = a.ring_tcnt[ti];
+          if (rc != GT_NONE) {
+            for (uint32_t q = 0; q < rc; q++) ihave(a.ring_tgt[ti * GT_W + q]);
+            continue;
+          }
+        }
       }
       const uint4* rp = reinterpret_cast<const uint4*>(mrp);
 #pragma unroll
@@ -624,25 +653,6 @@ __global__ __launch_bounds__(TB) void k_gossip(RelaxArgs a) {
       uint32_t r = (uint32_t)(((uint64_t)nonmesh * a.gf_milli) / 1000);
       if (r < a.d_lazy) r = a.d_lazy;
       if (r > nonmesh) r = nonmesh;
-      auto ihave = [&](uint32_t w) {  // v's IHAVE to w; IWANT + answer if w has not seen it
-        const uint32_t sw = a.stage[w];
-        const uint64_t ti = T + L.lat[sv * S + sw];
-        if (ti < lo || ti >= hi) return;
-        const uint64_t sd = L.sd[sw];
-        const uint64_t A = ti + L.lat[sw * S + sv] + ser + L.lat[sv * S + sw] + (sd > ser ? sd - ser : 0);
-        if (a.churn && (ev_lost(a, m, ti, w) || ev_lost(a, m, A, w))) return;  // IHAVE or answer lost
-        const size_t dst = (size_t)w * LL + slot;
-        const uint64_t kw = a.keys[dst];
-        if (kw != INF64 && (kw >> a.tshift) <= ti) return;  // already seen: no IWANT
-        iw++;
-        if (A > a.tmax) err |= ERR_TIME;
-        if (hp + 1 >= (1u << HOP_BITS)) err |= ERR_HOPS;
-        const uint64_t nk = (A << a.tshift) | ((uint64_t)(hp + 1) << a.sb) | u;
-        if (nk < kw) {
-          atomicMin((unsigned long long*)&a.keys[dst], (unsigned long long)nk);
-          nmin = nk < nmin ? nk : nmin;
-        }
-      };
 #pragma unroll
       for (int q = 0; q < (int)GOSSIP_R_REG; q++)
         if ((uint32_t)q < r) ihave(ww[q]);
