@@ -440,6 +440,7 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
   const size_t gseg = (size_t)wave * a.gl_cap;
   uint64_t nmin = INF64, nonfin = 0;
   uint32_t cnt = 0, gcnt = 0, err = 0;
+  const uint64_t hspan = GOSSIP ? (uint64_t)a.hist * a.hb_ns : 0;
   for (uint64_t tile = uniform64(wave); tile < ntiles; tile += nwaves) {
     if constexpr (SKIP) {
       // untouched since its last scan and nothing due in this bucket: the
@@ -479,12 +480,16 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
       nonfin += (valid && !fin && slot % FP < a.F) ? 1u : 0u;  // padded fragments never arrive
       bool gwork = false;
       uint64_t gnext = INF64;
-      if (fin) {
-        const uint32_t m = slot / FP, sv = a.stage[u];
-        const uint64_t r0 = a.rel0[m], lmn = L.lmin[sv], lmx = L.lmax[sv];
+      // the first gossip heartbeat T_j0 < max(t, rel0) + hb, so a lane with
+      // max(t, rel0) + hist*hb + lmax < lo is past its last IHAVE: skip it
+      // before the division
+      const uint32_t sv = fin ? a.stage[u] : 0, m = slot / FP;
+      const uint64_t r0 = fin ? a.rel0[m] : 0;
+      if (fin && a.hist && (t > r0 ? t : r0) + hspan + L.lmax[sv] >= lo) {
+        const uint64_t lmn = L.lmin[sv], lmx = L.lmax[sv];
         const uint64_t j0 = first_hb(t, r0, a.hb_ns);
         const uint64_t tlast = r0 + (j0 + a.hist - 1) * a.hb_ns;
-        if (a.hist && tlast + lmx >= lo) {
+        if (tlast + lmx >= lo) {
           for (uint32_t k = 0; k < a.hist; k++) {
             const uint64_t T = r0 + (j0 + k) * a.hb_ns;
             gwork |= (T + lmx >= lo && T + lmn < hi);

@@ -308,3 +308,19 @@ def test_churn_errors():
     sim, _ = gpu_sim(p, 1, (50, 50, 50, 50))
     with pytest.raises(gossipsim.GossipSimError, match="2\\^20 heartbeats"):
         sim.run(_sched(2, 200))
+
+
+@pytest.mark.parametrize("connect_to", [20, 30])
+def test_churn_gossip_wide_target_lists(connect_to):
+    """Lazy gossip under churn where many peers have more IHAVE targets than the
+    per-epoch precomputed list holds (GT_W = 8; degree ~2*CONNECTTO, targets =
+    max(d_lazy, gossip_factor * candidates)): those peers take k_gossip's own
+    selection (GT_NONE), the rest the k_gossip_targets list; both bit-exact
+    against the oracle."""
+    kw = dict(churn_ppm=20000, lazy_gossip=1, connect_to=connect_to, heartbeat_ns=100_000_000,
+              hb_phase_ns=T0 - 2_000_000_000 + 37_000_000, churn_down=8, churn_horizon=12)
+    p = oracle.params(peers=500, seed=61, **kw)
+    sim, res = compare(p, 5, (50, 150, 40, 130), _sched(16, 500), batch=8)
+    st = sim.stats()
+    assert 0 < st["deliveries"] < 16 * 499
+    assert st["gossip_iwant"] > 0
