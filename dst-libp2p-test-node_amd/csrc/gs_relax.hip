@@ -697,7 +697,11 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     ra.N = N; ra.B = B; ra.F = F; ra.L = L; ra.S = c.S; ra.sb = b.sb; ra.tshift = b.tshift;
     ra.idw = (c.cfg.idontwant && b.payload >= c.cfg.idontwant) ? 1 : 0;
     const uint64_t need = (total + TB - 1) / TB;
-    const unsigned grid = (unsigned)std::min<uint64_t>(need, (uint64_t)dev_cus * 16);
+    const char* bpc_env = getenv("GS_SPLIT_BLOCKS_PER_CU");  // A/B knob for the split path's grid
+    // 4 blocks per CU measured best on config #3 (k_scan 177 -> 136 us, k_frontier
+    // 65 -> 38 us per bucket vs 16; 1-2 and 32-64 slower): fewer, longer scan waves
+    const uint64_t bpc = bpc_env && *bpc_env ? std::max(1, atoi(bpc_env)) : 4;
+    const unsigned grid = (unsigned)std::min<uint64_t>(need, (uint64_t)dev_cus * bpc);
     if (variant & 8) {  // frontier segments: one per scan wave
       const uint64_t nwaves = (uint64_t)grid * (TB / 64), ntiles = (total + 63) / 64;
       ra.seg_cap = (uint32_t)(((ntiles + nwaves - 1) / nwaves) * (64 / FP));
