@@ -179,7 +179,7 @@ CONFIGS = {
     "c1_1k_uniform_F1": dict(peers=1000, knobs={}, links=(1, 50, 50, 50, 50), fragments=1, batch=1024, msgs=1024),
     "c2_10k_F8": dict(peers=10_000, knobs={}, links=(5, 50, 150, 40, 130), fragments=8, batch=128, msgs=1024),
     "c3_100k_gossip_churn": dict(
-        peers=100_000, links=(5, 50, 150, 40, 130), fragments=1, batch=256, msgs=512,
+        peers=100_000, links=(5, 50, 150, 40, 130), fragments=1, batch=1024, msgs=1024,
         knobs=dict(lazy_gossip=1, churn_ppm=10_000, churn_down=10, churn_horizon=16,
                    heartbeat_ns=1_000_000_000, hb_phase_ns=gossipsim.T0_NS - 20 * 1_000_000_000 + 370_000_000)),
 }

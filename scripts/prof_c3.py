@@ -13,6 +13,8 @@ name = sys.argv[1] if len(sys.argv) > 1 else "c3_100k_gossip_churn"
 c = dict(bench.CONFIGS[name])
 if len(sys.argv) > 2:
     c["batch"] = int(sys.argv[2])
+if len(sys.argv) > 3:
+    c["msgs"] = int(sys.argv[3])
 sim = gossipsim.Simulator(peers=c["peers"], batch=c["batch"], fragments=c["fragments"], seed=1, **c["knobs"])
 sim.set_topogen_links(c["links"][0], *c["links"][1:])
 t0 = time.perf_counter()
