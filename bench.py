@@ -54,6 +54,8 @@ def parse():
                     help="msg: message-sharded ranks (default); peer: peer-partitioned ranks")
     ap.add_argument("--also-peers", type=int, default=100_000,
                     help="second graph size reported beside the headline (metric names 100k & 1M; 0=off)")
+    ap.add_argument("--gossip-check", type=int, default=64,
+                    help="messages of the 1M-peer gossip-on vs eager-only delivery comparison (0=off)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="per-launch HBM bytes of the relax kernel from a rocprofv3 --pmc pass")
     return ap.parse_args()
@@ -93,8 +95,25 @@ def barrier_sync(torch, dist, world):
         torch.cuda.synchronize()
 
 
+def _pinned(core_set):
+    """Context: this process pinned to `core_set` (restored afterwards)."""
+    class _Pin:
+        def __enter__(self):
+            self.old = os.sched_getaffinity(0)
+            os.sched_setaffinity(0, core_set)
+
+        def __exit__(self, *a):
+            os.sched_setaffinity(0, self.old)
+    return _Pin()
+
+
 def cpu_baseline(sim, args, S, links, budget_s):
-    """Single-threaded CPU oracle on the same graph + mesh, a bounded message sample."""
+    """The CPU oracle on the same graph + mesh and the same knobs, a bounded
+    message sample (SURVEY §8d): (1) single-threaded, pinned to one core;
+    (2) message-parallel (OpenMP) on the host cores this process may use,
+    capped at 16 (the box's CPU share per GPU); (3) the single-core eager-only
+    rate (lazy gossip off) beside it, since the oracle simulates every IHAVE
+    while the GPU proves them no-ops."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # checker / baseline only
     N = args.peers
@@ -104,25 +123,76 @@ def cpu_baseline(sim, args, S, links, budget_s):
     stage = (np.arange(N) % S).astype(np.uint8)
     kw = {n: getattr(sim.cfg.c, n) for n, _ in oracle.OrParams._fields_}
     p = oracle.OrParams(**kw)
-    t, pub, size = gossipsim.shard_messages(10_000, 0, 1, 64, N, args.msg_size)
-    deliv, elapsed, k = 0, 0.0, 0
-    tcs, hps = [], []
-    while k < 64 and (elapsed < budget_s or k == 0):
-        t0 = time.perf_counter()
-        tc, hp, st = oracle.run(p, row, col, mesh, cnt, stage, lat, bw, bw, t[k:k + 1], pub[k:k + 1],
-                                size[k:k + 1])
-        elapsed += time.perf_counter() - t0
-        deliv += st["deliveries"]
-        tcs.append(tc[0])
-        hps.append(hp[0])
-        k += 1
-    # parity of the sampled messages (outside every timed region)
-    res = sim.run((t[:k], pub[:k], size[:k]), collect=True)
-    same = bool((res["t_complete"] == np.stack(tcs)).all() and (res["hops"] == np.stack(hps)).all())
-    return {"value": deliv / elapsed, "unit": "deliveries/s", "cores": 1, "kind": "port",
-            "sample": "oracle/gs_oracle.c or_run (binary-heap event simulation), %d messages on the "
-                      "same %d-peer graph+mesh, %.1f s single-threaded" % (k, N, elapsed),
+    t, pub, size = gossipsim.shard_messages(10_000, 0, 1, 256, N, args.msg_size)
+    cores = sorted(os.sched_getaffinity(0))
+
+    def timed(params, k_max, threads=0, budget=budget_s):
+        deliv, elapsed, k, tcs, hps = 0, 0.0, 0, [], []
+        step = max(1, threads)
+        while k + step <= k_max and (elapsed < budget or k == 0):
+            t0 = time.perf_counter()
+            tc, hp, st = oracle.run(params, row, col, mesh, cnt, stage, lat, bw, bw, t[k:k + step], pub[k:k + step],
+                                    size[k:k + step], threads=threads)
+            elapsed += time.perf_counter() - t0
+            deliv += st["deliveries"]
+            tcs.append(tc)
+            hps.append(hp)
+            k += step
+        return deliv / elapsed, k, elapsed, np.concatenate(tcs), np.concatenate(hps)
+
+    with _pinned({cores[0]}):
+        v1, k1, e1, tcs, hps = timed(p, 64)
+        pe = oracle.OrParams(**dict(kw, lazy_gossip=0))
+        ve, ke, ee, _, _ = timed(pe, 64, budget=budget_s / 3)
+    nthr = min(16, len(cores))
+    vm, km, em, _, _ = timed(p, 256, threads=nthr)
+    # parity of the single-core sample (outside every timed region)
+    res = sim.run((t[:k1], pub[:k1], size[:k1]), collect=True)
+    same = bool((res["t_complete"] == tcs).all() and (res["hops"] == hps).all())
+    return {"value": v1, "unit": "deliveries/s", "cores": 1, "kind": "port",
+            "sample": "oracle/gs_oracle.c or_run (binary-heap event simulation incl. every lazy-gossip IHAVE), "
+                      "%d messages on the same %d-peer graph+mesh, %.1f s, pinned to core %d" % (k1, N, e1, cores[0]),
+            "all_cores": {"value": vm, "cores": nthr, "host_cpus_allowed": len(cores), "nproc": os.cpu_count(),
+                          "sample": "or_run_mt (OpenMP, message-parallel), %d messages, %.1f s" % (km, em)},
+            "eager_only_1core": {"value": ve, "sample": "lazy_gossip=0, %d messages, %.1f s" % (ke, ee)},
+            "shadow": "not measured (no Shadow installation on the GPU box)",
             "parity_with_gpu_on_sample": same}
+
+
+def gossip_check(args, S, links, local, msgs=64):
+    """Does lazy gossip (on in rust-test-node, main.rs:230,235) change any
+    delivery of the headline workload? Default phase (publish 3 ms after a
+    heartbeat): the library's per-batch no-op proof. Heartbeats 370 ms after
+    the publish (mid-dissemination): gossip on the push path vs eager-only on
+    the pull path, on the same graph and mesh, counting the (peer, message)
+    completions that differ."""
+    out = {"default_phase": "publish 3 ms after a heartbeat (gossipsim.T0_NS): proven no-op per batch"}
+    phase = (gossipsim.T0_NS + 370_000_000) % 1_000_000_000
+    sched = gossipsim.shard_messages(0, 0, 1, msgs, args.peers, args.msg_size)
+    res = {}
+    for name, kw in (("gossip", dict(lazy_gossip=1, hb_phase_ns=phase)), ("eager", dict(lazy_gossip=0))):
+        sim = gossipsim.Simulator(peers=args.peers, batch=msgs, fragments=args.fragments, seed=args.seed,
+                                  device=local, **kw)
+        sim.set_topogen_links(S, *links)
+        sim.connect_gossipsub_peers()
+        sim.mesh_converge(args.max_heartbeats)
+        t0 = time.perf_counter()
+        r = sim.run(sched, collect=True)
+        r["s"] = time.perf_counter() - t0
+        r["stats"] = sim.stats()
+        res[name] = r
+        sim.close()
+    g, e = res["gossip"], res["eager"]
+    diff = g["t_complete"] != e["t_complete"]
+    earlier = g["t_complete"] < e["t_complete"]
+    out["heartbeat_370ms"] = {
+        "msgs": msgs, "peers": args.peers, "completions_differ": int(diff.sum()),
+        "completions_earlier_via_iwant": int(earlier.sum()),
+        "hops_differ": int((g["hops"] != e["hops"]).sum()),
+        "gossip_iwant": int(g["stats"]["gossip_iwant"]), "fallback_batches": int(g["stats"]["gossip_fallback_batches"]),
+        "max_latency_ms_gossip": int(g["stats"]["latency_max_ms"]), "max_latency_ms_eager": int(e["stats"]["latency_max_ms"]),
+        "run_s_gossip_push": g["s"], "run_s_eager_pull": e["s"]}
+    return out
 
 
 def make_sim(args, peers, S, links, local):
@@ -200,9 +270,11 @@ def config_rates(args, local):
         sim.run(sched, collect=False)
         dt = time.perf_counter() - t0
         st = sim.stats()
+        push = c["knobs"].get("churn_ppm") or st["gossip_fallback_batches"]
         out[name] = {"value": st["deliveries"] / dt, "unit": "deliveries/s", "msgs": c["msgs"],
-                     "ms": dt * 1e3, "deliveries": int(st["deliveries"]),
-                     "kernel_path": "push (k_scan+k_frontier+k_gossip)" if c["knobs"] else "pull (k_pull)"}
+                     "ms": dt * 1e3, "deliveries": int(st["deliveries"]), "batches": int(st["batches"]),
+                     "gossip_iwant": int(st["gossip_iwant"]), "gossip_noop_msgs": int(st["gossip_noop_msgs"]),
+                     "kernel_path": "push (k_scan+k_frontier+k_gossip)" if push else "pull (k_pull)"}
         sim.close()
     return out
 
@@ -259,6 +331,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0 and args.mode == "msg":
         cpu = cpu_baseline(sim, args, S, links, args.cpu_seconds)
+    gcheck = None
+    if rank == 0 and world == 1 and args.gossip_check and args.mode == "msg":
+        gcheck = gossip_check(args, S, links, local, args.gossip_check)
 
     if rank == 0:
         out = {
@@ -273,7 +348,8 @@ def main():
             "scaling": "weak" if args.mode == "msg" else "strong",
             "vs_baseline": None,
             "dtype": "u64",
-            "data": "synthetic (random-ID dial graph + converged mesh, run.sh publish schedule)",
+            "data": "synthetic (random-ID dial graph + subscription/heartbeat-converged mesh, run.sh publish "
+                    "schedule, rust preset incl. lazy gossip)",
             "config": {
                 "workload": "%d peers, %d-stage topogen links (%d-%d Mbit, %d-%d ms), CONNECTTO=10, "
                             "D=6/4/8, F=%d, %d B msgs, %d msgs/step%s"
@@ -291,6 +367,9 @@ def main():
             "buckets_per_step": st["buckets"] / max(1, args.steps),
             "at_%dk_peers" % (args.also_peers // 1000) if extra else "at_second_size": extra,
             "roofline": roof,
+            "gossip": {"lazy_gossip": int(sim.cfg.c.lazy_gossip), "noop_msgs": int(st["gossip_noop_msgs"]),
+                       "fallback_batches": int(st["gossip_fallback_batches"]), "iwant": int(st["gossip_iwant"]),
+                       "check": gcheck},
             "cpu_baseline": cpu,
             "configs_1gpu": cfg_rates,
         }

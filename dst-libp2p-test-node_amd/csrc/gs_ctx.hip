@@ -14,6 +14,7 @@ namespace gs {
 Ctx::~Ctx() {
   for (auto e : ev_pool) (void)hipEventDestroy(e);
   if (h_pinned) (void)hipHostFree(h_pinned);
+  if (h_block) (void)hipHostFree(h_block);
   if (stream) (void)hipStreamDestroy(stream);
 }
 

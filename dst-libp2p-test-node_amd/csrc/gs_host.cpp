@@ -8,6 +8,7 @@
 #include <string.h>
 #include <strings.h>
 
+#include <new>
 #include <string>
 #include <vector>
 
@@ -32,7 +33,7 @@ extern "C" void gs_config_default(gs_config* c) {
   c->backoff_ns = 60000000000ull;        // main.rs:229
   c->flood_publish = 1;           // main.rs:227
   c->idontwant = 0;
-  c->lazy_gossip = 0;
+  c->lazy_gossip = 1;             // gossip_lazy(6) + gossip_factor(0.25): rust always gossips (main.rs:230,235)
   c->self_log = 0;                // rust: no self delivery
   c->seed = 1;
   c->device = 0;
@@ -43,6 +44,7 @@ extern "C" void gs_config_default(gs_config* c) {
   c->churn_down = 10;             // rejoin after 10 epochs
   c->churn_horizon = 16;
   c->node = GS_NODE_RUST;
+  c->sub_graft = 1;               // handle_received_subscriptions grafts during the 20 s pump (main.rs:357-379)
 }
 
 extern "C" gs_status gs_config_preset(gs_config* c, uint32_t node) {
@@ -54,6 +56,7 @@ extern "C" gs_status gs_config_preset(gs_config* c, uint32_t node) {
     c->idontwant = 1000;          // IDontWantMessageThreshold = 1000 (main.go:165)
     c->signed_msgs = 0;           // WithMessageSignaturePolicy(StrictNoSign) (main.go:383)
     c->self_log = 1;              // the node's own subscription delivers its publish (readLoop, main.go:52-60)
+    c->sub_graft = 0;             // go-libp2p-pubsub grafts from the heartbeat only (upstream, not vendored)
   } else if (node == GS_NODE_NIM) {  // nim-test-node/gossipsub-queues/main.nim
     c->dial_extra = 0;            // dials CONNECTTO peers (main.nim:396)
     c->max_connections = 250;     // withMaxConnections(MAXCONNECTIONS, default 250) (main.nim:429)
@@ -61,6 +64,7 @@ extern "C" gs_status gs_config_preset(gs_config* c, uint32_t node) {
     c->d_lazy = c->d;             // GOSSIPSUB_D_LAZY default d (main.nim:259)
     c->signed_msgs = 0;           // initializeGossipsub(switch, anonymize = true) (main.nim:447)
     c->self_log = 1;              // triggerSelf = SELFTRIGGER, default true (main.nim:245)
+    c->sub_graft = 0;             // nim-libp2p rebalances the mesh in its heartbeat (upstream, not vendored)
   }
   return GS_OK;
 }
@@ -130,6 +134,8 @@ extern "C" gs_status gs_config_from_env(gs_config* c, char* err, size_t err_len)
   if (env_u64("GS_CHURN_DOWN", &x, err, err_len, &bad)) c->churn_down = (uint32_t)x;
   if (env_u64("GS_CHURN_HORIZON", &x, err, err_len, &bad)) c->churn_horizon = (uint32_t)x;
   if (env_u64("GS_HB_PHASE_NS", &x, err, err_len, &bad)) c->hb_phase_ns = x;
+  if (env_u64("GS_LAZY_GOSSIP", &x, err, err_len, &bad)) c->lazy_gossip = x ? 1 : 0;
+  if (env_u64("GS_SUB_GRAFT", &x, err, err_len, &bad)) c->sub_graft = x ? 1 : 0;
   const char* gf = getenv("GOSSIPSUB_GOSSIP_FACTOR");
   if (gf && *gf) {
     char* end = nullptr;
@@ -532,6 +538,8 @@ extern "C" gs_status gs_schedule_runsh(uint32_t n_msgs, uint32_t peers, uint32_t
     out[i].t_pub_ns = t0_ns + (uint64_t)i * delay_ns;
     out[i].publisher = (uint32_t)(((uint64_t)publisher_id + (uint64_t)i * rotation) % peers);
     out[i].msg_size = msg_size;
+    out[i].frags = 0;  // cfg.fragments (FRAGMENTS of every node, env.rs:64-67)
+    out[i].reserved = 0;
   }
   return GS_OK;
 }
@@ -563,6 +571,64 @@ extern "C" gs_status gs_write_latency_log(const char* path, const gs_publish* sc
   return GS_OK;
 }
 
+// One arrival line of a node flavour (rust main.rs:93 / go main.go:49: tx_time;
+// nim main.nim:150: msgId) in grep's path:line:text form (shadow/run.sh:61).
+namespace {
+uint64_t nim_msg_id(const gs_config* cfg, const gs_publish& p) {  // msgId = rand(high(int64)) (main.nim:162)
+  return gs::rng(cfg->seed, gs::P_MSGID, p.publisher, (uint32_t)(p.t_pub_ns >> 32), (uint32_t)p.t_pub_ns) >> 1;
+}
+void log_line(FILE* f, const gs_config* cfg, uint32_t u, uint64_t line, const gs_publish& p, uint64_t t) {
+  const int64_t ms = ((int64_t)t - (int64_t)p.t_pub_ns) / 1000000;  // i64 division, main.rs:91-93
+  if (cfg->node == GS_NODE_NIM)
+    fprintf(f, "shadow.data/hosts/peer%u/main.1000.stdout:%llu:%llu milliseconds: %lld\n", u,
+            (unsigned long long)line, (unsigned long long)nim_msg_id(cfg, p), (long long)ms);
+  else
+    fprintf(f, "shadow.data/hosts/peer%u/main.1000.stdout:%llu:%lld milliseconds: %lld\n", u,
+            (unsigned long long)line, (long long)p.t_pub_ns, (long long)ms);
+}
+}  // namespace
+
+struct gs_log {
+  gs_config cfg;
+  FILE* f = nullptr;
+  std::vector<uint64_t> line;  // per-peer line counter (grep -n numbers lines per host file)
+  std::vector<char> buf;
+};
+
+extern "C" gs_status gs_log_open(const gs_config* cfg, const char* path, gs_log** out) {
+  if (!cfg || !path || !out || cfg->node > GS_NODE_NIM) return GS_EINVAL;
+  *out = nullptr;
+  gs_log* L = new (std::nothrow) gs_log();
+  if (!L) return GS_ENOMEM;
+  L->cfg = *cfg;
+  L->f = fopen(path, "w");
+  if (!L->f) { delete L; return GS_EINVAL; }
+  L->buf.resize(1 << 22);
+  setvbuf(L->f, L->buf.data(), _IOFBF, L->buf.size());
+  L->line.assign(cfg->peers, 0);
+  *out = L;
+  return GS_OK;
+}
+
+extern "C" gs_status gs_log_write(gs_log* L, const gs_publish* sched, uint32_t n_msgs, const uint64_t* tc) {
+  if (!L || (!sched && n_msgs) || (!tc && n_msgs)) return GS_EINVAL;
+  const uint32_t N = L->cfg.peers;
+  for (uint32_t m = 0; m < n_msgs; m++)
+    for (uint32_t u = 0; u < N; u++) {
+      const uint64_t t = tc[(size_t)m * N + u];
+      if (t == GS_UNDELIVERED || (u == sched[m].publisher && !L->cfg.self_log)) continue;
+      log_line(L->f, &L->cfg, u, ++L->line[u], sched[m], t);
+    }
+  return ferror(L->f) ? GS_EINVAL : GS_OK;
+}
+
+extern "C" gs_status gs_log_close(gs_log* L) {
+  if (!L) return GS_EINVAL;
+  const int rc = fclose(L->f);
+  delete L;
+  return rc ? GS_EINVAL : GS_OK;
+}
+
 extern "C" gs_status gs_write_node_log(const gs_config* cfg, const char* path, const gs_publish* sched,
                                        uint64_t n_msgs, const uint64_t* t_complete_ns) {
   if (!cfg || cfg->node > GS_NODE_NIM) return GS_EINVAL;
@@ -573,19 +639,13 @@ extern "C" gs_status gs_write_node_log(const gs_config* cfg, const char* path, c
   if (!f) return GS_EINVAL;
   std::vector<char> buf(1 << 20);
   setvbuf(f, buf.data(), _IOFBF, buf.size());
-  std::vector<uint64_t> ids(n_msgs);  // msgId = uint64(rand(high(int64))) (main.nim:162), drawn per message
-  for (uint64_t m = 0; m < n_msgs; m++)
-    ids[m] = gs::rng(cfg->seed, gs::P_MSGID, sched[m].publisher, (uint32_t)(sched[m].t_pub_ns >> 32),
-                     (uint32_t)sched[m].t_pub_ns) >> 1;
   for (uint32_t u = 0; u < cfg->peers; u++) {
     uint64_t line = 0;
     for (uint64_t m = 0; m < n_msgs; m++) {
       const uint64_t t = t_complete_ns[m * cfg->peers + u];
       if (t == GS_UNDELIVERED) continue;
       if (u == sched[m].publisher && !cfg->self_log) continue;
-      const int64_t ms = ((int64_t)t - (int64_t)sched[m].t_pub_ns) / 1000000;  // delay.inMilliseconds()
-      fprintf(f, "shadow.data/hosts/peer%u/main.1000.stdout:%llu:%llu milliseconds: %lld\n", u,
-              (unsigned long long)++line, (unsigned long long)ids[m], (long long)ms);
+      log_line(f, cfg, u, ++line, sched[m], t);  // delay.inMilliseconds() (nim) = the same truncation
     }
   }
   if (fclose(f)) return GS_EINVAL;

@@ -57,6 +57,7 @@ enum : uint32_t {
 // Per-batch geometry (gs_relax.hip setup_batch).
 struct Batch {
   uint32_t B = 0, L = 0, F = 0, FP = 1, sb = 0, tshift = 0, Fe = 1;
+  uint64_t lat_min = 0;  // smallest latency between used link classes (lazy-gossip no-op proof)
   bool collide = false;
   uint64_t payload = 0, tmax = 0, delta = 1;
   std::vector<uint64_t> tpub;
@@ -135,7 +136,15 @@ struct Ctx {
   bool rpos_valid = false;
   DevBuf<uint64_t> d_pctrl;  // [3][4] pass control slots
   DevBuf<uint64_t> d_counters;  // [C_COUNT]
+  DevBuf<uint64_t> d_cnt_save;  // [C_COUNT] counters before a batch (gossip fallback restores them)
   uint64_t* h_pinned = nullptr; // pinned host mirror of ctrl + counters
+  // per-message reductions of k_complete / k_pct (gs_relax.hip)
+  DevBuf<uint64_t> d_mstat;     // [B][MS_COLS]
+  DevBuf<uint32_t> d_hist;      // [B][GS_HIST_BINS]
+  DevBuf<uint32_t> d_pbin;      // [B][2]
+  DevBuf<uint32_t> d_fine;      // [B][2][GS_HIST_MS]
+  void* h_block = nullptr;      // pinned staging of streamed result blocks (gs_result_sink.on_block)
+  size_t h_block_bytes = 0;
 
   // peer-partitioned mode (gs_part.h): this context holds keys of peers [u0, u0 + un)
   uint32_t part_parts = 1, part_idx = 0, part_u0 = 0, part_un = 0;
@@ -149,6 +158,7 @@ struct Ctx {
   gs_stats stats{};
   std::vector<hipEvent_t> ev_pool;
   int num_cus = 0;
+  uint32_t split_bpc = 0;  // blocks per CU of the split path's grid (split_blocks_per_cu)
 
   ~Ctx();
   void fail(gs_status c, const std::string& m) { throw Error(c, m); }

@@ -37,6 +37,7 @@ struct MeshArgs {
   uint64_t* counters;
   uint64_t seed;
   uint32_t N, S, epoch, bo, d, d_lo, d_hi, d_out;
+  uint32_t sub;  // the subscription epoch 0: handshake-ordered grafts
 };
 
 __device__ __forceinline__ bool is_off(const uint64_t* off, uint32_t u) {
@@ -124,9 +125,33 @@ __global__ __launch_bounds__(TB) void k_heartbeat(MeshArgs a) {
   auto flag_of = [&](uint32_t sel) {  // flags of entry sel, from the lane holding it
     return ((uint32_t)__shfl(fpack, (int)(sel & 63)) >> (8 * (sel >> 6))) & 0xFFu;
   };
+  uint64_t key[HB_PER_LANE];
+  if (a.sub) {  // subscription epoch: the first D_lo connections in subscription-arrival order
+    const uint32_t su = a.stage[u];
+#pragma unroll
+    for (int k = 0; k < HB_PER_LANE; k++) {
+      key[k] = INF64;
+      if (k * 64 < (int)deg && (uint32_t)(k * 64 + lane) < deg && !(f[k] & F_MESH)) {
+        const uint32_t sw = a.stage[w[k]];
+        const uint64_t lwu = a.lat[sw * a.S + su];
+        key[k] = (uint64_t)HS_RTTS * (a.lat[su * a.S + sw] + lwu) + lwu;
+      }
+    }
+    for (uint32_t q = 0; q < a.d_lo; q++) {
+      uint64_t bk;
+      uint32_t bi;
+      lane_min(key, lane, bk, bi);
+      const uint32_t sel = wave_argmin(bk, bi);
+      if (sel == ~0u) break;
+      if ((int)(sel & 63) == lane) {
+        drop_key(key, sel);
+        a.prop[b + sel] |= PR_GRAFT;
+      }
+    }
+    return;
+  }
   uint32_t mm = m, oo = o;
   uint32_t graft = 0;  // bit k: entry k*64 + lane grafted this epoch
-  uint64_t key[HB_PER_LANE];
   if (m < a.d_lo) {  // graft mesh_n - |mesh| random eligible peers
 #pragma unroll
     for (int k = 0; k < HB_PER_LANE; k++) {
@@ -219,7 +244,11 @@ __global__ __launch_bounds__(TB) void k_handle_graft(MeshArgs a) {
       f[k] = a.flags[b + i];
       p[k] = a.prop[b + i];
       r[k] = a.rev[b + i];
-      if (a.prop[r[k]] & PR_GRAFT) lvl[k] = a.lat[a.stage[a.col[b + i]] * a.S + sw];
+      if (a.prop[r[k]] & PR_GRAFT) {  // arrival order: latency u->w (heartbeat), handshake (subscription)
+        const uint32_t su = a.stage[a.col[b + i]];
+        lvl[k] = a.sub ? (uint64_t)(HS_RTTS + 1) * (a.lat[su * a.S + sw] + a.lat[sw * a.S + su])
+                       : a.lat[su * a.S + sw];
+      }
     }
     c += (uint32_t)__popcll(__ballot(((f[k] & F_MESH) && !(p[k] & PR_PRUNE)) || (p[k] & PR_GRAFT)));
   }
@@ -416,6 +445,22 @@ MeshArgs mesh_args(Ctx& c) {
   return a;
 }
 
+// The subscription epoch 0 from the cleared mesh (everyone online; DESIGN.md
+// §2.3): handshake-ordered grafts, GRAFT handling, apply.
+void sub_epoch(Ctx& c, MeshArgs a) {
+  if (!c.cfg.sub_graft) return;
+  const uint32_t N = c.cfg.peers;
+  hipStream_t s = c.stream;
+  a.sub = 1;
+  a.epoch = 0;
+  a.off = nullptr;
+  GS_HIP(hipMemsetAsync(c.d_prop.p, 0, c.nnz ? c.nnz : 1, s));
+  k_heartbeat<<<(N + TB / 64 - 1) / (TB / 64), TB, 0, s>>>(a);
+  k_handle_graft<<<(N + TB / 64 - 1) / (TB / 64), TB, 0, s>>>(a);
+  k_apply<<<(N + TB / 64 - 1) / (TB / 64), TB, 0, s>>>(a);
+  GS_HIP(hipGetLastError());
+}
+
 // One heartbeat epoch h >= 1 under churn: the offline set into `off`, the
 // disconnects, then A/B/C as without churn.
 void churn_epoch(Ctx& c, MeshArgs& a, uint64_t h, uint64_t* off) {
@@ -446,12 +491,17 @@ void churn_ring(Ctx& c, uint64_t h_lo, uint64_t h_hi) {
   MeshArgs a = mesh_args(c);
   if (h_lo < c.ring_lo) {  // replay from epoch 0
     if (c.nnz) k_clear_mesh<<<blocks(c.nnz), TB, 0, s>>>(c.nnz, c.d_flags.p, c.d_until.p);
-    GS_HIP(hipMemsetAsync(c.d_ring_mesh.p, 0xFF, (size_t)N * MESH_W * 4, s));  // slot 0: empty
-    GS_HIP(hipMemsetAsync(c.d_ring_off.p, 0, w64 * 8, s));
+    sub_epoch(c, a);
     c.churn_state = 0;
-    c.ring_lo = 0;
     c.ring_hi = 0;
-    ring_targets(c, 0, 0);
+    c.ring_lo = 1;
+    if (h_lo == 0) {  // slot 0: the mesh after the subscription exchange (empty without it); a
+      // row may be wider than the ELL before heartbeat 1 prunes it (GS_ERANGE below)
+      k_extract<<<blocks(N), TB, 0, s>>>(a, c.d_ring_mesh.p, nullptr);
+      GS_HIP(hipMemsetAsync(c.d_ring_off.p, 0, w64 * 8, s));
+      ring_targets(c, 0, 0);
+      c.ring_lo = 0;
+    }
   }
   for (uint64_t h = c.churn_state + 1; h <= h_hi; h++) {
     const size_t slot = (size_t)(h % R);
@@ -477,6 +527,7 @@ uint32_t run_mesh(Ctx& c, uint32_t max_hb) {
   MeshArgs a = mesh_args(c);
   if (c.nnz) k_clear_mesh<<<blocks(c.nnz), TB, 0, s>>>(c.nnz, c.d_flags.p, c.d_until.p);
   GS_HIP(hipMemsetAsync(c.d_counters.p + C_ERR, 0, 8, s));
+  sub_epoch(c, a);
   uint32_t epoch = 1, last = 0;
   uint64_t* h = c.h_pinned;
   if (c.cfg.churn_ppm) {  // no fixed point under churn: exactly max_hb epochs

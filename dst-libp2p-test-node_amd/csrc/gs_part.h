@@ -221,12 +221,12 @@ uint64_t part_begin(Ctx& c, const gs_publish* sched, uint64_t n_msgs) {
   if (c.part_open) c.fail(GS_ESTATE, "a partitioned batch is in flight (gs_part_finish first)");
   if (n_msgs < 1 || n_msgs > c.cfg.batch) c.fail(GS_EINVAL, "partitioned batch needs 1..cfg.batch messages");
   check_schedule(c, sched, n_msgs);
+  const uint32_t F = frags_of(c, sched[0]);
   for (uint64_t i = 1; i < n_msgs; i++)
-    if (sched[i].msg_size != sched[0].msg_size) c.fail(GS_EINVAL, "partitioned batch needs equal msg_size");
-  if (c.cfg.lazy_gossip) c.fail(GS_EUNSUPPORTED, "lazy gossip is not supported in partitioned mode");
+    if (sched[i].msg_size != sched[0].msg_size || frags_of(c, sched[i]) != F)
+      c.fail(GS_EINVAL, "partitioned batch needs equal msg_size and frags");
   if (c.cfg.churn_ppm) c.fail(GS_EUNSUPPORTED, "churn is not supported in partitioned mode");
-  const uint32_t F = c.cfg.fragments;
-  if (c.cfg.idontwant && sched[0].msg_size / F >= c.cfg.idontwant)
+  if (c.cfg.idontwant && frag_payload(c.cfg.node, sched[0].msg_size, F) >= c.cfg.idontwant)
     c.fail(GS_EUNSUPPORTED, "IDONTWANT is not supported in partitioned mode");
   const uint32_t FP = pow2_at_least(F), Bmax = c.cfg.batch, un = c.part_un;
   if ((uint64_t)un * Bmax * FP >= (1ull << 32)) c.fail(GS_EUNSUPPORTED, "partition needs own peers*batch*FP < 2^32");
@@ -247,7 +247,8 @@ uint64_t part_begin(Ctx& c, const gs_publish* sched, uint64_t n_msgs) {
   if (FP > 1) GS_HIP(hipMemsetAsync(c.d_busy.p, 0, (size_t)un * b.B * 8, s));
   GS_HIP(hipMemsetAsync(c.d_fbits.p, 0, (total + 63) / 64 * 8, s));
   GS_HIP(hipMemsetAsync(c.d_ctrl.p, 0xFF, 4 * 8, s));
-  c.part_grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((total + TB - 1) / TB, (uint64_t)c.num_cus * 16));
+  c.part_grid = (unsigned)std::max<uint64_t>(
+      1, std::min<uint64_t>((total + TB - 1) / TB, (uint64_t)c.num_cus * split_blocks_per_cu(c)));
   const uint64_t nwaves = (uint64_t)c.part_grid * (TB / 64), ntiles = (total + 63) / 64;
   c.part_seg_cap = (uint32_t)(((ntiles + nwaves - 1) / nwaves) * (64 / FP));
   c.d_fr_idx.alloc(nwaves * c.part_seg_cap);
@@ -328,10 +329,32 @@ uint64_t part_relax(Ctx& c, uint64_t bucket_key, const gs_part_record* rec, uint
   return c.h_pinned[0];
 }
 
+// Lazy gossip in partitioned mode: the eager result stands when gossip is a
+// no-op (gossip_noop). Each part checks its own peers; the
+// condition holds for the whole graph iff it holds in every part, so a part
+// whose peers could take an IWANT fails the batch (GS_EUNSUPPORTED) rather
+// than return a result without the gossip relaxations.
 void part_finish(Ctx& c, const gs_result_sink* sink) {
   if (!c.part_open) c.fail(GS_ESTATE, "gs_part_begin first");
   c.part_open = false;
-  launch_complete(c, c.part_b, c.part_u0, c.part_un, sink, 0);
-  c.stats.messages += c.part_b.B;
+  const Batch& b = c.part_b;
+  const bool gossip = c.cfg.lazy_gossip != 0;
+  run_complete(c, b, c.part_u0, c.part_un, gossip || (sink && sink->summary), sink && sink->summary);
+  if (gossip) {
+    std::vector<uint64_t> ms((size_t)b.B * MS_COLS), rel0(b.B);
+    GS_HIP(hipMemcpyAsync(ms.data(), c.d_mstat.p, ms.size() * 8, hipMemcpyDeviceToHost, c.stream));
+    GS_HIP(hipStreamSynchronize(c.stream));
+    const uint64_t hb = c.cfg.heartbeat_ns, ph = c.cfg.hb_phase_ns;
+    for (uint32_t q = 0; q < b.B; q++) {
+      const uint64_t tp = b.tpub[q], h0 = tp <= ph ? 0 : (tp - ph + hb - 1) / hb;
+      rel0[q] = ph + h0 * hb - tp;
+    }
+    if (!gossip_noop(b, ms.data(), rel0))
+      c.fail(GS_EUNSUPPORTED, "lazy gossip can change this batch (an IHAVE lands before the last delivery); "
+                              "partitioned mode runs eager forwarding only: use gs_run");
+    c.stats.gossip_noop_msgs += b.B;
+  }
+  deliver(c, b, c.part_u0, c.part_un, sink, 0);
+  c.stats.messages += b.B;
   collect_stats(c);
 }

@@ -16,6 +16,10 @@
 // with 64-bit atomicMin pushes into the same (m,f) slot of the targets, and
 // reduces the next pending key to pick the next bucket on the device
 // (triple-buffered ctrl words; no host round trip per bucket).
+#include <string.h>
+
+#include <algorithm>
+
 #include "gs_internal.h"
 
 namespace gs {
@@ -121,20 +125,72 @@ struct CompArgs {
   uint64_t* tc;     // [N][B] peer-major, like the keys
   uint8_t* hops;    // [N][B]
   uint64_t* counters;
-  uint32_t N, B, F, FP, L, sb, tshift, collide;
+  uint64_t* mstat;  // [B][MS_COLS] per-message reductions (k_complete / k_pct)
+  uint32_t* hist;   // [B][GS_HIST_BINS] 100 ms latency bins (summary requested), else nullptr
+  const uint32_t* pbin;  // k_pct: [B][2] the 100 ms bins holding p50 / p95
+  uint32_t* fine;   // k_pct: [B][2][GS_HIST_MS] 1 ms counts inside those bins
+  uint32_t N, B, F, FP, L, sb, tshift, collide, self_log, MT;
   uint32_t u0;  // global id of keys row 0
 };
 
+// per-message columns of mstat
+enum : uint32_t { MS_TMAX = 0, MS_UNDEL = 1, MS_LOGGED = 2, MS_LSUM = 3, MS_LMAX = 4, MS_COLS = 8 };
+
+// Lane -> (message, row offset) of the message-tiled completion kernels: a
+// wave covers MT consecutive messages of 64/MT consecutive rows (MT = 64 for
+// batches of >= 64 messages), so every load is a contiguous piece of a row
+// and every lane keeps one message for the whole kernel (per-message
+// reductions stay in registers). grid = (row chunks, message tiles).
+struct MsgTile {
+  uint32_t m, uoff, rstep;
+  bool mv;
+  __device__ MsgTile(uint32_t MT, uint32_t B) {
+    const uint32_t lane = threadIdx.x & 63;
+    m = blockIdx.y * MT + lane % MT;
+    uoff = (threadIdx.x >> 6) * (64 / MT) + lane / MT;
+    rstep = gridDim.x * (TB / 64) * (64 / MT);
+    mv = m < B;
+  }
+};
+
+// Sum per-lane values of the block's lanes that hold the same message and add
+// them to the message's global counter (LDS staging, one atomic per message).
+template <bool MAX>
+__device__ __forceinline__ void msg_flush(uint64_t v, uint64_t* lds, uint32_t MT, uint32_t m0, uint32_t B,
+                                          uint64_t* dst, uint32_t col) {
+  __syncthreads();
+  lds[threadIdx.x] = v;
+  __syncthreads();
+  if (threadIdx.x < MT && m0 + threadIdx.x < B) {
+    uint64_t t = 0;
+    for (uint32_t i = threadIdx.x; i < TB; i += MT) t = MAX ? (lds[i] > t ? lds[i] : t) : t + lds[i];
+    if (t) {
+      unsigned long long* p = (unsigned long long*)&dst[(size_t)(m0 + threadIdx.x) * MS_COLS + col];
+      if (MAX) atomicMax(p, (unsigned long long)t); else atomicAdd(p, (unsigned long long)t);
+    }
+  }
+}
+
 // Reassembly (main.rs:79-99): completion = max over fragments of the first
-// arrival. keys[(u*B + m)*FP + f] -> tc[u*B + m]: one coalesced stream (a
-// message-major write would put ~1000 resident blocks on 64 rows 8 MB apart
-// each and thrash the TLB; the transpose runs only when results are copied out).
-template <int FP>
+// arrival. keys[(u*B + m)*FP + f] -> tc[u*B + m] (peer-major; the transpose to
+// the caller's message-major sink runs only when results are copied out).
+// Per message it also reduces: the latest relative completion and the number
+// of non-publishers that never complete (the lazy-gossip no-op proof of
+// DESIGN.md §2.7), and with HIST the log lines, their latency sum / max and a
+// 100 ms histogram (gs_msg_summary).
+template <int FP, bool HIST>
 __global__ __launch_bounds__(TB) void k_complete(CompArgs a) {
-  const uint64_t total = (uint64_t)a.N * a.B;
-  uint64_t deliv = 0, lsum = 0, lmax = 0;
-  for (uint64_t i = (uint64_t)blockIdx.x * TB + threadIdx.x; i < total; i += (uint64_t)gridDim.x * TB) {
-    const uint32_t u = (uint32_t)(i / a.B), m = (uint32_t)(i - (uint64_t)u * a.B);
+  __shared__ uint64_t red[TB];
+  __shared__ uint32_t sh[HIST ? 64 * GS_HIST_BINS : 1];
+  const MsgTile mt(a.MT, a.B);
+  if (HIST)
+    for (uint32_t i = threadIdx.x; i < 64 * GS_HIST_BINS; i += TB) sh[i] = 0;
+  if (HIST) __syncthreads();
+  uint64_t deliv = 0, lsum = 0, lmax = 0, tmax = 0, undel = 0, logged = 0, lgsum = 0, lgmax = 0;
+  const uint32_t pm = mt.mv ? a.pub[mt.m] : EMPTY;
+  const uint64_t tp = mt.mv ? a.tpub[mt.m] : 0;
+  for (uint32_t u = blockIdx.x * (TB / 64) * (64 / a.MT) + mt.uoff; mt.mv && u < a.N; u += mt.rstep) {
+    const size_t i = (size_t)u * a.B + mt.m;
     const uint64_t* kp = a.keys + i * FP;
     uint64_t mk = 0;
     bool ok = true;
@@ -146,11 +202,14 @@ __global__ __launch_bounds__(TB) void k_complete(CompArgs a) {
     }
     uint64_t tc = INF64;
     uint8_t h = 0xFF;
-    const uint64_t tp = a.tpub[m];
-    if (u + a.u0 == a.pub[m]) {  // its own key is set unless it published nothing (churn)
-      if (kp[0] != INF64) { tc = tp; h = 0; }
-    }
-    else if (!a.collide && ok) {
+    int64_t lms = -1;  // logged latency in ms
+    if (u + a.u0 == pm) {  // its own key is set unless it published nothing (churn)
+      if (kp[0] != INF64) {
+        tc = tp;
+        h = 0;
+        if (a.self_log) lms = 0;
+      }
+    } else if (!a.collide && ok) {
       const uint64_t trel = mk >> a.tshift;
       tc = tp + trel;
       h = (uint8_t)((mk >> a.sb) & ((1u << HOP_BITS) - 1));
@@ -158,23 +217,78 @@ __global__ __launch_bounds__(TB) void k_complete(CompArgs a) {
       deliv++;
       lsum += ms;
       lmax = ms > lmax ? ms : lmax;
+      tmax = trel > tmax ? trel : tmax;
+      lms = (int64_t)ms;
+    } else {
+      undel++;
+    }
+    if (HIST && lms >= 0) {
+      logged++;
+      lgsum += (uint64_t)lms;
+      lgmax = (uint64_t)lms > lgmax ? (uint64_t)lms : lgmax;
+      const uint32_t bin = (uint64_t)lms / GS_HIST_MS < GS_HIST_BINS ? (uint32_t)((uint64_t)lms / GS_HIST_MS)
+                                                                       : GS_HIST_BINS - 1;
+      atomicAdd(&sh[((threadIdx.x & 63) % a.MT) * GS_HIST_BINS + bin], 1u);
     }
     a.tc[i] = tc;
     a.hops[i] = h;
   }
-  deliv = wave_sum(deliv);
-  lsum = wave_sum(lsum);
-  for (int off = 32; off > 0; off >>= 1) {
-    const uint64_t x = __shfl_xor(lmax, off);
-    lmax = x > lmax ? x : lmax;
+  {
+    const uint64_t d = wave_sum(deliv), s = wave_sum(lsum);
+    uint64_t mx = lmax;
+    for (int off = 32; off > 0; off >>= 1) {
+      const uint64_t x = __shfl_xor(mx, off);
+      mx = x > mx ? x : mx;
+    }
+    if ((threadIdx.x & 63) == 0 && d) {
+      atomicAdd((unsigned long long*)&a.counters[C_DELIV], (unsigned long long)d);
+      atomicAdd((unsigned long long*)&a.counters[C_LAT_SUM], (unsigned long long)s);
+      atomicMax((unsigned long long*)&a.counters[C_LAT_MAX], (unsigned long long)mx);
+    }
   }
-  if ((threadIdx.x & 63) == 0 && deliv) {
-    atomicAdd((unsigned long long*)&a.counters[C_DELIV], (unsigned long long)deliv);
-    atomicAdd((unsigned long long*)&a.counters[C_LAT_SUM], (unsigned long long)lsum);
-    atomicMax((unsigned long long*)&a.counters[C_LAT_MAX], (unsigned long long)lmax);
+  if (!a.mstat) return;  // block-uniform
+  const uint32_t m0 = blockIdx.y * a.MT;
+  msg_flush<true>(tmax, red, a.MT, m0, a.B, a.mstat, MS_TMAX);
+  msg_flush<false>(undel, red, a.MT, m0, a.B, a.mstat, MS_UNDEL);
+  if constexpr (HIST) {
+    msg_flush<false>(logged, red, a.MT, m0, a.B, a.mstat, MS_LOGGED);
+    msg_flush<false>(lgsum, red, a.MT, m0, a.B, a.mstat, MS_LSUM);
+    msg_flush<true>(lgmax, red, a.MT, m0, a.B, a.mstat, MS_LMAX);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < a.MT * GS_HIST_BINS; i += TB) {
+      const uint32_t mm = m0 + i / GS_HIST_BINS;
+      if (sh[i] && mm < a.B) atomicAdd(&a.hist[(size_t)mm * GS_HIST_BINS + i % GS_HIST_BINS], sh[i]);
+    }
   }
 }
 
+// Exact percentiles, second pass: 1 ms counts inside the two 100 ms bins that
+// hold each message's p50 / p95 rank (the host picked them from the histogram).
+__global__ __launch_bounds__(TB) void k_pct(CompArgs a) {
+  __shared__ uint32_t sf[64 * 2 * GS_HIST_MS];
+  const MsgTile mt(a.MT, a.B);
+  for (uint32_t i = threadIdx.x; i < 64 * 2 * GS_HIST_MS; i += TB) sf[i] = 0;
+  __syncthreads();
+  const uint32_t pm = mt.mv ? a.pub[mt.m] : EMPTY;
+  const uint64_t tp = mt.mv ? a.tpub[mt.m] : 0;
+  const uint32_t b50 = mt.mv ? a.pbin[mt.m * 2] : ~0u, b95 = mt.mv ? a.pbin[mt.m * 2 + 1] : ~0u;
+  const uint32_t ml = (threadIdx.x & 63) % a.MT;
+  for (uint32_t u = blockIdx.x * (TB / 64) * (64 / a.MT) + mt.uoff; mt.mv && u < a.N; u += mt.rstep) {
+    const uint64_t t = a.tc[(size_t)u * a.B + mt.m];
+    if (t == INF64 || (u + a.u0 == pm && !a.self_log)) continue;
+    const uint64_t ms = (t - tp) / 1000000ull;
+    const uint32_t bin = ms / GS_HIST_MS < GS_HIST_BINS ? (uint32_t)(ms / GS_HIST_MS) : GS_HIST_BINS - 1;
+    const uint32_t r = bin == GS_HIST_BINS - 1 ? GS_HIST_MS - 1 : (uint32_t)(ms % GS_HIST_MS);
+    if (bin == b50) atomicAdd(&sf[(ml * 2) * GS_HIST_MS + r], 1u);
+    if (bin == b95) atomicAdd(&sf[(ml * 2 + 1) * GS_HIST_MS + r], 1u);
+  }
+  __syncthreads();
+  const uint32_t m0 = blockIdx.y * a.MT;
+  for (uint32_t i = threadIdx.x; i < a.MT * 2 * GS_HIST_MS; i += TB) {
+    const uint32_t mm = m0 + i / (2 * GS_HIST_MS);
+    if (sf[i] && mm < a.B) atomicAdd(&a.fine[(size_t)mm * 2 * GS_HIST_MS + i % (2 * GS_HIST_MS)], sf[i]);
+  }
+}
 
 // [N][B] -> [B][N] through a 64x64 LDS tile, for the caller's message-major
 // sink (include/gossipsim.h); not on the device-resident path.
@@ -306,10 +420,15 @@ uint32_t pow2_at_least(uint32_t x) { uint32_t p = 1; while (p < x) p <<= 1; retu
 
 }  // namespace
 
+// Chunks of one publish (PublishCommand.chunks, main.rs:65-71,163-168): the
+// row's own count, 0 = FRAGMENTS of the node (env.rs:64-67).
+static uint32_t frags_of(const Ctx& c, const gs_publish& p) { return p.frags ? p.frags : c.cfg.fragments; }
+
 static void check_schedule(Ctx& c, const gs_publish* sched, uint64_t n_msgs) {
   for (uint64_t i = 0; i < n_msgs; i++) {
     if (sched[i].publisher >= c.cfg.peers) c.fail(GS_EINVAL, "publisher id out of range");
-    if (frag_invalid(c.cfg.node, sched[i].msg_size, c.cfg.fragments))  // the node's publish fails
+    if (sched[i].frags > MAX_FRAGS) c.fail(GS_EINVAL, "frags must be in 0..16 (0 = cfg.fragments)");
+    if (frag_invalid(c.cfg.node, sched[i].msg_size, frags_of(c, sched[i])))  // the node's publish fails
       c.fail(GS_EINVAL, c.cfg.node == NODE_RUST ? "fragment payload shorter than the 8-byte tx_time stamp"
                         : c.cfg.node == NODE_GO ? "fragment too short for its chunk byte (payload[10])"
                                                 : "fragment shorter than the 16-byte nim header + chunk byte");
@@ -321,7 +440,7 @@ static void check_schedule(Ctx& c, const gs_publish* sched, uint64_t n_msgs) {
 static Batch setup_batch(Ctx& c, const gs_publish* sched, uint64_t i0, uint64_t i1) {
   Batch b;
   const uint32_t N = c.cfg.peers, S = c.S;
-  b.F = c.cfg.fragments;
+  b.F = frags_of(c, sched[i0]);
   b.FP = pow2_at_least(b.F);
   b.B = (uint32_t)(i1 - i0);
   b.L = b.B * b.FP;
@@ -351,6 +470,7 @@ static Batch setup_batch(Ctx& c, const gs_publish* sched, uint64_t i0, uint64_t 
     if (c.stage_used[x]) min_ser = std::min(min_ser, up);
   }
   b.delta = std::max<uint64_t>(1, min_lat + min_ser);
+  b.lat_min = min_lat;
   b.tpub.resize(b.B);
   for (uint32_t q = 0; q < b.B; q++) { pub[q] = sched[i0 + q].publisher; b.tpub[q] = sched[i0 + q].t_pub_ns; }
   c.d_pub.alloc(c.cfg.batch);
@@ -394,38 +514,183 @@ static void launch_seed(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, uint64
   GS_HIP(hipGetLastError());
 }
 
-// Completion of the keys rows [0, un) (global ids u0 + row) into d_tc/d_hops,
-// then the message-major copy into sink[q * un + row] for q < B.
-static void launch_complete(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, const gs_result_sink* sink,
-                            uint64_t sink_row0) {
+// k_complete over the keys rows [0, un) (global ids u0 + row) into d_tc /
+// d_hops; with `mstat` also the per-message reductions, with `hist` the
+// 100 ms histograms of gs_msg_summary.
+static void run_complete(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, bool mstat, bool hist) {
   hipStream_t s = c.stream;
   CompArgs ca{};
   ca.keys = c.d_keys.p; ca.pub = c.d_pub.p; ca.tpub = c.d_tpub.p; ca.tc = c.d_tc.p;
   ca.hops = c.d_hops.p; ca.counters = c.d_counters.p; ca.N = un; ca.B = b.B; ca.F = b.F;
   ca.FP = b.FP; ca.L = b.L; ca.sb = b.sb; ca.tshift = b.tshift; ca.collide = b.collide ? 1 : 0;
   ca.u0 = u0;
-  const unsigned cgrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(((uint64_t)un * b.B + TB - 1) / TB,
-                                                                            (uint64_t)c.num_cus * 16));
-  switch (b.FP) {
-    case 1: k_complete<1><<<cgrid, TB, 0, s>>>(ca); break;
-    case 2: k_complete<2><<<cgrid, TB, 0, s>>>(ca); break;
-    case 4: k_complete<4><<<cgrid, TB, 0, s>>>(ca); break;
-    case 8: k_complete<8><<<cgrid, TB, 0, s>>>(ca); break;
-    default: k_complete<16><<<cgrid, TB, 0, s>>>(ca); break;
+  ca.self_log = c.cfg.self_log;
+  ca.MT = std::min<uint32_t>(64, pow2_at_least(b.B));
+  if (mstat || hist) {
+    c.d_mstat.alloc((size_t)c.cfg.batch * MS_COLS);
+    GS_HIP(hipMemsetAsync(c.d_mstat.p, 0, (size_t)b.B * MS_COLS * 8, s));
+    ca.mstat = c.d_mstat.p;
   }
+  if (hist) {
+    c.d_hist.alloc((size_t)c.cfg.batch * GS_HIST_BINS);
+    GS_HIP(hipMemsetAsync(c.d_hist.p, 0, (size_t)b.B * GS_HIST_BINS * 4, s));
+    ca.hist = c.d_hist.p;
+  }
+  const uint32_t tiles = (b.B + ca.MT - 1) / ca.MT;
+  const uint64_t rows_per_block = (TB / 64) * (64 / ca.MT);
+  const uint64_t want = std::max<uint64_t>(1, (uint64_t)c.num_cus * 16 / tiles);
+  dim3 grid((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((un + rows_per_block - 1) / rows_per_block, want)),
+            tiles);
+#define GS_COMPLETE(FPV)                                                      \
+  if (hist) k_complete<FPV, true><<<grid, TB, 0, s>>>(ca);                    \
+  else k_complete<FPV, false><<<grid, TB, 0, s>>>(ca);
+  switch (b.FP) {
+    case 1: GS_COMPLETE(1) break;
+    case 2: GS_COMPLETE(2) break;
+    case 4: GS_COMPLETE(4) break;
+    case 8: GS_COMPLETE(8) break;
+    default: GS_COMPLETE(16) break;
+  }
+#undef GS_COMPLETE
   GS_HIP(hipGetLastError());
-  if (sink && (sink->t_complete_ns || sink->hops)) {  // message-major copy-out
+}
+
+// Nearest-rank percentile (rank ceil(q*n)) resolved from the 100 ms histogram:
+// the bin holding the rank, and the rank left inside that bin.
+static void pct_bin(const uint32_t* h, uint64_t n, uint32_t q100, uint32_t* bin, uint64_t* rest) {
+  const uint64_t rank = (n * q100 + 99) / 100;
+  uint64_t acc = 0;
+  for (uint32_t k = 0; k < GS_HIST_BINS; k++) {
+    if (acc + h[k] >= rank) { *bin = k; *rest = rank - acc; return; }
+    acc += h[k];
+  }
+  *bin = GS_HIST_BINS - 1;
+  *rest = 0;
+}
+
+// gs_msg_summary of the batch's messages (rows [0, un) of d_tc): counts and
+// histograms from k_complete, exact p50 / p95 from k_pct's 1 ms counts inside
+// the two bins (a rank in the open last bin is read from the message's column).
+static void fill_summary(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, gs_msg_summary* out) {
+  hipStream_t s = c.stream;
+  const uint32_t B = b.B;
+  std::vector<uint64_t> ms((size_t)B * MS_COLS);
+  std::vector<uint32_t> hist((size_t)B * GS_HIST_BINS), pbin((size_t)B * 2, ~0u), rest((size_t)B * 2, 0);
+  GS_HIP(hipMemcpyAsync(ms.data(), c.d_mstat.p, ms.size() * 8, hipMemcpyDeviceToHost, s));
+  GS_HIP(hipMemcpyAsync(hist.data(), c.d_hist.p, hist.size() * 4, hipMemcpyDeviceToHost, s));
+  GS_HIP(hipStreamSynchronize(s));
+  std::vector<uint32_t> slow;  // messages whose p50 or p95 lies in the open last bin
+  for (uint32_t q = 0; q < B; q++) {
+    gs_msg_summary& r = out[q];
+    memset(&r, 0, sizeof r);
+    r.delivered = ms[(size_t)q * MS_COLS + MS_LOGGED];
+    r.lat_sum_ms = ms[(size_t)q * MS_COLS + MS_LSUM];
+    r.max_ms = (uint32_t)ms[(size_t)q * MS_COLS + MS_LMAX];
+    memcpy(r.hist, &hist[(size_t)q * GS_HIST_BINS], sizeof r.hist);
+    if (!r.delivered) continue;
+    uint64_t rs[2];
+    uint32_t bn[2];
+    pct_bin(r.hist, r.delivered, 50, &bn[0], &rs[0]);
+    pct_bin(r.hist, r.delivered, 95, &bn[1], &rs[1]);
+    if (bn[0] == GS_HIST_BINS - 1 || bn[1] == GS_HIST_BINS - 1) { slow.push_back(q); continue; }
+    for (int k = 0; k < 2; k++) { pbin[q * 2 + k] = bn[k]; rest[q * 2 + k] = (uint32_t)rs[k]; }
+  }
+  c.d_pbin.alloc((size_t)c.cfg.batch * 2);
+  c.d_fine.alloc((size_t)c.cfg.batch * 2 * GS_HIST_MS);
+  GS_HIP(hipMemcpyAsync(c.d_pbin.p, pbin.data(), pbin.size() * 4, hipMemcpyHostToDevice, s));
+  GS_HIP(hipMemsetAsync(c.d_fine.p, 0, (size_t)B * 2 * GS_HIST_MS * 4, s));
+  CompArgs ca{};
+  ca.pub = c.d_pub.p; ca.tpub = c.d_tpub.p; ca.tc = c.d_tc.p; ca.N = un; ca.B = B; ca.u0 = u0;
+  ca.self_log = c.cfg.self_log; ca.pbin = c.d_pbin.p; ca.fine = c.d_fine.p;
+  ca.MT = std::min<uint32_t>(64, pow2_at_least(B));
+  const uint32_t tiles = (B + ca.MT - 1) / ca.MT;
+  const uint64_t rows_per_block = (TB / 64) * (64 / ca.MT);
+  dim3 grid((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((un + rows_per_block - 1) / rows_per_block,
+                                                               std::max<uint64_t>(1, (uint64_t)c.num_cus * 8 / tiles))),
+            tiles);
+  k_pct<<<grid, TB, 0, s>>>(ca);
+  GS_HIP(hipGetLastError());
+  std::vector<uint32_t> fine((size_t)B * 2 * GS_HIST_MS);
+  GS_HIP(hipMemcpyAsync(fine.data(), c.d_fine.p, fine.size() * 4, hipMemcpyDeviceToHost, s));
+  GS_HIP(hipStreamSynchronize(s));
+  for (uint32_t q = 0; q < B; q++) {
+    if (pbin[q * 2] == ~0u) continue;
+    for (int k = 0; k < 2; k++) {
+      const uint32_t* f = &fine[((size_t)q * 2 + k) * GS_HIST_MS];
+      uint64_t acc = 0;
+      uint32_t r = 0;
+      while (r < GS_HIST_MS - 1 && acc + f[r] < rest[q * 2 + k]) acc += f[r++];
+      (k ? out[q].p95_ms : out[q].p50_ms) = pbin[q * 2 + k] * GS_HIST_MS + r;
+    }
+  }
+  for (uint32_t q : slow) {  // rare (heavy churn tails): the column, sorted on the host
+    std::vector<uint64_t> col(un);
+    GS_HIP(hipMemcpy2DAsync(col.data(), 8, c.d_tc.p + q, (size_t)B * 8, 8, un, hipMemcpyDeviceToHost, s));
+    std::vector<uint32_t> pub(1);
+    GS_HIP(hipMemcpyAsync(pub.data(), c.d_pub.p + q, 4, hipMemcpyDeviceToHost, s));
+    GS_HIP(hipStreamSynchronize(s));
+    std::vector<uint64_t> v;
+    for (uint32_t u = 0; u < un; u++)
+      if (col[u] != INF64 && (u + u0 != pub[0] || c.cfg.self_log)) v.push_back((col[u] - b.tpub[q]) / 1000000ull);
+    std::sort(v.begin(), v.end());
+    const uint64_t n = v.size();
+    out[q].p50_ms = (uint32_t)v[(n * 50 + 99) / 100 - 1];
+    out[q].p95_ms = (uint32_t)v[(n * 95 + 99) / 100 - 1];
+  }
+}
+
+// Results of the batch to the caller: message-major copy into the sink
+// arrays (rows sink_row0..), or streamed in blocks through on_block; then the
+// per-message summaries.
+static void deliver(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, const gs_result_sink* sink,
+                    uint64_t sink_row0) {
+  if (!sink) return;
+  hipStream_t s = c.stream;
+  const bool want_tc = sink->t_complete_ns != nullptr, want_h = sink->hops != nullptr;
+  if (want_tc || want_h) {
     c.d_tc_t.alloc((size_t)un * c.cfg.batch);
     c.d_hops_t.alloc((size_t)un * c.cfg.batch);
     dim3 tg((un + 63) / 64, (b.B + 63) / 64);
     k_transpose<<<tg, TB, 0, s>>>(c.d_tc.p, c.d_hops.p, c.d_tc_t.p, c.d_hops_t.p, un, b.B);
     GS_HIP(hipGetLastError());
-    if (sink->t_complete_ns)
-      GS_HIP(hipMemcpyAsync(sink->t_complete_ns + sink_row0 * un, c.d_tc_t.p, (size_t)b.B * un * 8,
-                            hipMemcpyDeviceToHost, s));
-    if (sink->hops)
-      GS_HIP(hipMemcpyAsync(sink->hops + sink_row0 * un, c.d_hops_t.p, (size_t)b.B * un, hipMemcpyDeviceToHost, s));
+    if (!sink->on_block) {
+      if (want_tc)
+        GS_HIP(hipMemcpyAsync(sink->t_complete_ns + sink_row0 * un, c.d_tc_t.p, (size_t)b.B * un * 8,
+                              hipMemcpyDeviceToHost, s));
+      if (want_h)
+        GS_HIP(hipMemcpyAsync(sink->hops + sink_row0 * un, c.d_hops_t.p, (size_t)b.B * un, hipMemcpyDeviceToHost, s));
+    } else {  // stream: blocks of bm messages through one pinned staging buffer
+      const uint32_t bm = std::max<uint32_t>(1, std::min<uint32_t>(sink->block_msgs ? sink->block_msgs : 64, b.B));
+      const size_t need = (size_t)bm * un * 9;
+      if (c.h_block_bytes < need) {
+        if (c.h_block) GS_HIP(hipHostFree(c.h_block));
+        c.h_block = nullptr;
+        c.h_block_bytes = 0;
+        GS_HIP(hipHostMalloc(&c.h_block, need, hipHostMallocDefault));
+        c.h_block_bytes = need;
+      }
+      uint64_t* htc = (uint64_t*)c.h_block;
+      uint8_t* hh = (uint8_t*)(htc + (size_t)bm * un);
+      for (uint32_t q0 = 0; q0 < b.B; q0 += bm) {
+        const uint32_t n = std::min(bm, b.B - q0);
+        if (want_tc)
+          GS_HIP(hipMemcpyAsync(htc, c.d_tc_t.p + (size_t)q0 * un, (size_t)n * un * 8, hipMemcpyDeviceToHost, s));
+        if (want_h)
+          GS_HIP(hipMemcpyAsync(hh, c.d_hops_t.p + (size_t)q0 * un, (size_t)n * un, hipMemcpyDeviceToHost, s));
+        GS_HIP(hipStreamSynchronize(s));
+        sink->on_block(sink->user, sink_row0 + q0, n, un, want_tc ? htc : nullptr, want_h ? hh : nullptr);
+      }
+    }
   }
+  if (sink->summary) fill_summary(c, b, u0, un, sink->summary + sink_row0);
+}
+
+// Completion + delivery of a finished batch.
+static void launch_complete(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, const gs_result_sink* sink,
+                            uint64_t sink_row0) {
+  const bool hist = sink && sink->summary;
+  run_complete(c, b, u0, un, hist, hist);
+  deliver(c, b, u0, un, sink, sink_row0);
 }
 
 // Per-peer traffic of the batch just finished (keys final, before the next reset).
@@ -544,32 +809,56 @@ extern "C" int gs_debug_pull_prof(uint64_t* out) {  // 32 passes x 8 slots; read
 }
 #endif
 
+// Blocks per CU of the split (push) path's scan / frontier / gossip grid: 4
+// measured best on config #3 (k_scan 177 -> 136 us, k_frontier 65 -> 38 us per
+// bucket vs 16; 1-2 and 32-64 slower, profiles/r01_v10/c3_grid_sweep.txt).
+// GS_SPLIT_BLOCKS_PER_CU overrides it (read once per context).
+static uint32_t split_blocks_per_cu(Ctx& c) {
+  if (!c.split_bpc) {
+    const char* e = getenv("GS_SPLIT_BLOCKS_PER_CU");
+    c.split_bpc = e && *e ? (uint32_t)std::max(1, atoi(e)) : 4u;
+  }
+  return c.split_bpc;
+}
+
+// Lazy gossip is a no-op for message q when every non-publisher completed and
+// the last completion lies before the first IHAVE can arrive: the earliest
+// gossip heartbeat is rel0 (the first one at or after t_pub; every gossiping
+// peer holds the message by then at the latest) and an IHAVE travels at least
+// the smallest link latency. Then every IHAVE target has seen the message, no
+// IWANT is sent and no key changes.
+static bool gossip_noop(const Batch& b, const uint64_t* ms, const std::vector<uint64_t>& rel0) {
+  for (uint32_t q = 0; q < b.B; q++)
+    if (ms[(size_t)q * MS_COLS + MS_UNDEL] || ms[(size_t)q * MS_COLS + MS_TMAX] >= rel0[q] + b.lat_min) return false;
+  return true;
+}
+
 void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_result_sink* sink) {
-  const uint32_t N = c.cfg.peers, F = c.cfg.fragments, FP = pow2_at_least(F);
+  const uint32_t N = c.cfg.peers;
   const uint32_t Bmax = c.cfg.batch;
   hipStream_t s = c.stream;
   GS_HIP(hipMemsetAsync(c.d_counters.p + C_ERR, 0, 8, s));
   check_schedule(c, sched, n_msgs);
+  uint32_t Fmax = 1;
+  for (uint64_t i = 0; i < n_msgs; i++) Fmax = std::max(Fmax, frags_of(c, sched[i]));
+  const uint32_t FPmax = pow2_at_least(Fmax);
   const char* var_env = getenv("GS_RELAX_VARIANT");
   // default: owner-computes pull (32); without it the push path: split (8) + final bitset (4) + read filter (1)
   uint32_t variant = var_env && *var_env ? (uint32_t)atoi(var_env) : 45u;
-  if ((uint64_t)N * Bmax * FP >= (1ull << 32)) {  // frontier indices are u32
-    if (c.cfg.lazy_gossip) c.fail(GS_EUNSUPPORTED, "lazy gossip needs peers*batch*FP < 2^32");
-    variant &= ~8u;
-  }
+  const bool lanes32 = (uint64_t)N * Bmax * FPmax < (1ull << 32);  // frontier indices are u32
+  if (!lanes32) variant &= ~8u;
   const bool gossip = c.cfg.lazy_gossip != 0;
   // the pull path needs rows in LDS and no cross-row reads (IDONTWANT reads the
-  // target's key, lazy gossip pushes from heartbeats): those stay on the push path
+  // target's key) and one mesh per batch (churn uses one per epoch): those stay
+  // on the push path. Lazy gossip runs on the pull path when the batch proves
+  // it a no-op (gossip_noop), else the batch is re-run on the push path.
   const bool idw_any = c.cfg.idontwant != 0;
   const bool churn = c.cfg.churn_ppm != 0;  // per-epoch mesh lookups live on the push path
-  if (c.traffic && (gossip || churn))
-    c.fail(GS_EUNSUPPORTED, "per-peer traffic covers eager forwarding: turn off lazy gossip and churn");
-  const bool pull = (variant & 32) && !gossip && !idw_any && !churn;
-  // pull rows live in registers: cap the batch at PULL_LMAX / FP messages
-  const uint32_t Bcap = pull ? std::max<uint32_t>(1, std::min<uint32_t>(Bmax, PULL_LMAX / FP)) : Bmax;
-  if (gossip || churn) {  // gossip and churn run on the split path only, without tile skip
-    variant = (variant | 8u) & ~2u;
-  }
+  if (c.traffic && churn) c.fail(GS_EUNSUPPORTED, "per-peer traffic covers a frozen mesh: turn off churn");
+  const bool pull_any = (variant & 32) && !idw_any && !churn;
+  // the push path with gossip or churn runs split, without tile skip
+  const uint32_t pvariant = (gossip || churn) ? ((variant | 8u) & ~2u & ~32u) : (variant & ~32u);
+  if (churn && !lanes32) c.fail(GS_EUNSUPPORTED, "churn needs peers*batch*FP < 2^32");
   std::vector<uint64_t> q0v(Bmax), r0v(Bmax), ep(churn ? n_msgs : 0);
   if (churn) {  // epoch of every publish; the snapshot ring
     const uint64_t hb = c.cfg.heartbeat_ns, ph = c.cfg.hb_phase_ns;
@@ -581,7 +870,8 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     if (!c.ring_R) {
       const uint64_t w64 = ((uint64_t)N + 63) / 64;
       const uint64_t per_slot = (uint64_t)N * MESH_W * 4 + w64 * 8 + (gossip ? (uint64_t)N * (GT_W * 4 + 1) : 0);
-      const uint64_t budget = 8ull << 30;
+      const char* rb = getenv("GS_RING_BUDGET_MB");  // test knob: force batch cuts at the ring size
+      const uint64_t budget = rb && *rb ? (uint64_t)atoll(rb) << 20 : 16ull << 30;
       const uint64_t want = (uint64_t)Bmax + c.cfg.churn_horizon + 1;
       c.ring_R = (uint32_t)std::min<uint64_t>(want, std::max<uint64_t>(c.cfg.churn_horizon + 2, budget / per_slot));
       c.d_ring_mesh.alloc((size_t)c.ring_R * N * MESH_W);
@@ -592,13 +882,14 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       }
     }
   }
-  const size_t max_tiles = ((size_t)N * Bmax * FP + 63) / 64;
-  c.d_keys.alloc((size_t)N * Bmax * FP);
+  const size_t max_tiles = ((size_t)N * Bmax * FPmax + 63) / 64;
+  c.d_keys.alloc((size_t)N * Bmax * FPmax);
   c.d_meta.alloc(max_tiles * sizeof(TileMeta) / 8);
   c.d_fbits.alloc(max_tiles);
-  if (FP > 1) c.d_busy.alloc((size_t)N * Bmax);
+  if (FPmax > 1) c.d_busy.alloc((size_t)N * Bmax);
   c.d_tc.alloc((size_t)N * Bmax);
   c.d_hops.alloc((size_t)N * Bmax);
+  c.d_cnt_save.alloc(C_COUNT);
   std::vector<uint64_t> rel0(Bmax), habs0(Bmax);
   // Timing events come from a per-context pool: [0] run start, [1] run end,
   // then one (start, scan end, end) triple around every relaxation launch.
@@ -620,10 +911,16 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
   const int dev_cus = c.num_cus;
   uint64_t i0 = 0;
   while (i0 < n_msgs) {
-    // a batch: up to B messages of equal size (serialisation tables are per batch)
+    // a batch: up to B messages of equal size and chunk count (serialisation
+    // tables and the lane layout are per batch); the pull path holds a row in
+    // registers, so its batch is capped at PULL_LMAX / FP messages
+    const uint32_t F0 = frags_of(c, sched[i0]);
+    const uint32_t Bcap = pull_any ? std::max<uint32_t>(1, std::min<uint32_t>(Bmax, PULL_LMAX / pow2_at_least(F0)))
+                                   : Bmax;
     uint64_t i1 = i0 + 1;
     uint64_t h_lo = churn ? ep[i0] : 0, h_hi = churn ? ep[i0] : 0;  // churn: publish epochs of the batch
-    while (i1 < n_msgs && i1 - i0 < Bcap && sched[i1].msg_size == sched[i0].msg_size) {
+    while (i1 < n_msgs && i1 - i0 < Bcap && sched[i1].msg_size == sched[i0].msg_size &&
+           frags_of(c, sched[i1]) == F0) {
       if (churn) {  // the batch's epochs (+ lifetime) must fit the ring
         const uint64_t lo2 = std::min(h_lo, ep[i1]), hi2 = std::max(h_hi, ep[i1]);
         if (hi2 + c.cfg.churn_horizon - lo2 + 1 > c.ring_R) break;
@@ -633,6 +930,7 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       i1++;
     }
     const Batch b = setup_batch(c, sched, i0, i1);
+    const uint32_t FP = b.FP, F = b.F;
     if (churn) {
       churn_ring(c, h_lo, h_hi + c.cfg.churn_horizon);
       const uint64_t hb = c.cfg.heartbeat_ns, ph = c.cfg.hb_phase_ns;
@@ -659,111 +957,152 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       c.d_habs0.alloc(Bmax);
       GS_HIP(hipMemcpyAsync(c.d_rel0.p, rel0.data(), B * 8, hipMemcpyHostToDevice, s));
       GS_HIP(hipMemcpyAsync(c.d_habs0.p, habs0.data(), B * 8, hipMemcpyHostToDevice, s));
+      GS_HIP(hipStreamSynchronize(s));  // rel0 / habs0 host vectors are rewritten by the next batch
     }
     const uint64_t total = (uint64_t)N * L;
-    GS_HIP(hipMemsetAsync(c.d_keys.p, 0xFF, total * 8, s));
-    if (FP > 1) GS_HIP(hipMemsetAsync(c.d_busy.p, 0, (size_t)N * B * 8, s));
-    if (variant & 2) GS_HIP(hipMemsetAsync(c.d_meta.p, 0, (total + 63) / 64 * sizeof(TileMeta), s));
-    if ((variant & 12) && !pull) GS_HIP(hipMemsetAsync(c.d_fbits.p, 0, (total + 63) / 64 * 8, s));
-    if ((variant & 10) == 10) {  // split + tile skip: tmin 0 forces every tile's first scan
-      c.d_tmin.alloc(max_tiles);
-      c.d_touched.alloc(max_tiles);
-      GS_HIP(hipMemsetAsync(c.d_tmin.p, 0, (total + 63) / 64 * 8, s));
-      GS_HIP(hipMemsetAsync(c.d_touched.p, 0, (total + 63) / 64, s));
+    auto reset = [&](uint32_t v, bool with_gossip) {  // fresh keys and bucket state for this batch
+      GS_HIP(hipMemsetAsync(c.d_keys.p, 0xFF, total * 8, s));
+      if (FP > 1) GS_HIP(hipMemsetAsync(c.d_busy.p, 0, (size_t)N * B * 8, s));
+      if (v & 32) return;
+      if (v & 2) GS_HIP(hipMemsetAsync(c.d_meta.p, 0, (total + 63) / 64 * sizeof(TileMeta), s));
+      if (v & 12) GS_HIP(hipMemsetAsync(c.d_fbits.p, 0, (total + 63) / 64 * 8, s));
+      if ((v & 10) == 10) {  // split + tile skip: tmin 0 forces every tile's first scan
+        c.d_tmin.alloc(max_tiles);
+        c.d_touched.alloc(max_tiles);
+        GS_HIP(hipMemsetAsync(c.d_tmin.p, 0, (total + 63) / 64 * 8, s));
+        GS_HIP(hipMemsetAsync(c.d_touched.p, 0, (total + 63) / 64, s));
+      }
+      GS_HIP(hipMemsetAsync(c.d_ctrl.p, 0xFF, 4 * 8, s));
+      // with gossip the first bucket is [0, Delta): the publisher's own IHAVEs
+      // can land before the first eager arrival
+      if (with_gossip) GS_HIP(hipMemsetAsync(c.d_ctrl.p, 0, 8, s));
+    };
+    // One batch on the push path: k_seed, then bucket launches in chunks of 8
+    // until the ctrl word of the next bucket is empty.
+    auto push_run = [&](uint32_t v, bool with_gossip) {
+      reset(v, with_gossip);
+      launch_seed(c, b, 0, N);
+      RelaxArgs ra{};
+      set_churn_args(c, ra);
+      ra.keys = c.d_keys.p; ra.busy = c.d_busy.p; ra.mesh = c.d_mesh.p; ra.pub = c.d_pub.p;
+      ra.meta = reinterpret_cast<TileMeta*>(c.d_meta.p);
+      ra.fbits = c.d_fbits.p;
+      ra.tmin = c.d_tmin.p;
+      ra.touched = c.d_touched.p;
+      ra.stage = c.d_stage.p; ra.tables = c.d_tables.p; ra.ctrl = c.d_ctrl.p;
+      ra.counters = c.d_counters.p; ra.total = total; ra.delta = b.delta; ra.tmax = b.tmax;
+      ra.N = N; ra.B = B; ra.F = F; ra.L = L; ra.S = c.S; ra.sb = b.sb; ra.tshift = b.tshift;
+      ra.idw = (c.cfg.idontwant && b.payload >= c.cfg.idontwant) ? 1 : 0;
+      const uint64_t need = (total + TB - 1) / TB;
+      const unsigned grid = (unsigned)std::min<uint64_t>(need, (uint64_t)dev_cus * split_blocks_per_cu(c));
+      if (v & 8) {  // frontier segments: one per scan wave
+        const uint64_t nwaves = (uint64_t)grid * (TB / 64), ntiles = (total + 63) / 64;
+        ra.seg_cap = (uint32_t)(((ntiles + nwaves - 1) / nwaves) * (64 / FP));
+        c.d_fr_idx.alloc(nwaves * ra.seg_cap);
+        if (FP == 1) c.d_fr_key.alloc(nwaves * ra.seg_cap);
+        c.d_fr_cnt.alloc(nwaves);
+        ra.fr_idx = c.d_fr_idx.p;
+        ra.fr_key = c.d_fr_key.p;
+        ra.fr_cnt = c.d_fr_cnt.p;
+        if (with_gossip) {  // gossip list: per-lane entries, one segment per scan wave
+          ra.gl_cap = (uint32_t)(((ntiles + nwaves - 1) / nwaves) * 64);
+          c.d_gl_idx.alloc(nwaves * ra.gl_cap);
+          c.d_gl_cnt.alloc(nwaves);
+          c.d_nonfinal.alloc(3);
+          GS_HIP(hipMemsetAsync(c.d_nonfinal.p, 0, 3 * 8, s));
+          ra.gl_idx = c.d_gl_idx.p;
+          ra.gl_cnt = c.d_gl_cnt.p;
+          ra.nonfinal = c.d_nonfinal.p;
+          ra.rel0 = c.d_rel0.p;
+          ra.habs0 = c.d_habs0.p;
+          ra.row = c.d_row.p;
+          ra.col = c.d_col.p;
+          ra.hb_ns = c.cfg.heartbeat_ns;
+          ra.seed = c.cfg.seed;
+          ra.gossip = 1;
+          if (churn) {
+            ra.ring_tgt = c.d_ring_tgt.p;
+            ra.ring_tcnt = c.d_ring_tcnt.p;
+          }
+          ra.hist = c.cfg.history_gossip;
+          ra.d_lazy = c.cfg.d_lazy;
+          ra.gf_milli = c.cfg.gossip_factor_milli;
+        }
+      }
+      uint32_t launch = 0;
+      const uint32_t chunk = 8;
+      for (;;) {
+        for (uint32_t q = 0; q < chunk; q++) {
+          ra.launch = launch++;
+          if (c.timing) {  // (start, scan end, end) per bucket
+            GS_HIP(hipEventRecord(ev(n_ev), s));
+            const hipEvent_t mid = ev(n_ev + 1);
+            if (v & 8) relax_dispatch(FP, v, ra, grid, s, mid);
+            else {
+              relax_dispatch(FP, v, ra, grid, s);
+              GS_HIP(hipEventRecord(mid, s));
+            }
+            GS_HIP(hipEventRecord(ev(n_ev + 2), s));
+            n_ev += 3;
+          } else {
+            relax_dispatch(FP, v, ra, grid, s);
+          }
+        }
+        GS_HIP(hipGetLastError());
+        GS_HIP(hipMemcpyAsync(c.h_pinned, c.d_ctrl.p, 3 * 8, hipMemcpyDeviceToHost, s));
+        GS_HIP(hipStreamSynchronize(s));
+        if (c.h_pinned[launch % 3] == INF64) break;
+      }
+      c.stats.relax_launches += launch;
+    };
+    // Lazy gossip on a frozen mesh: run eager forwarding first (the pull pass,
+    // or the push path without gossip when IDONTWANT needs it) and keep it if
+    // the batch proves gossip a no-op; otherwise discard its counters and run
+    // the push path with gossip. Under churn some peers never
+    // complete, so the proof cannot hold and gossip runs directly.
+    const bool pull_ok = pull_any && b.delta >= pull_grain(b.tshift);
+    bool done = false;
+    if (pull_ok || (gossip && !churn)) {
+      if (gossip) GS_HIP(hipMemcpyAsync(c.d_cnt_save.p, c.d_counters.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));
+      if (pull_ok) {
+        reset(variant, false);
+        run_pull_batch(c, b, ev, n_ev, dev_cus);
+      } else {
+        push_run(variant & ~32u, false);
+      }
+      if (!gossip) {
+        if (c.traffic) launch_traffic(c, b);
+        launch_complete(c, b, 0, N, sink, i0);
+        done = true;
+      } else {  // keep the eager result only if gossip provably changes nothing
+        run_complete(c, b, 0, N, true, sink && sink->summary);
+        std::vector<uint64_t> ms((size_t)B * MS_COLS);
+        GS_HIP(hipMemcpyAsync(ms.data(), c.d_mstat.p, ms.size() * 8, hipMemcpyDeviceToHost, s));
+        GS_HIP(hipStreamSynchronize(s));
+        if (gossip_noop(b, ms.data(), rel0)) {
+          if (c.traffic) launch_traffic(c, b);
+          deliver(c, b, 0, N, sink, i0);
+          c.stats.gossip_noop_msgs += B;
+          done = true;
+        } else {  // gossip can change this batch: discard the eager run's counters
+          GS_HIP(hipMemcpyAsync(c.d_counters.p, c.d_cnt_save.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));
+          c.stats.gossip_fallback_batches++;
+        }
+      }
     }
-    GS_HIP(hipMemsetAsync(c.d_ctrl.p, 0xFF, 4 * 8, s));
-    // with gossip the first bucket is [0, Delta): the publisher's own IHAVEs
-    // can land before the first eager arrival
-    if (gossip) GS_HIP(hipMemsetAsync(c.d_ctrl.p, 0, 8, s));
-    if (pull && b.delta >= pull_grain(b.tshift)) {
-      run_pull_batch(c, b, ev, n_ev, dev_cus);
-      c.stats.messages += B;
+    if (!done) {
+      if (c.traffic && gossip)
+        c.fail(GS_EUNSUPPORTED, "per-peer traffic covers eager forwarding; lazy gossip sends IWANT "
+                                "answers in this batch");
+      if (gossip && !lanes32)
+        c.fail(GS_EUNSUPPORTED, "lazy gossip changes this batch and the push path needs "
+                                "peers*batch*FP < 2^32: use a smaller batch");
+      push_run(pvariant, gossip);
       if (c.traffic) launch_traffic(c, b);
       launch_complete(c, b, 0, N, sink, i0);
-      i0 = i1;
-      continue;
     }
-    launch_seed(c, b, 0, N);
-
-    RelaxArgs ra{};
-    set_churn_args(c, ra);
-    ra.keys = c.d_keys.p; ra.busy = c.d_busy.p; ra.mesh = c.d_mesh.p; ra.pub = c.d_pub.p;
-    ra.meta = reinterpret_cast<TileMeta*>(c.d_meta.p);
-    ra.fbits = c.d_fbits.p;
-    ra.tmin = c.d_tmin.p;
-    ra.touched = c.d_touched.p;
-    ra.stage = c.d_stage.p; ra.tables = c.d_tables.p; ra.ctrl = c.d_ctrl.p;
-    ra.counters = c.d_counters.p; ra.total = total; ra.delta = b.delta; ra.tmax = b.tmax;
-    ra.N = N; ra.B = B; ra.F = F; ra.L = L; ra.S = c.S; ra.sb = b.sb; ra.tshift = b.tshift;
-    ra.idw = (c.cfg.idontwant && b.payload >= c.cfg.idontwant) ? 1 : 0;
-    const uint64_t need = (total + TB - 1) / TB;
-    const char* bpc_env = getenv("GS_SPLIT_BLOCKS_PER_CU");  // A/B knob for the split path's grid
-    // 4 blocks per CU measured best on config #3 (k_scan 177 -> 136 us, k_frontier
-    // 65 -> 38 us per bucket vs 16; 1-2 and 32-64 slower): fewer, longer scan waves
-    const uint64_t bpc = bpc_env && *bpc_env ? std::max(1, atoi(bpc_env)) : 4;
-    const unsigned grid = (unsigned)std::min<uint64_t>(need, (uint64_t)dev_cus * bpc);
-    if (variant & 8) {  // frontier segments: one per scan wave
-      const uint64_t nwaves = (uint64_t)grid * (TB / 64), ntiles = (total + 63) / 64;
-      ra.seg_cap = (uint32_t)(((ntiles + nwaves - 1) / nwaves) * (64 / FP));
-      c.d_fr_idx.alloc(nwaves * ra.seg_cap);
-      if (FP == 1) c.d_fr_key.alloc(nwaves * ra.seg_cap);
-      c.d_fr_cnt.alloc(nwaves);
-      ra.fr_idx = c.d_fr_idx.p;
-      ra.fr_key = c.d_fr_key.p;
-      ra.fr_cnt = c.d_fr_cnt.p;
-      if (gossip) {  // gossip list: per-lane entries, one segment per scan wave
-        ra.gl_cap = (uint32_t)(((ntiles + nwaves - 1) / nwaves) * 64);
-        c.d_gl_idx.alloc(nwaves * ra.gl_cap);
-        c.d_gl_cnt.alloc(nwaves);
-        c.d_nonfinal.alloc(3);
-        GS_HIP(hipMemsetAsync(c.d_nonfinal.p, 0, 3 * 8, s));
-        ra.gl_idx = c.d_gl_idx.p;
-        ra.gl_cnt = c.d_gl_cnt.p;
-        ra.nonfinal = c.d_nonfinal.p;
-        ra.rel0 = c.d_rel0.p;
-        ra.habs0 = c.d_habs0.p;
-        ra.row = c.d_row.p;
-        ra.col = c.d_col.p;
-        ra.hb_ns = c.cfg.heartbeat_ns;
-        ra.seed = c.cfg.seed;
-        ra.gossip = 1;
-        if (churn) {
-          ra.ring_tgt = c.d_ring_tgt.p;
-          ra.ring_tcnt = c.d_ring_tcnt.p;
-        }
-        ra.hist = c.cfg.history_gossip;
-        ra.d_lazy = c.cfg.d_lazy;
-        ra.gf_milli = c.cfg.gossip_factor_milli;
-      }
-    }
-    uint32_t launch = 0;
-    const uint32_t chunk = 8;
-    for (;;) {
-      for (uint32_t q = 0; q < chunk; q++) {
-        ra.launch = launch++;
-        if (c.timing) {  // (start, scan end, end) per bucket
-          GS_HIP(hipEventRecord(ev(n_ev), s));
-          const hipEvent_t mid = ev(n_ev + 1);
-          if (variant & 8) relax_dispatch(FP, variant, ra, grid, s, mid);
-          else {
-            relax_dispatch(FP, variant, ra, grid, s);
-            GS_HIP(hipEventRecord(mid, s));
-          }
-          GS_HIP(hipEventRecord(ev(n_ev + 2), s));
-          n_ev += 3;
-        } else {
-          relax_dispatch(FP, variant, ra, grid, s);
-        }
-      }
-      GS_HIP(hipGetLastError());
-      GS_HIP(hipMemcpyAsync(c.h_pinned, c.d_ctrl.p, 3 * 8, hipMemcpyDeviceToHost, s));
-      GS_HIP(hipStreamSynchronize(s));
-      if (c.h_pinned[launch % 3] == INF64) break;
-    }
-    c.stats.relax_launches += launch;
-    if (c.traffic) launch_traffic(c, b);
-    launch_complete(c, b, 0, N, sink, i0);
     c.stats.messages += B;
+    c.stats.batches++;
     i0 = i1;
   }
   if (c.timing) GS_HIP(hipEventRecord(ev(1), s));

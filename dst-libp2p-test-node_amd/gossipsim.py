@@ -26,7 +26,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GOSSIPSIM_LIB", os.path.join(HERE, "libgossipsim.so"))
-ABI_VERSION = 3
+ABI_VERSION = 4
 MESH_W = 16
 UNDELIVERED = np.uint64(0xFFFFFFFFFFFFFFFF)
 MUXERS = {"yamux": 0, "quic": 1, "mplex": 2}
@@ -45,15 +45,27 @@ class GsConfig(ctypes.Structure):
         ("heartbeat_ns", u64), ("backoff_ns", u64)] + [
         (n, u32) for n in ("flood_publish", "idontwant", "lazy_gossip", "self_log")] + [
         ("seed", u64), ("device", i32), ("batch", u32), ("history_gossip", u32), ("hb_phase_ns", u64)] + [
-        (n, u32) for n in ("churn_ppm", "churn_down", "churn_horizon", "node")]
+        (n, u32) for n in ("churn_ppm", "churn_down", "churn_horizon", "node", "sub_graft")]
 
 
 class GsPublish(ctypes.Structure):
-    _fields_ = [("t_pub_ns", u64), ("publisher", u32), ("msg_size", u32)]
+    _fields_ = [("t_pub_ns", u64), ("publisher", u32), ("msg_size", u32), ("frags", u32), ("reserved", u32)]
+
+
+HIST_BINS, HIST_MS = 64, 100  # GS_HIST_BINS / GS_HIST_MS
+
+
+class GsMsgSummary(ctypes.Structure):
+    _fields_ = [("delivered", u64), ("lat_sum_ms", u64), ("p50_ms", u32), ("p95_ms", u32), ("max_ms", u32),
+                ("reserved", u32), ("hist", u32 * HIST_BINS)]
+
+
+BLOCK_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, u64, u32, u32, P(u64), P(u8))
 
 
 class GsResultSink(ctypes.Structure):
-    _fields_ = [("t_complete_ns", P(u64)), ("hops", P(u8))]
+    _fields_ = [("t_complete_ns", P(u64)), ("hops", P(u8)), ("on_block", BLOCK_FN), ("user", ctypes.c_void_p),
+                ("block_msgs", u32), ("reserved", u32), ("summary", P(GsMsgSummary))]
 
 
 class GsStats(ctypes.Structure):
@@ -62,7 +74,7 @@ class GsStats(ctypes.Structure):
         "latency_sum_ms", "latency_max_ms", "relax_launches", "buckets")] + [
         ("relax_ms", ctypes.c_double), ("run_ms", ctypes.c_double), ("relax_bytes_alg", u64),
         ("pushes", u64), ("scan_ms", ctypes.c_double), ("frontier_ms", ctypes.c_double),
-        ("gossip_iwant", u64)]
+        ("gossip_iwant", u64), ("gossip_noop_msgs", u64), ("gossip_fallback_batches", u64), ("batches", u64)]
 
 
 class GsPartRecord(ctypes.Structure):
@@ -74,6 +86,9 @@ SIGNATURES = {
     "gs_config_default": (None, [P(GsConfig)]),
     "gs_config_preset": (i32, [P(GsConfig), u32]),
     "gs_write_node_log": (i32, [P(GsConfig), ctypes.c_char_p, P(GsPublish), u64, P(u64)]),
+    "gs_log_open": (i32, [P(GsConfig), ctypes.c_char_p, P(ctypes.c_void_p)]),
+    "gs_log_write": (i32, [ctypes.c_void_p, P(GsPublish), u32, P(u64)]),
+    "gs_log_close": (i32, [ctypes.c_void_p]),
     "gs_config_from_env": (i32, [P(GsConfig), ctypes.c_char_p, ctypes.c_size_t]),
     "gs_wire_bytes": (u64, [u64, u32, u32]),
     "gs_wire_packets": (None, [u64, u32, u32, P(u64), P(u64)]),
@@ -222,8 +237,16 @@ def schedule_runsh(n_msgs, peers, publisher_id, rotation, t0_ns, delay_ns, msg_s
 
 # Schedule constants of the benchmark workload: Shadow epoch 2000-01-01 plus the
 # injector start (shadow/topogen.py:130), 1000 ms spacing and publisher
-# (6 + i) mod N with rotation (shadow/README.md:57, run.sh:34-36).
-T0_NS = 946684800_000_000_000 + 500_000_000_000
+# (6 + i) mod N with rotation (shadow/README.md:57, run.sh:34-36). The injector
+# POSTs over a fresh TCP connection across the 1 ms injector-hub links
+# (topogen.py:64-69): the request reaches the node 1.5 round trips = 3 ms after
+# the injector's send, and the node stamps tx_time then (main.rs:105-111).
+# Heartbeats tick on whole seconds (process start 5 s, topogen.py:106, plus
+# libp2p-gossipsub's 5 s heartbeat_initial_delay; hb_phase_ns = 0 is the same
+# phase), so a publish lands 3 ms after a heartbeat.
+INJECTOR_START_NS = 946684800_000_000_000 + 500_000_000_000
+HTTP_TRANSIT_NS = 3_000_000
+T0_NS = INJECTOR_START_NS + HTTP_TRANSIT_NS
 # Heartbeat 0 when every node starts (Shadow starts processes at 5 s,
 # shadow/topogen.py:106): the phase churn runs need.
 SHADOW_START_NS = 946684800_000_000_000 + 5_000_000_000
@@ -371,31 +394,69 @@ class Simulator:
         self._sched.append((int(t_pub_ns), int(publisher), int(msg_size)))
 
     def _schedule(self, schedule):
+        """(t, publisher, msg_size[, frags]) arrays or a GsPublish array -> GsPublish array."""
         if schedule is None:
             schedule = (GsPublish * len(self._sched))(*[GsPublish(*r) for r in self._sched])
             self._sched = []
         elif not isinstance(schedule, ctypes.Array):
-            t, p, s = schedule
+            t, p, s = schedule[:3]
+            fr = schedule[3] if len(schedule) > 3 else np.zeros(len(t), np.uint32)
             arr = (GsPublish * len(t))()
             for i in range(len(t)):
-                arr[i] = GsPublish(int(t[i]), int(p[i]), int(s[i]))
+                arr[i] = GsPublish(int(t[i]), int(p[i]), int(s[i]), int(fr[i]), 0)
             schedule = arr
         return schedule
 
-    def run(self, schedule=None, collect=True):
-        """Simulate the queued publishes (or `schedule`); returns t_complete/hops [M, N]."""
+    def run(self, schedule=None, collect=True, summary=False, on_block=None, block_msgs=0):
+        """Simulate the queued publishes (or `schedule`); returns t_complete/hops [M, N].
+
+        summary: also return the device's per-message latency reductions
+        (gs_msg_summary: delivered, lat_sum_ms, p50/p95/max ms, 100 ms histogram).
+        on_block(first_msg, t_complete[n, N], hops[n, N]): stream the results in
+        blocks of `block_msgs` messages instead of returning [M, N] arrays."""
         schedule = self._schedule(schedule)
         M = len(schedule)
         res = {"schedule": schedule}
-        if collect:
+        sink = GsResultSink()
+        keep = []
+        if on_block is not None:
+            N = self.peers
+
+            def _cb(user, first, n, peers, tc, hp):
+                a = np.ctypeslib.as_array(tc, (n, peers)) if tc else None
+                h = np.ctypeslib.as_array(hp, (n, peers)) if hp else None
+                on_block(int(first), a, h)
+
+            cb = BLOCK_FN(_cb)
+            keep.append(cb)
+            flag = np.zeros(1, np.uint64)
+            flag8 = np.zeros(1, np.uint8)
+            keep += [flag, flag8]
+            sink.t_complete_ns = _ptr(flag, u64)
+            sink.hops = _ptr(flag8, u8)
+            sink.on_block = cb
+            sink.block_msgs = block_msgs
+        elif collect:
             tc = np.zeros(M * self.peers, np.uint64)
             hops = np.zeros(M * self.peers, np.uint8)
-            sink = GsResultSink(_ptr(tc, u64), _ptr(hops, u8))
-            self._check(lib().gs_run(self.ctx, schedule, M, ctypes.byref(sink)))
+            sink.t_complete_ns = _ptr(tc, u64)
+            sink.hops = _ptr(hops, u8)
             res["t_complete"] = tc.reshape(M, self.peers)
             res["hops"] = hops.reshape(M, self.peers)
-        else:
-            self._check(lib().gs_run(self.ctx, schedule, M, None))
+        if summary:
+            sm = (GsMsgSummary * M)()
+            sink.summary = ctypes.cast(sm, P(GsMsgSummary))
+            keep.append(sm)
+        use_sink = on_block is not None or collect or summary
+        self._check(lib().gs_run(self.ctx, schedule, M, ctypes.byref(sink) if use_sink else None))
+        if summary:
+            res["summary"] = {
+                "delivered": np.array([x.delivered for x in sm], np.uint64),
+                "lat_sum_ms": np.array([x.lat_sum_ms for x in sm], np.uint64),
+                "p50_ms": np.array([x.p50_ms for x in sm], np.uint32),
+                "p95_ms": np.array([x.p95_ms for x in sm], np.uint32),
+                "max_ms": np.array([x.max_ms for x in sm], np.uint32),
+                "hist": np.array([list(x.hist) for x in sm], np.uint32).reshape(M, HIST_BINS)}
         return res
 
     def stats(self):
@@ -422,6 +483,10 @@ class Simulator:
     def write_node_metrics(self, path):
         """Every peer's Prometheus metrics (rust-test-node/src/metrics.rs names) after traffic runs."""
         write_node_metrics(self.cfg, path, self.csr()[0], self.mesh()[1], self.traffic())
+
+    def open_log(self, path):
+        """Streaming arrival log (gs_log_open); feed it with LogStream.write(schedule_rows, t_complete)."""
+        return LogStream(self.cfg, path)
 
     def write_latency_log(self, path, res):
         """Arrival lines as `grep -rne 'milliseconds\\|BW' shadow.data/` prints them."""
@@ -474,3 +539,30 @@ class Simulator:
         else:
             self._check(lib().gs_part_finish(self.ctx, None))
         return res
+
+
+class LogStream:
+    """gs_log_*: the arrival log written block by block (message-major blocks
+    from Simulator.run(on_block=...)), identical lines to write_latency_log."""
+
+    def __init__(self, cfg, path):
+        self.h = ctypes.c_void_p()
+        rc = lib().gs_log_open(ctypes.byref(cfg.c), path.encode(), ctypes.byref(self.h))
+        if rc:
+            raise GossipSimError(rc, "gs_log_open %s" % path)
+
+    def write(self, sched_rows, t_complete):
+        """sched_rows: GsPublish array (or slice) of the block; t_complete [n, N] uint64."""
+        tc = np.ascontiguousarray(t_complete, np.uint64)
+        n = tc.shape[0]
+        rows = (GsPublish * n)(*sched_rows[:n]) if not isinstance(sched_rows, ctypes.Array) else sched_rows
+        rc = lib().gs_log_write(self.h, rows, n, _ptr(tc, u64))
+        if rc:
+            raise GossipSimError(rc, "gs_log_write failed")
+
+    def close(self):
+        if self.h:
+            rc = lib().gs_log_close(self.h)
+            self.h = ctypes.c_void_p()
+            if rc:
+                raise GossipSimError(rc, "gs_log_close failed")

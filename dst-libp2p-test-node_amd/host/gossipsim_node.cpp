@@ -24,7 +24,7 @@ void usage() {
   fprintf(stderr,
           "usage: gossipsim-node [-bl MBIT] [-bh MBIT] [-ll MS] [-lh MS] [-st STAGES] [--shortest]\n"
           "         [-s MSG_BYTES] [-m MESSAGES] [--publisher ID] [--rotation 0|1]\n"
-          "         [--delay-ms MS] [--t0-s SECONDS] [--max-heartbeats H] [--latencies PATH]\n"
+          "         [--delay-ms MS] [--t0-s SECONDS] [--http-us US] [--max-heartbeats H] [--latencies PATH]\n"
           "         [--gml network_topology.gml --yaml shadow.yaml] [--shadowlog PATH] [--metrics PATH]\n"
           "env: PEERS CONNECTTO FRAGMENTS MUXER MAXCONNECTIONS GOSSIPSUB_* SELFTRIGGER GS_NODE GS_SEED GS_BATCH\n"
           "     GS_DEVICE\n");
@@ -42,7 +42,10 @@ int main(int argc, char** argv) {
   // topogen.py defaults (topogen.py:15-26) and run.sh's fixed publisher knobs
   uint32_t bl = 50, bh = 50, ll = 100, lh = 100, stages = 1, mode = GS_LINKS_DIRECT;
   uint32_t msg_size = 1500, n_msgs = 10, publisher = 6, rotation = 1, max_hb = 400;
-  uint64_t delay_ms = 1000, t0_s = 946684800ull + 500ull;  // Shadow epoch + injector start
+  uint64_t delay_ms = 1000, t0_s = 946684800ull + 500ull;  // Shadow epoch + injector start (topogen.py:130)
+  // the POST reaches the node 1.5 round trips over the 1 ms injector-hub links
+  // after the injector sends it (topogen.py:64-69); tx_time is stamped then
+  uint64_t http_us = 3000;
   std::string latencies, gml, yaml, shadowlog, metrics;
   for (int i = 1; i < argc; i++) {
     std::string a = argv[i];
@@ -62,6 +65,7 @@ int main(int argc, char** argv) {
     else if (a == "--rotation") rotation = (uint32_t)atoi(next());
     else if (a == "--delay-ms") delay_ms = strtoull(next(), nullptr, 10);
     else if (a == "--t0-s") t0_s = strtoull(next(), nullptr, 10);
+    else if (a == "--http-us") http_us = strtoull(next(), nullptr, 10);
     else if (a == "--max-heartbeats") max_hb = (uint32_t)atoi(next());
     else if (a == "--latencies") latencies = next();
     else if (a == "--gml") gml = next();            // a Shadow experiment's network graph ...
@@ -113,7 +117,7 @@ int main(int argc, char** argv) {
   if ((st = gs_mesh_converge(ctx, max_hb, &epochs)) != GS_OK) return die(ctx, st, "gs_mesh_converge");
 
   std::vector<gs_publish> sched(n_msgs);
-  gs_schedule_runsh(n_msgs, cfg.peers, publisher, rotation, t0_s * 1000000000ull,
+  gs_schedule_runsh(n_msgs, cfg.peers, publisher, rotation, t0_s * 1000000000ull + http_us * 1000ull,
                     delay_ms * 1000000ull, msg_size, sched.data());
   std::vector<uint64_t> tc((size_t)n_msgs * cfg.peers);
   gs_result_sink sink{tc.data(), nullptr};

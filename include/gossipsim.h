@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 3u
+#define GS_ABI_VERSION 4u
 
 /* Sentinel for "never delivered" in t_complete_ns. */
 #define GS_UNDELIVERED UINT64_MAX
@@ -100,20 +100,62 @@ typedef struct gs_config {
     uint32_t churn_horizon;      /* message lifetime in heartbeats under churn: no  */
                                  /* event past epoch(t_pub) + horizon (default 16)  */
     uint32_t node;               /* GS_NODE_*: fragment layout + log line */
+    /* subscription-time grafting (libp2p-gossipsub handle_received_subscriptions,
+     * reached through the 20 s connection pump of main.rs:357-379): before
+     * heartbeat 1 every peer grafts its first D_lo connections in handshake
+     * order. 1 in the rust preset. */
+    uint32_t sub_graft;
 } gs_config;
 
-/* One publish injection (replaces POST /publish, main.rs:50-56,152-168). */
+/* One publish injection (replaces POST /publish, main.rs:50-56,152-168; the
+ * PublishCommand of main.rs:65-71 carries msg_size and chunks). */
 typedef struct gs_publish {
     uint64_t t_pub_ns;    /* absolute publish time = tx_time stamped at main.rs:105-111 */
     uint32_t publisher;   /* peer id that publishes                                     */
     uint32_t msg_size;    /* msgSize of the request; fragment payload = msg_size/F      */
+    uint32_t frags;       /* F of this message (chunks, main.rs:163-168); 0 = cfg.fragments */
+    uint32_t reserved;    /* 0                                                          */
 } gs_publish;
 
-/* Caller-allocated result arrays, message-major: element [m*peers + u].
- * Either pointer may be NULL (that output is then not copied back). */
+/* Latency histogram bins of gs_msg_summary: 100 ms each (hop_lat of
+ * shadow/summary_latency.awk:8), the last one open-ended. */
+#define GS_HIST_BINS 64u
+#define GS_HIST_MS 100u
+
+/* Per-message reduction of one run, computed on the device:
+ * latency = (t_complete - tx_time) / 1e6 truncated, as logged (main.rs:91-93),
+ * over the peers that log the message (the publisher only with self_log). */
+typedef struct gs_msg_summary {
+    uint64_t delivered;            /* log lines of this message                          */
+    uint64_t lat_sum_ms;
+    uint32_t p50_ms, p95_ms;       /* nearest-rank percentiles: value at rank ceil(q*n)  */
+    uint32_t max_ms;
+    uint32_t reserved;
+    uint32_t hist[GS_HIST_BINS];   /* hist[min(ms / 100, 63)]                            */
+} gs_msg_summary;
+
+/* Streaming receiver of results: called from gs_run on the caller's thread
+ * with message-major blocks of at most `block_msgs` messages; the arrays are
+ * library-owned and valid only during the call ([n_msgs][peers], either may
+ * be NULL when the matching sink pointer request is off). */
+typedef void (*gs_block_fn)(void* user, uint64_t first_msg, uint32_t n_msgs, uint32_t peers,
+                            const uint64_t* t_complete_ns, const uint8_t* hops);
+
+/* Where gs_run puts results. Every member may be NULL / 0.
+ *  - t_complete_ns / hops: caller arrays, message-major [n_msgs][peers]
+ *    (without on_block), or flags that on_block wants that output (any
+ *    non-NULL value; nothing is written through it);
+ *  - on_block: streaming delivery instead of the arrays (no [n_msgs][peers]
+ *    host array is needed for large N);
+ *  - summary: [n_msgs] per-message latency reductions. */
 typedef struct gs_result_sink {
     uint64_t* t_complete_ns;  /* completion time of message m at peer u (GS_UNDELIVERED if never) */
     uint8_t*  hops;           /* hop count of the completing fragment (0 at the publisher)        */
+    gs_block_fn on_block;
+    void*     user;
+    uint32_t  block_msgs;     /* messages per on_block call; 0 = 64                               */
+    uint32_t  reserved;
+    gs_msg_summary* summary;
 } gs_result_sink;
 
 /* Counters accumulated since gs_create / gs_reset_stats. */
@@ -135,6 +177,12 @@ typedef struct gs_stats {
     double   scan_ms;           /* relax_ms split: bucket scan + compaction kernel     */
     double   frontier_ms;       /* relax_ms split: frontier forwarding kernel          */
     uint64_t gossip_iwant;      /* IWANT responses sent (counted in relaxations too)   */
+    uint64_t gossip_noop_msgs;  /* lazy gossip on the pull path: messages proven to      */
+                                /* finish everywhere before their first IHAVE can land    */
+                                /* (no IWANT possible)                   */
+    uint64_t gossip_fallback_batches; /* batches re-run on the push path with gossip    */
+    uint64_t batches;           /* device batches run (gs_run splits at cfg.batch, size /  */
+                                /* chunk changes and the churn snapshot ring)             */
 } gs_stats;
 
 /* ---- host-only helpers (no device work) ---------------------------------- */
@@ -210,6 +258,18 @@ gs_status gs_write_latency_log(const char* path, const gs_publish* sched, uint64
  * (seed, publisher, t_pub) in place of the node's rand(high(int64)). */
 gs_status gs_write_node_log(const gs_config* cfg, const char* path, const gs_publish* sched,
                             uint64_t n_msgs, const uint64_t* t_complete_ns);
+
+/* Streaming arrival log (the same lines as gs_write_node_log) for runs too
+ * large for a [n_msgs][peers] host array: feed it the message-major blocks of
+ * gs_result_sink.on_block. Lines come out block by block (message-major within
+ * a block) instead of grouped by peer; the per-peer line numbers count across
+ * blocks exactly as the grouped writer counts them, so every line is
+ * identical and the awk summaries are unchanged. */
+typedef struct gs_log gs_log;
+gs_status gs_log_open(const gs_config* cfg, const char* path, gs_log** out);
+/* sched = the block's n_msgs schedule rows, t_complete_ns = [n_msgs][peers]. */
+gs_status gs_log_write(gs_log* log, const gs_publish* sched, uint32_t n_msgs, const uint64_t* t_complete_ns);
+gs_status gs_log_close(gs_log* log);
 
 /* Packets and header bytes of one fragment send in the same model as
  * gs_wire_bytes: TCP/IPv4 segments of <= 1460 B carrying 40 B of headers each,
@@ -298,8 +358,9 @@ gs_status gs_set_timing(struct gs_ctx* ctx, uint32_t enable);
  * send of a fragment adds its wire bytes / packets / header bytes to the
  * sender's tx and the receiver's rx columns. Counted after each batch from the
  * final keys (one extra pass over them), so it is off by default. Covers
- * eager forwarding incl. IDONTWANT; gs_run returns GS_EUNSUPPORTED with lazy
- * gossip or churn while it is on. Enabling zeroes the counters, as does
+ * eager forwarding incl. IDONTWANT, and lazy gossip when it is a no-op (no
+ * IWANT, gs_stats.gossip_noop_msgs); gs_run returns GS_EUNSUPPORTED for a
+ * batch whose gossip sends IWANT answers, and with churn. Enabling zeroes the counters, as does
  * gs_reset_stats. */
 gs_status gs_set_traffic(struct gs_ctx* ctx, uint32_t enable);
 /* Copy the per-peer counters out: traffic[peers][GS_TRAFFIC_COLS]. */

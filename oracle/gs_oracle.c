@@ -14,6 +14,9 @@
 #include "gs_oracle.h"
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #define INF64 UINT64_MAX
 #define HOP_BITS 6u
@@ -303,14 +306,30 @@ static int mesh_ws_init(const or_params* p, const uint64_t* row_ptr, const uint3
     return 0;
 }
 
+/* Handshake model of the subscription exchange: every peer
+ * dials at the same instant (rust-test-node/src/main.rs:336-354 after the
+ * common 60 s sleep, main.rs:457); a connection completes HS_RTTS round trips
+ * later (TCP + multistream + Noise XX + yamux, a model constant) and each side
+ * then sends its subscription, so w's subscription reaches u at
+ * HS_RTTS*rtt(u,w) + lat(w->u), and u's GRAFT reaches w one lat(u->w) later. */
+#define HS_RTTS 3u
+static uint64_t rtt_of(const uint64_t* lat_ns, uint32_t S, uint32_t su, uint32_t sw) {
+    return lat_ns[su * S + sw] + lat_ns[sw * S + su];
+}
+
 /* One synchronous heartbeat epoch: A) every peer decides
  * grafts/prunes from the start-of-epoch state; B) every receiver handles
  * incoming GRAFTs in (latency, id) order; C) PRUNEs and rejections are
  * applied, both ends back off. off = offline flags of the epoch (NULL: no
- * churn; §2.8). Returns the number of GRAFT/PRUNE changes. */
+ * churn; §2.8). sub = the subscription epoch 0 (libp2p-gossipsub
+ * handle_received_subscriptions, upstream, not vendored; reached through the
+ * 20 s event pump of rust-test-node/src/main.rs:357-379): A grafts the first
+ * min(D_lo, deg) connections in subscription-arrival order
+ * (HS_RTTS*rtt + lat(w->u), id) and B takes GRAFTs in arrival order
+ * ((HS_RTTS+1)*rtt, id). Returns the number of GRAFT/PRUNE changes. */
 static uint64_t mesh_epoch(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
                            uint8_t* flags, const uint8_t* stage, uint32_t S, const uint64_t* lat_ns,
-                           mesh_ws* ws, uint32_t epoch, const uint8_t* off) {
+                           mesh_ws* ws, uint32_t epoch, const uint8_t* off, int sub) {
     uint32_t N = p->peers;
     uint64_t nnz = row_ptr[N], changes = 0;
     uint32_t* until = ws->until; uint8_t* prop = ws->prop; const uint64_t* rev = ws->rev; sel_t* sel = ws->sel;
@@ -321,8 +340,22 @@ static uint64_t mesh_epoch(const or_params* p, const uint64_t* row_ptr, const ui
         for (uint32_t u = 0; u < N; u++)
             for (uint64_t e = row_ptr[u]; e < row_ptr[u + 1]; e++)
                 if (off[u] || off[col[e]]) flags[e] &= (uint8_t)~BIT_MESH;
+    /* ---- A0: subscription-time grafts (epoch 0 only) ---- */
+    for (uint32_t u = 0; sub && u < N; u++) {
+        uint64_t b = row_ptr[u], en = row_ptr[u + 1];
+        uint32_t nc = 0;
+        for (uint64_t e = b; e < en; e++)
+            if (!(flags[e] & BIT_MESH)) {
+                const uint32_t su = stage[u], sw = stage[col[e]];
+                sel[nc].key = HS_RTTS * rtt_of(lat_ns, S, su, sw) + lat_ns[sw * S + su];
+                sel[nc].e = e; nc++;
+            }
+        qsort(sel, nc, sizeof(sel_t), cmp_sel);
+        uint32_t want = p->d_lo < nc ? p->d_lo : nc;
+        for (uint32_t q = 0; q < want; q++) prop[sel[q].e] |= 1;
+    }
     /* ---- A: heartbeat decisions ---- */
-    for (uint32_t u = 0; u < N; u++) {
+    for (uint32_t u = 0; !sub && u < N; u++) {
         if (off && off[u]) continue;
         uint64_t b = row_ptr[u], en = row_ptr[u + 1];
         uint32_t m = 0, o = 0;
@@ -372,9 +405,11 @@ static uint64_t mesh_epoch(const or_params* p, const uint64_t* row_ptr, const ui
             if (((flags[e] & BIT_MESH) && !(prop[e] & 2)) || (prop[e] & 1)) c++;
         for (uint64_t e = b; e < en; e++)
             if (prop[rev[e]] & 1) {
-                sel[nin].key = lat_ns[(uint32_t)stage[col[e]] * S + stage[w]]; sel[nin].e = e; nin++;
+                const uint32_t su = stage[col[e]], sw = stage[w];
+                sel[nin].key = sub ? (HS_RTTS + 1) * rtt_of(lat_ns, S, su, sw) : lat_ns[su * S + sw];
+                sel[nin].e = e; nin++;
             }
-        /* order by (latency u->w, u): stable wrt ascending ids */
+        /* order by (arrival, u): stable wrt ascending ids */
         for (uint32_t i = 1; i < nin; i++) {
             sel_t x = sel[i]; int32_t j = (int32_t)i - 1;
             while (j >= 0 && sel[j].key > x.key) { sel[j + 1] = sel[j]; j--; }
@@ -430,14 +465,15 @@ int or_mesh_converge(const or_params* p, const uint64_t* row_ptr, const uint32_t
     uint8_t* off = p->churn_ppm ? (uint8_t*)malloc(N ? N : 1) : NULL;
     if (p->churn_ppm && !off) { mesh_ws_free(&ws); return -2; }
     uint32_t epoch = 1, last = 0;
+    if (p->sub_graft) mesh_epoch(p, row_ptr, col, flags, stage, S, lat_ns, &ws, 0, NULL, 1);
     while (epoch <= max_hb) {
         if (off) { /* churn: no fixed point, every epoch runs */
             for (uint32_t u = 0; u < N; u++) off[u] = (uint8_t)or_offline(p, u, epoch);
-            mesh_epoch(p, row_ptr, col, flags, stage, S, lat_ns, &ws, epoch, off);
+            mesh_epoch(p, row_ptr, col, flags, stage, S, lat_ns, &ws, epoch, off, 0);
             last = epoch++;
             continue;
         }
-        uint64_t changes = mesh_epoch(p, row_ptr, col, flags, stage, S, lat_ns, &ws, epoch, NULL);
+        uint64_t changes = mesh_epoch(p, row_ptr, col, flags, stage, S, lat_ns, &ws, epoch, NULL, 0);
         last = epoch;
         if (changes) { epoch++; continue; }
         /* quiescent: next epoch at which a back-off expiry can wake a peer */
@@ -466,7 +502,8 @@ int or_mesh_converge(const or_params* p, const uint64_t* row_ptr, const uint32_t
 }
 
 /* Mesh snapshots under churn: heartbeats 1..h_hi from the empty mesh; slot
- * h - h_lo holds the mesh after heartbeat h (h = 0: the empty initial mesh)
+ * h - h_lo holds the mesh after heartbeat h (h = 0: the initial mesh, after
+ * the subscription epoch when sub_graft is on)
  * and the offline flags of epoch h, for h in [h_lo, h_hi]. */
 int or_mesh_churn(const or_params* p, const uint64_t* row_ptr, const uint32_t* col, const uint8_t* flags_in,
                   const uint8_t* stage, uint32_t S, const uint64_t* lat_ns, uint32_t h_lo, uint32_t h_hi,
@@ -484,7 +521,9 @@ int or_mesh_churn(const or_params* p, const uint64_t* row_ptr, const uint32_t* c
     for (uint32_t h = 0; h <= h_hi && !rc; h++) {
         if (h > 0) {
             for (uint32_t u = 0; u < N; u++) off[u] = (uint8_t)or_offline(p, u, h);
-            mesh_epoch(p, row_ptr, col, flags, stage, S, lat_ns, &ws, h, off);
+            mesh_epoch(p, row_ptr, col, flags, stage, S, lat_ns, &ws, h, off, 0);
+        } else if (p->sub_graft) {  /* epoch 0: the subscription exchange, everyone online */
+            mesh_epoch(p, row_ptr, col, flags, stage, S, lat_ns, &ws, 0, NULL, 1);
         }
         if (h >= h_lo) {
             size_t o = (size_t)(h - h_lo);
@@ -653,16 +692,17 @@ static int sched_gossip(const or_params* p, const uint64_t* row_ptr, const uint3
  *  nim publishNewMessage (nim-test-node/gossipsub-queues/main.nim:158-175):
  *    16-byte header (stamp, random msgId) + msg_size div F - 16 bytes,
  *    nowBytes[16] = chunk (IndexDefect when msg_size div F <= 16). */
-static uint64_t frag_payload(const or_params* p, uint64_t msg_size) {
-    return msg_size / p->fragments + (p->node == 1 ? 8 : 0);
+static uint64_t frag_payload(const or_params* p, uint64_t msg_size, uint32_t F) {
+    return msg_size / F + (p->node == 1 ? 8 : 0);
 }
-static int frag_invalid(const or_params* p, uint64_t msg_size) {
-    uint64_t q = msg_size / p->fragments;
+static int frag_invalid(const or_params* p, uint64_t msg_size, uint32_t F) {
+    uint64_t q = msg_size / F;
     return p->node == 1 ? q <= 2 : p->node == 2 ? q <= 16 : q < 8;
 }
-static int frag_collide(const or_params* p, uint64_t msg_size) {
-    return p->node == 0 && p->fragments > 1 && msg_size / p->fragments <= 10;
+static int frag_collide(const or_params* p, uint64_t msg_size, uint32_t F) {
+    return p->node == 0 && F > 1 && msg_size / F <= 10;
 }
+#define MAX_F 16u
 
 /* One publish -> receive -> forward -> reassemble pass per message:
  *  publish_new_message (main.rs:101-143): F fragments (layout above),
@@ -681,14 +721,14 @@ static int frag_collide(const or_params* p, uint64_t msg_size) {
 static int run_impl(const or_params* p, const uint64_t* row_ptr, const uint32_t* col, const mesh_src* ms0,
                     const uint8_t* stage, uint32_t S, const uint64_t* lat_ns, const uint64_t* bw_up,
                     const uint64_t* bw_dn, const uint64_t* sched_t, const uint32_t* sched_pub,
-                    const uint32_t* sched_size, uint64_t n_msgs, uint64_t* t_complete, uint8_t* hops,
-                    or_stats* st, uint64_t* tr) {
-    uint32_t N = p->peers, F = p->fragments;
-    if (F == 0 || F > 16) return -6;
+                    const uint32_t* sched_size, const uint32_t* sched_frags, uint64_t n_msgs,
+                    uint64_t* t_complete, uint8_t* hops, or_stats* st, uint64_t* tr) {
+    uint32_t N = p->peers, F = p->fragments;  /* per message: its chunk count (rows of F slots) */
+    if (p->fragments == 0 || p->fragments > MAX_F) return -6;
     uint32_t sb = bits_for(N), tshift = sb + HOP_BITS;
     uint64_t tmax = (tshift >= 64) ? 0 : (UINT64_MAX >> tshift);
     uint64_t hmask = (1ull << HOP_BITS) - 1, smask = (1ull << sb) - 1;
-    size_t NF = (size_t)N * F;
+    size_t NF = (size_t)N * MAX_F;
     uint32_t maxdeg = 0;
     for (uint32_t u = 0; u < N; u++)
         if (row_ptr[u + 1] - row_ptr[u] > maxdeg) maxdeg = (uint32_t)(row_ptr[u + 1] - row_ptr[u]);
@@ -704,10 +744,15 @@ static int run_impl(const or_params* p, const uint64_t* row_ptr, const uint32_t*
     if (!best || !fin || !busy || !su || !sd || !gsel || !gtg || !ftg) { rc = -2; goto out; }
     for (uint64_t mi = 0; mi < n_msgs; mi++) {
         uint32_t pub = sched_pub[mi];
-        uint64_t payload = frag_payload(p, sched_size[mi]);
-        if (pub >= N || frag_invalid(p, sched_size[mi])) { rc = -1; goto out; } /* the node's publish fails */
-        int collide = frag_collide(p, sched_size[mi]);                      /* defect D8 */
-        uint32_t Fe = collide ? 1 : F;
+        /* chunks of this PublishCommand (main.rs:65-71,163-168); 0 = FRAGMENTS */
+        const uint32_t Fm = (sched_frags && sched_frags[mi]) ? sched_frags[mi] : p->fragments;
+        if (Fm > MAX_F) { rc = -1; goto out; }
+        uint64_t payload = frag_payload(p, sched_size[mi], Fm);
+        if (pub >= N || frag_invalid(p, sched_size[mi], Fm)) { rc = -1; goto out; } /* the node's publish fails */
+        int collide = frag_collide(p, sched_size[mi], Fm);                      /* defect D8 */
+        uint32_t Fe = collide ? 1 : Fm;
+        F = Fm;
+        NF = (size_t)N * F;
         uint64_t wire = or_wire_bytes(payload, p->muxer, p->signed_msgs), wpk = 0, whd = 0;
         or_wire_packets(payload, p->muxer, p->signed_msgs, &wpk, &whd);
         /* per-peer traffic: a send adds to the sender's tx, an arrival to the receiver's rx */
@@ -837,7 +882,7 @@ static int run_impl(const or_params* p, const uint64_t* row_ptr, const uint32_t*
             size_t o = (size_t)mi * N + u;
             if (u == pub) { t_complete[o] = tp; hops[o] = 0; continue; }
             uint64_t mk = 0; int ok = !collide;
-            for (uint32_t f = 0; f < F && ok; f++) {
+            for (uint32_t f = 0; f < Fm && ok; f++) {
                 uint64_t k = best[(size_t)u * F + f];
                 if (k == INF64) ok = 0; else if (k > mk) mk = k;
             }
@@ -862,10 +907,10 @@ int or_run(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
            const uint32_t* mesh, const uint8_t* cnt, const uint8_t* stage, uint32_t S,
            const uint64_t* lat_ns, const uint64_t* bw_up, const uint64_t* bw_dn,
            const uint64_t* sched_t, const uint32_t* sched_pub, const uint32_t* sched_size,
-           uint64_t n_msgs, uint64_t* t_complete, uint8_t* hops, or_stats* st) {
+           const uint32_t* sched_frags, uint64_t n_msgs, uint64_t* t_complete, uint8_t* hops, or_stats* st) {
     mesh_src ms = {mesh, cnt, NULL, NULL, NULL, 0, 0, 0};
     return run_impl(p, row_ptr, col, &ms, stage, S, lat_ns, bw_up, bw_dn, sched_t, sched_pub, sched_size,
-                    n_msgs, t_complete, hops, st, NULL);
+                    sched_frags, n_msgs, t_complete, hops, st, NULL);
 }
 
 int or_run_churn(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
@@ -873,10 +918,11 @@ int or_run_churn(const or_params* p, const uint64_t* row_ptr, const uint32_t* co
                  uint32_t h_lo, uint32_t n_snap, const uint8_t* stage, uint32_t S,
                  const uint64_t* lat_ns, const uint64_t* bw_up, const uint64_t* bw_dn,
                  const uint64_t* sched_t, const uint32_t* sched_pub, const uint32_t* sched_size,
-                 uint64_t n_msgs, uint64_t* t_complete, uint8_t* hops, or_stats* st) {
+                 const uint32_t* sched_frags, uint64_t n_msgs, uint64_t* t_complete, uint8_t* hops,
+                 or_stats* st) {
     mesh_src ms = {NULL, NULL, snap_mesh, snap_cnt, snap_off, h_lo, n_snap, 0};
     return run_impl(p, row_ptr, col, &ms, stage, S, lat_ns, bw_up, bw_dn, sched_t, sched_pub, sched_size,
-                    n_msgs, t_complete, hops, st, NULL);
+                    sched_frags, n_msgs, t_complete, hops, st, NULL);
 }
 
 /* or_run plus per-peer traffic tr[N][8] (tx bytes, rx bytes, tx packets, rx
@@ -886,8 +932,45 @@ int or_run_traffic(const or_params* p, const uint64_t* row_ptr, const uint32_t* 
                    const uint32_t* mesh, const uint8_t* cnt, const uint8_t* stage, uint32_t S,
                    const uint64_t* lat_ns, const uint64_t* bw_up, const uint64_t* bw_dn,
                    const uint64_t* sched_t, const uint32_t* sched_pub, const uint32_t* sched_size,
-                   uint64_t n_msgs, uint64_t* t_complete, uint8_t* hops, or_stats* st, uint64_t* tr) {
+                   const uint32_t* sched_frags, uint64_t n_msgs, uint64_t* t_complete, uint8_t* hops,
+                   or_stats* st, uint64_t* tr) {
     mesh_src ms = {mesh, cnt, NULL, NULL, NULL, 0, 0, 0};
     return run_impl(p, row_ptr, col, &ms, stage, S, lat_ns, bw_up, bw_dn, sched_t, sched_pub, sched_size,
-                    n_msgs, t_complete, hops, st, tr);
+                    sched_frags, n_msgs, t_complete, hops, st, tr);
+}
+
+/* or_run message-parallel on `threads` host threads (OpenMP): messages are
+ * independent given the frozen mesh, so each thread runs the
+ * same single-message event simulation on its own messages. Used only as the
+ * all-core CPU baseline of bench.py. */
+int or_run_mt(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
+              const uint32_t* mesh, const uint8_t* cnt, const uint8_t* stage, uint32_t S,
+              const uint64_t* lat_ns, const uint64_t* bw_up, const uint64_t* bw_dn,
+              const uint64_t* sched_t, const uint32_t* sched_pub, const uint32_t* sched_size,
+              const uint32_t* sched_frags, uint64_t n_msgs, uint64_t* t_complete, uint8_t* hops, or_stats* st,
+              int threads) {
+    or_stats* ps = (or_stats*)calloc(n_msgs ? n_msgs : 1, sizeof(or_stats));
+    if (!ps) return -2;
+    const mesh_src ms = {mesh, cnt, NULL, NULL, NULL, 0, 0, 0};
+    const size_t N = p->peers;
+    int rc = 0;
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 1)
+    for (int64_t m = 0; m < (int64_t)n_msgs; m++) {
+        int r = run_impl(p, row_ptr, col, &ms, stage, S, lat_ns, bw_up, bw_dn, sched_t + m, sched_pub + m,
+                         sched_size + m, sched_frags ? sched_frags + m : NULL, 1, t_complete + (size_t)m * N,
+                         hops + (size_t)m * N, &ps[m], NULL);
+        if (r) {
+#pragma omp critical
+            rc = r;
+        }
+    }
+    for (uint64_t m = 0; m < n_msgs; m++) {
+        st->messages += ps[m].messages; st->deliveries += ps[m].deliveries;
+        st->frag_deliveries += ps[m].frag_deliveries; st->relaxations += ps[m].relaxations;
+        st->latency_sum_ms += ps[m].latency_sum_ms; st->gossip_iwant += ps[m].gossip_iwant;
+        if (ps[m].latency_max_ms > st->latency_max_ms) st->latency_max_ms = ps[m].latency_max_ms;
+    }
+    st->bytes_alg = 16 * st->frag_deliveries + 12 * st->relaxations + 8 * st->deliveries;
+    free(ps);
+    return rc;
 }

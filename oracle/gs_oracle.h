@@ -31,6 +31,7 @@ typedef struct or_params {
     uint64_t hb_phase_ns;
     uint32_t churn_ppm, churn_down, churn_horizon; /* DESIGN.md §2.8; 0 ppm = no churn */
     uint32_t node; /* payload layout of the node flavour: 0 rust, 1 go, 2 nim */
+    uint32_t sub_graft; /* subscription-time grafting before heartbeat 1 */
 } or_params;
 
 typedef struct or_stats {
@@ -47,7 +48,7 @@ int or_run_traffic(const or_params* p, const uint64_t* row_ptr, const uint32_t* 
                    const uint32_t* mesh, const uint8_t* cnt, const uint8_t* stage, uint32_t S,
                    const uint64_t* lat_ns, const uint64_t* bw_up, const uint64_t* bw_dn,
                    const uint64_t* sched_t, const uint32_t* sched_pub, const uint32_t* sched_size,
-                   uint64_t n_msgs, uint64_t* t_complete, uint8_t* hops, struct or_stats* st, uint64_t* tr);
+                   const uint32_t* sched_frags, uint64_t n_msgs, uint64_t* t_complete, uint8_t* hops, struct or_stats* st, uint64_t* tr);
 int or_topogen_links(uint32_t S, uint32_t bl, uint32_t bh, uint32_t ll, uint32_t lh,
                      uint32_t mode, uint64_t* lat_ns, uint64_t* bw_bps);
 uint32_t or_dials_per_peer(const or_params* p);
@@ -72,12 +73,21 @@ int or_run_churn(const or_params* p, const uint64_t* row_ptr, const uint32_t* co
                  uint32_t h_lo, uint32_t n_snap, const uint8_t* stage, uint32_t S,
                  const uint64_t* lat_ns, const uint64_t* bw_up, const uint64_t* bw_dn,
                  const uint64_t* sched_t, const uint32_t* sched_pub, const uint32_t* sched_size,
-                 uint64_t n_msgs, uint64_t* t_complete, uint8_t* hops, or_stats* st);
+                 const uint32_t* sched_frags, uint64_t n_msgs, uint64_t* t_complete, uint8_t* hops, or_stats* st);
+/* sched_frags: chunks per message (main.rs:65-71), NULL or 0 entries = p->fragments. */
 int or_run(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
            const uint32_t* mesh, const uint8_t* cnt, const uint8_t* stage, uint32_t S,
            const uint64_t* lat_ns, const uint64_t* bw_up, const uint64_t* bw_dn,
            const uint64_t* sched_t, const uint32_t* sched_pub, const uint32_t* sched_size,
-           uint64_t n_msgs, uint64_t* t_complete, uint8_t* hops, or_stats* st);
+           const uint32_t* sched_frags, uint64_t n_msgs, uint64_t* t_complete, uint8_t* hops, or_stats* st);
+
+/* or_run on `threads` host threads, messages in parallel (bench.py's all-core baseline). */
+int or_run_mt(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
+              const uint32_t* mesh, const uint8_t* cnt, const uint8_t* stage, uint32_t S,
+              const uint64_t* lat_ns, const uint64_t* bw_up, const uint64_t* bw_dn,
+              const uint64_t* sched_t, const uint32_t* sched_pub, const uint32_t* sched_size,
+              const uint32_t* sched_frags, uint64_t n_msgs, uint64_t* t_complete, uint8_t* hops, or_stats* st,
+              int threads);
 
 #ifdef __cplusplus
 }

@@ -30,7 +30,7 @@ class OrParams(ctypes.Structure):
         ("heartbeat_ns", ctypes.c_uint64), ("backoff_ns", ctypes.c_uint64)] + [
         (n, ctypes.c_uint32) for n in ("flood_publish", "idontwant", "lazy_gossip", "self_log")] + [
         ("seed", ctypes.c_uint64), ("history_gossip", ctypes.c_uint32), ("hb_phase_ns", ctypes.c_uint64)] + [
-        (n, ctypes.c_uint32) for n in ("churn_ppm", "churn_down", "churn_horizon", "node")]
+        (n, ctypes.c_uint32) for n in ("churn_ppm", "churn_down", "churn_horizon", "node", "sub_graft")]
 
 
 class OrStats(ctypes.Structure):
@@ -43,7 +43,7 @@ def build(force=False):
     """Compile the oracle with gcc into oracle/_build (git-ignored)."""
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
     if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(SRC):
-        subprocess.check_call(["gcc", "-O2", "-shared", "-fPIC", "-o", LIB, SRC])
+        subprocess.check_call(["gcc", "-O2", "-fopenmp", "-shared", "-fPIC", "-o", LIB, SRC])
     return LIB
 
 
@@ -63,7 +63,7 @@ def lib():
         L.or_wire_bytes.argtypes = [u64, u32, u32]
         L.or_wire_packets.argtypes = [u64, u32, u32, P(u64), P(u64)]
         L.or_run_traffic.argtypes = [P(OrParams), P(u64), P(u32), P(u32), P(u8), P(u8), u32, P(u64),
-                                     P(u64), P(u64), P(u64), P(u32), P(u32), u64, P(u64), P(u8),
+                                     P(u64), P(u64), P(u64), P(u32), P(u32), P(u32), u64, P(u64), P(u8),
                                      P(OrStats), P(u64)]
         L.or_topogen_links.argtypes = [u32, u32, u32, u32, u32, u32, P(u64), P(u64)]
         L.or_dials_per_peer.restype = u32
@@ -72,13 +72,14 @@ def lib():
         L.or_mesh_converge.argtypes = [P(OrParams), P(u64), P(u32), P(u8), P(u8), u32, P(u64),
                                        u32, P(u32), P(u8), P(u32)]
         L.or_run.argtypes = [P(OrParams), P(u64), P(u32), P(u32), P(u8), P(u8), u32, P(u64),
-                             P(u64), P(u64), P(u64), P(u32), P(u32), u64, P(u64), P(u8),
+                             P(u64), P(u64), P(u64), P(u32), P(u32), P(u32), u64, P(u64), P(u8),
                              P(OrStats)]
         L.or_offline.argtypes = [P(OrParams), u32, u64]
+        L.or_run_mt.argtypes = L.or_run.argtypes + [ctypes.c_int]
         L.or_mesh_churn.argtypes = [P(OrParams), P(u64), P(u32), P(u8), P(u8), u32, P(u64), u32, u32,
                                     P(u32), P(u8), P(u8)]
         L.or_run_churn.argtypes = [P(OrParams), P(u64), P(u32), P(u32), P(u8), P(u8), u32, u32, P(u8), u32,
-                                   P(u64), P(u64), P(u64), P(u64), P(u32), P(u32), u64, P(u64), P(u8),
+                                   P(u64), P(u64), P(u64), P(u64), P(u32), P(u32), P(u32), u64, P(u64), P(u8),
                                    P(OrStats)]
         _lib = L
     return _lib
@@ -93,8 +94,8 @@ def params(**kw):
     d = dict(peers=100, connect_to=10, dial_extra=1, max_connections=0, fragments=1,
              muxer=0, signed_msgs=1, d=6, d_lo=4, d_hi=8, d_lazy=6, d_out=3,
              gossip_factor_milli=250, heartbeat_ns=1_000_000_000, backoff_ns=60_000_000_000,
-             flood_publish=1, idontwant=0, lazy_gossip=0, self_log=0, seed=1, history_gossip=3,
-             hb_phase_ns=0, churn_ppm=0, churn_down=10, churn_horizon=16, node=0)
+             flood_publish=1, idontwant=0, lazy_gossip=1, self_log=0, seed=1, history_gossip=3,
+             hb_phase_ns=0, churn_ppm=0, churn_down=10, churn_horizon=16, node=0, sub_graft=1)
     d.update(kw)
     return OrParams(**d)
 
@@ -108,10 +109,11 @@ def params_for(node, **kw):
     node = {"rust": 0, "go": 1, "nim": 2}.get(node, node)
     d = dict(node=node)
     if node == 1:
-        d.update(d_out=2, idontwant=1000, signed_msgs=0, self_log=1)
+        d.update(d_out=2, idontwant=1000, signed_msgs=0, self_log=1, sub_graft=0)
     elif node == 2:
         D = kw.get("d", 6)
-        d.update(dial_extra=0, max_connections=250, d_out=D // 2, d_lazy=D, signed_msgs=0, self_log=1)
+        d.update(dial_extra=0, max_connections=250, d_out=D // 2, d_lazy=D, signed_msgs=0, self_log=1,
+                 sub_graft=0)
     d.update(kw)
     return params(**d)
 
@@ -150,7 +152,9 @@ def build_topology(p):
     return row_ptr, col[:n].copy(), flags[:n].copy()
 
 
-def mesh_converge(p, row_ptr, col, flags, stage, lat, max_hb=400):
+def mesh_converge(p, row_ptr, col, flags, stage, lat, max_hb=400, allow_wide=False):
+    """allow_wide: a mesh row wider than the ELL (possible before heartbeat 1
+    prunes it) returns (flags, None, None, epochs) instead of raising."""
     N = p.peers
     S = lat.shape[0]
     flags = flags.copy()
@@ -164,6 +168,8 @@ def mesh_converge(p, row_ptr, col, flags, stage, lat, max_hb=400):
                                 _p(stage, ctypes.c_uint8), S, _p(lat, ctypes.c_uint64), max_hb,
                                 _p(mesh, ctypes.c_uint32), _p(cnt, ctypes.c_uint8),
                                 ctypes.byref(ep))
+    if rc == -5 and allow_wide:
+        return flags, None, None, ep.value
     if rc:
         raise ValueError("or_mesh_converge rc=%d" % rc)
     return flags, mesh.reshape(N, MESH_W), cnt, ep.value
@@ -198,7 +204,16 @@ def mesh_churn(p, row_ptr, col, flags, stage, lat, h_lo, h_hi):
     return mesh.reshape(E, N, MESH_W), cnt.reshape(E, N), off.reshape(E, N)
 
 
-def run_churn(p, row_ptr, col, snaps, h_lo, stage, lat, bw_up, bw_dn, sched_t, sched_pub, sched_size):
+def _frags_ptr(sched_frags, M):
+    """Per-message chunk counts (0 = p.fragments) -> (array keeping it alive, pointer or None)."""
+    if sched_frags is None:
+        return None, None
+    a = np.ascontiguousarray(np.broadcast_to(np.asarray(sched_frags, np.uint32), (M,)), np.uint32)
+    return a, _p(a, ctypes.c_uint32)
+
+
+def run_churn(p, row_ptr, col, snaps, h_lo, stage, lat, bw_up, bw_dn, sched_t, sched_pub, sched_size,
+              sched_frags=None):
     N = p.peers
     S = lat.shape[0]
     M = len(sched_t)
@@ -212,12 +227,13 @@ def run_churn(p, row_ptr, col, snaps, h_lo, stage, lat, bw_up, bw_dn, sched_t, s
     sched_pub, sched_size = a32(sched_pub), a32(sched_size)
     smesh, scnt, soff = a32(smesh.reshape(-1)), np.ascontiguousarray(scnt.reshape(-1), np.uint8), \
         np.ascontiguousarray(soff.reshape(-1), np.uint8)
+    fa, fp = _frags_ptr(sched_frags, M)
     stage = np.ascontiguousarray(stage, np.uint8)
     rc = lib().or_run_churn(ctypes.byref(p), _p(row_ptr, ctypes.c_uint64), _p(col, ctypes.c_uint32),
                             _p(smesh, ctypes.c_uint32), _p(scnt, ctypes.c_uint8), _p(soff, ctypes.c_uint8),
                             h_lo, len(scnt) // N, _p(stage, ctypes.c_uint8), S, _p(lat, ctypes.c_uint64),
                             _p(bw_up, ctypes.c_uint64), _p(bw_dn, ctypes.c_uint64), _p(sched_t, ctypes.c_uint64),
-                            _p(sched_pub, ctypes.c_uint32), _p(sched_size, ctypes.c_uint32), M,
+                            _p(sched_pub, ctypes.c_uint32), _p(sched_size, ctypes.c_uint32), fp, M,
                             _p(tc, ctypes.c_uint64), _p(hops, ctypes.c_uint8), ctypes.byref(st))
     if rc:
         raise ValueError("or_run_churn rc=%d" % rc)
@@ -231,8 +247,11 @@ def wire_packets(payload, muxer=0, signed=1):
     return pk.value, hd.value
 
 
-def run(p, row_ptr, col, mesh, cnt, stage, lat, bw_up, bw_dn, sched_t, sched_pub, sched_size, traffic=None):
-    """traffic: optional uint64 [N, 8] accumulated per-peer counters (or_run_traffic)."""
+def run(p, row_ptr, col, mesh, cnt, stage, lat, bw_up, bw_dn, sched_t, sched_pub, sched_size, sched_frags=None,
+        traffic=None, threads=0):
+    """traffic: optional uint64 [N, 8] accumulated per-peer counters (or_run_traffic);
+    sched_frags: chunks per message (0 = p.fragments); threads > 0: messages in
+    parallel on that many host threads (or_run_mt)."""
     N = p.peers
     S = lat.shape[0]
     M = len(sched_t)
@@ -245,13 +264,16 @@ def run(p, row_ptr, col, mesh, cnt, stage, lat, bw_up, bw_dn, sched_t, sched_pub
     sched_pub, sched_size = a32(sched_pub), a32(sched_size)
     mesh = a32(mesh.reshape(-1))
     stage = np.ascontiguousarray(stage, np.uint8)
+    fa, fp = _frags_ptr(sched_frags, M)
     args = (ctypes.byref(p), _p(row_ptr, ctypes.c_uint64), _p(col, ctypes.c_uint32),
             _p(mesh, ctypes.c_uint32), _p(cnt, ctypes.c_uint8), _p(stage, ctypes.c_uint8),
             S, _p(lat, ctypes.c_uint64), _p(bw_up, ctypes.c_uint64),
             _p(bw_dn, ctypes.c_uint64), _p(sched_t, ctypes.c_uint64),
-            _p(sched_pub, ctypes.c_uint32), _p(sched_size, ctypes.c_uint32), M,
+            _p(sched_pub, ctypes.c_uint32), _p(sched_size, ctypes.c_uint32), fp, M,
             _p(tc, ctypes.c_uint64), _p(hops, ctypes.c_uint8), ctypes.byref(st))
-    if traffic is None:
+    if threads:
+        rc = lib().or_run_mt(*args, int(threads))
+    elif traffic is None:
         rc = lib().or_run(*args)
     else:
         assert traffic.dtype == np.uint64 and traffic.shape == (N, 8) and traffic.flags.c_contiguous
@@ -269,18 +291,19 @@ def simulate(p, stages=1, links=(50, 50, 50, 50), mode=0, sched=None, max_hb=400
     stage = (np.arange(p.peers) % stages).astype(np.uint8)
     row_ptr, col, flags0 = build_topology(p)
     flags, mesh, cnt, epochs = mesh_converge(p, row_ptr, col, flags0, stage, lat, max_hb)
-    t, pub, size = sched
+    t, pub, size = sched[:3]
+    frags = sched[3] if len(sched) > 3 else None
     out = dict(lat=lat, bw=bw, stage=stage, row_ptr=row_ptr, col=col, flags=flags, mesh=mesh,
                cnt=cnt, epochs=epochs)
     if p.churn_ppm:  # time-varying mesh: snapshots of every epoch the schedule can use
         h_lo = min(epoch_at(p, x) for x in t)
         h_hi = max(epoch_at(p, x) for x in t) + p.churn_horizon
         snaps = mesh_churn(p, row_ptr, col, flags0, stage, lat, h_lo, h_hi)
-        tc, hops, stats = run_churn(p, row_ptr, col, snaps, h_lo, stage, lat, bw, bw, t, pub, size)
+        tc, hops, stats = run_churn(p, row_ptr, col, snaps, h_lo, stage, lat, bw, bw, t, pub, size, frags)
         out.update(snaps=snaps, h_lo=h_lo)
     else:
         tr = np.zeros((p.peers, 8), np.uint64) if traffic else None
-        tc, hops, stats = run(p, row_ptr, col, mesh, cnt, stage, lat, bw, bw, t, pub, size, traffic=tr)
+        tc, hops, stats = run(p, row_ptr, col, mesh, cnt, stage, lat, bw, bw, t, pub, size, frags, traffic=tr)
         if traffic:
             out["traffic"] = tr
     out.update(t_complete=tc, hops=hops, stats=stats)

@@ -139,7 +139,8 @@ def oracle_fixtures():
     }
     for name, (kw, S, links, M, size) in cases.items():
         p = oracle.params(**kw)
-        t = 946684800_000_000_000 + 500_000_000_000 + np.arange(M, dtype=np.uint64) * 1_000_000_000
+        # tx_time: injector start + 3 ms HTTP transit (gossipsim.T0_NS)
+        t = 946684800_000_000_000 + 500_003_000_000 + np.arange(M, dtype=np.uint64) * 1_000_000_000
         pub = (6 + np.arange(M)) % p.peers
         r = oracle.simulate(p, S, links, sched=(t, pub, np.full(M, size)))
         np.savez_compressed(os.path.join(HERE, "oracle_%s.npz" % name),

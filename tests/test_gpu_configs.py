@@ -67,7 +67,7 @@ def test_config2_10k_peers_f8_1000_msgs():
     row, col, _ = sim.csr()
     mesh, cnt = sim.mesh()
     lat, bw, stage = _links(p, S, LINKS)
-    idx = np.array([0, 517, 999])
+    idx = np.linspace(0, M - 1, 17).astype(int)  # 17 messages spread over all 8 batches
     otc, ohp, _ = oracle.run(p, row, col, mesh, cnt, stage, lat, bw, bw, *_sub(sched, idx))
     np.testing.assert_array_equal(tc[idx], otc)
     np.testing.assert_array_equal(hp[idx], ohp)
@@ -98,10 +98,12 @@ def test_config3_100k_hetero_gossip_churn():
     ep_pub = (sched[0] - np.uint64(p.hb_phase_ns)) // np.uint64(hb)
     limit = np.uint64(p.hb_phase_ns) + (ep_pub + np.uint64(p.churn_horizon + 1)) * np.uint64(hb)
     assert (tc[got] < np.broadcast_to(limit[:, None], tc.shape)[got]).all()
-    # sampled parity: the oracle replays churn from epoch 0 on the GPU's graph
+    # sampled parity: the oracle replays churn from epoch 0 on the GPU's graph;
+    # 16 messages from the first two 64-message batches, half of them after the
+    # first ring advance
     row, col, flags = sim.csr()
     lat, bw, stage = _links(p, S, LINKS)
-    idx = np.array([0, 1])
+    idx = np.array([0, 1, 9, 17, 30, 41, 55, 63, 64, 65, 77, 88, 99, 110, 121, 127])
     t, pub, size = _sub(sched, idx)
     h_lo = min(oracle.epoch_at(p, x) for x in t)
     h_hi = max(oracle.epoch_at(p, x) for x in t) + p.churn_horizon
@@ -109,6 +111,7 @@ def test_config3_100k_hetero_gossip_churn():
     otc, ohp, ost = oracle.run_churn(p, row, col, snaps, h_lo, stage, lat, bw, bw, t, pub, size)
     np.testing.assert_array_equal(tc[idx], otc)
     np.testing.assert_array_equal(hp[idx], ohp)
+    del snaps
     # message sharding under churn: a fresh context on a later shard reproduces it
     r2 = _sim(p, S, LINKS, batch=64).run(_sub(sched, slice(600, 700)))
     np.testing.assert_array_equal(r2["t_complete"], tc[600:700])
@@ -138,6 +141,28 @@ def test_config4_1m_peers_peer_partitioned():
     row, col, _ = whole.csr()
     mesh, cnt = whole.mesh()
     lat, bw, stage = _links(p, S, LINKS)
-    otc, ohp, _ = oracle.run(p, row, col, mesh, cnt, stage, lat, bw, bw, *_sub(sched, np.array([5])))
-    np.testing.assert_array_equal(ref["t_complete"][5:6], otc)
-    np.testing.assert_array_equal(ref["hops"][5:6], ohp)
+    idx = np.array([0, 3, 5, 7])
+    otc, ohp, _ = oracle.run(p, row, col, mesh, cnt, stage, lat, bw, bw, *_sub(sched, idx))
+    np.testing.assert_array_equal(ref["t_complete"][idx], otc)
+    np.testing.assert_array_equal(ref["hops"][idx], ohp)
+
+
+def test_config3_small_ring_cuts_batches(monkeypatch):
+    """Churn + lazy gossip with a snapshot ring too small for the batch
+    (GS_RING_BUDGET_MB): gs_run cuts batches at the ring size and advances the
+    ring between them (incl. the IHAVE target lists); bit-exact against the
+    oracle on every message."""
+    monkeypatch.setenv("GS_RING_BUDGET_MB", "1")
+    N, M, S = 700, 40, 5
+    hb = 100_000_000
+    p = oracle.params(peers=N, seed=33, lazy_gossip=1, churn_ppm=20000, churn_down=8, churn_horizon=12,
+                      heartbeat_ns=hb, hb_phase_ns=T0 - 2_000_000_000 + 37_000_000)
+    sched = _sched(M, N)
+    sim = _sim(p, S, LINKS, batch=64)
+    res = sim.run(sched)
+    ref = oracle.simulate(p, S, LINKS, sched=sched)
+    np.testing.assert_array_equal(res["t_complete"], ref["t_complete"])
+    np.testing.assert_array_equal(res["hops"], ref["hops"])
+    st = sim.stats()
+    for k in ("deliveries", "relaxations", "gossip_iwant", "latency_sum_ms"):
+        assert st[k] == ref["stats"][k], k

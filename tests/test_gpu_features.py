@@ -1,0 +1,145 @@
+"""GPU tests of the round-2 features, each bit-exact against the CPU oracle:
+config #0 (shadow/run.sh), subscription-time grafting, lazy gossip on the
+owner-computes pull path (the no-op proof and the push-path fallback),
+per-message fragment counts, the device-side per-message latency summary and
+the streaming result sink / arrival log."""
+import numpy as np
+import pytest
+
+import gossipsim
+import oracle
+from test_gpu_parity import T0, UND, _knobs, _sched, compare, gpu_sim
+
+pytestmark = pytest.mark.gpu
+
+
+def test_config0_shadow_runsh_100_peers():
+    """Config #0 exactly as SURVEY §8(d) defines it (shadow/run.sh:9-19,38 with
+    topogen.py's defaults 1 stage / 50 Mbit / 100 ms, topogen.py:15-20): 100
+    peers, CONNECTTO 10, one 15 000 B message, FRAGMENTS 1, publisher 4, seed 1."""
+    p = oracle.params(peers=100, connect_to=10, seed=1)
+    sched = (np.array([T0], np.uint64), np.array([4]), np.array([15000]))
+    sim, res = compare(p, 1, (50, 50, 100, 100), sched, batch=1)
+    st = sim.stats()
+    assert st["deliveries"] == 99 and st["gossip_iwant"] == 0
+    assert res["t_complete"][0, 4] == T0 and res["hops"][0, 4] == 0
+
+
+def test_subscription_grafting_on_heterogeneous_links():
+    """A5 (i) on the device: the converged mesh built from the handshake-ordered
+    subscription epoch equals the oracle's (compare checks CSR flags and mesh),
+    and it differs from heartbeat-only formation (sub_graft = 0)."""
+    p = oracle.params(peers=1500, seed=91)
+    sim, _ = compare(p, 5, (50, 150, 40, 130), _sched(8, 1500), batch=8)
+    p0 = oracle.params(peers=1500, seed=91, sub_graft=0)
+    sim0, _ = compare(p0, 5, (50, 150, 40, 130), _sched(8, 1500), batch=8)
+    assert (sim.mesh()[0] != sim0.mesh()[0]).any()
+
+
+def test_lazy_gossip_noop_proof_on_pull_path():
+    """The rust preset gossips (main.rs:230,235). With publishes 3 ms after a
+    heartbeat the first IHAVE lands after the last delivery: the pull path
+    proves it per batch and keeps its result (bit-exact against the oracle
+    with gossip on, no IWANT)."""
+    p = oracle.params(peers=2000, seed=92, lazy_gossip=1)
+    sim, _ = compare(p, 5, (50, 150, 40, 130), _sched(40, 2000), batch=16)
+    st = sim.stats()
+    assert st["gossip_noop_msgs"] == 40 and st["gossip_fallback_batches"] == 0 and st["gossip_iwant"] == 0
+
+
+@pytest.mark.parametrize("phase_ms", [0, 120])
+def test_lazy_gossip_fallback_to_push_path(phase_ms):
+    """A heartbeat at (or shortly after) the publish instant: IHAVEs can land
+    before the last delivery, the batch is re-run with gossip on the push path
+    and the eager run's counters are discarded (bit-exact, IWANTs taken)."""
+    p = oracle.params(peers=2000, seed=93, lazy_gossip=1,
+                      hb_phase_ns=(T0 + phase_ms * 1_000_000) % 1_000_000_000)
+    sim, _ = compare(p, 5, (50, 150, 40, 130), _sched(24, 2000), batch=8)
+    st = sim.stats()
+    assert st["gossip_fallback_batches"] == 3 and st["gossip_noop_msgs"] == 0 and st["gossip_iwant"] > 0
+
+
+def test_per_message_fragment_counts():
+    """gs_publish.frags (PublishCommand.chunks, main.rs:65-71): batches split
+    where the chunk count changes; 0 = FRAGMENTS."""
+    p = oracle.params(peers=900, seed=94, fragments=2)
+    t, pub, size = _sched(20, 900)
+    frags = np.array([0, 0, 3, 3, 3, 1, 8, 8, 0, 5, 5, 5, 5, 16, 2, 2, 0, 0, 4, 4], np.uint32)
+    sim, res = compare(p, 5, (50, 150, 40, 130), (t, pub, size, frags), batch=6)
+    assert sim.stats()["deliveries"] == 20 * 899
+
+
+def _np_summary(res, sched, self_log=False):
+    tc = res["t_complete"].astype(np.uint64)
+    M, N = tc.shape
+    out = {k: [] for k in ("delivered", "lat_sum_ms", "p50_ms", "p95_ms", "max_ms")}
+    hist = np.zeros((M, gossipsim.HIST_BINS), np.uint32)
+    for m in range(M):
+        ok = tc[m] != UND
+        if not self_log:
+            ok[sched[1][m]] = False
+        ms = np.sort(((tc[m][ok] - np.uint64(sched[0][m])) // np.uint64(1_000_000)).astype(np.int64))
+        n = len(ms)
+        out["delivered"].append(n)
+        out["lat_sum_ms"].append(int(ms.sum()))
+        out["max_ms"].append(int(ms.max()) if n else 0)
+        out["p50_ms"].append(int(ms[(n * 50 + 99) // 100 - 1]) if n else 0)
+        out["p95_ms"].append(int(ms[(n * 95 + 99) // 100 - 1]) if n else 0)
+        np.add.at(hist[m], np.minimum(ms // gossipsim.HIST_MS, gossipsim.HIST_BINS - 1), 1)
+    return out, hist
+
+
+@pytest.mark.parametrize("case", ["hetero", "slow_links", "churn", "nim_self_log"])
+def test_device_latency_summary(case):
+    """gs_msg_summary: delivered count, latency sum / max, the
+    100 ms histogram of summary_latency.awk's hop_lat and exact nearest-rank
+    p50 / p95, reduced on the device, equal numpy on the copied-out results
+    (slow links put the percentiles in the open last bin: the column path)."""
+    N, M = 1200, 20
+    kw = dict(peers=N, seed=95)
+    S, links = 5, (50, 150, 40, 130)
+    if case == "slow_links":
+        S, links = 1, (50, 50, 3000, 3000)
+        kw.update(lazy_gossip=0)
+    elif case == "churn":
+        kw.update(churn_ppm=20000, hb_phase_ns=gossipsim.SHADOW_START_NS)
+    elif case == "nim_self_log":
+        p = oracle.params_for("nim", **kw)
+    p = p if case == "nim_self_log" else oracle.params(**kw)
+    sched = _sched(M, N)
+    sim, _ = gpu_sim(p, S, links, batch=8)
+    res = sim.run(sched, summary=True)
+    ref, hist = _np_summary(res, sched, self_log=bool(p.self_log))
+    for k, v in ref.items():
+        np.testing.assert_array_equal(res["summary"][k], np.array(v), err_msg=k)
+    np.testing.assert_array_equal(res["summary"]["hist"], hist)
+    if case == "slow_links":
+        assert (res["summary"]["p50_ms"] >= 6300).all()
+
+
+def test_streaming_sink_and_log(tmp_path):
+    """gs_result_sink.on_block streams message-major blocks (no [M][N] host
+    array); gs_log_* writes the same lines as the grouped writer."""
+    N, M = 3000, 70
+    p = oracle.params(peers=N, seed=96)
+    sched = _sched(M, N)
+    sim, _ = gpu_sim(p, 5, (50, 150, 40, 130), batch=32)
+    whole = sim.run(sched)
+    sim.write_latency_log(str(tmp_path / "grouped"), whole)
+    sch = whole["schedule"]
+    log = sim.open_log(str(tmp_path / "stream"))
+    blocks, seen = [], []
+
+    def on_block(first, tc, hp):
+        seen.append((first, tc.shape[0]))
+        np.testing.assert_array_equal(tc, whole["t_complete"][first:first + tc.shape[0]])
+        np.testing.assert_array_equal(hp, whole["hops"][first:first + tc.shape[0]])
+        log.write(sch[first:first + tc.shape[0]], tc)
+        blocks.append(first)
+
+    sim.run(sched, on_block=on_block, block_msgs=10)
+    log.close()
+    assert sum(n for _, n in seen) == M and [f for f, _ in seen] == sorted(f for f, _ in seen)
+    a = sorted(open(str(tmp_path / "grouped")).read().splitlines())
+    b = sorted(open(str(tmp_path / "stream")).read().splitlines())
+    assert a == b and len(a) == M * (N - 1)

@@ -171,10 +171,17 @@ def test_peer_traffic_counters(kw):
 
 
 def test_peer_traffic_unsupported_modes():
-    p = oracle.params(peers=300, seed=72, lazy_gossip=1)
+    """Traffic counters cover eager forwarding: lazy gossip that sends IWANT
+    answers (heartbeat at the publish instant) and churn are refused."""
+    p = oracle.params(peers=300, seed=72, lazy_gossip=1, hb_phase_ns=T0 % 1_000_000_000)
     sim, _ = gpu_sim(p, 1, (50, 50, 50, 50))
     with pytest.raises(gossipsim.GossipSimError, match="GS_ESTATE"):
         sim.traffic()
+    sim.set_traffic(True)
+    with pytest.raises(gossipsim.GossipSimError, match="GS_EUNSUPPORTED"):
+        sim.run(_sched(2, 300))
+    p = oracle.params(peers=300, seed=72, churn_ppm=10000, hb_phase_ns=gossipsim.SHADOW_START_NS)
+    sim, _ = gpu_sim(p, 1, (50, 50, 50, 50))
     sim.set_traffic(True)
     with pytest.raises(gossipsim.GossipSimError, match="GS_EUNSUPPORTED"):
         sim.run(_sched(2, 300))

@@ -72,11 +72,22 @@ def test_partitioned_knobs():
         _check(oracle.params(**kw), S, links, 2, _sched(7, kw["peers"]))
 
 
+@pytest.mark.parametrize("frags", [1, 2])
+def test_partitioned_p8_10k_peers(frags):
+    """The config #4 split (P = 8) as loop-back partitions on one GPU, 10k peers."""
+    p = oracle.params(peers=10_000, seed=57, fragments=frags)
+    info = _check(p, 5, (50, 150, 40, 130), 8, _sched(8, 10_000))
+    assert info["buckets"] > 0
+
+
 def test_partitioned_unsupported_modes_fail_loudly():
-    p = oracle.params(peers=300, seed=55, lazy_gossip=1)
+    """Lazy gossip runs in partitioned mode only as the proven no-op (every part
+    checks its peers at gs_part_finish); a heartbeat at the publish instant
+    makes IWANTs possible and the batch fails instead of dropping them."""
+    p = oracle.params(peers=300, seed=55, lazy_gossip=1, hb_phase_ns=T0 % 1_000_000_000)
     (s,) = _parts(p, 1, (50, 50, 50, 50), 1, 4)
     with pytest.raises(gossipsim.GossipSimError, match="GS_EUNSUPPORTED"):
-        s.part_begin(_sched(4, 300))
+        partition.run_partitioned([s], _sched(4, 300), partition.LoopbackExchange())
     p = oracle.params(peers=300, seed=56, idontwant=1000)
     (s,) = _parts(p, 1, (50, 50, 50, 50), 1, 4)
     with pytest.raises(gossipsim.GossipSimError, match="GS_EUNSUPPORTED"):

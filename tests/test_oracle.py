@@ -121,6 +121,73 @@ def test_mesh_invariants():
     assert r["epochs"] < 400
 
 
+def _py_subscription_epoch(p, row, col, out, stage, lat):
+    """Pure-Python restatement of the subscription epoch 0 (DESIGN.md §2.3;
+    libp2p-gossipsub handle_received_subscriptions / handle_graft, upstream,
+    reached through the 20 s pump of rust-test-node/src/main.rs:357-379): every
+    peer grafts its first D_lo connections in subscription-arrival order
+    (3 rtt + lat(w->u), id); receivers take the GRAFTs in arrival order
+    (4 rtt, id) and refuse beyond D_hi unless they dialed the grafter."""
+    N, HS = p.peers, 3
+    rtt = lambda a, b: int(lat[a, b]) + int(lat[b, a])
+    nb = [[int(w) for w in col[row[u]:row[u + 1]]] for u in range(N)]
+    prop = [set() for _ in range(N)]
+    for u in range(N):
+        order = sorted(nb[u], key=lambda w: (HS * rtt(stage[u], stage[w]) + int(lat[stage[w], stage[u]]), w))
+        prop[u] = set(order[:p.d_lo])
+    mesh = [set() for _ in range(N)]
+    accepted = set()
+    for w in range(N):
+        c = len(prop[w])
+        for u in sorted((u for u in nb[w] if w in prop[u]), key=lambda u: ((HS + 1) * rtt(stage[u], stage[w]), u)):
+            if u in prop[w]:
+                accepted.add((u, w))
+                continue
+            if c >= p.d_hi and (w, u) not in out:
+                continue
+            accepted.add((u, w))
+            mesh[w].add(u)
+            c += 1
+    for u in range(N):
+        for w in prop[u]:
+            if (u, w) in accepted:
+                mesh[u].add(w)
+    return mesh
+
+
+@pytest.mark.parametrize("S,links", [(5, (50, 150, 40, 130)), (3, (30, 90, 20, 80)), (5, (20, 200, 10, 90))])
+def test_subscription_epoch_is_handshake_ordered(S, links):
+    """A5 (i): the mesh before heartbeat 1 equals the pure-Python restatement,
+    is symmetric, and is latency-ordered on heterogeneous links: its links are
+    markedly shorter than the connections they were chosen from. (GRAFTs from
+    peers a receiver dialed are always accepted, so a popular low-latency peer
+    can hold more than GS_MESH_W links before heartbeat 1 prunes it to D: the
+    mesh is read from the CSR flags.)"""
+    p = oracle.params(peers=400, seed=13)
+    lat, _ = oracle.topogen_links(S, *links)
+    stage = (np.arange(p.peers) % S).astype(np.uint8)
+    row, col, flags0 = oracle.build_topology(p)
+    row = row.astype(np.int64)
+    flags, _, _, ep = oracle.mesh_converge(p, row.astype(np.uint64), col, flags0, stage, lat, max_hb=0,
+                                           allow_wide=True)
+    assert ep == 0
+    out = set((u, int(col[e])) for u in range(p.peers) for e in range(row[u], row[u + 1]) if flags0[e] & 1)
+    ref = _py_subscription_epoch(p, row, col, out, stage, lat)
+    got = [set(int(col[e]) for e in range(row[u], row[u + 1]) if flags[e] & 2) for u in range(p.peers)]
+    assert got == ref
+    assert all(u in got[w] for u in range(p.peers) for w in got[u])
+    lat_mesh = np.mean([lat[stage[u], stage[w]] for u in range(p.peers) for w in got[u]])
+    lat_conn = np.mean([lat[stage[u], stage[col[e]]] for u in range(p.peers) for e in range(row[u], row[u + 1])])
+    assert lat_mesh < 0.9 * lat_conn
+    # without it (go / nim presets) the mesh before heartbeat 1 is empty
+    p0 = oracle.params(peers=400, seed=13, sub_graft=0)
+    _, _, cnt0, _ = oracle.mesh_converge(p0, row.astype(np.uint64), col, flags0, stage, lat, max_hb=0)
+    assert not cnt0.any()
+    # heartbeat 1 prunes every row back under D_hi (the converged mesh fits the ELL)
+    _, mesh1, cnt1, _ = oracle.mesh_converge(p, row.astype(np.uint64), col, flags0, stage, lat, max_hb=400)
+    assert cnt1.max() <= p.d_hi
+
+
 def _py_gossip_targets(p, r, v, h, ch=None):
     row, col = r["row_ptr"].astype(np.int64), r["col"]
     mesh, cnt = (r["mesh"], r["cnt"]) if ch is None else ch.snap(h)
