@@ -477,6 +477,108 @@ extern "C" gs_status gs_shadow_hosts(const char* path, uint32_t peers, uint8_t* 
   return GS_OK;
 }
 
+// The controller host of topogen's shadow.yaml (topogen.py:125-136):
+//   pod-<N>:
+//     processes:
+//     - path: /usr/bin/python
+//       args: ../../../traffic_sync.py -s 15000 -m 10 -d 1000.0 -n 100 --peer-selection
+//         id                                      (PyYAML folds long scalars)
+//       start_time: 500s
+extern "C" gs_status gs_shadow_injector(const char* path, gs_injector* out) {
+  if (!path || !out) return GS_EINVAL;
+  FILE* f = fopen(path, "r");
+  if (!f) return GS_EINVAL;
+  std::string args, start;
+  bool in_args = false;
+  size_t args_ind = 0;
+  char line[4096];
+  while (fgets(line, sizeof line, f)) {
+    std::string s(line);
+    while (!s.empty() && (s.back() == '\n' || s.back() == '\r')) s.pop_back();
+    const size_t ind = s.find_first_not_of(' ');
+    if (ind == std::string::npos) continue;
+    std::string body = s.substr(ind);
+    if (body.compare(0, 2, "- ") == 0) body = body.substr(2);
+    if (in_args && ind > args_ind && body.find(':') == std::string::npos) {  // folded continuation
+      args += " " + body;
+      continue;
+    }
+    in_args = false;
+    if (body.compare(0, 5, "args:") == 0 && body.find("traffic_sync") != std::string::npos) {
+      args = body.substr(5);
+      in_args = true;
+      args_ind = ind;
+    } else if (body.compare(0, 11, "start_time:") == 0 && !args.empty() && start.empty()) {
+      start = body.substr(11);
+    }
+  }
+  fclose(f);
+  if (args.empty()) return GS_EINVAL;  // no injector host in this config
+  memset(out, 0, sizeof *out);
+  out->start_ns = 500000000000ull;  // topogen.py:133
+  if (!start.empty()) {
+    char* end = nullptr;
+    const double v = strtod(start.c_str(), &end);
+    std::string u(end ? end : "");
+    u.erase(0, u.find_first_not_of(" '\""));
+    const double mul = (u.compare(0, 2, "ms") == 0) ? 1e6 : (u.compare(0, 3, "min") == 0) ? 6e10 : 1e9;
+    out->start_ns = (uint64_t)(v * mul + 0.5);
+  }
+  // tokens after the script name
+  std::vector<std::string> tok;
+  for (size_t i = 0; i < args.size();) {
+    while (i < args.size() && isspace((unsigned char)args[i])) i++;
+    size_t j = i;
+    while (j < args.size() && !isspace((unsigned char)args[j])) j++;
+    if (j > i) tok.push_back(args.substr(i, j - i));
+    i = j;
+  }
+  for (size_t i = 0; i + 1 < tok.size(); i++) {
+    const std::string& k = tok[i];
+    const char* v = tok[i + 1].c_str();
+    if (k == "-s" || k == "--msg-size") out->msg_size = (uint32_t)strtoul(v, nullptr, 10);
+    else if (k == "-m" || k == "--messages") out->messages = (uint32_t)strtoul(v, nullptr, 10);
+    else if (k == "-n" || k == "--network-size") out->peers = (uint32_t)strtoul(v, nullptr, 10);
+    else if (k == "-d" || k == "--delay") out->delay_ns = (uint64_t)(strtod(v, nullptr) * 1e6 + 0.5);  // ms (run.sh:36)
+  }
+  return (out->msg_size && out->messages) ? GS_OK : GS_EINVAL;
+}
+
+extern "C" gs_status gs_read_schedule(const char* path, gs_publish* out, uint64_t cap, uint64_t* n) {
+  if (!path || !n) return GS_EINVAL;
+  FILE* f = fopen(path, "r");
+  if (!f) return GS_EINVAL;
+  char line[1024];
+  uint64_t rows = 0;
+  gs_status st = GS_OK;
+  while (fgets(line, sizeof line, f)) {
+    char* h = strchr(line, '#');
+    if (h) *h = 0;
+    unsigned long long t = 0;
+    unsigned pub = 0, size = 0, fr = 0;
+    const int k = sscanf(line, "%llu %u %u %u", &t, &pub, &size, &fr);
+    if (k <= 0) {
+      char* q = line;
+      while (*q && isspace((unsigned char)*q)) q++;
+      if (*q) { st = GS_EINVAL; break; }  // not a number
+      continue;                           // blank / comment
+    }
+    if (k < 3) { st = GS_EINVAL; break; }
+    if (out && rows < cap) {
+      out[rows].t_pub_ns = t;
+      out[rows].publisher = pub;
+      out[rows].msg_size = size;
+      out[rows].frags = k == 4 ? fr : 0;
+      out[rows].reserved = 0;
+    }
+    rows++;
+  }
+  fclose(f);
+  *n = rows;
+  if (st != GS_OK) return st;
+  return rows > cap ? GS_ERANGE : GS_OK;
+}
+
 // The node's custom metrics (rust-test-node/src/metrics.rs:60-132, names shared
 // with go metrics.go and nim gossipsub-queues/main.nim:25-78) for every peer,
 // in prometheus-client's OpenMetrics text encoding (the format store_metrics

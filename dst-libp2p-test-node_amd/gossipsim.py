@@ -77,6 +77,11 @@ class GsStats(ctypes.Structure):
         ("gossip_iwant", u64), ("gossip_noop_msgs", u64), ("gossip_fallback_batches", u64), ("batches", u64)]
 
 
+class GsInjector(ctypes.Structure):
+    _fields_ = [("start_ns", u64), ("delay_ns", u64), ("msg_size", u32), ("messages", u32), ("peers", u32),
+                ("reserved", u32)]
+
+
 class GsPartRecord(ctypes.Structure):
     _fields_ = [("key", u64), ("start", u64), ("peer", u32), ("slot", u32)]
 
@@ -100,6 +105,8 @@ SIGNATURES = {
     "gs_get_traffic": (i32, [ctypes.c_void_p, P(u64)]),
     "gs_topogen_links": (i32, [u32, u32, u32, u32, u32, u32, P(u64), P(u64)]),
     "gs_schedule_runsh": (i32, [u32, u32, u32, u32, u64, u64, u32, P(GsPublish)]),
+    "gs_shadow_injector": (i32, [ctypes.c_char_p, P(GsInjector)]),
+    "gs_read_schedule": (i32, [ctypes.c_char_p, P(GsPublish), u64, P(u64)]),
     "gs_write_latency_log": (i32, [ctypes.c_char_p, P(GsPublish), u64, u32, P(u64), u32]),
     "gs_create": (i32, [P(GsConfig), P(ctypes.c_void_p)]),
     "gs_destroy": (i32, [ctypes.c_void_p]),
@@ -232,6 +239,28 @@ def schedule_runsh(n_msgs, peers, publisher_id, rotation, t0_ns, delay_ns, msg_s
                                  out)
     if rc:
         raise GossipSimError(rc, "invalid schedule")
+    return out
+
+
+def shadow_injector(path):
+    """The injector process of a Shadow config (traffic_sync.py args + start_time, topogen.py:125-136)."""
+    inj = GsInjector()
+    rc = lib().gs_shadow_injector(path.encode(), ctypes.byref(inj))
+    if rc:
+        raise GossipSimError(rc, "no injector host in %s" % path)
+    return {n: getattr(inj, n) for n, _ in GsInjector._fields_ if n != "reserved"}
+
+
+def read_schedule(path):
+    """Schedule file rows "t_pub_ns publisher msg_size [frags]" -> GsPublish array."""
+    n = u64()
+    rc = lib().gs_read_schedule(path.encode(), None, 0, ctypes.byref(n))
+    if rc not in (0, GS_ERANGE):
+        raise GossipSimError(rc, "malformed schedule %s" % path)
+    out = (GsPublish * n.value)()
+    rc = lib().gs_read_schedule(path.encode(), out, n.value, ctypes.byref(n))
+    if rc:
+        raise GossipSimError(rc, "malformed schedule %s" % path)
     return out
 
 

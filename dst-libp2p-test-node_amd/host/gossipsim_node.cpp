@@ -12,7 +12,6 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -25,9 +24,45 @@ void usage() {
           "usage: gossipsim-node [-bl MBIT] [-bh MBIT] [-ll MS] [-lh MS] [-st STAGES] [--shortest]\n"
           "         [-s MSG_BYTES] [-m MESSAGES] [--publisher ID] [--rotation 0|1]\n"
           "         [--delay-ms MS] [--t0-s SECONDS] [--http-us US] [--max-heartbeats H] [--latencies PATH]\n"
-          "         [--gml network_topology.gml --yaml shadow.yaml] [--shadowlog PATH] [--metrics PATH]\n"
+          "         [--gml network_topology.gml --yaml shadow.yaml] [--schedule FILE] [--shadowlog PATH] [--metrics PATH]\n"
+          "  --yaml also supplies the injector's -s/-m/-d and start_time unless given on the command line\n"
           "env: PEERS CONNECTTO FRAGMENTS MUXER MAXCONNECTIONS GOSSIPSUB_* SELFTRIGGER GS_NODE GS_SEED GS_BATCH\n"
           "     GS_DEVICE\n");
+}
+
+// Results arrive in message-major blocks (gs_result_sink.on_block): the log is
+// streamed through gs_log_* and the latencies folded into a 1 ms histogram, so
+// no [messages][peers] host array is held.
+struct Stream {
+  gs_log* log = nullptr;
+  const gs_publish* sched = nullptr;
+  uint32_t self_log = 0;
+  gs_status st = GS_OK;
+  std::vector<uint64_t> hist_ms;
+};
+
+void on_block(void* user, uint64_t first, uint32_t n, uint32_t peers, const uint64_t* tc, const uint8_t*) {
+  Stream* S = (Stream*)user;
+  if (S->log && S->st == GS_OK) S->st = gs_log_write(S->log, S->sched + first, n, tc);
+  for (uint32_t m = 0; m < n; m++) {
+    const gs_publish& p = S->sched[first + m];
+    for (uint32_t u = 0; u < peers; u++) {
+      const uint64_t t = tc[(size_t)m * peers + u];
+      if (t == GS_UNDELIVERED || (u == p.publisher && !S->self_log)) continue;
+      const uint64_t ms = (t - p.t_pub_ns) / 1000000ull;
+      if (ms >= S->hist_ms.size()) S->hist_ms.resize(ms + 1, 0);
+      S->hist_ms[ms]++;
+    }
+  }
+}
+
+// nearest-rank percentile (rank ceil(q*n)) of the 1 ms histogram
+uint64_t pct(const std::vector<uint64_t>& h, uint64_t n, uint32_t q100) {
+  const uint64_t rank = (n * q100 + 99) / 100;
+  uint64_t acc = 0;
+  for (size_t i = 0; i < h.size(); i++)
+    if ((acc += h[i]) >= rank && rank) return i;
+  return 0;
 }
 
 int die(gs_ctx* ctx, gs_status st, const char* what) {
@@ -46,7 +81,8 @@ int main(int argc, char** argv) {
   // the POST reaches the node 1.5 round trips over the 1 ms injector-hub links
   // after the injector sends it (topogen.py:64-69); tx_time is stamped then
   uint64_t http_us = 3000;
-  std::string latencies, gml, yaml, shadowlog, metrics;
+  std::string latencies, gml, yaml, shadowlog, metrics, schedule;
+  bool set_size = false, set_msgs = false, set_delay = false, set_t0 = false;
   for (int i = 1; i < argc; i++) {
     std::string a = argv[i];
     auto next = [&](void) -> const char* {
@@ -59,12 +95,12 @@ int main(int argc, char** argv) {
     else if (a == "-lh") lh = (uint32_t)atoi(next());
     else if (a == "-st") stages = (uint32_t)atoi(next());
     else if (a == "--shortest") mode = GS_LINKS_SHORTEST;
-    else if (a == "-s") msg_size = (uint32_t)atoi(next());
-    else if (a == "-m") n_msgs = (uint32_t)atoi(next());
+    else if (a == "-s") { msg_size = (uint32_t)atoi(next()); set_size = true; }
+    else if (a == "-m") { n_msgs = (uint32_t)atoi(next()); set_msgs = true; }
     else if (a == "--publisher") publisher = (uint32_t)atoi(next());
     else if (a == "--rotation") rotation = (uint32_t)atoi(next());
-    else if (a == "--delay-ms") delay_ms = strtoull(next(), nullptr, 10);
-    else if (a == "--t0-s") t0_s = strtoull(next(), nullptr, 10);
+    else if (a == "--delay-ms") { delay_ms = strtoull(next(), nullptr, 10); set_delay = true; }
+    else if (a == "--t0-s") { t0_s = strtoull(next(), nullptr, 10); set_t0 = true; }
     else if (a == "--http-us") http_us = strtoull(next(), nullptr, 10);
     else if (a == "--max-heartbeats") max_hb = (uint32_t)atoi(next());
     else if (a == "--latencies") latencies = next();
@@ -72,6 +108,7 @@ int main(int argc, char** argv) {
     else if (a == "--yaml") yaml = next();          // ... and its host placement (topogen.py output)
     else if (a == "--shadowlog") shadowlog = next(); // tracker counters for summary_shadowlog.awk
     else if (a == "--metrics") metrics = next();    // the node metrics (rust-test-node/src/metrics.rs)
+    else if (a == "--schedule") schedule = next();  // rows: t_pub_ns publisher msg_size [frags]
     else { usage(); return 2; }
   }
   gs_config cfg;
@@ -116,33 +153,52 @@ int main(int argc, char** argv) {
   uint32_t epochs = 0;
   if ((st = gs_mesh_converge(ctx, max_hb, &epochs)) != GS_OK) return die(ctx, st, "gs_mesh_converge");
 
-  std::vector<gs_publish> sched(n_msgs);
-  gs_schedule_runsh(n_msgs, cfg.peers, publisher, rotation, t0_s * 1000000000ull + http_us * 1000ull,
-                    delay_ms * 1000000ull, msg_size, sched.data());
-  std::vector<uint64_t> tc((size_t)n_msgs * cfg.peers);
-  gs_result_sink sink{tc.data(), nullptr};
+  std::vector<gs_publish> sched;
+  if (!schedule.empty()) {  // an explicit publish schedule stands in for the HTTP injector
+    uint64_t rows = 0;
+    st = gs_read_schedule(schedule.c_str(), nullptr, 0, &rows);
+    if (st != GS_OK && st != GS_ERANGE) { fprintf(stderr, "malformed schedule %s\n", schedule.c_str()); return die(ctx, st, "gs_read_schedule"); }
+    sched.resize(rows);
+    if ((st = gs_read_schedule(schedule.c_str(), sched.data(), rows, &rows)) != GS_OK) return die(ctx, st, "gs_read_schedule");
+    n_msgs = (uint32_t)rows;
+  } else {
+    uint64_t t0_ns = t0_s * 1000000000ull;
+    gs_injector inj;
+    if (!yaml.empty() && gs_shadow_injector(yaml.c_str(), &inj) == GS_OK) {  // traffic_sync.py args (topogen.py:125-136)
+      if (!set_size) msg_size = inj.msg_size;
+      if (!set_msgs) n_msgs = inj.messages;
+      if (!set_delay && inj.delay_ns) delay_ms = inj.delay_ns / 1000000ull;
+      if (!set_t0) t0_ns = 946684800000000000ull + inj.start_ns;  // Shadow epoch + the controller's start_time
+    }
+    sched.resize(n_msgs);
+    gs_schedule_runsh(n_msgs, cfg.peers, publisher, rotation, t0_ns + http_us * 1000ull, delay_ms * 1000000ull,
+                      msg_size, sched.data());
+  }
+  Stream strm;
+  strm.sched = sched.data();
+  strm.self_log = cfg.self_log;
+  if (!latencies.empty() && (st = gs_log_open(&cfg, latencies.c_str(), &strm.log)) != GS_OK)
+    return die(ctx, st, "gs_log_open");
+  uint64_t flag = 0;
+  gs_result_sink sink{};
+  sink.t_complete_ns = &flag;  // wanted, streamed through on_block
+  sink.on_block = on_block;
+  sink.user = &strm;
+  sink.block_msgs = 16;
   if ((st = gs_run(ctx, sched.data(), n_msgs, &sink)) != GS_OK) return die(ctx, st, "gs_run");
+  if (strm.log && ((st = gs_log_close(strm.log)) != GS_OK || (st = strm.st) != GS_OK))
+    return die(ctx, st, "gs_log_write");
   gs_stats s;
   gs_get_stats(ctx, &s);
-
-  std::vector<uint64_t> ms;
-  ms.reserve(s.deliveries);
-  for (uint32_t m = 0; m < n_msgs; m++)
-    for (uint32_t u = 0; u < cfg.peers; u++) {
-      const uint64_t t = tc[(size_t)m * cfg.peers + u];
-      if (t != GS_UNDELIVERED && u != sched[m].publisher) ms.push_back((t - sched[m].t_pub_ns) / 1000000ull);
-    }
-  std::sort(ms.begin(), ms.end());
-  auto pct = [&](double q) { return ms.empty() ? 0 : ms[std::min(ms.size() - 1, (size_t)(q * (ms.size() - 1)))]; };
+  uint64_t n = 0;
+  for (uint64_t c : strm.hist_ms) n += c;
   fprintf(stderr,
           "peers=%u mesh_epochs=%u messages=%llu deliveries=%llu frag_deliveries=%llu "
-          "relaxations=%llu latency_ms p50=%llu p95=%llu max=%llu\n",
+          "relaxations=%llu gossip_iwant=%llu latency_ms p50=%llu p95=%llu max=%llu\n",
           cfg.peers, epochs, (unsigned long long)s.messages, (unsigned long long)s.deliveries,
           (unsigned long long)s.frag_deliveries, (unsigned long long)s.relaxations,
-          (unsigned long long)pct(0.5), (unsigned long long)pct(0.95), (unsigned long long)pct(1.0));
-  if (!latencies.empty() &&
-      (st = gs_write_node_log(&cfg, latencies.c_str(), sched.data(), n_msgs, tc.data())) != GS_OK)
-    return die(ctx, st, "gs_write_node_log");
+          (unsigned long long)s.gossip_iwant, (unsigned long long)pct(strm.hist_ms, n, 50),
+          (unsigned long long)pct(strm.hist_ms, n, 95), (unsigned long long)pct(strm.hist_ms, n, 100));
   if (counters) {
     std::vector<uint64_t> tr((size_t)cfg.peers * GS_TRAFFIC_COLS), row((size_t)cfg.peers + 1);
     std::vector<uint8_t> mc(cfg.peers);

@@ -237,6 +237,27 @@ gs_status gs_links_from_gml(const char* gml_path, uint32_t mode, uint32_t max_no
  * injector) are skipped; a peer without a host is GS_EINVAL. */
 gs_status gs_shadow_hosts(const char* yaml_path, uint32_t peers, uint8_t* stage_of_peer);
 
+/* The publish injector of a Shadow config (shadow.yaml as topogen.py:125-136
+ * writes it): the controller host's process `args`
+ * "traffic_sync.py -s <msg_size> -m <messages> -d <delay> -n <peers> ..." and
+ * its start_time. The delay is read in milliseconds, the unit shadow/run.sh:36
+ * passes (topogen.py:26's help text says seconds). */
+typedef struct gs_injector {
+    uint64_t start_ns;    /* process start_time (500s in topogen.py:133)          */
+    uint64_t delay_ns;    /* -d: inter-message delay                              */
+    uint32_t msg_size;    /* -s                                                   */
+    uint32_t messages;    /* -m                                                   */
+    uint32_t peers;       /* -n                                                   */
+    uint32_t reserved;
+} gs_injector;
+gs_status gs_shadow_injector(const char* yaml_path, gs_injector* out);
+
+/* A publish schedule file: one row per message, "t_pub_ns publisher msg_size
+ * [frags]" (whitespace separated, '#' comments). Returns GS_ERANGE with
+ * *n = rows when cap is too small (call again with room), GS_EINVAL on a
+ * malformed row. */
+gs_status gs_read_schedule(const char* path, gs_publish* out, uint64_t cap, uint64_t* n);
+
 /* Publish schedule of shadow/run.sh:34-36 (publisher_id, publisher_rotation,
  * inter_message_delay): row i = {t0 + i*delay, (pub0 + i*rotation) mod N, size}. */
 gs_status gs_schedule_runsh(uint32_t n_msgs, uint32_t peers, uint32_t publisher_id,

@@ -227,9 +227,45 @@ def test_cli_runs_a_shadow_experiment(tmp_path):
     sched = gossipsim.schedule_runsh(4, 100, 6, 1, gossipsim.T0_NS, gossipsim.DELAY_NS, 15000)
     res = sim.run(sched)
     sim.write_latency_log(str(tmp_path / "py_lat"), res)
-    assert open(out["lat"]).read() == open(str(tmp_path / "py_lat")).read()
+    # the CLI streams its log block by block: same lines, message-major order
+    assert sorted(open(out["lat"]).read().splitlines()) == sorted(open(str(tmp_path / "py_lat")).read().splitlines())
     assert len(open(out["shadowlog"]).read().splitlines()) == 100
     assert open(out["metrics"]).read().endswith("# EOF\n")
+
+
+def test_cli_injector_args_and_schedule_file(tmp_path):
+    """A1 inputs: (1) --gml/--yaml alone takes traffic_sync.py's -s/-m/-d and
+    start_time from shadow.yaml (topogen.py:125-136); (2) --schedule FILE with
+    per-message chunk counts; both bit-exact against the oracle."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(gossipsim.LIB_PATH), "gossipsim-node")
+    gml, yml = (os.path.join(GOLDEN, "topogen_runsh_example." + x) for x in ("gml", "yaml"))
+    env = dict(os.environ, PEERS="100", CONNECTTO="10", FRAGMENTS="1", GS_SEED="7")
+    p = oracle.params(peers=100, seed=7)
+    inj = gossipsim.shadow_injector(yml)
+    t = np.uint64(946684800_000_000_000 + inj["start_ns"] + gossipsim.HTTP_TRANSIT_NS) + \
+        np.arange(inj["messages"], dtype=np.uint64) * np.uint64(inj["delay_ns"])
+    pub = (6 + np.arange(inj["messages"])) % 100
+    ref = oracle.simulate(p, 5, (50, 150, 40, 130), sched=(t, pub, np.full(len(t), inj["msg_size"])))
+    subprocess.run([exe, "--gml", gml, "--yaml", yml, "--latencies", str(tmp_path / "a")], env=env, check=True,
+                   timeout=60)
+    sim = gossipsim.Simulator(**_knobs(p))
+    sched = gossipsim.schedule_runsh(len(t), 100, 6, 1, int(t[0]), inj["delay_ns"], inj["msg_size"])
+    sim.write_latency_log(str(tmp_path / "b"), {"schedule": sched, "t_complete": ref["t_complete"]})
+    assert sorted(open(str(tmp_path / "a")).read().splitlines()) == sorted(open(str(tmp_path / "b")).read().splitlines())
+    # schedule file: mixed chunk counts, publishes 700 ms apart (overlapping in time)
+    rows = [(int(T0) + i * 700_000_000, (11 * i + 3) % 100, 15000, [0, 3, 8, 1, 2, 16][i % 6]) for i in range(9)]
+    (tmp_path / "sched").write_text("".join("%d %d %d %d\n" % r for r in rows))
+    env2 = dict(env, FRAGMENTS="2")
+    p2 = oracle.params(peers=100, seed=7, fragments=2)
+    subprocess.run([exe, "--gml", gml, "--yaml", yml, "--schedule", str(tmp_path / "sched"), "--latencies",
+                    str(tmp_path / "c")], env=env2, check=True, timeout=60)
+    cols = [np.array([r[k] for r in rows]) for k in range(4)]
+    ref2 = oracle.simulate(p2, 5, (50, 150, 40, 130), sched=(cols[0].astype(np.uint64), cols[1], cols[2], cols[3]))
+    sched2 = gossipsim.read_schedule(str(tmp_path / "sched"))
+    sim2 = gossipsim.Simulator(**_knobs(p2))
+    sim2.write_latency_log(str(tmp_path / "d"), {"schedule": sched2, "t_complete": ref2["t_complete"]})
+    assert sorted(open(str(tmp_path / "c")).read().splitlines()) == sorted(open(str(tmp_path / "d")).read().splitlines())
 
 
 def test_fragment_collision_defect_d8():

@@ -324,3 +324,84 @@ def test_shard_messages_partition():
     assert idx == list(range(steps * world * B))
     for t, p in seen:
         assert p == (6 + (t - gossipsim.T0_NS) // gossipsim.DELAY_NS) % N
+
+
+def test_shadow_injector_from_topogen_yaml():
+    """The controller host topogen writes (topogen.py:125-136): traffic_sync.py's
+    -s / -m / -d / -n args and its start_time, from the committed topogen output."""
+    inj = gossipsim.shadow_injector(os.path.join(GOLDEN, "topogen_runsh_example.yaml"))
+    assert inj == dict(start_ns=500_000_000_000, delay_ns=1_000_000_000, msg_size=15000, messages=10, peers=100)
+    with pytest.raises(gossipsim.GossipSimError):
+        gossipsim.shadow_injector(os.path.join(GOLDEN, "topogen_runsh_example.gml"))
+
+
+def test_read_schedule_file(tmp_path):
+    path = tmp_path / "sched.txt"
+    path.write_text("# t_pub_ns publisher msg_size [frags]\n"
+                    "946685300003000000 6 15000\n\n"
+                    "946685301003000000 7 15000 3   # three chunks\n"
+                    "946685302003000000 8 4000 0\n")
+    rows = gossipsim.read_schedule(str(path))
+    got = [(r.t_pub_ns, r.publisher, r.msg_size, r.frags) for r in rows]
+    assert got == [(946685300003000000, 6, 15000, 0), (946685301003000000, 7, 15000, 3),
+                   (946685302003000000, 8, 4000, 0)]
+    bad = tmp_path / "bad.txt"
+    bad.write_text("946685300003000000 6\n")
+    with pytest.raises(gossipsim.GossipSimError, match="GS_EINVAL"):
+        gossipsim.read_schedule(str(bad))
+
+
+def _oracle_run_for_log(N=400, M=12, seed=17, node="rust"):
+    p = oracle.params_for(node, peers=N, seed=seed)
+    t = np.uint64(gossipsim.T0_NS) + np.arange(M, dtype=np.uint64) * np.uint64(gossipsim.DELAY_NS)
+    pub = ((6 + np.arange(M)) % N).astype(np.uint32)
+    r = oracle.simulate(p, 5, (50, 150, 40, 130), sched=(t, pub, np.full(M, 15000)))
+    sched = gossipsim.schedule_runsh(M, N, 6, 1, gossipsim.T0_NS, gossipsim.DELAY_NS, 15000)
+    cfg = gossipsim.PeerConfig(node=node, peers=N, seed=seed)
+    return cfg, sched, r["t_complete"]
+
+
+@pytest.mark.parametrize("node", ["rust", "nim"])
+def test_streaming_log_equals_grouped_writer(tmp_path, node):
+    """gs_log_* (blocks of message-major results, as gs_result_sink.on_block
+    hands them over) writes exactly the lines of the grouped writer; only the
+    order differs (block by block instead of peer by peer)."""
+    cfg, sched, tc = _oracle_run_for_log(node=node)
+    grouped = str(tmp_path / "grouped")
+    rc = gossipsim.lib().gs_write_node_log(ctypes.byref(cfg.c), grouped.encode(), sched, len(sched),
+                                           tc.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)))
+    assert rc == 0
+    log = gossipsim.LogStream(cfg, str(tmp_path / "stream"))
+    for q0 in range(0, len(sched), 5):
+        log.write(sched[q0:q0 + 5], tc[q0:q0 + 5])
+    log.close()
+    a = open(grouped).read().splitlines()
+    b = open(str(tmp_path / "stream")).read().splitlines()
+    assert sorted(a) == sorted(b) and len(a) > 0
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_SHADOW) or not shutil.which("awk"),
+                    reason="reference awk scripts only in the build container")
+def test_streaming_log_round_trips_through_summary_latency_large(tmp_path):
+    """The streamed log through the reference's summary_latency_large.awk: its
+    per-message "MAX delay" lines equal the per-message maxima of the results
+    (the max_ms of gs_msg_summary), and its message count is the schedule's."""
+    cfg, sched, tc = _oracle_run_for_log()
+    log = gossipsim.LogStream(cfg, str(tmp_path / "lat"))
+    for q0 in range(0, len(sched), 4):
+        log.write(sched[q0:q0 + 4], tc[q0:q0 + 4])
+    log.close()
+    got = subprocess.check_output(["awk", "-f", os.path.join(REF_SHADOW, "summary_latency_large.awk"),
+                                   str(tmp_path / "lat")]).decode()
+    mx = {}
+    for line in got.splitlines():
+        m = re.match(r"MAX delay for\s+(\d+)\s+is\s+(\d+)", line)
+        if m:
+            mx[int(m.group(1))] = int(m.group(2))
+    want = {}
+    for q, row in enumerate(sched):
+        ok = tc[q] != np.iinfo(np.uint64).max
+        ok[row.publisher] = False
+        want[row.t_pub_ns] = int(((tc[q][ok] - np.uint64(row.t_pub_ns)) // np.uint64(1_000_000)).max())
+    assert mx == want
+    assert "Total Messages Published :  %d" % len(sched) in got
