@@ -25,7 +25,7 @@ struct Error {
 };
 
 // Device-side error word bits (set by kernels, checked by the host).
-enum : uint32_t { ERR_TIME = 1, ERR_HOPS = 2, ERR_MESH = 4, ERR_DEG = 8 };
+enum : uint32_t { ERR_TIME = 1, ERR_HOPS = 2, ERR_MESH = 4, ERR_DEG = 8, ERR_SYNC = 16 };
 
 // Device buffer owned by a context.
 template <class T>
@@ -104,6 +104,7 @@ struct Ctx {
   uint32_t ring_R = 0;
   uint64_t churn_state = 0, ring_lo = 1, ring_hi = 0;  // mesh state epoch; valid ring epochs
   DevBuf<uint8_t> d_mcnt;    // [N]
+  DevBuf<uint32_t> d_bar;    // k_epochs grid barrier counter
 
   // dissemination (per batch)
   DevBuf<uint64_t> d_keys;   // [N * B * FP] peer-major (u, m, f)
@@ -115,6 +116,9 @@ struct Ctx {
   DevBuf<uint32_t> d_fr_cnt;
   DevBuf<uint64_t> d_tmin;   // split tile skip: min pending key per tile
   DevBuf<uint8_t> d_touched; // split tile skip: pushed since last scan
+  DevBuf<uint64_t> d_tgmin;  // split tile skip + gossip: next IHAVE arrival per tile
+  DevBuf<uint32_t> d_tnf;    // split tile skip + gossip: non-final lanes per tile
+  DevBuf<uint32_t> d_tstamp; // split tile skip + gossip: launch + 1 of the last scan
   DevBuf<uint32_t> d_gl_idx; // lazy gossip: lanes with an IHAVE arrival in the bucket
   DevBuf<uint32_t> d_gl_cnt;
   DevBuf<uint64_t> d_nonfinal;  // [3]

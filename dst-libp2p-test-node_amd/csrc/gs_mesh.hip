@@ -54,13 +54,17 @@ __global__ __launch_bounds__(TB) void k_offline(uint32_t N, uint64_t seed, uint3
 
 // Links to offline peers leave the mesh (a disconnect, not a PRUNE: no back-off).
 // One peer per wave, lane per CSR entry.
-__global__ __launch_bounds__(TB) void k_disconnect(MeshArgs a) {
-  const uint32_t u = blockIdx.x * (TB / 64) + (threadIdx.x >> 6);
-  if (u >= a.N) return;  // wave-uniform
+template <int G>
+__device__ __forceinline__ void row_disconnect(const MeshArgs& a, uint32_t u) {
   const bool ou = is_off(a.off, u);
   const uint64_t b = a.row[u], en = a.row[u + 1];
-  for (uint64_t e = b + (threadIdx.x & 63); e < en; e += 64)
+  for (uint64_t e = b + (threadIdx.x & (G - 1)); e < en; e += G)
     if (ou || is_off(a.off, a.col[e])) a.flags[e] &= (uint8_t)~F_MESH;
+}
+template <int G>
+__global__ __launch_bounds__(TB) void k_disconnect(MeshArgs a) {
+  const uint32_t u = (blockIdx.x * TB + threadIdx.x) / G;
+  if (u < a.N) row_disconnect<G>(a, u);  // group-uniform
 }
 
 // Heartbeat decisions of one peer per wave (lane l holds CSR entries l, l+64,
@@ -72,35 +76,57 @@ __global__ __launch_bounds__(TB) void k_disconnect(MeshArgs a) {
 constexpr int HB_PER_LANE = (int)(MAX_DEG / 64);
 static_assert(MAX_DEG % 64 == 0 && HB_PER_LANE <= 4, "k_heartbeat covers MAX_DEG entries with 64 lanes");
 
-// wave argmin over (key, idx); ~0u if every key is INF64
-__device__ __forceinline__ uint32_t wave_argmin(uint64_t key, uint32_t idx) {
-  for (int off = 32; off > 0; off >>= 1) {
+// Row kernels run one peer per group of G lanes (G = 64, or 16 when every
+// row has at most 4*16 entries: four rows per wave, four times the memory
+// requests in flight of the latency-bound one-row-per-wave form). Lane l of a
+// group holds entries k*G + l, k < HB_PER_LANE.
+
+// the calling lane's group bits of a wave ballot
+template <int G>
+__device__ __forceinline__ uint64_t gballot(bool p) {
+  const uint64_t m = __ballot(p);
+  if constexpr (G == 64) {
+    return m;
+  } else {
+    const int gbase = (threadIdx.x & 63) & ~(G - 1);
+    return (m >> gbase) & ((1ull << G) - 1);
+  }
+}
+
+// group argmin over (key, idx); ~0u if every key is INF64
+template <int G>
+__device__ __forceinline__ uint32_t group_argmin(uint64_t key, uint32_t idx) {
+  for (int off = G / 2; off > 0; off >>= 1) {
     const uint64_t k2 = __shfl_xor(key, off);
     const uint32_t i2 = (uint32_t)__shfl_xor((int)idx, off);
     if (k2 < key || (k2 == key && i2 < idx)) { key = k2; idx = i2; }
   }
-  return key == INF64 ? ~0u : (uint32_t)__builtin_amdgcn_readfirstlane(idx);
+  return key == INF64 ? ~0u : idx;
 }
 
-// This lane's smallest (key, entry) among its entries k*64 + lane.
+// This lane's smallest (key, entry) among its entries k*G + lane.
+template <int G>
 __device__ __forceinline__ void lane_min(const uint64_t (&key)[HB_PER_LANE], int lane, uint64_t& bk, uint32_t& bi) {
   bk = INF64;
   bi = ~0u;
 #pragma unroll
   for (int k = 0; k < HB_PER_LANE; k++)  // ascending k: a tie keeps the lower entry
-    if (key[k] < bk) { bk = key[k]; bi = (uint32_t)(k * 64 + lane); }
+    if (key[k] < bk) { bk = key[k]; bi = (uint32_t)(k * G + lane); }
 }
 
+template <int G>
 __device__ __forceinline__ void drop_key(uint64_t (&key)[HB_PER_LANE], uint32_t sel) {
 #pragma unroll
   for (int k = 0; k < HB_PER_LANE; k++)
-    if ((uint32_t)k == (sel >> 6)) key[k] = INF64;
+    if ((uint32_t)k == (sel / G)) key[k] = INF64;
 }
 
-__global__ __launch_bounds__(TB) void k_heartbeat(MeshArgs a) {
-  const uint32_t u = blockIdx.x * (TB / 64) + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (u >= a.N || is_off(a.off, u)) return;  // wave-uniform
+template <int G>
+__device__ __forceinline__ void row_heartbeat(const MeshArgs& a, uint32_t u) {
+  const int lane = threadIdx.x & (G - 1);
+  const int gbase = (threadIdx.x & 63) & ~(G - 1);
+  (void)gbase;
+  if (is_off(a.off, u)) return;  // wave-uniform
   const uint64_t b = a.row[u], en = a.row[u + 1];
   const uint32_t deg = (uint32_t)(en - b);
   uint32_t f[HB_PER_LANE], w[HB_PER_LANE];
@@ -108,22 +134,22 @@ __global__ __launch_bounds__(TB) void k_heartbeat(MeshArgs a) {
   uint32_t m = 0, o = 0;
 #pragma unroll
   for (int k = 0; k < HB_PER_LANE; k++) {
-    const uint32_t i = (uint32_t)(k * 64 + lane);
+    const uint32_t i = (uint32_t)(k * G + lane);
     f[k] = 0;
     w[k] = 0;
     elig[k] = false;
-    if (k * 64 >= (int)deg) continue;  // wave-uniform
+    if (k * G >= (int)deg) continue;  // wave-uniform
     if (i < deg) {
       f[k] = a.flags[b + i];
       w[k] = a.col[b + i];
       elig[k] = !(f[k] & F_MESH) && a.epoch > a.until[b + i] && !is_off(a.off, w[k]);
     }
-    m += (uint32_t)__popcll(__ballot(f[k] & F_MESH));
-    o += (uint32_t)__popcll(__ballot((f[k] & F_MESH) && (f[k] & F_OUT)));
+    m += (uint32_t)__popcll(gballot<G>(f[k] & F_MESH));
+    o += (uint32_t)__popcll(gballot<G>((f[k] & F_MESH) && (f[k] & F_OUT)));
   }
   const int fpack = (int)(f[0] | (f[1] << 8) | (f[2] << 16) | (f[3] << 24));
   auto flag_of = [&](uint32_t sel) {  // flags of entry sel, from the lane holding it
-    return ((uint32_t)__shfl(fpack, (int)(sel & 63)) >> (8 * (sel >> 6))) & 0xFFu;
+    return ((uint32_t)__shfl(fpack, gbase + (int)(sel % G)) >> (8 * (sel / G))) & 0xFFu;
   };
   uint64_t key[HB_PER_LANE];
   if (a.sub) {  // subscription epoch: the first D_lo connections in subscription-arrival order
@@ -131,7 +157,7 @@ __global__ __launch_bounds__(TB) void k_heartbeat(MeshArgs a) {
 #pragma unroll
     for (int k = 0; k < HB_PER_LANE; k++) {
       key[k] = INF64;
-      if (k * 64 < (int)deg && (uint32_t)(k * 64 + lane) < deg && !(f[k] & F_MESH)) {
+      if (k * G < (int)deg && (uint32_t)(k * G + lane) < deg && !(f[k] & F_MESH)) {
         const uint32_t sw = a.stage[w[k]];
         const uint64_t lwu = a.lat[sw * a.S + su];
         key[k] = (uint64_t)HS_RTTS * (a.lat[su * a.S + sw] + lwu) + lwu;
@@ -140,11 +166,11 @@ __global__ __launch_bounds__(TB) void k_heartbeat(MeshArgs a) {
     for (uint32_t q = 0; q < a.d_lo; q++) {
       uint64_t bk;
       uint32_t bi;
-      lane_min(key, lane, bk, bi);
-      const uint32_t sel = wave_argmin(bk, bi);
+      lane_min<G>(key, lane, bk, bi);
+      const uint32_t sel = group_argmin<G>(bk, bi);
       if (sel == ~0u) break;
-      if ((int)(sel & 63) == lane) {
-        drop_key(key, sel);
+      if ((int)(sel % G) == lane) {
+        drop_key<G>(key, sel);
         a.prop[b + sel] |= PR_GRAFT;
       }
     }
@@ -156,17 +182,17 @@ __global__ __launch_bounds__(TB) void k_heartbeat(MeshArgs a) {
 #pragma unroll
     for (int k = 0; k < HB_PER_LANE; k++) {
       key[k] = INF64;
-      if (k * 64 < (int)deg && elig[k]) key[k] = rng(a.seed, P_GRAFT, u, a.epoch, w[k]);
+      if (k * G < (int)deg && elig[k]) key[k] = rng(a.seed, P_GRAFT, u, a.epoch, w[k]);
     }
     for (uint32_t q = 0; q < a.d - m; q++) {
       uint64_t bk;
       uint32_t bi;
-      lane_min(key, lane, bk, bi);
-      const uint32_t sel = wave_argmin(bk, bi);
+      lane_min<G>(key, lane, bk, bi);
+      const uint32_t sel = group_argmin<G>(bk, bi);
       if (sel == ~0u) break;
-      if ((int)(sel & 63) == lane) {
-        drop_key(key, sel);
-        graft |= 1u << (sel >> 6);
+      if ((int)(sel % G) == lane) {
+        drop_key<G>(key, sel);
+        graft |= 1u << (sel / G);
         a.prop[b + sel] |= PR_GRAFT;
       }
       mm++;
@@ -180,20 +206,20 @@ __global__ __launch_bounds__(TB) void k_heartbeat(MeshArgs a) {
 #pragma unroll
     for (int k = 0; k < HB_PER_LANE; k++) {
       key[k] = INF64;
-      if (k * 64 < (int)deg && (f[k] & F_MESH)) key[k] = rng(a.seed, P_PRUNE, u, a.epoch, w[k]);
+      if (k * G < (int)deg && (f[k] & F_MESH)) key[k] = rng(a.seed, P_PRUNE, u, a.epoch, w[k]);
     }
     for (uint32_t q = 0; q < m && removed < excess; q++) {
       uint64_t bk;
       uint32_t bi;
-      lane_min(key, lane, bk, bi);
-      const uint32_t sel = wave_argmin(bk, bi);
+      lane_min<G>(key, lane, bk, bi);
+      const uint32_t sel = group_argmin<G>(bk, bi);
       if (sel == ~0u) break;
-      if ((int)(sel & 63) == lane) drop_key(key, sel);
+      if ((int)(sel % G) == lane) drop_key<G>(key, sel);
       if (flag_of(sel) & F_OUT) {
         if (oo <= a.d_out) continue;
         oo--;
       }
-      if ((int)(sel & 63) == lane) a.prop[b + sel] |= PR_PRUNE;
+      if ((int)(sel % G) == lane) a.prop[b + sel] |= PR_PRUNE;
       removed++;
       mm--;
     }
@@ -203,30 +229,47 @@ __global__ __launch_bounds__(TB) void k_heartbeat(MeshArgs a) {
     for (int k = 0; k < HB_PER_LANE; k++)
     {
       key[k] = INF64;
-      if (k * 64 < (int)deg && elig[k] && (f[k] & F_OUT) && !((graft >> k) & 1u))
+      if (k * G < (int)deg && elig[k] && (f[k] & F_OUT) && !((graft >> k) & 1u))
         key[k] = rng(a.seed, P_OUT_GRAFT, u, a.epoch, w[k]);
     }
     for (uint32_t q = 0; q < a.d_out - oo; q++) {
       uint64_t bk;
       uint32_t bi;
-      lane_min(key, lane, bk, bi);
-      const uint32_t sel = wave_argmin(bk, bi);
+      lane_min<G>(key, lane, bk, bi);
+      const uint32_t sel = group_argmin<G>(bk, bi);
       if (sel == ~0u) break;
-      if ((int)(sel & 63) == lane) {
-        drop_key(key, sel);
+      if ((int)(sel % G) == lane) {
+        drop_key<G>(key, sel);
         a.prop[b + sel] |= PR_GRAFT;
       }
     }
   }
 }
 
+template <int G>
+__global__ __launch_bounds__(TB) void k_heartbeat(MeshArgs a) {
+  const uint32_t u = (blockIdx.x * TB + threadIdx.x) / G;
+  if (u < a.N) row_heartbeat<G>(a, u);  // group-uniform
+}
+
+// Disconnects and heartbeat decisions of an epoch in one pass: both read and
+// write only the peer's own row.
+template <int G>
+__global__ __launch_bounds__(TB) void k_disc_heartbeat(MeshArgs a) {
+  const uint32_t u = (blockIdx.x * TB + threadIdx.x) / G;
+  if (u >= a.N) return;  // group-uniform
+  row_disconnect<G>(a, u);
+  row_heartbeat<G>(a, u);
+}
+
 // GRAFT handling at receiver w, one peer per wave: the proposals of w's
 // neighbours are found in parallel (lane per entry), then taken in arrival
 // order — (latency u->w, id), by wave argmin — with the running mesh size c.
-__global__ __launch_bounds__(TB) void k_handle_graft(MeshArgs a) {
-  const uint32_t w = blockIdx.x * (TB / 64) + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (w >= a.N) return;  // wave-uniform
+template <int G>
+__device__ __forceinline__ void row_handle_graft(const MeshArgs& a, uint32_t w) {
+  const int lane = threadIdx.x & (G - 1);
+  const int gbase = (threadIdx.x & 63) & ~(G - 1);
+  (void)gbase;
   const uint64_t b = a.row[w], en = a.row[w + 1];
   const uint32_t deg = (uint32_t)(en - b);
   const uint32_t sw = a.stage[w];
@@ -235,7 +278,7 @@ __global__ __launch_bounds__(TB) void k_handle_graft(MeshArgs a) {
   uint32_t c = 0;
 #pragma unroll
   for (int k = 0; k < HB_PER_LANE; k++) {
-    const uint32_t i = (uint32_t)(k * 64 + lane);
+    const uint32_t i = (uint32_t)(k * G + lane);
     f[k] = 0;
     p[k] = 0;
     r[k] = 0;
@@ -250,28 +293,28 @@ __global__ __launch_bounds__(TB) void k_handle_graft(MeshArgs a) {
                        : a.lat[su * a.S + sw];
       }
     }
-    c += (uint32_t)__popcll(__ballot(((f[k] & F_MESH) && !(p[k] & PR_PRUNE)) || (p[k] & PR_GRAFT)));
+    c += (uint32_t)__popcll(gballot<G>(((f[k] & F_MESH) && !(p[k] & PR_PRUNE)) || (p[k] & PR_GRAFT)));
   }
   const int fpack = (int)(f[0] | (f[1] << 8) | (f[2] << 16) | (f[3] << 24));
   const int ppack = (int)(p[0] | (p[1] << 8) | (p[2] << 16) | (p[3] << 24));
   for (;;) {
     uint64_t bk;
     uint32_t bi;
-    lane_min(lvl, lane, bk, bi);
-    const uint32_t sel = wave_argmin(bk, bi);  // entry (w -> u) of the next GRAFT to arrive
+    lane_min<G>(lvl, lane, bk, bi);
+    const uint32_t sel = group_argmin<G>(bk, bi);  // entry (w -> u) of the next GRAFT to arrive
     if (sel == ~0u) break;
-    const int src = (int)(sel & 63), sh = (int)(8 * (sel >> 6));
+    const int src = gbase + (int)(sel % G), sh = (int)(8 * (sel / G));
     const uint32_t fs = ((uint32_t)__shfl(fpack, src) >> sh) & 0xFFu, ps = ((uint32_t)__shfl(ppack, src) >> sh) & 0xFFu;
     const bool in_mesh = ((fs & F_MESH) && !(ps & PR_PRUNE)) || (ps & PR_GRAFT);
     const uint64_t e = b + sel;
     const uint32_t us = a.until[e];  // every lane, before the owner writes
     const bool rej = !in_mesh && (a.epoch < us || (c >= a.d_hi && !(fs & F_OUT)));
-    if (lane == src) {
-      drop_key(lvl, sel);
+    if ((int)(threadIdx.x & 63) == src) {
+      drop_key<G>(lvl, sel);
       uint32_t rs = 0;
 #pragma unroll
       for (int k = 0; k < HB_PER_LANE; k++)
-        if ((uint32_t)k == (sel >> 6)) rs = r[k];
+        if ((uint32_t)k == (sel / G)) rs = r[k];
       if (rej) a.until[e] = a.epoch + a.bo;  // PRUNE back, both ends back off
       else a.prop[rs] |= PR_ACCEPT;
       if (!in_mesh && !rej) a.flags[e] = (uint8_t)(fs | F_MESH);
@@ -279,18 +322,24 @@ __global__ __launch_bounds__(TB) void k_handle_graft(MeshArgs a) {
     if (!in_mesh && !rej) c++;
   }
 }
+template <int G>
+__global__ __launch_bounds__(TB) void k_handle_graft(MeshArgs a) {
+  const uint32_t w = (blockIdx.x * TB + threadIdx.x) / G;
+  if (w < a.N) row_handle_graft<G>(a, w);  // group-uniform
+}
 
 // Apply the epoch's decisions, one peer per wave (lane per entry). The change
 // flag only has to be non-zero when anything changed (run_mesh's fixed-point
 // test), so every wave with a change stores 1: no atomics.
-__global__ __launch_bounds__(TB) void k_apply(MeshArgs a) {
-  const uint32_t u = blockIdx.x * (TB / 64) + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (u >= a.N) return;  // wave-uniform
+template <int G>
+__device__ __forceinline__ bool row_apply(const MeshArgs& a, uint32_t u) {
+  const int lane = threadIdx.x & (G - 1);
+  const int gbase = (threadIdx.x & 63) & ~(G - 1);
+  (void)gbase;
   const uint64_t b = a.row[u];
   const uint32_t deg = (uint32_t)(a.row[u + 1] - b);
   bool changed = false;
-  for (uint32_t i = (uint32_t)lane; i < deg; i += 64) {
+  for (uint32_t i = (uint32_t)lane; i < deg; i += G) {
     const uint64_t e = b + i;
     const uint8_t p = a.prop[e];
     uint8_t f = a.flags[e];
@@ -303,7 +352,13 @@ __global__ __launch_bounds__(TB) void k_apply(MeshArgs a) {
     if (a.prop[a.rev[e]] & PR_PRUNE) { f &= (uint8_t)~F_MESH; a.until[e] = a.epoch + a.bo; }
     a.flags[e] = f;
   }
-  if (__ballot(changed) && lane == 0) a.counters[C_MESH_CHANGES] = 1;
+  return gballot<G>(changed) != 0;
+}
+template <int G>
+__global__ __launch_bounds__(TB) void k_apply(MeshArgs a) {
+  const uint32_t u = (blockIdx.x * TB + threadIdx.x) / G;
+  if (u >= a.N) return;  // group-uniform
+  if (row_apply<G>(a, u) && (threadIdx.x & (G - 1)) == 0) a.counters[C_MESH_CHANGES] = 1;
 }
 
 // Quiescent epoch: earliest back-off expiry that can wake a hungry peer.
@@ -415,7 +470,214 @@ __global__ __launch_bounds__(TB) void k_gossip_targets(const uint64_t* __restric
   tcnt[u] = (uint8_t)r;
 }
 
+// ---- fused churn epochs (one cooperative launch for a run of epochs) ----
+// The per-epoch kernels above take ~196 us per epoch at 100k peers in 7
+// launches, latency- and launch-bound (the mesh state is Infinity-Cache
+// resident). k_epochs runs epochs [h0, h1] in one persistent cooperative grid
+// with two grid barriers per epoch, because only two steps read other rows:
+//   1  own rows: disconnect, heartbeat decisions (GRAFT/PRUNE proposals)
+//   -- barrier --
+//   2  offline bits of epoch h+1; GRAFT handling (reads the proposers' rows)
+//   -- barrier --
+//   3  own rows: apply (reads the neighbours' PRUNEs), ELL extraction into
+//      the ring slot, IHAVE targets of (u, h)
+// Step 3 of epoch h and step 1 of epoch h+1 touch only their own rows, so
+// they need no barrier between them. Proposals are double-buffered by epoch
+// parity: a wave clears its own row of prop[h & 1] in step 1 of epoch h, when
+// every reader of epoch h-2 is past the barriers of epoch h-1.
+
+// Offline bitset of epoch h into off (grid-strided waves of 64 peers).
+__device__ __forceinline__ void offline_words(uint32_t N, uint64_t seed, uint32_t ppm, uint32_t down, uint64_t h,
+                                              uint64_t* off, uint32_t gw, uint32_t nw) {
+  const int lane = threadIdx.x & 63;
+  for (uint32_t base = gw * 64; base < N; base += nw * 64) {
+    const uint32_t u = base + lane;
+    const uint64_t m = __ballot(u < N && offline_draw(seed, ppm, down, u, h));
+    if (lane == 0) off[base >> 6] = m;
+  }
+}
+
+// ELL row of u from its CSR flags (packed stage<<24 | peer, ascending ids).
+template <int G>
+__device__ __forceinline__ void row_extract(const MeshArgs& a, uint32_t u, uint32_t* mesh) {
+  const int lane = threadIdx.x & (G - 1);
+  const int gbase = (threadIdx.x & 63) & ~(G - 1);
+  (void)gbase;
+  const uint64_t b = a.row[u];
+  const uint32_t deg = (uint32_t)(a.row[u + 1] - b);
+  uint32_t cnt = 0;
+  for (uint32_t i0 = 0; i0 < deg; i0 += G) {
+    const uint32_t i = i0 + (uint32_t)lane;
+    const bool in = i < deg && (a.flags[b + i] & F_MESH);
+    const uint64_t m = gballot<G>(in);
+    const uint32_t pos = cnt + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+    if (in && pos < MESH_W) {
+      const uint32_t w = a.col[b + i];
+      mesh[(size_t)u * MESH_W + pos] = ((uint32_t)a.stage[w] << STAGE_SHIFT) | w;
+    }
+    cnt += (uint32_t)__popcll(m);
+  }
+  if (cnt > MESH_W && lane == 0) atomicOr((unsigned*)&a.counters[C_ERR], ERR_MESH);
+  if ((uint32_t)lane >= cnt && lane < (int)MESH_W) mesh[(size_t)u * MESH_W + lane] = EMPTY;
+}
+
+// IHAVE targets of (u, h) from its CSR flags (= k_gossip_targets: the r
+// smallest (rng(GOSSIP, u, h, w), w) among u's online non-mesh connections).
+template <int G>
+__device__ __forceinline__ void row_targets(const MeshArgs& a, uint32_t u, uint32_t h, uint32_t d_lazy,
+                                            uint32_t gf_milli, uint32_t* tgt, uint8_t* tcnt) {
+  const int lane = threadIdx.x & (G - 1);
+  const int gbase = (threadIdx.x & 63) & ~(G - 1);
+  (void)gbase;
+  if (is_off(a.off, u)) {
+    if (lane == 0) tcnt[u] = 0;
+    return;
+  }
+  const uint64_t b = a.row[u];
+  const uint32_t deg = (uint32_t)(a.row[u + 1] - b);
+  uint64_t key[HB_PER_LANE];
+  uint32_t w[HB_PER_LANE];
+  uint32_t nonmesh = 0;
+#pragma unroll
+  for (int k = 0; k < HB_PER_LANE; k++) {
+    const uint32_t i = (uint32_t)(k * G + lane);
+    key[k] = INF64;
+    w[k] = 0;
+    if (k * G >= (int)deg) continue;  // wave-uniform
+    bool el = false;
+    if (i < deg) {
+      w[k] = a.col[b + i];
+      el = !(a.flags[b + i] & F_MESH) && !is_off(a.off, w[k]);
+      if (el) key[k] = rng(a.seed, P_GOSSIP, u, h, w[k]);
+    }
+    nonmesh += (uint32_t)__popcll(gballot<G>(el));
+  }
+  uint32_t r = (uint32_t)(((uint64_t)nonmesh * gf_milli) / 1000);
+  if (r < d_lazy) r = d_lazy;
+  if (r > nonmesh) r = nonmesh;
+  if (r > GT_W) {
+    if (lane == 0) tcnt[u] = GT_NONE;
+    return;
+  }
+  for (uint32_t q = 0; q < r; q++) {  // ties by entry index = ascending id
+    uint64_t bk;
+    uint32_t bi;
+    lane_min<G>(key, lane, bk, bi);
+    const uint32_t sel = group_argmin<G>(bk, bi);
+    if ((int)(sel % G) == lane) {
+      uint32_t ws = 0;
+#pragma unroll
+      for (int k = 0; k < HB_PER_LANE; k++)
+        if ((uint32_t)k == (sel / G)) ws = w[k];
+      tgt[(size_t)u * GT_W + q] = ws;
+      drop_key<G>(key, sel);
+    }
+  }
+  if (lane == 0) tcnt[u] = (uint8_t)r;
+}
+
+// Grid barrier for the co-resident grid of k_epochs: a monotonic arrival
+// counter (zeroed before the launch), the k-th barrier waits for k * blocks
+// arrivals. Agent-scope release before arriving and acquire after leaving
+// make the other blocks' row updates visible across XCDs. The spin is bounded:
+// a barrier that does not complete (a block that never got a CU) raises
+// ERR_SYNC and lets every wave run to the end of the kernel instead of hanging.
+constexpr uint64_t BARRIER_SPINS = 1ull << 22;  // x ~1 us sleeps
+__device__ __forceinline__ void grid_barrier(uint32_t* bar, uint32_t nblocks, uint32_t& target, uint64_t* counters) {
+  __syncthreads();
+  target += nblocks;
+  if (threadIdx.x == 0) {
+    __threadfence();
+    atomicAdd(bar, 1u);
+    uint64_t spins = 0;
+    uint32_t* err = (uint32_t*)&counters[C_ERR];
+    while (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(8);
+      if ((++spins & 1023) == 0 && (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ERR_SYNC))
+        break;  // another block timed out: run to the end
+      if (spins > BARRIER_SPINS) {
+        atomicOr(err, ERR_SYNC);
+        break;
+      }
+    }
+    __threadfence();
+  }
+  __syncthreads();
+}
+
+// Step C of a churn epoch for one peer per group: apply the epoch's
+// decisions, then (own row only, no barrier needed) the ELL snapshot into the
+// ring slot and the peer's IHAVE targets of epoch h.
+template <int G>
+__global__ __launch_bounds__(TB) void k_apply_snap(MeshArgs a, uint32_t* mesh, uint32_t* tgt, uint8_t* tcnt, uint32_t h,
+                                                   uint32_t d_lazy, uint32_t gf_milli) {
+  const uint32_t u = (blockIdx.x * TB + threadIdx.x) / G;
+  if (u >= a.N) return;  // group-uniform
+  row_apply<G>(a, u);
+  row_extract<G>(a, u, mesh);
+  if (tgt) row_targets<G>(a, u, h, d_lazy, gf_milli, tgt, tcnt);
+}
+
+struct EpochArgs {
+  MeshArgs m;
+  uint32_t* bar;         // grid barrier counter (zeroed before the launch)
+  uint8_t* prop2;        // [2][nnz] proposals by epoch parity
+  uint64_t* off;         // [off_R][w64] offline bitsets, slot h % off_R
+  uint32_t* ring_mesh;   // [ring_R][N][MESH_W] or nullptr (no snapshots)
+  uint32_t* ring_tgt;    // [ring_R][N][GT_W] or nullptr (no lazy gossip)
+  uint8_t* ring_tcnt;
+  uint64_t h0, h1;
+  uint32_t off_R, ring_R, w64, ppm, down, d_lazy, gf_milli;
+};
+
+__global__ __launch_bounds__(TB) void k_epochs(EpochArgs e) {
+  uint32_t target = 0;
+  const uint32_t gw = blockIdx.x * (TB / 64) + (threadIdx.x >> 6), nw = gridDim.x * (TB / 64);
+  const uint32_t N = e.m.N;
+  const uint64_t nnz = e.m.row[N];
+  offline_words(N, e.m.seed, e.ppm, e.down, e.h0, e.off + (size_t)(e.h0 % e.off_R) * e.w64, gw, nw);
+  grid_barrier(e.bar, gridDim.x, target, e.m.counters);
+  for (uint64_t h = e.h0; h <= e.h1; h++) {  // every wave runs every epoch: the barriers are grid-uniform
+    MeshArgs a = e.m;
+    a.epoch = (uint32_t)h;
+    a.off = e.off + (size_t)(h % e.off_R) * e.w64;
+    a.prop = e.prop2 + (size_t)(h & 1) * nnz;
+    for (uint32_t u = gw; u < N; u += nw) {
+      const uint64_t b = a.row[u], en = a.row[u + 1];
+      for (uint64_t x = b + (threadIdx.x & 63); x < en; x += 64) a.prop[x] = 0;
+      row_disconnect<64>(a, u);
+      row_heartbeat<64>(a, u);
+    }
+    grid_barrier(e.bar, gridDim.x, target, e.m.counters);
+    if (h < e.h1)
+      offline_words(N, e.m.seed, e.ppm, e.down, h + 1, e.off + (size_t)((h + 1) % e.off_R) * e.w64, gw, nw);
+    for (uint32_t u = gw; u < N; u += nw) row_handle_graft<64>(a, u);
+    grid_barrier(e.bar, gridDim.x, target, e.m.counters);
+    const size_t slot = (size_t)(h % (e.ring_R ? e.ring_R : 1));
+    for (uint32_t u = gw; u < N; u += nw) {
+      row_apply<64>(a, u);
+      if (e.ring_mesh) row_extract<64>(a, u, e.ring_mesh + slot * N * MESH_W);
+      if (e.ring_tgt)
+        row_targets<64>(a, u, (uint32_t)h, e.d_lazy, e.gf_milli, e.ring_tgt + slot * N * GT_W, e.ring_tcnt + slot * N);
+    }
+  }
+}
+
 inline unsigned blocks(uint64_t n) { return (unsigned)((n + TB - 1) / TB); }
+
+// Lanes per peer of the row kernels: 16 (four peers per wave) when every row
+// fits 4 x 16 entries, else 64 (GS_ROW_GROUP=64 forces one peer per wave).
+inline uint32_t row_group(const Ctx& c) {
+  static const char* e = getenv("GS_ROW_GROUP");
+  if (e && atoi(e) == 64) return 64u;
+  return c.max_degree <= 4 * 16 ? 16u : 64u;
+}
+inline unsigned row_blocks(uint32_t N, uint32_t G) { return (unsigned)(((uint64_t)N * G + TB - 1) / TB); }
+#define GS_ROWS(kernel, G, N, s, ...)                                                   \
+  do {                                                                                   \
+    if ((G) == 16) kernel<16><<<row_blocks(N, 16), TB, 0, s>>>(__VA_ARGS__);            \
+    else kernel<64><<<row_blocks(N, 64), TB, 0, s>>>(__VA_ARGS__);                      \
+  } while (0)
 
 // Targets of the snapshot in ring slot `slot` (epoch h), when lazy gossip is on.
 void ring_targets(Ctx& c, uint64_t h, size_t slot) {
@@ -431,7 +693,7 @@ void ring_targets(Ctx& c, uint64_t h, size_t slot) {
 MeshArgs mesh_args(Ctx& c) {
   const uint32_t N = c.cfg.peers;
   c.d_until.alloc(c.nnz ? c.nnz : 1);
-  c.d_prop.alloc(c.nnz ? c.nnz : 1);
+  c.d_prop.alloc(2 * (c.nnz ? c.nnz : 1));  // two epoch parities (k_epochs); the per-epoch kernels use the first
   c.d_lat32.alloc((size_t)c.S * c.S);
   std::vector<uint32_t> lat32(c.lat_ns.begin(), c.lat_ns.end());
   GS_HIP(hipMemcpyAsync(c.d_lat32.p, lat32.data(), lat32.size() * 4, hipMemcpyHostToDevice, c.stream));
@@ -455,26 +717,97 @@ void sub_epoch(Ctx& c, MeshArgs a) {
   a.epoch = 0;
   a.off = nullptr;
   GS_HIP(hipMemsetAsync(c.d_prop.p, 0, c.nnz ? c.nnz : 1, s));
-  k_heartbeat<<<(N + TB / 64 - 1) / (TB / 64), TB, 0, s>>>(a);
-  k_handle_graft<<<(N + TB / 64 - 1) / (TB / 64), TB, 0, s>>>(a);
-  k_apply<<<(N + TB / 64 - 1) / (TB / 64), TB, 0, s>>>(a);
+  const uint32_t G = row_group(c);
+  GS_ROWS(k_heartbeat, G, N, s, a);
+  GS_ROWS(k_handle_graft, G, N, s, a);
+  GS_ROWS(k_apply, G, N, s, a);
   GS_HIP(hipGetLastError());
 }
 
 // One heartbeat epoch h >= 1 under churn: the offline set into `off`, the
-// disconnects, then A/B/C as without churn.
-void churn_epoch(Ctx& c, MeshArgs& a, uint64_t h, uint64_t* off) {
+// disconnects and heartbeat decisions, GRAFT handling, then apply + the ELL
+// snapshot (+ IHAVE targets) into `mesh` / `tgt` (mesh nullptr: the mesh
+// state only, as in gs_mesh_converge).
+void churn_epoch(Ctx& c, MeshArgs& a, uint64_t h, uint64_t* off, uint32_t* mesh, uint32_t* tgt, uint8_t* tcnt) {
   const uint32_t N = c.cfg.peers;
   hipStream_t s = c.stream;
   k_offline<<<blocks(N), TB, 0, s>>>(N, c.cfg.seed, c.cfg.churn_ppm, c.cfg.churn_down, h, off);
   a.off = off;
   a.epoch = (uint32_t)h;
   GS_HIP(hipMemsetAsync(c.d_prop.p, 0, c.nnz ? c.nnz : 1, s));
-  k_disconnect<<<(N + TB / 64 - 1) / (TB / 64), TB, 0, s>>>(a);
-  k_heartbeat<<<(N + TB / 64 - 1) / (TB / 64), TB, 0, s>>>(a);
-  k_handle_graft<<<(N + TB / 64 - 1) / (TB / 64), TB, 0, s>>>(a);
-  k_apply<<<(N + TB / 64 - 1) / (TB / 64), TB, 0, s>>>(a);
+  const uint32_t G = row_group(c);
+  GS_ROWS(k_disc_heartbeat, G, N, s, a);
+  GS_ROWS(k_handle_graft, G, N, s, a);
+  if (mesh) GS_ROWS(k_apply_snap, G, N, s, a, mesh, tgt, tcnt, (uint32_t)h, c.cfg.d_lazy, c.cfg.gossip_factor_milli);
+  else GS_ROWS(k_apply, G, N, s, a);
   GS_HIP(hipGetLastError());
+}
+
+// Churn epochs [h0, h1] from the current mesh state: the fused cooperative
+// kernel (k_epochs), or the per-epoch launches when GS_MESH_FUSED=0 or the
+// device cannot launch cooperatively. off: bitsets in slots h % off_R; `ring`:
+// also the ELL snapshots (+ IHAVE targets) into the ring slots h % ring_R.
+void run_epochs(Ctx& c, MeshArgs a, uint64_t h0, uint64_t h1, uint64_t* off, uint32_t off_R, bool ring) {
+  const uint32_t N = c.cfg.peers;
+  const size_t w64 = ((size_t)N + 63) / 64;
+  hipStream_t s = c.stream;
+  const char* fe = getenv("GS_MESH_FUSED");
+  int coop = 0;
+  (void)hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, c.cfg.device);
+  if (!(fe && *fe == '1') || !coop) {
+    const bool tg = ring && c.cfg.lazy_gossip && c.d_ring_tcnt.p;
+    for (uint64_t h = h0; h <= h1; h++) {
+      const size_t slot = (size_t)(h % (ring ? c.ring_R : off_R));
+      churn_epoch(c, a, h, off + (size_t)(h % off_R) * w64, ring ? c.d_ring_mesh.p + slot * N * MESH_W : nullptr,
+                  tg ? c.d_ring_tgt.p + slot * N * GT_W : nullptr, tg ? c.d_ring_tcnt.p + slot * N : nullptr);
+    }
+    GS_HIP(hipGetLastError());
+    return;
+  }
+  EpochArgs e{};
+  e.m = a;
+  e.m.sub = 0;
+  e.prop2 = c.d_prop.p;
+  e.off = off;
+  e.off_R = off_R;
+  e.w64 = (uint32_t)w64;
+  e.ppm = c.cfg.churn_ppm;
+  e.down = c.cfg.churn_down;
+  e.h0 = h0;
+  e.h1 = h1;
+  if (ring) {
+    e.ring_R = c.ring_R;
+    e.ring_mesh = c.d_ring_mesh.p;
+    if (c.cfg.lazy_gossip && c.d_ring_tcnt.p) {
+      e.ring_tgt = c.d_ring_tgt.p;
+      e.ring_tcnt = c.d_ring_tcnt.p;
+      e.d_lazy = c.cfg.d_lazy;
+      e.gf_milli = c.cfg.gossip_factor_milli;
+    }
+  }
+  int per_cu = 0;
+  GS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_epochs, TB, 0));
+  if (c.num_cus == 0) {
+    hipDeviceProp_t prop;
+    c.num_cus = hipGetDeviceProperties(&prop, c.cfg.device) == hipSuccess ? prop.multiProcessorCount : 256;
+  }
+  // co-resident blocks only (the grid barrier needs every block running): at
+  // most 2 per CU, well inside the occupancy limit; more waves than rows would
+  // only spin at the barriers
+  const uint64_t need = ((uint64_t)N + TB / 64 - 1) / (TB / 64);
+  const char* bpc = getenv("GS_EPOCH_BLOCKS_PER_CU");
+  const int want = bpc && *bpc ? atoi(bpc) : per_cu;
+  const unsigned grid = (unsigned)std::max<uint64_t>(
+      1, std::min<uint64_t>((uint64_t)std::min(std::max(per_cu, 1), std::max(want, 1)) * c.num_cus, need));
+  c.d_bar.alloc(1);
+  GS_HIP(hipMemsetAsync(c.d_bar.p, 0, 4, s));
+  e.bar = c.d_bar.p;
+  void* args[] = {&e};
+  GS_HIP(hipLaunchCooperativeKernel((const void*)k_epochs, dim3(grid), dim3(TB), args, 0, s));
+  GS_HIP(hipGetLastError());
+  GS_HIP(hipMemcpyAsync(c.h_pinned, c.d_counters.p + C_ERR, 8, hipMemcpyDeviceToHost, s));
+  GS_HIP(hipStreamSynchronize(s));
+  if (c.h_pinned[0] & ERR_SYNC) c.fail(GS_EDEVICE, "k_epochs grid barrier timed out (blocks not co-resident)");
 }
 
 }  // namespace
@@ -503,13 +836,8 @@ void churn_ring(Ctx& c, uint64_t h_lo, uint64_t h_hi) {
       c.ring_lo = 0;
     }
   }
-  for (uint64_t h = c.churn_state + 1; h <= h_hi; h++) {
-    const size_t slot = (size_t)(h % R);
-    uint64_t* off = c.d_ring_off.p + slot * w64;
-    churn_epoch(c, a, h, off);
-    k_extract<<<blocks(N), TB, 0, s>>>(a, c.d_ring_mesh.p + slot * N * MESH_W, nullptr);
-    ring_targets(c, h, slot);
-  }
+  if (c.churn_state + 1 <= h_hi)
+    run_epochs(c, a, c.churn_state + 1, h_hi, c.d_ring_off.p, R, true);
   GS_HIP(hipGetLastError());
   if (h_hi > c.churn_state) {
     c.churn_state = h_hi;
@@ -531,8 +859,8 @@ uint32_t run_mesh(Ctx& c, uint32_t max_hb) {
   uint32_t epoch = 1, last = 0;
   uint64_t* h = c.h_pinned;
   if (c.cfg.churn_ppm) {  // no fixed point under churn: exactly max_hb epochs
-    c.d_off.alloc(((size_t)N + 63) / 64);
-    for (; epoch <= max_hb; epoch++) churn_epoch(c, a, epoch, c.d_off.p);
+    c.d_off.alloc(2 * (((size_t)N + 63) / 64));
+    if (max_hb >= 1) run_epochs(c, a, 1, max_hb, c.d_off.p, 2, false);
     last = max_hb;
     c.churn_state = max_hb;  // the ring restarts after this state
     c.ring_lo = (uint64_t)max_hb + 1;
@@ -543,9 +871,10 @@ uint32_t run_mesh(Ctx& c, uint32_t max_hb) {
     a.epoch = epoch;
     GS_HIP(hipMemsetAsync(c.d_prop.p, 0, c.nnz ? c.nnz : 1, s));
     GS_HIP(hipMemsetAsync(c.d_counters.p + C_MESH_CHANGES, 0, 8, s));
-    k_heartbeat<<<(N + TB / 64 - 1) / (TB / 64), TB, 0, s>>>(a);
-    k_handle_graft<<<(N + TB / 64 - 1) / (TB / 64), TB, 0, s>>>(a);
-    k_apply<<<(N + TB / 64 - 1) / (TB / 64), TB, 0, s>>>(a);
+    const uint32_t G = row_group(c);
+    GS_ROWS(k_heartbeat, G, N, s, a);
+    GS_ROWS(k_handle_graft, G, N, s, a);
+    GS_ROWS(k_apply, G, N, s, a);
     GS_HIP(hipGetLastError());
     GS_HIP(hipMemcpyAsync(h, c.d_counters.p + C_MESH_CHANGES, 8, hipMemcpyDeviceToHost, s));
     GS_HIP(hipStreamSynchronize(s));

@@ -857,7 +857,10 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
   if (c.traffic && churn) c.fail(GS_EUNSUPPORTED, "per-peer traffic covers a frozen mesh: turn off churn");
   const bool pull_any = (variant & 32) && !idw_any && !churn;
   // the push path with gossip or churn runs split, without tile skip
-  const uint32_t pvariant = (gossip || churn) ? ((variant | 8u) & ~2u & ~32u) : (variant & ~32u);
+  // the push path with gossip or churn runs split + tile skip (its long tail of
+  // IHAVE and churn buckets touches few tiles); GS_RELAX_VARIANT can turn the skip off
+  const uint32_t pvariant = (gossip || churn) ? (((variant | 8u) & ~32u) | (var_env && *var_env ? 0u : 2u))
+                                              : (variant & ~32u);
   if (churn && !lanes32) c.fail(GS_EUNSUPPORTED, "churn needs peers*batch*FP < 2^32");
   std::vector<uint64_t> q0v(Bmax), r0v(Bmax), ep(churn ? n_msgs : 0);
   if (churn) {  // epoch of every publish; the snapshot ring
@@ -971,6 +974,12 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
         c.d_touched.alloc(max_tiles);
         GS_HIP(hipMemsetAsync(c.d_tmin.p, 0, (total + 63) / 64 * 8, s));
         GS_HIP(hipMemsetAsync(c.d_touched.p, 0, (total + 63) / 64, s));
+        if (with_gossip) {
+          c.d_tgmin.alloc(max_tiles);
+          c.d_tnf.alloc(max_tiles);
+          c.d_tstamp.alloc(max_tiles);
+          GS_HIP(hipMemsetAsync(c.d_tstamp.p, 0, (total + 63) / 64 * 4, s));
+        }
       }
       GS_HIP(hipMemsetAsync(c.d_ctrl.p, 0xFF, 4 * 8, s));
       // with gossip the first bucket is [0, Delta): the publisher's own IHAVEs
@@ -997,7 +1006,10 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       const unsigned grid = (unsigned)std::min<uint64_t>(need, (uint64_t)dev_cus * split_blocks_per_cu(c));
       if (v & 8) {  // frontier segments: one per scan wave
         const uint64_t nwaves = (uint64_t)grid * (TB / 64), ntiles = (total + 63) / 64;
-        ra.seg_cap = (uint32_t)(((ntiles + nwaves - 1) / nwaves) * (64 / FP));
+        // tiles one scan wave can visit: groups of 64 with tile skip (k_scan), single tiles without
+        const uint64_t gt = (v & 2) ? 64 : 1;
+        const uint64_t wave_tiles = ((ntiles + gt - 1) / gt + nwaves - 1) / nwaves * gt;
+        ra.seg_cap = (uint32_t)(wave_tiles * (64 / FP));
         c.d_fr_idx.alloc(nwaves * ra.seg_cap);
         if (FP == 1) c.d_fr_key.alloc(nwaves * ra.seg_cap);
         c.d_fr_cnt.alloc(nwaves);
@@ -1005,7 +1017,7 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
         ra.fr_key = c.d_fr_key.p;
         ra.fr_cnt = c.d_fr_cnt.p;
         if (with_gossip) {  // gossip list: per-lane entries, one segment per scan wave
-          ra.gl_cap = (uint32_t)(((ntiles + nwaves - 1) / nwaves) * 64);
+          ra.gl_cap = (uint32_t)(wave_tiles * 64);
           c.d_gl_idx.alloc(nwaves * ra.gl_cap);
           c.d_gl_cnt.alloc(nwaves);
           c.d_nonfinal.alloc(3);
@@ -1020,6 +1032,11 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
           ra.hb_ns = c.cfg.heartbeat_ns;
           ra.seed = c.cfg.seed;
           ra.gossip = 1;
+          if ((v & 10) == 10) {
+            ra.tgmin = c.d_tgmin.p;
+            ra.tnf = c.d_tnf.p;
+            ra.tstamp = c.d_tstamp.p;
+          }
           if (churn) {
             ra.ring_tgt = c.d_ring_tgt.p;
             ra.ring_tcnt = c.d_ring_tcnt.p;

@@ -18,7 +18,9 @@
 //
 // Option bits (all exact):
 //   1 FILTER  read the target key first, atomicMin only when smaller
-//   2 SKIP    per-tile {min pending key, scan stamp, push stamp} (fused only)
+//   2 SKIP    per-tile {min pending key, scan stamp, push stamp} (fused); split:
+//             per-tile min pending key + touched flag (+ next IHAVE arrival,
+//             non-final count and scan stamp with lazy gossip)
 //   4 FB      final bitset, 1 bit per key (N*L/8 bytes, L2/MALL resident),
 //             written by the scanner; a push to a final target is dropped (a
 //             final key cannot improve: every push lands >= the bucket end)
@@ -40,6 +42,9 @@ struct RelaxArgs {
   uint32_t* fr_cnt;   // frontier: items per wave segment
   uint64_t* tmin;     // split SKIP: min pending key per tile at its last scan
   uint8_t* touched;   // split SKIP: tile received a push since its last scan
+  uint64_t* tgmin;    // split SKIP + gossip: next IHAVE arrival time of the tile's lanes (INF none)
+  uint32_t* tnf;      // split SKIP + gossip: non-final lanes of the tile at its last scan
+  uint32_t* tstamp;   // split SKIP + gossip: launch + 1 of the tile's last scan (k_gossip's seen filter)
   // lazy gossip
   uint32_t* gl_idx;   // gossip list: lane gid with an IHAVE arrival in this bucket
   uint32_t* gl_cnt;   // per scan wave
@@ -441,17 +446,45 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
   uint64_t nmin = INF64, nonfin = 0;
   uint32_t cnt = 0, gcnt = 0, err = 0;
   const uint64_t hspan = GOSSIP ? (uint64_t)a.hist * a.hb_ns : 0;
-  for (uint64_t tile = uniform64(wave); tile < ntiles; tile += nwaves) {
-    if constexpr (SKIP) {
-      // untouched since its last scan and nothing due in this bucket: the
-      // tile's keys are unchanged, its min pending key stands for it
-      const uint64_t tm = uniform64(a.tmin[tile]);
-      const uint32_t tc = __builtin_amdgcn_readfirstlane((uint32_t)a.touched[tile]);
-      if (!tc && (tm == INF64 || (tm >> a.tshift) >= hi)) {
+  // Tiles are visited per wave in groups: with SKIP a group is 64 consecutive
+  // tiles whose metadata every lane loads at once (one coalesced load each,
+  // instead of a dependent scalar chain per tile), and only the tiles that
+  // cannot be skipped are scanned; without SKIP a group is one tile.
+  constexpr uint64_t GT = SKIP ? 64 : 1;
+  const uint64_t ngroups = (ntiles + GT - 1) / GT;
+  for (uint64_t grp = uniform64(wave); grp < ngroups; grp += nwaves) {
+   uint64_t todo = 1;
+   if constexpr (SKIP) {
+    // untouched since its last scan and nothing due in this bucket: the
+    // tile's keys are unchanged, its min pending key stands for it. With
+    // gossip its final lanes' next IHAVE arrival must lie beyond the bucket
+    // too, and its non-final count stands.
+    const uint64_t mt = grp * GT + lane;
+    bool skip = false;
+    if (mt < ntiles) {
+      const uint64_t tm = a.tmin[mt];
+      skip = !a.touched[mt] && (tm == INF64 || (tm >> a.tshift) >= hi);
+      uint64_t gm = INF64;
+      if constexpr (GOSSIP) {
+        if (skip) gm = a.tgmin[mt];
+        skip = skip && (gm == INF64 || gm >= hi);
+      }
+      if (skip) {
         nmin = tm < nmin ? tm : nmin;
-        continue;
+        if constexpr (GOSSIP) {
+          if (gm != INF64) {
+            const uint64_t gk = gm << a.tshift;
+            nmin = gk < nmin ? gk : nmin;
+          }
+          nonfin += a.tnf[mt];
+        }
       }
     }
+    todo = __ballot(mt < ntiles && !skip);
+   }
+   while (todo) {  // wave-uniform
+    const uint64_t tile = grp * GT + (uint64_t)__builtin_ctzll(todo);
+    todo &= todo - 1;
     const uint64_t gid = (tile << 6) + lane;
     const bool valid = gid < a.total;
     const uint64_t key = valid ? a.keys[gid] : INF64;
@@ -509,6 +542,15 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
       const uint64_t gm = __ballot(gwork);
       if (gwork) a.gl_idx[gseg + gcnt + (uint32_t)__popcll(gm & ((1ull << lane) - 1))] = (uint32_t)gid;
       gcnt += (uint32_t)__popcll(gm);
+      if constexpr (SKIP) {  // the tile's gossip state for later skips
+        const uint64_t tg = wave_min(gnext);
+        const uint32_t nf = (uint32_t)__popcll(__ballot(valid && !fin && slot % FP < a.F));
+        if (lane == 0) {
+          a.tgmin[tile] = tg;
+          a.tnf[tile] = nf;
+          a.tstamp[tile] = a.launch + 1;
+        }
+      }
     }
     const uint64_t am = __ballot(active);
     if (am == 0) continue;
@@ -526,6 +568,7 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
       if (leader) a.fr_idx[seg + cnt + (uint32_t)__popcll(lm & ((1ull << lane) - 1))] = (uint32_t)(gid / FP);
       cnt += (uint32_t)__popcll(lm);
     }
+   }
   }
   if (lane == 0) a.fr_cnt[wave] = cnt;
   nmin = wave_min(nmin);
@@ -594,6 +637,9 @@ __global__ __launch_bounds__(TB) void k_gossip(RelaxArgs a) {
         const uint64_t A = ti + L.lat[sw * S + sv] + ser + L.lat[sv * S + sw] + (sd > ser ? sd - ser : 0);
         if (a.churn && (ev_lost(a, m, ti, w) || ev_lost(a, m, A, w))) return;  // IHAVE or answer lost
         const size_t dst = (size_t)w * LL + slot;
+        // final before this bucket (its tile's final bit from an earlier scan:
+        // key time < that bucket's end <= lo <= t_i): seen, no key read
+        if (a.tstamp && ((a.fbits[dst >> 6] >> (dst & 63)) & 1) && a.tstamp[dst >> 6] != a.launch + 1) return;
         const uint64_t kw = a.keys[dst];
         if (kw != INF64 && (kw >> a.tshift) <= ti) return;  // already seen: no IWANT
         iw++;
@@ -602,6 +648,7 @@ __global__ __launch_bounds__(TB) void k_gossip(RelaxArgs a) {
         const uint64_t nk = (A << a.tshift) | ((uint64_t)(hp + 1) << a.sb) | u;
         if (nk < kw) {
           atomicMin((unsigned long long*)&a.keys[dst], (unsigned long long)nk);
+          if (a.tstamp) a.touched[dst >> 6] = 1;
           nmin = nk < nmin ? nk : nmin;
         }
       };
@@ -731,7 +778,8 @@ __global__ __launch_bounds__(TB) void k_frontier(RelaxArgs a) {
 template <int FP>
 void relax_fp(uint32_t variant, const RelaxArgs& a, unsigned grid, hipStream_t s, hipEvent_t mid) {
   if (variant & 8) {
-    if (a.gossip) k_scan<FP, false, true><<<grid, TB, 0, s>>>(a);
+    if (a.gossip && (variant & 2)) k_scan<FP, true, true><<<grid, TB, 0, s>>>(a);
+    else if (a.gossip) k_scan<FP, false, true><<<grid, TB, 0, s>>>(a);
     else if (variant & 2) k_scan<FP, true, false><<<grid, TB, 0, s>>>(a);
     else k_scan<FP, false, false><<<grid, TB, 0, s>>>(a);
     if (mid) (void)hipEventRecord(mid, s);  // splits scan / frontier time when timing

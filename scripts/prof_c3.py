@@ -20,7 +20,7 @@ sim.set_topogen_links(c["links"][0], *c["links"][1:])
 t0 = time.perf_counter()
 sim.connect_gossipsub_peers()
 sim.mesh_converge(400)
-print("setup %.1f ms" % ((time.perf_counter() - t0) * 1e3))
+print("setup %.1f ms" % ((time.perf_counter() - t0) * 1e3), flush=True)
 sim.run(gossipsim.shard_messages(0, 0, 1, c["batch"], c["peers"], 15000), collect=False)
 sim.reset_stats()
 t0 = time.perf_counter()
