@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--configs", type=int, default=1, help="also time BASELINE configs #1-#3 (1 GPU runs)")
     ap.add_argument("--mode", choices=("msg", "peer"), default="msg",
                     help="msg: message-sharded ranks (default); peer: peer-partitioned ranks")
+    ap.add_argument("--parts", type=int, default=1,
+                    help="--mode peer on one process: this many loop-back parts (1 = an RCCL rank of one)")
     ap.add_argument("--also-peers", type=int, default=100_000,
                     help="second graph size reported beside the headline (metric names 100k & 1M; 0=off)")
     ap.add_argument("--gossip-check", type=int, default=64,
@@ -202,20 +204,31 @@ def make_sim(args, peers, S, links, local):
     sim.set_topogen_links(S, *links)
     sim.connect_gossipsub_peers()
     epochs = sim.mesh_converge(args.max_heartbeats)
+    sim._bench_links = (S, links)
     return sim, epochs, time.perf_counter() - t_setup
 
 
 def measure(args, sim, peers, world, rank, torch, dist):
     """W untimed + K timed steps between barrier+synchronize; -> (max elapsed, stats, sums)."""
+    sims = [sim]
     if args.mode == "peer":
-        import partition
-        exch = partition.DistExchange(device=torch.device("cuda", torch.cuda.current_device())) \
-            if world > 1 else partition.LoopbackExchange()
-        bufs = [partition.RecordBuffer(torch.device("cuda", sim.cfg.c.device), capacity=1 << 22)]
+        # gs_run_partitioned (C ABI): RCCL across ranks (rank 0's unique id
+        # broadcast over torch.distributed), or loop-back parts in this process
+        if world > 1 or args.parts == 1:
+            uid = gossipsim.Comm.get_id() if rank == 0 else None
+            if world > 1:
+                box = [uid]
+                dist.broadcast_object_list(box, src=0)
+                uid = box[0]
+            comm = gossipsim.Comm(nranks=world, rank=rank, uid=uid, device=sim.cfg.c.device)
+        else:
+            comm = gossipsim.Comm(local_parts=args.parts)
+            sims += [make_sim(args, peers, *sim._bench_links, sim.cfg.c.device)[0] for _ in range(args.parts - 1)]
+        sim._bench_comm = comm
 
         def step(i):  # every rank works on the same batch, each over its own peers
-            partition.run_partitioned([sim], gossipsim.shard_messages(i, 0, 1, args.batch, peers, args.msg_size),
-                                      exch, bufs=bufs, collect=False)
+            comm.run_partitioned(sims, gossipsim.shard_messages(i, 0, 1, args.batch, peers, args.msg_size),
+                                 collect=False)
     else:
         def step(i):
             sim.run(gossipsim.shard_messages(i, rank, world, args.batch, peers, args.msg_size),
@@ -223,8 +236,9 @@ def measure(args, sim, peers, world, rank, torch, dist):
 
     for i in range(args.warmup):
         step(i)
-    sim.reset_stats()
-    sim.set_timing(True)
+    for x in sims:
+        x.reset_stats()
+        x.set_timing(True)
     barrier_sync(torch, dist, world)
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -232,7 +246,13 @@ def measure(args, sim, peers, world, rank, torch, dist):
     barrier_sync(torch, dist, world)
     elapsed = time.perf_counter() - t0
     st = sim.stats()
-    sim.set_timing(False)
+    if len(sims) > 1:  # loop-back parts: the job's counters are the parts' sum
+        for x in sims[1:]:
+            sx = x.stats()
+            for k in ("deliveries", "frag_deliveries", "relaxations", "bytes_alg", "relax_bytes_alg"):
+                st[k] += sx[k]
+    for x in sims:
+        x.set_timing(False)
     SUM = dist.ReduceOp.SUM if dist is not None else None
     MAX = dist.ReduceOp.MAX if dist is not None else None
     (max_elapsed,) = allreduce(torch, dist, world, [elapsed], MAX)
@@ -285,8 +305,6 @@ def main():
     S, bl, bh, ll, lh = [int(x) for x in args.links.split(",")]
     links = (bl, bh, ll, lh)
     sim, epochs, t_setup = make_sim(args, args.peers, S, links, local)
-    if args.mode == "peer":
-        sim.set_partition(world, rank)
     steps = measure(args, sim, args.peers, world, rank, torch, dist)
     max_elapsed, st, tot = steps
     deliveries = tot[0]
@@ -356,7 +374,10 @@ def main():
                             % (args.peers, S, bl, bh, ll, lh, args.fragments, args.msg_size, args.batch,
                                "/GPU, message-sharded" if args.mode == "msg" else ", peer-partitioned"),
                 "peers": args.peers, "batch": args.batch, "fragments": args.fragments,
-                "msg_size": args.msg_size, "links": args.links, "parallelism": ("msg-shard%d" if args.mode == "msg" else "peer-part%d") % world,
+                "msg_size": args.msg_size, "links": args.links,
+                "parallelism": "msg-shard%d" % world if args.mode == "msg" else
+                ("peer-part%d (RCCL ranks)" % world if world > 1 or args.parts == 1 else
+                 "peer-part%d (loop-back parts on one GPU)" % args.parts),
             },
             "deliveries": int(deliveries),
             "frag_deliveries": int(tot[1]),

@@ -1,0 +1,345 @@
+// gs_comm.hip — multi-GPU communicator and the library-driven peer-partitioned
+// run (include/gossipsim.h gs_comm_*, gs_run_partitioned).
+//
+// The reference scales by running one process per peer (Shadow / K8s pods,
+// rust-test-node/src/main.rs:466-477 drives one swarm task per process); here
+// one process drives one GPU, and the only data that crosses GPUs is a
+// bucket's arrival records. Per bucket, every part
+//   1. scans its own keys and counts its records per destination part (a
+//      record goes only to the parts owning one of its forward targets),
+//   2. all-gathers the count vectors (RCCL) — the one host read per bucket,
+//   3. exports its records grouped by destination and exchanges them with
+//      grouped send/recv (all-to-all-v),
+//   4. relaxes the received records into its own peers and MIN-all-reduces
+//      the next bucket key on the device (ncclUint64 / ncclMin).
+// Two backends: RCCL over xGMI (one rank per process and GPU), and an
+// in-process loopback for several parts driven by one thread (device copies),
+// which the tests use to run P parts on one GPU.
+#include <dlfcn.h>
+#include <string.h>
+#include <rccl/rccl.h>  // types and enums only: the functions are resolved with dlsym
+
+#include <algorithm>
+#include <new>
+#include <vector>
+
+#include "gs_internal.h"
+
+struct gs_ctx : gs::Ctx {};
+
+namespace gs {
+namespace {
+
+// RCCL entry points, loaded on first use so that libgossipsim loads (and
+// single-GPU runs work) where no RCCL is installed.
+struct Rccl {
+  void* h = nullptr;
+  ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*GroupStart)() = nullptr;
+  ncclResult_t (*GroupEnd)() = nullptr;
+  const char* (*ErrorString)(ncclResult_t) = nullptr;
+};
+
+Rccl* rccl() {
+  static Rccl r;
+  static bool tried = false;
+  if (!tried) {
+    tried = true;
+    const char* names[] = {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"};
+    for (const char* n : names)
+      if ((r.h = dlopen(n, RTLD_NOW | RTLD_LOCAL))) break;
+    if (r.h) {
+#define GS_SYM(f, name) r.f = (decltype(r.f))dlsym(r.h, name)
+      GS_SYM(GetUniqueId, "ncclGetUniqueId");
+      GS_SYM(CommInitRank, "ncclCommInitRank");
+      GS_SYM(CommDestroy, "ncclCommDestroy");
+      GS_SYM(AllReduce, "ncclAllReduce");
+      GS_SYM(AllGather, "ncclAllGather");
+      GS_SYM(Send, "ncclSend");
+      GS_SYM(Recv, "ncclRecv");
+      GS_SYM(GroupStart, "ncclGroupStart");
+      GS_SYM(GroupEnd, "ncclGroupEnd");
+      GS_SYM(ErrorString, "ncclGetErrorString");
+#undef GS_SYM
+      if (!r.GetUniqueId || !r.CommInitRank || !r.CommDestroy || !r.AllReduce || !r.AllGather || !r.Send ||
+          !r.Recv || !r.GroupStart || !r.GroupEnd || !r.ErrorString) {
+        dlclose(r.h);
+        r.h = nullptr;
+      }
+    }
+  }
+  return r.h ? &r : nullptr;
+}
+
+#define GS_NCCL(call)                                                                               \
+  do {                                                                                              \
+    ncclResult_t r_ = (call);                                                                       \
+    if (r_ != ncclSuccess) throw gs::Error(GS_EDEVICE, std::string(#call) + ": " + rccl()->ErrorString(r_)); \
+  } while (0)
+
+}  // namespace
+}  // namespace gs
+
+using namespace gs;
+
+struct gs_comm {
+  uint32_t local = 0;    // 1: in-process parts, 0: RCCL
+  uint32_t nranks = 1, rank = 0;
+  int32_t device = 0;
+  ncclComm_t nc = nullptr;
+  uint64_t* d_scratch = nullptr;  // RCCL: [parts * parts] count matrix + 1 flag word
+};
+
+extern "C" gs_status gs_comm_get_id(gs_comm_id* out) {
+  static_assert(sizeof(gs_comm_id) == sizeof(ncclUniqueId), "gs_comm_id must hold an ncclUniqueId");
+  if (!out) return GS_EINVAL;
+  Rccl* r = rccl();
+  if (!r) return GS_EUNSUPPORTED;
+  ncclUniqueId id;
+  if (r->GetUniqueId(&id) != ncclSuccess) return GS_EDEVICE;
+  memcpy(out, &id, sizeof id);
+  return GS_OK;
+}
+
+extern "C" gs_status gs_comm_init(uint32_t nranks, uint32_t rank, const gs_comm_id* id, int32_t device,
+                                  gs_comm** out) {
+  if (!out || !id || nranks < 1 || nranks > 64 || rank >= nranks) return GS_EINVAL;
+  *out = nullptr;
+  Rccl* r = rccl();
+  if (!r) return GS_EUNSUPPORTED;
+  if (hipSetDevice(device) != hipSuccess) return GS_EDEVICE;
+  gs_comm* c = new (std::nothrow) gs_comm();
+  if (!c) return GS_ENOMEM;
+  c->nranks = nranks;
+  c->rank = rank;
+  c->device = device;
+  ncclUniqueId nid;
+  memcpy(&nid, id, sizeof nid);
+  if (r->CommInitRank(&c->nc, (int)nranks, nid, (int)rank) != ncclSuccess ||
+      hipMalloc((void**)&c->d_scratch, ((size_t)nranks * nranks + 1) * 8) != hipSuccess) {
+    if (c->nc) r->CommDestroy(c->nc);
+    delete c;
+    return GS_EDEVICE;
+  }
+  *out = c;
+  return GS_OK;
+}
+
+extern "C" gs_status gs_comm_init_local(uint32_t nparts, gs_comm** out) {
+  if (!out || nparts < 1 || nparts > 64) return GS_EINVAL;
+  gs_comm* c = new (std::nothrow) gs_comm();
+  if (!c) return GS_ENOMEM;
+  c->local = 1;
+  c->nranks = nparts;
+  *out = c;
+  return GS_OK;
+}
+
+extern "C" gs_status gs_comm_destroy(gs_comm* c) {
+  if (!c) return GS_EINVAL;
+  if (c->nc) {
+    (void)hipSetDevice(c->device);
+    rccl()->CommDestroy(c->nc);
+  }
+  if (c->d_scratch) (void)hipFree(c->d_scratch);
+  delete c;
+  return GS_OK;
+}
+
+namespace {
+
+// One batch of the partitioned protocol over this process's parts.
+void run_batch(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched, uint64_t i0, uint32_t B,
+               const gs_result_sink* sinks) {
+  const uint32_t P = cm->nranks;
+  Rccl* r = cm->local ? nullptr : rccl();
+  std::vector<uint64_t> key0(nctx);
+  for (uint32_t i = 0; i < nctx; i++) {
+    GS_HIP(hipSetDevice(cx[i]->cfg.device));
+    key0[i] = part_begin(*cx[i], sched + i0, B);  // the seeded min is also left in ctrl[0]
+  }
+  // mat[s * P + d] = records part s sends to part d (this bucket)
+  std::vector<uint64_t> mat((size_t)P * P), ctl(nctx);
+  auto host_min_to_ctrl = [&](uint64_t k) {
+    for (uint32_t i = 0; i < nctx; i++) {
+      GS_HIP(hipSetDevice(cx[i]->cfg.device));
+      cx[i]->h_pinned[0] = k;
+      GS_HIP(hipMemcpyAsync(cx[i]->d_ctrl.p, cx[i]->h_pinned, 8, hipMemcpyHostToDevice, cx[i]->stream));
+      GS_HIP(hipStreamSynchronize(cx[i]->stream));
+    }
+  };
+  if (cm->local) host_min_to_ctrl(*std::min_element(key0.begin(), key0.end()));
+  else GS_NCCL(r->AllReduce(cx[0]->d_ctrl.p, cx[0]->d_ctrl.p, 1, ncclUint64, ncclMin, cm->nc, cx[0]->stream));
+  for (;;) {
+    // 1. scan + per-destination counts
+    for (uint32_t i = 0; i < nctx; i++) {
+      GS_HIP(hipSetDevice(cx[i]->cfg.device));
+      part_dev_bucket(*cx[i], P);
+      part_dev_scan_count(*cx[i], P);
+    }
+    // 2. the count matrix and the bucket key on the host (the one read per bucket)
+    uint64_t key = INF64;
+    if (cm->local) {
+      for (uint32_t i = 0; i < nctx; i++) {
+        GS_HIP(hipSetDevice(cx[i]->cfg.device));
+        GS_HIP(hipMemcpyAsync(&mat[(size_t)i * P], cx[i]->d_dcnt.p, P * 8, hipMemcpyDeviceToHost, cx[i]->stream));
+        GS_HIP(hipMemcpyAsync(&ctl[i], cx[i]->d_ctrl.p, 8, hipMemcpyDeviceToHost, cx[i]->stream));
+      }
+      for (uint32_t i = 0; i < nctx; i++) GS_HIP(hipStreamSynchronize(cx[i]->stream));
+      key = ctl[0];
+    } else {
+      Ctx& c = *cx[0];
+      GS_NCCL(r->AllGather(c.d_dcnt.p, cm->d_scratch, P, ncclUint64, cm->nc, c.stream));
+      GS_HIP(hipMemcpyAsync(mat.data(), cm->d_scratch, (size_t)P * P * 8, hipMemcpyDeviceToHost, c.stream));
+      GS_HIP(hipMemcpyAsync(&ctl[0], c.d_ctrl.p, 8, hipMemcpyDeviceToHost, c.stream));
+      GS_HIP(hipStreamSynchronize(c.stream));
+      key = ctl[0];
+    }
+    if (key == INF64) break;  // every part agrees: the MIN all-reduce made it the same everywhere
+    // 3. export grouped by destination, exchange (all-to-all-v)
+    std::vector<uint64_t> nrecv(nctx, 0);
+    for (uint32_t i = 0; i < nctx; i++) {
+      Ctx& c = *cx[i];
+      const uint32_t me = cm->local ? i : cm->rank;
+      uint64_t ns = 0, nr = 0;
+      for (uint32_t d = 0; d < P; d++) ns += mat[(size_t)me * P + d];
+      for (uint32_t s = 0; s < P; s++) nr += mat[(size_t)s * P + me];
+      nrecv[i] = nr;
+      GS_HIP(hipSetDevice(c.cfg.device));
+      c.d_pout.alloc(std::max<uint64_t>(ns, 1));
+      c.d_pin.alloc(std::max<uint64_t>(nr, 1));
+      part_dev_export(c, P, c.d_pout.p);
+    }
+    const size_t RB = sizeof(gs_part_record);
+    if (cm->local) {
+      for (uint32_t i = 0; i < nctx; i++) GS_HIP(hipStreamSynchronize(cx[i]->stream));  // every export done
+      for (uint32_t i = 0; i < nctx; i++) {  // part i receives from every s, in source order
+        GS_HIP(hipSetDevice(cx[i]->cfg.device));
+        uint64_t roff = 0;
+        for (uint32_t s = 0; s < nctx; s++) {
+          uint64_t soff = 0;
+          for (uint32_t d = 0; d < i; d++) soff += mat[(size_t)s * P + d];
+          const uint64_t n = mat[(size_t)s * P + i];
+          if (n)
+            GS_HIP(hipMemcpyAsync(cx[i]->d_pin.p + roff, cx[s]->d_pout.p + soff, n * RB, hipMemcpyDeviceToDevice,
+                                  cx[i]->stream));
+          roff += n;
+        }
+      }
+    } else {
+      Ctx& c = *cx[0];
+      const uint32_t me = cm->rank;
+      // peak buckets at 1M peers move GBs per pair: point-to-point transfers in
+      // pieces of at most 2^30 bytes (RCCL's p2p path mishandles single
+      // transfers past 2^31 bytes); both ends cut the same count the same way
+      const uint64_t piece = (1ull << 30) / RB;
+      GS_NCCL(r->GroupStart());
+      uint64_t soff = 0, roff = 0;
+      for (uint32_t d = 0; d < P; d++) {
+        const uint64_t n = mat[(size_t)me * P + d];
+        for (uint64_t k = 0; k < n; k += piece)
+          GS_NCCL(r->Send(c.d_pout.p + soff + k, std::min(piece, n - k) * RB, ncclUint8, (int)d, cm->nc, c.stream));
+        soff += n;
+      }
+      for (uint32_t s = 0; s < P; s++) {
+        const uint64_t n = mat[(size_t)s * P + me];
+        for (uint64_t k = 0; k < n; k += piece)
+          GS_NCCL(r->Recv(c.d_pin.p + roff + k, std::min(piece, n - k) * RB, ncclUint8, (int)s, cm->nc, c.stream));
+        roff += n;
+      }
+      GS_NCCL(r->GroupEnd());
+    }
+    // 4. relax into own peers; next bucket = MIN over parts
+    for (uint32_t i = 0; i < nctx; i++) {
+      GS_HIP(hipSetDevice(cx[i]->cfg.device));
+      part_dev_relax_next(*cx[i], cx[i]->d_pin.p, nrecv[i]);
+    }
+    if (cm->local) {
+      for (uint32_t i = 0; i < nctx; i++) {
+        GS_HIP(hipSetDevice(cx[i]->cfg.device));
+        GS_HIP(hipMemcpyAsync(&ctl[i], cx[i]->d_ctrl.p, 8, hipMemcpyDeviceToHost, cx[i]->stream));
+      }
+      for (uint32_t i = 0; i < nctx; i++) GS_HIP(hipStreamSynchronize(cx[i]->stream));
+      host_min_to_ctrl(*std::min_element(ctl.begin(), ctl.end()));
+    } else {
+      GS_NCCL(r->AllReduce(cx[0]->d_ctrl.p, cx[0]->d_ctrl.p, 1, ncclUint64, ncclMin, cm->nc, cx[0]->stream));
+    }
+  }
+  // lazy gossip: the eager result stands only where every part proves it a no-op
+  bool ok = true;
+  for (uint32_t i = 0; i < nctx; i++) {
+    GS_HIP(hipSetDevice(cx[i]->cfg.device));
+    ok = part_dev_complete(*cx[i], sinks && sinks[i].summary) && ok;
+  }
+  if (!cm->local && cx[0]->cfg.lazy_gossip) {
+    Ctx& c = *cx[0];
+    c.h_pinned[0] = ok ? 1 : 0;
+    GS_HIP(hipMemcpyAsync(cm->d_scratch + (size_t)P * P, c.h_pinned, 8, hipMemcpyHostToDevice, c.stream));
+    GS_NCCL(r->AllReduce(cm->d_scratch + (size_t)P * P, cm->d_scratch + (size_t)P * P, 1, ncclUint64, ncclMin, cm->nc,
+                         c.stream));
+    GS_HIP(hipMemcpyAsync(c.h_pinned, cm->d_scratch + (size_t)P * P, 8, hipMemcpyDeviceToHost, c.stream));
+    GS_HIP(hipStreamSynchronize(c.stream));
+    ok = c.h_pinned[0] != 0;
+  }
+  if (!ok) {
+    std::string why;
+    for (uint32_t i = 0; i < nctx; i++) {
+      part_abort(*cx[i]);
+      if (why.empty()) why = cx[i]->gossip_why;
+    }
+    throw Error(GS_EUNSUPPORTED, "lazy gossip can change this batch (an IHAVE lands before the last delivery; " +
+                                     (why.empty() ? std::string("another rank") : why) +
+                                     "); partitioned mode runs eager forwarding only: use gs_run");
+  }
+  for (uint32_t i = 0; i < nctx; i++) {
+    GS_HIP(hipSetDevice(cx[i]->cfg.device));
+    part_dev_finish(*cx[i], sinks ? &sinks[i] : nullptr, i0);
+  }
+}
+
+}  // namespace
+
+extern "C" gs_status gs_run_partitioned(gs_ctx* const* ctxs, uint32_t nctx, gs_comm* comm, const gs_publish* sched,
+                                        uint64_t n_msgs, const gs_result_sink* sinks) {
+  if (!ctxs || !nctx || !comm || (!sched && n_msgs)) return GS_EINVAL;
+  for (uint32_t i = 0; i < nctx; i++)
+    if (!ctxs[i]) return GS_EINVAL;
+  Ctx* c0 = ctxs[0];
+  try {
+    if (comm->local ? nctx != comm->nranks : nctx != 1)
+      c0->fail(GS_EINVAL, "gs_run_partitioned: pass one context per part (local) or this rank's context (RCCL)");
+    std::vector<Ctx*> cx(nctx);
+    for (uint32_t i = 0; i < nctx; i++) {
+      cx[i] = ctxs[i];
+      if (!cx[i]->mesh_built) cx[i]->fail(GS_ESTATE, "gs_mesh_converge first");
+      if (cx[i]->cfg.peers != c0->cfg.peers || cx[i]->cfg.batch != c0->cfg.batch)
+        c0->fail(GS_EINVAL, "every part needs the same peers and batch");
+      GS_HIP(hipSetDevice(cx[i]->cfg.device));
+      part_set(*cx[i], comm->nranks, comm->local ? i : comm->rank);
+    }
+    if (!comm->local && c0->cfg.device != comm->device)
+      c0->fail(GS_EINVAL, "the context and the communicator must use the same device");
+    uint64_t i0 = 0;
+    while (i0 < n_msgs) {  // batches of equal size and chunk count, at most cfg.batch messages
+      uint64_t i1 = i0 + 1;
+      while (i1 < n_msgs && i1 - i0 < c0->cfg.batch && sched[i1].msg_size == sched[i0].msg_size &&
+             sched[i1].frags == sched[i0].frags)
+        i1++;
+      run_batch(comm, cx.data(), nctx, sched, i0, (uint32_t)(i1 - i0), sinks);
+      i0 = i1;
+    }
+  } catch (const Error& e) {
+    c0->last_error = e.msg;
+    return e.code;
+  } catch (const std::exception& e) {
+    c0->last_error = e.what();
+    return GS_ENOMEM;
+  }
+  return GS_OK;
+}

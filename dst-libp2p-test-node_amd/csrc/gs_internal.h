@@ -157,12 +157,15 @@ struct Ctx {
   unsigned part_grid = 0;
   uint32_t part_seg_cap = 0;
   DevBuf<uint64_t> d_pcnt;      // [4] frontier groups, records, relax min key, spare
+  DevBuf<uint64_t> d_dcnt, d_dpos;  // [64] records per destination part / their write cursors
+  DevBuf<gs_part_record> d_pout, d_pin;  // gs_run_partitioned: records sent / received this bucket
 
   // stats
   gs_stats stats{};
   std::vector<hipEvent_t> ev_pool;
   int num_cus = 0;
   uint32_t split_bpc = 0;  // blocks per CU of the split path's grid (split_blocks_per_cu)
+  std::string gossip_why;  // the message that broke the last partitioned gossip no-op proof
 
   ~Ctx();
   void fail(gs_status c, const std::string& m) { throw Error(c, m); }
@@ -178,6 +181,14 @@ uint64_t part_begin(Ctx& c, const gs_publish* sched, uint64_t n_msgs);
 bool part_scan(Ctx& c, uint64_t bucket_key, gs_part_record* rec, uint64_t cap, uint64_t* n, uint64_t* m1);
 uint64_t part_relax(Ctx& c, uint64_t bucket_key, const gs_part_record* rec, uint64_t n);
 void part_finish(Ctx& c, const gs_result_sink* sink);
+// device-driven partitioned protocol (gs_comm.hip)
+void part_dev_bucket(Ctx& c, uint32_t parts);
+void part_dev_scan_count(Ctx& c, uint32_t parts);
+void part_dev_export(Ctx& c, uint32_t parts, gs_part_record* out);
+void part_dev_relax_next(Ctx& c, const gs_part_record* in, uint64_t n);
+bool part_dev_complete(Ctx& c, bool hist);
+void part_dev_finish(Ctx& c, const gs_result_sink* sink, uint64_t row0);
+void part_abort(Ctx& c);
 
 // small device helpers
 void device_exclusive_scan(Ctx& c, const uint64_t* in, uint64_t* out, uint32_t n);

@@ -177,6 +177,140 @@ __global__ __launch_bounds__(TB) void k_precv(RelaxArgs a, const gs_part_record*
   }
 }
 
+// Owner of peer w among `parts` equal ranges [p*N/parts, (p+1)*N/parts).
+__device__ __forceinline__ uint32_t part_of(uint32_t w, uint32_t N, uint32_t parts) {
+  uint32_t p = (uint32_t)(((uint64_t)w * parts) / N);
+  while (p + 1 < parts && (uint64_t)(p + 1) * N / parts <= w) p++;
+  while (p > 0 && (uint64_t)p * N / parts > w) p--;
+  return p;
+}
+
+// Routed export of a bucket's arrivals (gs_run_partitioned): a record goes
+// only to the parts that own one of its forward targets (all-to-all-v instead
+// of an all-gather). COUNT: records per destination part into dcnt (no state
+// change); else the records themselves, destination d's at the offset
+// sum(dcnt[< d]) of `rec`, with the FD / R counters and the uplink FIFO fold.
+template <int FP, bool COUNT>
+__global__ __launch_bounds__(TB) void k_pexport_dest(RelaxArgs a, gs_part_record* __restrict__ rec, uint64_t* dcnt,
+                                                     uint64_t* dpos, uint32_t parts, uint32_t Nglob) {
+  __shared__ BucketLds L;
+  __shared__ uint64_t s_off[64];
+  load_tables(L, a);
+  if (!COUNT && threadIdx.x == 0) {
+    uint64_t o = 0;
+    for (uint32_t d = 0; d < parts; d++) { s_off[d] = o; o += dcnt[d]; }
+  }
+  __syncthreads();
+  const uint64_t cur = a.ctrl[0];
+  if (cur == INF64) return;  // block-uniform: no bucket left
+  const uint64_t lo = ((cur >> a.tshift) / a.delta) * a.delta, hi = lo + a.delta;
+  const uint32_t LL = a.L;
+  const uint32_t wave = blockIdx.x * (TB / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const uint32_t n = __builtin_amdgcn_readfirstlane(a.fr_cnt[wave]);
+  const size_t seg = (size_t)wave * a.seg_cap;
+  constexpr uint32_t GPW = 64 / FP;
+  const uint64_t smask = (1ull << a.sb) - 1;
+  uint64_t fd = 0, nr = 0;
+  uint32_t err = 0;
+  for (uint32_t base = 0; base < n; base += GPW) {
+    const uint32_t gi = base + (uint32_t)lane / FP;
+    const bool valid = gi < n;
+    uint64_t gid, key;
+    if constexpr (FP == 1) {
+      gid = valid ? a.fr_idx[seg + gi] : 0;
+      key = valid ? a.fr_key[seg + gi] : INF64;
+    } else {
+      gid = valid ? (uint64_t)a.fr_idx[seg + gi] * FP + (lane & (FP - 1)) : 0;
+      key = valid ? a.keys[gid] : INF64;
+    }
+    const uint64_t t = key >> a.tshift;
+    const uint32_t u = (uint32_t)(gid / LL);
+    const uint32_t slot = (uint32_t)(gid - (uint64_t)u * LL);
+    const uint32_t ug = u + a.u0;
+    const uint32_t pm = valid ? a.pub[slot / FP] : EMPTY;
+    const bool active = valid && key != INF64 && t >= lo && t < hi && ug != pm;
+    const uint32_t src = (uint32_t)(key & smask);
+    uint32_t cnt = 0;
+    uint64_t dmask = 0;  // destination parts of the record
+    if (active) {
+      uint32_t row[MESH_W];
+      load_mesh_row(a.mesh, ug, row);
+#pragma unroll
+      for (int j = 0; j < (int)MESH_W; j++) {
+        const uint32_t w = row[j] & 0xFFFFFFu;
+        if (row[j] != EMPTY && w != src && w != pm) {
+          cnt++;
+          dmask |= 1ull << part_of(w, Nglob, parts);
+        }
+      }
+    }
+    uint64_t start = 0;
+    if constexpr (!COUNT) {
+      const uint32_t ser = L.su[a.stage[valid ? ug : a.u0]];
+      start = uplink_start<FP>(a.busy, (size_t)u * a.B + slot / FP, active, key, cnt, ser, a.tshift);
+      if (active) {
+        fd++;
+        nr += cnt;
+        const uint32_t hp = (uint32_t)((key >> a.sb) & ((1u << HOP_BITS) - 1));
+        if (cnt && hp + 1 >= (1u << HOP_BITS)) err |= ERR_HOPS;
+      }
+    }
+    for (uint32_t d = 0; d < parts; d++) {  // wave-uniform
+      const bool want = active && ((dmask >> d) & 1);
+      const uint64_t wm = __ballot(want);
+      if (wm == 0) continue;
+      if constexpr (COUNT) {
+        if (lane == 0) atomicAdd((unsigned long long*)&dcnt[d], (unsigned long long)__popcll(wm));
+      } else {
+        uint64_t wbase = 0;
+        if (lane == 0) wbase = atomicAdd((unsigned long long*)&dpos[d], (unsigned long long)__popcll(wm));
+        wbase = uniform64(wbase);
+        if (want) {
+          gs_part_record r;
+          r.key = key;
+          r.start = start;
+          r.peer = ug;
+          r.slot = slot;
+          rec[s_off[d] + wbase + (uint64_t)__popcll(wm & ((1ull << lane) - 1))] = r;
+        }
+      }
+    }
+  }
+  if constexpr (!COUNT) {
+    fd = wave_sum(fd);
+    nr = wave_sum(nr);
+    for (int off = 32; off > 0; off >>= 1) err |= __shfl_xor(err, off);
+    if (lane == 0) {
+      if (fd) atomicAdd((unsigned long long*)&a.counters[C_FD], (unsigned long long)fd);
+      if (nr) atomicAdd((unsigned long long*)&a.counters[C_R_FWD], (unsigned long long)nr);
+      if (err) atomicOr((unsigned*)&a.counters[C_ERR], err);
+    }
+  }
+}
+
+// Bucket bookkeeping of the device-driven protocol: the bucket key is
+// already in ctrl[0] (the MIN all-reduce wrote it); reset the rest.
+__global__ void k_pbucket_dev(uint64_t* ctrl, uint64_t* pcnt, uint64_t* dcnt, uint64_t* dpos, uint32_t parts) {
+  if (threadIdx.x == 0) {
+    ctrl[1] = INF64;
+    ctrl[2] = INF64;
+    pcnt[0] = 0;
+    pcnt[1] = 0;
+    pcnt[2] = INF64;
+  }
+  if (threadIdx.x < parts) {
+    dcnt[threadIdx.x] = 0;
+    dpos[threadIdx.x] = 0;
+  }
+}
+
+// This part's candidate for the next bucket: min(scan's next pending key,
+// relax's min pushed key) into ctrl[0], ready for the MIN all-reduce.
+__global__ void k_pnext(uint64_t* ctrl, const uint64_t* pcnt) {
+  if (threadIdx.x == 0) ctrl[0] = ctrl[1] < pcnt[2] ? ctrl[1] : pcnt[2];
+}
+
 template <int FP>
 void part_export_fp(const RelaxArgs& a, unsigned grid, hipStream_t s, gs_part_record* rec, uint64_t cap,
                     uint64_t* pcnt) {
@@ -334,6 +468,124 @@ uint64_t part_relax(Ctx& c, uint64_t bucket_key, const gs_part_record* rec, uint
 // condition holds for the whole graph iff it holds in every part, so a part
 // whose peers could take an IWANT fails the batch (GS_EUNSUPPORTED) rather
 // than return a result without the gossip relaxations.
+// ---- steps of the library-driven protocol (gs_comm.hip, gs_run_partitioned);
+// every one is stream-ordered on the context's stream, no host synchronisation.
+
+void part_dev_bucket(Ctx& c, uint32_t parts) {
+  c.d_dcnt.alloc(64);
+  c.d_dpos.alloc(64);
+  k_pbucket_dev<<<1, 64, 0, c.stream>>>(c.d_ctrl.p, c.d_pcnt.p, c.d_dcnt.p, c.d_dpos.p, parts);
+  GS_HIP(hipGetLastError());
+}
+
+// k_scan of the bucket in ctrl[0] + the per-destination record counts (d_dcnt).
+void part_dev_scan_count(Ctx& c, uint32_t parts) {
+  hipStream_t s = c.stream;
+  const Batch& b = c.part_b;
+  const RelaxArgs ra = part_args(c);
+  const unsigned grid = c.part_grid;
+  switch (b.FP) {
+    case 1: k_scan<1, false, false><<<grid, TB, 0, s>>>(ra); break;
+    case 2: k_scan<2, false, false><<<grid, TB, 0, s>>>(ra); break;
+    case 4: k_scan<4, false, false><<<grid, TB, 0, s>>>(ra); break;
+    case 8: k_scan<8, false, false><<<grid, TB, 0, s>>>(ra); break;
+    default: k_scan<16, false, false><<<grid, TB, 0, s>>>(ra); break;
+  }
+#define GS_PCOUNT(F) k_pexport_dest<F, true><<<grid, TB, 0, s>>>(ra, nullptr, c.d_dcnt.p, c.d_dpos.p, parts, c.cfg.peers)
+  switch (b.FP) {
+    case 1: GS_PCOUNT(1); break;
+    case 2: GS_PCOUNT(2); break;
+    case 4: GS_PCOUNT(4); break;
+    case 8: GS_PCOUNT(8); break;
+    default: GS_PCOUNT(16); break;
+  }
+#undef GS_PCOUNT
+  GS_HIP(hipGetLastError());
+  c.stats.relax_launches++;
+}
+
+// The records, grouped by destination part (offsets = prefix of d_dcnt).
+void part_dev_export(Ctx& c, uint32_t parts, gs_part_record* out) {
+  hipStream_t s = c.stream;
+  const Batch& b = c.part_b;
+  const RelaxArgs ra = part_args(c);
+  const unsigned grid = c.part_grid;
+#define GS_PEXP(F) k_pexport_dest<F, false><<<grid, TB, 0, s>>>(ra, out, c.d_dcnt.p, c.d_dpos.p, parts, c.cfg.peers)
+  switch (b.FP) {
+    case 1: GS_PEXP(1); break;
+    case 2: GS_PEXP(2); break;
+    case 4: GS_PEXP(4); break;
+    case 8: GS_PEXP(8); break;
+    default: GS_PEXP(16); break;
+  }
+#undef GS_PEXP
+  GS_HIP(hipGetLastError());
+}
+
+// Received records into own peers, then this part's next-bucket candidate in ctrl[0].
+void part_dev_relax_next(Ctx& c, const gs_part_record* in, uint64_t n) {
+  hipStream_t s = c.stream;
+  const Batch& b = c.part_b;
+  if (n) {
+    const RelaxArgs ra = part_args(c);
+    const unsigned grid = (unsigned)std::min<uint64_t>((n + TB - 1) / TB, (uint64_t)c.num_cus * 16);
+    switch (b.FP) {
+      case 1: part_recv_fp<1>(ra, grid, s, in, n, c.d_pcnt.p); break;
+      case 2: part_recv_fp<2>(ra, grid, s, in, n, c.d_pcnt.p); break;
+      case 4: part_recv_fp<4>(ra, grid, s, in, n, c.d_pcnt.p); break;
+      case 8: part_recv_fp<8>(ra, grid, s, in, n, c.d_pcnt.p); break;
+      default: part_recv_fp<16>(ra, grid, s, in, n, c.d_pcnt.p); break;
+    }
+  }
+  k_pnext<<<1, 64, 0, s>>>(c.d_ctrl.p, c.d_pcnt.p);
+  GS_HIP(hipGetLastError());
+}
+
+// Completion of this part's own peers (k_complete, with the 100 ms histograms
+// when a summary is wanted) and, with lazy gossip, this part's half of the
+// no-op proof (gossip_noop over its own peers; the batch stands iff every
+// part's holds). Returns true without lazy gossip.
+bool part_dev_complete(Ctx& c, bool hist) {
+  const Batch& b = c.part_b;
+  run_complete(c, b, c.part_u0, c.part_un, true, hist);
+  if (!c.cfg.lazy_gossip) return true;
+  std::vector<uint64_t> ms((size_t)b.B * MS_COLS), rel0(b.B);
+  GS_HIP(hipMemcpyAsync(ms.data(), c.d_mstat.p, ms.size() * 8, hipMemcpyDeviceToHost, c.stream));
+  GS_HIP(hipStreamSynchronize(c.stream));
+  const uint64_t hb = c.cfg.heartbeat_ns, ph = c.cfg.hb_phase_ns;
+  for (uint32_t q = 0; q < b.B; q++) {
+    const uint64_t tp = b.tpub[q], h0 = tp <= ph ? 0 : (tp - ph + hb - 1) / hb;
+    rel0[q] = ph + h0 * hb - tp;
+  }
+  const bool ok = gossip_noop(b, ms.data(), rel0);
+  if (!ok)
+    for (uint32_t q = 0; q < b.B; q++) {
+      const uint64_t und = ms[(size_t)q * MS_COLS + MS_UNDEL], tm = ms[(size_t)q * MS_COLS + MS_TMAX];
+      if (und || tm >= rel0[q] + b.lat_min) {
+        c.gossip_why = "part " + std::to_string(c.part_idx) + " message " + std::to_string(q) + ": " +
+                       std::to_string(und) + " peers never complete, last completion " + std::to_string(tm) +
+                       " ns >= first IHAVE " + std::to_string(rel0[q] + b.lat_min) + " ns";
+        break;
+      }
+    }
+  return ok;
+}
+
+// Finish a completed batch whose gossip proof holds everywhere: delivery into
+// sink rows [row0, row0 + B), counters.
+void part_dev_finish(Ctx& c, const gs_result_sink* sink, uint64_t row0) {
+  if (!c.part_open) c.fail(GS_ESTATE, "gs_part_begin first");
+  c.part_open = false;
+  const Batch& b = c.part_b;
+  deliver(c, b, c.part_u0, c.part_un, sink, row0);
+  if (c.cfg.lazy_gossip) c.stats.gossip_noop_msgs += b.B;
+  c.stats.messages += b.B;
+  c.stats.batches++;
+  collect_stats(c);
+}
+
+void part_abort(Ctx& c) { c.part_open = false; }
+
 void part_finish(Ctx& c, const gs_result_sink* sink) {
   if (!c.part_open) c.fail(GS_ESTATE, "gs_part_begin first");
   c.part_open = false;

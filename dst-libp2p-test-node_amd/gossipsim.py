@@ -126,7 +126,13 @@ SIGNATURES = {
     "gs_part_scan": (i32, [ctypes.c_void_p, u64, ctypes.c_void_p, u64, P(u64), P(u64)]),
     "gs_part_relax": (i32, [ctypes.c_void_p, u64, ctypes.c_void_p, u64, P(u64)]),
     "gs_part_finish": (i32, [ctypes.c_void_p, P(GsResultSink)]),
+    "gs_comm_get_id": (i32, [ctypes.c_char_p]),
+    "gs_comm_init": (i32, [u32, u32, ctypes.c_char_p, i32, P(ctypes.c_void_p)]),
+    "gs_comm_init_local": (i32, [u32, P(ctypes.c_void_p)]),
+    "gs_comm_destroy": (i32, [ctypes.c_void_p]),
+    "gs_run_partitioned": (i32, [P(ctypes.c_void_p), u32, ctypes.c_void_p, P(GsPublish), u64, P(GsResultSink)]),
 }
+COMM_ID_BYTES = 128
 GS_ERANGE = -5
 KEY_NONE = (1 << 64) - 1  # empty-bucket marker of the partitioned protocol
 
@@ -595,3 +601,69 @@ class LogStream:
             self.h = ctypes.c_void_p()
             if rc:
                 raise GossipSimError(rc, "gs_log_close failed")
+
+
+class Comm:
+    """gs_comm: the parts of a peer-partitioned run (include/gossipsim.h).
+
+    Comm(local_parts=P)                     P parts driven by this process
+    Comm(nranks, rank, uid, device)         one rank of an RCCL communicator;
+                                            uid = Comm.get_id() on rank 0,
+                                            handed to the others out of band"""
+
+    def __init__(self, nranks=1, rank=0, uid=None, device=0, local_parts=None):
+        self.h = ctypes.c_void_p()
+        if local_parts is not None:
+            rc = lib().gs_comm_init_local(local_parts, ctypes.byref(self.h))
+            self.parts, self.local = local_parts, True
+        else:
+            if uid is None:
+                uid = Comm.get_id()
+            rc = lib().gs_comm_init(nranks, rank, uid, device, ctypes.byref(self.h))
+            self.parts, self.local, self.rank = nranks, False, rank
+        if rc:
+            raise GossipSimError(rc, "gs_comm_init failed")
+
+    @staticmethod
+    def get_id():
+        buf = ctypes.create_string_buffer(COMM_ID_BYTES)
+        rc = lib().gs_comm_get_id(buf)
+        if rc:
+            raise GossipSimError(rc, "gs_comm_get_id failed (RCCL not loadable?)")
+        return buf.raw
+
+    def run_partitioned(self, sims, schedule, collect=True):
+        """gs_run_partitioned over this process's Simulators (local: one per part,
+        in part order; RCCL: this rank's). -> per part {"t_complete", "hops",
+        "peer_range"} [M, own peers] (collect) or None."""
+        schedule = sims[0]._schedule(schedule)
+        M = len(schedule)
+        arr = (ctypes.c_void_p * len(sims))(*[s.ctx for s in sims])
+        sinks, keep, out = (GsResultSink * len(sims))(), [], []
+        for i, sim in enumerate(sims):
+            part = i if self.local else self.rank
+            u0, u1 = part * sim.peers // self.parts, (part + 1) * sim.peers // self.parts
+            sim.part_range = (u0, u1)
+            if collect:
+                tc = np.zeros(M * (u1 - u0), np.uint64)
+                hp = np.zeros(M * (u1 - u0), np.uint8)
+                keep += [tc, hp]
+                sinks[i].t_complete_ns = _ptr(tc, u64)
+                sinks[i].hops = _ptr(hp, u8)
+                out.append({"t_complete": tc.reshape(M, u1 - u0), "hops": hp.reshape(M, u1 - u0),
+                            "peer_range": (u0, u1)})
+        rc = lib().gs_run_partitioned(arr, len(sims), self.h, schedule, M, sinks if collect else None)
+        if rc:
+            raise GossipSimError(rc, lib().gs_last_error(sims[0].ctx).decode())
+        return out if collect else None
+
+    def close(self):
+        if self.h:
+            lib().gs_comm_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

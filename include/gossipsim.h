@@ -422,6 +422,36 @@ gs_status gs_part_relax(struct gs_ctx* ctx, uint64_t bucket_key, const gs_part_r
 /* sink arrays are [n_msgs][own peers] (message-major over this part's peers) */
 gs_status gs_part_finish(struct gs_ctx* ctx, const gs_result_sink* sink);
 
+/* ---- multi-GPU communicator and the library-driven partitioned run ---------
+ * (SURVEY §8b gs_comm_init, §8e; the reference's process boundary is one swarm
+ * task per process, rust-test-node/src/main.rs:466-477.) One rank per process
+ * and GPU over RCCL (xGMI), or several parts in one process (loopback device
+ * copies: tests, several parts on one GPU). */
+typedef struct gs_comm gs_comm;
+#define GS_COMM_ID_BYTES 128
+typedef struct gs_comm_id { char internal[GS_COMM_ID_BYTES]; } gs_comm_id;
+/* An RCCL unique id: rank 0 creates it and hands it to the other ranks out of
+ * band (as ncclGetUniqueId). GS_EUNSUPPORTED when RCCL cannot be loaded. */
+gs_status gs_comm_get_id(gs_comm_id* out);
+/* This process's rank of an nranks-rank RCCL communicator on HIP device
+ * `device` (collective: every rank calls it). */
+gs_status gs_comm_init(uint32_t nranks, uint32_t rank, const gs_comm_id* id, int32_t device, gs_comm** out);
+/* nparts parts driven by this process (one context each, any devices). */
+gs_status gs_comm_init_local(uint32_t nparts, gs_comm** out);
+gs_status gs_comm_destroy(gs_comm* comm);
+/* gs_run with the peers partitioned over the communicator's parts: ctxs are
+ * this process's contexts (RCCL: nctx = 1, the rank's; local: nctx = nparts,
+ * part i = ctxs[i]), all built with the same config, topology and mesh. The
+ * library sets each context's partition, runs every batch's bucket protocol
+ * (per bucket: own scan, records routed only to the parts owning a target
+ * with grouped send/recv, relax into own peers, MIN all-reduce of the next
+ * bucket key on the device; one host read of the count matrix per bucket)
+ * and writes part i's peers to sinks[i] ([n_msgs][own peers]; sinks may be
+ * NULL). Collective over the communicator. Results are bit-identical to
+ * gs_run; lazy gossip runs as the proven no-op only (GS_EUNSUPPORTED otherwise). */
+gs_status gs_run_partitioned(struct gs_ctx* const* ctxs, uint32_t nctx, gs_comm* comm, const gs_publish* sched,
+                             uint64_t n_msgs, const gs_result_sink* sinks);
+
 #ifdef __cplusplus
 }
 #endif

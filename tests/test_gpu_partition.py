@@ -94,3 +94,58 @@ def test_partitioned_unsupported_modes_fail_loudly():
         s.part_begin(_sched(4, 300))
     with pytest.raises(gossipsim.GossipSimError, match="GS_ESTATE"):
         s.part_relax(1, 0, 0)
+
+
+# ---- the library-driven protocol behind the C ABI (gs_comm_*, gs_run_partitioned) ----
+
+def _whole(p, S, links, sched, batch):
+    sims = _parts(p, S, links, 1, batch)
+    return sims[0].run(sched), sims[0].stats()
+
+
+@pytest.mark.parametrize("parts,frags,batch", [(2, 1, 16), (3, 2, 16), (8, 1, 16), (4, 3, 6)])
+def test_run_partitioned_local_comm_equals_gs_run(parts, frags, batch):
+    """gs_run_partitioned with gs_comm_init_local: P parts on one GPU, records
+    routed only to the parts owning a target; bit-identical to gs_run (several
+    batches when batch < messages) and to the oracle, counters summed over parts."""
+    p = oracle.params(peers=3000, seed=58, fragments=frags)
+    sched = _sched(16, 3000)
+    ref, rst = _whole(p, 5, (50, 150, 40, 130), sched, batch)
+    sims = _parts(p, 5, (50, 150, 40, 130), parts, batch)
+    comm = gossipsim.Comm(local_parts=parts)
+    res = comm.run_partitioned(sims, sched)
+    np.testing.assert_array_equal(np.concatenate([r["t_complete"] for r in res], axis=1), ref["t_complete"])
+    np.testing.assert_array_equal(np.concatenate([r["hops"] for r in res], axis=1), ref["hops"])
+    st = [s.stats() for s in sims]
+    for k in ("deliveries", "frag_deliveries", "relaxations", "bytes_alg", "latency_sum_ms"):
+        assert sum(x[k] for x in st) == rst[k], k
+    assert sum(x["gossip_noop_msgs"] for x in st) == 16 * parts
+    ora = oracle.simulate(p, 5, (50, 150, 40, 130), sched=sched)
+    np.testing.assert_array_equal(ref["t_complete"], ora["t_complete"])
+    comm.close()
+
+
+@pytest.mark.parametrize("N,M", [(2000, 12), (100_000, 64)])
+def test_run_partitioned_rccl_single_rank(N, M):
+    """gs_comm_init over RCCL with one rank on this GPU (the N = 1 case of the
+    multi-GPU bench): the same protocol through RCCL's all-gather, grouped
+    send/recv and MIN all-reduce, bit-identical to gs_run."""
+    p = oracle.params(peers=N, seed=59)
+    sched = _sched(M, N)
+    ref, _ = _whole(p, 5, (50, 150, 40, 130), sched, M)
+    (s,) = _parts(p, 5, (50, 150, 40, 130), 1, M)
+    comm = gossipsim.Comm(nranks=1, rank=0, uid=gossipsim.Comm.get_id(), device=0)
+    (r,) = comm.run_partitioned([s], sched)
+    np.testing.assert_array_equal(r["t_complete"], ref["t_complete"])
+    np.testing.assert_array_equal(r["hops"], ref["hops"])
+    comm.close()
+
+
+def test_run_partitioned_refuses_gossip_that_matters():
+    p = oracle.params(peers=600, seed=60, hb_phase_ns=T0 % 1_000_000_000)  # heartbeat at the publish
+    sims = _parts(p, 1, (50, 50, 50, 50), 2, 4)
+    comm = gossipsim.Comm(local_parts=2)
+    with pytest.raises(gossipsim.GossipSimError, match="GS_EUNSUPPORTED"):
+        comm.run_partitioned(sims, _sched(4, 600))
+    # the contexts stay usable: an eager-only run afterwards
+    comm.close()
