@@ -171,12 +171,9 @@ uint64_t cdiv(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 // protobuf RPC{publish: Message{from, data, seqno, topic, signature}}
 // length-prefixed, then the MUXER stack (rust-test-node/src/main.rs:418-440).
 namespace {
-// -> wire bytes; *pkts / *hdr = packets and their header bytes (the last layer)
-uint64_t wire_model(uint64_t payload, uint32_t muxer, uint32_t signed_msgs, uint64_t* pkts, uint64_t* hdr) {
-  uint64_t body = pb_field(payload) + pb_field(4);               // data, topic "test"
-  if (signed_msgs) body += pb_field(38) + pb_field(8) + pb_field(64);  // from, seqno, sig
-  const uint64_t rpc = pb_field(body);
-  const uint64_t frame = varint_len(rpc) + rpc;
+// A length-delimited RPC frame through the MUXER stack -> wire bytes; *pkts /
+// *hdr = packets of the last layer and their header bytes
+uint64_t stack_model(uint64_t frame, uint32_t muxer, uint64_t* pkts, uint64_t* hdr) {
   if (muxer == GS_MUX_QUIC) {
     *pkts = cdiv(frame, 1415);
     *hdr = *pkts * 65;
@@ -189,7 +186,36 @@ uint64_t wire_model(uint64_t payload, uint32_t muxer, uint32_t signed_msgs, uint
   *hdr = *pkts * 40;
   return noise + *hdr;
 }
+uint64_t wire_model(uint64_t payload, uint32_t muxer, uint32_t signed_msgs, uint64_t* pkts, uint64_t* hdr) {
+  uint64_t body = pb_field(payload) + pb_field(4);               // data, topic "test"
+  if (signed_msgs) body += pb_field(38) + pb_field(8) + pb_field(64);  // from, seqno, sig
+  const uint64_t rpc = pb_field(body);
+  return stack_model(varint_len(rpc) + rpc, muxer, pkts, hdr);
+}
 }  // namespace
+
+// Lazy-gossip control RPCs with one message id:
+// RPC{control: ControlMessage{ihave: ControlIHave{topic "test", ids}}} and
+// RPC{control: {iwant: ControlIWant{ids}}}. The id is the node's
+// message_id_fn: rust's DefaultHasher u64 in decimal (main.rs:73-77) and nim's
+// $hash (gossipsub-queues/main.nim:123-124), up to 20 chars (modelled at 20);
+// go's sha256 digest (go-test-node/main.go:26-29), 32 bytes. A pure ACK is
+// one header-only packet.
+extern "C" void gs_control_packets(uint32_t kind, uint32_t node, uint32_t muxer, uint64_t* bytes,
+                                   uint64_t* packets, uint64_t* header_bytes) {
+  uint64_t w, p = 1, h;
+  if (kind == GS_CTRL_ACK) {
+    w = h = muxer == GS_MUX_QUIC ? 65 : 40;
+  } else {
+    const uint64_t id = node == GS_NODE_GO ? 32 : 20;
+    const uint64_t cm = kind == GS_CTRL_IHAVE ? pb_field(pb_field(4) + pb_field(id)) : pb_field(pb_field(id));
+    const uint64_t rpc = pb_field(cm);
+    w = stack_model(varint_len(rpc) + rpc, muxer, &p, &h);
+  }
+  if (bytes) *bytes = w;
+  if (packets) *packets = p;
+  if (header_bytes) *header_bytes = h;
+}
 
 extern "C" uint64_t gs_wire_bytes(uint64_t payload, uint32_t muxer, uint32_t signed_msgs) {
   uint64_t p, h;
@@ -210,29 +236,31 @@ extern "C" void gs_wire_packets(uint64_t payload, uint32_t muxer, uint32_t signe
 // then four ';'-separated groups of 12 counters (inbound / outbound localhost,
 // inbound / outbound remote): packets, bytes, control packets, control header
 // bytes, 2 control retransmit counters, data packets, data header bytes, data
-// payload bytes, 3 data retransmit counters. The simulator has no localhost
-// traffic, control packets (ACKs) or retransmissions: those stay 0.
+// payload bytes, 3 data retransmit counters. Control packets are the modelled
+// pure ACKs (header only); the simulator has no localhost traffic and no
+// retransmissions: those stay 0.
 extern "C" gs_status gs_write_shadow_heartbeat(const char* path, uint32_t peers, const uint64_t* tr,
                                                uint64_t sim_seconds) {
   if (!path || !tr) return GS_EINVAL;
   FILE* f = fopen(path, "w");
   if (!f) return GS_EINVAL;
   const unsigned long long hh = sim_seconds / 3600, mm = sim_seconds / 60 % 60, ss = sim_seconds % 60;
+  typedef unsigned long long ull;
   for (uint32_t u = 0; u < peers; u++) {
     const uint64_t* r = tr + (size_t)u * GS_TRAFFIC_COLS;
-    auto grp = [&](uint64_t pk, uint64_t by, uint64_t hd) {
-      char b[256];
-      snprintf(b, sizeof b, "%llu,%llu,0,0,0,0,%llu,%llu,%llu,0,0,0", (unsigned long long)pk, (unsigned long long)by,
-               (unsigned long long)pk, (unsigned long long)hd, (unsigned long long)(by - hd));
+    auto grp = [&](uint64_t pk, uint64_t by, uint64_t hd, uint64_t cpk, uint64_t chd) {
+      char b[320];
+      snprintf(b, sizeof b, "%llu,%llu,%llu,%llu,0,0,%llu,%llu,%llu,0,0,0", (ull)(pk + cpk), (ull)(by + chd),
+               (ull)cpk, (ull)chd, (ull)pk, (ull)hd, (ull)(by - hd));
       return std::string(b);
     };
     const std::string zero = "0,0,0,0,0,0,0,0,0,0,0,0";
     fprintf(f, "00:00:00.000000 [thread-0] %02llu:%02llu:%02llu.000000000 [message] [pod-%u] [tracker] "
                "[_tracker_logNode] [shadow-heartbeat] [node] %llu,%llu,%llu,0,0,0;%s;%s;%s;%s\n",
-            hh, mm, ss, u, (unsigned long long)sim_seconds, (unsigned long long)r[GS_TR_RX_BYTES],
-            (unsigned long long)r[GS_TR_TX_BYTES], zero.c_str(), zero.c_str(),
-            grp(r[GS_TR_RX_PKTS], r[GS_TR_RX_BYTES], r[GS_TR_RX_HDR]).c_str(),
-            grp(r[GS_TR_TX_PKTS], r[GS_TR_TX_BYTES], r[GS_TR_TX_HDR]).c_str());
+            hh, mm, ss, u, (ull)sim_seconds, (ull)(r[GS_TR_RX_BYTES] + r[GS_TR_RX_CTRL_HDR]),
+            (ull)(r[GS_TR_TX_BYTES] + r[GS_TR_TX_CTRL_HDR]), zero.c_str(), zero.c_str(),
+            grp(r[GS_TR_RX_PKTS], r[GS_TR_RX_BYTES], r[GS_TR_RX_HDR], r[GS_TR_RX_CTRL_PKTS], r[GS_TR_RX_CTRL_HDR]).c_str(),
+            grp(r[GS_TR_TX_PKTS], r[GS_TR_TX_BYTES], r[GS_TR_TX_HDR], r[GS_TR_TX_CTRL_PKTS], r[GS_TR_TX_CTRL_HDR]).c_str());
   }
   if (fclose(f)) return GS_EINVAL;
   return GS_OK;

@@ -360,6 +360,7 @@ uint64_t part_begin(Ctx& c, const gs_publish* sched, uint64_t n_msgs) {
     if (sched[i].msg_size != sched[0].msg_size || frags_of(c, sched[i]) != F)
       c.fail(GS_EINVAL, "partitioned batch needs equal msg_size and frags");
   if (c.cfg.churn_ppm) c.fail(GS_EUNSUPPORTED, "churn is not supported in partitioned mode");
+  if (c.traffic) c.fail(GS_EUNSUPPORTED, "per-peer traffic is not supported in partitioned mode");
   if (c.cfg.idontwant && frag_payload(c.cfg.node, sched[0].msg_size, F) >= c.cfg.idontwant)
     c.fail(GS_EUNSUPPORTED, "IDONTWANT is not supported in partitioned mode");
   const uint32_t FP = pow2_at_least(F), Bmax = c.cfg.batch, un = c.part_un;

@@ -29,6 +29,7 @@ constexpr int TB = 256;
 
 #include "gs_relax_kernel.h"
 #include "gs_pull_kernel.h"
+#include "gs_traffic.h"
 
 
 struct SeedArgs {
@@ -318,104 +319,6 @@ __global__ __launch_bounds__(TB) void k_transpose(const uint64_t* __restrict__ t
   }
 }
 
-struct TrafficArgs {
-  const uint64_t* keys;
-  const uint32_t* mesh;
-  const uint32_t* pub;
-  const uint8_t* stage;
-  const uint32_t* tables;  // lat[S*S] | ...
-  const uint64_t* row;
-  const uint32_t* col;
-  uint64_t* traffic;       // [N][GS_TRAFFIC_COLS]
-  uint64_t W, pk, hdr;     // wire bytes, packets, header bytes of one fragment send
-  uint32_t N, L, FP, Fe, S, sb, tshift, idw, flood, collide;
-};
-
-// Per-peer traffic of a finished batch (gs_set_traffic), from the final keys:
-// the first receipt of (m, f) at u != publisher sent one copy to each of
-// mesh(u) \ {src, publisher} minus the IDONTWANT skips — exactly the forward
-// sends the relaxation counted (R). One wave per row u; lane k < deg ends with
-// the number of copies u sent to its mesh entry k. The sender's tx columns are
-// written by its own wave only; rx columns take atomics.
-template <int FP>
-__global__ __launch_bounds__(TB) void k_traffic(TrafficArgs a) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t nw = gridDim.x * (TB / 64);
-  const uint64_t smask = (1ull << a.sb) - 1;
-  for (uint32_t u = (blockIdx.x * TB + threadIdx.x) >> 6; u < a.N; u += nw) {
-    const uint32_t e = lane < (int)MESH_W ? a.mesh[(size_t)u * MESH_W + lane] : EMPTY;
-    const uint32_t deg = (uint32_t)__popcll(__ballot(e != EMPTY));
-    const uint32_t su = a.stage[u];
-    uint32_t cnt = 0, done = 0;
-    for (uint32_t i0 = 0; i0 < a.L; i0 += 64) {
-      const uint32_t i = i0 + lane;
-      const bool in = i < a.L && (i & (FP - 1)) < a.Fe;
-      const uint64_t key = in ? a.keys[(size_t)u * a.L + i] : INF64;
-      const uint32_t pm = in ? a.pub[i / FP] : EMPTY;
-      const bool got = key != INF64 && pm != u;
-      {  // completed messages (reassembly, main.rs:79-99): every fragment of the group received
-        constexpr uint64_t gmask = (FP == 64) ? ~0ull : ((1ull << FP) - 1);
-        const uint64_t ok = __ballot(i < a.L && ((i & (FP - 1)) >= a.Fe || got));
-        const bool lead = (lane & (FP - 1)) == 0 && i < a.L && got && !a.collide &&
-                          ((ok >> (lane & ~(FP - 1))) & gmask) == gmask;
-        done += (uint32_t)__popcll(__ballot(lead));
-      }
-      const uint32_t src = (uint32_t)(key & smask);
-      const uint64_t t = key >> a.tshift;
-      for (uint32_t k = 0; k < deg; k++) {  // wave-uniform
-        const uint32_t y = __builtin_amdgcn_readlane(e, k), w = y & 0xFFFFFFu;
-        bool send = got && w != src && w != pm;
-        if (send && a.idw) {  // go's IDONTWANT (main.go:165): w announced it before u's receipt
-          const uint64_t kw = a.keys[(size_t)w * a.L + i];
-          if (kw != INF64 && (kw >> a.tshift) + a.tables[(y >> STAGE_SHIFT) * a.S + su] <= t) send = false;
-        }
-        const uint32_t c = (uint32_t)__popcll(__ballot(send));
-        cnt += lane == (int)k ? c : 0u;
-      }
-    }
-    const uint64_t tot = wave_sum((uint64_t)cnt);
-    if (lane == 0 && (tot || done)) {
-      uint64_t* r = a.traffic + (size_t)u * GS_TRAFFIC_COLS;
-      r[GS_TR_TX_BYTES] += tot * a.W;
-      r[GS_TR_TX_PKTS] += tot * a.pk;
-      r[GS_TR_TX_HDR] += tot * a.hdr;
-      r[GS_TR_RECEIVED] += done;
-    }
-    if (cnt) {
-      uint64_t* r = a.traffic + (size_t)(e & 0xFFFFFFu) * GS_TRAFFIC_COLS;
-      atomicAdd((unsigned long long*)&r[GS_TR_RX_BYTES], (unsigned long long)cnt * a.W);
-      atomicAdd((unsigned long long*)&r[GS_TR_RX_PKTS], (unsigned long long)cnt * a.pk);
-      atomicAdd((unsigned long long*)&r[GS_TR_RX_HDR], (unsigned long long)cnt * a.hdr);
-    }
-  }
-}
-
-// The publishers' own sends (main.rs:123 with flood_publish, main.rs:227):
-// every fragment to every connection (or to the mesh without flood publish).
-// One block per message; runs after k_traffic (same stream), so the atomics
-// on the publisher's tx do not race its row's plain updates.
-__global__ __launch_bounds__(TB) void k_traffic_pub(TrafficArgs a) {
-  const uint32_t p = a.pub[blockIdx.x];
-  uint32_t deg = 0;
-  const uint32_t* tg;
-  if (a.flood) { deg = (uint32_t)(a.row[p + 1] - a.row[p]); tg = a.col + a.row[p]; }
-  else { tg = a.mesh + (size_t)p * MESH_W; while (deg < MESH_W && tg[deg] != EMPTY) deg++; }
-  if (threadIdx.x == 0) {
-    uint64_t* r = a.traffic + (size_t)p * GS_TRAFFIC_COLS;
-    const unsigned long long n = (unsigned long long)a.Fe * deg;
-    atomicAdd((unsigned long long*)&r[GS_TR_TX_BYTES], n * a.W);
-    atomicAdd((unsigned long long*)&r[GS_TR_TX_PKTS], n * a.pk);
-    atomicAdd((unsigned long long*)&r[GS_TR_TX_HDR], n * a.hdr);
-    atomicAdd((unsigned long long*)&r[GS_TR_PUBLISHED], 1ull);
-  }
-  for (uint32_t j = threadIdx.x; j < deg; j += TB) {
-    uint64_t* r = a.traffic + (size_t)(tg[j] & 0xFFFFFFu) * GS_TRAFFIC_COLS;
-    atomicAdd((unsigned long long*)&r[GS_TR_RX_BYTES], (unsigned long long)a.Fe * a.W);
-    atomicAdd((unsigned long long*)&r[GS_TR_RX_PKTS], (unsigned long long)a.Fe * a.pk);
-    atomicAdd((unsigned long long*)&r[GS_TR_RX_HDR], (unsigned long long)a.Fe * a.hdr);
-  }
-}
-
 uint32_t pow2_at_least(uint32_t x) { uint32_t p = 1; while (p < x) p <<= 1; return p; }
 
 }  // namespace
@@ -693,27 +596,66 @@ static void launch_complete(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, co
   deliver(c, b, u0, un, sink, sink_row0);
 }
 
-// Per-peer traffic of the batch just finished (keys final, before the next reset).
+// The batch's fields of RelaxArgs shared by the bucket launches and the
+// traffic passes: keys, graph, link tables, churn ring, and with `gossip` the
+// lazy-gossip inputs (heartbeats per message, CSR, IHAVE target ring).
+static RelaxArgs relax_args(Ctx& c, const Batch& b, bool gossip) {
+  RelaxArgs ra{};
+  set_churn_args(c, ra);
+  ra.keys = c.d_keys.p; ra.mesh = c.d_mesh.p; ra.pub = c.d_pub.p;
+  ra.stage = c.d_stage.p; ra.tables = c.d_tables.p;
+  ra.total = (uint64_t)c.cfg.peers * b.L; ra.tmax = b.tmax;
+  ra.N = c.cfg.peers; ra.B = b.B; ra.F = b.F; ra.L = b.L; ra.S = c.S; ra.sb = b.sb; ra.tshift = b.tshift;
+  ra.idw = (c.cfg.idontwant && b.payload >= c.cfg.idontwant) ? 1 : 0;
+  ra.row = c.d_row.p;
+  ra.col = c.d_col.p;
+  if (gossip) {
+    ra.rel0 = c.d_rel0.p;
+    ra.habs0 = c.d_habs0.p;
+    ra.hb_ns = c.cfg.heartbeat_ns;
+    ra.seed = c.cfg.seed;
+    ra.gossip = 1;
+    if (c.cfg.churn_ppm) {
+      ra.ring_tgt = c.d_ring_tgt.p;
+      ra.ring_tcnt = c.d_ring_tcnt.p;
+    }
+    ra.hist = c.cfg.history_gossip;
+    ra.d_lazy = c.cfg.d_lazy;
+    ra.gf_milli = c.cfg.gossip_factor_milli;
+  }
+  return ra;
+}
+
+// Per-peer traffic of the batch just finished (keys final, before the next
+// reset; gs_traffic.h).
 static void launch_traffic(Ctx& c, const Batch& b) {
+  const bool gossip = c.cfg.lazy_gossip != 0;
+  const RelaxArgs ra = relax_args(c, b, gossip);
   TrafficArgs ta{};
-  ta.keys = c.d_keys.p; ta.mesh = c.d_mesh.p; ta.pub = c.d_pub.p; ta.stage = c.d_stage.p;
-  ta.tables = c.d_tables.p; ta.row = c.d_row.p; ta.col = c.d_col.p; ta.traffic = c.d_traffic.p;
+  ta.traffic = c.d_traffic.p;
   ta.W = gs_wire_bytes(b.payload, c.cfg.muxer, c.cfg.signed_msgs);
   gs_wire_packets(b.payload, c.cfg.muxer, c.cfg.signed_msgs, &ta.pk, &ta.hdr);
-  ta.N = c.cfg.peers; ta.L = b.L; ta.FP = b.FP; ta.Fe = b.Fe; ta.S = c.S; ta.sb = b.sb; ta.tshift = b.tshift;
-  ta.idw = (c.cfg.idontwant && b.payload >= c.cfg.idontwant) ? 1 : 0;
+  gs_control_packets(GS_CTRL_IHAVE, c.cfg.node, c.cfg.muxer, &ta.ihw, &ta.ihpk, &ta.ihhd);
+  gs_control_packets(GS_CTRL_IWANT, c.cfg.node, c.cfg.muxer, &ta.iww, &ta.iwpk, &ta.iwhd);
+  gs_control_packets(GS_CTRL_ACK, c.cfg.node, c.cfg.muxer, &ta.ack, nullptr, nullptr);
+  ta.Fe = b.Fe;
   ta.flood = c.cfg.flood_publish;
   ta.collide = b.collide ? 1 : 0;
-  const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(((uint64_t)ta.N + 3) / 4,
+  hipStream_t s = c.stream;
+  const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((ra.total + TB - 1) / TB,
                                                                            (uint64_t)c.num_cus * 8));
+  k_traffic_pub<<<b.B, TB, 0, s>>>(ra, ta);
+#define GS_TRAFFIC(FPV)                                                    \
+  k_traffic_fwd<FPV><<<grid, TB, 0, s>>>(ra, ta);                          \
+  if (gossip && c.cfg.history_gossip) k_traffic_gossip<FPV><<<grid, TB, 0, s>>>(ra, ta);
   switch (b.FP) {
-    case 1: k_traffic<1><<<grid, TB, 0, c.stream>>>(ta); break;
-    case 2: k_traffic<2><<<grid, TB, 0, c.stream>>>(ta); break;
-    case 4: k_traffic<4><<<grid, TB, 0, c.stream>>>(ta); break;
-    case 8: k_traffic<8><<<grid, TB, 0, c.stream>>>(ta); break;
-    default: k_traffic<16><<<grid, TB, 0, c.stream>>>(ta); break;
+    case 1: GS_TRAFFIC(1) break;
+    case 2: GS_TRAFFIC(2) break;
+    case 4: GS_TRAFFIC(4) break;
+    case 8: GS_TRAFFIC(8) break;
+    default: GS_TRAFFIC(16) break;
   }
-  k_traffic_pub<<<b.B, TB, 0, c.stream>>>(ta);
+#undef GS_TRAFFIC
   GS_HIP(hipGetLastError());
 }
 
@@ -854,7 +796,6 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
   // it a no-op (gossip_noop), else the batch is re-run on the push path.
   const bool idw_any = c.cfg.idontwant != 0;
   const bool churn = c.cfg.churn_ppm != 0;  // per-epoch mesh lookups live on the push path
-  if (c.traffic && churn) c.fail(GS_EUNSUPPORTED, "per-peer traffic covers a frozen mesh: turn off churn");
   const bool pull_any = (variant & 32) && !idw_any && !churn;
   // the push path with gossip or churn runs split, without tile skip
   // the push path with gossip or churn runs split + tile skip (its long tail of
@@ -933,7 +874,7 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       i1++;
     }
     const Batch b = setup_batch(c, sched, i0, i1);
-    const uint32_t FP = b.FP, F = b.F;
+    const uint32_t FP = b.FP;
     if (churn) {
       churn_ring(c, h_lo, h_hi + c.cfg.churn_horizon);
       const uint64_t hb = c.cfg.heartbeat_ns, ph = c.cfg.hb_phase_ns;
@@ -991,17 +932,14 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     auto push_run = [&](uint32_t v, bool with_gossip) {
       reset(v, with_gossip);
       launch_seed(c, b, 0, N);
-      RelaxArgs ra{};
-      set_churn_args(c, ra);
-      ra.keys = c.d_keys.p; ra.busy = c.d_busy.p; ra.mesh = c.d_mesh.p; ra.pub = c.d_pub.p;
+      RelaxArgs ra = relax_args(c, b, with_gossip);
+      ra.busy = c.d_busy.p;
       ra.meta = reinterpret_cast<TileMeta*>(c.d_meta.p);
       ra.fbits = c.d_fbits.p;
       ra.tmin = c.d_tmin.p;
       ra.touched = c.d_touched.p;
-      ra.stage = c.d_stage.p; ra.tables = c.d_tables.p; ra.ctrl = c.d_ctrl.p;
-      ra.counters = c.d_counters.p; ra.total = total; ra.delta = b.delta; ra.tmax = b.tmax;
-      ra.N = N; ra.B = B; ra.F = F; ra.L = L; ra.S = c.S; ra.sb = b.sb; ra.tshift = b.tshift;
-      ra.idw = (c.cfg.idontwant && b.payload >= c.cfg.idontwant) ? 1 : 0;
+      ra.ctrl = c.d_ctrl.p;
+      ra.counters = c.d_counters.p; ra.delta = b.delta;
       const uint64_t need = (total + TB - 1) / TB;
       const unsigned grid = (unsigned)std::min<uint64_t>(need, (uint64_t)dev_cus * split_blocks_per_cu(c));
       if (v & 8) {  // frontier segments: one per scan wave
@@ -1025,25 +963,11 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
           ra.gl_idx = c.d_gl_idx.p;
           ra.gl_cnt = c.d_gl_cnt.p;
           ra.nonfinal = c.d_nonfinal.p;
-          ra.rel0 = c.d_rel0.p;
-          ra.habs0 = c.d_habs0.p;
-          ra.row = c.d_row.p;
-          ra.col = c.d_col.p;
-          ra.hb_ns = c.cfg.heartbeat_ns;
-          ra.seed = c.cfg.seed;
-          ra.gossip = 1;
           if ((v & 10) == 10) {
             ra.tgmin = c.d_tgmin.p;
             ra.tnf = c.d_tnf.p;
             ra.tstamp = c.d_tstamp.p;
           }
-          if (churn) {
-            ra.ring_tgt = c.d_ring_tgt.p;
-            ra.ring_tcnt = c.d_ring_tcnt.p;
-          }
-          ra.hist = c.cfg.history_gossip;
-          ra.d_lazy = c.cfg.d_lazy;
-          ra.gf_milli = c.cfg.gossip_factor_milli;
         }
       }
       uint32_t launch = 0;
@@ -1108,9 +1032,6 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       }
     }
     if (!done) {
-      if (c.traffic && gossip)
-        c.fail(GS_EUNSUPPORTED, "per-peer traffic covers eager forwarding; lazy gossip sends IWANT "
-                                "answers in this batch");
       if (gossip && !lanes32)
         c.fail(GS_EUNSUPPORTED, "lazy gossip changes this batch and the push path needs "
                                 "peers*batch*FP < 2^32: use a smaller batch");

@@ -228,7 +228,7 @@ __device__ __forceinline__ uint64_t uplink_start(uint64_t* busy, size_t bi, bool
 #pragma unroll
     for (int g = FP - 1; g >= 0; g--) if (kk[g] != INF64) first = g;
     if (first >= 0) {
-      uint64_t cb = busy[bi];
+      uint64_t cb = busy ? busy[bi] : 0;  // no busy array: the FIFO starts empty (gs_traffic.h)
       uint64_t pk = 0;
       int pg = -1;
 #pragma unroll
@@ -250,7 +250,7 @@ __device__ __forceinline__ uint64_t uplink_start(uint64_t* busy, size_t bi, bool
         pk = bk;
         pg = bg;
       }
-      if (lane - gb == first) busy[bi] = cb;
+      if (busy && lane - gb == first) busy[bi] = cb;
     }
   }
   return start;
@@ -597,6 +597,87 @@ __device__ __forceinline__ bool pair_lt(uint64_t k1, uint32_t w1, uint64_t k2, u
   return k1 < k2 || (k1 == k2 && w1 < w2);
 }
 
+// gossip_targets(u, hab) (libp2p-gossipsub emit_gossip, upstream; DESIGN.md
+// §2.7): the r smallest (rng(GOSSIP, u, h, w), w) among u's non-mesh
+// connections (online ones under churn, over the epoch's mesh), r =
+// max(D_lazy, floor(factor * |non-mesh|)) capped at |non-mesh|; fn(w) per
+// target in that order. The caller checks that u gossips at hab.
+template <class Fn>
+__device__ __forceinline__ void for_each_gossip_target(const RelaxArgs& a, uint32_t u, uint64_t hab, Fn&& fn) {
+  const uint32_t h = (uint32_t)hab;
+  uint32_t mrow[MESH_W];
+  const uint32_t* mrp = a.mesh + (size_t)u * MESH_W;
+  if (a.churn) {
+    mrp = ep_mesh(a, hab, u);
+    if (a.ring_tcnt) {  // targets of (u, h) precomputed with the epoch's snapshot (k_gossip_targets)
+      const size_t ti = (size_t)((uint32_t)hab % a.ring_R) * a.N + u;
+      const uint32_t rc = a.ring_tcnt[ti];
+      if (rc != GT_NONE) {
+        for (uint32_t q = 0; q < rc; q++) fn(a.ring_tgt[ti * GT_W + q]);
+        return;
+      }
+    }
+  }
+  const uint4* rp = reinterpret_cast<const uint4*>(mrp);
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const uint4 x = rp[q];
+    mrow[4 * q] = x.x & 0xFFFFFFu; mrow[4 * q + 1] = x.y & 0xFFFFFFu;
+    mrow[4 * q + 2] = x.z & 0xFFFFFFu; mrow[4 * q + 3] = x.w & 0xFFFFFFu;
+  }
+  // r smallest (rng(GOSSIP, u, h, w), w) among non-mesh connections. The
+  // first GOSSIP_R_REG stay sorted in registers (static indices: no
+  // scratch); r depends on |non-mesh|, so it is cut after counting, and
+  // the rare targets beyond GOSSIP_R_REG are found by rescanning for the
+  // next smallest pair.
+  uint64_t kk[GOSSIP_R_REG];
+  uint32_t ww[GOSSIP_R_REG];
+#pragma unroll
+  for (int q = 0; q < (int)GOSSIP_R_REG; q++) { kk[q] = ~0ull; ww[q] = ~0u; }
+  uint32_t nonmesh = 0;
+  const uint64_t e0 = a.row[u], e1 = a.row[u + 1];
+  auto eligible = [&](uint32_t w) {
+    bool inm = false;
+#pragma unroll
+    for (int q = 0; q < (int)MESH_W; q++) inm |= mrow[q] == w;
+    return !inm && !(a.churn && ep_off(a, hab, w));
+  };
+  for (uint64_t e = e0; e < e1; e++) {
+    const uint32_t w = a.col[e];
+    if (!eligible(w)) continue;
+    nonmesh++;
+    const uint64_t rk = rng(a.seed, P_GOSSIP, u, h, w);
+    if (!pair_lt(rk, w, kk[GOSSIP_R_REG - 1], ww[GOSSIP_R_REG - 1])) continue;
+#pragma unroll
+    for (int q = (int)GOSSIP_R_REG - 1; q > 0; q--) {  // insert, shifting the larger pairs up
+      if (pair_lt(rk, w, kk[q - 1], ww[q - 1])) { kk[q] = kk[q - 1]; ww[q] = ww[q - 1]; }
+      else if (pair_lt(rk, w, kk[q], ww[q])) { kk[q] = rk; ww[q] = w; }
+    }
+    if (pair_lt(rk, w, kk[0], ww[0])) { kk[0] = rk; ww[0] = w; }
+  }
+  uint32_t r = (uint32_t)(((uint64_t)nonmesh * a.gf_milli) / 1000);
+  if (r < a.d_lazy) r = a.d_lazy;
+  if (r > nonmesh) r = nonmesh;
+#pragma unroll
+  for (int q = 0; q < (int)GOSSIP_R_REG; q++)
+    if ((uint32_t)q < r) fn(ww[q]);
+  uint64_t pk = kk[GOSSIP_R_REG - 1];
+  uint32_t pw = ww[GOSSIP_R_REG - 1];
+  for (uint32_t q = GOSSIP_R_REG; q < r; q++) {  // rare: more than GOSSIP_R_REG targets
+    uint64_t bk = ~0ull;
+    uint32_t bw = ~0u;
+    for (uint64_t e = e0; e < e1; e++) {
+      const uint32_t w = a.col[e];
+      if (!eligible(w)) continue;
+      const uint64_t rk = rng(a.seed, P_GOSSIP, u, h, w);
+      if (pair_lt(pk, pw, rk, w) && pair_lt(rk, w, bk, bw)) { bk = rk; bw = w; }
+    }
+    fn(bw);
+    pk = bk;
+    pw = bw;
+  }
+}
+
 template <int FP>
 __global__ __launch_bounds__(TB) void k_gossip(RelaxArgs a) {
   __shared__ BucketLds L;
@@ -610,7 +691,6 @@ __global__ __launch_bounds__(TB) void k_gossip(RelaxArgs a) {
   const int lane = threadIdx.x & 63;
   const uint32_t n = __builtin_amdgcn_readfirstlane(a.gl_cnt[wave]);
   const size_t seg = (size_t)wave * a.gl_cap;
-  const uint64_t smask = (1ull << a.sb) - 1;
   uint64_t nmin = INF64, iw = 0;
   uint32_t err = 0;
   for (uint32_t i = lane; i < n; i += 64) {
@@ -623,12 +703,10 @@ __global__ __launch_bounds__(TB) void k_gossip(RelaxArgs a) {
     const uint64_t ser = L.su[sv];
     const uint64_t r0 = a.rel0[m];
     const uint64_t j0 = first_hb(t, r0, a.hb_ns);
-    uint32_t mrow[MESH_W];
     for (uint32_t k = 0; k < a.hist; k++) {
       const uint64_t T = r0 + (j0 + k) * a.hb_ns;
       if (T + L.lmax[sv] < lo || T + L.lmin[sv] >= hi) continue;
       const uint64_t hab = a.habs0[m] + j0 + k;
-      const uint32_t h = (uint32_t)hab;
       auto ihave = [&](uint32_t w) {  // v's IHAVE to w; IWANT + answer if w has not seen it
         const uint32_t sw = a.stage[w];
         const uint64_t ti = T + L.lat[sv * S + sw];
@@ -652,79 +730,10 @@ __global__ __launch_bounds__(TB) void k_gossip(RelaxArgs a) {
           nmin = nk < nmin ? nk : nmin;
         }
       };
-      const uint32_t* mrp = a.mesh + (size_t)u * MESH_W;
-      if (a.churn) {  // v gossips only while online, within the message's lifetime, over its epoch's mesh
-        if (hab > a.q0[m] + a.horizon || ep_off(a, hab, u)) continue;
-        mrp = ep_mesh(a, hab, u);
-        if (a.ring_tcnt) {  // targets of (u, h) precomputed with the epoch's snapshot (k_gossip_targets)
-          const size_t ti = (size_t)((uint32_t)hab % a.ring_R) * a.N + u;
-          const uint32_t rc = a.ring_tcnt[ti];
-          if (rc != GT_NONE) {
-            for (uint32_t q = 0; q < rc; q++) ihave(a.ring_tgt[ti * GT_W + q]);
-            continue;
-          }
-        }
-      }
-      const uint4* rp = reinterpret_cast<const uint4*>(mrp);
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const uint4 x = rp[q];
-        mrow[4 * q] = x.x & 0xFFFFFFu; mrow[4 * q + 1] = x.y & 0xFFFFFFu;
-        mrow[4 * q + 2] = x.z & 0xFFFFFFu; mrow[4 * q + 3] = x.w & 0xFFFFFFu;
-      }
-      // r smallest (rng(GOSSIP, u, h, w), w) among non-mesh connections. The
-      // first GOSSIP_R_REG stay sorted in registers (static indices: no
-      // scratch); r depends on |non-mesh|, so it is cut after counting, and
-      // the rare targets beyond GOSSIP_R_REG are found by rescanning for the
-      // next smallest pair.
-      uint64_t kk[GOSSIP_R_REG];
-      uint32_t ww[GOSSIP_R_REG];
-#pragma unroll
-      for (int q = 0; q < (int)GOSSIP_R_REG; q++) { kk[q] = ~0ull; ww[q] = ~0u; }
-      uint32_t nonmesh = 0;
-      const uint64_t e0 = a.row[u], e1 = a.row[u + 1];
-      auto eligible = [&](uint32_t w) {
-        bool inm = false;
-#pragma unroll
-        for (int q = 0; q < (int)MESH_W; q++) inm |= mrow[q] == w;
-        return !inm && !(a.churn && ep_off(a, hab, w));
-      };
-      for (uint64_t e = e0; e < e1; e++) {
-        const uint32_t w = a.col[e];
-        if (!eligible(w)) continue;
-        nonmesh++;
-        const uint64_t rk = rng(a.seed, P_GOSSIP, u, h, w);
-        if (!pair_lt(rk, w, kk[GOSSIP_R_REG - 1], ww[GOSSIP_R_REG - 1])) continue;
-#pragma unroll
-        for (int q = (int)GOSSIP_R_REG - 1; q > 0; q--) {  // insert, shifting the larger pairs up
-          if (pair_lt(rk, w, kk[q - 1], ww[q - 1])) { kk[q] = kk[q - 1]; ww[q] = ww[q - 1]; }
-          else if (pair_lt(rk, w, kk[q], ww[q])) { kk[q] = rk; ww[q] = w; }
-        }
-        if (pair_lt(rk, w, kk[0], ww[0])) { kk[0] = rk; ww[0] = w; }
-      }
-      uint32_t r = (uint32_t)(((uint64_t)nonmesh * a.gf_milli) / 1000);
-      if (r < a.d_lazy) r = a.d_lazy;
-      if (r > nonmesh) r = nonmesh;
-#pragma unroll
-      for (int q = 0; q < (int)GOSSIP_R_REG; q++)
-        if ((uint32_t)q < r) ihave(ww[q]);
-      uint64_t pk = kk[GOSSIP_R_REG - 1];
-      uint32_t pw = ww[GOSSIP_R_REG - 1];
-      for (uint32_t q = GOSSIP_R_REG; q < r; q++) {  // rare: more than GOSSIP_R_REG targets
-        uint64_t bk = ~0ull;
-        uint32_t bw = ~0u;
-        for (uint64_t e = e0; e < e1; e++) {
-          const uint32_t w = a.col[e];
-          if (!eligible(w)) continue;
-          const uint64_t rk = rng(a.seed, P_GOSSIP, u, h, w);
-          if (pair_lt(pk, pw, rk, w) && pair_lt(rk, w, bk, bw)) { bk = rk; bw = w; }
-        }
-        ihave(bw);
-        pk = bk;
-        pw = bw;
-      }
+      // v gossips only while online, within the message's lifetime
+      if (a.churn && (hab > a.q0[m] + a.horizon || ep_off(a, hab, u))) continue;
+      for_each_gossip_target(a, u, hab, ihave);
     }
-    (void)smask;
   }
   nmin = wave_min(nmin);
   iw = wave_sum(iw);

@@ -26,7 +26,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GOSSIPSIM_LIB", os.path.join(HERE, "libgossipsim.so"))
-ABI_VERSION = 4
+ABI_VERSION = 5
 MESH_W = 16
 UNDELIVERED = np.uint64(0xFFFFFFFFFFFFFFFF)
 MUXERS = {"yamux": 0, "quic": 1, "mplex": 2}
@@ -97,6 +97,7 @@ SIGNATURES = {
     "gs_config_from_env": (i32, [P(GsConfig), ctypes.c_char_p, ctypes.c_size_t]),
     "gs_wire_bytes": (u64, [u64, u32, u32]),
     "gs_wire_packets": (None, [u64, u32, u32, P(u64), P(u64)]),
+    "gs_control_packets": (None, [u32, u32, u32, P(u64), P(u64), P(u64)]),
     "gs_write_shadow_heartbeat": (i32, [ctypes.c_char_p, u32, P(u64), u64]),
     "gs_links_from_gml": (i32, [ctypes.c_char_p, u32, u32, P(u32), P(u64), P(u64), P(u64)]),
     "gs_shadow_hosts": (i32, [ctypes.c_char_p, u32, P(u8)]),
@@ -178,12 +179,26 @@ def wire_packets(payload, muxer="yamux", signed=True):
     return pk.value, hd.value
 
 
+CTRL_KINDS = {"ihave": 0, "iwant": 1, "ack": 2}
+
+
+def control_packets(kind, node="rust", muxer="yamux"):
+    """-> (wire bytes, packets, header bytes) of one IHAVE / IWANT RPC (one
+    message id) or one pure ACK packet (gs_control_packets)."""
+    b, pk, hd = u64(), u64(), u64()
+    lib().gs_control_packets(CTRL_KINDS.get(kind, kind), NODES.get(node, node) if isinstance(node, str) else node,
+                             MUXERS[muxer] if isinstance(muxer, str) else muxer,
+                             ctypes.byref(b), ctypes.byref(pk), ctypes.byref(hd))
+    return b.value, pk.value, hd.value
+
+
 TRAFFIC_COLS = ("tx_bytes", "rx_bytes", "tx_packets", "rx_packets", "tx_header_bytes", "rx_header_bytes",
-                "received", "published")
+                "received", "published", "tx_ctrl_packets", "rx_ctrl_packets", "tx_ctrl_header_bytes",
+                "rx_ctrl_header_bytes")
 
 
 def write_shadow_heartbeat(path, traffic, sim_seconds=900):
-    """Per-peer traffic [N, 8] as Shadow tracker "[node]" lines (shadow/summary_shadowlog.awk);
+    """Per-peer traffic [N, len(TRAFFIC_COLS)] as Shadow tracker "[node]" lines (shadow/summary_shadowlog.awk);
     sim_seconds defaults to topogen's 15-minute stop time (shadow/topogen.py:82)."""
     tr = np.ascontiguousarray(traffic, np.uint64)
     rc = lib().gs_write_shadow_heartbeat(path.encode(), tr.shape[0], _ptr(tr, u64), sim_seconds)
@@ -510,7 +525,7 @@ class Simulator:
         self._check(lib().gs_set_traffic(self.ctx, 1 if on else 0))
 
     def traffic(self):
-        """-> uint64 [N, 8] in TRAFFIC_COLS order."""
+        """-> uint64 [N, len(TRAFFIC_COLS)] in TRAFFIC_COLS order."""
         tr = np.zeros((self.peers, len(TRAFFIC_COLS)), np.uint64)
         self._check(lib().gs_get_traffic(self.ctx, _ptr(tr, u64)))
         return tr

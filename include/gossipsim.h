@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 4u
+#define GS_ABI_VERSION 5u
 
 /* Sentinel for "never delivered" in t_complete_ns. */
 #define GS_UNDELIVERED UINT64_MAX
@@ -298,12 +298,25 @@ gs_status gs_log_close(gs_log* log);
 void gs_wire_packets(uint64_t payload, uint32_t muxer, uint32_t signed_msgs, uint64_t* packets,
                      uint64_t* header_bytes);
 
-/* Columns of a per-peer traffic row (gs_get_traffic). */
+/* Wire size of one lazy-gossip control RPC carrying one message id (IHAVE:
+ * RPC{control{ihave{topic "test", id}}}, IWANT: RPC{control{iwant{id}}}; the
+ * id is 20 bytes for the rust / nim nodes' decimal hashes, 32 for go's sha256)
+ * through the muxer stack, or one pure ACK packet (header only). */
+enum { GS_CTRL_IHAVE = 0, GS_CTRL_IWANT = 1, GS_CTRL_ACK = 2 };
+void gs_control_packets(uint32_t kind, uint32_t node, uint32_t muxer, uint64_t* bytes, uint64_t* packets,
+                        uint64_t* header_bytes);
+
+/* Columns of a per-peer traffic row (gs_get_traffic). Data columns count every
+ * packet that carries bytes of a gossipsub RPC (message sends, IWANT answers,
+ * IHAVE and IWANT control RPCs); the ctrl columns count the pure TCP/QUIC ACKs
+ * (one per <= 2 data packets received, sent back to the sender). */
 enum { GS_TR_TX_BYTES = 0, GS_TR_RX_BYTES = 1, GS_TR_TX_PKTS = 2, GS_TR_RX_PKTS = 3,
        GS_TR_TX_HDR = 4, GS_TR_RX_HDR = 5,
        GS_TR_RECEIVED = 6,   /* completed messages (main.rs:94 inc_received_message)   */
        GS_TR_PUBLISHED = 7,  /* messages published (main.rs:515 inc_messages_published) */
-       GS_TRAFFIC_COLS = 8 };
+       GS_TR_TX_CTRL_PKTS = 8, GS_TR_RX_CTRL_PKTS = 9,  /* pure ACK packets            */
+       GS_TR_TX_CTRL_HDR = 10, GS_TR_RX_CTRL_HDR = 11,  /* their (header-only) bytes    */
+       GS_TRAFFIC_COLS = 12 };
 
 /* Shadow's per-host heartbeat counters for the same runs, one "[node]" line
  * per peer as Shadow's tracker logs them (recv/send bytes, then inbound and
@@ -374,14 +387,13 @@ gs_status gs_reset_stats(struct gs_ctx* ctx);
 /* 1: record HIP events around every relaxation launch and around gs_run. */
 gs_status gs_set_timing(struct gs_ctx* ctx, uint32_t enable);
 
-/* 1: account every data send of gs_run per peer (the byte counters Shadow's
- * tracker keeps per host, summary_shadowlog.awk): a flood-publish or forward
- * send of a fragment adds its wire bytes / packets / header bytes to the
- * sender's tx and the receiver's rx columns. Counted after each batch from the
- * final keys (one extra pass over them), so it is off by default. Covers
- * eager forwarding incl. IDONTWANT, and lazy gossip when it is a no-op (no
- * IWANT, gs_stats.gossip_noop_msgs); gs_run returns GS_EUNSUPPORTED for a
- * batch whose gossip sends IWANT answers, and with churn. Enabling zeroes the counters, as does
+/* 1: account every send of gs_run per peer (the counters Shadow's tracker
+ * keeps per host, summary_shadowlog.awk): flood-publish and forward sends of a
+ * fragment, lazy gossip's IHAVE and IWANT RPCs and IWANT answers, each to the
+ * sender's tx and — unless lost to churn (receiver offline or the message's
+ * lifetime over at the arrival) — the receiver's rx columns, plus the ACKs the
+ * receiver returns. Counted after each batch from the final keys (extra passes
+ * over them), so it is off by default. Enabling zeroes the counters, as does
  * gs_reset_stats. */
 gs_status gs_set_traffic(struct gs_ctx* ctx, uint32_t enable);
 /* Copy the per-peer counters out: traffic[peers][GS_TRAFFIC_COLS]. */

@@ -59,11 +59,16 @@ static uint64_t cdiv(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
  * main.rs:418-440: yamux 12 B per <=16 KiB frame, noise 18 B per <=65519 B,
  * TCP/IPv4 40 B per 1460 B segment; QUIC 65 B per 1415 B of stream data;
  * mplex 4 B per <=1 MiB frame. */
+static uint64_t stack_bytes(uint64_t frame, uint32_t muxer);
 uint64_t or_wire_bytes(uint64_t payload, uint32_t muxer, uint32_t signed_msgs) {
     uint64_t msg = pb_field(payload) + pb_field(4);
     if (signed_msgs) msg += pb_field(38) + pb_field(8) + pb_field(64);
     uint64_t rpc = pb_field(msg);
-    uint64_t frame = varint_len(rpc) + rpc;
+    return stack_bytes(varint_len(rpc) + rpc, muxer);
+}
+
+/* A length-delimited RPC frame through the muxer stack. */
+static uint64_t stack_bytes(uint64_t frame, uint32_t muxer) {
     if (muxer == 1) /* quic */
         return frame + cdiv(frame, 1415) * 65;
     uint64_t a = (muxer == 2) ? frame + cdiv(frame, 1048576) * 4 : frame + cdiv(frame, 16384) * 12;
@@ -79,6 +84,26 @@ void or_wire_packets(uint64_t payload, uint32_t muxer, uint32_t signed_msgs, uin
     uint64_t n = cdiv(w, per); /* every packet but the last is full: ceil(wire / full packet) */
     *packets = n;
     *header_bytes = n * (muxer == 1 ? 65 : 40);
+}
+
+/* Lazy-gossip control RPCs, one message id each (model constants, DESIGN.md
+ * §2.4): RPC{control: ControlMessage{ihave: ControlIHave{topic "test", id}}}
+ * or RPC{control: {iwant: ControlIWant{id}}}. The id is the node's
+ * message_id_fn output: rust DefaultHasher u64 as decimal (main.rs:73-77) and
+ * nim $hash (gossipsub-queues/main.nim:123-124), up to 20 chars, modelled at
+ * 20; go sha256 (go-test-node/main.go:26-29), 32 bytes. kind 2 = a pure ACK
+ * packet (no payload): packets 1, bytes = header = one packet header. */
+void or_ctrl_packets(uint32_t kind, uint32_t node, uint32_t muxer, uint64_t* bytes, uint64_t* packets,
+                     uint64_t* header_bytes) {
+    const uint64_t ph = muxer == 1 ? 65 : 40, per = muxer == 1 ? 1415 + 65 : 1460 + 40;
+    if (kind == 2) { *bytes = ph; *packets = 1; *header_bytes = ph; return; }
+    const uint64_t id = node == 1 ? 32 : 20;
+    const uint64_t cm = kind == 0 ? pb_field(pb_field(4) + pb_field(id)) : pb_field(pb_field(id));
+    const uint64_t rpc = pb_field(cm);
+    const uint64_t w = stack_bytes(varint_len(rpc) + rpc, muxer);
+    *bytes = w;
+    *packets = cdiv(w, per);
+    *header_bytes = *packets * ph;
 }
 
 /* ---------------------------------------------------------- link model ---- */
@@ -639,19 +664,49 @@ static uint32_t gossip_targets(const or_params* p, const uint64_t* row_ptr, cons
     return r;
 }
 
+/* Per-peer traffic (gs_set_traffic; columns = the ABI's GS_TR_*): a send adds
+ * its bytes / packets / header bytes to the sender's tx; a send that arrives
+ * adds them to the receiver's rx, and the receiver answers every 2 packets
+ * with a pure ACK (delayed ACK, one per <= 2 segments; a model constant), which
+ * lands in its tx ctrl and the sender's rx ctrl columns. Lost sends (churn)
+ * are not retransmitted: the connection is gone. */
+typedef struct {
+    uint64_t* tr;
+    uint64_t w, pk, hd;          /* one data fragment send (or_wire_bytes / or_wire_packets) */
+    uint64_t ihw, ihpk, ihhd;    /* one IHAVE RPC */
+    uint64_t iww, iwpk, iwhd;    /* one IWANT RPC */
+    uint64_t ack;                /* header bytes of one ACK packet */
+} tr_t;
+enum { TRC_TXB = 0, TRC_RXB = 1, TRC_TXP = 2, TRC_RXP = 3, TRC_TXH = 4, TRC_RXH = 5, TRC_RCV = 6, TRC_PUB = 7,
+       TRC_TXCP = 8, TRC_RXCP = 9, TRC_TXCH = 10, TRC_RXCH = 11 };
+static void tr_send(const tr_t* T, uint32_t x, uint64_t b, uint64_t pk, uint64_t hd) {
+    uint64_t* r = T->tr + (size_t)x * OR_TR_COLS;
+    r[TRC_TXB] += b; r[TRC_TXP] += pk; r[TRC_TXH] += hd;
+}
+static void tr_deliver(const tr_t* T, uint32_t s, uint32_t x, uint64_t b, uint64_t pk, uint64_t hd) {
+    uint64_t* r = T->tr + (size_t)x * OR_TR_COLS;
+    uint64_t* q = T->tr + (size_t)s * OR_TR_COLS;
+    const uint64_t acks = (pk + 1) / 2;
+    r[TRC_RXB] += b; r[TRC_RXP] += pk; r[TRC_RXH] += hd;
+    r[TRC_TXCP] += acks; r[TRC_TXCH] += acks * T->ack;
+    q[TRC_RXCP] += acks; q[TRC_RXCH] += acks * T->ack;
+}
+
 /* Events in time order; at equal time arrivals (type 0) precede IHAVE
- * arrivals (type 1), so "w has seen m by t" reads w's finality at the IHAVE. */
+ * arrivals (types 1, 2), so "w has seen m by t" reads w's finality at the
+ * IHAVE. Type 2 = an IHAVE whose answer will be lost (churn; traffic only). */
 
 /* Lazy gossip of (v, f) first received at t_v (relative to t_pub): IHAVE at
  * the history_gossip heartbeats T >= t_v to gossip_targets(v, h); the IHAVE
  * reaches w at T + lat(v,w); an IWANT comes back and v's answer lands at
  * T + 2 lat(v,w) + lat(w,v) + ser_up(v) + dn. Under churn v
  * gossips only while online, and an IHAVE or answer reaching an offline w is
- * lost (§2.8). */
+ * lost (§2.8). With traffic (tm) the IHAVE sends are counted here. */
 static int sched_gossip(const or_params* p, const uint64_t* row_ptr, const uint32_t* col, const mesh_src* ms,
                         const uint8_t* stage, uint32_t S, const uint64_t* lat_ns, const uint64_t* su,
                         const uint64_t* sd, uint64_t t_pub, uint32_t v, uint32_t f, uint64_t tv, uint64_t hp,
-                        uint32_t tshift, uint32_t sb, uint64_t tmax, sel_t* gsel, uint32_t* gtg, heap_t* h) {
+                        uint32_t tshift, uint32_t sb, uint64_t tmax, sel_t* gsel, uint32_t* gtg, heap_t* h,
+                        const tr_t* tm) {
     const uint32_t N = p->peers;
     const uint64_t hmask = (1ull << HOP_BITS) - 1;
     const uint64_t tabs = t_pub + tv;
@@ -670,11 +725,18 @@ static int sched_gossip(const or_params* p, const uint64_t* row_ptr, const uint3
             const uint64_t dn = sd[sw] > su[sv] ? sd[sw] - su[sv] : 0;
             const uint64_t A = ti + lat_ns[sw * S + sv] + su[sv] + lat_ns[sv * S + sw] + dn;
             if (A > tmax) return -5;
+            int lost_i = 0, lost_a = 0;
             if (ms->snap_off) {
                 const int64_t si = slot_of(ms, epoch_at(p, t_pub + ti)), sa = slot_of(ms, epoch_at(p, t_pub + A));
-                if (si < 0 || sa < 0 || offline_at(ms, N, si, w) || offline_at(ms, N, sa, w)) continue;
+                lost_i = si < 0 || offline_at(ms, N, si, w);
+                lost_a = sa < 0 || offline_at(ms, N, sa, w);
             }
-            ev_t ge = {ti, (A << tshift) | ((hp + 1) << sb) | v, w, f, 1};
+            if (tm) {
+                tr_send(tm, v, tm->ihw, tm->ihpk, tm->ihhd);
+                if (!lost_i) tr_deliver(tm, v, w, tm->ihw, tm->ihpk, tm->ihhd);
+            }
+            if (lost_i || (lost_a && !tm)) continue;
+            ev_t ge = {ti, (A << tshift) | ((hp + 1) << sb) | v, w, f, lost_a ? 2u : 1u};
             if (heap_push(h, ge)) return -2;
         }
     }
@@ -753,11 +815,13 @@ static int run_impl(const or_params* p, const uint64_t* row_ptr, const uint32_t*
         uint32_t Fe = collide ? 1 : Fm;
         F = Fm;
         NF = (size_t)N * F;
-        uint64_t wire = or_wire_bytes(payload, p->muxer, p->signed_msgs), wpk = 0, whd = 0;
-        or_wire_packets(payload, p->muxer, p->signed_msgs, &wpk, &whd);
-        /* per-peer traffic: a send adds to the sender's tx, an arrival to the receiver's rx */
-#define TR_SEND(x) if (tr) { tr[(size_t)(x) * 8 + 0] += wire; tr[(size_t)(x) * 8 + 2] += wpk; tr[(size_t)(x) * 8 + 4] += whd; }
-#define TR_RECV(x) if (tr) { tr[(size_t)(x) * 8 + 1] += wire; tr[(size_t)(x) * 8 + 3] += wpk; tr[(size_t)(x) * 8 + 5] += whd; }
+        uint64_t wire = or_wire_bytes(payload, p->muxer, p->signed_msgs);
+        tr_t trm = {tr, wire, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        or_wire_packets(payload, p->muxer, p->signed_msgs, &trm.pk, &trm.hd);
+        or_ctrl_packets(0, p->node, p->muxer, &trm.ihw, &trm.ihpk, &trm.ihhd);
+        or_ctrl_packets(1, p->node, p->muxer, &trm.iww, &trm.iwpk, &trm.iwhd);
+        { uint64_t x, y; or_ctrl_packets(2, p->node, p->muxer, &trm.ack, &x, &y); }
+        const tr_t* T = tr ? &trm : NULL;
         const uint64_t tp = sched_t[mi];
         mesh_src msg_ms = *ms0;
         msg_ms.h_cap = epoch_at(p, tp) + p->churn_horizon;
@@ -777,13 +841,13 @@ static int run_impl(const or_params* p, const uint64_t* row_ptr, const uint32_t*
             continue;
         }
         /* publisher: self key, flood through the uplink FIFO */
-        if (tr) tr[(size_t)pub * 8 + 7] += 1; /* published (main.rs:515) */
+        if (tr) tr[(size_t)pub * OR_TR_COLS + TRC_PUB] += 1; /* published (main.rs:515) */
         uint32_t sp = stage[pub];
         for (uint32_t f = 0; f < Fe; f++) { best[(size_t)pub * F + f] = (uint64_t)pub; fin[(size_t)pub * F + f] = 1; }
         if (p->lazy_gossip)
             for (uint32_t f = 0; f < Fe; f++)
                 if ((rc = sched_gossip(p, row_ptr, col, ms, stage, S, lat_ns, su, sd, tp, pub, f, 0, 0, tshift, sb,
-                                       tmax, gsel, gtg, &h)))
+                                       tmax, gsel, gtg, &h, T)))
                     goto out;
         uint32_t deg = 0;
         if (p->flood_publish) {
@@ -802,12 +866,12 @@ static int run_impl(const or_params* p, const uint64_t* row_ptr, const uint32_t*
                 if (arr > tmax) { rc = -5; goto out; }
                 uint64_t key = (arr << tshift) | (1ull << sb) | pub;
                 st->relaxations++;
-                TR_SEND(pub);
+                if (T) tr_send(T, pub, wire, T->pk, T->hd);
                 if (ms->snap_off) {  /* lost: past the lifetime, or w offline at the arrival */
                     const int64_t sl = slot_of(ms, epoch_at(p, tp + arr));
                     if (sl < 0 || offline_at(ms, N, sl, w)) continue;
                 }
-                TR_RECV(w);
+                if (T) tr_deliver(T, pub, w, wire, T->pk, T->hd);
                 if (key < best[(size_t)w * F + f]) best[(size_t)w * F + f] = key;
                 ev_t ev = {arr, key, w, f, 0};
                 if (heap_push(&h, ev)) { rc = -2; goto out; }
@@ -815,12 +879,18 @@ static int run_impl(const or_params* p, const uint64_t* row_ptr, const uint32_t*
         while (h.n) {
             ev_t ev = heap_pop(&h);
             size_t idx = (size_t)ev.dst * F + ev.frag;
-            if (ev.type == 1) { /* IHAVE arrives at w: IWANT unless w already has it */
+            if (ev.type != 0) { /* IHAVE arrives at w: IWANT unless w already has it */
                 if (fin[idx]) continue;
+                const uint32_t v = (uint32_t)(ev.key & smask);
+                if (T) { /* w's IWANT to v, v's answer to w (lost with type 2) */
+                    tr_send(T, ev.dst, T->iww, T->iwpk, T->iwhd);
+                    tr_deliver(T, ev.dst, v, T->iww, T->iwpk, T->iwhd);
+                    tr_send(T, v, wire, T->pk, T->hd);
+                    if (ev.type == 1) tr_deliver(T, v, ev.dst, wire, T->pk, T->hd);
+                }
+                if (ev.type == 2) continue;
                 st->gossip_iwant++;
                 st->relaxations++;
-                TR_SEND(ev.key & smask); /* the IWANT answer: src -> w */
-                TR_RECV(ev.dst);
                 if (ev.key < best[idx]) {
                     best[idx] = ev.key;
                     ev_t ne = {ev.key >> tshift, ev.key, ev.dst, ev.frag, 0};
@@ -851,7 +921,7 @@ static int run_impl(const or_params* p, const uint64_t* row_ptr, const uint32_t*
             }
             if (p->lazy_gossip &&
                 (rc = sched_gossip(p, row_ptr, col, ms, stage, S, lat_ns, su, sd, tp, u, ev.frag, t, hp, tshift, sb,
-                                   tmax, gsel, gtg, &h)))
+                                   tmax, gsel, gtg, &h, T)))
                 goto out;
             uint64_t start = (Fe > 1 && busy[u] > t) ? busy[u] : t;
             busy[u] = start + (uint64_t)n * su[su_];
@@ -863,12 +933,12 @@ static int run_impl(const or_params* p, const uint64_t* row_ptr, const uint32_t*
                 if (arr > tmax) { rc = -5; goto out; }
                 uint64_t key = (arr << tshift) | ((hp + 1) << sb) | u;
                 st->relaxations++;
-                TR_SEND(u);
+                if (T) tr_send(T, u, wire, T->pk, T->hd);
                 if (ms->snap_off) {
                     const int64_t sa = slot_of(ms, epoch_at(p, tp + arr));
                     if (sa < 0 || offline_at(ms, N, sa, w)) continue;
                 }
-                TR_RECV(w);
+                if (T) tr_deliver(T, u, w, wire, T->pk, T->hd);
                 size_t wi = (size_t)w * F + ev.frag;
                 if (key < best[wi]) {
                     best[wi] = key;
@@ -892,7 +962,7 @@ static int run_impl(const or_params* p, const uint64_t* row_ptr, const uint32_t*
             hops[o] = (uint8_t)((mk >> sb) & hmask);
             uint64_t ms_ = trel / 1000000ULL;
             st->deliveries++;
-            if (tr) tr[(size_t)u * 8 + 6] += 1; /* received (main.rs:94) */
+            if (tr) tr[(size_t)u * OR_TR_COLS + TRC_RCV] += 1; /* received (main.rs:94) */
             st->latency_sum_ms += ms_;
             if (ms_ > st->latency_max_ms) st->latency_max_ms = ms_;
         }
@@ -925,9 +995,10 @@ int or_run_churn(const or_params* p, const uint64_t* row_ptr, const uint32_t* co
                     sched_frags, n_msgs, t_complete, hops, st, NULL);
 }
 
-/* or_run plus per-peer traffic tr[N][8] (tx bytes, rx bytes, tx packets, rx
- * packets, tx header bytes, rx header bytes, completed messages, published
- * messages), accumulated (caller zeroes). */
+/* or_run plus per-peer traffic tr[N][OR_TR_COLS] (tx bytes, rx bytes, tx
+ * packets, rx packets, tx header bytes, rx header bytes, completed messages,
+ * published messages, tx / rx ACK packets, tx / rx ACK header bytes; see
+ * tr_t), accumulated (caller zeroes). */
 int or_run_traffic(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
                    const uint32_t* mesh, const uint8_t* cnt, const uint8_t* stage, uint32_t S,
                    const uint64_t* lat_ns, const uint64_t* bw_up, const uint64_t* bw_dn,
@@ -935,6 +1006,19 @@ int or_run_traffic(const or_params* p, const uint64_t* row_ptr, const uint32_t* 
                    const uint32_t* sched_frags, uint64_t n_msgs, uint64_t* t_complete, uint8_t* hops,
                    or_stats* st, uint64_t* tr) {
     mesh_src ms = {mesh, cnt, NULL, NULL, NULL, 0, 0, 0};
+    return run_impl(p, row_ptr, col, &ms, stage, S, lat_ns, bw_up, bw_dn, sched_t, sched_pub, sched_size,
+                    sched_frags, n_msgs, t_complete, hops, st, tr);
+}
+
+/* or_run_churn plus the per-peer traffic of or_run_traffic. */
+int or_run_churn_traffic(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
+                         const uint32_t* snap_mesh, const uint8_t* snap_cnt, const uint8_t* snap_off,
+                         uint32_t h_lo, uint32_t n_snap, const uint8_t* stage, uint32_t S,
+                         const uint64_t* lat_ns, const uint64_t* bw_up, const uint64_t* bw_dn,
+                         const uint64_t* sched_t, const uint32_t* sched_pub, const uint32_t* sched_size,
+                         const uint32_t* sched_frags, uint64_t n_msgs, uint64_t* t_complete, uint8_t* hops,
+                         or_stats* st, uint64_t* tr) {
+    mesh_src ms = {NULL, NULL, snap_mesh, snap_cnt, snap_off, h_lo, n_snap, 0};
     return run_impl(p, row_ptr, col, &ms, stage, S, lat_ns, bw_up, bw_dn, sched_t, sched_pub, sched_size,
                     sched_frags, n_msgs, t_complete, hops, st, tr);
 }

@@ -44,11 +44,23 @@ uint64_t or_rng(uint64_t seed, uint32_t purpose, uint32_t a, uint32_t b, uint32_
 uint64_t or_wire_bytes(uint64_t payload, uint32_t muxer, uint32_t signed_msgs);
 void or_wire_packets(uint64_t payload, uint32_t muxer, uint32_t signed_msgs, uint64_t* packets,
                      uint64_t* header_bytes);
+/* kind 0 IHAVE, 1 IWANT (one message id), 2 a pure ACK packet. */
+void or_ctrl_packets(uint32_t kind, uint32_t node, uint32_t muxer, uint64_t* bytes, uint64_t* packets,
+                     uint64_t* header_bytes);
+/* Per-peer traffic columns (the C ABI's GS_TR_*). */
+#define OR_TR_COLS 12
 int or_run_traffic(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
                    const uint32_t* mesh, const uint8_t* cnt, const uint8_t* stage, uint32_t S,
                    const uint64_t* lat_ns, const uint64_t* bw_up, const uint64_t* bw_dn,
                    const uint64_t* sched_t, const uint32_t* sched_pub, const uint32_t* sched_size,
                    const uint32_t* sched_frags, uint64_t n_msgs, uint64_t* t_complete, uint8_t* hops, struct or_stats* st, uint64_t* tr);
+int or_run_churn_traffic(const or_params* p, const uint64_t* row_ptr, const uint32_t* col,
+                         const uint32_t* snap_mesh, const uint8_t* snap_cnt, const uint8_t* snap_off,
+                         uint32_t h_lo, uint32_t n_snap, const uint8_t* stage, uint32_t S,
+                         const uint64_t* lat_ns, const uint64_t* bw_up, const uint64_t* bw_dn,
+                         const uint64_t* sched_t, const uint32_t* sched_pub, const uint32_t* sched_size,
+                         const uint32_t* sched_frags, uint64_t n_msgs, uint64_t* t_complete, uint8_t* hops,
+                         struct or_stats* st, uint64_t* tr);
 int or_topogen_links(uint32_t S, uint32_t bl, uint32_t bh, uint32_t ll, uint32_t lh,
                      uint32_t mode, uint64_t* lat_ns, uint64_t* bw_bps);
 uint32_t or_dials_per_peer(const or_params* p);

@@ -62,6 +62,7 @@ def lib():
         L.or_wire_bytes.restype = u64
         L.or_wire_bytes.argtypes = [u64, u32, u32]
         L.or_wire_packets.argtypes = [u64, u32, u32, P(u64), P(u64)]
+        L.or_ctrl_packets.argtypes = [u32, u32, u32, P(u64), P(u64), P(u64)]
         L.or_run_traffic.argtypes = [P(OrParams), P(u64), P(u32), P(u32), P(u8), P(u8), u32, P(u64),
                                      P(u64), P(u64), P(u64), P(u32), P(u32), P(u32), u64, P(u64), P(u8),
                                      P(OrStats), P(u64)]
@@ -81,6 +82,7 @@ def lib():
         L.or_run_churn.argtypes = [P(OrParams), P(u64), P(u32), P(u32), P(u8), P(u8), u32, u32, P(u8), u32,
                                    P(u64), P(u64), P(u64), P(u64), P(u32), P(u32), P(u32), u64, P(u64), P(u8),
                                    P(OrStats)]
+        L.or_run_churn_traffic.argtypes = L.or_run_churn.argtypes + [P(u64)]
         _lib = L
     return _lib
 
@@ -213,7 +215,8 @@ def _frags_ptr(sched_frags, M):
 
 
 def run_churn(p, row_ptr, col, snaps, h_lo, stage, lat, bw_up, bw_dn, sched_t, sched_pub, sched_size,
-              sched_frags=None):
+              sched_frags=None, traffic=None):
+    """traffic: optional uint64 [N, TR_COLS] accumulated per-peer counters (or_run_churn_traffic)."""
     N = p.peers
     S = lat.shape[0]
     M = len(sched_t)
@@ -229,12 +232,17 @@ def run_churn(p, row_ptr, col, snaps, h_lo, stage, lat, bw_up, bw_dn, sched_t, s
         np.ascontiguousarray(soff.reshape(-1), np.uint8)
     fa, fp = _frags_ptr(sched_frags, M)
     stage = np.ascontiguousarray(stage, np.uint8)
-    rc = lib().or_run_churn(ctypes.byref(p), _p(row_ptr, ctypes.c_uint64), _p(col, ctypes.c_uint32),
-                            _p(smesh, ctypes.c_uint32), _p(scnt, ctypes.c_uint8), _p(soff, ctypes.c_uint8),
-                            h_lo, len(scnt) // N, _p(stage, ctypes.c_uint8), S, _p(lat, ctypes.c_uint64),
-                            _p(bw_up, ctypes.c_uint64), _p(bw_dn, ctypes.c_uint64), _p(sched_t, ctypes.c_uint64),
-                            _p(sched_pub, ctypes.c_uint32), _p(sched_size, ctypes.c_uint32), fp, M,
-                            _p(tc, ctypes.c_uint64), _p(hops, ctypes.c_uint8), ctypes.byref(st))
+    args = (ctypes.byref(p), _p(row_ptr, ctypes.c_uint64), _p(col, ctypes.c_uint32),
+            _p(smesh, ctypes.c_uint32), _p(scnt, ctypes.c_uint8), _p(soff, ctypes.c_uint8),
+            h_lo, len(scnt) // N, _p(stage, ctypes.c_uint8), S, _p(lat, ctypes.c_uint64),
+            _p(bw_up, ctypes.c_uint64), _p(bw_dn, ctypes.c_uint64), _p(sched_t, ctypes.c_uint64),
+            _p(sched_pub, ctypes.c_uint32), _p(sched_size, ctypes.c_uint32), fp, M,
+            _p(tc, ctypes.c_uint64), _p(hops, ctypes.c_uint8), ctypes.byref(st))
+    if traffic is None:
+        rc = lib().or_run_churn(*args)
+    else:
+        assert traffic.dtype == np.uint64 and traffic.shape == (N, TR_COLS) and traffic.flags.c_contiguous
+        rc = lib().or_run_churn_traffic(*args, _p(traffic, ctypes.c_uint64))
     if rc:
         raise ValueError("or_run_churn rc=%d" % rc)
     stats = {n: getattr(st, n) for n, _ in OrStats._fields_}
@@ -247,9 +255,20 @@ def wire_packets(payload, muxer=0, signed=1):
     return pk.value, hd.value
 
 
+def ctrl_packets(kind, node=0, muxer=0):
+    """(bytes, packets, header bytes) of one IHAVE (kind 0) / IWANT (1) RPC or one ACK (2)."""
+    b, pk, hd = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    lib().or_ctrl_packets(kind, node, muxer, ctypes.byref(b), ctypes.byref(pk), ctypes.byref(hd))
+    return b.value, pk.value, hd.value
+
+
+# per-peer traffic columns (gossipsim.h GS_TR_*)
+TR_COLS = 12
+
+
 def run(p, row_ptr, col, mesh, cnt, stage, lat, bw_up, bw_dn, sched_t, sched_pub, sched_size, sched_frags=None,
         traffic=None, threads=0):
-    """traffic: optional uint64 [N, 8] accumulated per-peer counters (or_run_traffic);
+    """traffic: optional uint64 [N, TR_COLS] accumulated per-peer counters (or_run_traffic);
     sched_frags: chunks per message (0 = p.fragments); threads > 0: messages in
     parallel on that many host threads (or_run_mt)."""
     N = p.peers
@@ -276,7 +295,7 @@ def run(p, row_ptr, col, mesh, cnt, stage, lat, bw_up, bw_dn, sched_t, sched_pub
     elif traffic is None:
         rc = lib().or_run(*args)
     else:
-        assert traffic.dtype == np.uint64 and traffic.shape == (N, 8) and traffic.flags.c_contiguous
+        assert traffic.dtype == np.uint64 and traffic.shape == (N, TR_COLS) and traffic.flags.c_contiguous
         rc = lib().or_run_traffic(*args, _p(traffic, ctypes.c_uint64))
     if rc:
         raise ValueError("or_run rc=%d" % rc)
@@ -285,7 +304,7 @@ def run(p, row_ptr, col, mesh, cnt, stage, lat, bw_up, bw_dn, sched_t, sched_pub
 
 
 def simulate(p, stages=1, links=(50, 50, 50, 50), mode=0, sched=None, max_hb=400, traffic=False):
-    """Whole pipeline on the CPU: links -> topology -> mesh -> run (+ per-peer traffic [N, 8])."""
+    """Whole pipeline on the CPU: links -> topology -> mesh -> run (+ per-peer traffic [N, TR_COLS])."""
     bl, bh, ll, lh = links
     lat, bw = topogen_links(stages, bl, bh, ll, lh, mode)
     stage = (np.arange(p.peers) % stages).astype(np.uint8)
@@ -295,16 +314,17 @@ def simulate(p, stages=1, links=(50, 50, 50, 50), mode=0, sched=None, max_hb=400
     frags = sched[3] if len(sched) > 3 else None
     out = dict(lat=lat, bw=bw, stage=stage, row_ptr=row_ptr, col=col, flags=flags, mesh=mesh,
                cnt=cnt, epochs=epochs)
+    tr = np.zeros((p.peers, TR_COLS), np.uint64) if traffic else None
     if p.churn_ppm:  # time-varying mesh: snapshots of every epoch the schedule can use
         h_lo = min(epoch_at(p, x) for x in t)
         h_hi = max(epoch_at(p, x) for x in t) + p.churn_horizon
         snaps = mesh_churn(p, row_ptr, col, flags0, stage, lat, h_lo, h_hi)
-        tc, hops, stats = run_churn(p, row_ptr, col, snaps, h_lo, stage, lat, bw, bw, t, pub, size, frags)
+        tc, hops, stats = run_churn(p, row_ptr, col, snaps, h_lo, stage, lat, bw, bw, t, pub, size, frags,
+                                    traffic=tr)
         out.update(snaps=snaps, h_lo=h_lo)
     else:
-        tr = np.zeros((p.peers, 8), np.uint64) if traffic else None
         tc, hops, stats = run(p, row_ptr, col, mesh, cnt, stage, lat, bw, bw, t, pub, size, frags, traffic=tr)
-        if traffic:
-            out["traffic"] = tr
+    if traffic:
+        out["traffic"] = tr
     out.update(t_complete=tc, hops=hops, stats=stats)
     return out

@@ -152,12 +152,18 @@ def test_node_presets(node):
         sim.run(_sched(1, 800, size=small - 3))
 
 
+_IWANT_PHASE = T0 % 1_000_000_000  # a heartbeat at the publish instant: IHAVEs race the eager wave
+
+
 @pytest.mark.parametrize("kw", [dict(), dict(fragments=3), dict(flood_publish=0), dict(node=1, fragments=2),
-                                dict(muxer=1, signed_msgs=0)])
+                                dict(muxer=1, signed_msgs=0), dict(lazy_gossip=0),
+                                dict(hb_phase_ns=_IWANT_PHASE), dict(hb_phase_ns=_IWANT_PHASE, fragments=4),
+                                dict(node=2, hb_phase_ns=_IWANT_PHASE)])
 def test_peer_traffic_counters(kw):
-    """gs_set_traffic: per-peer tx/rx bytes, packets and header bytes (Shadow's
-    tracker counters) bit-exact against the oracle, on the pull path and (go
-    preset: IDONTWANT) the push path, accumulated over two runs."""
+    """gs_set_traffic: per-peer tx/rx bytes, packets, header bytes and ACKs
+    (Shadow's tracker counters) bit-exact against the oracle, on the pull path
+    (gossip a no-op: IHAVEs only), the push path (go preset: IDONTWANT) and
+    with gossip sending IWANTs, accumulated over two runs."""
     p = oracle.params_for(kw.pop("node", 0), peers=900, seed=71, **kw)
     sched = _sched(12, 900)
     ref = oracle.simulate(p, 5, (50, 150, 40, 130), sched=sched, traffic=True)
@@ -166,25 +172,38 @@ def test_peer_traffic_counters(kw):
     sim.run((sched[0][:5], sched[1][:5], sched[2][:5]))
     sim.run((sched[0][5:], sched[1][5:], sched[2][5:]))
     np.testing.assert_array_equal(sim.traffic(), ref["traffic"])
+    if p.hb_phase_ns == _IWANT_PHASE:
+        assert ref["stats"]["gossip_iwant"] > 0
     sim.reset_stats()
     assert not sim.traffic().any()
 
 
-def test_peer_traffic_unsupported_modes():
-    """Traffic counters cover eager forwarding: lazy gossip that sends IWANT
-    answers (heartbeat at the publish instant) and churn are refused."""
-    p = oracle.params(peers=300, seed=72, lazy_gossip=1, hb_phase_ns=T0 % 1_000_000_000)
+@pytest.mark.parametrize("kw", [dict(), dict(fragments=2), dict(flood_publish=0, lazy_gossip=0)])
+def test_peer_traffic_under_churn(kw):
+    """Config #3 semantics (heterogeneous links, churn, lazy gossip with IWANTs):
+    lost sends count at the sender only, ACKs only for arrivals; bit-exact
+    against the oracle."""
+    N = 1500
+    p = oracle.params(peers=N, seed=73, churn_ppm=20000, heartbeat_ns=200_000_000,
+                      hb_phase_ns=T0 - 2_000_000_000, churn_horizon=10, **kw)
+    sched = _sched(24, N)
+    ref = oracle.simulate(p, 5, (50, 150, 40, 130), sched=sched, traffic=True)
+    sim, _ = gpu_sim(p, 5, (50, 150, 40, 130), batch=8)
+    sim.set_traffic(True)
+    res = sim.run(sched)
+    np.testing.assert_array_equal(res["t_complete"], ref["t_complete"])
+    tr = sim.traffic()
+    np.testing.assert_array_equal(tr, ref["traffic"])
+    assert tr[:, 0].sum() > tr[:, 1].sum()
+
+
+def test_peer_traffic_needs_enabling():
+    """gs_get_traffic before gs_set_traffic(ctx, 1) is a state error (the
+    partitioned mode refuses traffic: test_gpu_partition)."""
+    p = oracle.params(peers=300, seed=72)
     sim, _ = gpu_sim(p, 1, (50, 50, 50, 50))
     with pytest.raises(gossipsim.GossipSimError, match="GS_ESTATE"):
         sim.traffic()
-    sim.set_traffic(True)
-    with pytest.raises(gossipsim.GossipSimError, match="GS_EUNSUPPORTED"):
-        sim.run(_sched(2, 300))
-    p = oracle.params(peers=300, seed=72, churn_ppm=10000, hb_phase_ns=gossipsim.SHADOW_START_NS)
-    sim, _ = gpu_sim(p, 1, (50, 50, 50, 50))
-    sim.set_traffic(True)
-    with pytest.raises(gossipsim.GossipSimError, match="GS_EUNSUPPORTED"):
-        sim.run(_sched(2, 300))
 
 
 def test_shadow_experiment_files_drive_the_run():

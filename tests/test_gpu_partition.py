@@ -83,7 +83,8 @@ def test_partitioned_p8_10k_peers(frags):
 def test_partitioned_unsupported_modes_fail_loudly():
     """Lazy gossip runs in partitioned mode only as the proven no-op (every part
     checks its peers at gs_part_finish); a heartbeat at the publish instant
-    makes IWANTs possible and the batch fails instead of dropping them."""
+    makes IWANTs possible and the batch fails instead of dropping them.
+    IDONTWANT and per-peer traffic are refused at gs_part_begin."""
     p = oracle.params(peers=300, seed=55, lazy_gossip=1, hb_phase_ns=T0 % 1_000_000_000)
     (s,) = _parts(p, 1, (50, 50, 50, 50), 1, 4)
     with pytest.raises(gossipsim.GossipSimError, match="GS_EUNSUPPORTED"):
@@ -94,6 +95,11 @@ def test_partitioned_unsupported_modes_fail_loudly():
         s.part_begin(_sched(4, 300))
     with pytest.raises(gossipsim.GossipSimError, match="GS_ESTATE"):
         s.part_relax(1, 0, 0)
+    p = oracle.params(peers=300, seed=57)
+    (s,) = _parts(p, 1, (50, 50, 50, 50), 1, 4)
+    s.set_traffic(True)  # no traffic pass in partitioned mode
+    with pytest.raises(gossipsim.GossipSimError, match="GS_EUNSUPPORTED"):
+        s.part_begin(_sched(4, 300))
 
 
 # ---- the library-driven protocol behind the C ABI (gs_comm_*, gs_run_partitioned) ----

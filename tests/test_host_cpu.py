@@ -66,10 +66,23 @@ def test_wire_packets_match_oracle(muxer, signed):
         assert hd == pk * (65 if muxer == 1 else 40) and pk >= 1
 
 
+def test_control_packets_match_oracle():
+    for node in ("rust", "go", "nim"):
+        for muxer in ("yamux", "quic", "mplex"):
+            for kind in ("ihave", "iwant", "ack"):
+                got = gossipsim.control_packets(kind, node, muxer)
+                assert got == oracle.ctrl_packets(gossipsim.CTRL_KINDS[kind], gossipsim.NODES[node],
+                                                  gossipsim.MUXERS[muxer])
+
+
 def _shadow_log(tmp_path):
-    p = oracle.params(peers=80, seed=5, fragments=2)
+    """A config #3-style report (heterogeneous links, lazy gossip with IWANTs,
+    churn) from the oracle's per-peer traffic."""
+    p = oracle.params(peers=300, seed=5, fragments=2, churn_ppm=20000, heartbeat_ns=200_000_000,
+                      hb_phase_ns=gossipsim.T0_NS - 2_000_000_000, churn_horizon=10)
     t = np.uint64(gossipsim.T0_NS) + np.arange(3, dtype=np.uint64) * np.uint64(10 ** 9)
     r = oracle.simulate(p, 3, (20, 80, 30, 60), sched=(t, np.array([1, 40, 79]), np.full(3, 15000)), traffic=True)
+    assert r["stats"]["gossip_iwant"] > 0
     out = str(tmp_path / "shadowlog")
     gossipsim.write_shadow_heartbeat(out, r["traffic"], sim_seconds=900)
     return r["traffic"], out
@@ -82,10 +95,13 @@ def test_shadow_heartbeat_lines(tmp_path):
     for u, ln in enumerate(lines):
         f = ln.split()
         assert f[4] == "[pod-%d]" % u and f[8] == "[node]"
-        arr = re.split(",|;", f[9])
-        assert int(arr[1]) == tr[u, 1] and int(arr[2]) == tr[u, 0]
-        assert int(arr[30]) == tr[u, 3] and int(arr[31]) == tr[u, 1] and int(arr[38]) == tr[u, 1] - tr[u, 5]
-        assert int(arr[42]) == tr[u, 2] and int(arr[43]) == tr[u, 0] and int(arr[48]) == tr[u, 2]
+        arr = [int(x) for x in re.split(",|;", f[9])]
+        assert arr[1] == tr[u, 1] + tr[u, 11] and arr[2] == tr[u, 0] + tr[u, 10]
+        ri, ro = 6 + 24, 6 + 36  # remote in / out groups (0-based; awk's arr[idx] is 1-based)
+        assert arr[ri:ri + 9] == [tr[u, 3] + tr[u, 9], tr[u, 1] + tr[u, 11], tr[u, 9], tr[u, 11], 0, 0,
+                                  tr[u, 3], tr[u, 5], tr[u, 1] - tr[u, 5]]
+        assert arr[ro:ro + 9] == [tr[u, 2] + tr[u, 8], tr[u, 0] + tr[u, 10], tr[u, 8], tr[u, 10], 0, 0,
+                                  tr[u, 2], tr[u, 4], tr[u, 0] - tr[u, 4]]
 
 
 @pytest.mark.skipif(not os.path.isdir(REF_SHADOW) or not shutil.which("awk"),
@@ -93,12 +109,17 @@ def test_shadow_heartbeat_lines(tmp_path):
 def test_shadow_heartbeat_round_trips_through_reference_awk(tmp_path):
     tr, out = _shadow_log(tmp_path)
     got = subprocess.check_output(["awk", "-f", os.path.join(REF_SHADOW, "summary_shadowlog.awk"), out]).decode()
+    s = lambda c: int(tr[:, c].sum())
     m = re.search(r"Total Bytes Received :\s+(\d+)\s+Total Bytes Transferred :\s+(\d+)", got)
-    assert m and int(m.group(1)) == int(tr[:, 1].sum()) and int(m.group(2)) == int(tr[:, 0].sum())
-    m = re.search(r"Remote IN pkt:\s+(\d+)\s+Bytes :\s+(\d+).*DataPkt:\s+(\d+)\s+DataHdrBytes:\s+(\d+)\s+DataBytes\s+(\d+)",
-                  got)
-    assert m and [int(x) for x in m.groups()] == [int(tr[:, 3].sum()), int(tr[:, 1].sum()), int(tr[:, 3].sum()),
-                                                  int(tr[:, 5].sum()), int((tr[:, 1] - tr[:, 5]).sum())]
+    assert m and int(m.group(1)) == s(1) + s(11) and int(m.group(2)) == s(0) + s(10)
+    num = r"\s+(\d+)\s+"
+    pat = ("Remote %s pkt:" + num + "Bytes :" + num + "ctrlPkt:" + num + "ctrlHdrBytes:" + num + "DataPkt:" + num +
+           "DataHdrBytes:" + num + r"DataBytes\s+(\d+)")
+    m = re.search(pat % "IN", got)
+    assert m and [int(x) for x in m.groups()] == [s(3) + s(9), s(1) + s(11), s(9), s(11), s(3), s(5), s(1) - s(5)]
+    m = re.search(pat.replace("Bytes :" + num, r"Bytes :\s+(\d*)\s+") % "OUT", got)  # the awk prints an unset name
+    assert m and [int(x) for x in m.groups()[2:]] == [s(8), s(10), s(2), s(4), s(0) - s(4)]
+    assert s(0) > s(1)  # churn: lost sends
 
 
 def test_node_metrics_openmetrics(tmp_path):

@@ -366,9 +366,10 @@ def test_fragment_layout_per_node(node, bad, good):
 
 @pytest.mark.parametrize("kw", [dict(), dict(fragments=3), dict(flood_publish=0), dict(idontwant=1000)])
 def test_traffic_identities(kw):
-    """Every send is one relaxation and, without churn, one receipt: sum(tx) =
-    sum(rx) = R x wire bytes; a non-publisher's sends = its forwards."""
-    p = oracle.params(peers=300, seed=7, **kw)
+    """Eager forwarding only: every send is one relaxation and, without churn,
+    one receipt: sum(tx) = sum(rx) = R x wire bytes; a non-publisher's sends
+    = its forwards; every receipt of k packets returns ceil(k/2) ACKs."""
+    p = oracle.params(peers=300, seed=7, lazy_gossip=0, **kw)
     t = np.uint64(T0) + np.arange(4, dtype=np.uint64) * np.uint64(10 ** 9)
     r = oracle.simulate(p, 5, (50, 150, 40, 130), sched=(t, np.array([3, 50, 120, 299]), np.full(4, 15000)),
                         traffic=True)
@@ -381,6 +382,58 @@ def test_traffic_identities(kw):
     assert tr[:, 6].sum() == st["deliveries"] and tr[:, 7].sum() == st["messages"] == 4
     got = (r["t_complete"] != np.iinfo(np.uint64).max).sum(axis=0) - np.bincount([3, 50, 120, 299], minlength=300)
     np.testing.assert_array_equal(tr[:, 6], got)
+    ack = oracle.ctrl_packets(2, p.node, p.muxer)[0]
+    np.testing.assert_array_equal(tr[:, 8], tr[:, 3] // pk * ((pk + 1) // 2))  # ACKs sent per packets received
+    assert tr[:, 8].sum() == tr[:, 9].sum() and (tr[:, 10] == tr[:, 8] * ack).all() and (tr[:, 11] == tr[:, 9] * ack).all()
+    np.testing.assert_array_equal(tr[:, 9], tr[:, 2] // pk * ((pk + 1) // 2))  # ACKs back per send
+
+
+def test_control_rpc_sizes():
+    """IHAVE / IWANT RPCs with one 20-byte (rust / nim) or 32-byte (go) id:
+    protobuf sizes + yamux 12 + noise 18 + one TCP/IPv4 header (QUIC 65)."""
+    ih = 1 + 1 + (1 + 1 + (1 + 1 + 4) + (1 + 1 + 20))  # RPC.control{ihave{topic, id}}
+    iw = 1 + 1 + (1 + 1 + (1 + 1 + 20))              # RPC.control{iwant{id}}
+    assert oracle.ctrl_packets(0, 0, 0) == (1 + ih + 12 + 18 + 40, 1, 40)
+    assert oracle.ctrl_packets(1, 0, 0) == (1 + iw + 12 + 18 + 40, 1, 40)
+    assert oracle.ctrl_packets(1, 1, 0)[0] == oracle.ctrl_packets(1, 0, 0)[0] + 12
+    assert oracle.ctrl_packets(0, 0, 1) == (1 + ih + 65, 1, 65)
+    assert oracle.ctrl_packets(2, 0, 0) == (40, 1, 40) and oracle.ctrl_packets(2, 2, 1) == (65, 1, 65)
+
+
+@pytest.mark.parametrize("case", ["noop", "iwant", "churn"])
+def test_traffic_with_gossip_and_churn(case):
+    """Lazy gossip adds IHAVE RPCs (every target, every history heartbeat) and,
+    for targets that had not seen the message, IWANT RPCs + answers; churn
+    loses sends (counted at the sender only) and their ACKs."""
+    kw = dict(peers=400, seed=17, hb_phase_ns=T0 % 1_000_000_000)  # heartbeat at the publish instant
+    if case == "noop":  # first gossip heartbeat 2.997 s after every publish: all IHAVEs land late
+        kw.update(heartbeat_ns=3_000_000_000, hb_phase_ns=T0 - 3_000_000)
+    if case == "churn":
+        kw.update(churn_ppm=30000, hb_phase_ns=T0 - 4_000_000_000, heartbeat_ns=200_000_000, churn_horizon=8)
+    p = oracle.params(**kw)
+    t = np.uint64(T0) + np.arange(5, dtype=np.uint64) * np.uint64(3 * 10 ** 9)
+    sched = (t, np.array([3, 50, 120, 299, 7]), np.full(5, 15000))
+    r = oracle.simulate(p, 5, (50, 150, 40, 130), sched=sched, traffic=True)
+    tr, st = r["traffic"].astype(np.int64), r["stats"]
+    W = oracle.wire_bytes(15000, 0, 1)
+    ihw = oracle.ctrl_packets(0)[0]
+    iww = oracle.ctrl_packets(1)[0]
+    ack = oracle.ctrl_packets(2)[0]
+    # tx = R x W (eager sends + IWANT answers) + IHAVEs + IWANTs; R counts only answers that arrive
+    extra = tr[:, 0].sum() - st["relaxations"] * W - st["gossip_iwant"] * iww
+    if case == "noop":
+        assert st["gossip_iwant"] == 0 and extra > 0 and extra % ihw == 0
+        e = oracle.simulate(oracle.params(lazy_gossip=0, **kw), 5, (50, 150, 40, 130), sched=sched, traffic=True)
+        d = tr - e["traffic"].astype(np.int64)  # gossip adds IHAVE traffic and nothing else
+        assert (d[:, 0] % ihw == 0).all() and (d[:, 6:8] == 0).all() and d[:, 0].sum() == d[:, 1].sum()
+    if case == "iwant":
+        assert st["gossip_iwant"] > 0 and extra > 0 and extra % ihw == 0
+    if case == "churn":
+        assert tr[:, 0].sum() > tr[:, 1].sum()  # lost sends: tx without rx
+    else:
+        assert tr[:, 0].sum() == tr[:, 1].sum() and tr[:, 2].sum() == tr[:, 3].sum()
+    assert tr[:, 8].sum() == tr[:, 9].sum() and (tr[:, 10] == tr[:, 8] * ack).all()
+    assert tr[:, 6].sum() == st["deliveries"]
 
 
 def test_stats_identities():
