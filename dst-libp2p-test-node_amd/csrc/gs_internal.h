@@ -104,6 +104,8 @@ struct Ctx {
   uint32_t ring_R = 0;
   uint64_t churn_state = 0, ring_lo = 1, ring_hi = 0;  // mesh state epoch; valid ring epochs
   DevBuf<uint8_t> d_mcnt;    // [N]
+  DevBuf<uint8_t> d_pst;     // event-driven churn epochs: [PS_PLANES][N] per-peer flags and counts
+  DevBuf<uint64_t> d_offlin; // offline bitsets of a run of churn epochs, [epochs + 1][(N+63)/64]
   DevBuf<uint32_t> d_bar;    // k_epochs grid barrier counter
 
   // dissemination (per batch)

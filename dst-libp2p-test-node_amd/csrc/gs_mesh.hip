@@ -4,7 +4,7 @@
 // The reference runs libp2p-gossipsub's heartbeat every 1 s
 // (rust-test-node/src/main.rs:228) with mesh_n/low/high 6/4/8, outbound min 3,
 // prune back-off 60 s (main.rs:229-236); scoring is inert (main.rs:260-269).
-// Each epoch is three one-thread-per-peer kernels over the CSR:
+// Each epoch is three row steps over the CSR (a group of lanes per peer):
 //   A  heartbeat decisions (graft to D below D_lo, prune to D above D_hi
 //      keeping D_out outbound, graft outbound peers when short),
 //   B  GRAFT handling at the receiver in (latency, id) order (back-off and
@@ -12,11 +12,12 @@
 //   C  PRUNEs and rejections applied, both ends back off.
 // Random choices use per-(peer, epoch, candidate) keys: take the r smallest.
 //
-// Churn: each epoch first draws the offline set (k_offline),
-// drops mesh links of offline peers without back-off (k_disconnect), and the
-// heartbeat grafts online candidates only. gs_run keeps a ring of per-epoch
-// snapshots {mesh ELL, offline bitset} (slot = epoch mod R) that the
-// relaxation kernels index by the epoch each event falls in.
+// Churn: each epoch has its offline set (offline_draw), drops
+// mesh links of offline peers without back-off, and the heartbeat grafts
+// online candidates only. The epochs run event-driven (ev_epochs: a row runs
+// a step only when the step can change it). gs_run keeps a ring of per-epoch
+// snapshots {mesh ELL, offline bitset, IHAVE targets} (slot = epoch mod R)
+// that the relaxation kernels index by the epoch each event falls in.
 #include "gs_internal.h"
 
 namespace gs {
@@ -38,28 +39,59 @@ struct MeshArgs {
   uint64_t seed;
   uint32_t N, S, epoch, bo, d, d_lo, d_hi, d_out;
   uint32_t sub;  // the subscription epoch 0: handshake-ordered grafts
+  // event-driven churn epochs (run_epochs): per-peer state planes, nullptr when
+  // every row runs every step
+  uint8_t* pst;              // [PS_PLANES][N]
+  const uint64_t* off_prev;  // offline bitsets of the previous and the next epoch
+  const uint64_t* off_next;  // (nullptr: the last epoch of the run)
+};
+
+// Planes of MeshArgs::pst. A row runs the heavy per-row code of an epoch step
+// only when one of its flags says the step can change it; the flags are set by
+// the rows (or the offline draw) that cause the change.
+enum : uint32_t {
+  PS_PROPD = 0,   // the row wrote GRAFT/PRUNE proposals this epoch (cleared by its next heartbeat step)
+  PS_INBOX = 1,   // a neighbour proposed a GRAFT to the row
+  PS_PRUNED = 2,  // a neighbour PRUNEd the row
+  PS_NBROFF = 3,  // a mesh neighbour went offline this epoch
+  PS_DIRTY = 4,   // the row's mesh flags changed this epoch (recount, re-extract its ELL row)
+  PS_MC = 5,      // mesh count after the last epoch
+  PS_OC = 6,      // outbound mesh count after the last epoch
+  PS_PLANES = 7
 };
 
 __device__ __forceinline__ bool is_off(const uint64_t* off, uint32_t u) {
   return off && ((off[u >> 6] >> (u & 63)) & 1);
 }
 
-// Offline set of epoch h: one bit per peer, one u64 word per wave.
-__global__ __launch_bounds__(TB) void k_offline(uint32_t N, uint64_t seed, uint32_t ppm, uint32_t down, uint64_t h,
-                                                uint64_t* off) {
-  const uint32_t u = blockIdx.x * TB + threadIdx.x;
-  const uint64_t m = __ballot(u < N && offline_draw(seed, ppm, down, u, h));
-  if ((threadIdx.x & 63) == 0 && u < N) off[u >> 6] = m;
+// the calling lane's group bits of a wave ballot
+template <int G>
+__device__ __forceinline__ uint64_t gballot(bool p) {
+  const uint64_t m = __ballot(p);
+  if constexpr (G == 64) {
+    return m;
+  } else {
+    const int gbase = (threadIdx.x & 63) & ~(G - 1);
+    return (m >> gbase) & ((1ull << G) - 1);
+  }
 }
 
 // Links to offline peers leave the mesh (a disconnect, not a PRUNE: no back-off).
 // One peer per wave, lane per CSR entry.
+// Returns (group-uniform) whether a mesh link was dropped.
 template <int G>
-__device__ __forceinline__ void row_disconnect(const MeshArgs& a, uint32_t u) {
+__device__ __forceinline__ bool row_disconnect(const MeshArgs& a, uint32_t u) {
   const bool ou = is_off(a.off, u);
   const uint64_t b = a.row[u], en = a.row[u + 1];
-  for (uint64_t e = b + (threadIdx.x & (G - 1)); e < en; e += G)
-    if (ou || is_off(a.off, a.col[e])) a.flags[e] &= (uint8_t)~F_MESH;
+  bool ch = false;
+  for (uint64_t e = b + (threadIdx.x & (G - 1)); e < en; e += G) {
+    const uint8_t f = a.flags[e];
+    if ((f & F_MESH) && (ou || is_off(a.off, a.col[e]))) {
+      a.flags[e] = (uint8_t)(f & ~F_MESH);
+      ch = true;
+    }
+  }
+  return gballot<G>(ch) != 0;
 }
 template <int G>
 __global__ __launch_bounds__(TB) void k_disconnect(MeshArgs a) {
@@ -80,18 +112,6 @@ static_assert(MAX_DEG % 64 == 0 && HB_PER_LANE <= 4, "k_heartbeat covers MAX_DEG
 // row has at most 4*16 entries: four rows per wave, four times the memory
 // requests in flight of the latency-bound one-row-per-wave form). Lane l of a
 // group holds entries k*G + l, k < HB_PER_LANE.
-
-// the calling lane's group bits of a wave ballot
-template <int G>
-__device__ __forceinline__ uint64_t gballot(bool p) {
-  const uint64_t m = __ballot(p);
-  if constexpr (G == 64) {
-    return m;
-  } else {
-    const int gbase = (threadIdx.x & 63) & ~(G - 1);
-    return (m >> gbase) & ((1ull << G) - 1);
-  }
-}
 
 // group argmin over (key, idx); ~0u if every key is INF64
 template <int G>
@@ -176,6 +196,17 @@ __device__ __forceinline__ void row_heartbeat(const MeshArgs& a, uint32_t u) {
     }
     return;
   }
+  // event-driven epochs: the receivers of this row's proposals are flagged
+  // for GRAFT handling / apply (the lane holding the chosen entry stores)
+  auto mark = [&](uint32_t sel, uint32_t plane) {
+    if (!a.pst) return;
+    uint32_t ws = 0;
+#pragma unroll
+    for (int k = 0; k < HB_PER_LANE; k++)
+      if ((uint32_t)k == (sel / G)) ws = w[k];
+    a.pst[(size_t)plane * a.N + ws] = 1;
+  };
+  bool proposed = false;
   uint32_t mm = m, oo = o;
   uint32_t graft = 0;  // bit k: entry k*64 + lane grafted this epoch
   if (m < a.d_lo) {  // graft mesh_n - |mesh| random eligible peers
@@ -194,7 +225,9 @@ __device__ __forceinline__ void row_heartbeat(const MeshArgs& a, uint32_t u) {
         drop_key<G>(key, sel);
         graft |= 1u << (sel / G);
         a.prop[b + sel] |= PR_GRAFT;
+        mark(sel, PS_INBOX);
       }
+      proposed = true;
       mm++;
       oo += flag_of(sel) & F_OUT;
     }
@@ -219,7 +252,11 @@ __device__ __forceinline__ void row_heartbeat(const MeshArgs& a, uint32_t u) {
         if (oo <= a.d_out) continue;
         oo--;
       }
-      if ((int)(sel % G) == lane) a.prop[b + sel] |= PR_PRUNE;
+      if ((int)(sel % G) == lane) {
+        a.prop[b + sel] |= PR_PRUNE;
+        mark(sel, PS_PRUNED);
+      }
+      proposed = true;
       removed++;
       mm--;
     }
@@ -241,8 +278,14 @@ __device__ __forceinline__ void row_heartbeat(const MeshArgs& a, uint32_t u) {
       if ((int)(sel % G) == lane) {
         drop_key<G>(key, sel);
         a.prop[b + sel] |= PR_GRAFT;
+        mark(sel, PS_INBOX);
       }
+      proposed = true;
     }
+  }
+  if (a.pst && proposed && lane == 0) {
+    a.pst[(size_t)PS_PROPD * a.N + u] = 1;
+    a.pst[(size_t)PS_DIRTY * a.N + u] = 1;
   }
 }
 
@@ -252,21 +295,12 @@ __global__ __launch_bounds__(TB) void k_heartbeat(MeshArgs a) {
   if (u < a.N) row_heartbeat<G>(a, u);  // group-uniform
 }
 
-// Disconnects and heartbeat decisions of an epoch in one pass: both read and
-// write only the peer's own row.
-template <int G>
-__global__ __launch_bounds__(TB) void k_disc_heartbeat(MeshArgs a) {
-  const uint32_t u = (blockIdx.x * TB + threadIdx.x) / G;
-  if (u >= a.N) return;  // group-uniform
-  row_disconnect<G>(a, u);
-  row_heartbeat<G>(a, u);
-}
-
 // GRAFT handling at receiver w, one peer per wave: the proposals of w's
 // neighbours are found in parallel (lane per entry), then taken in arrival
 // order — (latency u->w, id), by wave argmin — with the running mesh size c.
+// Returns (group-uniform) whether a GRAFT was accepted (w's mesh changed).
 template <int G>
-__device__ __forceinline__ void row_handle_graft(const MeshArgs& a, uint32_t w) {
+__device__ __forceinline__ bool row_handle_graft(const MeshArgs& a, uint32_t w) {
   const int lane = threadIdx.x & (G - 1);
   const int gbase = (threadIdx.x & 63) & ~(G - 1);
   (void)gbase;
@@ -297,6 +331,7 @@ __device__ __forceinline__ void row_handle_graft(const MeshArgs& a, uint32_t w) 
   }
   const int fpack = (int)(f[0] | (f[1] << 8) | (f[2] << 16) | (f[3] << 24));
   const int ppack = (int)(p[0] | (p[1] << 8) | (p[2] << 16) | (p[3] << 24));
+  bool acc = false;
   for (;;) {
     uint64_t bk;
     uint32_t bi;
@@ -319,8 +354,12 @@ __device__ __forceinline__ void row_handle_graft(const MeshArgs& a, uint32_t w) 
       else a.prop[rs] |= PR_ACCEPT;
       if (!in_mesh && !rej) a.flags[e] = (uint8_t)(fs | F_MESH);
     }
-    if (!in_mesh && !rej) c++;
+    if (!in_mesh && !rej) {
+      c++;
+      acc = true;
+    }
   }
+  return acc;
 }
 template <int G>
 __global__ __launch_bounds__(TB) void k_handle_graft(MeshArgs a) {
@@ -417,13 +456,11 @@ __global__ __launch_bounds__(TB) void k_extract(MeshArgs a, uint32_t* mesh, uint
 // selection is serial compute (one rng per connection, an 8-deep sorted
 // insert in registers with static indices), which a wave per peer would
 // leave mostly idle.
-__global__ __launch_bounds__(TB) void k_gossip_targets(const uint64_t* __restrict__ row, const uint32_t* __restrict__ col,
-                                                       const uint32_t* __restrict__ mesh, const uint64_t* __restrict__ off,
-                                                       uint32_t N, uint64_t seed, uint32_t h, uint32_t d_lazy,
-                                                       uint32_t gf_milli, uint32_t* __restrict__ tgt,
-                                                       uint8_t* __restrict__ tcnt) {
-  const uint32_t u = blockIdx.x * TB + threadIdx.x;
-  if (u >= N) return;
+__device__ __forceinline__ void gossip_targets_row(const uint64_t* __restrict__ row, const uint32_t* __restrict__ col,
+                                                   const uint32_t* __restrict__ mesh, const uint64_t* __restrict__ off,
+                                                   uint32_t N, uint64_t seed, uint32_t h, uint32_t d_lazy,
+                                                   uint32_t gf_milli, uint32_t* __restrict__ tgt,
+                                                   uint8_t* __restrict__ tcnt, uint32_t u) {
   if (is_off(off, u)) {  // offline peers gossip nothing (k_gossip skips them first)
     tcnt[u] = 0;
     return;
@@ -468,6 +505,34 @@ __global__ __launch_bounds__(TB) void k_gossip_targets(const uint64_t* __restric
   for (int q = 0; q < (int)GT_W; q++)
     if ((uint32_t)q < r) tgt[(size_t)u * GT_W + q] = ww[q];
   tcnt[u] = (uint8_t)r;
+}
+
+__global__ __launch_bounds__(TB) void k_gossip_targets(const uint64_t* __restrict__ row, const uint32_t* __restrict__ col,
+                                                       const uint32_t* __restrict__ mesh, const uint64_t* __restrict__ off,
+                                                       uint32_t N, uint64_t seed, uint32_t h, uint32_t d_lazy,
+                                                       uint32_t gf_milli, uint32_t* __restrict__ tgt,
+                                                       uint8_t* __restrict__ tcnt) {
+  const uint32_t u = blockIdx.x * TB + threadIdx.x;
+  if (u < N) gossip_targets_row(row, col, mesh, off, N, seed, h, d_lazy, gf_milli, tgt, tcnt, u);
+}
+
+// The same for the ring slots of epochs h0 + blockIdx.y (one launch after a
+// run of event-driven epochs: the targets depend only on each epoch's
+// snapshot, so they are not on the epochs' sequential path).
+__global__ __launch_bounds__(TB) void k_gossip_targets_range(const uint64_t* __restrict__ row,
+                                                             const uint32_t* __restrict__ col,
+                                                             const uint32_t* __restrict__ ring_mesh,
+                                                             const uint64_t* __restrict__ ring_off, uint32_t N,
+                                                             uint32_t w64, uint32_t R, uint64_t seed, uint64_t h0,
+                                                             uint32_t d_lazy, uint32_t gf_milli,
+                                                             uint32_t* __restrict__ ring_tgt,
+                                                             uint8_t* __restrict__ ring_tcnt) {
+  const uint32_t u = blockIdx.x * TB + threadIdx.x;
+  const uint64_t h = h0 + blockIdx.y;
+  const size_t slot = (size_t)(h % R);
+  if (u < N)
+    gossip_targets_row(row, col, ring_mesh + slot * N * MESH_W, ring_off + slot * w64, N, seed, (uint32_t)h, d_lazy,
+                       gf_milli, ring_tgt + slot * N * GT_W, ring_tcnt + slot * N, u);
 }
 
 // ---- fused churn epochs (one cooperative launch for a run of epochs) ----
@@ -605,19 +670,6 @@ __device__ __forceinline__ void grid_barrier(uint32_t* bar, uint32_t nblocks, ui
   __syncthreads();
 }
 
-// Step C of a churn epoch for one peer per group: apply the epoch's
-// decisions, then (own row only, no barrier needed) the ELL snapshot into the
-// ring slot and the peer's IHAVE targets of epoch h.
-template <int G>
-__global__ __launch_bounds__(TB) void k_apply_snap(MeshArgs a, uint32_t* mesh, uint32_t* tgt, uint8_t* tcnt, uint32_t h,
-                                                   uint32_t d_lazy, uint32_t gf_milli) {
-  const uint32_t u = (blockIdx.x * TB + threadIdx.x) / G;
-  if (u >= a.N) return;  // group-uniform
-  row_apply<G>(a, u);
-  row_extract<G>(a, u, mesh);
-  if (tgt) row_targets<G>(a, u, h, d_lazy, gf_milli, tgt, tcnt);
-}
-
 struct EpochArgs {
   MeshArgs m;
   uint32_t* bar;         // grid barrier counter (zeroed before the launch)
@@ -662,6 +714,156 @@ __global__ __launch_bounds__(TB) void k_epochs(EpochArgs e) {
     }
   }
 }
+
+// ---- event-driven churn epochs (the default run_epochs path) ----
+// Under churn most rows do nothing in a given epoch (1 % departures per epoch:
+// ~18 % of the rows change, most of them by one dropped link). Each step of an
+// epoch therefore tests a few per-peer flags (MeshArgs::pst) and runs the
+// row code only where the step can change the row; every rule is the one of
+// the per-row kernels above, so the result is the same mesh:
+//  heartbeat step: rows going offline, rows with a mesh neighbour going
+//    offline (flagged by that neighbour), rows outside [D_lo, D_hi] or below
+//    D_out (the only ones a heartbeat can change), rows whose last proposals
+//    must be cleared;
+//  GRAFT handling: rows a neighbour proposed to;
+//  apply: proposers and PRUNEd rows; rows whose mesh changed are recounted
+//    and re-extracted into the ring slot, the others copy their previous row.
+// Offline bitsets and IHAVE targets do not depend on the epoch sequence and
+// run batched over the whole range (k_offline_range, k_gossip_targets_range).
+
+// Mesh links of u (all, outbound) from its CSR flags.
+template <int G>
+__device__ __forceinline__ void row_counts(const MeshArgs& a, uint32_t u, uint32_t& m, uint32_t& o) {
+  const uint64_t b = a.row[u], en = a.row[u + 1];
+  m = 0;
+  o = 0;
+  for (uint64_t e0 = b; e0 < en; e0 += G) {  // group-uniform
+    const uint64_t e = e0 + (threadIdx.x & (G - 1));
+    const uint8_t f = e < en ? a.flags[e] : 0;
+    m += (uint32_t)__popcll(gballot<G>(f & F_MESH));
+    o += (uint32_t)__popcll(gballot<G>((f & F_MESH) && (f & F_OUT)));
+  }
+}
+
+// u goes offline at the next epoch: flag its mesh neighbours (their links to
+// u leave the mesh there).
+template <int G>
+__device__ __forceinline__ void mark_departure(const MeshArgs& a, uint32_t u) {
+  const uint64_t b = a.row[u], en = a.row[u + 1];
+  for (uint64_t e = b + (threadIdx.x & (G - 1)); e < en; e += G)
+    if (a.flags[e] & F_MESH) a.pst[(size_t)PS_NBROFF * a.N + a.col[e]] = 1;
+}
+
+// Offline bitsets of epochs h0 + y, y < gridDim.y, into lin[y] (w64 words
+// each) and, for epochs >= ring_h0 and a ring, into ring slot h % R.
+__global__ __launch_bounds__(TB) void k_offline_range(uint32_t N, uint64_t seed, uint32_t ppm, uint32_t down,
+                                                      uint64_t h0, uint64_t* lin, uint32_t w64, uint64_t* ring,
+                                                      uint32_t R, uint64_t ring_h0) {
+  const uint32_t u = blockIdx.x * TB + threadIdx.x;
+  const uint64_t h = h0 + blockIdx.y;
+  const uint64_t m = __ballot(u < N && offline_draw(seed, ppm, down, u, h));
+  if ((threadIdx.x & 63) == 0 && u < N) {
+    lin[(size_t)blockIdx.y * w64 + (u >> 6)] = m;
+    if (ring && h >= ring_h0) ring[(size_t)(h % R) * w64 + (u >> 6)] = m;
+  }
+}
+
+// Start of a run of epochs: mesh counts, and the departures of its first
+// epoch. Grid-stride, one row per group of G lanes (group-uniform loop).
+template <int G>
+__global__ __launch_bounds__(TB) void k_ev_init(MeshArgs a) {
+  const int lane = threadIdx.x & (G - 1);
+  for (uint32_t u = (blockIdx.x * TB + threadIdx.x) / G; u < a.N; u += gridDim.x * (TB / G)) {
+    uint32_t m, o;
+    row_counts<G>(a, u, m, o);
+    if (lane == 0) {
+      a.pst[(size_t)PS_MC * a.N + u] = (uint8_t)(m < 255 ? m : 255);
+      a.pst[(size_t)PS_OC * a.N + u] = (uint8_t)(o < 255 ? o : 255);
+    }
+    if (is_off(a.off, u) && !is_off(a.off_prev, u)) mark_departure<G>(a, u);
+  }
+}
+
+// One step of an event-driven epoch. A block owns EV_ROWS consecutive rows:
+// its first wave tests them one thread per row and compacts the rows the step
+// can change into LDS; then every group of G lanes takes active rows (most
+// blocks have a handful, so one round). Steps:
+enum : int { EV_HB = 0, EV_GRAFT = 1, EV_APPLY = 2 };
+constexpr uint32_t EV_ROWS = 64;
+template <int G, int STEP>
+__global__ __launch_bounds__(TB) void k_ev_step(MeshArgs a, uint32_t* mesh, const uint32_t* mesh_prev) {
+  __shared__ uint32_t act[EV_ROWS];
+  __shared__ uint32_t nact;
+  uint8_t* P = a.pst;
+  const uint32_t N = a.N;
+  const uint32_t base = blockIdx.x * EV_ROWS;
+  if (STEP == EV_APPLY && mesh && mesh_prev) {  // unchanged rows keep their ELL row: copy the block's rows
+    const uint32_t nrow = base + EV_ROWS <= N ? EV_ROWS : N - base;
+    const uint4* src = reinterpret_cast<const uint4*>(mesh_prev + (size_t)base * MESH_W);
+    uint4* dst = reinterpret_cast<uint4*>(mesh + (size_t)base * MESH_W);
+    for (uint32_t i = threadIdx.x; i < nrow * (MESH_W / 4); i += TB) dst[i] = src[i];
+  }
+  if (threadIdx.x < 64) {
+    const uint32_t u = base + threadIdx.x;
+    bool on = false;
+    if (u < N) {
+      if (STEP == EV_HB) {
+        const bool off = is_off(a.off, u), leaving = off && !is_off(a.off_prev, u);
+        const uint32_t mc = P[(size_t)PS_MC * N + u], oc = P[(size_t)PS_OC * N + u];
+        on = leaving || P[(size_t)PS_NBROFF * N + u] || P[(size_t)PS_PROPD * N + u] ||
+             (!off && (mc < a.d_lo || mc > a.d_hi || oc < a.d_out));
+      } else if (STEP == EV_GRAFT) {
+        on = P[(size_t)PS_INBOX * N + u];
+      } else {
+        on = P[(size_t)PS_PROPD * N + u] || P[(size_t)PS_PRUNED * N + u] || P[(size_t)PS_DIRTY * N + u] ||
+             (a.off_next && !is_off(a.off, u) && is_off(a.off_next, u)) || (mesh && !mesh_prev);
+      }
+    }
+    const uint64_t bm = __ballot(on);
+    if (on) act[__popcll(bm & ((1ull << threadIdx.x) - 1))] = u;
+    if (threadIdx.x == 0) nact = (uint32_t)__popcll(bm);
+  }
+  __syncthreads();  // also orders the ELL copy before the re-extracted rows
+  const int lane = threadIdx.x & (G - 1);
+  const uint32_t n = nact;
+  for (uint32_t i = threadIdx.x / G; i < n; i += TB / G) {  // group-uniform
+    const uint32_t u = act[i];
+    if (STEP == EV_HB) {
+      if (P[(size_t)PS_PROPD * N + u])  // last epoch's proposals (read by the neighbours until its apply step)
+        for (uint64_t e = a.row[u] + lane; e < a.row[u + 1]; e += G) a.prop[e] = 0;
+      if (lane == 0) {
+        P[(size_t)PS_PROPD * N + u] = 0;
+        P[(size_t)PS_NBROFF * N + u] = 0;
+      }
+      if (row_disconnect<G>(a, u) && lane == 0) P[(size_t)PS_DIRTY * N + u] = 1;
+      row_heartbeat<G>(a, u);
+    } else if (STEP == EV_GRAFT) {
+      const bool acc = row_handle_graft<G>(a, u);
+      if (lane == 0) {
+        P[(size_t)PS_INBOX * N + u] = 0;
+        if (acc) P[(size_t)PS_DIRTY * N + u] = 1;
+      }
+    } else {
+      const bool need = P[(size_t)PS_PROPD * N + u] || P[(size_t)PS_PRUNED * N + u];
+      const bool dirty = need || P[(size_t)PS_DIRTY * N + u] || (mesh && !mesh_prev);
+      if (need) row_apply<G>(a, u);
+      if (dirty) {
+        uint32_t m, o;
+        row_counts<G>(a, u, m, o);
+        if (lane == 0) {
+          P[(size_t)PS_MC * N + u] = (uint8_t)(m < 255 ? m : 255);
+          P[(size_t)PS_OC * N + u] = (uint8_t)(o < 255 ? o : 255);
+          P[(size_t)PS_DIRTY * N + u] = 0;
+          P[(size_t)PS_PRUNED * N + u] = 0;
+        }
+        if (mesh) row_extract<G>(a, u, mesh);
+      }
+      // the departures of the next epoch flag their mesh neighbours
+      if (a.off_next && !is_off(a.off, u) && is_off(a.off_next, u)) mark_departure<G>(a, u);
+    }
+  }
+}
+
 
 inline unsigned blocks(uint64_t n) { return (unsigned)((n + TB - 1) / TB); }
 
@@ -724,29 +926,77 @@ void sub_epoch(Ctx& c, MeshArgs a) {
   GS_HIP(hipGetLastError());
 }
 
-// One heartbeat epoch h >= 1 under churn: the offline set into `off`, the
-// disconnects and heartbeat decisions, GRAFT handling, then apply + the ELL
-// snapshot (+ IHAVE targets) into `mesh` / `tgt` (mesh nullptr: the mesh
-// state only, as in gs_mesh_converge).
-void churn_epoch(Ctx& c, MeshArgs& a, uint64_t h, uint64_t* off, uint32_t* mesh, uint32_t* tgt, uint8_t* tcnt) {
+// Event-driven churn epochs [h0, h1] (see k_ev_step): offline bitsets
+// of [h0-1, h1] in one launch (and into the ring), three row steps per epoch,
+// then the IHAVE targets of every ring slot written.
+void ev_epochs(Ctx& c, MeshArgs a, uint64_t h0, uint64_t h1, bool ring) {
   const uint32_t N = c.cfg.peers;
+  const uint32_t w64 = (N + 63) / 64;
   hipStream_t s = c.stream;
-  k_offline<<<blocks(N), TB, 0, s>>>(N, c.cfg.seed, c.cfg.churn_ppm, c.cfg.churn_down, h, off);
-  a.off = off;
-  a.epoch = (uint32_t)h;
+  const uint64_t E = h1 - h0 + 1;
+  // the range may be longer than the ring: only its last ring_R epochs keep
+  // their slots (offline bits and targets are written in parallel over epochs)
+  const uint64_t hr = ring && E > c.ring_R ? h1 + 1 - c.ring_R : h0;
+  c.d_offlin.alloc((size_t)(E + 1) * w64);
+  for (uint64_t y0 = 0; y0 < E + 1; y0 += 32768) {  // grid.y limit
+    const uint32_t ny = (uint32_t)std::min<uint64_t>(32768, E + 1 - y0);
+    k_offline_range<<<dim3(blocks(N), ny), TB, 0, s>>>(N, c.cfg.seed, c.cfg.churn_ppm, c.cfg.churn_down,
+                                                       h0 - 1 + y0, c.d_offlin.p + y0 * w64, w64,
+                                                       ring ? c.d_ring_off.p : nullptr, c.ring_R, hr);
+  }
+  c.d_pst.alloc((size_t)PS_PLANES * N);
+  GS_HIP(hipMemsetAsync(c.d_pst.p, 0, (size_t)PS_MC * N, s));         // flags clear
+  GS_HIP(hipMemsetAsync(c.d_pst.p + (size_t)PS_DIRTY * N, 1, N, s));  // first epoch: extract every row
   GS_HIP(hipMemsetAsync(c.d_prop.p, 0, c.nnz ? c.nnz : 1, s));
+  const uint64_t* lin = c.d_offlin.p;  // lin[y] = epoch h0 - 1 + y
+  a.pst = c.d_pst.p;
+  a.off = lin + w64;
+  a.off_prev = lin;
+  a.off_next = nullptr;
   const uint32_t G = row_group(c);
-  GS_ROWS(k_disc_heartbeat, G, N, s, a);
-  GS_ROWS(k_handle_graft, G, N, s, a);
-  if (mesh) GS_ROWS(k_apply_snap, G, N, s, a, mesh, tgt, tcnt, (uint32_t)h, c.cfg.d_lazy, c.cfg.gossip_factor_milli);
-  else GS_ROWS(k_apply, G, N, s, a);
+  if (c.num_cus == 0) {
+    hipDeviceProp_t prop;
+    c.num_cus = hipGetDeviceProperties(&prop, c.cfg.device) == hipSuccess ? prop.multiProcessorCount : 256;
+  }
+  const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(row_blocks(N, G), (uint64_t)c.num_cus * 8));
+  const unsigned sgrid = (unsigned)((N + EV_ROWS - 1) / EV_ROWS);
+#define GS_EVS(STEP, ...)                                                          \
+  do {                                                                             \
+    if (G == 16) k_ev_step<16, STEP><<<sgrid, TB, 0, s>>>(__VA_ARGS__);            \
+    else k_ev_step<64, STEP><<<sgrid, TB, 0, s>>>(__VA_ARGS__);                    \
+  } while (0)
+  if (G == 16) k_ev_init<16><<<grid, TB, 0, s>>>(a);
+  else k_ev_init<64><<<grid, TB, 0, s>>>(a);
+  for (uint64_t h = h0; h <= h1; h++) {
+    const uint64_t y = h - h0 + 1;
+    a.epoch = (uint32_t)h;
+    a.off = lin + y * w64;
+    a.off_prev = lin + (y - 1) * w64;
+    a.off_next = h < h1 ? lin + (y + 1) * w64 : nullptr;
+    uint32_t* mesh = ring ? c.d_ring_mesh.p + (size_t)(h % c.ring_R) * N * MESH_W : nullptr;
+    const uint32_t* prev = ring && h > h0 ? c.d_ring_mesh.p + (size_t)((h - 1) % c.ring_R) * N * MESH_W : nullptr;
+    GS_EVS(EV_HB, a, nullptr, nullptr);
+    GS_EVS(EV_GRAFT, a, nullptr, nullptr);
+    GS_EVS(EV_APPLY, a, mesh, prev);
+  }
+#undef GS_EVS
   GS_HIP(hipGetLastError());
+  if (ring && c.cfg.lazy_gossip && c.d_ring_tcnt.p) {
+    const uint64_t ER = h1 + 1 - hr;
+    for (uint64_t y0 = 0; y0 < ER; y0 += 32768) {
+      const uint32_t ny = (uint32_t)std::min<uint64_t>(32768, ER - y0);
+      k_gossip_targets_range<<<dim3(blocks(N), ny), TB, 0, s>>>(
+          c.d_row.p, c.d_col.p, c.d_ring_mesh.p, c.d_ring_off.p, N, w64, c.ring_R, c.cfg.seed, hr + y0,
+          c.cfg.d_lazy, c.cfg.gossip_factor_milli, c.d_ring_tgt.p, c.d_ring_tcnt.p);
+    }
+    GS_HIP(hipGetLastError());
+  }
 }
 
-// Churn epochs [h0, h1] from the current mesh state: the fused cooperative
-// kernel (k_epochs), or the per-epoch launches when GS_MESH_FUSED=0 or the
-// device cannot launch cooperatively. off: bitsets in slots h % off_R; `ring`:
-// also the ELL snapshots (+ IHAVE targets) into the ring slots h % ring_R.
+// Churn epochs [h0, h1] from the current mesh state: event-driven (ev_epochs),
+// or with GS_MESH_FUSED=1 the cooperative kernel k_epochs (off: bitsets in
+// slots h % off_R). `ring`: also the ELL snapshots (+ IHAVE targets) into the
+// ring slots h % ring_R.
 void run_epochs(Ctx& c, MeshArgs a, uint64_t h0, uint64_t h1, uint64_t* off, uint32_t off_R, bool ring) {
   const uint32_t N = c.cfg.peers;
   const size_t w64 = ((size_t)N + 63) / 64;
@@ -755,13 +1005,7 @@ void run_epochs(Ctx& c, MeshArgs a, uint64_t h0, uint64_t h1, uint64_t* off, uin
   int coop = 0;
   (void)hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, c.cfg.device);
   if (!(fe && *fe == '1') || !coop) {
-    const bool tg = ring && c.cfg.lazy_gossip && c.d_ring_tcnt.p;
-    for (uint64_t h = h0; h <= h1; h++) {
-      const size_t slot = (size_t)(h % (ring ? c.ring_R : off_R));
-      churn_epoch(c, a, h, off + (size_t)(h % off_R) * w64, ring ? c.d_ring_mesh.p + slot * N * MESH_W : nullptr,
-                  tg ? c.d_ring_tgt.p + slot * N * GT_W : nullptr, tg ? c.d_ring_tcnt.p + slot * N : nullptr);
-    }
-    GS_HIP(hipGetLastError());
+    ev_epochs(c, a, h0, h1, ring);
     return;
   }
   EpochArgs e{};

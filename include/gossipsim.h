@@ -415,8 +415,9 @@ gs_status gs_get_traffic(struct gs_ctx* ctx, uint64_t* traffic);
  * passed to gs_part_relax must be complete when it is called (synchronise the
  * stream that gathered them). A scan whose records exceed `capacity` returns
  * GS_ERANGE with *out_n = the capacity needed and changes no state: call it
- * again with a larger buffer. IDONTWANT and lazy gossip are not supported in
- * this mode (GS_EUNSUPPORTED). Results are bit-identical to gs_run. */
+ * again with a larger buffer. IDONTWANT, churn and per-peer traffic are not
+ * supported in this mode, lazy gossip only as the proven no-op
+ * (GS_EUNSUPPORTED). Results are bit-identical to gs_run. */
 typedef struct gs_part_record {
     uint64_t key;      /* packed first-arrival key (t_rel | hops | src)          */
     uint64_t start;    /* uplink start of its forward (FIFO fold by the owner)   */

@@ -15,6 +15,10 @@ if len(sys.argv) > 2:
     c["batch"] = int(sys.argv[2])
 if len(sys.argv) > 3:
     c["msgs"] = int(sys.argv[3])
+# C3_KNOBS="lazy_gossip=0,churn_ppm=0": override config knobs (A/B of the mesh / gossip parts)
+for kv in filter(None, os.environ.get("C3_KNOBS", "").split(",")):
+    k, v = kv.split("=")
+    c["knobs"] = dict(c["knobs"], **{k: int(v)})
 sim = gossipsim.Simulator(peers=c["peers"], batch=c["batch"], fragments=c["fragments"], seed=1, **c["knobs"])
 sim.set_topogen_links(c["links"][0], *c["links"][1:])
 t0 = time.perf_counter()
