@@ -458,9 +458,10 @@ __global__ __launch_bounds__(TB) void k_extract(MeshArgs a, uint32_t* mesh, uint
 // leave mostly idle.
 __device__ __forceinline__ void gossip_targets_row(const uint64_t* __restrict__ row, const uint32_t* __restrict__ col,
                                                    const uint32_t* __restrict__ mesh, const uint64_t* __restrict__ off,
-                                                   uint32_t N, uint64_t seed, uint32_t h, uint32_t d_lazy,
-                                                   uint32_t gf_milli, uint32_t* __restrict__ tgt,
-                                                   uint8_t* __restrict__ tcnt, uint32_t u) {
+                                                   const uint8_t* __restrict__ stage, uint32_t N, uint64_t seed,
+                                                   uint32_t h, uint32_t d_lazy, uint32_t gf_milli,
+                                                   uint32_t* __restrict__ tgt, uint8_t* __restrict__ tcnt,
+                                                   uint32_t u) {
   if (is_off(off, u)) {  // offline peers gossip nothing (k_gossip skips them first)
     tcnt[u] = 0;
     return;
@@ -503,17 +504,17 @@ __device__ __forceinline__ void gossip_targets_row(const uint64_t* __restrict__ 
   }
 #pragma unroll
   for (int q = 0; q < (int)GT_W; q++)
-    if ((uint32_t)q < r) tgt[(size_t)u * GT_W + q] = ww[q];
+    if ((uint32_t)q < r) tgt[(size_t)u * GT_W + q] = ((uint32_t)stage[ww[q]] << STAGE_SHIFT) | ww[q];
   tcnt[u] = (uint8_t)r;
 }
 
 __global__ __launch_bounds__(TB) void k_gossip_targets(const uint64_t* __restrict__ row, const uint32_t* __restrict__ col,
                                                        const uint32_t* __restrict__ mesh, const uint64_t* __restrict__ off,
-                                                       uint32_t N, uint64_t seed, uint32_t h, uint32_t d_lazy,
-                                                       uint32_t gf_milli, uint32_t* __restrict__ tgt,
-                                                       uint8_t* __restrict__ tcnt) {
+                                                       const uint8_t* __restrict__ stage, uint32_t N, uint64_t seed,
+                                                       uint32_t h, uint32_t d_lazy, uint32_t gf_milli,
+                                                       uint32_t* __restrict__ tgt, uint8_t* __restrict__ tcnt) {
   const uint32_t u = blockIdx.x * TB + threadIdx.x;
-  if (u < N) gossip_targets_row(row, col, mesh, off, N, seed, h, d_lazy, gf_milli, tgt, tcnt, u);
+  if (u < N) gossip_targets_row(row, col, mesh, off, stage, N, seed, h, d_lazy, gf_milli, tgt, tcnt, u);
 }
 
 // The same for the ring slots of epochs h0 + blockIdx.y (one launch after a
@@ -522,7 +523,8 @@ __global__ __launch_bounds__(TB) void k_gossip_targets(const uint64_t* __restric
 __global__ __launch_bounds__(TB) void k_gossip_targets_range(const uint64_t* __restrict__ row,
                                                              const uint32_t* __restrict__ col,
                                                              const uint32_t* __restrict__ ring_mesh,
-                                                             const uint64_t* __restrict__ ring_off, uint32_t N,
+                                                             const uint64_t* __restrict__ ring_off,
+                                                             const uint8_t* __restrict__ stage, uint32_t N,
                                                              uint32_t w64, uint32_t R, uint64_t seed, uint64_t h0,
                                                              uint32_t d_lazy, uint32_t gf_milli,
                                                              uint32_t* __restrict__ ring_tgt,
@@ -531,7 +533,7 @@ __global__ __launch_bounds__(TB) void k_gossip_targets_range(const uint64_t* __r
   const uint64_t h = h0 + blockIdx.y;
   const size_t slot = (size_t)(h % R);
   if (u < N)
-    gossip_targets_row(row, col, ring_mesh + slot * N * MESH_W, ring_off + slot * w64, N, seed, (uint32_t)h, d_lazy,
+    gossip_targets_row(row, col, ring_mesh + slot * N * MESH_W, ring_off + slot * w64, stage, N, seed, (uint32_t)h, d_lazy,
                        gf_milli, ring_tgt + slot * N * GT_W, ring_tcnt + slot * N, u);
 }
 
@@ -634,7 +636,7 @@ __device__ __forceinline__ void row_targets(const MeshArgs& a, uint32_t u, uint3
 #pragma unroll
       for (int k = 0; k < HB_PER_LANE; k++)
         if ((uint32_t)k == (sel / G)) ws = w[k];
-      tgt[(size_t)u * GT_W + q] = ws;
+      tgt[(size_t)u * GT_W + q] = ((uint32_t)a.stage[ws] << STAGE_SHIFT) | ws;
       drop_key<G>(key, sel);
     }
   }
@@ -887,7 +889,7 @@ void ring_targets(Ctx& c, uint64_t h, size_t slot) {
   const uint32_t N = c.cfg.peers;
   const size_t w64 = ((size_t)N + 63) / 64;
   k_gossip_targets<<<blocks(N), TB, 0, c.stream>>>(
-      c.d_row.p, c.d_col.p, c.d_ring_mesh.p + slot * N * MESH_W, c.d_ring_off.p + slot * w64, N, c.cfg.seed,
+      c.d_row.p, c.d_col.p, c.d_ring_mesh.p + slot * N * MESH_W, c.d_ring_off.p + slot * w64, c.d_stage.p, N, c.cfg.seed,
       (uint32_t)h, c.cfg.d_lazy, c.cfg.gossip_factor_milli, c.d_ring_tgt.p + slot * N * GT_W,
       c.d_ring_tcnt.p + slot * N);
 }
@@ -986,7 +988,7 @@ void ev_epochs(Ctx& c, MeshArgs a, uint64_t h0, uint64_t h1, bool ring) {
     for (uint64_t y0 = 0; y0 < ER; y0 += 32768) {
       const uint32_t ny = (uint32_t)std::min<uint64_t>(32768, ER - y0);
       k_gossip_targets_range<<<dim3(blocks(N), ny), TB, 0, s>>>(
-          c.d_row.p, c.d_col.p, c.d_ring_mesh.p, c.d_ring_off.p, N, w64, c.ring_R, c.cfg.seed, hr + y0,
+          c.d_row.p, c.d_col.p, c.d_ring_mesh.p, c.d_ring_off.p, c.d_stage.p, N, w64, c.ring_R, c.cfg.seed, hr + y0,
           c.cfg.d_lazy, c.cfg.gossip_factor_milli, c.d_ring_tgt.p, c.d_ring_tcnt.p);
     }
     GS_HIP(hipGetLastError());

@@ -63,7 +63,7 @@ struct RelaxArgs {
   const uint64_t* r0;         // [B] t_pub - start of that epoch
   uint32_t churn, ring_R, w64, horizon;
   const uint32_t* ring_tgt;   // churn + gossip: [R][N][GT_W] IHAVE targets of (peer, epoch)
-  const uint8_t* ring_tcnt;   // [R][N] their count, GT_NONE = more than GT_W (recompute)
+  const uint8_t* ring_tcnt;   // [R][N] their count, GT_NONE = more than GT_W (recompute); entries stage<<24 | id
   const uint32_t* mesh;
   const uint32_t* pub;
   const uint8_t* stage;
@@ -105,6 +105,11 @@ __device__ __forceinline__ bool ep_off(const A& a, uint64_t h, uint32_t w) {
 template <class A>
 __device__ __forceinline__ const uint32_t* ep_mesh(const A& a, uint64_t h, uint32_t u) {
   return a.ring_mesh + ((size_t)((uint32_t)h % a.ring_R) * a.N + u) * MESH_W;
+}
+// Epoch of a time x >= 0 after heartbeat hab (heartbeat h opens epoch h): no
+// division when x is shorter than a heartbeat.
+__device__ __forceinline__ uint64_t ep_plus(uint64_t hab, uint64_t x, uint64_t hb) {
+  return hab + (x < hb ? 0 : udiv53(x, hb));
 }
 // a delivery to w at relative time t is lost: past the message's lifetime or w offline
 template <class A>
@@ -600,8 +605,9 @@ __device__ __forceinline__ bool pair_lt(uint64_t k1, uint32_t w1, uint64_t k2, u
 // gossip_targets(u, hab) (libp2p-gossipsub emit_gossip, upstream; DESIGN.md
 // §2.7): the r smallest (rng(GOSSIP, u, h, w), w) among u's non-mesh
 // connections (online ones under churn, over the epoch's mesh), r =
-// max(D_lazy, floor(factor * |non-mesh|)) capped at |non-mesh|; fn(w) per
-// target in that order. The caller checks that u gossips at hab.
+// max(D_lazy, floor(factor * |non-mesh|)) capped at |non-mesh|; fn(e) per
+// target in that order, e = stage << STAGE_SHIFT | id (as a mesh entry). The
+// caller checks that u gossips at hab.
 template <class Fn>
 __device__ __forceinline__ void for_each_gossip_target(const RelaxArgs& a, uint32_t u, uint64_t hab, Fn&& fn) {
   const uint32_t h = (uint32_t)hab;
@@ -660,7 +666,7 @@ __device__ __forceinline__ void for_each_gossip_target(const RelaxArgs& a, uint3
   if (r > nonmesh) r = nonmesh;
 #pragma unroll
   for (int q = 0; q < (int)GOSSIP_R_REG; q++)
-    if ((uint32_t)q < r) fn(ww[q]);
+    if ((uint32_t)q < r) fn(((uint32_t)a.stage[ww[q]] << STAGE_SHIFT) | ww[q]);
   uint64_t pk = kk[GOSSIP_R_REG - 1];
   uint32_t pw = ww[GOSSIP_R_REG - 1];
   for (uint32_t q = GOSSIP_R_REG; q < r; q++) {  // rare: more than GOSSIP_R_REG targets
@@ -672,7 +678,7 @@ __device__ __forceinline__ void for_each_gossip_target(const RelaxArgs& a, uint3
       const uint64_t rk = rng(a.seed, P_GOSSIP, u, h, w);
       if (pair_lt(pk, pw, rk, w) && pair_lt(rk, w, bk, bw)) { bk = rk; bw = w; }
     }
-    fn(bw);
+    fn(((uint32_t)a.stage[bw] << STAGE_SHIFT) | bw);
     pk = bk;
     pw = bw;
   }
@@ -707,13 +713,18 @@ __global__ __launch_bounds__(TB) void k_gossip(RelaxArgs a) {
       const uint64_t T = r0 + (j0 + k) * a.hb_ns;
       if (T + L.lmax[sv] < lo || T + L.lmin[sv] >= hi) continue;
       const uint64_t hab = a.habs0[m] + j0 + k;
-      auto ihave = [&](uint32_t w) {  // v's IHAVE to w; IWANT + answer if w has not seen it
-        const uint32_t sw = a.stage[w];
-        const uint64_t ti = T + L.lat[sv * S + sw];
+      auto ihave = [&](uint32_t e) {  // v's IHAVE to w; IWANT + answer if w has not seen it
+        const uint32_t w = e & 0xFFFFFFu, sw = e >> STAGE_SHIFT;
+        const uint64_t lvw = L.lat[sv * S + sw];
+        const uint64_t ti = T + lvw;
         if (ti < lo || ti >= hi) return;
         const uint64_t sd = L.sd[sw];
-        const uint64_t A = ti + L.lat[sw * S + sv] + ser + L.lat[sv * S + sw] + (sd > ser ? sd - ser : 0);
-        if (a.churn && (ev_lost(a, m, ti, w) || ev_lost(a, m, A, w))) return;  // IHAVE or answer lost
+        const uint64_t A = ti + L.lat[sw * S + sv] + ser + lvw + (sd > ser ? sd - ser : 0);
+        if (a.churn) {  // IHAVE or answer lost: epochs counted from the heartbeat's (= ev_epoch)
+          const uint64_t lim = a.q0[m] + a.horizon;
+          const uint64_t hi_ = ep_plus(hab, lvw, a.hb_ns), ha = ep_plus(hab, A - T, a.hb_ns);
+          if (hi_ > lim || ep_off(a, hi_, w) || ha > lim || ep_off(a, ha, w)) return;
+        }
         const size_t dst = (size_t)w * LL + slot;
         // final before this bucket (its tile's final bit from an earlier scan:
         // key time < that bucket's end <= lo <= t_i): seen, no key read

@@ -201,8 +201,8 @@ __global__ __launch_bounds__(TB) void k_traffic_gossip(RelaxArgs a, TrafficArgs 
       const uint64_t T = r0 + (j0 + k) * a.hb_ns;
       const uint64_t hab = a.habs0[m] + j0 + k;
       if (a.churn && (hab > a.q0[m] + a.horizon || ep_off(a, hab, u))) continue;
-      for_each_gossip_target(a, u, hab, [&](uint32_t w) {
-        const uint32_t sw = a.stage[w];
+      for_each_gossip_target(a, u, hab, [&](uint32_t e) {
+        const uint32_t w = e & 0xFFFFFFu, sw = e >> STAGE_SHIFT;
         const uint64_t ti = T + a.tables[sv * S + sw];
         const uint64_t sd = a.tables[S * S + S + sw];
         const uint64_t A = ti + a.tables[sw * S + sv] + ser + a.tables[sv * S + sw] + (sd > ser ? sd - ser : 0);
