@@ -19,8 +19,8 @@ constexpr uint32_t HOP_BITS = 6;      // key = t_rel | hops | src (DESIGN.md §2
 constexpr uint32_t MAX_STAGES = 16;   // link classes (topogen -st), LDS-resident
 constexpr uint32_t MAX_DIALS = 64;    // dials per peer held in registers/scratch
 constexpr uint32_t MAX_DEG = 256;     // per-row working sets of the mesh kernels
-constexpr uint32_t GT_W = 8;          // lazy gossip + churn: IHAVE targets kept per (peer, epoch)
-constexpr uint8_t GT_NONE = 0xFF;     // more than GT_W targets: k_gossip selects them itself
+constexpr uint32_t GT_W = 8;          // gossip target selection: pairs kept sorted in registers
+constexpr uint32_t GT_IN = 16;        // lazy gossip + churn: IHAVE senders kept per (peer, epoch)
 constexpr uint32_t MAX_FRAGS = 16;    // FRAGMENTS (topogen allows 1..9)
 constexpr uint32_t STAGE_SHIFT = 24;  // packed mesh entry: stage << 24 | peer
 // Subscription exchange: a connection completes HS_RTTS round

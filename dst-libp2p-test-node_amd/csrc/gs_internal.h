@@ -98,8 +98,8 @@ struct Ctx {
   DevBuf<uint64_t> d_off;       // offline bitset scratch (gs_mesh_converge)
   DevBuf<uint32_t> d_ring_mesh; // [R][N][MESH_W]
   DevBuf<uint64_t> d_ring_off;  // [R][(N+63)/64]
-  DevBuf<uint32_t> d_ring_tgt;  // lazy gossip: [R][N][GT_W] IHAVE targets per (peer, epoch)
-  DevBuf<uint8_t> d_ring_tcnt;  // [R][N] (GT_NONE: more than GT_W, recomputed in k_gossip)
+  DevBuf<uint32_t> d_ring_in;     // lazy gossip: [R][N][GT_IN] senders of the IHAVEs reaching a peer per epoch
+  DevBuf<uint32_t> d_ring_incnt;  // [R][N] their number (above GT_IN: k_gossip recomputes)
   DevBuf<uint64_t> d_q0, d_r0;  // [B] epoch of t_pub, t_pub - start of that epoch
   uint32_t ring_R = 0;
   uint64_t churn_state = 0, ring_lo = 1, ring_hi = 0;  // mesh state epoch; valid ring epochs

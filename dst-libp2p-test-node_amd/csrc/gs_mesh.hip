@@ -448,24 +448,24 @@ __global__ __launch_bounds__(TB) void k_extract(MeshArgs a, uint32_t* mesh, uint
   for (uint32_t q = c; q < MESH_W; q++) mesh[(size_t)u * MESH_W + q] = EMPTY;
 }
 
-// Lazy gossip under churn: the IHAVE targets of every peer u at epoch h
-// (DESIGN.md §2.7 — the r smallest (rng(GOSSIP, u, h, w), w) among u's online
+// Lazy gossip under churn: who sends IHAVEs to whom at epoch h. Peer u's
+// targets are the r smallest (rng(GOSSIP, u, h, w), w) among its online
 // connections outside its epoch-h mesh, r = max(D_lazy, factor·|non-mesh|)
-// capped at |non-mesh|), computed once per epoch snapshot instead of by every
-// (lane, bucket) of k_gossip that needs them. One peer per thread: the
+// capped at |non-mesh|. They are stored inverted, per
+// target: in[w] lists the senders v whose epoch-h IHAVEs reach w (packed
+// stage << 24 | v, at most GT_IN; incnt[w] counts all of them, so a count
+// above GT_IN tells k_gossip to recompute). The receiver side of lazy gossip
+// (k_gossip, receiver-centric under churn) then reads only the lists of the
+// lanes that have not yet received a message. One sender per thread: the
 // selection is serial compute (one rng per connection, an 8-deep sorted
-// insert in registers with static indices), which a wave per peer would
-// leave mostly idle.
-__device__ __forceinline__ void gossip_targets_row(const uint64_t* __restrict__ row, const uint32_t* __restrict__ col,
-                                                   const uint32_t* __restrict__ mesh, const uint64_t* __restrict__ off,
-                                                   const uint8_t* __restrict__ stage, uint32_t N, uint64_t seed,
-                                                   uint32_t h, uint32_t d_lazy, uint32_t gf_milli,
-                                                   uint32_t* __restrict__ tgt, uint8_t* __restrict__ tcnt,
-                                                   uint32_t u) {
-  if (is_off(off, u)) {  // offline peers gossip nothing (k_gossip skips them first)
-    tcnt[u] = 0;
-    return;
-  }
+// insert in registers with static indices; the rare fan-outs above 8 rescan
+// for the next pair).
+__device__ __forceinline__ void gossip_in_scatter(const uint64_t* __restrict__ row, const uint32_t* __restrict__ col,
+                                                  const uint32_t* __restrict__ mesh, const uint64_t* __restrict__ off,
+                                                  const uint8_t* __restrict__ stage, uint64_t seed, uint32_t h,
+                                                  uint32_t d_lazy, uint32_t gf_milli, uint32_t* __restrict__ in,
+                                                  uint32_t* __restrict__ incnt, uint32_t u) {
+  if (is_off(off, u)) return;  // offline peers gossip nothing
   uint32_t mrow[MESH_W];
   const uint4* rp = reinterpret_cast<const uint4*>(mesh + (size_t)u * MESH_W);
 #pragma unroll
@@ -474,67 +474,78 @@ __device__ __forceinline__ void gossip_targets_row(const uint64_t* __restrict__ 
     mrow[4 * q] = x.x & 0xFFFFFFu; mrow[4 * q + 1] = x.y & 0xFFFFFFu;
     mrow[4 * q + 2] = x.z & 0xFFFFFFu; mrow[4 * q + 3] = x.w & 0xFFFFFFu;
   }
+  auto eligible = [&](uint32_t w) {
+    bool inm = false;
+#pragma unroll
+    for (int q = 0; q < (int)MESH_W; q++) inm |= mrow[q] == w;
+    return !inm && !is_off(off, w);
+  };
+  auto lt = [](uint64_t k1, uint32_t w1, uint64_t k2, uint32_t w2) { return k1 < k2 || (k1 == k2 && w1 < w2); };
+  const uint32_t me = ((uint32_t)stage[u] << STAGE_SHIFT) | u;
+  auto emit = [&](uint32_t w) {
+    const uint32_t pos = atomicAdd(&incnt[w], 1u);
+    if (pos < GT_IN) in[(size_t)w * GT_IN + pos] = me;
+  };
   uint64_t kk[GT_W];
   uint32_t ww[GT_W];
 #pragma unroll
   for (int q = 0; q < (int)GT_W; q++) { kk[q] = INF64; ww[q] = ~0u; }
   uint32_t nonmesh = 0;
-  for (uint64_t e = row[u]; e < row[u + 1]; e++) {
+  const uint64_t e0 = row[u], e1 = row[u + 1];
+  for (uint64_t e = e0; e < e1; e++) {
     const uint32_t w = col[e];
-    bool inm = false;
-#pragma unroll
-    for (int q = 0; q < (int)MESH_W; q++) inm |= mrow[q] == w;
-    if (inm || is_off(off, w)) continue;
+    if (!eligible(w)) continue;
     nonmesh++;
     const uint64_t rk = rng(seed, P_GOSSIP, u, h, w);
-    if (!(rk < kk[GT_W - 1] || (rk == kk[GT_W - 1] && w < ww[GT_W - 1]))) continue;
+    if (!lt(rk, w, kk[GT_W - 1], ww[GT_W - 1])) continue;
 #pragma unroll
     for (int q = (int)GT_W - 1; q > 0; q--) {  // insert, shifting the larger pairs up
-      if (rk < kk[q - 1] || (rk == kk[q - 1] && w < ww[q - 1])) { kk[q] = kk[q - 1]; ww[q] = ww[q - 1]; }
-      else if (rk < kk[q] || (rk == kk[q] && w < ww[q])) { kk[q] = rk; ww[q] = w; }
+      if (lt(rk, w, kk[q - 1], ww[q - 1])) { kk[q] = kk[q - 1]; ww[q] = ww[q - 1]; }
+      else if (lt(rk, w, kk[q], ww[q])) { kk[q] = rk; ww[q] = w; }
     }
-    if (rk < kk[0] || (rk == kk[0] && w < ww[0])) { kk[0] = rk; ww[0] = w; }
+    if (lt(rk, w, kk[0], ww[0])) { kk[0] = rk; ww[0] = w; }
   }
   uint32_t r = (uint32_t)(((uint64_t)nonmesh * gf_milli) / 1000);
   if (r < d_lazy) r = d_lazy;
   if (r > nonmesh) r = nonmesh;
-  if (r > GT_W) {
-    tcnt[u] = GT_NONE;
-    return;
-  }
 #pragma unroll
   for (int q = 0; q < (int)GT_W; q++)
-    if ((uint32_t)q < r) tgt[(size_t)u * GT_W + q] = ((uint32_t)stage[ww[q]] << STAGE_SHIFT) | ww[q];
-  tcnt[u] = (uint8_t)r;
+    if ((uint32_t)q < r) emit(ww[q]);
+  uint64_t pk = kk[GT_W - 1];
+  uint32_t pw = ww[GT_W - 1];
+  for (uint32_t q = GT_W; q < r; q++) {  // rare: more than GT_W targets
+    uint64_t bk = ~0ull;
+    uint32_t bw = ~0u;
+    for (uint64_t e = e0; e < e1; e++) {
+      const uint32_t w = col[e];
+      if (!eligible(w)) continue;
+      const uint64_t rk = rng(seed, P_GOSSIP, u, h, w);
+      if (lt(pk, pw, rk, w) && lt(rk, w, bk, bw)) { bk = rk; bw = w; }
+    }
+    emit(bw);
+    pk = bk;
+    pw = bw;
+  }
 }
 
-__global__ __launch_bounds__(TB) void k_gossip_targets(const uint64_t* __restrict__ row, const uint32_t* __restrict__ col,
-                                                       const uint32_t* __restrict__ mesh, const uint64_t* __restrict__ off,
-                                                       const uint8_t* __restrict__ stage, uint32_t N, uint64_t seed,
-                                                       uint32_t h, uint32_t d_lazy, uint32_t gf_milli,
-                                                       uint32_t* __restrict__ tgt, uint8_t* __restrict__ tcnt) {
-  const uint32_t u = blockIdx.x * TB + threadIdx.x;
-  if (u < N) gossip_targets_row(row, col, mesh, off, stage, N, seed, h, d_lazy, gf_milli, tgt, tcnt, u);
-}
-
-// The same for the ring slots of epochs h0 + blockIdx.y (one launch after a
-// run of event-driven epochs: the targets depend only on each epoch's
-// snapshot, so they are not on the epochs' sequential path).
-__global__ __launch_bounds__(TB) void k_gossip_targets_range(const uint64_t* __restrict__ row,
-                                                             const uint32_t* __restrict__ col,
-                                                             const uint32_t* __restrict__ ring_mesh,
-                                                             const uint64_t* __restrict__ ring_off,
-                                                             const uint8_t* __restrict__ stage, uint32_t N,
-                                                             uint32_t w64, uint32_t R, uint64_t seed, uint64_t h0,
-                                                             uint32_t d_lazy, uint32_t gf_milli,
-                                                             uint32_t* __restrict__ ring_tgt,
-                                                             uint8_t* __restrict__ ring_tcnt) {
+// Inverse IHAVE lists of the ring slots of epochs h0 + blockIdx.y (one launch
+// after a run of epochs: they depend only on each epoch's snapshot, so they
+// are not on the epochs' sequential path). The slots' counters are zeroed
+// before the launch.
+__global__ __launch_bounds__(TB) void k_gossip_in_range(const uint64_t* __restrict__ row,
+                                                        const uint32_t* __restrict__ col,
+                                                        const uint32_t* __restrict__ ring_mesh,
+                                                        const uint64_t* __restrict__ ring_off,
+                                                        const uint8_t* __restrict__ stage, uint32_t N, uint32_t w64,
+                                                        uint32_t R, uint64_t seed, uint64_t h0, uint32_t d_lazy,
+                                                        uint32_t gf_milli, uint32_t* __restrict__ ring_in,
+                                                        uint32_t* __restrict__ ring_incnt) {
   const uint32_t u = blockIdx.x * TB + threadIdx.x;
   const uint64_t h = h0 + blockIdx.y;
   const size_t slot = (size_t)(h % R);
   if (u < N)
-    gossip_targets_row(row, col, ring_mesh + slot * N * MESH_W, ring_off + slot * w64, stage, N, seed, (uint32_t)h, d_lazy,
-                       gf_milli, ring_tgt + slot * N * GT_W, ring_tcnt + slot * N, u);
+    gossip_in_scatter(row, col, ring_mesh + slot * N * MESH_W, ring_off + slot * w64, stage, seed, (uint32_t)h,
+                      d_lazy, gf_milli, ring_in + slot * N * GT_IN, ring_incnt + slot * N, u);
 }
 
 // ---- fused churn epochs (one cooperative launch for a run of epochs) ----
@@ -588,61 +599,6 @@ __device__ __forceinline__ void row_extract(const MeshArgs& a, uint32_t u, uint3
   if ((uint32_t)lane >= cnt && lane < (int)MESH_W) mesh[(size_t)u * MESH_W + lane] = EMPTY;
 }
 
-// IHAVE targets of (u, h) from its CSR flags (= k_gossip_targets: the r
-// smallest (rng(GOSSIP, u, h, w), w) among u's online non-mesh connections).
-template <int G>
-__device__ __forceinline__ void row_targets(const MeshArgs& a, uint32_t u, uint32_t h, uint32_t d_lazy,
-                                            uint32_t gf_milli, uint32_t* tgt, uint8_t* tcnt) {
-  const int lane = threadIdx.x & (G - 1);
-  const int gbase = (threadIdx.x & 63) & ~(G - 1);
-  (void)gbase;
-  if (is_off(a.off, u)) {
-    if (lane == 0) tcnt[u] = 0;
-    return;
-  }
-  const uint64_t b = a.row[u];
-  const uint32_t deg = (uint32_t)(a.row[u + 1] - b);
-  uint64_t key[HB_PER_LANE];
-  uint32_t w[HB_PER_LANE];
-  uint32_t nonmesh = 0;
-#pragma unroll
-  for (int k = 0; k < HB_PER_LANE; k++) {
-    const uint32_t i = (uint32_t)(k * G + lane);
-    key[k] = INF64;
-    w[k] = 0;
-    if (k * G >= (int)deg) continue;  // wave-uniform
-    bool el = false;
-    if (i < deg) {
-      w[k] = a.col[b + i];
-      el = !(a.flags[b + i] & F_MESH) && !is_off(a.off, w[k]);
-      if (el) key[k] = rng(a.seed, P_GOSSIP, u, h, w[k]);
-    }
-    nonmesh += (uint32_t)__popcll(gballot<G>(el));
-  }
-  uint32_t r = (uint32_t)(((uint64_t)nonmesh * gf_milli) / 1000);
-  if (r < d_lazy) r = d_lazy;
-  if (r > nonmesh) r = nonmesh;
-  if (r > GT_W) {
-    if (lane == 0) tcnt[u] = GT_NONE;
-    return;
-  }
-  for (uint32_t q = 0; q < r; q++) {  // ties by entry index = ascending id
-    uint64_t bk;
-    uint32_t bi;
-    lane_min<G>(key, lane, bk, bi);
-    const uint32_t sel = group_argmin<G>(bk, bi);
-    if ((int)(sel % G) == lane) {
-      uint32_t ws = 0;
-#pragma unroll
-      for (int k = 0; k < HB_PER_LANE; k++)
-        if ((uint32_t)k == (sel / G)) ws = w[k];
-      tgt[(size_t)u * GT_W + q] = ((uint32_t)a.stage[ws] << STAGE_SHIFT) | ws;
-      drop_key<G>(key, sel);
-    }
-  }
-  if (lane == 0) tcnt[u] = (uint8_t)r;
-}
-
 // Grid barrier for the co-resident grid of k_epochs: a monotonic arrival
 // counter (zeroed before the launch), the k-th barrier waits for k * blocks
 // arrivals. Agent-scope release before arriving and acquire after leaving
@@ -678,8 +634,6 @@ struct EpochArgs {
   uint8_t* prop2;        // [2][nnz] proposals by epoch parity
   uint64_t* off;         // [off_R][w64] offline bitsets, slot h % off_R
   uint32_t* ring_mesh;   // [ring_R][N][MESH_W] or nullptr (no snapshots)
-  uint32_t* ring_tgt;    // [ring_R][N][GT_W] or nullptr (no lazy gossip)
-  uint8_t* ring_tcnt;
   uint64_t h0, h1;
   uint32_t off_R, ring_R, w64, ppm, down, d_lazy, gf_milli;
 };
@@ -711,8 +665,6 @@ __global__ __launch_bounds__(TB) void k_epochs(EpochArgs e) {
     for (uint32_t u = gw; u < N; u += nw) {
       row_apply<64>(a, u);
       if (e.ring_mesh) row_extract<64>(a, u, e.ring_mesh + slot * N * MESH_W);
-      if (e.ring_tgt)
-        row_targets<64>(a, u, (uint32_t)h, e.d_lazy, e.gf_milli, e.ring_tgt + slot * N * GT_W, e.ring_tcnt + slot * N);
     }
   }
 }
@@ -731,7 +683,7 @@ __global__ __launch_bounds__(TB) void k_epochs(EpochArgs e) {
 //  apply: proposers and PRUNEd rows; rows whose mesh changed are recounted
 //    and re-extracted into the ring slot, the others copy their previous row.
 // Offline bitsets and IHAVE targets do not depend on the epoch sequence and
-// run batched over the whole range (k_offline_range, k_gossip_targets_range).
+// run batched over the whole range (k_offline_range, k_gossip_in_range).
 
 // Mesh links of u (all, outbound) from its CSR flags.
 template <int G>
@@ -883,15 +835,24 @@ inline unsigned row_blocks(uint32_t N, uint32_t G) { return (unsigned)(((uint64_
     else kernel<64><<<row_blocks(N, 64), TB, 0, s>>>(__VA_ARGS__);                      \
   } while (0)
 
-// Targets of the snapshot in ring slot `slot` (epoch h), when lazy gossip is on.
-void ring_targets(Ctx& c, uint64_t h, size_t slot) {
-  if (!c.cfg.lazy_gossip || !c.d_ring_tcnt.p) return;
-  const uint32_t N = c.cfg.peers;
-  const size_t w64 = ((size_t)N + 63) / 64;
-  k_gossip_targets<<<blocks(N), TB, 0, c.stream>>>(
-      c.d_row.p, c.d_col.p, c.d_ring_mesh.p + slot * N * MESH_W, c.d_ring_off.p + slot * w64, c.d_stage.p, N, c.cfg.seed,
-      (uint32_t)h, c.cfg.d_lazy, c.cfg.gossip_factor_milli, c.d_ring_tgt.p + slot * N * GT_W,
-      c.d_ring_tcnt.p + slot * N);
+// Inverse IHAVE lists of the ring snapshots of epochs [h0, h1] (h1 - h0 <
+// ring_R), when lazy gossip is on: zero the slots' counters, then one launch.
+void ring_in_lists(Ctx& c, uint64_t h0, uint64_t h1) {
+  if (!c.cfg.lazy_gossip || !c.d_ring_incnt.p) return;
+  const uint32_t N = c.cfg.peers, R = c.ring_R, w64 = (N + 63) / 64;
+  hipStream_t s = c.stream;
+  const uint64_t E = h1 - h0 + 1;
+  const uint64_t s0 = h0 % R, first = std::min<uint64_t>(E, R - s0);  // slots s0.. then 0.. on a wrap
+  GS_HIP(hipMemsetAsync(c.d_ring_incnt.p + s0 * N, 0, first * N * 4, s));
+  if (E > first) GS_HIP(hipMemsetAsync(c.d_ring_incnt.p, 0, (E - first) * N * 4, s));
+  for (uint64_t y0 = 0; y0 < E; y0 += 32768) {  // grid.y limit
+    const uint32_t ny = (uint32_t)std::min<uint64_t>(32768, E - y0);
+    k_gossip_in_range<<<dim3(blocks(N), ny), TB, 0, s>>>(c.d_row.p, c.d_col.p, c.d_ring_mesh.p, c.d_ring_off.p,
+                                                         c.d_stage.p, N, w64, R, c.cfg.seed, h0 + y0, c.cfg.d_lazy,
+                                                         c.cfg.gossip_factor_milli, c.d_ring_in.p,
+                                                         c.d_ring_incnt.p);
+  }
+  GS_HIP(hipGetLastError());
 }
 
 MeshArgs mesh_args(Ctx& c) {
@@ -983,16 +944,7 @@ void ev_epochs(Ctx& c, MeshArgs a, uint64_t h0, uint64_t h1, bool ring) {
   }
 #undef GS_EVS
   GS_HIP(hipGetLastError());
-  if (ring && c.cfg.lazy_gossip && c.d_ring_tcnt.p) {
-    const uint64_t ER = h1 + 1 - hr;
-    for (uint64_t y0 = 0; y0 < ER; y0 += 32768) {
-      const uint32_t ny = (uint32_t)std::min<uint64_t>(32768, ER - y0);
-      k_gossip_targets_range<<<dim3(blocks(N), ny), TB, 0, s>>>(
-          c.d_row.p, c.d_col.p, c.d_ring_mesh.p, c.d_ring_off.p, c.d_stage.p, N, w64, c.ring_R, c.cfg.seed, hr + y0,
-          c.cfg.d_lazy, c.cfg.gossip_factor_milli, c.d_ring_tgt.p, c.d_ring_tcnt.p);
-    }
-    GS_HIP(hipGetLastError());
-  }
+  if (ring) ring_in_lists(c, hr, h1);
 }
 
 // Churn epochs [h0, h1] from the current mesh state: event-driven (ev_epochs),
@@ -1024,12 +976,6 @@ void run_epochs(Ctx& c, MeshArgs a, uint64_t h0, uint64_t h1, uint64_t* off, uin
   if (ring) {
     e.ring_R = c.ring_R;
     e.ring_mesh = c.d_ring_mesh.p;
-    if (c.cfg.lazy_gossip && c.d_ring_tcnt.p) {
-      e.ring_tgt = c.d_ring_tgt.p;
-      e.ring_tcnt = c.d_ring_tcnt.p;
-      e.d_lazy = c.cfg.d_lazy;
-      e.gf_milli = c.cfg.gossip_factor_milli;
-    }
   }
   int per_cu = 0;
   GS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_epochs, TB, 0));
@@ -1054,6 +1000,7 @@ void run_epochs(Ctx& c, MeshArgs a, uint64_t h0, uint64_t h1, uint64_t* off, uin
   GS_HIP(hipMemcpyAsync(c.h_pinned, c.d_counters.p + C_ERR, 8, hipMemcpyDeviceToHost, s));
   GS_HIP(hipStreamSynchronize(s));
   if (c.h_pinned[0] & ERR_SYNC) c.fail(GS_EDEVICE, "k_epochs grid barrier timed out (blocks not co-resident)");
+  if (ring) ring_in_lists(c, h1 - h0 + 1 > c.ring_R ? h1 + 1 - c.ring_R : h0, h1);
 }
 
 }  // namespace
@@ -1078,7 +1025,7 @@ void churn_ring(Ctx& c, uint64_t h_lo, uint64_t h_hi) {
       // row may be wider than the ELL before heartbeat 1 prunes it (GS_ERANGE below)
       k_extract<<<blocks(N), TB, 0, s>>>(a, c.d_ring_mesh.p, nullptr);
       GS_HIP(hipMemsetAsync(c.d_ring_off.p, 0, w64 * 8, s));
-      ring_targets(c, 0, 0);
+      ring_in_lists(c, 0, 0);
       c.ring_lo = 0;
     }
   }

@@ -616,8 +616,8 @@ static RelaxArgs relax_args(Ctx& c, const Batch& b, bool gossip) {
     ra.seed = c.cfg.seed;
     ra.gossip = 1;
     if (c.cfg.churn_ppm) {
-      ra.ring_tgt = c.d_ring_tgt.p;
-      ra.ring_tcnt = c.d_ring_tcnt.p;
+      ra.ring_in = c.d_ring_in.p;
+      ra.ring_incnt = c.d_ring_incnt.p;
     }
     ra.hist = c.cfg.history_gossip;
     ra.d_lazy = c.cfg.d_lazy;
@@ -813,16 +813,16 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     }
     if (!c.ring_R) {
       const uint64_t w64 = ((uint64_t)N + 63) / 64;
-      const uint64_t per_slot = (uint64_t)N * MESH_W * 4 + w64 * 8 + (gossip ? (uint64_t)N * (GT_W * 4 + 1) : 0);
+      const uint64_t per_slot = (uint64_t)N * MESH_W * 4 + w64 * 8 + (gossip ? (uint64_t)N * (GT_IN * 4 + 4) : 0);
       const char* rb = getenv("GS_RING_BUDGET_MB");  // test knob: force batch cuts at the ring size
       const uint64_t budget = rb && *rb ? (uint64_t)atoll(rb) << 20 : 16ull << 30;
       const uint64_t want = (uint64_t)Bmax + c.cfg.churn_horizon + 1;
       c.ring_R = (uint32_t)std::min<uint64_t>(want, std::max<uint64_t>(c.cfg.churn_horizon + 2, budget / per_slot));
       c.d_ring_mesh.alloc((size_t)c.ring_R * N * MESH_W);
       c.d_ring_off.alloc((size_t)c.ring_R * w64);
-      if (gossip) {  // IHAVE targets per (peer, epoch) beside the snapshots (k_gossip_targets)
-        c.d_ring_tgt.alloc((size_t)c.ring_R * N * GT_W);
-        c.d_ring_tcnt.alloc((size_t)c.ring_R * N);
+      if (gossip) {  // inverse IHAVE lists per (peer, epoch) beside the snapshots (k_gossip_in_range)
+        c.d_ring_in.alloc((size_t)c.ring_R * N * GT_IN);
+        c.d_ring_incnt.alloc((size_t)c.ring_R * N);
       }
     }
   }

@@ -62,8 +62,10 @@ struct RelaxArgs {
   const uint64_t* q0;         // [B] epoch of t_pub
   const uint64_t* r0;         // [B] t_pub - start of that epoch
   uint32_t churn, ring_R, w64, horizon;
-  const uint32_t* ring_tgt;   // churn + gossip: [R][N][GT_W] IHAVE targets of (peer, epoch)
-  const uint8_t* ring_tcnt;   // [R][N] their count, GT_NONE = more than GT_W (recompute); entries stage<<24 | id
+  // churn + gossip: receiver-centric lazy gossip over the inverse IHAVE lists
+  // of each epoch (k_gossip_in_range): [R][N][GT_IN] senders (stage<<24 | id)
+  const uint32_t* ring_in;
+  const uint32_t* ring_incnt;  // [R][N] their number (> GT_IN: recompute)
   const uint32_t* mesh;
   const uint32_t* pub;
   const uint8_t* stage;
@@ -181,6 +183,7 @@ struct BucketLds {
   uint32_t lat[MAX_STAGES * MAX_STAGES];
   uint32_t su[MAX_STAGES], sd[MAX_STAGES];
   uint32_t lmin[MAX_STAGES], lmax[MAX_STAGES];  // min/max latency out of each stage
+  uint32_t imin[MAX_STAGES], imax[MAX_STAGES];  // min/max latency into each stage
 };
 
 __device__ __forceinline__ void load_tables(BucketLds& L, const RelaxArgs& a) {
@@ -197,6 +200,15 @@ __device__ __forceinline__ void load_tables(BucketLds& L, const RelaxArgs& a) {
     }
     L.lmin[threadIdx.x] = mn;
     L.lmax[threadIdx.x] = mx;
+    mn = ~0u;
+    mx = 0;
+    for (uint32_t s = 0; s < S; s++) {
+      const uint32_t l = a.tables[s * S + threadIdx.x];
+      mn = l < mn ? l : mn;
+      mx = l > mx ? l : mx;
+    }
+    L.imin[threadIdx.x] = mn;
+    L.imax[threadIdx.x] = mx;
   }
 }
 
@@ -521,9 +533,33 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
       // the first gossip heartbeat T_j0 < max(t, rel0) + hb, so a lane with
       // max(t, rel0) + hist*hb + lmax < lo is past its last IHAVE: skip it
       // before the division
-      const uint32_t sv = fin ? a.stage[u] : 0, m = slot / FP;
-      const uint64_t r0 = fin ? a.rel0[m] : 0;
-      if (fin && a.hist && (t > r0 ? t : r0) + hspan + L.lmax[sv] >= lo) {
+      const uint32_t sv = (fin || a.ring_in) && valid ? a.stage[u] : 0, m = slot / FP;
+      const uint64_t r0 = (fin || a.ring_in) && valid ? a.rel0[m] : 0;
+      if (a.ring_in) {
+        // receiver-centric (churn): a lane without a key before this bucket
+        // lists itself when an IHAVE of one of its message's heartbeats T_k
+        // can reach its peer inside [lo, hi) (T_k + min / max latency into
+        // its stage), up to the message's lifetime
+        // (a message whose publisher was offline at t_pub has no holder: skip)
+        if (valid && slot % FP < a.F && !(pending && t < lo) && a.hist && a.habs0[m] <= a.q0[m] + a.horizon &&
+            !ep_off(a, a.q0[m], a.pub[m])) {
+          const uint64_t imn = L.imin[sv], imx = L.imax[sv];
+          const uint64_t kl = a.q0[m] + a.horizon - a.habs0[m];  // last heartbeat index in the lifetime
+          const uint64_t k0 = lo > r0 + imx ? udiv53(lo - r0 - imx + a.hb_ns - 1, a.hb_ns) : 0;
+          // an IHAVE to a peer offline at its arrival is lost: with windows
+          // shorter than a heartbeat, a window lies in the epoch of its T_k,
+          // so the peer's offline epochs are skipped (its tile sleeps)
+          const bool one_ep = imx < a.hb_ns;
+          const uint64_t hab0 = a.habs0[m];
+          gwork = k0 <= kl && r0 + k0 * a.hb_ns + imn < hi && !(one_ep && ep_off(a, hab0 + k0, u));
+          // the next bucket that can hold one of these arrivals: the first
+          // window still open at hi (a window spans several buckets) with the
+          // peer online
+          uint64_t k1 = hi > r0 + imx ? udiv53(hi - r0 - imx + a.hb_ns - 1, a.hb_ns) : 0;
+          if (one_ep && k1 <= kl && ep_off(a, hab0 + k1, u)) k1++;  // (one step: later ones are found then)
+          if (k1 <= kl) gnext = r0 + k1 * a.hb_ns + imn > hi ? r0 + k1 * a.hb_ns + imn : hi;
+        }
+      } else if (fin && a.hist && (t > r0 ? t : r0) + hspan + L.lmax[sv] >= lo) {
         const uint64_t lmn = L.lmin[sv], lmx = L.lmax[sv];
         const uint64_t j0 = first_hb(t, r0, a.hb_ns);
         const uint64_t tlast = r0 + (j0 + a.hist - 1) * a.hb_ns;
@@ -613,17 +649,7 @@ __device__ __forceinline__ void for_each_gossip_target(const RelaxArgs& a, uint3
   const uint32_t h = (uint32_t)hab;
   uint32_t mrow[MESH_W];
   const uint32_t* mrp = a.mesh + (size_t)u * MESH_W;
-  if (a.churn) {
-    mrp = ep_mesh(a, hab, u);
-    if (a.ring_tcnt) {  // targets of (u, h) precomputed with the epoch's snapshot (k_gossip_targets)
-      const size_t ti = (size_t)((uint32_t)hab % a.ring_R) * a.N + u;
-      const uint32_t rc = a.ring_tcnt[ti];
-      if (rc != GT_NONE) {
-        for (uint32_t q = 0; q < rc; q++) fn(a.ring_tgt[ti * GT_W + q]);
-        return;
-      }
-    }
-  }
+  if (a.churn) mrp = ep_mesh(a, hab, u);
   const uint4* rp = reinterpret_cast<const uint4*>(mrp);
 #pragma unroll
   for (int q = 0; q < 4; q++) {
@@ -684,6 +710,83 @@ __device__ __forceinline__ void for_each_gossip_target(const RelaxArgs& a, uint3
   }
 }
 
+// Receiver-centric lazy gossip of one bucket (churn): every listed lane
+// (w, m, f) — no key before the bucket — reads, for each of its message's
+// heartbeats T_k whose IHAVEs can reach w inside [lo, hi), the inverse IHAVE
+// list of (w, epoch of T_k): each sender v that holds (m, f) by T_k with T_k
+// among its history_gossip heartbeats (v's final key) sent an IHAVE arriving
+// at t_i = T_k + lat(v, w); if w has not seen (m, f) by t_i (its own key) and
+// neither the IHAVE nor the answer is lost, that is one IWANT and a candidate
+// answer key. The lane keeps the smallest (one atomicMin). Exactly the IHAVE
+// decisions of the sender-centric form, without touching the ~97 % of IHAVEs
+// whose target already has the message.
+template <int FP>
+__device__ __forceinline__ void gossip_receiver(const RelaxArgs& a, const BucketLds& L, uint64_t lo, uint64_t hi,
+                                                uint32_t gid, uint64_t& nmin, uint64_t& iw, uint32_t& err) {
+  const uint32_t LL = a.L, S = a.S;
+  const uint64_t kw = a.keys[gid];
+  const uint64_t tw = kw == INF64 ? INF64 : kw >> a.tshift;
+  const uint32_t w = row_of(gid, LL), slot = (uint32_t)(gid - (uint64_t)w * LL);
+  const uint32_t m = slot / FP, sw = a.stage[w];
+  const uint64_t r0 = a.rel0[m], hb = a.hb_ns, lim = a.q0[m] + a.horizon;
+  const uint64_t imn = L.imin[sw], imx = L.imax[sw], sdw = L.sd[sw];
+  uint64_t best = INF64;
+  uint64_t k = lo > r0 + imx ? udiv53(lo - r0 - imx + hb - 1, hb) : 0;
+  for (;; k++) {
+    const uint64_t T = r0 + k * hb;
+    const uint64_t hab = a.habs0[m] + k;
+    if (T + imn >= hi || hab > lim) break;
+    if (imx < hb && ep_off(a, hab, w)) continue;  // every IHAVE of this heartbeat reaches w offline
+    auto ihave = [&](uint32_t e) {  // the IHAVE v -> w of heartbeat hab
+      const uint32_t v = e & 0xFFFFFFu, sv = e >> STAGE_SHIFT;
+      const uint64_t lvw = L.lat[sv * S + sw];
+      const uint64_t ti = T + lvw;
+      if (ti < lo || ti >= hi || tw <= ti) return;  // another bucket, or w has seen it
+      const uint64_t hi_ = ep_plus(hab, lvw, hb);
+      if (hi_ > lim || ep_off(a, hi_, w)) return;  // IHAVE lost
+      const uint64_t kv = a.keys[(size_t)v * LL + slot];
+      if (kv == INF64 || (kv >> a.tshift) > T) return;  // v does not hold it at T
+      const uint64_t j0 = first_hb(kv >> a.tshift, r0, hb);
+      if (k < j0 || k >= j0 + a.hist) return;  // T is not one of v's gossip heartbeats
+      const uint64_t ser = L.su[sv];
+      const uint64_t A = ti + L.lat[sw * S + sv] + ser + lvw + (sdw > ser ? sdw - ser : 0);
+      const uint64_t ha = ep_plus(hab, A - T, hb);
+      if (ha > lim || ep_off(a, ha, w)) return;  // answer lost
+      const uint32_t hp = (uint32_t)((kv >> a.sb) & ((1u << HOP_BITS) - 1));
+      iw++;
+      if (A > a.tmax) err |= ERR_TIME;
+      if (hp + 1 >= (1u << HOP_BITS)) err |= ERR_HOPS;
+      const uint64_t nk = (A << a.tshift) | ((uint64_t)(hp + 1) << a.sb) | v;
+      best = nk < best ? nk : best;
+    };
+    const size_t li = (size_t)((uint32_t)hab % a.ring_R) * a.N + w;
+    const uint32_t cnt = a.ring_incnt[li];
+    if (cnt <= GT_IN) {
+      const uint4* lp = reinterpret_cast<const uint4*>(a.ring_in + li * GT_IN);
+      for (uint32_t q0 = 0; q0 < cnt; q0 += 4) {
+        const uint4 x = lp[q0 / 4];
+        ihave(x.x);
+        if (q0 + 1 < cnt) ihave(x.y);
+        if (q0 + 2 < cnt) ihave(x.z);
+        if (q0 + 3 < cnt) ihave(x.w);
+      }
+    } else {  // more senders than the list holds (rare): w's online non-mesh neighbours that pick w
+      for (uint64_t e = a.row[w]; e < a.row[w + 1]; e++) {
+        const uint32_t v = a.col[e];
+        if (ep_off(a, hab, v)) continue;
+        for_each_gossip_target(a, v, hab, [&](uint32_t x) {
+          if ((x & 0xFFFFFFu) == w) ihave(((uint32_t)a.stage[v] << STAGE_SHIFT) | v);
+        });
+      }
+    }
+  }
+  if (best < kw) {
+    atomicMin((unsigned long long*)&a.keys[gid], (unsigned long long)best);
+    if (a.tstamp) a.touched[gid >> 6] = 1;
+    nmin = best < nmin ? best : nmin;
+  }
+}
+
 template <int FP>
 __global__ __launch_bounds__(TB) void k_gossip(RelaxArgs a) {
   __shared__ BucketLds L;
@@ -699,6 +802,9 @@ __global__ __launch_bounds__(TB) void k_gossip(RelaxArgs a) {
   const size_t seg = (size_t)wave * a.gl_cap;
   uint64_t nmin = INF64, iw = 0;
   uint32_t err = 0;
+  if (a.ring_in)
+    for (uint32_t i = lane; i < n; i += 64) gossip_receiver<FP>(a, L, lo, hi, a.gl_idx[seg + i], nmin, iw, err);
+  else
   for (uint32_t i = lane; i < n; i += 64) {
     const uint64_t gid = a.gl_idx[seg + i];
     const uint64_t key = a.keys[gid];
