@@ -231,8 +231,10 @@ __global__ __launch_bounds__(TB) void k_complete(CompArgs a) {
                                                                        : GS_HIST_BINS - 1;
       atomicAdd(&sh[((threadIdx.x & 63) % a.MT) * GS_HIST_BINS + bin], 1u);
     }
-    a.tc[i] = tc;
-    a.hops[i] = h;
+    if (a.tc) {  // results kept only when a sink will read them
+      a.tc[i] = tc;
+      a.hops[i] = h;
+    }
   }
   {
     const uint64_t d = wave_sum(deliv), s = wave_sum(lsum);
@@ -420,10 +422,13 @@ static void launch_seed(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, uint64
 // k_complete over the keys rows [0, un) (global ids u0 + row) into d_tc /
 // d_hops; with `mstat` also the per-message reductions, with `hist` the
 // 100 ms histograms of gs_msg_summary.
-static void run_complete(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, bool mstat, bool hist) {
+// store: write d_tc / d_hops (results go to a sink); without it only the
+// counters and reductions are produced (a device-resident run).
+static void run_complete(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, bool mstat, bool hist,
+                         bool store = true) {
   hipStream_t s = c.stream;
   CompArgs ca{};
-  ca.keys = c.d_keys.p; ca.pub = c.d_pub.p; ca.tpub = c.d_tpub.p; ca.tc = c.d_tc.p;
+  ca.keys = c.d_keys.p; ca.pub = c.d_pub.p; ca.tpub = c.d_tpub.p; ca.tc = store ? c.d_tc.p : nullptr;
   ca.hops = c.d_hops.p; ca.counters = c.d_counters.p; ca.N = un; ca.B = b.B; ca.F = b.F;
   ca.FP = b.FP; ca.L = b.L; ca.sb = b.sb; ca.tshift = b.tshift; ca.collide = b.collide ? 1 : 0;
   ca.u0 = u0;
@@ -592,7 +597,7 @@ static void deliver(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, const gs_r
 static void launch_complete(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, const gs_result_sink* sink,
                             uint64_t sink_row0) {
   const bool hist = sink && sink->summary;
-  run_complete(c, b, u0, un, hist, hist);
+  run_complete(c, b, u0, un, hist, hist, sink != nullptr);
   deliver(c, b, u0, un, sink, sink_row0);
 }
 
@@ -1016,7 +1021,7 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
         launch_complete(c, b, 0, N, sink, i0);
         done = true;
       } else {  // keep the eager result only if gossip provably changes nothing
-        run_complete(c, b, 0, N, true, sink && sink->summary);
+        run_complete(c, b, 0, N, true, sink && sink->summary, sink != nullptr);
         std::vector<uint64_t> ms((size_t)B * MS_COLS);
         GS_HIP(hipMemcpyAsync(ms.data(), c.d_mstat.p, ms.size() * 8, hipMemcpyDeviceToHost, s));
         GS_HIP(hipStreamSynchronize(s));
