@@ -25,7 +25,7 @@ struct Error {
 };
 
 // Device-side error word bits (set by kernels, checked by the host).
-enum : uint32_t { ERR_TIME = 1, ERR_HOPS = 2, ERR_MESH = 4, ERR_DEG = 8, ERR_SYNC = 16 };
+enum : uint32_t { ERR_TIME = 1, ERR_HOPS = 2, ERR_MESH = 4, ERR_DEG = 8 };
 
 // Device buffer owned by a context.
 template <class T>
@@ -51,6 +51,7 @@ struct DevBuf {
 enum : uint32_t {
   C_FD = 0, C_R = 1, C_DELIV = 2, C_LAT_SUM = 3, C_LAT_MAX = 4, C_BUCKETS = 5,
   C_R_FWD = 6, C_MESH_CHANGES = 7, C_MESH_WAKE = 8, C_ERR = 9, C_PUSH = 10, C_GOSSIP = 11, C_PASSES = 12,
+  C_GLISTED = 13, C_TSCANNED = 14,  // diagnostics (GS_DEBUG_COUNTS): gossip-listed lanes, tiles scanned
   C_COUNT = 16
 };
 
@@ -95,7 +96,6 @@ struct Ctx {
   DevBuf<uint32_t> d_mesh;   // [N*MESH_W] packed stage<<24|peer, EMPTY padded
   DevBuf<uint32_t> d_lat32;  // [S*S] u32 latency for the mesh kernels
   // churn: ring of per-epoch snapshots, slot = epoch % ring_R
-  DevBuf<uint64_t> d_off;       // offline bitset scratch (gs_mesh_converge)
   DevBuf<uint32_t> d_ring_mesh; // [R][N][MESH_W]
   DevBuf<uint64_t> d_ring_off;  // [R][(N+63)/64]
   DevBuf<uint32_t> d_ring_in;     // lazy gossip: [R][N][GT_IN] senders of the IHAVEs reaching a peer per epoch
@@ -106,7 +106,6 @@ struct Ctx {
   DevBuf<uint8_t> d_mcnt;    // [N]
   DevBuf<uint8_t> d_pst;     // event-driven churn epochs: [PS_PLANES][N] per-peer flags and counts
   DevBuf<uint64_t> d_offlin; // offline bitsets of a run of churn epochs, [epochs + 1][(N+63)/64]
-  DevBuf<uint32_t> d_bar;    // k_epochs grid barrier counter
 
   // dissemination (per batch)
   DevBuf<uint64_t> d_keys;   // [N * B * FP] peer-major (u, m, f)
@@ -123,6 +122,7 @@ struct Ctx {
   DevBuf<uint32_t> d_tstamp; // split tile skip + gossip: launch + 1 of the last scan
   DevBuf<uint32_t> d_gl_idx; // lazy gossip: lanes with an IHAVE arrival in the bucket
   DevBuf<uint32_t> d_gl_cnt;
+  DevBuf<uint64_t> d_gl_key; // receiver-centric gossip: the listed lane's key (saves its re-read)
   DevBuf<uint64_t> d_nonfinal;  // [3]
   DevBuf<uint64_t> d_rel0;   // [B] first heartbeat >= t_pub (relative ns)
   DevBuf<uint64_t> d_habs0;  // [B] its absolute heartbeat index

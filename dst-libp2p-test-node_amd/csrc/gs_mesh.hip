@@ -548,32 +548,21 @@ __global__ __launch_bounds__(TB) void k_gossip_in_range(const uint64_t* __restri
                       d_lazy, gf_milli, ring_in + slot * N * GT_IN, ring_incnt + slot * N, u);
 }
 
-// ---- fused churn epochs (one cooperative launch for a run of epochs) ----
-// The per-epoch kernels above take ~196 us per epoch at 100k peers in 7
-// launches, latency- and launch-bound (the mesh state is Infinity-Cache
-// resident). k_epochs runs epochs [h0, h1] in one persistent cooperative grid
-// with two grid barriers per epoch, because only two steps read other rows:
-//   1  own rows: disconnect, heartbeat decisions (GRAFT/PRUNE proposals)
-//   -- barrier --
-//   2  offline bits of epoch h+1; GRAFT handling (reads the proposers' rows)
-//   -- barrier --
-//   3  own rows: apply (reads the neighbours' PRUNEs), ELL extraction into
-//      the ring slot, IHAVE targets of (u, h)
-// Step 3 of epoch h and step 1 of epoch h+1 touch only their own rows, so
-// they need no barrier between them. Proposals are double-buffered by epoch
-// parity: a wave clears its own row of prop[h & 1] in step 1 of epoch h, when
-// every reader of epoch h-2 is past the barriers of epoch h-1.
-
-// Offline bitset of epoch h into off (grid-strided waves of 64 peers).
-__device__ __forceinline__ void offline_words(uint32_t N, uint64_t seed, uint32_t ppm, uint32_t down, uint64_t h,
-                                              uint64_t* off, uint32_t gw, uint32_t nw) {
-  const int lane = threadIdx.x & 63;
-  for (uint32_t base = gw * 64; base < N; base += nw * 64) {
-    const uint32_t u = base + lane;
-    const uint64_t m = __ballot(u < N && offline_draw(seed, ppm, down, u, h));
-    if (lane == 0) off[base >> 6] = m;
-  }
-}
+// ---- event-driven churn epochs (the default run_epochs path) ----
+// Under churn most rows do nothing in a given epoch (1 % departures per epoch:
+// ~18 % of the rows change, most of them by one dropped link). Each step of an
+// epoch therefore tests a few per-peer flags (MeshArgs::pst) and runs the
+// row code only where the step can change the row; every rule is the one of
+// the per-row kernels above, so the result is the same mesh:
+//  heartbeat step: rows going offline, rows with a mesh neighbour going
+//    offline (flagged by that neighbour), rows outside [D_lo, D_hi] or below
+//    D_out (the only ones a heartbeat can change), rows whose last proposals
+//    must be cleared;
+//  GRAFT handling: rows a neighbour proposed to;
+//  apply: proposers and PRUNEd rows; rows whose mesh changed are recounted
+//    and re-extracted into the ring slot, the others copy their previous row.
+// Offline bitsets and IHAVE targets do not depend on the epoch sequence and
+// run batched over the whole range (k_offline_range, k_gossip_in_range).
 
 // ELL row of u from its CSR flags (packed stage<<24 | peer, ascending ids).
 template <int G>
@@ -598,92 +587,6 @@ __device__ __forceinline__ void row_extract(const MeshArgs& a, uint32_t u, uint3
   if (cnt > MESH_W && lane == 0) atomicOr((unsigned*)&a.counters[C_ERR], ERR_MESH);
   if ((uint32_t)lane >= cnt && lane < (int)MESH_W) mesh[(size_t)u * MESH_W + lane] = EMPTY;
 }
-
-// Grid barrier for the co-resident grid of k_epochs: a monotonic arrival
-// counter (zeroed before the launch), the k-th barrier waits for k * blocks
-// arrivals. Agent-scope release before arriving and acquire after leaving
-// make the other blocks' row updates visible across XCDs. The spin is bounded:
-// a barrier that does not complete (a block that never got a CU) raises
-// ERR_SYNC and lets every wave run to the end of the kernel instead of hanging.
-constexpr uint64_t BARRIER_SPINS = 1ull << 22;  // x ~1 us sleeps
-__device__ __forceinline__ void grid_barrier(uint32_t* bar, uint32_t nblocks, uint32_t& target, uint64_t* counters) {
-  __syncthreads();
-  target += nblocks;
-  if (threadIdx.x == 0) {
-    __threadfence();
-    atomicAdd(bar, 1u);
-    uint64_t spins = 0;
-    uint32_t* err = (uint32_t*)&counters[C_ERR];
-    while (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(8);
-      if ((++spins & 1023) == 0 && (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ERR_SYNC))
-        break;  // another block timed out: run to the end
-      if (spins > BARRIER_SPINS) {
-        atomicOr(err, ERR_SYNC);
-        break;
-      }
-    }
-    __threadfence();
-  }
-  __syncthreads();
-}
-
-struct EpochArgs {
-  MeshArgs m;
-  uint32_t* bar;         // grid barrier counter (zeroed before the launch)
-  uint8_t* prop2;        // [2][nnz] proposals by epoch parity
-  uint64_t* off;         // [off_R][w64] offline bitsets, slot h % off_R
-  uint32_t* ring_mesh;   // [ring_R][N][MESH_W] or nullptr (no snapshots)
-  uint64_t h0, h1;
-  uint32_t off_R, ring_R, w64, ppm, down, d_lazy, gf_milli;
-};
-
-__global__ __launch_bounds__(TB) void k_epochs(EpochArgs e) {
-  uint32_t target = 0;
-  const uint32_t gw = blockIdx.x * (TB / 64) + (threadIdx.x >> 6), nw = gridDim.x * (TB / 64);
-  const uint32_t N = e.m.N;
-  const uint64_t nnz = e.m.row[N];
-  offline_words(N, e.m.seed, e.ppm, e.down, e.h0, e.off + (size_t)(e.h0 % e.off_R) * e.w64, gw, nw);
-  grid_barrier(e.bar, gridDim.x, target, e.m.counters);
-  for (uint64_t h = e.h0; h <= e.h1; h++) {  // every wave runs every epoch: the barriers are grid-uniform
-    MeshArgs a = e.m;
-    a.epoch = (uint32_t)h;
-    a.off = e.off + (size_t)(h % e.off_R) * e.w64;
-    a.prop = e.prop2 + (size_t)(h & 1) * nnz;
-    for (uint32_t u = gw; u < N; u += nw) {
-      const uint64_t b = a.row[u], en = a.row[u + 1];
-      for (uint64_t x = b + (threadIdx.x & 63); x < en; x += 64) a.prop[x] = 0;
-      row_disconnect<64>(a, u);
-      row_heartbeat<64>(a, u);
-    }
-    grid_barrier(e.bar, gridDim.x, target, e.m.counters);
-    if (h < e.h1)
-      offline_words(N, e.m.seed, e.ppm, e.down, h + 1, e.off + (size_t)((h + 1) % e.off_R) * e.w64, gw, nw);
-    for (uint32_t u = gw; u < N; u += nw) row_handle_graft<64>(a, u);
-    grid_barrier(e.bar, gridDim.x, target, e.m.counters);
-    const size_t slot = (size_t)(h % (e.ring_R ? e.ring_R : 1));
-    for (uint32_t u = gw; u < N; u += nw) {
-      row_apply<64>(a, u);
-      if (e.ring_mesh) row_extract<64>(a, u, e.ring_mesh + slot * N * MESH_W);
-    }
-  }
-}
-
-// ---- event-driven churn epochs (the default run_epochs path) ----
-// Under churn most rows do nothing in a given epoch (1 % departures per epoch:
-// ~18 % of the rows change, most of them by one dropped link). Each step of an
-// epoch therefore tests a few per-peer flags (MeshArgs::pst) and runs the
-// row code only where the step can change the row; every rule is the one of
-// the per-row kernels above, so the result is the same mesh:
-//  heartbeat step: rows going offline, rows with a mesh neighbour going
-//    offline (flagged by that neighbour), rows outside [D_lo, D_hi] or below
-//    D_out (the only ones a heartbeat can change), rows whose last proposals
-//    must be cleared;
-//  GRAFT handling: rows a neighbour proposed to;
-//  apply: proposers and PRUNEd rows; rows whose mesh changed are recounted
-//    and re-extracted into the ring slot, the others copy their previous row.
-// Offline bitsets and IHAVE targets do not depend on the epoch sequence and
-// run batched over the whole range (k_offline_range, k_gossip_in_range).
 
 // Mesh links of u (all, outbound) from its CSR flags.
 template <int G>
@@ -858,7 +761,7 @@ void ring_in_lists(Ctx& c, uint64_t h0, uint64_t h1) {
 MeshArgs mesh_args(Ctx& c) {
   const uint32_t N = c.cfg.peers;
   c.d_until.alloc(c.nnz ? c.nnz : 1);
-  c.d_prop.alloc(2 * (c.nnz ? c.nnz : 1));  // two epoch parities (k_epochs); the per-epoch kernels use the first
+  c.d_prop.alloc(c.nnz ? c.nnz : 1);
   c.d_lat32.alloc((size_t)c.S * c.S);
   std::vector<uint32_t> lat32(c.lat_ns.begin(), c.lat_ns.end());
   GS_HIP(hipMemcpyAsync(c.d_lat32.p, lat32.data(), lat32.size() * 4, hipMemcpyHostToDevice, c.stream));
@@ -947,61 +850,9 @@ void ev_epochs(Ctx& c, MeshArgs a, uint64_t h0, uint64_t h1, bool ring) {
   if (ring) ring_in_lists(c, hr, h1);
 }
 
-// Churn epochs [h0, h1] from the current mesh state: event-driven (ev_epochs),
-// or with GS_MESH_FUSED=1 the cooperative kernel k_epochs (off: bitsets in
-// slots h % off_R). `ring`: also the ELL snapshots (+ IHAVE targets) into the
-// ring slots h % ring_R.
-void run_epochs(Ctx& c, MeshArgs a, uint64_t h0, uint64_t h1, uint64_t* off, uint32_t off_R, bool ring) {
-  const uint32_t N = c.cfg.peers;
-  const size_t w64 = ((size_t)N + 63) / 64;
-  hipStream_t s = c.stream;
-  const char* fe = getenv("GS_MESH_FUSED");
-  int coop = 0;
-  (void)hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, c.cfg.device);
-  if (!(fe && *fe == '1') || !coop) {
-    ev_epochs(c, a, h0, h1, ring);
-    return;
-  }
-  EpochArgs e{};
-  e.m = a;
-  e.m.sub = 0;
-  e.prop2 = c.d_prop.p;
-  e.off = off;
-  e.off_R = off_R;
-  e.w64 = (uint32_t)w64;
-  e.ppm = c.cfg.churn_ppm;
-  e.down = c.cfg.churn_down;
-  e.h0 = h0;
-  e.h1 = h1;
-  if (ring) {
-    e.ring_R = c.ring_R;
-    e.ring_mesh = c.d_ring_mesh.p;
-  }
-  int per_cu = 0;
-  GS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_epochs, TB, 0));
-  if (c.num_cus == 0) {
-    hipDeviceProp_t prop;
-    c.num_cus = hipGetDeviceProperties(&prop, c.cfg.device) == hipSuccess ? prop.multiProcessorCount : 256;
-  }
-  // co-resident blocks only (the grid barrier needs every block running): at
-  // most 2 per CU, well inside the occupancy limit; more waves than rows would
-  // only spin at the barriers
-  const uint64_t need = ((uint64_t)N + TB / 64 - 1) / (TB / 64);
-  const char* bpc = getenv("GS_EPOCH_BLOCKS_PER_CU");
-  const int want = bpc && *bpc ? atoi(bpc) : per_cu;
-  const unsigned grid = (unsigned)std::max<uint64_t>(
-      1, std::min<uint64_t>((uint64_t)std::min(std::max(per_cu, 1), std::max(want, 1)) * c.num_cus, need));
-  c.d_bar.alloc(1);
-  GS_HIP(hipMemsetAsync(c.d_bar.p, 0, 4, s));
-  e.bar = c.d_bar.p;
-  void* args[] = {&e};
-  GS_HIP(hipLaunchCooperativeKernel((const void*)k_epochs, dim3(grid), dim3(TB), args, 0, s));
-  GS_HIP(hipGetLastError());
-  GS_HIP(hipMemcpyAsync(c.h_pinned, c.d_counters.p + C_ERR, 8, hipMemcpyDeviceToHost, s));
-  GS_HIP(hipStreamSynchronize(s));
-  if (c.h_pinned[0] & ERR_SYNC) c.fail(GS_EDEVICE, "k_epochs grid barrier timed out (blocks not co-resident)");
-  if (ring) ring_in_lists(c, h1 - h0 + 1 > c.ring_R ? h1 + 1 - c.ring_R : h0, h1);
-}
+// Churn epochs [h0, h1] from the current mesh state (ev_epochs); `ring`:
+// also the ELL snapshots (+ inverse IHAVE lists) into the ring slots h % ring_R.
+void run_epochs(Ctx& c, MeshArgs a, uint64_t h0, uint64_t h1, bool ring) { ev_epochs(c, a, h0, h1, ring); }
 
 }  // namespace
 
@@ -1030,7 +881,7 @@ void churn_ring(Ctx& c, uint64_t h_lo, uint64_t h_hi) {
     }
   }
   if (c.churn_state + 1 <= h_hi)
-    run_epochs(c, a, c.churn_state + 1, h_hi, c.d_ring_off.p, R, true);
+    run_epochs(c, a, c.churn_state + 1, h_hi, true);
   GS_HIP(hipGetLastError());
   if (h_hi > c.churn_state) {
     c.churn_state = h_hi;
@@ -1052,8 +903,7 @@ uint32_t run_mesh(Ctx& c, uint32_t max_hb) {
   uint32_t epoch = 1, last = 0;
   uint64_t* h = c.h_pinned;
   if (c.cfg.churn_ppm) {  // no fixed point under churn: exactly max_hb epochs
-    c.d_off.alloc(2 * (((size_t)N + 63) / 64));
-    if (max_hb >= 1) run_epochs(c, a, 1, max_hb, c.d_off.p, 2, false);
+    if (max_hb >= 1) run_epochs(c, a, 1, max_hb, false);
     last = max_hb;
     c.churn_state = max_hb;  // the ring restarts after this state
     c.ring_lo = (uint64_t)max_hb + 1;

@@ -16,6 +16,7 @@
 // with 64-bit atomicMin pushes into the same (m,f) slot of the targets, and
 // reduces the next pending key to pick the next bucket on the device
 // (triple-buffered ctrl words; no host round trip per bucket).
+#include <stdio.h>
 #include <string.h>
 
 #include <algorithm>
@@ -682,6 +683,11 @@ static void collect_stats(Ctx& c) {
   c.stats.bytes_alg = 16 * h[C_FD] + 12 * c.stats.relaxations + 8 * h[C_DELIV];
   c.stats.relax_bytes_alg = 16 * h[C_FD] + 12 * h[C_R_FWD];
   c.stats.pushes = h[C_PUSH];
+  static const bool dbg = getenv("GS_DEBUG_COUNTS") != nullptr;
+  if (dbg)
+    fprintf(stderr, "[gs] buckets %llu gossip-listed lanes %llu tiles scanned %llu iwant %llu\n",
+            (unsigned long long)h[C_BUCKETS], (unsigned long long)h[C_GLISTED], (unsigned long long)h[C_TSCANNED],
+            (unsigned long long)h[C_GOSSIP]);
 }
 
 static void ensure_cus(Ctx& c) {
@@ -967,6 +973,10 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
           GS_HIP(hipMemsetAsync(c.d_nonfinal.p, 0, 3 * 8, s));
           ra.gl_idx = c.d_gl_idx.p;
           ra.gl_cnt = c.d_gl_cnt.p;
+          if (ra.ring_in) {
+            c.d_gl_key.alloc(nwaves * ra.gl_cap);
+            ra.gl_key = c.d_gl_key.p;
+          }
           ra.nonfinal = c.d_nonfinal.p;
           if ((v & 10) == 10) {
             ra.tgmin = c.d_tgmin.p;

@@ -66,6 +66,7 @@ struct RelaxArgs {
   // of each epoch (k_gossip_in_range): [R][N][GT_IN] senders (stage<<24 | id)
   const uint32_t* ring_in;
   const uint32_t* ring_incnt;  // [R][N] their number (> GT_IN: recompute)
+  uint64_t* gl_key;            // receiver-centric: the listed lane's key
   const uint32_t* mesh;
   const uint32_t* pub;
   const uint8_t* stage;
@@ -460,7 +461,7 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
   const uint64_t nwaves = (uint64_t)gridDim.x * (TB / 64);
   const size_t seg = (size_t)wave * a.seg_cap;
   const size_t gseg = (size_t)wave * a.gl_cap;
-  uint64_t nmin = INF64, nonfin = 0;
+  uint64_t nmin = INF64, nonfin = 0, nscan = 0;
   uint32_t cnt = 0, gcnt = 0, err = 0;
   const uint64_t hspan = GOSSIP ? (uint64_t)a.hist * a.hb_ns : 0;
   // Tiles are visited per wave in groups: with SKIP a group is 64 consecutive
@@ -502,6 +503,7 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
    while (todo) {  // wave-uniform
     const uint64_t tile = grp * GT + (uint64_t)__builtin_ctzll(todo);
     todo &= todo - 1;
+    nscan++;
     const uint64_t gid = (tile << 6) + lane;
     const bool valid = gid < a.total;
     const uint64_t key = valid ? a.keys[gid] : INF64;
@@ -581,7 +583,11 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
         nmin = gk < nmin ? gk : nmin;
       }
       const uint64_t gm = __ballot(gwork);
-      if (gwork) a.gl_idx[gseg + gcnt + (uint32_t)__popcll(gm & ((1ull << lane) - 1))] = (uint32_t)gid;
+      if (gwork) {
+        const uint32_t pos = gcnt + (uint32_t)__popcll(gm & ((1ull << lane) - 1));
+        a.gl_idx[gseg + pos] = (uint32_t)gid;
+        if (a.gl_key) a.gl_key[gseg + pos] = key;
+      }
       gcnt += (uint32_t)__popcll(gm);
       if constexpr (SKIP) {  // the tile's gossip state for later skips
         const uint64_t tg = wave_min(gnext);
@@ -621,10 +627,12 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
       if (err) atomicOr((unsigned*)&a.counters[C_ERR], err);
     }
   }
-  __shared__ uint64_t s_red[TB / 64 * 2];
-  const uint64_t ws[1] = {nonfin};
-  unsigned long long* const ps[1] = {GOSSIP ? (unsigned long long*)&a.nonfinal[a.launch % 3] : nullptr};
-  block_flush<TB / 64, 1>(nmin, ws, (unsigned long long*)&a.ctrl[(a.launch + 1) % 3], ps, s_red, 2);
+  __shared__ uint64_t s_red[TB / 64 * 4];
+  const uint64_t ws[3] = {nonfin, GOSSIP ? (uint64_t)gcnt : 0, nscan};
+  unsigned long long* const ps[3] = {GOSSIP ? (unsigned long long*)&a.nonfinal[a.launch % 3] : nullptr,
+                                     (unsigned long long*)&a.counters[C_GLISTED],
+                                     (unsigned long long*)&a.counters[C_TSCANNED]};
+  block_flush<TB / 64, 3>(nmin, ws, (unsigned long long*)&a.ctrl[(a.launch + 1) % 3], ps, s_red, 4);
 }
 
 // Lazy gossip of one bucket: for every listed final lane
@@ -722,9 +730,9 @@ __device__ __forceinline__ void for_each_gossip_target(const RelaxArgs& a, uint3
 // whose target already has the message.
 template <int FP>
 __device__ __forceinline__ void gossip_receiver(const RelaxArgs& a, const BucketLds& L, uint64_t lo, uint64_t hi,
-                                                uint32_t gid, uint64_t& nmin, uint64_t& iw, uint32_t& err) {
+                                                uint32_t gid, uint64_t kw, uint64_t& nmin, uint64_t& iw,
+                                                uint32_t& err) {
   const uint32_t LL = a.L, S = a.S;
-  const uint64_t kw = a.keys[gid];
   const uint64_t tw = kw == INF64 ? INF64 : kw >> a.tshift;
   const uint32_t w = row_of(gid, LL), slot = (uint32_t)(gid - (uint64_t)w * LL);
   const uint32_t m = slot / FP, sw = a.stage[w];
@@ -803,7 +811,8 @@ __global__ __launch_bounds__(TB) void k_gossip(RelaxArgs a) {
   uint64_t nmin = INF64, iw = 0;
   uint32_t err = 0;
   if (a.ring_in)
-    for (uint32_t i = lane; i < n; i += 64) gossip_receiver<FP>(a, L, lo, hi, a.gl_idx[seg + i], nmin, iw, err);
+    for (uint32_t i = lane; i < n; i += 64)
+      gossip_receiver<FP>(a, L, lo, hi, a.gl_idx[seg + i], a.gl_key[seg + i], nmin, iw, err);
   else
   for (uint32_t i = lane; i < n; i += 64) {
     const uint64_t gid = a.gl_idx[seg + i];
