@@ -51,7 +51,8 @@ struct DevBuf {
 enum : uint32_t {
   C_FD = 0, C_R = 1, C_DELIV = 2, C_LAT_SUM = 3, C_LAT_MAX = 4, C_BUCKETS = 5,
   C_R_FWD = 6, C_MESH_CHANGES = 7, C_MESH_WAKE = 8, C_ERR = 9, C_PUSH = 10, C_GOSSIP = 11, C_PASSES = 12,
-  C_GLISTED = 13, C_TSCANNED = 14,  // diagnostics (GS_DEBUG_COUNTS): gossip-listed lanes, tiles scanned
+  C_GLISTED = 13, C_TSCANNED = 14, C_TSCANNED_G = 15,  // diagnostics (GS_DEBUG_COUNTS): gossip-listed
+                                                       // lanes, tiles scanned, of them only for gossip
   C_COUNT = 16
 };
 

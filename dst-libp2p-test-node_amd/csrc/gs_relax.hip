@@ -685,9 +685,9 @@ static void collect_stats(Ctx& c) {
   c.stats.pushes = h[C_PUSH];
   static const bool dbg = getenv("GS_DEBUG_COUNTS") != nullptr;
   if (dbg)
-    fprintf(stderr, "[gs] buckets %llu gossip-listed lanes %llu tiles scanned %llu iwant %llu\n",
+    fprintf(stderr, "[gs] buckets %llu gossip-listed lanes %llu tiles scanned %llu (for gossip only %llu) iwant %llu\n",
             (unsigned long long)h[C_BUCKETS], (unsigned long long)h[C_GLISTED], (unsigned long long)h[C_TSCANNED],
-            (unsigned long long)h[C_GOSSIP]);
+            (unsigned long long)h[C_TSCANNED_G], (unsigned long long)h[C_GOSSIP]);
 }
 
 static void ensure_cus(Ctx& c) {

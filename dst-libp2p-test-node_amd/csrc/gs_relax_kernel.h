@@ -461,7 +461,7 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
   const uint64_t nwaves = (uint64_t)gridDim.x * (TB / 64);
   const size_t seg = (size_t)wave * a.seg_cap;
   const size_t gseg = (size_t)wave * a.gl_cap;
-  uint64_t nmin = INF64, nonfin = 0, nscan = 0;
+  uint64_t nmin = INF64, nonfin = 0, nscan = 0, nscan_g = 0;
   uint32_t cnt = 0, gcnt = 0, err = 0;
   const uint64_t hspan = GOSSIP ? (uint64_t)a.hist * a.hb_ns : 0;
   // Tiles are visited per wave in groups: with SKIP a group is 64 consecutive
@@ -478,10 +478,11 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
     // gossip its final lanes' next IHAVE arrival must lie beyond the bucket
     // too, and its non-final count stands.
     const uint64_t mt = grp * GT + lane;
-    bool skip = false;
+    bool skip = false, eskip = false;
     if (mt < ntiles) {
       const uint64_t tm = a.tmin[mt];
       skip = !a.touched[mt] && (tm == INF64 || (tm >> a.tshift) >= hi);
+      eskip = skip;
       uint64_t gm = INF64;
       if constexpr (GOSSIP) {
         if (skip) gm = a.tgmin[mt];
@@ -499,6 +500,7 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
       }
     }
     todo = __ballot(mt < ntiles && !skip);
+    if (GOSSIP) nscan_g += (uint64_t)__popcll(__ballot(mt < ntiles && eskip && !skip));
    }
    while (todo) {  // wave-uniform
     const uint64_t tile = grp * GT + (uint64_t)__builtin_ctzll(todo);
@@ -627,12 +629,13 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
       if (err) atomicOr((unsigned*)&a.counters[C_ERR], err);
     }
   }
-  __shared__ uint64_t s_red[TB / 64 * 4];
-  const uint64_t ws[3] = {nonfin, GOSSIP ? (uint64_t)gcnt : 0, nscan};
-  unsigned long long* const ps[3] = {GOSSIP ? (unsigned long long*)&a.nonfinal[a.launch % 3] : nullptr,
+  __shared__ uint64_t s_red[TB / 64 * 5];
+  const uint64_t ws[4] = {nonfin, GOSSIP ? (uint64_t)gcnt : 0, nscan, nscan_g};
+  unsigned long long* const ps[4] = {GOSSIP ? (unsigned long long*)&a.nonfinal[a.launch % 3] : nullptr,
                                      (unsigned long long*)&a.counters[C_GLISTED],
-                                     (unsigned long long*)&a.counters[C_TSCANNED]};
-  block_flush<TB / 64, 3>(nmin, ws, (unsigned long long*)&a.ctrl[(a.launch + 1) % 3], ps, s_red, 4);
+                                     (unsigned long long*)&a.counters[C_TSCANNED],
+                                     (unsigned long long*)&a.counters[C_TSCANNED_G]};
+  block_flush<TB / 64, 4>(nmin, ws, (unsigned long long*)&a.ctrl[(a.launch + 1) % 3], ps, s_red, 5);
 }
 
 // Lazy gossip of one bucket: for every listed final lane
