@@ -25,7 +25,7 @@ struct Error {
 };
 
 // Device-side error word bits (set by kernels, checked by the host).
-enum : uint32_t { ERR_TIME = 1, ERR_HOPS = 2, ERR_MESH = 4, ERR_DEG = 8 };
+enum : uint32_t { ERR_TIME = 1, ERR_HOPS = 2, ERR_MESH = 4, ERR_DEG = 8, ERR_LIST = 16 };  // ERR_LIST: list pull overflow (re-run on k_pull)
 
 // Device buffer owned by a context.
 template <class T>
@@ -60,6 +60,8 @@ enum : uint32_t {
 struct Batch {
   uint32_t B = 0, L = 0, F = 0, FP = 1, sb = 0, tshift = 0, Fe = 1;
   uint64_t lat_min = 0;  // smallest latency between used link classes (lazy-gossip no-op proof)
+  uint64_t ser_max = 0;      // largest uplink serialisation of a used link class
+  uint64_t lat_adj_max = 0;  // largest lat(x->y) + max(0, ser_dn(y) - ser_up(x)) over used classes
   bool collide = false;
   uint64_t payload = 0, tmax = 0, delta = 1;
   std::vector<uint64_t> tpub;
@@ -141,7 +143,15 @@ struct Ctx {
   DevBuf<uint32_t> d_lcnt;   // [2][N]
   DevBuf<uint8_t> d_rpos;    // [N][MESH_W] index of w in mesh(mesh[w][j])
   bool rpos_valid = false;
+  bool keys_log = false;       // keys hold the list pull path's final logs (not dense rows): k_lcomplete
+  uint32_t mesh_dmax = 0;      // widest frozen-mesh row (list pull ring bound); 0 = not known
   DevBuf<uint64_t> d_pctrl;  // [3][4] pass control slots
+  // list pull path (gs_lpull_kernel.h)
+  DevBuf<uint64_t> d_lblk;   // [K][N][L] candidate lists per destination-window slot
+  DevBuf<uint32_t> d_lst;    // [N][16] list lengths per destination window, final-log length
+  DevBuf<uint64_t> d_lp_save;  // [C_COUNT] counters before a list pull batch (overflow re-run)
+  DevBuf<uint32_t> d_lfin;   // [N][32] final bits
+  DevBuf<uint16_t> d_flane;  // [N][L] lanes of the final log
   DevBuf<uint64_t> d_counters;  // [C_COUNT]
   DevBuf<uint64_t> d_cnt_save;  // [C_COUNT] counters before a batch (gossip fallback restores them)
   uint64_t* h_pinned = nullptr; // pinned host mirror of ctrl + counters

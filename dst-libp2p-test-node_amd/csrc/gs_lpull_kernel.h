@@ -1,0 +1,619 @@
+// gs_lpull_kernel.h — owner-computes Delta-window pass over per-row candidate
+// lists, the default eager path when its bounds hold.
+// Included by gs_relax.hip after gs_pull_kernel.h (namespace gs::{anon}).
+//
+// Why: k_pull keeps every (peer, message) key in a dense row and re-reads the
+// live 64-lane chunks of the row in every window pass. At the peak of a
+// 1024-message batch every chunk holds a due key, so each of the ~17 windows
+// re-reads the whole 8 KB row and writes back every 64-B sector holding a
+// changed lane: 2.3x the algorithmic bytes (profiles/r02_v5). Here a lane's
+// state is never kept in a dense row during the passes:
+//
+//  - fin[w]: one bit per lane, set when the lane's key is final (emitted),
+//    held in registers (u32 word j in lane j) while the row is processed;
+//  - candidates that do not fall in the window being emitted are appended to
+//    the row's list for their destination window c' (slot c' % K of a ring of
+//    K lists of up to L entries); st[w] holds the K list lengths and the
+//    length of the row's final log, and is read with the row's header, so
+//    the pass that emits window c knows where its entries are without a
+//    dependent load;
+//  - final keys are appended to a per-row log (the keys buffer, emission
+//    order, lanes in flane) and scattered back to the dense [N][L] layout
+//    once per batch (k_lfinal) for k_complete.
+//
+// A pass PULLing window b's records (emitting c = b+1) min-reduces, per lane
+// in LDS, the entries listed for c and this pass's candidates from the
+// neighbours' records; final lanes are dropped when the minima are
+// classified. A lane whose minimum lies in window c is final (Delta-stepping:
+// every later candidate is >= the start of window c+1); a lane whose minimum
+// lies later is appended once, as the best of this pass, to the list of its
+// window. Candidates worse than a listed one are harmless: the lane is final
+// by the time their window comes. The candidate arithmetic and the records are
+// k_pull's, so the keys are bit-identical. A list that would outgrow L entries
+// sets ERR_LIST and the host re-runs the batch on k_pull.
+//
+// Entry (u64): t - (c' * Delta) | hops | src | lane, the key's low (hops |
+// src) bits kept as they are; the host checks the widths fit.
+
+constexpr uint32_t LP_KMAX = 12;  // ring of destination-window lists
+constexpr uint32_t LP_SW = 16;    // u32 words of per-row state: list lengths [0..11] (slot = window % K), log length
+constexpr uint32_t LP_LOG = 15;   // state word holding the final-log length
+
+struct LPullArgs {
+  uint64_t* keys;       // [N][L] final log during the passes; dense again after k_lfinal
+  uint16_t* flane;      // [N][L] lane of each log entry
+  uint64_t* busy;       // [N][B] uplink FIFO end per (peer, message), FP > 1
+  uint64_t* blk;        // [K][N][ls] candidate lists per destination-window slot
+  uint32_t* st;         // [N][LP_SW]
+  uint32_t* fin;        // [N][32] final bits, 32 lanes per word
+  uint64_t* lrec;       // [2][N][L] per-row arrival records (k_pull's format)
+  uint32_t* lcnt;       // [2][N]
+  const uint32_t* mesh;
+  const uint8_t* rpos;
+  const uint32_t* pub;
+  const uint8_t* stage;
+  const uint32_t* tables;
+  uint64_t* ctrl;       // [3][4] k_pull's pass control slots
+  uint64_t* counters;
+  uint64_t delta, tmax;
+  uint32_t N, B, L, S, sb, tshift, pass, K, lb, dG;  // lb = lane bits, dG = Delta in key hi-word grains
+  uint32_t ls, lcap;  // list stride (max(L, 256) entries) and capacity (ls; GS_LPULL_CAP lowers it)
+};
+
+constexpr uint32_t LP_FW = PULL_LMAX / 32;  // u32 final-bit words per row
+
+__device__ __forceinline__ uint32_t sat32(uint64_t x) { return x > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)x; }
+
+// Offset of key hi word hx from the emitted window (thr[k] = start of window c + k).
+__device__ __forceinline__ uint32_t lp_rof(uint32_t hx, const uint32_t (&thr)[LP_KMAX + 1], uint32_t K) {
+  uint32_t r = 0;
+#pragma unroll
+  for (uint32_t k = 1; k <= LP_KMAX; k++) r += (k <= K && hx >= thr[k]) ? 1u : 0u;
+  return r;  // r == K: beyond the ring (an error the host bound rules out)
+}
+
+template <int FP>
+__global__ __launch_bounds__(TB, 4) void k_lpull(LPullArgs a) {
+  __shared__ PullLds Ls;  // 40 KB: 4 blocks (16 waves) per CU, as k_pull
+  // ---- decide this pass from the previous slot (grid-uniform; k_pull's rule) ----
+  const uint64_t* pv = a.ctrl + ((a.pass + 2) % 3) * 4;
+  uint64_t lo, mode;
+  if (pv[1] != PM_DONE && pv[2]) { mode = PM_PULL; lo = pv[1] == PM_PULL ? pv[0] + a.delta : pv[0]; }
+  else if (pv[3] != INF64) { mode = PM_EMIT; lo = ((pv[3] >> a.tshift) / a.delta) * a.delta; }
+  else { mode = PM_DONE; lo = pv[0]; }
+  uint64_t* me = a.ctrl + (a.pass % 3) * 4;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    me[0] = lo;
+    me[1] = mode;
+    uint64_t* nx = a.ctrl + ((a.pass + 1) % 3) * 4;
+    nx[2] = 0;
+    nx[3] = INF64;
+    if (mode != PM_DONE) atomicAdd((unsigned long long*)&a.counters[C_PASSES], 1ull);
+    if (mode == PM_PULL) atomicAdd((unsigned long long*)&a.counters[C_BUCKETS], 1ull);
+  }
+  if (mode == PM_DONE) return;
+
+  const bool pull = mode == PM_PULL;
+  const uint64_t wlo = pull ? lo + a.delta : lo;  // the window this pass emits
+  const uint64_t c = wlo / a.delta;                // its index (scalar division, once)
+  const uint32_t K = a.K, LL = a.L, S = a.S;
+  const uint32_t cslot = (uint32_t)(c % K);
+  const uint64_t hlo64 = c * a.dG;
+  uint32_t thr[LP_KMAX + 1];
+#pragma unroll
+  for (uint32_t k = 0; k <= LP_KMAX; k++) thr[k] = sat32(hlo64 + (uint64_t)k * a.dG);
+  const uint32_t hlo = thr[0], hspan = a.dG;  // hi words of window c: [hlo, hlo + dG)
+  const size_t NL = (size_t)a.N * LL;
+  const uint32_t pb = (a.pass + 1) & 1, nb = a.pass & 1;  // records read / written
+  const uint64_t* rrec = a.lrec + pb * NL;
+  const uint32_t* rcnt = a.lcnt + (size_t)pb * a.N;
+  uint64_t* wrec = a.lrec + nb * NL;
+  uint32_t* wcnt = a.lcnt + (size_t)nb * a.N;
+  const uint32_t* lat = a.tables;
+  const uint32_t* sup = a.tables + S * S;
+  const uint32_t* sdn = a.tables + S * S + S;
+
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint64_t* CW = Ls.cw[wv];
+  uint16_t* LST = Ls.lst[wv];
+  const uint64_t smask = (1ull << a.sb) - 1;
+  const uint32_t hmask = (1u << HOP_BITS) - 1;
+  const uint64_t lanelt = (1ull << lane) - 1;
+  const uint64_t lowmask = (1ull << a.tshift) - 1;
+  // per state lane j < K: the window its counter slot stands for, as a hi word
+  const uint32_t lwin = lane < (int)K ? (uint32_t)(((uint32_t)lane + K - cslot) % K) : 0u;
+  const uint32_t lwhi = sat32(hlo64 + (uint64_t)lwin * a.dG);
+  uint64_t fd = 0, nr = 0, np = 0, nrec = 0;
+  uint32_t nmh = ~0u;
+  uint32_t err = 0;
+#ifdef GS_PULL_PROF
+  uint64_t pp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+
+#pragma unroll
+  for (int q = 0; q < (int)PULL_CH; q++) CW[q * 64 + lane] = INF64;
+  wave_lds_sync();
+
+  const uint32_t stride = gridDim.x * PULL_WAVES;
+  uint32_t w = blockIdx.x * PULL_WAVES + wv;
+  uint32_t ej = EMPTY, cj = 0, rj = 0, sv = 0;
+  if (w < a.N && lane < (int)MESH_W) {
+    ej = a.mesh[(size_t)w * MESH_W + lane];
+    rj = a.rpos[(size_t)w * MESH_W + lane];
+    if (pull && ej != EMPTY) cj = rcnt[ej & 0xFFFFFFu];
+    sv = a.st[(size_t)w * LP_SW + lane];
+  }
+  for (; w < a.N; w += stride) {
+    PP_T(tA);
+    const uint32_t w2 = w + stride;
+    uint32_t ej2 = EMPTY, rj2 = 0, cj2 = 0, sv2 = 0;
+    if (w2 < a.N && lane < (int)MESH_W) {  // w2 < N is wave-uniform
+      ej2 = a.mesh[(size_t)w2 * MESH_W + lane];
+      rj2 = a.rpos[(size_t)w2 * MESH_W + lane];
+      sv2 = a.st[(size_t)w2 * LP_SW + lane];
+    }
+    const uint64_t cand = __ballot(cj != 0);
+    const uint32_t due = __builtin_amdgcn_readlane(sv, cslot);  // entries destined to window c
+    if (cand == 0 && due == 0) {  // nothing to apply, nothing due: the pending windows stay
+      if (lane == 0) wcnt[w] = 0;
+      if (lane < (int)K && sv) nmh = umin32(nmh, lwhi);
+      if (pull && lane < (int)MESH_W && ej2 != EMPTY) cj2 = rcnt[ej2 & 0xFFFFFFu];
+      ej = ej2; rj = rj2; cj = cj2; sv = sv2;
+      PP_T(tS);
+      PP_ADD(0, tS - tA);
+      continue;
+    }
+    PP_ADD(7, 1);
+    const uint32_t sw = a.stage[w];
+    uint32_t fin32 = lane < (int)LP_FW ? a.fin[(size_t)w * LP_FW + lane] : 0u;
+    // 1. the entries listed for window c (final lanes are dropped in step 3)
+    uint32_t cb = 0;
+    if (due) {
+      const uint64_t* lst = a.blk + ((size_t)cslot * a.N + w) * a.ls;
+      const uint32_t lmask = (1u << a.lb) - 1, tsh = a.tshift + a.lb;
+      for (uint32_t f0 = 0; f0 < due; f0 += 256) {
+        uint64_t e[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const uint32_t f = f0 + u * 64 + lane;
+          e[u] = f < due ? lst[f] : ~0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          if (e[u] == ~0ull) continue;
+          const uint32_t li = (uint32_t)e[u] & lmask;
+          const uint64_t key = ((wlo + (e[u] >> tsh)) << a.tshift) | ((e[u] >> a.lb) & lowmask);
+          atomicMin((unsigned long long*)&CW[li], (unsigned long long)key);
+          cb |= 1u << (li >> 6);
+        }
+      }
+    }
+    PP_T(tG);
+    PP_ADD(1, tG - tA);
+    // 2. this pass's candidates from the neighbours' records of window lo
+    if (pull) {
+      const uint32_t sd = sdn[sw];
+      uint64_t cmk = cand;
+      while (cmk) {
+        uint32_t U[4], R4[4], NN[4], SER[4];
+        uint64_t BASE[4];
+        uint32_t maxn = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          U[k] = 0; R4[k] = 0; NN[k] = 0; SER[k] = 0; BASE[k] = 0;
+          if (cmk) {  // wave-uniform
+            const int j = __builtin_ctzll(cmk);
+            cmk &= cmk - 1;
+            const uint32_t e = __builtin_amdgcn_readlane(ej, j);
+            U[k] = e & 0xFFFFFFu;
+            R4[k] = __builtin_amdgcn_readlane(rj, j);
+            NN[k] = __builtin_amdgcn_readlane(cj, j);
+            const uint32_t su = e >> STAGE_SHIFT;
+            SER[k] = sup[su];
+            BASE[k] = lo + lat[su * S + sw] + (sd > SER[k] ? sd - SER[k] : 0);
+            maxn = NN[k] > maxn ? NN[k] : maxn;
+          }
+        }
+        for (uint32_t i0 = 0; i0 < maxn; i0 += 128) {
+          uint64_t rec[4][2];
+#pragma unroll
+          for (int k = 0; k < 4; k++)
+#pragma unroll
+            for (int cc = 0; cc < 2; cc++) {
+              const uint32_t i = i0 + cc * 64 + lane;
+              rec[k][cc] = i < NN[k] ? rrec[(size_t)U[k] * LL + i] : ~0ull;
+            }
+#pragma unroll
+          for (int k = 0; k < 4; k++)
+#pragma unroll
+            for (int cc = 0; cc < 2; cc++) {
+              const uint64_t rc = rec[k][cc];
+              if (rc == ~0ull) continue;  // no record (records never have all bits set)
+              const uint32_t lo32 = (uint32_t)rc, r = R4[k];
+              const uint32_t js = (lo32 >> 21) & 31u, jp = (lo32 >> 16) & 31u;
+              if (js == r || jp == r) continue;  // w is the source or the publisher
+              const uint32_t slot = lo32 & 0xFFFFu;
+              const uint32_t pos = r + 1 - (js < r ? 1u : 0u) - ((jp < r && jp != js) ? 1u : 0u);
+              const uint64_t arr = BASE[k] + (rc >> 32) + (uint64_t)(pos * SER[k]);
+              if (arr > a.tmax) err |= ERR_TIME;
+              const uint64_t hp1 = ((lo32 >> 26) & hmask) + 1;
+              const uint64_t nk = (arr << a.tshift) | (hp1 << a.sb) | U[k];
+              atomicMin((unsigned long long*)&CW[slot], (unsigned long long)nk);
+              cb |= 1u << (slot >> 6);
+            }
+        }
+      }
+    }
+    for (int off = 32; off > 0; off >>= 1) cb |= __shfl_xor(cb, off);
+    cb = __builtin_amdgcn_readfirstlane(cb);
+    wave_lds_sync();
+    if (pull && lane < (int)MESH_W && ej2 != EMPTY) cj2 = rcnt[ej2 & 0xFFFFFFu];  // next row's lists
+    // 3. classify the minima of the touched chunks: final lanes are dropped
+    //    (candidates are not filtered on the way in), a minimum in window c is
+    //    final now (logged, marked, its lane / group indexed from the front of
+    //    LST), a later one is pending (indexed from the back). Keys stay where
+    //    they are in CW.
+    PP_T(tR);
+    PP_ADD(2, tR - tG);
+    const uint32_t log0 = __builtin_amdgcn_readlane(sv, LP_LOG);
+    uint32_t logc = log0, cnt = 0, npend = 0, nfin = 0;  // the finals are logged in step 4
+#pragma unroll
+    for (int q = 0; q < (int)PULL_CH; q++) {
+      if (!((cb >> q) & 1u)) continue;  // wave-uniform
+      const uint32_t i = q * 64 + lane;
+      const uint64_t fw = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(fin32, 2 * q) |
+                          ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(fin32, 2 * q + 1) << 32);
+      uint64_t x = CW[i];
+      if (x != INF64 && ((fw >> lane) & 1)) {  // final in an earlier window
+        x = INF64;
+        CW[i] = INF64;
+      }
+      const bool act = x != INF64 && ((uint32_t)(x >> 32) - hlo) < hspan;
+      const bool pend = x != INF64 && !act;
+      const uint64_t pm = __ballot(pend);
+      if (pend) LST[PULL_LMAX - 1 - (npend + (uint32_t)__popcll(pm & lanelt))] = (uint16_t)i;
+      npend += (uint32_t)__popcll(pm);
+      const uint64_t am = __ballot(act);
+      if (am) {  // wave-uniform
+        if (lane == 2 * q) fin32 |= (uint32_t)am;
+        if (lane == 2 * q + 1) fin32 |= (uint32_t)(am >> 32);
+        nfin = 1;
+        if constexpr (FP == 1) {
+          if (act) LST[cnt + (uint32_t)__popcll(am & lanelt)] = (uint16_t)i;
+          cnt += (uint32_t)__popcll(am);
+        } else {
+          constexpr uint64_t gmask = (FP == 64) ? ~0ull : ((1ull << FP) - 1);
+          const int gb = lane & ~(FP - 1);
+          const bool gact = ((am >> gb) & gmask) != 0;
+          const uint64_t lm = __ballot(gact && (lane & (FP - 1)) == 0);  // group leaders
+          if (gact && (lane & (FP - 1)) == 0) LST[cnt + (uint32_t)__popcll(lm & lanelt)] = (uint16_t)(i / FP);
+          cnt += (uint32_t)__popcll(lm);
+        }
+      }
+    }
+    wave_lds_sync();
+    PP_T(tC);
+    PP_ADD(3, tC - tR);
+    // 3b. the pending minima -> the lists of their windows c + r (r = 1..K-1),
+    //     appended after the entries already there
+    uint32_t ncnt[LP_KMAX], base[LP_KMAX];
+#pragma unroll
+    for (uint32_t k = 0; k < LP_KMAX; k++) {
+      ncnt[k] = 0;
+      base[k] = 0;
+    }
+    if (!pull && npend) err |= ERR_TIME;  // an EMIT pass's minima all lie in window c
+    if (pull && npend) {
+#pragma unroll
+      for (uint32_t k = 1; k < LP_KMAX; k++)
+        if (k < K) base[k] = (uint32_t)__builtin_amdgcn_readlane(sv, (cslot + k) % K);
+      const uint32_t lmax = a.lcap;
+      for (uint32_t j0 = 0; j0 < npend; j0 += 64) {
+        const bool jv = j0 + lane < npend;
+        const uint32_t li = jv ? LST[PULL_LMAX - 1 - (j0 + lane)] : 0u;
+        const uint64_t x = jv ? CW[li] : INF64;
+        const uint32_t r = jv ? lp_rof((uint32_t)(x >> 32), thr, K) : 0u;
+        if (jv && r >= K) err |= ERR_TIME;
+        uint32_t pos = 0, slot = 0;
+#pragma unroll
+        for (uint32_t k = 1; k < LP_KMAX; k++) {
+          if (k >= K) continue;
+          const uint64_t bm = __ballot(jv && r == k);
+          if (r == k) {
+            pos = base[k] + ncnt[k] + (uint32_t)__popcll(bm & lanelt);
+            slot = (cslot + k) % K;
+          }
+          ncnt[k] += (uint32_t)__popcll(bm);
+        }
+        if (jv && r > 0 && r < K) {
+          if (pos >= lmax) err |= ERR_LIST;
+          else {
+            const uint64_t toff = (x >> a.tshift) - (wlo + (uint64_t)r * a.delta);
+            a.blk[((size_t)slot * a.N + w) * a.ls + pos] = (toff << (a.tshift + a.lb)) | ((x & lowmask) << a.lb) | li;
+          }
+        }
+      }
+    }
+    np += npend + cnt;
+    PP_T(tP);
+    PP_ADD(4, tP - tC);
+    // 4. sparse: forward targets, uplink FIFO and one record per arrival (k_pull's step 4)
+    uint32_t ecnt = 0;
+    if (cnt) {
+      const uint32_t deg = (uint32_t)__popcll(__ballot(ej != EMPTY));  // rows are packed
+      const uint32_t serw = sup[sw];
+      constexpr uint32_t GPW = 64 / FP;
+      for (uint32_t g0 = 0; g0 < cnt; g0 += GPW) {
+        const uint32_t gi = g0 + (uint32_t)lane / FP;
+        const bool gv = gi < cnt;
+        const uint32_t grp = gv ? LST[gi] : 0;
+        const uint32_t i = grp * FP + (lane & (FP - 1));
+        const uint64_t x = gv ? CW[i] : INF64;  // final lanes were set to INF in step 3
+        const uint32_t pm = gv ? a.pub[grp] : EMPTY;
+        const bool act = gv && x != INF64 && ((uint32_t)(x >> 32) - hlo) < hspan && w != pm;
+        const uint32_t src = (uint32_t)(x & smask);
+        uint32_t js = J_NONE, jp = J_NONE;  // indices of src / publisher in mesh(w)
+        for (uint32_t k = 0; k < deg; k++) {  // wave-uniform: entry k from lane k
+          const uint32_t y = __builtin_amdgcn_readlane(ej, k) & 0xFFFFFFu;
+          js = y == src ? k : js;
+          jp = y == pm ? k : jp;
+        }
+        const uint32_t n = act ? deg - (js != J_NONE ? 1u : 0u) - ((jp != J_NONE && jp != js) ? 1u : 0u) : 0u;
+        const uint64_t start = uplink_start<FP>(a.busy, (size_t)w * a.B + grp, act, x, n, serw, a.tshift);
+        const uint32_t hp = (uint32_t)(x >> a.sb) & hmask;
+        if (act) {
+          fd++;
+          nr += n;
+          if (n && hp + 1 >= (1u << HOP_BITS)) err |= ERR_HOPS;
+          if (start - wlo >= (1ull << 32)) err |= ERR_TIME;
+        }
+        const uint64_t fm = __ballot(act);  // final log: 64 entries per store
+        if (act) {
+          const uint32_t p = logc + (uint32_t)__popcll(fm & lanelt);
+          a.keys[(size_t)w * LL + p] = x;
+          a.flane[(size_t)w * LL + p] = (uint16_t)i;
+        }
+        logc += (uint32_t)__popcll(fm);
+        const bool want = act && n != 0;
+        const uint64_t wm = __ballot(want);
+        if (want)
+          wrec[(size_t)w * LL + ecnt + (uint32_t)__popcll(wm & lanelt)] =
+              ((start - wlo) << 32) | ((uint64_t)hp << 26) | ((uint64_t)js << 21) | ((uint64_t)jp << 16) | i;
+        ecnt += (uint32_t)__popcll(wm);
+      }
+    }
+    PP_T(tD);
+    PP_ADD(5, tD - tP);
+    // 5. row state: final bits, pending list lengths, log length
+    if (nfin && lane < (int)LP_FW) a.fin[(size_t)w * LP_FW + lane] = fin32;
+    {
+      uint32_t add = 0;  // lane j < K: slot j stands for window c + lwin
+#pragma unroll
+      for (uint32_t k = 1; k < LP_KMAX; k++) add += (lwin == k) ? ncnt[k] : 0u;
+      uint32_t nv = sv;
+      if (lane < (int)K) nv = lane == (int)cslot ? 0u : sv + add;
+      if (lane == (int)LP_LOG) nv = logc;
+      if (lane <= (int)LP_LOG) a.st[(size_t)w * LP_SW + lane] = nv;
+      if (lane < (int)K && nv) nmh = umin32(nmh, lwhi);
+    }
+    if (lane == 0) wcnt[w] = ecnt;
+    nrec += ecnt;
+    // 6. LDS back to INF for the next row: the touched chunks
+#pragma unroll
+    for (int q = 0; q < (int)PULL_CH; q++)
+      if ((cb >> q) & 1u) CW[q * 64 + lane] = INF64;
+    wave_lds_sync();
+    ej = ej2; rj = rj2; cj = cj2; sv = sv2;
+    PP_T(tE);
+    PP_ADD(6, tE - tD);
+  }
+#ifdef GS_PULL_PROF
+  if (lane == 0 && a.pass < 32)
+    for (int k = 0; k < 8; k++) atomicAdd(&g_pull_prof[a.pass][k], (unsigned long long)pp[k]);
+#endif
+  for (int off = 32; off > 0; off >>= 1) nmh = umin32(nmh, __shfl_xor(nmh, off));
+  const uint64_t nmin = nmh == ~0u ? INF64 : (uint64_t)nmh << 32;
+  fd = wave_sum(fd);
+  nr = wave_sum(nr);
+  for (int off = 32; off > 0; off >>= 1) err |= __shfl_xor(err, off);
+  if (lane == 0) {
+    if (nrec) atomicAdd((unsigned long long*)&me[2], (unsigned long long)nrec);
+    if (nmin != INF64) atomicMin((unsigned long long*)&me[3], (unsigned long long)nmin);
+    if (fd) atomicAdd((unsigned long long*)&a.counters[C_FD], (unsigned long long)fd);
+    if (nr) atomicAdd((unsigned long long*)&a.counters[C_R_FWD], (unsigned long long)nr);
+    if (np) atomicAdd((unsigned long long*)&a.counters[C_PUSH], (unsigned long long)np);
+    if (err) atomicOr((unsigned*)&a.counters[C_ERR], err);
+  }
+}
+
+// Seeds -> lists: k_seed left the publishers' first sends in the dense keys
+// (+ chunkmin marks); every marked row appends them to the lists of their
+// windows d = 1..K (slot d % K). The publishers' own lanes (time 0) are left to
+// k_lpub. One wave per row.
+__global__ __launch_bounds__(TB) void k_lconv(LPullArgs a, const uint32_t* __restrict__ chunkmin) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t lanelt = (1ull << lane) - 1;
+  const uint32_t K = a.K, LL = a.L;
+  const uint64_t lowmask = (1ull << a.tshift) - 1;
+  uint32_t thr[LP_KMAX + 1];
+#pragma unroll
+  for (uint32_t k = 0; k <= LP_KMAX; k++) thr[k] = sat32((uint64_t)k * a.dG);
+  const uint32_t beyond = sat32((uint64_t)(K + 1) * a.dG);  // window K + 1 starts there
+  uint32_t err = 0;
+  for (uint32_t w = blockIdx.x * PULL_WAVES + (threadIdx.x >> 6); w < a.N; w += gridDim.x * PULL_WAVES) {
+    const uint32_t cm = lane < (int)PULL_CH ? chunkmin[(size_t)w * PULL_CH + lane] : ~0u;
+    const uint32_t live = (uint32_t)__ballot(cm != ~0u);
+    if (!live) continue;
+    uint32_t ncnt[LP_KMAX + 1];
+#pragma unroll
+    for (uint32_t k = 0; k <= LP_KMAX; k++) ncnt[k] = 0;
+#pragma unroll
+    for (int q = 0; q < (int)PULL_CH; q++) {
+      if (!((live >> q) & 1u)) continue;  // wave-uniform
+      const uint32_t i = q * 64 + lane;
+      const uint64_t v = i < LL ? a.keys[(size_t)w * LL + i] : INF64;
+      const bool seed = v != INF64 && (v >> a.tshift) != 0;
+      const uint32_t d = seed ? lp_rof((uint32_t)(v >> 32), thr, K) : 0u;  // the window index
+      if (seed && (d == 0 || (uint32_t)(v >> 32) >= beyond)) err |= ERR_TIME;
+#pragma unroll
+      for (uint32_t k = 1; k <= LP_KMAX; k++) {
+        if (k > K) continue;
+        const uint64_t bm = __ballot(seed && d == k);
+        if (seed && d == k) {
+          const uint64_t toff = (v >> a.tshift) - (uint64_t)k * a.delta;
+          a.blk[((size_t)(k % K) * a.N + w) * a.ls + ncnt[k] + (uint32_t)__popcll(bm & lanelt)] =
+              (toff << (a.tshift + a.lb)) | ((v & lowmask) << a.lb) | i;
+        }
+        ncnt[k] += (uint32_t)__popcll(bm);
+      }
+    }
+    if (lane < (int)K) {  // list lengths: window d sits in slot d % K
+      uint32_t nv = 0;
+#pragma unroll
+      for (uint32_t k = 1; k <= LP_KMAX; k++) nv += (k <= K && k % K == (uint32_t)lane) ? ncnt[k] : 0u;
+      a.st[(size_t)w * LP_SW + lane] = nv;
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) err |= __shfl_xor(err, off);
+  if (lane == 0 && err) atomicOr((unsigned*)&a.counters[C_ERR], err);
+}
+
+// The publishers' own lanes: final at time 0 (k_seed's key p), logged first.
+__global__ void k_lpub(LPullArgs a, uint32_t Fe) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t FP = a.L / a.B;
+  if (g >= a.B * Fe) return;
+  const uint32_t m = g / Fe, f = g % Fe, p = a.pub[m], i = m * FP + f;
+  atomicOr(&a.fin[(size_t)p * LP_FW + (i >> 5)], 1u << (i & 31));
+  const uint32_t pos = atomicAdd(&a.st[(size_t)p * LP_SW + LP_LOG], 1u);
+  a.keys[(size_t)p * a.L + pos] = (uint64_t)p;
+  a.flane[(size_t)p * a.L + pos] = (uint16_t)i;
+}
+
+// Final logs -> dense [N][L] key rows (INF where nothing arrived), in place:
+// one wave per row reads its whole log into LDS before writing the row.
+__global__ __launch_bounds__(TB) void k_lfinal(LPullArgs a) {
+  __shared__ uint64_t row[PULL_WAVES][PULL_LMAX];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint64_t* R = row[wv];
+  const uint32_t LL = a.L;
+  for (uint32_t w = blockIdx.x * PULL_WAVES + wv; w < a.N; w += gridDim.x * PULL_WAVES) {
+    for (uint32_t i = lane; i < LL; i += 64) R[i] = INF64;
+    wave_lds_sync();
+    const uint32_t n = a.st[(size_t)w * LP_SW + LP_LOG];
+    for (uint32_t i0 = 0; i0 < n; i0 += 256) {
+      uint64_t k4[4];
+      uint32_t l4[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const uint32_t i = i0 + u * 64 + lane;
+        k4[u] = i < n ? a.keys[(size_t)w * LL + i] : INF64;
+        l4[u] = i < n ? a.flane[(size_t)w * LL + i] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++)
+        if (k4[u] != INF64) R[l4[u]] = k4[u];
+    }
+    wave_lds_sync();
+    for (uint32_t i = lane; i < LL; i += 64) a.keys[(size_t)w * LL + i] = R[i];
+    wave_lds_sync();
+  }
+}
+
+// Completion from the final logs (FP == 1, results kept on the device): the
+// counters and per-message reductions of k_complete<1, false> without dense
+// rows. One wave per row scatters the row's log into LDS; lane j keeps the
+// reductions of messages j, j + 64, ... in registers over all its rows (a
+// log entry is a delivery unless the row is the message's publisher); one
+// flush per block through LDS.
+constexpr uint32_t LC_WAVES = 16;
+__global__ __launch_bounds__(LC_WAVES * 64) void k_lcomplete(LPullArgs a, uint64_t* mstat) {
+  __shared__ uint64_t R[LC_WAVES][PULL_LMAX];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t B = a.B, stride = gridDim.x * LC_WAVES;
+  uint64_t tm[PULL_CH];
+  uint32_t ud[PULL_CH], pm[PULL_CH];
+#pragma unroll
+  for (int j = 0; j < (int)PULL_CH; j++) {
+    const uint32_t m = j * 64 + lane;
+    tm[j] = 0;
+    ud[j] = 0;
+    pm[j] = m < B ? a.pub[m] : EMPTY;
+  }
+  uint64_t deliv = 0, lsum = 0, lmax = 0;
+  uint64_t* Rw = R[wv];
+  for (uint32_t w = blockIdx.x * LC_WAVES + wv; w < a.N; w += stride) {
+#pragma unroll
+    for (int j = 0; j < (int)PULL_CH; j++) Rw[j * 64 + lane] = INF64;
+    wave_lds_sync();
+    const uint32_t n = a.st[(size_t)w * LP_SW + LP_LOG];
+    for (uint32_t i0 = 0; i0 < n; i0 += 256) {
+      uint64_t k4[4];
+      uint32_t l4[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const uint32_t i = i0 + u * 64 + lane;
+        k4[u] = i < n ? a.keys[(size_t)w * a.L + i] : INF64;
+        l4[u] = i < n ? a.flane[(size_t)w * a.L + i] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++)
+        if (k4[u] != INF64) Rw[l4[u]] = k4[u];
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int j = 0; j < (int)PULL_CH; j++) {
+      const uint32_t m = j * 64 + lane;
+      if (m >= B || pm[j] == w) continue;  // the publisher's own key is no delivery
+      const uint64_t x = Rw[m];
+      if (x == INF64) { ud[j]++; continue; }
+      const uint64_t trel = x >> a.tshift, ms = trel / 1000000ull;
+      deliv++;
+      lsum += ms;
+      lmax = ms > lmax ? ms : lmax;
+      tm[j] = trel > tm[j] ? trel : tm[j];
+    }
+    wave_lds_sync();
+  }
+  deliv = wave_sum(deliv);
+  lsum = wave_sum(lsum);
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint64_t x = __shfl_xor(lmax, off);
+    lmax = x > lmax ? x : lmax;
+  }
+  if (lane == 0 && deliv) {
+    atomicAdd((unsigned long long*)&a.counters[C_DELIV], (unsigned long long)deliv);
+    atomicAdd((unsigned long long*)&a.counters[C_LAT_SUM], (unsigned long long)lsum);
+    atomicMax((unsigned long long*)&a.counters[C_LAT_MAX], (unsigned long long)lmax);
+  }
+  if (!mstat) return;  // block-uniform
+  // per-message flush: the waves' values through LDS, one atomic per message and block
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < (int)PULL_CH; j++) R[wv][j * 64 + lane] = tm[j];
+  __syncthreads();
+  for (uint32_t m = threadIdx.x; m < B; m += LC_WAVES * 64) {
+    uint64_t t = 0;
+    for (uint32_t q = 0; q < LC_WAVES; q++) t = R[q][m] > t ? R[q][m] : t;
+    if (t) atomicMax((unsigned long long*)&mstat[(size_t)m * MS_COLS + MS_TMAX], (unsigned long long)t);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < (int)PULL_CH; j++) R[wv][j * 64 + lane] = ud[j];
+  __syncthreads();
+  for (uint32_t m = threadIdx.x; m < B; m += LC_WAVES * 64) {
+    uint64_t u = 0;
+    for (uint32_t q = 0; q < LC_WAVES; q++) u += R[q][m];
+    if (u) atomicAdd((unsigned long long*)&mstat[(size_t)m * MS_COLS + MS_UNDEL], (unsigned long long)u);
+  }
+}
+
+void lpull_dispatch(uint32_t FP, const LPullArgs& a, unsigned grid, hipStream_t s) {
+  switch (FP) {
+    case 1: k_lpull<1><<<grid, TB, 0, s>>>(a); break;
+    case 2: k_lpull<2><<<grid, TB, 0, s>>>(a); break;
+    case 4: k_lpull<4><<<grid, TB, 0, s>>>(a); break;
+    case 8: k_lpull<8><<<grid, TB, 0, s>>>(a); break;
+    default: k_lpull<16><<<grid, TB, 0, s>>>(a); break;
+  }
+}

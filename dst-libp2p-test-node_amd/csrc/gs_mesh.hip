@@ -932,6 +932,7 @@ uint32_t run_mesh(Ctx& c, uint32_t max_hb) {
   }
   c.d_mesh.alloc((size_t)N * MESH_W);
   c.rpos_valid = false;
+  c.mesh_dmax = 0;
   c.d_mcnt.alloc(N);
   k_extract<<<blocks(N), TB, 0, s>>>(a, c.d_mesh.p, c.d_mcnt.p);
   GS_HIP(hipGetLastError());

@@ -378,6 +378,7 @@ uint64_t part_begin(Ctx& c, const gs_publish* sched, uint64_t n_msgs) {
   c.part_b = setup_batch(c, sched, 0, n_msgs);
   const Batch& b = c.part_b;
   const uint64_t total = (uint64_t)un * b.L;
+  c.keys_log = false;  // dense rows from here on (gs_relax.hip list pull path leaves logs)
   GS_HIP(hipMemsetAsync(c.d_keys.p, 0xFF, total * 8, s));
   if (FP > 1) GS_HIP(hipMemsetAsync(c.d_busy.p, 0, (size_t)un * b.B * 8, s));
   GS_HIP(hipMemsetAsync(c.d_fbits.p, 0, (total + 63) / 64 * 8, s));

@@ -322,6 +322,8 @@ __global__ __launch_bounds__(TB) void k_transpose(const uint64_t* __restrict__ t
   }
 }
 
+#include "gs_lpull_kernel.h"
+
 uint32_t pow2_at_least(uint32_t x) { uint32_t p = 1; while (p < x) p <<= 1; return p; }
 
 }  // namespace
@@ -376,6 +378,15 @@ static Batch setup_batch(Ctx& c, const gs_publish* sched, uint64_t i0, uint64_t 
     if (c.stage_used[x]) min_ser = std::min(min_ser, up);
   }
   b.delta = std::max<uint64_t>(1, min_lat + min_ser);
+  for (uint32_t x = 0; x < S; x++) {
+    if (!c.stage_used[x]) continue;
+    b.ser_max = std::max<uint64_t>(b.ser_max, tab[(size_t)S * S + x]);
+    for (uint32_t y = 0; y < S; y++) {
+      if (!c.stage_used[y]) continue;
+      const uint64_t up = tab[(size_t)S * S + x], dn = tab[(size_t)S * S + S + y];
+      b.lat_adj_max = std::max<uint64_t>(b.lat_adj_max, tab[(size_t)x * S + y] + (dn > up ? dn - up : 0));
+    }
+  }
   b.lat_min = min_lat;
   b.tpub.resize(b.B);
   for (uint32_t q = 0; q < b.B; q++) { pub[q] = sched[i0 + q].publisher; b.tpub[q] = sched[i0 + q].t_pub_ns; }
@@ -428,6 +439,21 @@ static void launch_seed(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, uint64
 static void run_complete(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, bool mstat, bool hist,
                          bool store = true) {
   hipStream_t s = c.stream;
+  if (c.keys_log) {  // list pull path, results on the device: reduce the final logs
+    if (hist || store || u0 || un != c.cfg.peers || b.FP != 1) c.fail(GS_EINVAL, "internal: final logs need k_lfinal");
+    LPullArgs la{};
+    la.keys = c.d_keys.p; la.flane = c.d_flane.p; la.st = c.d_lst.p; la.pub = c.d_pub.p;
+    la.counters = c.d_counters.p; la.N = un; la.B = b.B; la.L = b.L; la.tshift = b.tshift;
+    if (mstat) {
+      c.d_mstat.alloc((size_t)c.cfg.batch * MS_COLS);
+      GS_HIP(hipMemsetAsync(c.d_mstat.p, 0, (size_t)b.B * MS_COLS * 8, s));
+    }
+    const unsigned grid = (unsigned)std::max<uint64_t>(
+        1, std::min<uint64_t>(((uint64_t)un + LC_WAVES - 1) / LC_WAVES, (uint64_t)std::max(1, c.num_cus)));
+    k_lcomplete<<<grid, LC_WAVES * 64, 0, s>>>(la, mstat ? c.d_mstat.p : nullptr);
+    GS_HIP(hipGetLastError());
+    return;
+  }
   CompArgs ca{};
   ca.keys = c.d_keys.p; ca.pub = c.d_pub.p; ca.tpub = c.d_tpub.p; ca.tc = store ? c.d_tc.p : nullptr;
   ca.hops = c.d_hops.p; ca.counters = c.d_counters.p; ca.N = un; ca.B = b.B; ca.F = b.F;
@@ -754,6 +780,144 @@ static void run_pull_batch(Ctx& c, const Batch& b, EvFn& ev, size_t& n_ev, int d
   c.stats.relax_launches += pass;
 }
 
+// Ring size K of the list pull path (gs_lpull_kernel.h) for this batch, or 0
+// when it cannot take the batch (then k_pull runs). A candidate made from a
+// record of window b arrives before b*D + D (start inside the window) + the
+// fragment FIFO + the largest link latency + MESH_W serialisations, so its
+// destination is at most K - 1 windows after the emitted one; the entry
+// packs (t - window start) | hops | src | lane into 64 bits; the ring must fit
+// the device memory left.
+// Entries per candidate list: at least 256, so that rows of few lanes (small
+// batches) still hold several passes' appends of the same lanes.
+static uint32_t lpull_stride(const Batch& b) { return std::max<uint32_t>(b.L, 256); }
+
+static uint32_t lpull_ring(Ctx& c, const Batch& b, uint64_t delta, uint32_t* lb) {
+  if (!c.mesh_dmax) {  // widest mesh row, once per mesh
+    std::vector<uint32_t> m((size_t)c.cfg.peers * MESH_W);
+    GS_HIP(hipMemcpyAsync(m.data(), c.d_mesh.p, m.size() * 4, hipMemcpyDeviceToHost, c.stream));
+    GS_HIP(hipStreamSynchronize(c.stream));
+    uint32_t dmax = 1;
+    for (size_t u = 0; u < c.cfg.peers; u++) {
+      uint32_t d = 0;
+      while (d < MESH_W && m[u * MESH_W + d] != EMPTY) d++;
+      dmax = std::max(dmax, d);
+    }
+    c.mesh_dmax = dmax;
+  }
+  if (b.tshift >= 32 || b.L > PULL_LMAX || delta < 2) return 0;
+  // a fragment waits behind at most the other FP - 1 fragments' sends to the
+  // row's mesh peers (c.mesh_dmax, the widest mesh row)
+  const uint64_t dm = c.mesh_dmax ? c.mesh_dmax : MESH_W;
+  const uint64_t fifo = (uint64_t)(b.FP - 1) * dm * b.ser_max;
+  const uint64_t span = delta + fifo + b.lat_adj_max + dm * b.ser_max;
+  // k_seed's first sends (every fragment to every mesh peer, or to every
+  // connection with flood publish) land in windows 1 .. K of source window 0
+  const uint64_t sdeg = c.cfg.flood_publish ? std::max<uint64_t>(c.max_degree, 1) : dm;
+  const uint64_t seed_span = (uint64_t)b.FP * sdeg * b.ser_max + b.lat_adj_max;
+  const uint64_t K = std::max(span / delta + 2, seed_span / delta + 1);
+  if (K > LP_KMAX) return 0;
+  uint32_t tb = 0;
+  while ((1ull << tb) < delta) tb++;
+  *lb = bits_for(b.L);
+  if (tb + b.tshift + *lb > 64) return 0;
+  const uint32_t N = c.cfg.peers;
+  const uint64_t need = (uint64_t)K * N * lpull_stride(b) * 8 + (uint64_t)N * b.L * 2 + (uint64_t)N * (LP_SW + LP_FW) * 4;
+  const uint64_t have = (uint64_t)c.d_lblk.n * 8 + (uint64_t)c.d_flane.n * 2 + (uint64_t)(c.d_lst.n + c.d_lfin.n) * 4;
+  if (need > have) {
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess || need - have + (4ull << 30) > fr) return 0;
+  }
+  return (uint32_t)K;
+}
+
+// One batch on the list pull path: k_seed into the dense keys, seeds -> block
+// 0 (k_lconv), publishers' own lanes (k_lpub), then passes in chunks of 8 as
+// on the k_pull path, and the final logs back to dense rows (k_lfinal).
+// Returns false (counters restored) when a list overflowed: the caller re-runs
+// the batch on k_pull.
+template <class EvFn>
+static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvFn& ev, size_t& n_ev, int dev_cus,
+                            bool dense) {
+  const uint32_t N = c.cfg.peers, L = b.L;
+  hipStream_t s = c.stream;
+  const size_t NL = (size_t)N * L;
+  c.d_chunkmin.alloc((size_t)N * PULL_CH);
+  c.d_lrec.alloc(2 * NL);
+  c.d_lcnt.alloc(2 * (size_t)N);
+  c.d_pctrl.alloc(12);
+  const uint32_t ls = lpull_stride(b);
+  c.d_lblk.alloc((size_t)K * N * ls);
+  c.d_lst.alloc((size_t)N * LP_SW);
+  c.d_lfin.alloc((size_t)N * LP_FW);
+  c.d_flane.alloc(NL);
+  if (!c.rpos_valid) {
+    c.d_rpos.alloc((size_t)N * MESH_W);
+    GS_HIP(hipMemsetAsync(c.d_counters.p + C_ERR, 0, 8, s));
+    k_rpos<<<(unsigned)(((uint64_t)N * MESH_W + TB - 1) / TB), TB, 0, s>>>(c.d_mesh.p, c.d_rpos.p, N, c.d_counters.p);
+    GS_HIP(hipGetLastError());
+    if (read_counter(c, C_ERR) & ERR_MESH) c.fail(GS_ERANGE, "mesh is not symmetric");
+    c.rpos_valid = true;
+  }
+  GS_HIP(hipMemsetAsync(c.d_chunkmin.p, 0xFF, (size_t)N * PULL_CH * 4, s));
+  GS_HIP(hipMemsetAsync(c.d_lst.p, 0, (size_t)N * LP_SW * 4, s));
+  GS_HIP(hipMemsetAsync(c.d_lfin.p, 0, (size_t)N * LP_FW * 4, s));
+  GS_HIP(hipMemsetAsync(c.d_pctrl.p, 0, 12 * 8, s));  // every slot {lo 0, DONE, 0 records, min INF}
+  for (int q = 0; q < 3; q++) GS_HIP(hipMemsetAsync(c.d_pctrl.p + q * 4 + 3, 0xFF, 8, s));
+  c.d_lp_save.alloc(C_COUNT);
+  GS_HIP(hipMemcpyAsync(c.d_lp_save.p, c.d_counters.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));
+  launch_seed(c, b, 0, N, c.d_pctrl.p + 2 * 4 + 3, c.d_chunkmin.p);
+  LPullArgs la{};
+  la.keys = c.d_keys.p; la.flane = c.d_flane.p; la.busy = c.d_busy.p; la.blk = c.d_lblk.p;
+  la.st = c.d_lst.p; la.fin = c.d_lfin.p;
+  la.lrec = c.d_lrec.p; la.lcnt = c.d_lcnt.p; la.rpos = c.d_rpos.p;
+  la.mesh = c.d_mesh.p; la.pub = c.d_pub.p; la.stage = c.d_stage.p; la.tables = c.d_tables.p;
+  const uint64_t grain = pull_grain(b.tshift);
+  la.ctrl = c.d_pctrl.p; la.counters = c.d_counters.p; la.delta = b.delta / grain * grain;
+  la.tmax = b.tmax - grain;
+  la.N = N; la.B = b.B; la.L = L; la.S = c.S; la.sb = b.sb; la.tshift = b.tshift;
+  la.K = K; la.lb = lb; la.dG = (uint32_t)(la.delta / grain);
+  const char* cap = getenv("GS_LPULL_CAP");  // test knob: small lists force the overflow re-run
+  la.ls = ls;
+  la.lcap = cap && *cap ? (uint32_t)std::min<long>(std::max(1, atoi(cap)), (long)ls) : ls;
+  // 40 KB of LDS per block: 4 blocks (16 waves, 16 rows in flight) per CU
+  const unsigned grid = (unsigned)std::max<uint64_t>(
+      1, std::min<uint64_t>(((uint64_t)N + PULL_WAVES - 1) / PULL_WAVES, (uint64_t)dev_cus * 4));
+  k_lconv<<<grid, TB, 0, s>>>(la, c.d_chunkmin.p);
+  k_lpub<<<(b.B * b.Fe + 255) / 256, 256, 0, s>>>(la, b.Fe);
+  GS_HIP(hipGetLastError());
+  uint32_t pass = 0;
+  for (;;) {
+    for (uint32_t q = 0; q < 8; q++) {
+      la.pass = pass++;
+      if (c.timing) {  // (start, mid, end): the whole pass is frontier time
+        GS_HIP(hipEventRecord(ev(n_ev), s));
+        GS_HIP(hipEventRecord(ev(n_ev + 1), s));
+        lpull_dispatch(b.FP, la, grid, s);
+        GS_HIP(hipEventRecord(ev(n_ev + 2), s));
+        n_ev += 3;
+      } else {
+        lpull_dispatch(b.FP, la, grid, s);
+      }
+    }
+    GS_HIP(hipGetLastError());
+    GS_HIP(hipMemcpyAsync(c.h_pinned, c.d_pctrl.p, 12 * 8, hipMemcpyDeviceToHost, s));
+    GS_HIP(hipStreamSynchronize(s));
+    if (c.h_pinned[((pass - 1) % 3) * 4 + 1] == PM_DONE) break;
+  }
+  c.stats.relax_launches += pass;
+  if (read_counter(c, C_ERR) & ERR_LIST) {
+    GS_HIP(hipMemcpyAsync(c.d_counters.p, c.d_lp_save.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));
+    return false;
+  }
+  if (dense) {  // a sink, the traffic pass or a fragment group needs [N][L] rows
+    k_lfinal<<<grid, TB, 0, s>>>(la);
+    GS_HIP(hipGetLastError());
+  } else {
+    c.keys_log = true;
+  }
+  return true;
+}
+
 #ifdef GS_PULL_PROF
 extern "C" int gs_debug_pull_prof(uint64_t* out) {  // 32 passes x 8 slots; read and clear
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pull_prof), sizeof(g_pull_prof)) != hipSuccess) return -1;
@@ -796,8 +960,9 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
   for (uint64_t i = 0; i < n_msgs; i++) Fmax = std::max(Fmax, frags_of(c, sched[i]));
   const uint32_t FPmax = pow2_at_least(Fmax);
   const char* var_env = getenv("GS_RELAX_VARIANT");
-  // default: owner-computes pull (32); without it the push path: split (8) + final bitset (4) + read filter (1)
-  uint32_t variant = var_env && *var_env ? (uint32_t)atoi(var_env) : 45u;
+  // default: owner-computes pull over candidate lists (64 | 32; k_pull's dense rows without 64);
+  // without 32 the push path: split (8) + final bitset (4) + read filter (1)
+  uint32_t variant = var_env && *var_env ? (uint32_t)atoi(var_env) : 109u;
   const bool lanes32 = (uint64_t)N * Bmax * FPmax < (1ull << 32);  // frontier indices are u32
   if (!lanes32) variant &= ~8u;
   const bool gossip = c.cfg.lazy_gossip != 0;
@@ -916,6 +1081,7 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     }
     const uint64_t total = (uint64_t)N * L;
     auto reset = [&](uint32_t v, bool with_gossip) {  // fresh keys and bucket state for this batch
+      c.keys_log = false;
       GS_HIP(hipMemsetAsync(c.d_keys.p, 0xFF, total * 8, s));
       if (FP > 1) GS_HIP(hipMemsetAsync(c.d_busy.p, 0, (size_t)N * B * 8, s));
       if (v & 32) return;
@@ -1022,7 +1188,19 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       if (gossip) GS_HIP(hipMemcpyAsync(c.d_cnt_save.p, c.d_counters.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));
       if (pull_ok) {
         reset(variant, false);
-        run_pull_batch(c, b, ev, n_ev, dev_cus);
+        const uint64_t grain = pull_grain(b.tshift);
+        uint32_t lb = 0;
+        const uint32_t K = (variant & 64) ? lpull_ring(c, b, b.delta / grain * grain, &lb) : 0u;
+        if ((variant & 64) && !K && getenv("GS_REQUIRE_LPULL"))  // test knob: no silent k_pull fallback
+          c.fail(GS_EUNSUPPORTED, "list pull path cannot take this batch (GS_REQUIRE_LPULL)");
+        const bool dense = sink != nullptr || c.traffic || b.FP > 1;
+        if (!K || !run_lpull_batch(c, b, K, lb, ev, n_ev, dev_cus, dense)) {
+          if (K) {  // a candidate list overflowed: this batch runs on k_pull
+            if (getenv("GS_REQUIRE_LPULL")) c.fail(GS_EUNSUPPORTED, "list pull overflow (GS_REQUIRE_LPULL)");
+            reset(variant, false);
+          }
+          run_pull_batch(c, b, ev, n_ev, dev_cus);
+        }
       } else {
         push_run(variant & ~32u, false);
       }

@@ -333,15 +333,43 @@ def test_large_graph_properties_and_sampled_parity():
         np.testing.assert_array_equal(res["hops"][m], hp[0])
 
 
-@pytest.mark.parametrize("variant", list(range(8)) + [8, 9, 10, 11, 13, 15, 45])
+@pytest.mark.parametrize("variant", list(range(8)) + [8, 9, 10, 11, 13, 15, 45, 109])
 def test_relax_kernel_variants_exact(variant, monkeypatch):
     """Every bucket implementation (fused with read-filter / tile-skip / final-bitset,
-    split scan+frontier, owner-computes pull = 45, the default) is bit-exact."""
+    split scan+frontier, owner-computes pull over dense rows = 45, over candidate
+    lists = 109, the default) is bit-exact."""
     monkeypatch.setenv("GS_RELAX_VARIANT", str(variant))
-    p = oracle.params(peers=2000, seed=31, fragments=2)
+    if variant & 64:
+        monkeypatch.setenv("GS_REQUIRE_LPULL", "1")
+    # lazy gossip off: a wrong eager result must not hide behind the push-path
+    # fallback that a failed gossip no-op proof takes
+    p = oracle.params(peers=2000, seed=31, fragments=2, lazy_gossip=0)
     compare(p, 5, (50, 150, 40, 130), _sched(40, 2000), batch=16)
-    p = oracle.params(peers=3000, seed=32)
+    p = oracle.params(peers=3000, seed=32, lazy_gossip=0)
     compare(p, 3, (20, 200, 10, 90), _sched(70, 3000), batch=64)
+
+
+@pytest.mark.parametrize("variant,frags", [(45, 1), (109, 1), (109, 2), (109, 4)])
+def test_pull_wide_rows_exact(variant, frags, monkeypatch):
+    """Rows of 1024 lanes (16 chunks of 64, the bench layout) on both pull
+    kernels: every chunk of a row is live in the peak windows, candidate lists
+    span several destination windows, more than 64 lanes per row pend at once."""
+    monkeypatch.setenv("GS_RELAX_VARIANT", str(variant))
+    if variant & 64:
+        monkeypatch.setenv("GS_REQUIRE_LPULL", "1")
+    B = 1024 // frags
+    p = oracle.params(peers=2500, seed=33, fragments=frags, lazy_gossip=0)
+    sim, _ = compare(p, 5, (50, 150, 40, 130), _sched(B, 2500), batch=B)
+    assert sim.stats()["gossip_fallback_batches"] == 0
+
+
+def test_pull_list_overflow_reruns_on_dense_rows(monkeypatch):
+    """Candidate lists capped at 2 entries (GS_LPULL_CAP): the list pull path
+    overflows, restores the counters and re-runs the batch on k_pull; the
+    result is still bit-exact."""
+    monkeypatch.setenv("GS_LPULL_CAP", "2")
+    p = oracle.params(peers=2500, seed=34, lazy_gossip=0)
+    compare(p, 5, (50, 150, 40, 130), _sched(256, 2500), batch=256)
 
 
 @pytest.mark.parametrize("frags,gossip,fast,idw", [(1, 0, 0, 0), (2, 0, 0, 0), (1, 1, 0, 0), (1, 0, 1, 0),
