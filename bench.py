@@ -294,7 +294,8 @@ def config_rates(args, local):
         out[name] = {"value": st["deliveries"] / dt, "unit": "deliveries/s", "msgs": c["msgs"],
                      "ms": dt * 1e3, "deliveries": int(st["deliveries"]), "batches": int(st["batches"]),
                      "gossip_iwant": int(st["gossip_iwant"]), "gossip_noop_msgs": int(st["gossip_noop_msgs"]),
-                     "kernel_path": "push (k_scan+k_frontier+k_gossip)" if push else "pull (k_pull)"}
+                     "kernel_path": "push (k_scan+k_frontier+k_gossip)" if push else
+                     "pull (k_lpull)" if st["list_pull_batches"] else "pull (k_pull)"}
         sim.close()
     return out
 
@@ -315,18 +316,21 @@ def main():
         extra = {"peers": args.also_peers, "value": tot2[0] / e2, "ms_per_step": e2 * 1e3 / args.steps}
         sim2.close()
 
-    # one launch = one Delta-window pass: k_pull (default owner-computes path, its whole
-    # time is reported as frontier time) or k_scan + k_frontier (push path)
+    # one launch = one Delta-window pass: k_lpull / k_pull (owner-computes paths, their
+    # whole time is reported as frontier time) or k_scan + k_frontier (push path)
     launches = max(1, st["relax_launches"])
     pull = st["scan_ms"] <= 0.01 * max(st["relax_ms"], 1e-9)
-    kernel = ("k_pull<%d>" % fp_lanes(args.fragments)) if pull else \
+    lpull = pull and st.get("list_pull_batches", 0) > 0
+    kernel = ("k_lpull<%d>" % fp_lanes(args.fragments)) if lpull else \
+        ("k_pull<%d>" % fp_lanes(args.fragments)) if pull else \
         "k_scan<%d,false,false> + k_frontier<%d,true,false>" % ((fp_lanes(args.fragments),) * 2)
     achieved = st["relax_bytes_alg"] / (st["relax_ms"] / 1e3) / 1e9 if st["relax_ms"] > 0 else None
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            same_kernel = all(k.startswith("k_pull<") == pull for k in tj.get("kernels", []))
+            kprefix = kernel.split("<")[0] + "<"
+            same_kernel = bool(tj.get("kernels")) and all(k.startswith(kprefix) for k in tj["kernels"])
             if tj.get("peers") == args.peers and tj.get("batch") == args.batch and same_kernel:
                 traffic = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):

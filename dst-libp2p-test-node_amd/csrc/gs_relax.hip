@@ -909,6 +909,7 @@ static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvF
     GS_HIP(hipMemcpyAsync(c.d_counters.p, c.d_lp_save.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));
     return false;
   }
+  c.stats.list_pull_batches++;
   if (dense) {  // a sink, the traffic pass or a fragment group needs [N][L] rows
     k_lfinal<<<grid, TB, 0, s>>>(la);
     GS_HIP(hipGetLastError());
@@ -1193,7 +1194,9 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
         const uint32_t K = (variant & 64) ? lpull_ring(c, b, b.delta / grain * grain, &lb) : 0u;
         if ((variant & 64) && !K && getenv("GS_REQUIRE_LPULL"))  // test knob: no silent k_pull fallback
           c.fail(GS_EUNSUPPORTED, "list pull path cannot take this batch (GS_REQUIRE_LPULL)");
-        const bool dense = sink != nullptr || c.traffic || b.FP > 1;
+        // GS_LPULL_DENSE (diagnostic): dense rows + k_complete, whose known key
+        // stream calibrates the PMC read factor (scripts/pmc_summary.py)
+        const bool dense = sink != nullptr || c.traffic || b.FP > 1 || getenv("GS_LPULL_DENSE");
         if (!K || !run_lpull_batch(c, b, K, lb, ev, n_ev, dev_cus, dense)) {
           if (K) {  // a candidate list overflowed: this batch runs on k_pull
             if (getenv("GS_REQUIRE_LPULL")) c.fail(GS_EUNSUPPORTED, "list pull overflow (GS_REQUIRE_LPULL)");

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 5u
+#define GS_ABI_VERSION 6u
 
 /* Sentinel for "never delivered" in t_complete_ns. */
 #define GS_UNDELIVERED UINT64_MAX
@@ -183,6 +183,8 @@ typedef struct gs_stats {
     uint64_t gossip_fallback_batches; /* batches re-run on the push path with gossip    */
     uint64_t batches;           /* device batches run (gs_run splits at cfg.batch, size /  */
                                 /* chunk changes and the churn snapshot ring)             */
+    uint64_t list_pull_batches; /* batches whose eager passes ran on candidate lists      */
+                                /* (k_lpull) rather than dense rows       */
 } gs_stats;
 
 /* ---- host-only helpers (no device work) ---------------------------------- */

@@ -19,7 +19,7 @@ step() {  # name seconds cmd...
   return 0
 }
 PROFARGS="--steps ${PROF_STEPS:-6} --warmup 2 --cpu-seconds 0 --also-peers 0 --configs 0"
-KRE="k_pull|k_scan|k_frontier|k_complete"
+KRE="k_lpull|k_pull|k_scan|k_frontier|k_complete|k_lcomplete"
 for s in ${STEPS:-tests smoke bench prof}; do
   case $s in
     tests) step gpu_tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;

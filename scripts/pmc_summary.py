@@ -10,8 +10,9 @@ known exactly: k_complete streams every key once per batch (8 B x peers x
 batch x FP, 8-byte lanes, the same access width as the pull pass's row reads),
 or, on the push path, k_scan per non-empty bucket. The same factor is applied
 to every kernel's FETCH_SIZE ("corrected"); WRITE_SIZE is taken as is. The
-traffic json carries the relaxation kernel's bytes per launch (k_pull, or
-k_scan + k_frontier) for bench.py's roofline.traffic.
+traffic json carries the relaxation kernel's bytes per launch (k_lpull,
+k_pull, or k_scan + k_frontier) for bench.py's roofline.traffic. With the
+list pull path, profile under GS_LPULL_DENSE=1 so that k_complete runs.
 """
 import argparse
 import csv
@@ -71,7 +72,8 @@ def main():
                              "hbm_bytes_per_launch_corrected": fm * factor + wm}
     json.dump(out, open(a.out, "w"), indent=1)
     if a.traffic_json:
-        rel = [k for k in out["kernels"] if k.startswith("k_pull<")] or \
+        rel = [k for k in out["kernels"] if k.startswith("k_lpull<")] or \
+            [k for k in out["kernels"] if k.startswith("k_pull<")] or \
             [k for k in out["kernels"] if k.startswith("k_scan<") or k.startswith("k_frontier<")]
         launches = max(out["kernels"][k]["launches"] for k in rel)
         per_launch = sum(out["kernels"][k]["hbm_bytes_per_launch_corrected"] for k in rel)
