@@ -149,6 +149,9 @@ struct Ctx {
   // list pull path (gs_lpull_kernel.h)
   DevBuf<uint64_t> d_lblk;   // [K][N][L] candidate lists per destination-window slot
   DevBuf<uint32_t> d_lst;    // [N][16] list lengths per destination window, final-log length
+  DevBuf<uint64_t> d_skey;   // list pull path: the publishes' first sends (k_seed -> k_lseed)
+  DevBuf<uint32_t> d_slane;  // (row << 11) | lane
+  DevBuf<uint32_t> d_scnt;
   DevBuf<uint64_t> d_lp_save;  // [C_COUNT] counters before a list pull batch (overflow re-run)
   DevBuf<uint32_t> d_lfin;   // [N][32] final bits
   DevBuf<uint16_t> d_flane;  // [N][L] lanes of the final log

@@ -426,56 +426,26 @@ __global__ __launch_bounds__(TB, 4) void k_lpull(LPullArgs a) {
   }
 }
 
-// Seeds -> lists: k_seed left the publishers' first sends in the dense keys
-// (+ chunkmin marks); every marked row appends them to the lists of their
-// windows d = 1..K (slot d % K). The publishers' own lanes (time 0) are left to
-// k_lpub. One wave per row.
-__global__ __launch_bounds__(TB) void k_lconv(LPullArgs a, const uint32_t* __restrict__ chunkmin) {
-  const int lane = threadIdx.x & 63;
-  const uint64_t lanelt = (1ull << lane) - 1;
-  const uint32_t K = a.K, LL = a.L;
+// Seeds -> lists: k_seed appended the publishers' first sends (key, row << 11
+// | lane) to a seed list; each goes to the list of its window d = 1..K (slot
+// d % K) at a position taken from the row's list length. One thread per seed.
+__global__ __launch_bounds__(TB) void k_lseed(LPullArgs a, const uint64_t* __restrict__ skey,
+                                              const uint32_t* __restrict__ slane, const uint32_t* __restrict__ scnt) {
+  const uint32_t n = *scnt, K = a.K;
   const uint64_t lowmask = (1ull << a.tshift) - 1;
-  uint32_t thr[LP_KMAX + 1];
-#pragma unroll
-  for (uint32_t k = 0; k <= LP_KMAX; k++) thr[k] = sat32((uint64_t)k * a.dG);
-  const uint32_t beyond = sat32((uint64_t)(K + 1) * a.dG);  // window K + 1 starts there
   uint32_t err = 0;
-  for (uint32_t w = blockIdx.x * PULL_WAVES + (threadIdx.x >> 6); w < a.N; w += gridDim.x * PULL_WAVES) {
-    const uint32_t cm = lane < (int)PULL_CH ? chunkmin[(size_t)w * PULL_CH + lane] : ~0u;
-    const uint32_t live = (uint32_t)__ballot(cm != ~0u);
-    if (!live) continue;
-    uint32_t ncnt[LP_KMAX + 1];
-#pragma unroll
-    for (uint32_t k = 0; k <= LP_KMAX; k++) ncnt[k] = 0;
-#pragma unroll
-    for (int q = 0; q < (int)PULL_CH; q++) {
-      if (!((live >> q) & 1u)) continue;  // wave-uniform
-      const uint32_t i = q * 64 + lane;
-      const uint64_t v = i < LL ? a.keys[(size_t)w * LL + i] : INF64;
-      const bool seed = v != INF64 && (v >> a.tshift) != 0;
-      const uint32_t d = seed ? lp_rof((uint32_t)(v >> 32), thr, K) : 0u;  // the window index
-      if (seed && (d == 0 || (uint32_t)(v >> 32) >= beyond)) err |= ERR_TIME;
-#pragma unroll
-      for (uint32_t k = 1; k <= LP_KMAX; k++) {
-        if (k > K) continue;
-        const uint64_t bm = __ballot(seed && d == k);
-        if (seed && d == k) {
-          const uint64_t toff = (v >> a.tshift) - (uint64_t)k * a.delta;
-          a.blk[((size_t)(k % K) * a.N + w) * a.ls + ncnt[k] + (uint32_t)__popcll(bm & lanelt)] =
-              (toff << (a.tshift + a.lb)) | ((v & lowmask) << a.lb) | i;
-        }
-        ncnt[k] += (uint32_t)__popcll(bm);
-      }
-    }
-    if (lane < (int)K) {  // list lengths: window d sits in slot d % K
-      uint32_t nv = 0;
-#pragma unroll
-      for (uint32_t k = 1; k <= LP_KMAX; k++) nv += (k <= K && k % K == (uint32_t)lane) ? ncnt[k] : 0u;
-      a.st[(size_t)w * LP_SW + lane] = nv;
-    }
+  for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < n; i += gridDim.x * TB) {
+    const uint64_t key = skey[i];
+    const uint32_t w = slane[i] >> 11, l = slane[i] & 2047u;
+    const uint32_t d = (uint32_t)(key >> 32) / a.dG;  // the window index (hi-word grain)
+    if (d == 0 || d > K) { err |= ERR_TIME; continue; }
+    const uint32_t slot = d % K;
+    const uint32_t pos = atomicAdd(&a.st[(size_t)w * LP_SW + slot], 1u);
+    if (pos >= a.lcap) { err |= ERR_LIST; continue; }
+    const uint64_t toff = (key >> a.tshift) - (uint64_t)d * a.delta;
+    a.blk[((size_t)slot * a.N + w) * a.ls + pos] = (toff << (a.tshift + a.lb)) | ((key & lowmask) << a.lb) | l;
   }
-  for (int off = 32; off > 0; off >>= 1) err |= __shfl_xor(err, off);
-  if (lane == 0 && err) atomicOr((unsigned*)&a.counters[C_ERR], err);
+  if (err) atomicOr((unsigned*)&a.counters[C_ERR], err);
 }
 
 // The publishers' own lanes: final at time 0 (k_seed's key p), logged first.

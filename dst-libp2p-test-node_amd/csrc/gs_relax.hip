@@ -43,6 +43,11 @@ struct SeedArgs {
   const uint32_t* tables;
   uint64_t* ctrl;      // min seeded key (push: the first bucket; pull: slot 2's min)
   uint32_t* chunkmin;  // pull path: [N][16] min pending key hi-word per 64-lane chunk (push path: nullptr)
+  // list pull path: seeds appended to a list instead of the dense keys (k_lseed
+  // files them into the candidate lists); the publishers' own lanes go to k_lpub
+  uint64_t* skey;
+  uint32_t* slane;     // (row << 11) | lane
+  uint32_t* scnt;
   uint64_t* counters;
   uint64_t tmax;
   uint32_t L, FP, Fe, S, sb, tshift, flood;
@@ -67,7 +72,7 @@ __global__ __launch_bounds__(TB) void k_seed(SeedArgs a) {
   // churn: an offline publisher publishes nothing (the injector's POST finds no node)
   if (a.churn && ep_off(a, a.q0[m], p)) return;
   const bool own_pub = p - a.u0 < a.un;
-  if (own_pub && threadIdx.x < a.Fe) a.keys[(size_t)(p - a.u0) * a.L + (size_t)m * a.FP + threadIdx.x] = (uint64_t)p;
+  if (own_pub && threadIdx.x < a.Fe && !a.skey) a.keys[(size_t)(p - a.u0) * a.L + (size_t)m * a.FP + threadIdx.x] = (uint64_t)p;
   uint32_t deg;
   const uint32_t* tg;
   bool packed;
@@ -106,6 +111,13 @@ __global__ __launch_bounds__(TB) void k_seed(SeedArgs a) {
     const uint64_t nk = (arr << a.tshift) | (1ull << a.sb) | p;
     if (w - a.u0 >= a.un) continue;
     if (a.churn && ev_lost(a, m, arr, w)) continue;
+    if (a.skey) {  // one send per (target, fragment): no duplicates to reduce
+      const uint32_t q = atomicAdd(a.scnt, 1u);
+      a.skey[q] = nk;
+      a.slane[q] = ((w - a.u0) << 11) | (m * a.FP + f);
+      nmin = nk < nmin ? nk : nmin;
+      continue;
+    }
     atomicMin((unsigned long long*)&a.keys[(size_t)(w - a.u0) * a.L + (size_t)m * a.FP + f], (unsigned long long)nk);
     if (a.chunkmin)
       atomicMin(&a.chunkmin[(size_t)(w - a.u0) * PULL_CH + ((m * a.FP + f) >> 6)], (uint32_t)(nk >> 32));
@@ -418,8 +430,13 @@ static void set_churn_args(Ctx& c, A& a) {
 }
 
 static void launch_seed(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, uint64_t* seed_min = nullptr,
-                        uint32_t* chunkmin = nullptr) {
+                        uint32_t* chunkmin = nullptr, bool to_list = false) {
   SeedArgs sa{};
+  if (to_list) {
+    sa.skey = c.d_skey.p;
+    sa.slane = c.d_slane.p;
+    sa.scnt = c.d_scnt.p;
+  }
   set_churn_args(c, sa);
   sa.keys = c.d_keys.p; sa.row = c.d_row.p; sa.col = c.d_col.p; sa.mesh = c.d_mesh.p;
   sa.pub = c.d_pub.p; sa.stage = c.d_stage.p; sa.tables = c.d_tables.p;
@@ -804,7 +821,7 @@ static uint32_t lpull_ring(Ctx& c, const Batch& b, uint64_t delta, uint32_t* lb)
     }
     c.mesh_dmax = dmax;
   }
-  if (b.tshift >= 32 || b.L > PULL_LMAX || delta < 2) return 0;
+  if (b.tshift >= 32 || b.L > PULL_LMAX || delta < 2 || c.cfg.peers >= (1u << 21)) return 0;  // seed list: row << 11
   // a fragment waits behind at most the other FP - 1 fragments' sends to the
   // row's mesh peers (c.mesh_dmax, the widest mesh row)
   const uint64_t dm = c.mesh_dmax ? c.mesh_dmax : MESH_W;
@@ -830,9 +847,11 @@ static uint32_t lpull_ring(Ctx& c, const Batch& b, uint64_t delta, uint32_t* lb)
   return (uint32_t)K;
 }
 
-// One batch on the list pull path: k_seed into the dense keys, seeds -> block
-// 0 (k_lconv), publishers' own lanes (k_lpub), then passes in chunks of 8 as
-// on the k_pull path, and the final logs back to dense rows (k_lfinal).
+// One batch on the list pull path: k_seed appends the first sends to a seed
+// list (no dense key table to reset), k_lseed files them into the candidate
+// lists, k_lpub logs the publishers' own lanes, then passes in chunks of 8 as
+// on the k_pull path; completion reads the final logs (k_lcomplete) unless a
+// caller needs dense rows (k_lfinal).
 // Returns false (counters restored) when a list overflowed: the caller re-runs
 // the batch on k_pull.
 template <class EvFn>
@@ -841,7 +860,6 @@ static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvF
   const uint32_t N = c.cfg.peers, L = b.L;
   hipStream_t s = c.stream;
   const size_t NL = (size_t)N * L;
-  c.d_chunkmin.alloc((size_t)N * PULL_CH);
   c.d_lrec.alloc(2 * NL);
   c.d_lcnt.alloc(2 * (size_t)N);
   c.d_pctrl.alloc(12);
@@ -858,14 +876,19 @@ static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvF
     if (read_counter(c, C_ERR) & ERR_MESH) c.fail(GS_ERANGE, "mesh is not symmetric");
     c.rpos_valid = true;
   }
-  GS_HIP(hipMemsetAsync(c.d_chunkmin.p, 0xFF, (size_t)N * PULL_CH * 4, s));
   GS_HIP(hipMemsetAsync(c.d_lst.p, 0, (size_t)N * LP_SW * 4, s));
   GS_HIP(hipMemsetAsync(c.d_lfin.p, 0, (size_t)N * LP_FW * 4, s));
   GS_HIP(hipMemsetAsync(c.d_pctrl.p, 0, 12 * 8, s));  // every slot {lo 0, DONE, 0 records, min INF}
   for (int q = 0; q < 3; q++) GS_HIP(hipMemsetAsync(c.d_pctrl.p + q * 4 + 3, 0xFF, 8, s));
   c.d_lp_save.alloc(C_COUNT);
   GS_HIP(hipMemcpyAsync(c.d_lp_save.p, c.d_counters.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));
-  launch_seed(c, b, 0, N, c.d_pctrl.p + 2 * 4 + 3, c.d_chunkmin.p);
+  // seeds: one entry per (target, fragment) of every publish (flood: every connection)
+  const uint64_t scap = (uint64_t)b.B * b.Fe * std::max<uint64_t>(c.max_degree, MESH_W);
+  c.d_skey.alloc(scap);
+  c.d_slane.alloc(scap);
+  c.d_scnt.alloc(1);
+  GS_HIP(hipMemsetAsync(c.d_scnt.p, 0, 4, s));
+  launch_seed(c, b, 0, N, c.d_pctrl.p + 2 * 4 + 3, nullptr, true);
   LPullArgs la{};
   la.keys = c.d_keys.p; la.flane = c.d_flane.p; la.busy = c.d_busy.p; la.blk = c.d_lblk.p;
   la.st = c.d_lst.p; la.fin = c.d_lfin.p;
@@ -882,7 +905,8 @@ static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvF
   // 40 KB of LDS per block: 4 blocks (16 waves, 16 rows in flight) per CU
   const unsigned grid = (unsigned)std::max<uint64_t>(
       1, std::min<uint64_t>(((uint64_t)N + PULL_WAVES - 1) / PULL_WAVES, (uint64_t)dev_cus * 4));
-  k_lconv<<<grid, TB, 0, s>>>(la, c.d_chunkmin.p);
+  k_lseed<<<(unsigned)std::max<uint64_t>(1, std::min<uint64_t>((scap + TB - 1) / TB, (uint64_t)dev_cus * 4)), TB, 0, s>>>(
+      la, c.d_skey.p, c.d_slane.p, c.d_scnt.p);
   k_lpub<<<(b.B * b.Fe + 255) / 256, 256, 0, s>>>(la, b.Fe);
   GS_HIP(hipGetLastError());
   uint32_t pass = 0;
@@ -1081,9 +1105,9 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       GS_HIP(hipStreamSynchronize(s));  // rel0 / habs0 host vectors are rewritten by the next batch
     }
     const uint64_t total = (uint64_t)N * L;
-    auto reset = [&](uint32_t v, bool with_gossip) {  // fresh keys and bucket state for this batch
+    auto reset = [&](uint32_t v, bool with_gossip, bool dense_keys = true) {  // fresh keys and bucket state
       c.keys_log = false;
-      GS_HIP(hipMemsetAsync(c.d_keys.p, 0xFF, total * 8, s));
+      if (dense_keys) GS_HIP(hipMemsetAsync(c.d_keys.p, 0xFF, total * 8, s));  // the list pull path needs none
       if (FP > 1) GS_HIP(hipMemsetAsync(c.d_busy.p, 0, (size_t)N * B * 8, s));
       if (v & 32) return;
       if (v & 2) GS_HIP(hipMemsetAsync(c.d_meta.p, 0, (total + 63) / 64 * sizeof(TileMeta), s));
@@ -1188,10 +1212,10 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     if (pull_ok || (gossip && !churn)) {
       if (gossip) GS_HIP(hipMemcpyAsync(c.d_cnt_save.p, c.d_counters.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));
       if (pull_ok) {
-        reset(variant, false);
         const uint64_t grain = pull_grain(b.tshift);
         uint32_t lb = 0;
         const uint32_t K = (variant & 64) ? lpull_ring(c, b, b.delta / grain * grain, &lb) : 0u;
+        reset(variant, false, K == 0);
         if ((variant & 64) && !K && getenv("GS_REQUIRE_LPULL"))  // test knob: no silent k_pull fallback
           c.fail(GS_EUNSUPPORTED, "list pull path cannot take this batch (GS_REQUIRE_LPULL)");
         // GS_LPULL_DENSE (diagnostic): dense rows + k_complete, whose known key
