@@ -797,17 +797,17 @@ static void run_pull_batch(Ctx& c, const Batch& b, EvFn& ev, size_t& n_ev, int d
   c.stats.relax_launches += pass;
 }
 
+// Entries per candidate list: at least 256, so that rows of few lanes (small
+// batches) still hold several passes' appends of the same lanes.
+static uint32_t lpull_stride(const Batch& b) { return std::max<uint32_t>(b.L, 256); }
+
 // Ring size K of the list pull path (gs_lpull_kernel.h) for this batch, or 0
 // when it cannot take the batch (then k_pull runs). A candidate made from a
 // record of window b arrives before b*D + D (start inside the window) + the
 // fragment FIFO + the largest link latency + MESH_W serialisations, so its
 // destination is at most K - 1 windows after the emitted one; the entry
-// packs (t - window start) | hops | src | lane into 64 bits; the ring must fit
-// the device memory left.
-// Entries per candidate list: at least 256, so that rows of few lanes (small
-// batches) still hold several passes' appends of the same lanes.
-static uint32_t lpull_stride(const Batch& b) { return std::max<uint32_t>(b.L, 256); }
-
+// packs (t - window start) | hops | src | lane into 64 bits; the seed list
+// packs row << 11 | lane (N < 2^21); the lists must fit the device memory left.
 static uint32_t lpull_ring(Ctx& c, const Batch& b, uint64_t delta, uint32_t* lb) {
   if (!c.mesh_dmax) {  // widest mesh row, once per mesh
     std::vector<uint32_t> m((size_t)c.cfg.peers * MESH_W);

@@ -166,3 +166,36 @@ def test_config3_small_ring_cuts_batches(monkeypatch):
     st = sim.stats()
     for k in ("deliveries", "relaxations", "gossip_iwant", "latency_sum_ms"):
         assert st[k] == ref["stats"][k], k
+
+
+def test_list_pull_equals_dense_rows_at_1m(monkeypatch):
+    """The bench layout at full size (1M peers, rows of 512 lanes, 5-stage
+    topogen links): the list pull path (variant 109) and k_pull over dense rows
+    (45) agree lane for lane. Lazy gossip off so that neither result can hide
+    behind the push-path fallback; the completion times and hops stream out in
+    blocks of 64 messages and are compared by checksums of every block."""
+    N, B = 1_000_000, 512
+    p = oracle.params(peers=N, seed=1, lazy_gossip=0)
+    sim = _sim(p, 5, LINKS, B)
+    sched = _sched(B, N)
+    out = {}
+    for v in ("45", "109"):
+        monkeypatch.setenv("GS_RELAX_VARIANT", v)
+        if v == "109":
+            monkeypatch.setenv("GS_REQUIRE_LPULL", "1")
+        sums = []
+
+        def blk(first, tc, hp):
+            t = tc.view(np.uint64)
+            w = np.arange(t.size, dtype=np.uint64).reshape(t.shape) * np.uint64(0x9E3779B97F4A7C15)
+            sums.append((first, int(np.bitwise_xor.reduce(t, axis=None)), int(np.sum(t * (w | np.uint64(1)))),
+                         int(np.sum(hp.astype(np.uint64))), int((t == UND).sum())))
+
+        sim.reset_stats()
+        sim.run(sched, on_block=blk, block_msgs=64)
+        st = sim.stats()
+        assert st["deliveries"] == B * (N - 1)
+        out[v] = (sums, st["list_pull_batches"], st["relaxations"])
+    assert out["45"][1] == 0 and out["109"][1] >= 1
+    assert out["45"][2] == out["109"][2]
+    assert out["45"][0] == out["109"][0]
