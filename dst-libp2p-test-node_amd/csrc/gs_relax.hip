@@ -925,11 +925,12 @@ static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvF
     }
     GS_HIP(hipGetLastError());
     GS_HIP(hipMemcpyAsync(c.h_pinned, c.d_pctrl.p, 12 * 8, hipMemcpyDeviceToHost, s));
+    GS_HIP(hipMemcpyAsync(c.h_pinned + 12, c.d_counters.p + C_ERR, 8, hipMemcpyDeviceToHost, s));  // same sync
     GS_HIP(hipStreamSynchronize(s));
     if (c.h_pinned[((pass - 1) % 3) * 4 + 1] == PM_DONE) break;
   }
   c.stats.relax_launches += pass;
-  if (read_counter(c, C_ERR) & ERR_LIST) {
+  if (c.h_pinned[12] & ERR_LIST) {  // the error word as of the DONE pass
     GS_HIP(hipMemcpyAsync(c.d_counters.p, c.d_lp_save.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));
     return false;
   }
