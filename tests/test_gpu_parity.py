@@ -333,11 +333,11 @@ def test_large_graph_properties_and_sampled_parity():
         np.testing.assert_array_equal(res["hops"][m], hp[0])
 
 
-@pytest.mark.parametrize("variant", list(range(8)) + [8, 9, 10, 11, 13, 15, 45, 109])
+@pytest.mark.parametrize("variant", list(range(8)) + [8, 9, 10, 11, 13, 15, 45, 109, 237])
 def test_relax_kernel_variants_exact(variant, monkeypatch):
     """Every bucket implementation (fused with read-filter / tile-skip / final-bitset,
     split scan+frontier, owner-computes pull over dense rows = 45, over candidate
-    lists = 109, the default) is bit-exact."""
+    lists = 109, the default, and 237 = lists for fragmented batches too) is bit-exact."""
     monkeypatch.setenv("GS_RELAX_VARIANT", str(variant))
     if variant & 64:
         monkeypatch.setenv("GS_REQUIRE_LPULL", "1")
@@ -349,7 +349,7 @@ def test_relax_kernel_variants_exact(variant, monkeypatch):
     compare(p, 3, (20, 200, 10, 90), _sched(70, 3000), batch=64)
 
 
-@pytest.mark.parametrize("variant,frags", [(45, 1), (109, 1), (109, 2), (109, 4)])
+@pytest.mark.parametrize("variant,frags", [(45, 1), (109, 1), (237, 2), (237, 4)])
 def test_pull_wide_rows_exact(variant, frags, monkeypatch):
     """Rows of 1024 lanes (16 chunks of 64, the bench layout) on both pull
     kernels: every chunk of a row is live in the peak windows, candidate lists
