@@ -8,7 +8,7 @@ ks = sorted([(r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"
             key=lambda x: x[1])
 seeds = [i for i, k in enumerate(ks) if "k_seed" in k[0]]
 last = ks[seeds[-1]:]
-KN = ("k_lpull", "k_lconv", "k_lfinal", "k_lpub", "k_pull", "k_scan", "k_frontier", "k_complete", "k_seed")
+KN = ("k_lpull", "k_lseed", "k_lcomplete", "k_lfinal", "k_lpub", "k_pull", "k_scan", "k_frontier", "k_complete", "k_seed")
 short = lambda n: next((k for k in KN if k in n), n[:12])
 print(" ".join("%s:%.0f" % (short(n).replace("k_", ""), (e - s) / 1e3) for n, s, e in last if "copyBuf" not in n))
 tot = {}
