@@ -902,9 +902,16 @@ static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvF
   const char* cap = getenv("GS_LPULL_CAP");  // test knob: small lists force the overflow re-run
   la.ls = ls;
   la.lcap = cap && *cap ? (uint32_t)std::min<long>(std::max(1, atoi(cap)), (long)ls) : ls;
-  // 40 KB of LDS per block: 4 blocks (16 waves, 16 rows in flight) per CU
+  // 40 KB of LDS per block: 4 blocks (16 waves, 16 rows in flight) resident per
+  // CU; 16 blocks per CU are launched so that the pass's tail is made of short
+  // blocks (1M peers: 54.3 ms per step at 4, 53.1 at 16, 52.9-53.6 at 12-32,
+  // profiles/r02_v7/lpull_grid_sweep.txt); GS_LPULL_BPC overrides it
+  static const uint64_t bpc = [] {
+    const char* e = getenv("GS_LPULL_BPC");
+    return (uint64_t)(e && *e ? std::max(1, atoi(e)) : 16);
+  }();
   const unsigned grid = (unsigned)std::max<uint64_t>(
-      1, std::min<uint64_t>(((uint64_t)N + PULL_WAVES - 1) / PULL_WAVES, (uint64_t)dev_cus * 4));
+      1, std::min<uint64_t>(((uint64_t)N + PULL_WAVES - 1) / PULL_WAVES, (uint64_t)dev_cus * bpc));
   k_lseed<<<(unsigned)std::max<uint64_t>(1, std::min<uint64_t>((scap + TB - 1) / TB, (uint64_t)dev_cus * 4)), TB, 0, s>>>(
       la, c.d_skey.p, c.d_slane.p, c.d_scnt.p);
   k_lpub<<<(b.B * b.Fe + 255) / 256, 256, 0, s>>>(la, b.Fe);
