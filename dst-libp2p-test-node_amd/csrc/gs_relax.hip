@@ -903,15 +903,19 @@ static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvF
   la.ls = ls;
   la.lcap = cap && *cap ? (uint32_t)std::min<long>(std::max(1, atoi(cap)), (long)ls) : ls;
   // 40 KB of LDS per block: 4 blocks (16 waves, 16 rows in flight) resident per
-  // CU; 16 blocks per CU are launched so that the pass's tail is made of short
-  // blocks (1M peers: 54.3 ms per step at 4, 53.1 at 16, 52.9-53.6 at 12-32,
-  // profiles/r02_v7/lpull_grid_sweep.txt); GS_LPULL_BPC overrides it
+  // CU. Large graphs launch up to 16 blocks per CU so that a pass's tail is
+  // made of short blocks, keeping >= 32 rows per wave (1M peers: 54.3 ms per
+  // step at 4 blocks per CU, 53.1 at 16; 100k peers: 7.8 ms at 16, 6.8 at 4;
+  // profiles/r02_v7/lpull_grid_sweep.txt); GS_LPULL_BPC fixes blocks per CU
   static const uint64_t bpc = [] {
     const char* e = getenv("GS_LPULL_BPC");
-    return (uint64_t)(e && *e ? std::max(1, atoi(e)) : 16);
+    return (uint64_t)(e && *e ? std::max(1, atoi(e)) : 0);
   }();
-  const unsigned grid = (unsigned)std::max<uint64_t>(
-      1, std::min<uint64_t>(((uint64_t)N + PULL_WAVES - 1) / PULL_WAVES, (uint64_t)dev_cus * bpc));
+  // a power of two: 15 per CU measured 56.4 ms against 53.1 at 16 on one box
+  uint64_t auto_bpc = 4;
+  while (auto_bpc < 16 && (uint64_t)N >= (uint64_t)dev_cus * PULL_WAVES * 32 * auto_bpc * 2) auto_bpc *= 2;
+  const uint64_t want = (uint64_t)dev_cus * (bpc ? bpc : auto_bpc);  // whole blocks per CU
+  const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(((uint64_t)N + PULL_WAVES - 1) / PULL_WAVES, want));
   k_lseed<<<(unsigned)std::max<uint64_t>(1, std::min<uint64_t>((scap + TB - 1) / TB, (uint64_t)dev_cus * 4)), TB, 0, s>>>(
       la, c.d_skey.p, c.d_slane.p, c.d_scnt.p);
   k_lpub<<<(b.B * b.Fe + 255) / 256, 256, 0, s>>>(la, b.Fe);
