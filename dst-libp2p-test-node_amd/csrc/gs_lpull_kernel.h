@@ -10,7 +10,8 @@
 // state is never kept in a dense row during the passes:
 //
 //  - fin[w]: one bit per lane, set when the lane's key is final (emitted),
-//    held in registers (u32 word j in lane j) while the row is processed;
+//    held transposed in registers (lane j: bit q for lane q*64 + j) while the
+//    row is processed;
 //  - candidates that do not fall in the window being emitted are appended to
 //    the row's list for their destination window c' (slot c' % K of a ring of
 //    K lists of up to L entries); st[w] holds the K list lengths and the
@@ -45,7 +46,7 @@ struct LPullArgs {
   uint64_t* busy;       // [N][B] uplink FIFO end per (peer, message), FP > 1
   uint64_t* blk;        // [K][N][ls] candidate lists per destination-window slot
   uint32_t* st;         // [N][LP_SW]
-  uint32_t* fin;        // [N][32] final bits, 32 lanes per word
+  uint32_t* fin;        // [N][64] u16 final bits, transposed: u16 j bit q = lane q*64 + j
   uint64_t* lrec;       // [2][N][L] per-row arrival records (k_pull's format)
   uint32_t* lcnt;       // [2][N]
   const uint32_t* mesh;
@@ -165,7 +166,8 @@ __global__ __launch_bounds__(TB, 4) void k_lpull(LPullArgs a) {
     }
     PP_ADD(7, 1);
     const uint32_t sw = a.stage[w];
-    uint32_t fin32 = lane < (int)LP_FW ? a.fin[(size_t)w * LP_FW + lane] : 0u;
+    // final bits transposed: lane j holds bit q for lane q*64 + j (u16 per lane)
+    uint32_t finT = reinterpret_cast<const uint16_t*>(a.fin + (size_t)w * LP_FW)[lane];
     // 1. the entries listed for window c (final lanes are dropped in step 3)
     uint32_t cb = 0;
     if (due) {
@@ -261,10 +263,8 @@ __global__ __launch_bounds__(TB, 4) void k_lpull(LPullArgs a) {
     for (int q = 0; q < (int)PULL_CH; q++) {
       if (!((cb >> q) & 1u)) continue;  // wave-uniform
       const uint32_t i = q * 64 + lane;
-      const uint64_t fw = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(fin32, 2 * q) |
-                          ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(fin32, 2 * q + 1) << 32);
       uint64_t x = CW[i];
-      if (x != INF64 && ((fw >> lane) & 1)) {  // final in an earlier window
+      if (x != INF64 && ((finT >> q) & 1u)) {  // final in an earlier window
         x = INF64;
         CW[i] = INF64;
       }
@@ -275,8 +275,7 @@ __global__ __launch_bounds__(TB, 4) void k_lpull(LPullArgs a) {
       npend += (uint32_t)__popcll(pm);
       const uint64_t am = __ballot(act);
       if (am) {  // wave-uniform
-        if (lane == 2 * q) fin32 |= (uint32_t)am;
-        if (lane == 2 * q + 1) fin32 |= (uint32_t)(am >> 32);
+        finT |= act ? 1u << q : 0u;
         nfin = 1;
         if constexpr (FP == 1) {
           if (act) LST[cnt + (uint32_t)__popcll(am & lanelt)] = (uint16_t)i;
@@ -385,7 +384,7 @@ __global__ __launch_bounds__(TB, 4) void k_lpull(LPullArgs a) {
     PP_T(tD);
     PP_ADD(5, tD - tP);
     // 5. row state: final bits, pending list lengths, log length
-    if (nfin && lane < (int)LP_FW) a.fin[(size_t)w * LP_FW + lane] = fin32;
+    if (nfin) reinterpret_cast<uint16_t*>(a.fin + (size_t)w * LP_FW)[lane] = (uint16_t)finT;
     {
       uint32_t add = 0;  // lane j < K: slot j stands for window c + lwin
 #pragma unroll
@@ -454,7 +453,8 @@ __global__ void k_lpub(LPullArgs a, uint32_t Fe) {
   const uint32_t FP = a.L / a.B;
   if (g >= a.B * Fe) return;
   const uint32_t m = g / Fe, f = g % Fe, p = a.pub[m], i = m * FP + f;
-  atomicOr(&a.fin[(size_t)p * LP_FW + (i >> 5)], 1u << (i & 31));
+  const uint32_t j = i & 63, q = i >> 6;  // transposed: lane j's u16, bit q
+  atomicOr(&a.fin[(size_t)p * LP_FW + (j >> 1)], 1u << (16 * (j & 1) + q));
   const uint32_t pos = atomicAdd(&a.st[(size_t)p * LP_SW + LP_LOG], 1u);
   a.keys[(size_t)p * a.L + pos] = (uint64_t)p;
   a.flane[(size_t)p * a.L + pos] = (uint16_t)i;
