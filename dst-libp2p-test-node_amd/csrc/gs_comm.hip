@@ -154,15 +154,81 @@ extern "C" gs_status gs_comm_destroy(gs_comm* c) {
 
 namespace {
 
+// Bytes per ncclSend / ncclRecv piece of the record exchange: 2^30 by default
+// (DESIGN.md §5); GS_RCCL_PIECE_BYTES lowers it (tests force many pieces).
+uint64_t rccl_piece_bytes() {  // read per bucket: tests change it between runs
+  const char* e = getenv("GS_RCCL_PIECE_BYTES");
+  const long long x = e && *e ? atoll(e) : 0;
+  return x > 0 ? std::min<uint64_t>((uint64_t)x, 1ull << 30) : (1ull << 30);
+}
+
+// RCCL ranks agree on a status word (MAX): a rank that failed locally makes
+// every rank fail the call instead of leaving the others waiting in a
+// collective (the caller's error text names the failing rank's reason only
+// on that rank).
+void rank_status(gs_comm* cm, Ctx& c, uint64_t mine) {
+  if (cm->local) return;
+  Rccl* r = rccl();
+  uint64_t* w = cm->d_scratch + (size_t)cm->nranks * cm->nranks;
+  c.h_pinned[0] = mine;
+  GS_HIP(hipMemcpyAsync(w, c.h_pinned, 8, hipMemcpyHostToDevice, c.stream));
+  GS_NCCL(r->AllReduce(w, w, 1, ncclUint64, ncclMax, cm->nc, c.stream));
+  GS_HIP(hipMemcpyAsync(c.h_pinned, w, 8, hipMemcpyDeviceToHost, c.stream));
+  GS_HIP(hipStreamSynchronize(c.stream));
+  if (c.h_pinned[0] && !mine) throw Error(GS_EINVAL, "another rank failed this partitioned call");
+}
+
+// Every RCCL rank must run the same protocol: the knobs that decide the
+// batches and the collectives they enter are compared across ranks (MIN and
+// MAX of each word agree) before the first batch.
+void check_same_config(gs_comm* cm, Ctx& c, const gs_publish* sched, uint64_t n_msgs) {
+  if (cm->local) return;
+  Rccl* r = rccl();
+  uint64_t h = 1469598103934665603ull;  // FNV-1a over the schedule
+  for (uint64_t i = 0; i < n_msgs; i++) {
+    const uint64_t v[4] = {sched[i].t_pub_ns, sched[i].publisher, sched[i].msg_size, sched[i].frags};
+    for (uint64_t x : v) h = (h ^ x) * 1099511628211ull;
+  }
+  const uint64_t sig[8] = {c.cfg.peers, c.cfg.batch, c.cfg.lazy_gossip, c.cfg.idontwant,
+                           c.cfg.churn_ppm, c.cfg.fragments, c.cfg.seed, h ^ n_msgs};
+  DevBuf<uint64_t> d;
+  d.alloc(16);
+  memcpy(c.h_pinned, sig, sizeof sig);
+  GS_HIP(hipMemcpyAsync(d.p, c.h_pinned, sizeof sig, hipMemcpyHostToDevice, c.stream));
+  GS_HIP(hipMemcpyAsync(d.p + 8, c.h_pinned, sizeof sig, hipMemcpyHostToDevice, c.stream));
+  GS_NCCL(r->AllReduce(d.p, d.p, 8, ncclUint64, ncclMin, cm->nc, c.stream));
+  GS_NCCL(r->AllReduce(d.p + 8, d.p + 8, 8, ncclUint64, ncclMax, cm->nc, c.stream));
+  GS_HIP(hipMemcpyAsync(c.h_pinned, d.p, 16 * 8, hipMemcpyDeviceToHost, c.stream));
+  GS_HIP(hipStreamSynchronize(c.stream));
+  for (int k = 0; k < 8; k++)
+    if (c.h_pinned[k] != c.h_pinned[8 + k])
+      throw Error(GS_EINVAL, "RCCL ranks disagree on the partitioned run (peers, batch, lazy_gossip, idontwant, "
+                             "churn, fragments, seed or schedule)");
+}
+
 // One batch of the partitioned protocol over this process's parts.
 void run_batch(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched, uint64_t i0, uint32_t B,
                const gs_result_sink* sinks) {
   const uint32_t P = cm->nranks;
   Rccl* r = cm->local ? nullptr : rccl();
   std::vector<uint64_t> key0(nctx);
-  for (uint32_t i = 0; i < nctx; i++) {
-    GS_HIP(hipSetDevice(cx[i]->cfg.device));
-    key0[i] = part_begin(*cx[i], sched + i0, B);  // the seeded min is also left in ctrl[0]
+  if (cm->local) {
+    for (uint32_t i = 0; i < nctx; i++) {
+      GS_HIP(hipSetDevice(cx[i]->cfg.device));
+      key0[i] = part_begin(*cx[i], sched + i0, B);  // the seeded min is also left in ctrl[0]
+    }
+  } else {  // a rank whose batch set-up fails takes the others out with it
+    GS_HIP(hipSetDevice(cx[0]->cfg.device));
+    std::string why;
+    gs_status code = GS_OK;
+    try {
+      key0[0] = part_begin(*cx[0], sched + i0, B);
+    } catch (const Error& e) {
+      code = e.code;
+      why = e.msg;
+    }
+    rank_status(cm, *cx[0], code != GS_OK);
+    if (code != GS_OK) throw Error(code, why);
   }
   // mat[s * P + d] = records part s sends to part d (this bucket)
   std::vector<uint64_t> mat((size_t)P * P), ctl(nctx);
@@ -176,12 +242,27 @@ void run_batch(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched, ui
   };
   if (cm->local) host_min_to_ctrl(*std::min_element(key0.begin(), key0.end()));
   else GS_NCCL(r->AllReduce(cx[0]->d_ctrl.p, cx[0]->d_ctrl.p, 1, ncclUint64, ncclMin, cm->nc, cx[0]->stream));
+  // timing (gs_set_timing): per part and bucket three events on its stream —
+  // bucket start, scan + counts done (scan_ms), relax done (frontier_ms: the
+  // routed export, the exchange and the receive-side relaxation)
+  std::vector<size_t> nev(nctx, 0);
+  auto ev = [&](uint32_t i) {
+    Ctx& c = *cx[i];
+    while (c.ev_pool.size() <= nev[i]) {
+      hipEvent_t e;
+      GS_HIP(hipEventCreate(&e));
+      c.ev_pool.push_back(e);
+    }
+    GS_HIP(hipEventRecord(c.ev_pool[nev[i]++], c.stream));
+  };
   for (;;) {
     // 1. scan + per-destination counts
     for (uint32_t i = 0; i < nctx; i++) {
       GS_HIP(hipSetDevice(cx[i]->cfg.device));
+      if (cx[i]->timing) ev(i);
       part_dev_bucket(*cx[i], P);
       part_dev_scan_count(*cx[i], P);
+      if (cx[i]->timing) ev(i);
     }
     // 2. the count matrix and the bucket key on the host (the one read per bucket)
     uint64_t key = INF64;
@@ -236,9 +317,9 @@ void run_batch(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched, ui
       Ctx& c = *cx[0];
       const uint32_t me = cm->rank;
       // peak buckets at 1M peers move GBs per pair: point-to-point transfers in
-      // pieces of at most 2^30 bytes (RCCL's p2p path mishandles single
-      // transfers past 2^31 bytes); both ends cut the same count the same way
-      const uint64_t piece = (1ull << 30) / RB;
+      // pieces of at most rccl_piece_bytes(); both ends cut the
+      // same count the same way
+      const uint64_t piece = std::max<uint64_t>(1, rccl_piece_bytes() / RB);
       GS_NCCL(r->GroupStart());
       uint64_t soff = 0, roff = 0;
       for (uint32_t d = 0; d < P; d++) {
@@ -259,6 +340,7 @@ void run_batch(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched, ui
     for (uint32_t i = 0; i < nctx; i++) {
       GS_HIP(hipSetDevice(cx[i]->cfg.device));
       part_dev_relax_next(*cx[i], cx[i]->d_pin.p, nrecv[i]);
+      if (cx[i]->timing) ev(i);
     }
     if (cm->local) {
       for (uint32_t i = 0; i < nctx; i++) {
@@ -270,6 +352,28 @@ void run_batch(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched, ui
     } else {
       GS_NCCL(r->AllReduce(cx[0]->d_ctrl.p, cx[0]->d_ctrl.p, 1, ncclUint64, ncclMin, cm->nc, cx[0]->stream));
     }
+  }
+  for (uint32_t i = 0; i < nctx; i++) {  // bucket times (the loop ended on a stream sync)
+    Ctx& c = *cx[i];
+    if (!c.timing) continue;
+    GS_HIP(hipSetDevice(c.cfg.device));
+    GS_HIP(hipStreamSynchronize(c.stream));
+    double scan = 0, front = 0;
+    for (size_t q = 0; q + 2 < nev[i]; q += 3) {
+      float x = 0, y = 0;
+      GS_HIP(hipEventElapsedTime(&x, c.ev_pool[q], c.ev_pool[q + 1]));
+      GS_HIP(hipEventElapsedTime(&y, c.ev_pool[q + 1], c.ev_pool[q + 2]));
+      scan += x;
+      front += y;
+    }
+    if (nev[i] % 3 == 2) {  // the last scan, which found no bucket left
+      float x = 0;
+      GS_HIP(hipEventElapsedTime(&x, c.ev_pool[nev[i] - 2], c.ev_pool[nev[i] - 1]));
+      scan += x;
+    }
+    c.stats.scan_ms += scan;
+    c.stats.frontier_ms += front;
+    c.stats.relax_ms += scan + front;
   }
   // lazy gossip: the eager result stands only where every part proves it a no-op
   bool ok = true;
@@ -325,6 +429,7 @@ extern "C" gs_status gs_run_partitioned(gs_ctx* const* ctxs, uint32_t nctx, gs_c
     }
     if (!comm->local && c0->cfg.device != comm->device)
       c0->fail(GS_EINVAL, "the context and the communicator must use the same device");
+    check_same_config(comm, *c0, sched, n_msgs);
     uint64_t i0 = 0;
     while (i0 < n_msgs) {  // batches of equal size and chunk count, at most cfg.batch messages
       uint64_t i1 = i0 + 1;
@@ -335,9 +440,11 @@ extern "C" gs_status gs_run_partitioned(gs_ctx* const* ctxs, uint32_t nctx, gs_c
       i0 = i1;
     }
   } catch (const Error& e) {
+    for (uint32_t i = 0; i < nctx; i++) part_abort(*ctxs[i]);  // no context is left mid-batch
     c0->last_error = e.msg;
     return e.code;
   } catch (const std::exception& e) {
+    for (uint32_t i = 0; i < nctx; i++) part_abort(*ctxs[i]);
     c0->last_error = e.what();
     return GS_ENOMEM;
   }

@@ -209,6 +209,11 @@ extern "C" gs_status gs_run(gs_ctx* ctx, const gs_publish* sched, uint64_t n_msg
   GS_API_BEGIN(ctx)
   if (!ctx->mesh_built) ctx->fail(GS_ESTATE, "gs_mesh_converge first");
   if (!sched && n_msgs) ctx->fail(GS_EINVAL, "null schedule");
+  if (sink && sink->on_block && (sink->t_complete_ns || sink->hops))
+    ctx->fail(GS_EINVAL, "gs_result_sink: with on_block, t_complete_ns and hops must be NULL (select outputs "
+                         "with want, ABI 7)");
+  if (sink && (sink->want & ~(uint32_t)(GS_WANT_T_COMPLETE | GS_WANT_HOPS)))
+    ctx->fail(GS_EINVAL, "gs_result_sink.want: unknown bits");
   GS_HIP(hipSetDevice(ctx->cfg.device));
   if (n_msgs) run_messages(*ctx, sched, n_msgs, sink);
   GS_API_END(ctx)

@@ -25,7 +25,9 @@ struct Error {
 };
 
 // Device-side error word bits (set by kernels, checked by the host).
-enum : uint32_t { ERR_TIME = 1, ERR_HOPS = 2, ERR_MESH = 4, ERR_DEG = 8, ERR_LIST = 16 };  // ERR_LIST: list pull overflow (re-run on k_pull)
+// ERR_LIST: a list pull candidate list overflowed; ERR_RING: a list pull candidate
+// fell outside the K-window ring the host bound promised. Both re-run the batch on k_pull.
+enum : uint32_t { ERR_TIME = 1, ERR_HOPS = 2, ERR_MESH = 4, ERR_DEG = 8, ERR_LIST = 16, ERR_RING = 32 };
 
 // Device buffer owned by a context.
 template <class T>

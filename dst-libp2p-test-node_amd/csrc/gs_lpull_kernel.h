@@ -154,7 +154,9 @@ __global__ __launch_bounds__(TB, 4) void k_lpull(LPullArgs a) {
       sv2 = a.st[(size_t)w2 * LP_SW + lane];
     }
     const uint64_t cand = __ballot(cj != 0);
-    const uint32_t due = __builtin_amdgcn_readlane(sv, cslot);  // entries destined to window c
+    // entries destined to window c; a count past the capacity means entries were
+    // dropped (ERR_LIST, the batch re-runs on k_pull): read only what was written
+    const uint32_t due = umin32(__builtin_amdgcn_readlane(sv, cslot), a.lcap);
     if (cand == 0 && due == 0) {  // nothing to apply, nothing due: the pending windows stay
       if (lane == 0) wcnt[w] = 0;
       if (lane < (int)K && sv) nmh = umin32(nmh, lwhi);
@@ -301,7 +303,7 @@ __global__ __launch_bounds__(TB, 4) void k_lpull(LPullArgs a) {
       ncnt[k] = 0;
       base[k] = 0;
     }
-    if (!pull && npend) err |= ERR_TIME;  // an EMIT pass's minima all lie in window c
+    if (!pull && npend) err |= ERR_RING;  // an EMIT pass's minima all lie in window c
     if (pull && npend) {
 #pragma unroll
       for (uint32_t k = 1; k < LP_KMAX; k++)
@@ -312,7 +314,7 @@ __global__ __launch_bounds__(TB, 4) void k_lpull(LPullArgs a) {
         const uint32_t li = jv ? LST[PULL_LMAX - 1 - (j0 + lane)] : 0u;
         const uint64_t x = jv ? CW[li] : INF64;
         const uint32_t r = jv ? lp_rof((uint32_t)(x >> 32), thr, K) : 0u;
-        if (jv && r >= K) err |= ERR_TIME;
+        if (jv && r >= K) err |= ERR_RING;
         uint32_t pos = 0, slot = 0;
 #pragma unroll
         for (uint32_t k = 1; k < LP_KMAX; k++) {
@@ -437,7 +439,7 @@ __global__ __launch_bounds__(TB) void k_lseed(LPullArgs a, const uint64_t* __res
     const uint64_t key = skey[i];
     const uint32_t w = slane[i] >> 11, l = slane[i] & 2047u;
     const uint32_t d = (uint32_t)(key >> 32) / a.dG;  // the window index (hi-word grain)
-    if (d == 0 || d > K) { err |= ERR_TIME; continue; }
+    if (d == 0 || d > K) { err |= ERR_RING; continue; }
     const uint32_t slot = d % K;
     const uint32_t pos = atomicAdd(&a.st[(size_t)w * LP_SW + slot], 1u);
     if (pos >= a.lcap) { err |= ERR_LIST; continue; }

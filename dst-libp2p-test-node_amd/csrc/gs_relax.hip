@@ -598,7 +598,9 @@ static void deliver(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, const gs_r
                     uint64_t sink_row0) {
   if (!sink) return;
   hipStream_t s = c.stream;
-  const bool want_tc = sink->t_complete_ns != nullptr, want_h = sink->hops != nullptr;
+  const uint32_t want = sink->want ? sink->want : (GS_WANT_T_COMPLETE | GS_WANT_HOPS);
+  const bool want_tc = sink->on_block ? (want & GS_WANT_T_COMPLETE) != 0 : sink->t_complete_ns != nullptr;
+  const bool want_h = sink->on_block ? (want & GS_WANT_HOPS) != 0 : sink->hops != nullptr;
   if (want_tc || want_h) {
     c.d_tc_t.alloc((size_t)un * c.cfg.batch);
     c.d_hops_t.alloc((size_t)un * c.cfg.batch);
@@ -831,8 +833,11 @@ static uint32_t lpull_ring(Ctx& c, const Batch& b, uint64_t delta, uint32_t* lb)
   // connection with flood publish) land in windows 1 .. K of source window 0
   const uint64_t sdeg = c.cfg.flood_publish ? std::max<uint64_t>(c.max_degree, 1) : dm;
   const uint64_t seed_span = (uint64_t)b.FP * sdeg * b.ser_max + b.lat_adj_max;
-  const uint64_t K = std::max(span / delta + 2, seed_span / delta + 1);
+  uint64_t K = std::max(span / delta + 2, seed_span / delta + 1);
   if (K > LP_KMAX) return 0;
+  // test knob: a ring smaller than the bound forces ERR_RING and the k_pull re-run
+  static const char* kf = getenv("GS_LPULL_K");
+  if (kf && *kf) K = std::min<uint64_t>(K, (uint64_t)std::max(2, atoi(kf)));
   uint32_t tb = 0;
   while ((1ull << tb) < delta) tb++;
   *lb = bits_for(b.L);
@@ -939,9 +944,10 @@ static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvF
     GS_HIP(hipMemcpyAsync(c.h_pinned + 12, c.d_counters.p + C_ERR, 8, hipMemcpyDeviceToHost, s));  // same sync
     GS_HIP(hipStreamSynchronize(s));
     if (c.h_pinned[((pass - 1) % 3) * 4 + 1] == PM_DONE) break;
+    if (c.h_pinned[12] & (ERR_LIST | ERR_RING)) break;  // lost already: stop early, re-run on k_pull
   }
   c.stats.relax_launches += pass;
-  if (c.h_pinned[12] & ERR_LIST) {  // the error word as of the DONE pass
+  if (c.h_pinned[12] & (ERR_LIST | ERR_RING)) {  // the error word as of the last pass read
     GS_HIP(hipMemcpyAsync(c.d_counters.p, c.d_lp_save.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));
     return false;
   }

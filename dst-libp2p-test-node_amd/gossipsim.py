@@ -26,7 +26,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GOSSIPSIM_LIB", os.path.join(HERE, "libgossipsim.so"))
-ABI_VERSION = 6
+ABI_VERSION = 7
 MESH_W = 16
 UNDELIVERED = np.uint64(0xFFFFFFFFFFFFFFFF)
 MUXERS = {"yamux": 0, "quic": 1, "mplex": 2}
@@ -65,7 +65,10 @@ BLOCK_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, u64, u32, u32, P(u64), P(u8))
 
 class GsResultSink(ctypes.Structure):
     _fields_ = [("t_complete_ns", P(u64)), ("hops", P(u8)), ("on_block", BLOCK_FN), ("user", ctypes.c_void_p),
-                ("block_msgs", u32), ("reserved", u32), ("summary", P(GsMsgSummary))]
+                ("block_msgs", u32), ("want", u32), ("summary", P(GsMsgSummary))]
+
+
+WANT_T_COMPLETE, WANT_HOPS = 1, 2  # gs_result_sink.want (GS_WANT_*)
 
 
 class GsStats(ctypes.Structure):
@@ -135,6 +138,7 @@ SIGNATURES = {
     "gs_run_partitioned": (i32, [P(ctypes.c_void_p), u32, ctypes.c_void_p, P(GsPublish), u64, P(GsResultSink)]),
 }
 COMM_ID_BYTES = 128
+GS_EINVAL = -1
 GS_ERANGE = -5
 KEY_NONE = (1 << 64) - 1  # empty-bucket marker of the partitioned protocol
 
@@ -458,13 +462,15 @@ class Simulator:
             schedule = arr
         return schedule
 
-    def run(self, schedule=None, collect=True, summary=False, on_block=None, block_msgs=0):
+    def run(self, schedule=None, collect=True, summary=False, on_block=None, block_msgs=0,
+            want=WANT_T_COMPLETE | WANT_HOPS):
         """Simulate the queued publishes (or `schedule`); returns t_complete/hops [M, N].
 
         summary: also return the device's per-message latency reductions
         (gs_msg_summary: delivered, lat_sum_ms, p50/p95/max ms, 100 ms histogram).
         on_block(first_msg, t_complete[n, N], hops[n, N]): stream the results in
-        blocks of `block_msgs` messages instead of returning [M, N] arrays."""
+        blocks of `block_msgs` messages instead of returning [M, N] arrays;
+        `want` (WANT_* bits) selects which of the two it receives (None if not)."""
         schedule = self._schedule(schedule)
         M = len(schedule)
         res = {"schedule": schedule}
@@ -480,11 +486,7 @@ class Simulator:
 
             cb = BLOCK_FN(_cb)
             keep.append(cb)
-            flag = np.zeros(1, np.uint64)
-            flag8 = np.zeros(1, np.uint8)
-            keep += [flag, flag8]
-            sink.t_complete_ns = _ptr(flag, u64)
-            sink.hops = _ptr(flag8, u8)
+            sink.want = want
             sink.on_block = cb
             sink.block_msgs = block_msgs
         elif collect:

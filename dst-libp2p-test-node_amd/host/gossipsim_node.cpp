@@ -179,9 +179,8 @@ int main(int argc, char** argv) {
   strm.self_log = cfg.self_log;
   if (!latencies.empty() && (st = gs_log_open(&cfg, latencies.c_str(), &strm.log)) != GS_OK)
     return die(ctx, st, "gs_log_open");
-  uint64_t flag = 0;
   gs_result_sink sink{};
-  sink.t_complete_ns = &flag;  // wanted, streamed through on_block
+  sink.want = GS_WANT_T_COMPLETE;  // streamed through on_block
   sink.on_block = on_block;
   sink.user = &strm;
   sink.block_msgs = 16;

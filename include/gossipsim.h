@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 6u
+#define GS_ABI_VERSION 7u
 
 /* Sentinel for "never delivered" in t_complete_ns. */
 #define GS_UNDELIVERED UINT64_MAX
@@ -137,16 +137,21 @@ typedef struct gs_msg_summary {
 /* Streaming receiver of results: called from gs_run on the caller's thread
  * with message-major blocks of at most `block_msgs` messages; the arrays are
  * library-owned and valid only during the call ([n_msgs][peers], either may
- * be NULL when the matching sink pointer request is off). */
+ * be NULL when gs_result_sink.want does not select it). */
 typedef void (*gs_block_fn)(void* user, uint64_t first_msg, uint32_t n_msgs, uint32_t peers,
                             const uint64_t* t_complete_ns, const uint8_t* hops);
 
+/* Outputs an on_block sink streams (gs_result_sink.want). */
+enum { GS_WANT_T_COMPLETE = 1u, GS_WANT_HOPS = 2u };
+
 /* Where gs_run puts results. Every member may be NULL / 0.
- *  - t_complete_ns / hops: caller arrays, message-major [n_msgs][peers]
- *    (without on_block), or flags that on_block wants that output (any
- *    non-NULL value; nothing is written through it);
+ *  - t_complete_ns / hops: caller arrays, message-major [n_msgs][peers];
+ *    without on_block only; they must be NULL when on_block is set
+ *    (GS_EINVAL otherwise: nothing is ever written through them then);
  *  - on_block: streaming delivery instead of the arrays (no [n_msgs][peers]
- *    host array is needed for large N);
+ *    host array is needed for large N); `want` selects what it receives
+ *    (GS_WANT_* bits, 0 = both); ABI 7 (ABI 6 used non-NULL array pointers
+ *    as the selection flags);
  *  - summary: [n_msgs] per-message latency reductions. */
 typedef struct gs_result_sink {
     uint64_t* t_complete_ns;  /* completion time of message m at peer u (GS_UNDELIVERED if never) */
@@ -154,7 +159,7 @@ typedef struct gs_result_sink {
     gs_block_fn on_block;
     void*     user;
     uint32_t  block_msgs;     /* messages per on_block call; 0 = 64                               */
-    uint32_t  reserved;
+    uint32_t  want;           /* on_block only: GS_WANT_T_COMPLETE | GS_WANT_HOPS; 0 = both       */
     gs_msg_summary* summary;
 } gs_result_sink;
 

@@ -305,30 +305,41 @@ int or_offline(const or_params* p, uint32_t u, uint64_t h) {
     return 0;
 }
 
+/* Mesh epoch workspace. nt > 1: the per-peer loops of mesh_epoch run on nt
+ * OpenMP threads (every loop body writes only its own row's entries, and the
+ * accept bits of phase B go to acc[], which only phase C reads), with one
+ * selection buffer per thread; the result is the same as with nt = 1. */
 typedef struct {
-    uint32_t* until; uint8_t* prop; uint64_t* rev; sel_t* sel; uint64_t bo;
+    uint32_t* until; uint8_t* prop; uint8_t* acc; uint64_t* rev; sel_t* sel; uint64_t bo; uint32_t nt, sel_n;
 } mesh_ws;
 
-static void mesh_ws_free(mesh_ws* w) { free(w->until); free(w->prop); free(w->rev); free(w->sel); }
+static void mesh_ws_free(mesh_ws* w) { free(w->until); free(w->prop); free(w->acc); free(w->rev); free(w->sel); }
 
-static int mesh_ws_init(const or_params* p, const uint64_t* row_ptr, const uint32_t* col, uint8_t* flags,
-                        mesh_ws* w) {
+static int mesh_ws_init_nt(const or_params* p, const uint64_t* row_ptr, const uint32_t* col, uint8_t* flags,
+                           mesh_ws* w, uint32_t nt) {
     uint32_t N = p->peers;
     uint64_t nnz = row_ptr[N];
+    w->nt = nt ? nt : 1;
     w->bo = (p->backoff_ns + p->heartbeat_ns - 1) / p->heartbeat_ns;
     w->until = (uint32_t*)calloc(nnz ? nnz : 1, sizeof(uint32_t));
-    w->prop = (uint8_t*)calloc(nnz ? nnz : 1, 1); /* 1 graft, 2 prune, 4 accepted */
+    w->prop = (uint8_t*)calloc(nnz ? nnz : 1, 1); /* 1 graft, 2 prune */
+    w->acc = (uint8_t*)calloc(nnz ? nnz : 1, 1);  /* 1 accepted (phase B -> C) */
     w->rev = (uint64_t*)malloc(sizeof(uint64_t) * (nnz ? nnz : 1));
     uint32_t maxdeg = 0;
     for (uint32_t u = 0; u < N; u++) {
         uint32_t dg = (uint32_t)(row_ptr[u + 1] - row_ptr[u]); if (dg > maxdeg) maxdeg = dg;
     }
-    w->sel = (sel_t*)malloc(sizeof(sel_t) * (maxdeg + 1));
-    if (!w->until || !w->prop || !w->rev || !w->sel) { mesh_ws_free(w); return -2; }
+    w->sel_n = maxdeg + 1;
+    w->sel = (sel_t*)malloc(sizeof(sel_t) * w->sel_n * w->nt);
+    if (!w->until || !w->prop || !w->acc || !w->rev || !w->sel) { mesh_ws_free(w); return -2; }
     for (uint32_t u = 0; u < N; u++)
         for (uint64_t e = row_ptr[u]; e < row_ptr[u + 1]; e++) w->rev[e] = find_entry(row_ptr, col, col[e], u);
     for (uint64_t e = 0; e < nnz; e++) flags[e] &= (uint8_t)~BIT_MESH;
     return 0;
+}
+static int mesh_ws_init(const or_params* p, const uint64_t* row_ptr, const uint32_t* col, uint8_t* flags,
+                        mesh_ws* w) {
+    return mesh_ws_init_nt(p, row_ptr, col, flags, w, 1);
 }
 
 /* Handshake model of the subscription exchange: every peer
@@ -357,16 +368,22 @@ static uint64_t mesh_epoch(const or_params* p, const uint64_t* row_ptr, const ui
                            mesh_ws* ws, uint32_t epoch, const uint8_t* off, int sub) {
     uint32_t N = p->peers;
     uint64_t nnz = row_ptr[N], changes = 0;
-    uint32_t* until = ws->until; uint8_t* prop = ws->prop; const uint64_t* rev = ws->rev; sel_t* sel = ws->sel;
+    uint32_t* until = ws->until; uint8_t* prop = ws->prop; uint8_t* acc = ws->acc; const uint64_t* rev = ws->rev;
     const uint32_t bo = (uint32_t)ws->bo;
+    const int nt = (int)ws->nt;
     memset(prop, 0, nnz);
+    memset(acc, 0, nnz);
     /* ---- 0: links to offline peers leave the mesh (disconnect: no back-off) ---- */
-    if (off)
+    if (off) {
+#pragma omp parallel for num_threads(nt) if (nt > 1) schedule(static, 1024)
         for (uint32_t u = 0; u < N; u++)
             for (uint64_t e = row_ptr[u]; e < row_ptr[u + 1]; e++)
                 if (off[u] || off[col[e]]) flags[e] &= (uint8_t)~BIT_MESH;
+    }
     /* ---- A0: subscription-time grafts (epoch 0 only) ---- */
-    for (uint32_t u = 0; sub && u < N; u++) {
+#pragma omp parallel for num_threads(nt) if (nt > 1) schedule(static, 1024)
+    for (uint32_t u = 0; u < (sub ? N : 0); u++) {
+        sel_t* sel = ws->sel + (size_t)omp_get_thread_num() * ws->sel_n;
         uint64_t b = row_ptr[u], en = row_ptr[u + 1];
         uint32_t nc = 0;
         for (uint64_t e = b; e < en; e++)
@@ -380,7 +397,9 @@ static uint64_t mesh_epoch(const or_params* p, const uint64_t* row_ptr, const ui
         for (uint32_t q = 0; q < want; q++) prop[sel[q].e] |= 1;
     }
     /* ---- A: heartbeat decisions ---- */
-    for (uint32_t u = 0; !sub && u < N; u++) {
+#pragma omp parallel for num_threads(nt) if (nt > 1) schedule(static, 1024)
+    for (uint32_t u = 0; u < (sub ? 0 : N); u++) {
+        sel_t* sel = ws->sel + (size_t)omp_get_thread_num() * ws->sel_n;
         if (off && off[u]) continue;
         uint64_t b = row_ptr[u], en = row_ptr[u + 1];
         uint32_t m = 0, o = 0;
@@ -423,7 +442,9 @@ static uint64_t mesh_epoch(const or_params* p, const uint64_t* row_ptr, const ui
         }
     }
     /* ---- B: receivers handle GRAFTs ---- */
+#pragma omp parallel for num_threads(nt) if (nt > 1) schedule(static, 1024)
     for (uint32_t w = 0; w < N; w++) {
+        sel_t* sel = ws->sel + (size_t)omp_get_thread_num() * ws->sel_n;
         uint64_t b = row_ptr[w], en = row_ptr[w + 1];
         uint32_t c = 0, nin = 0;
         for (uint64_t e = b; e < en; e++)
@@ -443,19 +464,20 @@ static uint64_t mesh_epoch(const or_params* p, const uint64_t* row_ptr, const ui
         for (uint32_t q = 0; q < nin; q++) {
             uint64_t e = sel[q].e;               /* entry (w -> u) */
             int in_mesh = ((flags[e] & BIT_MESH) && !(prop[e] & 2)) || (prop[e] & 1);
-            if (in_mesh) { prop[rev[e]] |= 4; continue; }
+            if (in_mesh) { acc[rev[e]] = 1; continue; }
             if (epoch < until[e]) { until[e] = epoch + bo; continue; }
             if (c >= p->d_hi && !(flags[e] & BIT_OUT)) { until[e] = epoch + bo; continue; }
-            prop[rev[e]] |= 4; flags[e] |= BIT_MESH; c++;
+            acc[rev[e]] = 1; flags[e] |= BIT_MESH; c++;
         }
     }
     /* ---- C: apply prunes and rejections ---- */
+#pragma omp parallel for num_threads(nt) if (nt > 1) schedule(static, 1024) reduction(+ : changes)
     for (uint32_t u = 0; u < N; u++) {
         for (uint64_t e = row_ptr[u]; e < row_ptr[u + 1]; e++) {
             uint8_t pr = prop[e];
             if (pr & 1) {
                 changes++;
-                if (pr & 4) flags[e] |= BIT_MESH;
+                if (acc[e]) flags[e] |= BIT_MESH;
                 else { flags[e] &= (uint8_t)~BIT_MESH; until[e] = epoch + bo; }
             }
             if (pr & 2) { changes++; flags[e] &= (uint8_t)~BIT_MESH; until[e] = epoch + bo; }
@@ -554,6 +576,43 @@ int or_mesh_churn(const or_params* p, const uint64_t* row_ptr, const uint32_t* c
             size_t o = (size_t)(h - h_lo);
             rc = mesh_extract(p, row_ptr, col, flags, snap_mesh + o * N * MESH_W, snap_cnt + o * N);
             memcpy(snap_off + o * N, off, N);
+        }
+    }
+    mesh_ws_free(&ws);
+    free(flags); free(off);
+    return rc;
+}
+
+/* The same replay as or_mesh_churn, keeping only the epochs h <= h_hi with
+ * keep[h] != 0 (in ascending order, slot = rank among the kept), on `threads`
+ * OpenMP threads (0/1 = single-threaded; identical results). Test-side helper
+ * for sampling messages spread over a long schedule (tests/test_gpu_configs.py). */
+int or_mesh_churn_sel(const or_params* p, const uint64_t* row_ptr, const uint32_t* col, const uint8_t* flags_in,
+                      const uint8_t* stage, uint32_t S, const uint64_t* lat_ns, uint32_t h_hi, const uint8_t* keep,
+                      int threads, uint32_t* snap_mesh, uint8_t* snap_cnt, uint8_t* snap_off) {
+    uint32_t N = p->peers;
+    uint64_t nnz = row_ptr[N];
+    const int nt = threads > 1 ? threads : 1;
+    uint8_t* flags = (uint8_t*)malloc(nnz ? nnz : 1);
+    uint8_t* off = (uint8_t*)calloc(N ? N : 1, 1);
+    if (!flags || !off) { free(flags); free(off); return -2; }
+    memcpy(flags, flags_in, nnz);
+    mesh_ws ws;
+    if (mesh_ws_init_nt(p, row_ptr, col, flags, &ws, (uint32_t)nt)) { free(flags); free(off); return -2; }
+    int rc = 0;
+    size_t o = 0;
+    for (uint32_t h = 0; h <= h_hi && !rc; h++) {
+        if (h > 0) {
+#pragma omp parallel for num_threads(nt) if (nt > 1) schedule(static, 4096)
+            for (uint32_t u = 0; u < N; u++) off[u] = (uint8_t)or_offline(p, u, h);
+            mesh_epoch(p, row_ptr, col, flags, stage, S, lat_ns, &ws, h, off, 0);
+        } else if (p->sub_graft) {
+            mesh_epoch(p, row_ptr, col, flags, stage, S, lat_ns, &ws, 0, NULL, 1);
+        }
+        if (keep[h]) {
+            rc = mesh_extract(p, row_ptr, col, flags, snap_mesh + o * N * MESH_W, snap_cnt + o * N);
+            memcpy(snap_off + o * N, off, N);
+            o++;
         }
     }
     mesh_ws_free(&ws);

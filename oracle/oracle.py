@@ -79,6 +79,8 @@ def lib():
         L.or_run_mt.argtypes = L.or_run.argtypes + [ctypes.c_int]
         L.or_mesh_churn.argtypes = [P(OrParams), P(u64), P(u32), P(u8), P(u8), u32, P(u64), u32, u32,
                                     P(u32), P(u8), P(u8)]
+        L.or_mesh_churn_sel.argtypes = [P(OrParams), P(u64), P(u32), P(u8), P(u8), u32, P(u64), u32, P(u8),
+                                        ctypes.c_int, P(u32), P(u8), P(u8)]
         L.or_run_churn.argtypes = [P(OrParams), P(u64), P(u32), P(u32), P(u8), P(u8), u32, u32, P(u8), u32,
                                    P(u64), P(u64), P(u64), P(u64), P(u32), P(u32), P(u32), u64, P(u64), P(u8),
                                    P(OrStats)]
@@ -204,6 +206,39 @@ def mesh_churn(p, row_ptr, col, flags, stage, lat, h_lo, h_hi):
     if rc:
         raise ValueError("or_mesh_churn rc=%d" % rc)
     return mesh.reshape(E, N, MESH_W), cnt.reshape(E, N), off.reshape(E, N)
+
+
+def mesh_churn_ranges(p, row_ptr, col, flags, stage, lat, ranges, threads=0):
+    """One churn replay from epoch 0 (or_mesh_churn_sel, OpenMP over peers when
+    threads > 1), keeping only the epochs of `ranges` [(h_lo, h_hi), ...]:
+    returns {(h_lo, h_hi): (mesh [E, N, 16], cnt [E, N], offline [E, N])}, the
+    snapshot tuples mesh_churn would return for each range."""
+    N = p.peers
+    h_top = max(hi for _, hi in ranges)
+    keep = np.zeros(h_top + 1, np.uint8)
+    for lo, hi in ranges:
+        keep[lo:hi + 1] = 1
+    K = int(keep.sum())
+    mesh = np.zeros(K * N * MESH_W, np.uint32)
+    cnt = np.zeros(K * N, np.uint8)
+    off = np.zeros(K * N, np.uint8)
+    S = lat.shape[0]
+    lat = np.ascontiguousarray(lat.reshape(-1), np.uint64)
+    stage = np.ascontiguousarray(stage, np.uint8)
+    flags = np.ascontiguousarray(flags, np.uint8)
+    rc = lib().or_mesh_churn_sel(ctypes.byref(p), _p(row_ptr, ctypes.c_uint64), _p(col, ctypes.c_uint32),
+                                 _p(flags, ctypes.c_uint8), _p(stage, ctypes.c_uint8), S, _p(lat, ctypes.c_uint64),
+                                 h_top, _p(keep, ctypes.c_uint8), int(threads), _p(mesh, ctypes.c_uint32),
+                                 _p(cnt, ctypes.c_uint8), _p(off, ctypes.c_uint8))
+    if rc:
+        raise ValueError("or_mesh_churn_sel rc=%d" % rc)
+    slot = np.cumsum(keep) - 1  # epoch -> kept slot
+    mesh, cnt, off = mesh.reshape(K, N, MESH_W), cnt.reshape(K, N), off.reshape(K, N)
+    out = {}
+    for lo, hi in ranges:
+        a, b = int(slot[lo]), int(slot[hi]) + 1
+        out[(lo, hi)] = (mesh[a:b], cnt[a:b], off[a:b])
+    return out
 
 
 def _frags_ptr(sched_frags, M):

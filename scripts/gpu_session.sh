@@ -22,7 +22,8 @@ PROFARGS="--steps ${PROF_STEPS:-6} --warmup 2 --cpu-seconds 0 --also-peers 0 --c
 KRE="k_lpull|k_pull|k_scan|k_frontier|k_complete|k_lcomplete"
 for s in ${STEPS:-tests smoke bench prof}; do
   case $s in
-    tests) step gpu_tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    tests) step gpu_tests ${TESTS_SECS:-1200} python -u -m pytest tests -m gpu ${TEST_ARGS:--x} -v --timeout 300 --timeout-method thread ;;
+    probe) step rccl_probe 300 ./scripts/bin/rccl_p2p_probe ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --steps ${BENCH_STEPS:-20} --warmup 3 ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py $PROFARGS ;;

@@ -118,6 +118,97 @@ def test_config3_100k_hetero_gossip_churn():
     np.testing.assert_array_equal(r2["hops"], hp[600:700])
 
 
+def _oracle_churn_sample(p, sim, S, links, sched, idx, threads=8):
+    """The oracle on sampled messages of a churn run, on the GPU's graph: one
+    churn replay from epoch 0 keeping only the epochs the sample needs
+    (oracle.mesh_churn_ranges), then oracle.run_churn per group of messages
+    whose lifetimes overlap, groups on parallel host threads."""
+    from concurrent.futures import ThreadPoolExecutor
+    row, col, flags = sim.csr()
+    lat, bw, stage = _links(p, S, links)
+    t, pub, size = _sub(sched, idx)
+    ep = np.array([oracle.epoch_at(p, x) for x in t])
+    groups = []  # (h_lo, h_hi, positions in idx)
+    for k in np.argsort(ep, kind="stable"):
+        lo, hi = int(ep[k]), int(ep[k]) + p.churn_horizon
+        if groups and lo <= groups[-1][1]:
+            groups[-1][1] = max(groups[-1][1], hi)
+            groups[-1][2].append(k)
+        else:
+            groups.append([lo, hi, [k]])
+    snaps = oracle.mesh_churn_ranges(p, row, col, (flags & 1).astype(np.uint8), stage, lat,
+                                     [(g[0], g[1]) for g in groups], threads=threads)
+
+    def one(g):
+        ks = np.array(g[2])
+        return ks, oracle.run_churn(p, row, col, snaps[(g[0], g[1])], g[0], stage, lat, bw, bw,
+                                    t[ks], pub[ks], size[ks])
+
+    otc = np.zeros((len(idx), p.peers), np.uint64)
+    ohp = np.zeros((len(idx), p.peers), np.uint8)
+    with ThreadPoolExecutor(max_workers=threads) as ex:
+        for ks, (tc, hp, _) in ex.map(one, groups):
+            otc[ks], ohp[ks] = tc, hp
+    return otc, ohp
+
+
+@pytest.mark.timeout(900)
+def test_config3_bench_shape_batch1024_spread_sample():
+    """Config #3 at the shape bench.py times it (configs_1gpu.c3_100k_gossip_churn:
+    100k peers, 5-stage topogen links, lazy gossip, 1 % churn, the messages in
+    ONE batch of up to 1024): 18 messages spread over all 1000 (6 of them at
+    index >= 600, incl. the last two) bit-exact against the oracle, which
+    replays churn from epoch 0 on the GPU's graph."""
+    N, M, S = 100_000, 1000, 5
+    hb = 1_000_000_000
+    p = oracle.params(peers=N, seed=3, lazy_gossip=1, churn_ppm=10_000, churn_down=10, churn_horizon=16,
+                      heartbeat_ns=hb, hb_phase_ns=T0 - 20 * hb + 370_000_000)
+    sched = _sched(M, N)
+    sim = _sim(p, S, LINKS, batch=1024)
+    res = sim.run(sched)
+    st = sim.stats()
+    assert st["batches"] == 1 and st["gossip_iwant"] > 0
+    assert 0.5 * M * (N - 1) < st["deliveries"] < M * (N - 1)
+    idx = np.array([0, 1, 57, 130, 131, 250, 333, 402, 499, 555, 600, 601, 689, 777, 850, 912, 998, 999])
+    assert len(idx) >= 16 and (idx >= 600).sum() >= 4
+    otc, ohp = _oracle_churn_sample(p, sim, S, LINKS, sched, idx)
+    np.testing.assert_array_equal(res["t_complete"][idx], otc)
+    np.testing.assert_array_equal(res["hops"][idx], ohp)
+
+
+@pytest.mark.timeout(900)
+def test_config4_1m_peers_c_abi_p8_loopback():
+    """Config #4's split through the C ABI: gs_run_partitioned over
+    gs_comm_init_local(8) (eight parts of 125k peers on this GPU, records
+    routed per bucket to the parts owning a target) at 1M peers == gs_run on
+    one context == the oracle on 4 of the 8 messages."""
+    N, S, M = 1_000_000, 5, 8
+    p = oracle.params(peers=N, seed=41)
+    sched = _sched(M, N)
+    whole = _sim(p, S, LINKS, batch=M)
+    ref = whole.run(sched)
+    assert whole.stats()["deliveries"] == M * (N - 1)
+    row, col, _ = whole.csr()
+    mesh, cnt = whole.mesh()
+    whole.close()
+    sims = [_sim(p, S, LINKS, batch=M) for _ in range(8)]
+    for i, s in enumerate(sims):
+        s.set_partition(8, i)
+    comm = gossipsim.Comm(local_parts=8)
+    res = comm.run_partitioned(sims, sched)
+    np.testing.assert_array_equal(np.concatenate([r["t_complete"] for r in res], axis=1), ref["t_complete"])
+    np.testing.assert_array_equal(np.concatenate([r["hops"] for r in res], axis=1), ref["hops"])
+    assert sum(s.stats()["deliveries"] for s in sims) == M * (N - 1)
+    comm.close()
+    for s in sims:
+        s.close()
+    lat, bw, stage = _links(p, S, LINKS)
+    idx = np.array([0, 2, 5, 7])
+    otc, ohp, _ = oracle.run(p, row, col, mesh, cnt, stage, lat, bw, bw, *_sub(sched, idx), threads=4)
+    np.testing.assert_array_equal(ref["t_complete"][idx], otc)
+    np.testing.assert_array_equal(ref["hops"][idx], ohp)
+
+
 def test_config4_1m_peers_peer_partitioned():
     """Config #4 at 1M peers: peers partitioned over 2 contexts exchanging each
     window's records (loop-back all-gather, the same protocol as RCCL across

@@ -143,3 +143,38 @@ def test_streaming_sink_and_log(tmp_path):
     a = sorted(open(str(tmp_path / "grouped")).read().splitlines())
     b = sorted(open(str(tmp_path / "stream")).read().splitlines())
     assert a == b and len(a) == M * (N - 1)
+
+
+def test_streaming_sink_want_bits():
+    """ABI 7: an on_block sink selects its outputs with gs_result_sink.want
+    (GS_WANT_T_COMPLETE / GS_WANT_HOPS); array pointers set together with
+    on_block (the ABI-6 flag convention) are refused with GS_EINVAL."""
+    import ctypes
+    N, M = 1500, 12
+    p = oracle.params(peers=N, seed=97)
+    sched = _sched(M, N)
+    sim, _ = gpu_sim(p, 5, (50, 150, 40, 130), batch=16)
+    whole = sim.run(sched)
+    for want, has_tc, has_hp in ((gossipsim.WANT_T_COMPLETE, True, False), (gossipsim.WANT_HOPS, False, True),
+                                 (0, True, True)):
+        got = []
+
+        def blk(first, tc, hp):
+            got.append((first, None if tc is None else tc.copy(), None if hp is None else hp.copy()))
+
+        sim.run(sched, on_block=blk, block_msgs=5, want=want)
+        assert [g[0] for g in got] == [0, 5, 10]
+        for first, tc, hp in got:
+            assert (tc is not None) == has_tc and (hp is not None) == has_hp
+            if has_tc:
+                np.testing.assert_array_equal(tc, whole["t_complete"][first:first + tc.shape[0]])
+            if has_hp:
+                np.testing.assert_array_equal(hp, whole["hops"][first:first + hp.shape[0]])
+    lib = gossipsim.lib()
+    cb = gossipsim.BLOCK_FN(lambda *a: None)
+    flag = np.zeros(1, np.uint64)
+    sink = gossipsim.GsResultSink()
+    sink.t_complete_ns = flag.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+    sink.on_block = cb
+    rc = lib.gs_run(sim.ctx, sim._schedule(sched), M, ctypes.byref(sink))
+    assert rc == gossipsim.GS_EINVAL and b"want" in lib.gs_last_error(sim.ctx)

@@ -372,6 +372,30 @@ def test_pull_list_overflow_reruns_on_dense_rows(monkeypatch):
     compare(p, 5, (50, 150, 40, 130), _sched(256, 2500), batch=256)
 
 
+def test_pull_list_overflow_counts_past_stride(monkeypatch):
+    """Capacity 1 with 1024-lane rows and publishers up to the last peer: list
+    lengths run far past the capacity (and can pass the list stride); the pass
+    reads only the entries that were written (no read past the row's list or
+    the last slot), flags the overflow and the batch re-runs on k_pull."""
+    monkeypatch.setenv("GS_LPULL_CAP", "1")
+    N = 1200
+    p = oracle.params(peers=N, seed=35, lazy_gossip=0)
+    t, _, size = _sched(1024, N)
+    pub = (N - 1 - np.arange(1024) % 7).astype(np.int64)  # 7 publishers at the top of the id range
+    sim, _ = compare(p, 5, (50, 150, 40, 130), (t, pub, size), batch=1024)
+    assert sim.stats()["list_pull_batches"] == 0  # every batch went to k_pull
+
+
+def test_pull_ring_violation_reruns_on_dense_rows(monkeypatch):
+    """A ring of K = 2 destination windows (GS_LPULL_K), below the host bound:
+    candidates land beyond the ring, the pass flags ERR_RING (not the
+    time-overflow error) and the batch re-runs on k_pull, bit-exact."""
+    monkeypatch.setenv("GS_LPULL_K", "2")
+    p = oracle.params(peers=1500, seed=36, lazy_gossip=0)
+    sim, _ = compare(p, 5, (50, 150, 40, 130), _sched(128, 1500), batch=128)
+    assert sim.stats()["list_pull_batches"] == 0
+
+
 @pytest.mark.parametrize("frags,gossip,fast,idw", [(1, 0, 0, 0), (2, 0, 0, 0), (1, 1, 0, 0), (1, 0, 1, 0),
                                                    (1, 1, 1, 0), (2, 1, 1, 0), (1, 0, 1, 1)])
 def test_churn_time_varying_mesh(frags, gossip, fast, idw):

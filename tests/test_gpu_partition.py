@@ -147,6 +147,27 @@ def test_run_partitioned_rccl_single_rank(N, M):
     comm.close()
 
 
+@pytest.mark.parametrize("piece", [1 << 20, (1 << 22) + 24 * 7])
+def test_run_partitioned_rccl_many_pieces(monkeypatch, piece):
+    """The RCCL record exchange cut into many ncclSend / ncclRecv pieces
+    (GS_RCCL_PIECE_BYTES; 2^30 B by default): every bucket's
+    transfer of a 100k-peer, 64-message batch spans several pieces, incl. a
+    piece size that is not a multiple of the 24-B record; bit-identical to
+    gs_run."""
+    monkeypatch.setenv("GS_RCCL_PIECE_BYTES", str(piece))
+    N, M = 100_000, 64
+    p = oracle.params(peers=N, seed=61)
+    sched = _sched(M, N)
+    ref, rst = _whole(p, 5, (50, 150, 40, 130), sched, M)
+    (s,) = _parts(p, 5, (50, 150, 40, 130), 1, M)
+    comm = gossipsim.Comm(nranks=1, rank=0, uid=gossipsim.Comm.get_id(), device=0)
+    (r,) = comm.run_partitioned([s], sched)
+    np.testing.assert_array_equal(r["t_complete"], ref["t_complete"])
+    np.testing.assert_array_equal(r["hops"], ref["hops"])
+    assert s.stats()["relaxations"] == rst["relaxations"]
+    comm.close()
+
+
 def test_run_partitioned_refuses_gossip_that_matters():
     p = oracle.params(peers=600, seed=60, hb_phase_ns=T0 % 1_000_000_000)  # heartbeat at the publish
     sims = _parts(p, 1, (50, 50, 50, 50), 2, 4)

@@ -37,6 +37,38 @@ def test_library_exports_every_declared_symbol():
     assert set(syms) == set(gossipsim.SIGNATURES)
 
 
+def test_abi_struct_layouts_match_header(tmp_path):
+    """The ctypes mirror of the ABI structs (gossipsim.py) has the layout the
+    header gives a C compiler: sizes and every field offset of gs_result_sink
+    (incl. ABI 7's `want`), gs_config, gs_publish, gs_stats, gs_msg_summary;
+    GS_ABI_VERSION and the GS_WANT_* bits."""
+    import ctypes
+    import subprocess
+    structs = {"gs_result_sink": gossipsim.GsResultSink, "gs_config": gossipsim.GsConfig,
+               "gs_publish": gossipsim.GsPublish, "gs_stats": gossipsim.GsStats,
+               "gs_msg_summary": gossipsim.GsMsgSummary}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "gossipsim.h"', "int main(void) {",
+             '  printf("abi %u\\n", GS_ABI_VERSION);',
+             '  printf("want %u,%u\\n", (unsigned)GS_WANT_T_COMPLETE, (unsigned)GS_WANT_HOPS);']
+    for name, cls in structs.items():
+        lines.append('  printf("%s size %%zu\\n", sizeof(%s));' % (name, name))
+        for f, _ in cls._fields_:
+            lines.append('  printf("%s.%s %%zu\\n", offsetof(%s, %s));' % (name, f, name, f))
+    lines.append("  return 0;\n}")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-std=c11", "-I", os.path.dirname(HEADER), "-o", str(exe), str(src)])
+    got = dict(l.rsplit(" ", 1) for l in subprocess.check_output([str(exe)]).decode().splitlines())
+    assert int(got["abi"]) == gossipsim.ABI_VERSION == 7
+    assert got["want"] == "%d,%d" % (gossipsim.WANT_T_COMPLETE, gossipsim.WANT_HOPS)
+    for name, cls in structs.items():
+        assert int(got["%s size" % name]) == ctypes.sizeof(cls), name
+        for f, _ in cls._fields_:
+            assert int(got["%s.%s" % (name, f)]) == getattr(cls, f).offset, (name, f)
+    assert "want" in [f for f, _ in gossipsim.GsResultSink._fields_]
+
+
 def test_no_gpu_means_loud_failure():
     """Without a device the product raises; there is no CPU fallback path."""
     try:
