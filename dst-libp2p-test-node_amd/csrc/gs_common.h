@@ -26,7 +26,7 @@ constexpr uint32_t STAGE_SHIFT = 24;  // packed mesh entry: stage << 24 | peer
 // Subscription exchange: a connection completes HS_RTTS round
 // trips after the common dial instant (TCP + multistream + Noise XX + yamux, a
 // model constant); w's subscription then reaches u one lat(w->u) later.
-constexpr uint32_t HS_RTTS = 3;
+constexpr uint32_t HS_RTTS = 3;  // default of gs_config.hs_rtts
 
 enum : uint32_t { P_DIAL = 1, P_DIAL_ORDER = 2, P_GRAFT = 3, P_PRUNE = 4, P_OUT_GRAFT = 5, P_GOSSIP = 6, P_CHURN = 7,
                   P_MSGID = 8 };

@@ -45,6 +45,7 @@ extern "C" void gs_config_default(gs_config* c) {
   c->churn_horizon = 16;
   c->node = GS_NODE_RUST;
   c->sub_graft = 1;               // handle_received_subscriptions grafts during the 20 s pump (main.rs:357-379)
+  c->hs_rtts = gs::HS_RTTS;       // model constant (sensitivity table §3)
 }
 
 extern "C" gs_status gs_config_preset(gs_config* c, uint32_t node) {
@@ -136,6 +137,7 @@ extern "C" gs_status gs_config_from_env(gs_config* c, char* err, size_t err_len)
   if (env_u64("GS_HB_PHASE_NS", &x, err, err_len, &bad)) c->hb_phase_ns = x;
   if (env_u64("GS_LAZY_GOSSIP", &x, err, err_len, &bad)) c->lazy_gossip = x ? 1 : 0;
   if (env_u64("GS_SUB_GRAFT", &x, err, err_len, &bad)) c->sub_graft = x ? 1 : 0;
+  if (env_u64("GS_HS_RTTS", &x, err, err_len, &bad)) c->hs_rtts = (uint32_t)x;
   const char* gf = getenv("GOSSIPSUB_GOSSIP_FACTOR");
   if (gf && *gf) {
     char* end = nullptr;

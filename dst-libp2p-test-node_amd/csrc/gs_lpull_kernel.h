@@ -73,9 +73,19 @@ __device__ __forceinline__ uint32_t lp_rof(uint32_t hx, const uint32_t (&thr)[LP
   return r;  // r == K: beyond the ring (an error the host bound rules out)
 }
 
-template <int FP>
-__global__ __launch_bounds__(TB, 4) void k_lpull(LPullArgs a) {
-  __shared__ PullLds Ls;  // 40 KB: 4 blocks (16 waves) per CU, as k_pull
+// LDS of the pass per wave: CW = the row's candidate minima (CH 64-lane
+// chunks), LST = compacted lane / group indices. CH = 16: 10 KB per wave, 4
+// blocks (16 waves) per CU; CH = 8 (rows of <= 512 lanes): 5 KB, 8 blocks.
+template <uint32_t CH>
+struct LPullLds {
+  uint64_t cw[PULL_WAVES][CH * 64];
+  uint16_t lst[PULL_WAVES][CH * 64];
+};
+
+template <int FP, uint32_t CH>
+__global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
+  constexpr uint32_t LMAX = CH * 64;
+  __shared__ LPullLds<CH> Ls;
   // ---- decide this pass from the previous slot (grid-uniform; k_pull's rule) ----
   const uint64_t* pv = a.ctrl + ((a.pass + 2) % 3) * 4;
   uint64_t lo, mode;
@@ -132,7 +142,7 @@ __global__ __launch_bounds__(TB, 4) void k_lpull(LPullArgs a) {
 #endif
 
 #pragma unroll
-  for (int q = 0; q < (int)PULL_CH; q++) CW[q * 64 + lane] = INF64;
+  for (int q = 0; q < (int)CH; q++) CW[q * 64 + lane] = INF64;
   wave_lds_sync();
 
   const uint32_t stride = gridDim.x * PULL_WAVES;
@@ -262,7 +272,7 @@ __global__ __launch_bounds__(TB, 4) void k_lpull(LPullArgs a) {
     const uint32_t log0 = __builtin_amdgcn_readlane(sv, LP_LOG);
     uint32_t logc = log0, cnt = 0, npend = 0, nfin = 0;  // the finals are logged in step 4
 #pragma unroll
-    for (int q = 0; q < (int)PULL_CH; q++) {
+    for (int q = 0; q < (int)CH; q++) {
       if (!((cb >> q) & 1u)) continue;  // wave-uniform
       const uint32_t i = q * 64 + lane;
       uint64_t x = CW[i];
@@ -273,7 +283,7 @@ __global__ __launch_bounds__(TB, 4) void k_lpull(LPullArgs a) {
       const bool act = x != INF64 && ((uint32_t)(x >> 32) - hlo) < hspan;
       const bool pend = x != INF64 && !act;
       const uint64_t pm = __ballot(pend);
-      if (pend) LST[PULL_LMAX - 1 - (npend + (uint32_t)__popcll(pm & lanelt))] = (uint16_t)i;
+      if (pend) LST[LMAX - 1 - (npend + (uint32_t)__popcll(pm & lanelt))] = (uint16_t)i;
       npend += (uint32_t)__popcll(pm);
       const uint64_t am = __ballot(act);
       if (am) {  // wave-uniform
@@ -311,7 +321,7 @@ __global__ __launch_bounds__(TB, 4) void k_lpull(LPullArgs a) {
       const uint32_t lmax = a.lcap;
       for (uint32_t j0 = 0; j0 < npend; j0 += 64) {
         const bool jv = j0 + lane < npend;
-        const uint32_t li = jv ? LST[PULL_LMAX - 1 - (j0 + lane)] : 0u;
+        const uint32_t li = jv ? LST[LMAX - 1 - (j0 + lane)] : 0u;
         const uint64_t x = jv ? CW[li] : INF64;
         const uint32_t r = jv ? lp_rof((uint32_t)(x >> 32), thr, K) : 0u;
         if (jv && r >= K) err |= ERR_RING;
@@ -401,7 +411,7 @@ __global__ __launch_bounds__(TB, 4) void k_lpull(LPullArgs a) {
     nrec += ecnt;
     // 6. LDS back to INF for the next row: the touched chunks
 #pragma unroll
-    for (int q = 0; q < (int)PULL_CH; q++)
+    for (int q = 0; q < (int)CH; q++)
       if ((cb >> q) & 1u) CW[q * 64 + lane] = INF64;
     wave_lds_sync();
     ej = ej2; rj = rj2; cj = cj2; sv = sv2;
@@ -580,12 +590,29 @@ __global__ __launch_bounds__(LC_WAVES * 64) void k_lcomplete(LPullArgs a, uint64
   }
 }
 
+// Chunks per row of the pass: 8 when a row has <= 512 lanes (half the LDS,
+// twice the resident waves), else 16. GS_LPULL_CH=16 forces the wide form.
+uint32_t lpull_chunks(uint32_t L) {
+  const char* e = getenv("GS_LPULL_CH");  // per launch: A/B scripts switch it in one process
+  return (L <= 512 && !(e && atoi(e) == 16)) ? 8u : 16u;
+}
+
 void lpull_dispatch(uint32_t FP, const LPullArgs& a, unsigned grid, hipStream_t s) {
+  if (lpull_chunks(a.L) == 8) {
+    switch (FP) {
+      case 1: k_lpull<1, 8><<<grid, TB, 0, s>>>(a); break;
+      case 2: k_lpull<2, 8><<<grid, TB, 0, s>>>(a); break;
+      case 4: k_lpull<4, 8><<<grid, TB, 0, s>>>(a); break;
+      case 8: k_lpull<8, 8><<<grid, TB, 0, s>>>(a); break;
+      default: k_lpull<16, 8><<<grid, TB, 0, s>>>(a); break;
+    }
+    return;
+  }
   switch (FP) {
-    case 1: k_lpull<1><<<grid, TB, 0, s>>>(a); break;
-    case 2: k_lpull<2><<<grid, TB, 0, s>>>(a); break;
-    case 4: k_lpull<4><<<grid, TB, 0, s>>>(a); break;
-    case 8: k_lpull<8><<<grid, TB, 0, s>>>(a); break;
-    default: k_lpull<16><<<grid, TB, 0, s>>>(a); break;
+    case 1: k_lpull<1, 16><<<grid, TB, 0, s>>>(a); break;
+    case 2: k_lpull<2, 16><<<grid, TB, 0, s>>>(a); break;
+    case 4: k_lpull<4, 16><<<grid, TB, 0, s>>>(a); break;
+    case 8: k_lpull<8, 16><<<grid, TB, 0, s>>>(a); break;
+    default: k_lpull<16, 16><<<grid, TB, 0, s>>>(a); break;
   }
 }

@@ -38,7 +38,7 @@ struct MeshArgs {
   uint64_t* counters;
   uint64_t seed;
   uint32_t N, S, epoch, bo, d, d_lo, d_hi, d_out;
-  uint32_t sub;  // the subscription epoch 0: handshake-ordered grafts
+  uint32_t sub;  // the subscription epoch 0: handshake-ordered grafts; = handshake RTTs (0: a heartbeat)
   // event-driven churn epochs (run_epochs): per-peer state planes, nullptr when
   // every row runs every step
   uint8_t* pst;              // [PS_PLANES][N]
@@ -180,7 +180,7 @@ __device__ __forceinline__ void row_heartbeat(const MeshArgs& a, uint32_t u) {
       if (k * G < (int)deg && (uint32_t)(k * G + lane) < deg && !(f[k] & F_MESH)) {
         const uint32_t sw = a.stage[w[k]];
         const uint64_t lwu = a.lat[sw * a.S + su];
-        key[k] = (uint64_t)HS_RTTS * (a.lat[su * a.S + sw] + lwu) + lwu;
+        key[k] = (uint64_t)a.sub * (a.lat[su * a.S + sw] + lwu) + lwu;
       }
     }
     for (uint32_t q = 0; q < a.d_lo; q++) {
@@ -323,7 +323,7 @@ __device__ __forceinline__ bool row_handle_graft(const MeshArgs& a, uint32_t w) 
       r[k] = a.rev[b + i];
       if (a.prop[r[k]] & PR_GRAFT) {  // arrival order: latency u->w (heartbeat), handshake (subscription)
         const uint32_t su = a.stage[a.col[b + i]];
-        lvl[k] = a.sub ? (uint64_t)(HS_RTTS + 1) * (a.lat[su * a.S + sw] + a.lat[sw * a.S + su])
+        lvl[k] = a.sub ? (uint64_t)(a.sub + 1) * (a.lat[su * a.S + sw] + a.lat[sw * a.S + su])
                        : a.lat[su * a.S + sw];
       }
     }
@@ -781,7 +781,7 @@ void sub_epoch(Ctx& c, MeshArgs a) {
   if (!c.cfg.sub_graft) return;
   const uint32_t N = c.cfg.peers;
   hipStream_t s = c.stream;
-  a.sub = 1;
+  a.sub = c.cfg.hs_rtts ? c.cfg.hs_rtts : HS_RTTS;
   a.epoch = 0;
   a.off = nullptr;
   GS_HIP(hipMemsetAsync(c.d_prop.p, 0, c.nnz ? c.nnz : 1, s));

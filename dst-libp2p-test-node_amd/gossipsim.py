@@ -45,7 +45,7 @@ class GsConfig(ctypes.Structure):
         ("heartbeat_ns", u64), ("backoff_ns", u64)] + [
         (n, u32) for n in ("flood_publish", "idontwant", "lazy_gossip", "self_log")] + [
         ("seed", u64), ("device", i32), ("batch", u32), ("history_gossip", u32), ("hb_phase_ns", u64)] + [
-        (n, u32) for n in ("churn_ppm", "churn_down", "churn_horizon", "node", "sub_graft")]
+        (n, u32) for n in ("churn_ppm", "churn_down", "churn_horizon", "node", "sub_graft", "hs_rtts")]
 
 
 class GsPublish(ctypes.Structure):

@@ -105,6 +105,10 @@ typedef struct gs_config {
      * heartbeat 1 every peer grafts its first D_lo connections in handshake
      * order. 1 in the rust preset. */
     uint32_t sub_graft;
+    /* round trips from the common dial instant until a connection carries its
+     * first subscription (TCP + multistream + Noise XX + yamux; a model
+     * constant of the subscription epoch); 0 = 3 (default) */
+    uint32_t hs_rtts;
 } gs_config;
 
 /* One publish injection (replaces POST /publish, main.rs:50-56,152-168; the

@@ -348,7 +348,8 @@ static int mesh_ws_init(const or_params* p, const uint64_t* row_ptr, const uint3
  * later (TCP + multistream + Noise XX + yamux, a model constant) and each side
  * then sends its subscription, so w's subscription reaches u at
  * HS_RTTS*rtt(u,w) + lat(w->u), and u's GRAFT reaches w one lat(u->w) later. */
-#define HS_RTTS 3u
+#define HS_RTTS_DEFAULT 3u
+#define HS_RTTS (p->hs_rtts ? p->hs_rtts : HS_RTTS_DEFAULT)
 static uint64_t rtt_of(const uint64_t* lat_ns, uint32_t S, uint32_t su, uint32_t sw) {
     return lat_ns[su * S + sw] + lat_ns[sw * S + su];
 }

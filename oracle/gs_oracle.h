@@ -32,6 +32,7 @@ typedef struct or_params {
     uint32_t churn_ppm, churn_down, churn_horizon; /* DESIGN.md §2.8; 0 ppm = no churn */
     uint32_t node; /* payload layout of the node flavour: 0 rust, 1 go, 2 nim */
     uint32_t sub_graft; /* subscription-time grafting before heartbeat 1 */
+    uint32_t hs_rtts;   /* handshake round trips before the subscriptions (0 = 3) */
 } or_params;
 
 typedef struct or_stats {

@@ -30,7 +30,7 @@ class OrParams(ctypes.Structure):
         ("heartbeat_ns", ctypes.c_uint64), ("backoff_ns", ctypes.c_uint64)] + [
         (n, ctypes.c_uint32) for n in ("flood_publish", "idontwant", "lazy_gossip", "self_log")] + [
         ("seed", ctypes.c_uint64), ("history_gossip", ctypes.c_uint32), ("hb_phase_ns", ctypes.c_uint64)] + [
-        (n, ctypes.c_uint32) for n in ("churn_ppm", "churn_down", "churn_horizon", "node", "sub_graft")]
+        (n, ctypes.c_uint32) for n in ("churn_ppm", "churn_down", "churn_horizon", "node", "sub_graft", "hs_rtts")]
 
 
 class OrStats(ctypes.Structure):
@@ -99,7 +99,7 @@ def params(**kw):
              muxer=0, signed_msgs=1, d=6, d_lo=4, d_hi=8, d_lazy=6, d_out=3,
              gossip_factor_milli=250, heartbeat_ns=1_000_000_000, backoff_ns=60_000_000_000,
              flood_publish=1, idontwant=0, lazy_gossip=1, self_log=0, seed=1, history_gossip=3,
-             hb_phase_ns=0, churn_ppm=0, churn_down=10, churn_horizon=16, node=0, sub_graft=1)
+             hb_phase_ns=0, churn_ppm=0, churn_down=10, churn_horizon=16, node=0, sub_graft=1, hs_rtts=3)
     d.update(kw)
     return OrParams(**d)
 

@@ -24,6 +24,7 @@ for s in ${STEPS:-tests smoke bench prof}; do
   case $s in
     tests) step gpu_tests ${TESTS_SECS:-1200} python -u -m pytest tests -m gpu ${TEST_ARGS:--x} -v --timeout 300 --timeout-method thread ;;
     probe) step rccl_probe 300 ./scripts/bin/rccl_p2p_probe ;;
+    abbatch) step ab_batch 600 python -u scripts/ab_batch.py ${ABB_ARGS:-} ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --steps ${BENCH_STEPS:-20} --warmup 3 ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py $PROFARGS ;;
