@@ -836,7 +836,7 @@ static uint32_t lpull_ring(Ctx& c, const Batch& b, uint64_t delta, uint32_t* lb)
   uint64_t K = std::max(span / delta + 2, seed_span / delta + 1);
   if (K > LP_KMAX) return 0;
   // test knob: a ring smaller than the bound forces ERR_RING and the k_pull re-run
-  static const char* kf = getenv("GS_LPULL_K");
+  const char* kf = getenv("GS_LPULL_K");  // per batch: tests set it between runs
   if (kf && *kf) K = std::min<uint64_t>(K, (uint64_t)std::max(2, atoi(kf)));
   uint32_t tb = 0;
   while ((1ull << tb) < delta) tb++;

@@ -178,3 +178,36 @@ def test_streaming_sink_want_bits():
     sink.on_block = cb
     rc = lib.gs_run(sim.ctx, sim._schedule(sched), M, ctypes.byref(sink))
     assert rc == gossipsim.GS_EINVAL and b"want" in lib.gs_last_error(sim.ctx)
+
+
+def test_shadow_parity_harness_end_to_end(tmp_path):
+    """shadow_parity.py end to end on the GPU: a synthetic Shadow `latencies1`
+    (an oracle run written in the grep format run.sh:61 produces) -> schedule
+    rebuilt from the log -> the GPU run with gs_msg_summary's device
+    percentiles -> 0 error on every message's p50 / p95 / max; the same log with
+    every latency +8 % fails the +-5 % gate."""
+    import json
+    import shadow_parity as sp
+    N, M = 400, 5
+    p = oracle.params(peers=N, seed=21)
+    t = T0 + np.arange(M, dtype=np.uint64) * np.uint64(3_000_000_000)
+    sched = (t, (9 + 7 * np.arange(M)) % N, np.full(M, 15000))
+    ref = oracle.simulate(p, 5, (50, 150, 40, 130), sched=sched)
+    sim, _ = gpu_sim(p, 5, (50, 150, 40, 130), batch=8)
+    sim.write_latency_log(str(tmp_path / "latencies1"), {"schedule": sim._schedule(sched),
+                                                         "t_complete": ref["t_complete"]})
+    sim.close()
+    args = ["--latencies", str(tmp_path / "latencies1"), "--peers", str(N), "--seed", "21",
+            "--topogen", "5,50,150,40,130", "--json", str(tmp_path / "rep.json")]
+    assert sp.main(args) == 0
+    rep = json.load(open(tmp_path / "rep.json"))
+    assert rep["pass"] and rep["messages"] == M
+    assert rep["worst_abs_rel_err"] == {"p50": 0.0, "p95": 0.0, "max": 0.0}
+    assert rep["deliveries"]["sim"] == rep["deliveries"]["shadow"] == ref["stats"]["deliveries"]
+    lines = open(tmp_path / "latencies1").read().splitlines()
+    with open(tmp_path / "latencies2", "w") as f:
+        for ln in lines:
+            head, ms = ln.rsplit(" ", 1)
+            f.write("%s %d\n" % (head, int(ms) * 108 // 100))
+    args[1] = str(tmp_path / "latencies2")
+    assert sp.main(args) == 1
