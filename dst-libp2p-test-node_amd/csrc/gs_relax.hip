@@ -912,7 +912,7 @@ static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvF
   // made of short blocks, keeping >= 32 rows per wave (1M peers: 54.3 ms per
   // step at 4 blocks per CU, 53.1 at 16; 100k peers: 7.8 ms at 16, 6.8 at 4;
   // profiles/r02_v7/lpull_grid_sweep.txt); GS_LPULL_BPC fixes blocks per CU
-  static const uint64_t bpc = [] {
+  const uint64_t bpc = [] {  // per batch: A/B scripts switch it in one process
     const char* e = getenv("GS_LPULL_BPC");
     return (uint64_t)(e && *e ? std::max(1, atoi(e)) : 0);
   }();
@@ -920,7 +920,11 @@ static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvF
   uint64_t auto_bpc = 4;
   while (auto_bpc < 16 && (uint64_t)N >= (uint64_t)dev_cus * PULL_WAVES * 32 * auto_bpc * 2) auto_bpc *= 2;
   const uint64_t want = (uint64_t)dev_cus * (bpc ? bpc : auto_bpc);  // whole blocks per CU
-  const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(((uint64_t)N + PULL_WAVES - 1) / PULL_WAVES, want));
+  unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(((uint64_t)N + PULL_WAVES - 1) / PULL_WAVES, want));
+  if (lpull_team(L)) {  // two-wave teams, one row each: 12 resident per CU, GS_LPULL_BPC (or 48) per CU launched
+    const uint64_t tw = (uint64_t)dev_cus * (bpc ? bpc : 48);
+    grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(N, tw));
+  }
   k_lseed<<<(unsigned)std::max<uint64_t>(1, std::min<uint64_t>((scap + TB - 1) / TB, (uint64_t)dev_cus * 4)), TB, 0, s>>>(
       la, c.d_skey.p, c.d_slane.p, c.d_scnt.p);
   k_lpub<<<(b.B * b.Fe + 255) / 256, 256, 0, s>>>(la, b.Fe);

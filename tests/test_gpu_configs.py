@@ -259,13 +259,16 @@ def test_config3_small_ring_cuts_batches(monkeypatch):
         assert st[k] == ref["stats"][k], k
 
 
-def test_list_pull_equals_dense_rows_at_1m(monkeypatch):
-    """The bench layout at full size (1M peers, rows of 512 lanes, 5-stage
-    topogen links): the list pull path (variant 109) and k_pull over dense rows
-    (45) agree lane for lane. Lazy gossip off so that neither result can hide
-    behind the push-path fallback; the completion times and hops stream out in
-    blocks of 64 messages and are compared by checksums of every block."""
-    N, B = 1_000_000, 512
+@pytest.mark.parametrize("B", [512, 1024])
+def test_list_pull_equals_dense_rows_at_1m(monkeypatch, B):
+    """The bench layout at full size (1M peers, rows of 512 lanes — the
+    one-wave pass with 8 chunks — and of 1024 lanes — the two-wave row teams of
+    the bench —, 5-stage topogen links): the list pull path (variant 109) and
+    k_pull over dense rows (45) agree lane for lane. Lazy gossip off so that
+    neither result can hide behind the push-path fallback; the completion
+    times and hops stream out in blocks of 64 messages and are compared by
+    checksums of every block."""
+    N = 1_000_000
     p = oracle.params(peers=N, seed=1, lazy_gossip=0)
     sim = _sim(p, 5, LINKS, B)
     sched = _sched(B, N)

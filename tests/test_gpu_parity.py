@@ -363,6 +363,24 @@ def test_pull_wide_rows_exact(variant, frags, monkeypatch):
     assert sim.stats()["gossip_fallback_batches"] == 0
 
 
+@pytest.mark.parametrize("team", ["0", "5", "6"])
+def test_list_pass_row_team_forms_exact(team, monkeypatch):
+    """Rows of 1024 lanes run as two-wave teams sharing one LDS buffer
+    (k_lpull_team, 6 or 5 waves per SIMD) or one wave per row (k_lpull, team
+    off): each is bit-exact against the oracle, incl. the overflow re-run with
+    tiny lists."""
+    monkeypatch.setenv("GS_LPULL_TEAM", team)
+    monkeypatch.setenv("GS_REQUIRE_LPULL", "1")
+    p = oracle.params(peers=2300, seed=37, lazy_gossip=0)
+    sim, _ = compare(p, 5, (50, 150, 40, 130), _sched(1024, 2300), batch=1024)
+    assert sim.stats()["list_pull_batches"] == 1
+    monkeypatch.delenv("GS_REQUIRE_LPULL")
+    monkeypatch.setenv("GS_LPULL_CAP", "3")
+    p = oracle.params(peers=1700, seed=38, lazy_gossip=0, fragments=2)
+    monkeypatch.setenv("GS_RELAX_VARIANT", "237")
+    compare(p, 5, (50, 150, 40, 130), _sched(512, 1700), batch=512)
+
+
 def test_pull_list_overflow_reruns_on_dense_rows(monkeypatch):
     """Candidate lists capped at 2 entries (GS_LPULL_CAP): the list pull path
     overflows, restores the counters and re-runs the batch on k_pull; the
