@@ -310,6 +310,10 @@ CONFIGS = {
                              reps=5),
     "c2_10k_F8": dict(peers=10_000, knobs={}, links=(5, 50, 150, 40, 130), fragments=8, batch=128, msgs=1024,
                       reps=3),
+    # go-test-node flavour (gs_config_preset GS_NODE_GO: IDONTWANT >= 1000 B, main.go:165; Dout 2,
+    # unsigned, own message logged) at 100k peers, the IDONTWANT list pass
+    "go_100k_idontwant": dict(peers=100_000, knobs=dict(node="go"), links=(5, 50, 150, 40, 130), fragments=1,
+                              batch=1024, msgs=1024, reps=2),
     "c3_100k_gossip_churn": dict(
         peers=100_000, links=(5, 50, 150, 40, 130), fragments=1, batch=1024, msgs=1024,
         knobs=dict(lazy_gossip=1, churn_ppm=10_000, churn_down=10, churn_horizon=16,
@@ -337,7 +341,8 @@ def config_rates(args, local):
             d = time.perf_counter() - t0
             dt = d if dt is None else min(dt, d)
         st = sim.stats()
-        push = c["knobs"].get("churn_ppm") or st["gossip_fallback_batches"]
+        push = c["knobs"].get("churn_ppm") or st["gossip_fallback_batches"] or \
+            (st["list_pull_batches"] == 0 and sim.cfg.c.idontwant)
         out[name] = {"value": st["deliveries"] / dt, "unit": "deliveries/s", "msgs": c["msgs"], "best_of": c.get("reps", 1),
                      "ms": dt * 1e3, "deliveries": int(st["deliveries"]), "batches": int(st["batches"]),
                      "gossip_iwant": int(st["gossip_iwant"]), "gossip_noop_msgs": int(st["gossip_noop_msgs"]),

@@ -35,6 +35,18 @@
 //
 // Entry (u64): t - (c' * Delta) | hops | src | lane, the key's low (hops |
 // src) bits kept as they are; the host checks the widths fit.
+//
+// IDONTWANT (go preset; template IDW, rows of one fragment):
+// a final lane's key also goes to the dense keys[N][L] table (INF-initialised
+// for such batches; no final log), and the emit step reads the key of the same
+// lane at each mesh neighbour y: y is skipped when its key time + lat(y -> w)
+// <= t (only keys final before this window can pass the test, and those are
+// stable). The skipped neighbours change the uplink positions of the others,
+// so the record carries the 16-bit mask of every excluded mesh index (source,
+// publisher, IDONTWANT) instead of j_src / j_pub:
+//   start - window_lo (32) | hops (6) | exclusion mask (16) | lane (10);
+// the receiver at index r of the sender's row is skipped if bit r is set,
+// else its position is r + 1 - popcount(mask below r).
 
 constexpr uint32_t LP_KMAX = 12;  // ring of destination-window lists
 constexpr uint32_t LP_SW = 16;    // u32 words of per-row state: list lengths [0..11] (slot = window % K), log length
@@ -59,6 +71,7 @@ struct LPullArgs {
   uint64_t delta, tmax;
   uint32_t N, B, L, S, sb, tshift, pass, K, lb, dG;  // lb = lane bits, dG = Delta in key hi-word grains
   uint32_t ls, lcap;  // list stride (max(L, 256) entries) and capacity (ls; GS_LPULL_CAP lowers it)
+  uint32_t idw;       // IDONTWANT batch (k_lpull<.., true>): finals go to dense keys[N][L], no log
 };
 
 constexpr uint32_t LP_FW = PULL_LMAX / 32;  // u32 final-bit words per row
@@ -82,8 +95,13 @@ struct LPullLds {
   uint16_t lst[PULL_WAVES][CH * 64];
 };
 
-template <int FP, uint32_t CH>
+// Record step: groups of NG = 4 neighbours, RCH = 2 chunks of 64 records each
+// per iteration (8 loads in flight per lane; 8 x 64 measured 2 % slower,
+// profiles/r03_v1/ab_record_groups.txt).
+template <int FP, uint32_t CH, bool IDW = false>
 __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
+  constexpr uint32_t NG = 4, RCH = 2;
+  static_assert(!IDW || FP == 1, "IDONTWANT on the list pass: rows of single-fragment lanes");
   constexpr uint32_t LMAX = CH * 64;
   __shared__ LPullLds<CH> Ls;
   // ---- decide this pass from the previous slot (grid-uniform; k_pull's rule) ----
@@ -209,11 +227,11 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
       const uint32_t sd = sdn[sw];
       uint64_t cmk = cand;
       while (cmk) {
-        uint32_t U[4], R4[4], NN[4], SER[4];
-        uint64_t BASE[4];
+        uint32_t U[NG], R4[NG], NN[NG], SER[NG];
+        uint64_t BASE[NG];
         uint32_t maxn = 0;
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
+        for (int k = 0; k < (int)NG; k++) {
           U[k] = 0; R4[k] = 0; NN[k] = 0; SER[k] = 0; BASE[k] = 0;
           if (cmk) {  // wave-uniform
             const int j = __builtin_ctzll(cmk);
@@ -228,26 +246,34 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
             maxn = NN[k] > maxn ? NN[k] : maxn;
           }
         }
-        for (uint32_t i0 = 0; i0 < maxn; i0 += 128) {
-          uint64_t rec[4][2];
+        for (uint32_t i0 = 0; i0 < maxn; i0 += 64 * RCH) {
+          uint64_t rec[NG][RCH];
 #pragma unroll
-          for (int k = 0; k < 4; k++)
+          for (int k = 0; k < (int)NG; k++)
 #pragma unroll
-            for (int cc = 0; cc < 2; cc++) {
+            for (int cc = 0; cc < (int)RCH; cc++) {
               const uint32_t i = i0 + cc * 64 + lane;
               rec[k][cc] = i < NN[k] ? rrec[(size_t)U[k] * LL + i] : ~0ull;
             }
 #pragma unroll
-          for (int k = 0; k < 4; k++)
+          for (int k = 0; k < (int)NG; k++)
 #pragma unroll
-            for (int cc = 0; cc < 2; cc++) {
+            for (int cc = 0; cc < (int)RCH; cc++) {
               const uint64_t rc = rec[k][cc];
               if (rc == ~0ull) continue;  // no record (records never have all bits set)
               const uint32_t lo32 = (uint32_t)rc, r = R4[k];
-              const uint32_t js = (lo32 >> 21) & 31u, jp = (lo32 >> 16) & 31u;
-              if (js == r || jp == r) continue;  // w is the source or the publisher
-              const uint32_t slot = lo32 & 0xFFFFu;
-              const uint32_t pos = r + 1 - (js < r ? 1u : 0u) - ((jp < r && jp != js) ? 1u : 0u);
+              uint32_t slot, pos;
+              if constexpr (IDW) {  // exclusion mask of the sender's row
+                const uint32_t xm = (lo32 >> 10) & 0xFFFFu;
+                if ((xm >> r) & 1u) continue;
+                slot = lo32 & 0x3FFu;
+                pos = r + 1 - (uint32_t)__popc(xm & ((1u << r) - 1u));
+              } else {
+                const uint32_t js = (lo32 >> 21) & 31u, jp = (lo32 >> 16) & 31u;
+                if (js == r || jp == r) continue;  // w is the source or the publisher
+                slot = lo32 & 0xFFFFu;
+                pos = r + 1 - (js < r ? 1u : 0u) - ((jp < r && jp != js) ? 1u : 0u);
+              }
               const uint64_t arr = BASE[k] + (rc >> 32) + (uint64_t)(pos * SER[k]);
               if (arr > a.tmax) err |= ERR_TIME;
               const uint64_t hp1 = ((lo32 >> 26) & hmask) + 1;
@@ -364,12 +390,28 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
         const bool act = gv && x != INF64 && ((uint32_t)(x >> 32) - hlo) < hspan && w != pm;
         const uint32_t src = (uint32_t)(x & smask);
         uint32_t js = J_NONE, jp = J_NONE;  // indices of src / publisher in mesh(w)
-        for (uint32_t k = 0; k < deg; k++) {  // wave-uniform: entry k from lane k
-          const uint32_t y = __builtin_amdgcn_readlane(ej, k) & 0xFFFFFFu;
-          js = y == src ? k : js;
-          jp = y == pm ? k : jp;
+        uint32_t xm = 0;                    // IDW: every excluded mesh index
+        if constexpr (IDW) {
+          const uint64_t tw = x >> a.tshift;
+          for (uint32_t k = 0; k < deg; k++) {  // wave-uniform: entry k from lane k
+            const uint32_t e = __builtin_amdgcn_readlane(ej, k);
+            const uint32_t y = e & 0xFFFFFFu;
+            bool sk = y == src || y == pm;
+            if (act && !sk) {  // IDONTWANT from y already here
+              const uint64_t ky = a.keys[(size_t)y * LL + i];
+              sk = ky != INF64 && (ky >> a.tshift) + lat[(e >> STAGE_SHIFT) * S + sw] <= tw;
+            }
+            xm |= sk ? 1u << k : 0u;
+          }
+        } else {
+          for (uint32_t k = 0; k < deg; k++) {  // wave-uniform: entry k from lane k
+            const uint32_t y = __builtin_amdgcn_readlane(ej, k) & 0xFFFFFFu;
+            js = y == src ? k : js;
+            jp = y == pm ? k : jp;
+          }
         }
-        const uint32_t n = act ? deg - (js != J_NONE ? 1u : 0u) - ((jp != J_NONE && jp != js) ? 1u : 0u) : 0u;
+        const uint32_t n = !act ? 0u : IDW ? deg - (uint32_t)__popc(xm)
+                                           : deg - (js != J_NONE ? 1u : 0u) - ((jp != J_NONE && jp != js) ? 1u : 0u);
         const uint64_t start = uplink_start<FP>(a.busy, (size_t)w * a.B + grp, act, x, n, serw, a.tshift);
         const uint32_t hp = (uint32_t)(x >> a.sb) & hmask;
         if (act) {
@@ -379,17 +421,22 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
           if (start - wlo >= (1ull << 32)) err |= ERR_TIME;
         }
         const uint64_t fm = __ballot(act);  // final log: 64 entries per store
-        if (act) {
-          const uint32_t p = logc + (uint32_t)__popcll(fm & lanelt);
-          a.keys[(size_t)w * LL + p] = x;
-          a.flane[(size_t)w * LL + p] = (uint16_t)i;
+        if constexpr (IDW) {
+          if (act) a.keys[(size_t)w * LL + i] = x;  // dense: the neighbours' IDONTWANT tests read it
+        } else {
+          if (act) {
+            const uint32_t p = logc + (uint32_t)__popcll(fm & lanelt);
+            a.keys[(size_t)w * LL + p] = x;
+            a.flane[(size_t)w * LL + p] = (uint16_t)i;
+          }
+          logc += (uint32_t)__popcll(fm);
         }
-        logc += (uint32_t)__popcll(fm);
         const bool want = act && n != 0;
         const uint64_t wm = __ballot(want);
-        if (want)
-          wrec[(size_t)w * LL + ecnt + (uint32_t)__popcll(wm & lanelt)] =
-              ((start - wlo) << 32) | ((uint64_t)hp << 26) | ((uint64_t)js << 21) | ((uint64_t)jp << 16) | i;
+        if (want) {
+          const uint64_t low = IDW ? (((uint64_t)xm << 10) | i) : (((uint64_t)js << 21) | ((uint64_t)jp << 16) | i);
+          wrec[(size_t)w * LL + ecnt + (uint32_t)__popcll(wm & lanelt)] = ((start - wlo) << 32) | ((uint64_t)hp << 26) | low;
+        }
         ecnt += (uint32_t)__popcll(wm);
       }
     }
@@ -437,372 +484,6 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
   }
 }
 
-// ---- the row-team form of the pass (rows of more than 512 lanes) ----
-// k_lpull gives every row one wave and 10 KB of LDS, so a CU holds 16 rows in
-// flight at 4 waves per SIMD (LDS-bound), and each row's chain of steps is
-// latency-bound at that occupancy. Here a block of two waves
-// (a "team") owns one row at a time and shares the row's 10 KB buffer: the
-// waves split the row's work — the listed entries and the neighbours'
-// records (alternate neighbours) in steps 1-2, chunks 0-7 / 8-15 in
-// classification, the pending appends and the emit step of their own half —
-// with two block barriers per row. 5 KB of LDS and <= 80 VGPRs per wave: 6
-// waves per SIMD, 12 rows in flight per CU, each with half the chain length.
-// Positions in the row's lists, its final log and its record list come from
-// LDS cursors (list entries, log entries and records are unordered sets
-// within a row; every consumer is order-independent). Same candidates, same
-// keys: bit-identical to k_lpull.
-constexpr uint32_t LT_WAVES = 2;
-constexpr uint32_t LT_TB = 64 * LT_WAVES;
-constexpr uint32_t LT_LOG = LP_LOG, LT_REC = LP_SW;  // cursor slots: [0, K) lists, LT_LOG log, LT_REC records
-struct LTeamLds {
-  uint64_t cw[PULL_LMAX];    // the row's candidate minima
-  uint16_t lst[PULL_LMAX];   // wave w's compacted finals / pending in [w * 512, (w + 1) * 512)
-  uint32_t cur[LP_SW + 1];   // append cursors (list lengths, log length, records)
-  uint32_t cbw[LT_WAVES];    // touched chunks found by each wave
-};
-
-template <int FP, int OCC>
-__global__ __launch_bounds__(LT_TB, OCC) void k_lpull_team(LPullArgs a) {
-  constexpr uint32_t HALF = PULL_LMAX / LT_WAVES, HCH = PULL_CH / LT_WAVES;
-  __shared__ LTeamLds Ls;
-  const uint64_t* pv = a.ctrl + ((a.pass + 2) % 3) * 4;
-  uint64_t lo, mode;
-  if (pv[1] != PM_DONE && pv[2]) { mode = PM_PULL; lo = pv[1] == PM_PULL ? pv[0] + a.delta : pv[0]; }
-  else if (pv[3] != INF64) { mode = PM_EMIT; lo = ((pv[3] >> a.tshift) / a.delta) * a.delta; }
-  else { mode = PM_DONE; lo = pv[0]; }
-  uint64_t* me = a.ctrl + (a.pass % 3) * 4;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    me[0] = lo;
-    me[1] = mode;
-    uint64_t* nx = a.ctrl + ((a.pass + 1) % 3) * 4;
-    nx[2] = 0;
-    nx[3] = INF64;
-    if (mode != PM_DONE) atomicAdd((unsigned long long*)&a.counters[C_PASSES], 1ull);
-    if (mode == PM_PULL) atomicAdd((unsigned long long*)&a.counters[C_BUCKETS], 1ull);
-  }
-  if (mode == PM_DONE) return;
-
-  const bool pull = mode == PM_PULL;
-  const uint64_t wlo = pull ? lo + a.delta : lo;
-  const uint64_t c = wlo / a.delta;
-  const uint32_t K = a.K, LL = a.L, S = a.S;
-  const uint32_t cslot = (uint32_t)(c % K);
-  const uint64_t hlo64 = c * a.dG;
-  uint32_t thr[LP_KMAX + 1];
-#pragma unroll
-  for (uint32_t k = 0; k <= LP_KMAX; k++) thr[k] = sat32(hlo64 + (uint64_t)k * a.dG);
-  const uint32_t hlo = thr[0], hspan = a.dG;
-  const size_t NL = (size_t)a.N * LL;
-  const uint32_t pb = (a.pass + 1) & 1, nb = a.pass & 1;
-  const uint64_t* rrec = a.lrec + pb * NL;
-  const uint32_t* rcnt = a.lcnt + (size_t)pb * a.N;
-  uint64_t* wrec = a.lrec + nb * NL;
-  uint32_t* wcnt = a.lcnt + (size_t)nb * a.N;
-  const uint32_t* lat = a.tables;
-  const uint32_t* sup = a.tables + S * S;
-  const uint32_t* sdn = a.tables + S * S + S;
-
-  const int lane = threadIdx.x & 63;
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // 0 / 1: this wave's half (uniform)
-  uint64_t* CW = Ls.cw;
-  uint16_t* LST = Ls.lst + wv * HALF;
-  uint32_t* CUR = Ls.cur;
-  const uint64_t smask = (1ull << a.sb) - 1;
-  const uint32_t hmask = (1u << HOP_BITS) - 1;
-  const uint64_t lanelt = (1ull << lane) - 1;
-  const uint64_t lowmask = (1ull << a.tshift) - 1;
-  const uint32_t lwin = lane < (int)K ? (uint32_t)(((uint32_t)lane + K - cslot) % K) : 0u;
-  const uint32_t lwhi = sat32(hlo64 + (uint64_t)lwin * a.dG);
-  uint64_t fd = 0, nr = 0, np = 0, nrec = 0;
-  uint32_t nmh = ~0u;
-  uint32_t err = 0;
-
-#pragma unroll
-  for (int q = 0; q < (int)HCH; q++) CW[(wv * HCH + q) * 64 + lane] = INF64;
-  __syncthreads();
-
-  const uint32_t stride = gridDim.x;
-  uint32_t w = blockIdx.x;
-  uint32_t ej = EMPTY, cj = 0, rj = 0, sv = 0;
-  if (w < a.N && lane < (int)MESH_W) {
-    ej = a.mesh[(size_t)w * MESH_W + lane];
-    rj = a.rpos[(size_t)w * MESH_W + lane];
-    if (pull && ej != EMPTY) cj = rcnt[ej & 0xFFFFFFu];
-    sv = a.st[(size_t)w * LP_SW + lane];
-  }
-  for (; w < a.N; w += stride) {  // block-uniform
-    const uint32_t w2 = w + stride;
-    uint32_t ej2 = EMPTY, rj2 = 0, cj2 = 0, sv2 = 0;
-    if (w2 < a.N && lane < (int)MESH_W) {
-      ej2 = a.mesh[(size_t)w2 * MESH_W + lane];
-      rj2 = a.rpos[(size_t)w2 * MESH_W + lane];
-      sv2 = a.st[(size_t)w2 * LP_SW + lane];
-    }
-    const uint64_t cand = __ballot(cj != 0);
-    const uint32_t due = umin32(__builtin_amdgcn_readlane(sv, cslot), a.lcap);
-    if (cand == 0 && due == 0) {  // both waves hold the same header: a block-uniform skip
-      if (lane == 0 && wv == 0) wcnt[w] = 0;
-      if (wv == 0 && lane < (int)K && sv) nmh = umin32(nmh, lwhi);
-      if (pull && lane < (int)MESH_W && ej2 != EMPTY) cj2 = rcnt[ej2 & 0xFFFFFFu];
-      ej = ej2; rj = rj2; cj = cj2; sv = sv2;
-      continue;
-    }
-    const uint32_t sw = a.stage[w];
-    uint32_t finT = reinterpret_cast<const uint16_t*>(a.fin + (size_t)w * LP_FW)[lane];
-    // 1. the entries listed for window c: this wave's 128 of every 256
-    uint32_t cb = 0;
-    if (due) {
-      const uint64_t* lst = a.blk + ((size_t)cslot * a.N + w) * a.ls;
-      const uint32_t lmask = (1u << a.lb) - 1, tsh = a.tshift + a.lb;
-      for (uint32_t f0 = 0; f0 < due; f0 += 256) {
-        uint64_t e[2];
-#pragma unroll
-        for (int u = 0; u < 2; u++) {
-          const uint32_t f = f0 + wv * 128 + u * 64 + lane;
-          e[u] = f < due ? lst[f] : ~0ull;
-        }
-#pragma unroll
-        for (int u = 0; u < 2; u++) {
-          if (e[u] == ~0ull) continue;
-          const uint32_t li = (uint32_t)e[u] & lmask;
-          const uint64_t key = ((wlo + (e[u] >> tsh)) << a.tshift) | ((e[u] >> a.lb) & lowmask);
-          atomicMin((unsigned long long*)&CW[li], (unsigned long long)key);
-          cb |= 1u << (li >> 6);
-        }
-      }
-    }
-    // 2. this wave's neighbours (alternate ones of the row's candidates)
-    if (pull) {
-      const uint32_t sd = sdn[sw];
-      uint64_t cmk = 0;
-      {
-        uint64_t x = cand;
-        uint32_t r = 0;
-        while (x) {
-          const uint64_t bit = x & (~x + 1);
-          if ((r & 1u) == wv) cmk |= bit;
-          x ^= bit;
-          r++;
-        }
-      }
-      while (cmk) {
-        uint32_t U[4], R4[4], NN[4], SER[4];
-        uint64_t BASE[4];
-        uint32_t maxn = 0;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          U[k] = 0; R4[k] = 0; NN[k] = 0; SER[k] = 0; BASE[k] = 0;
-          if (cmk) {
-            const int j = __builtin_ctzll(cmk);
-            cmk &= cmk - 1;
-            const uint32_t e = __builtin_amdgcn_readlane(ej, j);
-            U[k] = e & 0xFFFFFFu;
-            R4[k] = __builtin_amdgcn_readlane(rj, j);
-            NN[k] = __builtin_amdgcn_readlane(cj, j);
-            const uint32_t su = e >> STAGE_SHIFT;
-            SER[k] = sup[su];
-            BASE[k] = lo + lat[su * S + sw] + (sd > SER[k] ? sd - SER[k] : 0);
-            maxn = NN[k] > maxn ? NN[k] : maxn;
-          }
-        }
-        for (uint32_t i0 = 0; i0 < maxn; i0 += 128) {
-          uint64_t rec[4][2];
-#pragma unroll
-          for (int k = 0; k < 4; k++)
-#pragma unroll
-            for (int cc = 0; cc < 2; cc++) {
-              const uint32_t i = i0 + cc * 64 + lane;
-              rec[k][cc] = i < NN[k] ? rrec[(size_t)U[k] * LL + i] : ~0ull;
-            }
-#pragma unroll
-          for (int k = 0; k < 4; k++)
-#pragma unroll
-            for (int cc = 0; cc < 2; cc++) {
-              const uint64_t rc = rec[k][cc];
-              if (rc == ~0ull) continue;
-              const uint32_t lo32 = (uint32_t)rc, r = R4[k];
-              const uint32_t js = (lo32 >> 21) & 31u, jp = (lo32 >> 16) & 31u;
-              if (js == r || jp == r) continue;
-              const uint32_t slot = lo32 & 0xFFFFu;
-              const uint32_t pos = r + 1 - (js < r ? 1u : 0u) - ((jp < r && jp != js) ? 1u : 0u);
-              const uint64_t arr = BASE[k] + (rc >> 32) + (uint64_t)(pos * SER[k]);
-              if (arr > a.tmax) err |= ERR_TIME;
-              const uint64_t hp1 = ((lo32 >> 26) & hmask) + 1;
-              const uint64_t nk = (arr << a.tshift) | (hp1 << a.sb) | U[k];
-              atomicMin((unsigned long long*)&CW[slot], (unsigned long long)nk);
-              cb |= 1u << (slot >> 6);
-            }
-        }
-      }
-    }
-    for (int off = 32; off > 0; off >>= 1) cb |= __shfl_xor(cb, off);
-    if (lane == 0) Ls.cbw[wv] = cb;
-    const uint32_t log0 = __builtin_amdgcn_readlane(sv, LP_LOG);
-    if (wv == 0) {  // the row's append cursors (wave 1 appends only after the barrier)
-      if (lane < (int)K) CUR[lane] = lane == (int)cslot ? 0u : sv;
-      if (lane == 0) {
-        CUR[LT_LOG] = log0;
-        CUR[LT_REC] = 0;
-      }
-    }
-    __syncthreads();  // B1: every candidate is in CW, cursors set
-    cb = __builtin_amdgcn_readfirstlane(Ls.cbw[0] | Ls.cbw[1]);
-    if (pull && lane < (int)MESH_W && ej2 != EMPTY) cj2 = rcnt[ej2 & 0xFFFFFFu];
-    // 3. classify the minima of this wave's touched chunks (k_lpull's step 3)
-    uint32_t cnt = 0, npend = 0, nfin = 0;
-#pragma unroll
-    for (int qq = 0; qq < (int)HCH; qq++) {
-      const int q = (int)wv * (int)HCH + qq;
-      if (!((cb >> q) & 1u)) continue;
-      const uint32_t i = q * 64 + lane;
-      uint64_t x = CW[i];
-      if (x != INF64 && ((finT >> q) & 1u)) {
-        x = INF64;
-        CW[i] = INF64;
-      }
-      const bool act = x != INF64 && ((uint32_t)(x >> 32) - hlo) < hspan;
-      const bool pend = x != INF64 && !act;
-      const uint64_t pm = __ballot(pend);
-      if (pend) LST[HALF - 1 - (npend + (uint32_t)__popcll(pm & lanelt))] = (uint16_t)i;
-      npend += (uint32_t)__popcll(pm);
-      const uint64_t am = __ballot(act);
-      if (am) {
-        finT |= act ? 1u << q : 0u;
-        nfin = 1;
-        if constexpr (FP == 1) {
-          if (act) LST[cnt + (uint32_t)__popcll(am & lanelt)] = (uint16_t)i;
-          cnt += (uint32_t)__popcll(am);
-        } else {
-          constexpr uint64_t gmask = (FP == 64) ? ~0ull : ((1ull << FP) - 1);
-          const int gb = lane & ~(FP - 1);
-          const bool gact = ((am >> gb) & gmask) != 0;
-          const uint64_t lm = __ballot(gact && (lane & (FP - 1)) == 0);
-          if (gact && (lane & (FP - 1)) == 0) LST[cnt + (uint32_t)__popcll(lm & lanelt)] = (uint16_t)(i / FP);
-          cnt += (uint32_t)__popcll(lm);
-        }
-      }
-    }
-    wave_lds_sync();
-    // 3b. this wave's pending minima -> the lists of their windows (LDS cursors)
-    if (!pull && npend) err |= ERR_RING;
-    if (pull && npend) {
-      const uint32_t lmax = a.lcap;
-      for (uint32_t j0 = 0; j0 < npend; j0 += 64) {
-        const bool jv = j0 + lane < npend;
-        const uint32_t li = jv ? LST[HALF - 1 - (j0 + lane)] : 0u;
-        const uint64_t x = jv ? CW[li] : INF64;
-        const uint32_t r = jv ? lp_rof((uint32_t)(x >> 32), thr, K) : 0u;
-        if (jv && r >= K) err |= ERR_RING;
-        uint32_t pos = 0, slot = 0;
-#pragma unroll
-        for (uint32_t k = 1; k < LP_KMAX; k++) {
-          if (k >= K) continue;
-          const uint64_t bm = __ballot(jv && r == k);
-          if (!bm) continue;
-          const uint32_t sk = (cslot + k) % K;
-          uint32_t b0 = 0;
-          if (lane == 0) b0 = atomicAdd(&CUR[sk], (uint32_t)__popcll(bm));
-          b0 = __builtin_amdgcn_readfirstlane(b0);
-          if (r == k) {
-            pos = b0 + (uint32_t)__popcll(bm & lanelt);
-            slot = sk;
-          }
-        }
-        if (jv && r > 0 && r < K) {
-          if (pos >= lmax) err |= ERR_LIST;
-          else {
-            const uint64_t toff = (x >> a.tshift) - (wlo + (uint64_t)r * a.delta);
-            a.blk[((size_t)slot * a.N + w) * a.ls + pos] = (toff << (a.tshift + a.lb)) | ((x & lowmask) << a.lb) | li;
-          }
-        }
-      }
-    }
-    np += npend + cnt;
-    // 4. sparse: forward targets, uplink FIFO, final log and records of this wave's finals
-    if (cnt) {
-      const uint32_t deg = (uint32_t)__popcll(__ballot(ej != EMPTY));
-      const uint32_t serw = sup[sw];
-      constexpr uint32_t GPW = 64 / FP;
-      for (uint32_t g0 = 0; g0 < cnt; g0 += GPW) {
-        const uint32_t gi = g0 + (uint32_t)lane / FP;
-        const bool gv = gi < cnt;
-        const uint32_t grp = gv ? LST[gi] : 0;
-        const uint32_t i = grp * FP + (lane & (FP - 1));
-        const uint64_t x = gv ? CW[i] : INF64;
-        const uint32_t pm = gv ? a.pub[grp] : EMPTY;
-        const bool act = gv && x != INF64 && ((uint32_t)(x >> 32) - hlo) < hspan && w != pm;
-        const uint32_t src = (uint32_t)(x & smask);
-        uint32_t js = J_NONE, jp = J_NONE;
-        for (uint32_t k = 0; k < deg; k++) {
-          const uint32_t y = __builtin_amdgcn_readlane(ej, k) & 0xFFFFFFu;
-          js = y == src ? k : js;
-          jp = y == pm ? k : jp;
-        }
-        const uint32_t n = act ? deg - (js != J_NONE ? 1u : 0u) - ((jp != J_NONE && jp != js) ? 1u : 0u) : 0u;
-        const uint64_t start = uplink_start<FP>(a.busy, (size_t)w * a.B + grp, act, x, n, serw, a.tshift);
-        const uint32_t hp = (uint32_t)(x >> a.sb) & hmask;
-        if (act) {
-          fd++;
-          nr += n;
-          if (n && hp + 1 >= (1u << HOP_BITS)) err |= ERR_HOPS;
-          if (start - wlo >= (1ull << 32)) err |= ERR_TIME;
-        }
-        const uint64_t fm = __ballot(act);
-        const bool want = act && n != 0;
-        const uint64_t wm = __ballot(want);
-        uint32_t lb0 = 0, rb0 = 0;
-        if (lane == 0) {
-          if (fm) lb0 = atomicAdd(&CUR[LT_LOG], (uint32_t)__popcll(fm));
-          if (wm) rb0 = atomicAdd(&CUR[LT_REC], (uint32_t)__popcll(wm));
-        }
-        lb0 = __builtin_amdgcn_readfirstlane(lb0);
-        rb0 = __builtin_amdgcn_readfirstlane(rb0);
-        if (act) {
-          const uint32_t p = lb0 + (uint32_t)__popcll(fm & lanelt);
-          a.keys[(size_t)w * LL + p] = x;
-          a.flane[(size_t)w * LL + p] = (uint16_t)i;
-        }
-        if (want)
-          wrec[(size_t)w * LL + rb0 + (uint32_t)__popcll(wm & lanelt)] =
-              ((start - wlo) << 32) | ((uint64_t)hp << 26) | ((uint64_t)js << 21) | ((uint64_t)jp << 16) | i;
-      }
-    }
-    // 5a. this wave's byte of the transposed final bits; 6. its chunks back to INF
-    if (nfin) reinterpret_cast<uint8_t*>(a.fin + (size_t)w * LP_FW)[2 * lane + wv] = (uint8_t)(finT >> (8 * wv));
-#pragma unroll
-    for (int qq = 0; qq < (int)HCH; qq++) {
-      const int q = (int)wv * (int)HCH + qq;
-      if ((cb >> q) & 1u) CW[q * 64 + lane] = INF64;
-    }
-    __syncthreads();  // B2: cursors final, CW clean
-    // 5b. row state from the cursors (wave 0)
-    if (wv == 0) {
-      uint32_t nv = sv;
-      if (lane < (int)K) nv = CUR[lane];
-      if (lane == (int)LP_LOG) nv = CUR[LT_LOG];
-      if (lane <= (int)LP_LOG) a.st[(size_t)w * LP_SW + lane] = nv;
-      if (lane < (int)K && nv) nmh = umin32(nmh, lwhi);
-      const uint32_t ecnt = CUR[LT_REC];
-      if (lane == 0) wcnt[w] = ecnt;
-      nrec += ecnt;
-    }
-    ej = ej2; rj = rj2; cj = cj2; sv = sv2;
-  }
-  for (int off = 32; off > 0; off >>= 1) nmh = umin32(nmh, __shfl_xor(nmh, off));
-  const uint64_t nmin = nmh == ~0u ? INF64 : (uint64_t)nmh << 32;
-  fd = wave_sum(fd);
-  nr = wave_sum(nr);
-  for (int off = 32; off > 0; off >>= 1) err |= __shfl_xor(err, off);
-  if (lane == 0) {
-    if (nrec) atomicAdd((unsigned long long*)&me[2], (unsigned long long)nrec);
-    if (nmin != INF64) atomicMin((unsigned long long*)&me[3], (unsigned long long)nmin);
-    if (fd) atomicAdd((unsigned long long*)&a.counters[C_FD], (unsigned long long)fd);
-    if (nr) atomicAdd((unsigned long long*)&a.counters[C_R_FWD], (unsigned long long)nr);
-    if (np) atomicAdd((unsigned long long*)&a.counters[C_PUSH], (unsigned long long)np);
-    if (err) atomicOr((unsigned*)&a.counters[C_ERR], err);
-  }
-}
-
 // Seeds -> lists: k_seed appended the publishers' first sends (key, row << 11
 // | lane) to a seed list; each goes to the list of its window d = 1..K (slot
 // d % K) at a position taken from the row's list length. One thread per seed.
@@ -833,6 +514,10 @@ __global__ void k_lpub(LPullArgs a, uint32_t Fe) {
   const uint32_t m = g / Fe, f = g % Fe, p = a.pub[m], i = m * FP + f;
   const uint32_t j = i & 63, q = i >> 6;  // transposed: lane j's u16, bit q
   atomicOr(&a.fin[(size_t)p * LP_FW + (j >> 1)], 1u << (16 * (j & 1) + q));
+  if (a.idw) {  // dense keys (IDONTWANT batches)
+    a.keys[(size_t)p * a.L + i] = (uint64_t)p;
+    return;
+  }
   const uint32_t pos = atomicAdd(&a.st[(size_t)p * LP_SW + LP_LOG], 1u);
   a.keys[(size_t)p * a.L + pos] = (uint64_t)p;
   a.flane[(size_t)p * a.L + pos] = (uint16_t)i;
@@ -963,34 +648,10 @@ uint32_t lpull_chunks(uint32_t L) {
   return (L <= 512 && !(e && atoi(e) == 16)) ? 8u : 16u;
 }
 
-// Rows of more than 512 lanes run as two-wave teams (k_lpull_team) unless
-// GS_LPULL_TEAM=0 (read per batch).
-// GS_LPULL_TEAM=5 bounds the team kernel at 5 waves per SIMD (96 VGPRs) instead of 6 (80).
-static int lpull_team_occ() {
-  const char* e = getenv("GS_LPULL_TEAM");
-  return e && *e ? atoi(e) : 6;
-}
-bool lpull_team(uint32_t L) { return lpull_chunks(L) == 16 && lpull_team_occ() != 0; }
-
 void lpull_dispatch(uint32_t FP, const LPullArgs& a, unsigned grid, hipStream_t s) {
-  if (lpull_team(a.L)) {
-    if (lpull_team_occ() == 5) {
-      switch (FP) {
-        case 1: k_lpull_team<1, 5><<<grid, LT_TB, 0, s>>>(a); break;
-        case 2: k_lpull_team<2, 5><<<grid, LT_TB, 0, s>>>(a); break;
-        case 4: k_lpull_team<4, 5><<<grid, LT_TB, 0, s>>>(a); break;
-        case 8: k_lpull_team<8, 5><<<grid, LT_TB, 0, s>>>(a); break;
-        default: k_lpull_team<16, 5><<<grid, LT_TB, 0, s>>>(a); break;
-      }
-      return;
-    }
-    switch (FP) {
-      case 1: k_lpull_team<1, 6><<<grid, LT_TB, 0, s>>>(a); break;
-      case 2: k_lpull_team<2, 6><<<grid, LT_TB, 0, s>>>(a); break;
-      case 4: k_lpull_team<4, 6><<<grid, LT_TB, 0, s>>>(a); break;
-      case 8: k_lpull_team<8, 6><<<grid, LT_TB, 0, s>>>(a); break;
-      default: k_lpull_team<16, 6><<<grid, LT_TB, 0, s>>>(a); break;
-    }
+  if (a.idw) {  // FP == 1 (the host sends fragmented IDONTWANT batches to the push path)
+    if (lpull_chunks(a.L) == 8) k_lpull<1, 8, true><<<grid, TB, 0, s>>>(a);
+    else k_lpull<1, 16, true><<<grid, TB, 0, s>>>(a);
     return;
   }
   if (lpull_chunks(a.L) == 8) {

@@ -861,7 +861,7 @@ static uint32_t lpull_ring(Ctx& c, const Batch& b, uint64_t delta, uint32_t* lb)
 // the batch on k_pull.
 template <class EvFn>
 static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvFn& ev, size_t& n_ev, int dev_cus,
-                            bool dense) {
+                            bool dense, bool idw) {
   const uint32_t N = c.cfg.peers, L = b.L;
   hipStream_t s = c.stream;
   const size_t NL = (size_t)N * L;
@@ -904,6 +904,7 @@ static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvF
   la.tmax = b.tmax - grain;
   la.N = N; la.B = b.B; la.L = L; la.S = c.S; la.sb = b.sb; la.tshift = b.tshift;
   la.K = K; la.lb = lb; la.dG = (uint32_t)(la.delta / grain);
+  la.idw = idw ? 1u : 0u;
   const char* cap = getenv("GS_LPULL_CAP");  // test knob: small lists force the overflow re-run
   la.ls = ls;
   la.lcap = cap && *cap ? (uint32_t)std::min<long>(std::max(1, atoi(cap)), (long)ls) : ls;
@@ -921,10 +922,6 @@ static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvF
   while (auto_bpc < 16 && (uint64_t)N >= (uint64_t)dev_cus * PULL_WAVES * 32 * auto_bpc * 2) auto_bpc *= 2;
   const uint64_t want = (uint64_t)dev_cus * (bpc ? bpc : auto_bpc);  // whole blocks per CU
   unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(((uint64_t)N + PULL_WAVES - 1) / PULL_WAVES, want));
-  if (lpull_team(L)) {  // two-wave teams, one row each: 12 resident per CU, GS_LPULL_BPC (or 48) per CU launched
-    const uint64_t tw = (uint64_t)dev_cus * (bpc ? bpc : 48);
-    grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(N, tw));
-  }
   k_lseed<<<(unsigned)std::max<uint64_t>(1, std::min<uint64_t>((scap + TB - 1) / TB, (uint64_t)dev_cus * 4)), TB, 0, s>>>(
       la, c.d_skey.p, c.d_slane.p, c.d_scnt.p);
   k_lpub<<<(b.B * b.Fe + 255) / 256, 256, 0, s>>>(la, b.Fe);
@@ -956,6 +953,7 @@ static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvF
     return false;
   }
   c.stats.list_pull_batches++;
+  if (idw) return true;  // the final keys are dense rows already
   if (dense) {  // a sink, the traffic pass or a fragment group needs [N][L] rows
     k_lfinal<<<grid, TB, 0, s>>>(la);
     GS_HIP(hipGetLastError());
@@ -1014,13 +1012,13 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
   const bool lanes32 = (uint64_t)N * Bmax * FPmax < (1ull << 32);  // frontier indices are u32
   if (!lanes32) variant &= ~8u;
   const bool gossip = c.cfg.lazy_gossip != 0;
-  // the pull path needs rows in LDS and no cross-row reads (IDONTWANT reads the
-  // target's key) and one mesh per batch (churn uses one per epoch): those stay
-  // on the push path. Lazy gossip runs on the pull path when the batch proves
-  // it a no-op (gossip_noop), else the batch is re-run on the push path.
-  const bool idw_any = c.cfg.idontwant != 0;
+  // the pull path needs rows in LDS and one mesh per batch (churn uses one per
+  // epoch: the push path). IDONTWANT batches run on the list pass with dense
+  // final keys when their rows are single-fragment (k_lpull<1, CH, true>),
+  // else on the push path. Lazy gossip runs on the pull path when the batch
+  // proves it a no-op (gossip_noop), else the batch is re-run on the push path.
   const bool churn = c.cfg.churn_ppm != 0;  // per-epoch mesh lookups live on the push path
-  const bool pull_any = (variant & 32) && !idw_any && !churn;
+  const bool pull_any = (variant & 32) && !churn;
   // the push path with gossip or churn runs split, without tile skip
   // the push path with gossip or churn runs split + tile skip (its long tail of
   // IHAVE and churn buckets touches few tiles); GS_RELAX_VARIANT can turn the skip off
@@ -1230,7 +1228,8 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     // the batch proves gossip a no-op; otherwise discard its counters and run
     // the push path with gossip. Under churn some peers never
     // complete, so the proof cannot hold and gossip runs directly.
-    const bool pull_ok = pull_any && b.delta >= pull_grain(b.tshift);
+    const bool idw_b = c.cfg.idontwant && b.payload >= c.cfg.idontwant;  // IDONTWANT active in this batch
+    const bool pull_ok = pull_any && b.delta >= pull_grain(b.tshift) && (!idw_b || (b.FP == 1 && (variant & 64)));
     bool done = false;
     if (pull_ok || (gossip && !churn)) {
       if (gossip) GS_HIP(hipMemcpyAsync(c.d_cnt_save.p, c.d_counters.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));
@@ -1241,18 +1240,21 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
         // with bit 128 (k_pull's dense rows measured 7 % faster on config #2)
         const bool lp = (variant & 64) && (b.FP == 1 || (variant & 128));
         const uint32_t K = lp ? lpull_ring(c, b, b.delta / grain * grain, &lb) : 0u;
-        reset(variant, false, K == 0);
+        reset(variant, false, K == 0 || idw_b);  // IDONTWANT: dense INF keys
         if (lp && !K && getenv("GS_REQUIRE_LPULL"))  // test knob: no silent k_pull fallback
           c.fail(GS_EUNSUPPORTED, "list pull path cannot take this batch (GS_REQUIRE_LPULL)");
         // GS_LPULL_DENSE (diagnostic): dense rows + k_complete, whose known key
-        // stream calibrates the PMC read factor (scripts/pmc_summary.py)
-        const bool dense = sink != nullptr || c.traffic || b.FP > 1 || getenv("GS_LPULL_DENSE");
-        if (!K || !run_lpull_batch(c, b, K, lb, ev, n_ev, dev_cus, dense)) {
-          if (K) {  // a candidate list overflowed: this batch runs on k_pull
-            if (getenv("GS_REQUIRE_LPULL")) c.fail(GS_EUNSUPPORTED, "list pull overflow (GS_REQUIRE_LPULL)");
-            reset(variant, false);
+        // stream calibrates the PMC read factor (scripts/pmc_summary.py);
+        // IDONTWANT batches keep their final keys dense all along
+        const bool dense = !idw_b && (sink != nullptr || c.traffic || b.FP > 1 || getenv("GS_LPULL_DENSE"));
+        if (!K || !run_lpull_batch(c, b, K, lb, ev, n_ev, dev_cus, dense, idw_b)) {
+          if (K && getenv("GS_REQUIRE_LPULL")) c.fail(GS_EUNSUPPORTED, "list pull overflow (GS_REQUIRE_LPULL)");
+          if (idw_b) {  // k_pull has no IDONTWANT: the push path takes the batch
+            push_run(variant & ~32u, false);
+          } else {  // a candidate list overflowed (or no ring fits): this batch runs on k_pull
+            if (K) reset(variant, false);
+            run_pull_batch(c, b, ev, n_ev, dev_cus);
           }
-          run_pull_batch(c, b, ev, n_ev, dev_cus);
         }
       } else {
         push_run(variant & ~32u, false);

@@ -261,10 +261,10 @@ def test_config3_small_ring_cuts_batches(monkeypatch):
 
 @pytest.mark.parametrize("B", [512, 1024])
 def test_list_pull_equals_dense_rows_at_1m(monkeypatch, B):
-    """The bench layout at full size (1M peers, rows of 512 lanes — the
-    one-wave pass with 8 chunks — and of 1024 lanes — the two-wave row teams of
-    the bench —, 5-stage topogen links): the list pull path (variant 109) and
-    k_pull over dense rows (45) agree lane for lane. Lazy gossip off so that
+    """The bench layout at full size (1M peers, rows of 512 lanes — the pass
+    with 8 chunks per row and 6 waves per SIMD — and of 1024 lanes — 16
+    chunks, the bench's —, 5-stage topogen links): the list pull path (variant
+    109) and k_pull over dense rows (45) agree lane for lane. Lazy gossip off so that
     neither result can hide behind the push-path fallback; the completion
     times and hops stream out in blocks of 64 messages and are compared by
     checksums of every block."""

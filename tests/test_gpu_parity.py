@@ -152,6 +152,37 @@ def test_node_presets(node):
         sim.run(_sched(1, 800, size=small - 3))
 
 
+@pytest.mark.parametrize("B,M", [(64, 70), (512, 512), (1024, 1024)])
+def test_idontwant_on_list_pass(monkeypatch, B, M):
+    """IDONTWANT (go preset: threshold 1000 B, go-test-node/main.go:165) on the
+    list pass: single-fragment batches keep their final keys dense, the emit
+    step tests every mesh neighbour's key and the records carry the exclusion
+    mask (rows of 64, 512 and 1024 lanes); bit-exact against the oracle, and
+    IDONTWANT really suppresses sends."""
+    monkeypatch.setenv("GS_REQUIRE_LPULL", "1")
+    p = oracle.params_for("go", peers=2000, seed=62, lazy_gossip=0)
+    sim, _ = compare(p, 5, (50, 150, 40, 130), _sched(M, 2000), batch=B)
+    st = sim.stats()
+    assert st["list_pull_batches"] >= 1
+    p0 = oracle.params_for("go", peers=2000, seed=62, lazy_gossip=0, idontwant=0)
+    ref0 = oracle.simulate(p0, 5, (50, 150, 40, 130), sched=_sched(M, 2000))
+    assert st["relaxations"] < ref0["stats"]["relaxations"]
+
+
+def test_idontwant_list_overflow_and_gossip(monkeypatch):
+    """An IDONTWANT batch whose candidate lists overflow re-runs on the push
+    path (k_pull has no IDONTWANT); with the go preset's lazy gossip the
+    batch's eager result stands when gossip is proven a no-op. Both bit-exact."""
+    monkeypatch.setenv("GS_LPULL_CAP", "2")
+    p = oracle.params_for("go", peers=1500, seed=63, lazy_gossip=0)
+    sim, _ = compare(p, 5, (50, 150, 40, 130), _sched(200, 1500), batch=200)
+    assert sim.stats()["list_pull_batches"] == 0
+    monkeypatch.delenv("GS_LPULL_CAP")
+    p = oracle.params_for("go", peers=1500, seed=64)
+    sim, _ = compare(p, 5, (50, 150, 40, 130), _sched(100, 1500), batch=100)
+    assert sim.stats()["list_pull_batches"] >= 1
+
+
 _IWANT_PHASE = T0 % 1_000_000_000  # a heartbeat at the publish instant: IHAVEs race the eager wave
 
 
@@ -361,24 +392,6 @@ def test_pull_wide_rows_exact(variant, frags, monkeypatch):
     p = oracle.params(peers=2500, seed=33, fragments=frags, lazy_gossip=0)
     sim, _ = compare(p, 5, (50, 150, 40, 130), _sched(B, 2500), batch=B)
     assert sim.stats()["gossip_fallback_batches"] == 0
-
-
-@pytest.mark.parametrize("team", ["0", "5", "6"])
-def test_list_pass_row_team_forms_exact(team, monkeypatch):
-    """Rows of 1024 lanes run as two-wave teams sharing one LDS buffer
-    (k_lpull_team, 6 or 5 waves per SIMD) or one wave per row (k_lpull, team
-    off): each is bit-exact against the oracle, incl. the overflow re-run with
-    tiny lists."""
-    monkeypatch.setenv("GS_LPULL_TEAM", team)
-    monkeypatch.setenv("GS_REQUIRE_LPULL", "1")
-    p = oracle.params(peers=2300, seed=37, lazy_gossip=0)
-    sim, _ = compare(p, 5, (50, 150, 40, 130), _sched(1024, 2300), batch=1024)
-    assert sim.stats()["list_pull_batches"] == 1
-    monkeypatch.delenv("GS_REQUIRE_LPULL")
-    monkeypatch.setenv("GS_LPULL_CAP", "3")
-    p = oracle.params(peers=1700, seed=38, lazy_gossip=0, fragments=2)
-    monkeypatch.setenv("GS_RELAX_VARIANT", "237")
-    compare(p, 5, (50, 150, 40, 130), _sched(512, 1700), batch=512)
 
 
 def test_pull_list_overflow_reruns_on_dense_rows(monkeypatch):
