@@ -289,7 +289,8 @@ def measure(args, sim, peers, world, rank, torch, dist):
     if len(sims) > 1:  # loop-back parts: the job's counters are the parts' sum
         for x in sims[1:]:
             sx = x.stats()
-            for k in ("deliveries", "frag_deliveries", "relaxations", "bytes_alg", "relax_bytes_alg"):
+            for k in ("deliveries", "frag_deliveries", "relaxations", "bytes_alg", "relax_bytes_alg", "relax_ms",
+                      "scan_ms", "frontier_ms", "relax_launches"):
                 st[k] += sx[k]
     for x in sims:
         x.set_timing(False)
@@ -374,7 +375,10 @@ def main():
     # HIP events around its scan and its export + exchange + relaxation
     launches = max(1, st["relax_launches"])
     fpl = fp_lanes(args.fragments)
-    if args.mode == "peer":
+    if args.mode == "peer" and st.get("list_pull_batches", 0) > 0:
+        kernel = "k_lpull<%d> over each part's rows (partitioned list pass; records exchanged between " \
+                 "passes, not timed here)" % fpl
+    elif args.mode == "peer":
         kernel = "k_scan<%d,false,false> + k_pexport_dest<%d> + record exchange + k_precv<%d> " \
                  "(partitioned push path)" % (fpl, fpl, fpl)
     else:

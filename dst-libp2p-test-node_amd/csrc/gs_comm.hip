@@ -93,7 +93,7 @@ struct gs_comm {
   uint32_t nranks = 1, rank = 0;
   int32_t device = 0;
   ncclComm_t nc = nullptr;
-  uint64_t* d_scratch = nullptr;  // RCCL: [parts * parts] count matrix + 1 flag word
+  uint64_t* d_scratch = nullptr;  // RCCL: [parts * parts] count matrix + 1 flag word + [parts][4] pass control
 };
 
 extern "C" gs_status gs_comm_get_id(gs_comm_id* out) {
@@ -122,7 +122,7 @@ extern "C" gs_status gs_comm_init(uint32_t nranks, uint32_t rank, const gs_comm_
   ncclUniqueId nid;
   memcpy(&nid, id, sizeof nid);
   if (r->CommInitRank(&c->nc, (int)nranks, nid, (int)rank) != ncclSuccess ||
-      hipMalloc((void**)&c->d_scratch, ((size_t)nranks * nranks + 1) * 8) != hipSuccess) {
+      hipMalloc((void**)&c->d_scratch, ((size_t)nranks * nranks + 1 + 4 * (size_t)nranks) * 8) != hipSuccess) {
     if (c->nc) r->CommDestroy(c->nc);
     delete c;
     return GS_EDEVICE;
@@ -206,9 +206,211 @@ void check_same_config(gs_comm* cm, Ctx& c, const gs_publish* sched, uint64_t n_
                              "churn, fragments, seed or schedule)");
 }
 
-// One batch of the partitioned protocol over this process's parts.
+// RCCL ranks: every rank's n words (n <= 4) -> out[rank * n + k] on the host.
+void rank_gather(gs_comm* cm, Ctx& c, const uint64_t* mine, uint32_t n, uint64_t* out) {
+  uint64_t* w = cm->d_scratch + (size_t)cm->nranks * cm->nranks + 1;
+  memcpy(c.h_pinned + 16, mine, n * 8);
+  GS_HIP(hipMemcpyAsync(w + (size_t)cm->rank * n, c.h_pinned + 16, n * 8, hipMemcpyHostToDevice, c.stream));
+  GS_NCCL(rccl()->AllGather(w + (size_t)cm->rank * n, w, n, ncclUint64, cm->nc, c.stream));
+  std::vector<uint64_t> h((size_t)cm->nranks * n);
+  GS_HIP(hipMemcpyAsync(h.data(), w, h.size() * 8, hipMemcpyDeviceToHost, c.stream));
+  GS_HIP(hipStreamSynchronize(c.stream));
+  memcpy(out, h.data(), h.size() * 8);
+}
+
+// The list pass over partitioned rows: every part runs the
+// window passes of gs_run over its own rows; between passes the parts agree
+// on the pass control (records emitted, min pending key, error word) and
+// exchange the pass's records, packed, with every peer's count and offset.
+// Returns false, with every part's state and counters as before, when the
+// list pass cannot take the batch (ring bound, memory, a knob) or a candidate
+// list overflowed: the caller runs the push protocol instead.
+bool run_batch_lp(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched, uint64_t i0, uint32_t B,
+                  const gs_result_sink* sinks) {
+  const uint32_t P = cm->nranks, N = cx[0]->cfg.peers;
+  Rccl* r = cm->local ? nullptr : rccl();
+  std::vector<uint64_t> smin(nctx, INF64);
+  uint64_t bad = 0;  // some part cannot take the batch on the list pass
+  for (uint32_t i = 0; i < nctx; i++) {
+    GS_HIP(hipSetDevice(cx[i]->cfg.device));
+    if (!cm->local) {
+      std::string why;
+      gs_status code = GS_OK;
+      bool ok = false;
+      try {
+        ok = part_lp_begin(*cx[i], sched + i0, B, &smin[i]);
+      } catch (const Error& e) {
+        code = e.code;
+        why = e.msg;
+      }
+      rank_status(cm, *cx[i], code != GS_OK);
+      if (code != GS_OK) throw Error(code, why);
+      bad |= ok ? 0u : 1u;
+    } else if (!part_lp_begin(*cx[i], sched + i0, B, &smin[i])) {
+      bad = 1;
+    }
+  }
+  if (!cm->local) {
+    uint64_t mine[2] = {bad, ~smin[0]}, all[2 * 64];
+    rank_gather(cm, *cx[0], mine, 2, all);
+    bad = 0;
+    smin[0] = INF64;
+    for (uint32_t k = 0; k < P; k++) {
+      bad |= all[2 * k];
+      smin[0] = std::min(smin[0], ~all[2 * k + 1]);
+    }
+  }
+  if (bad) {
+    for (uint32_t i = 0; i < nctx; i++) part_lp_abort(*cx[i]);
+    return false;
+  }
+  uint64_t key = *std::min_element(smin.begin(), smin.end());
+  for (uint32_t i = 0; i < nctx; i++) {
+    GS_HIP(hipSetDevice(cx[i]->cfg.device));
+    part_lp_set(*cx[i], 0, key);  // slot 2 as pass 0 reads it: no records, the min seeded key
+  }
+  std::vector<size_t> nev(nctx, 0);
+  auto ev = [&](uint32_t i) {
+    Ctx& c = *cx[i];
+    while (c.ev_pool.size() <= nev[i]) {
+      hipEvent_t e;
+      GS_HIP(hipEventCreate(&e));
+      c.ev_pool.push_back(e);
+    }
+    GS_HIP(hipEventRecord(c.ev_pool[nev[i]++], c.stream));
+  };
+  auto u0_of = [&](uint32_t p) { return (uint32_t)((uint64_t)p * N / P); };
+  const size_t RB = 8;  // bytes per record
+  std::vector<uint64_t> st((size_t)P * 4);  // per part: mode, records, min pending, error word
+  for (;;) {
+    for (uint32_t i = 0; i < nctx; i++) {
+      GS_HIP(hipSetDevice(cx[i]->cfg.device));
+      if (cx[i]->timing) ev(i);
+      part_lp_pass(*cx[i]);
+      if (cx[i]->timing) ev(i);
+    }
+    if (cm->local) {
+      for (uint32_t i = 0; i < nctx; i++) {
+        GS_HIP(hipSetDevice(cx[i]->cfg.device));
+        part_lp_read(*cx[i], &st[(size_t)i * 4]);
+      }
+    } else {
+      uint64_t mine[4];
+      part_lp_read(*cx[0], mine);
+      rank_gather(cm, *cx[0], mine, 4, st.data());
+    }
+    uint64_t recs = 0, minp = INF64, err = 0;
+    for (uint32_t p = 0; p < P; p++) {
+      recs += st[(size_t)p * 4 + 1];
+      minp = std::min(minp, st[(size_t)p * 4 + 2]);
+      err |= st[(size_t)p * 4 + 3];
+    }
+    if (err & (ERR_LIST | ERR_RING)) {  // lost entries somewhere: the push protocol takes the batch
+      for (uint32_t i = 0; i < nctx; i++) {
+        GS_HIP(hipSetDevice(cx[i]->cfg.device));
+        part_lp_abort(*cx[i]);
+      }
+      return false;
+    }
+    if (st[0] == 0) break;  // pass mode DONE (PM_DONE, gs_pull_kernel.h): grid- and part-uniform
+    for (uint32_t i = 0; i < nctx; i++) {
+      GS_HIP(hipSetDevice(cx[i]->cfg.device));
+      part_lp_set(*cx[i], recs, minp);
+    }
+    if (!recs) continue;  // the next pass emits a window: it reads no records
+    // pack (each part knows its offset in the packed records of all parts)
+    std::vector<uint64_t> base(P + 1, 0);
+    for (uint32_t p = 0; p < P; p++) base[p + 1] = base[p] + st[(size_t)p * 4 + 1];
+    for (uint32_t i = 0; i < nctx; i++) {
+      const uint32_t me = cm->local ? i : cm->rank;
+      GS_HIP(hipSetDevice(cx[i]->cfg.device));
+      cx[i]->d_rpk.alloc(recs);
+      part_lp_pack(*cx[i], base[me], st[(size_t)me * 4 + 1]);
+    }
+    if (cm->local) {
+      for (uint32_t i = 0; i < nctx; i++) GS_HIP(hipStreamSynchronize(cx[i]->stream));  // every pack done
+      for (uint32_t q = 0; q < nctx; q++) {
+        Ctx& d = *cx[q];
+        GS_HIP(hipSetDevice(d.cfg.device));
+        for (uint32_t p = 0; p < nctx; p++) {
+          Ctx& src = *cx[p];
+          const uint64_t n = st[(size_t)p * 4 + 1], u0 = u0_of(p), un = u0_of(p + 1) - u0;
+          if (n) GS_HIP(hipMemcpyAsync(d.d_rpk.p + base[p], src.d_pkout.p, n * RB, hipMemcpyDeviceToDevice, d.stream));
+          GS_HIP(hipMemcpyAsync(d.d_rcg.p + u0, part_lp_counts(src), un * 4, hipMemcpyDeviceToDevice, d.stream));
+          GS_HIP(hipMemcpyAsync(d.d_roffg.p + u0, src.d_pkroff.p, un * 8, hipMemcpyDeviceToDevice, d.stream));
+        }
+      }
+      for (uint32_t q = 0; q < nctx; q++) GS_HIP(hipStreamSynchronize(cx[q]->stream));  // sources reused next pass
+    } else {
+      Ctx& c = *cx[0];
+      const uint32_t me = cm->rank;
+      const uint64_t piece = std::max<uint64_t>(1, rccl_piece_bytes() / RB);
+      const uint64_t myn = st[(size_t)me * 4 + 1], my0 = u0_of(me), myun = u0_of(me + 1) - my0;
+      GS_NCCL(r->GroupStart());
+      for (uint32_t d = 0; d < P; d++) {
+        for (uint64_t k = 0; k < myn; k += piece)
+          GS_NCCL(r->Send(c.d_pkout.p + k, std::min(piece, myn - k), ncclUint64, (int)d, cm->nc, c.stream));
+        GS_NCCL(r->Send(part_lp_counts(c), myun, ncclUint32, (int)d, cm->nc, c.stream));
+        GS_NCCL(r->Send(c.d_pkroff.p, myun, ncclUint64, (int)d, cm->nc, c.stream));
+      }
+      for (uint32_t sr = 0; sr < P; sr++) {
+        const uint64_t n = st[(size_t)sr * 4 + 1], u0 = u0_of(sr), un = u0_of(sr + 1) - u0;
+        for (uint64_t k = 0; k < n; k += piece)
+          GS_NCCL(r->Recv(c.d_rpk.p + base[sr] + k, std::min(piece, n - k), ncclUint64, (int)sr, cm->nc, c.stream));
+        GS_NCCL(r->Recv(c.d_rcg.p + u0, un, ncclUint32, (int)sr, cm->nc, c.stream));
+        GS_NCCL(r->Recv(c.d_roffg.p + u0, un, ncclUint64, (int)sr, cm->nc, c.stream));
+      }
+      GS_NCCL(r->GroupEnd());
+    }
+  }
+  for (uint32_t i = 0; i < nctx; i++) {  // pass times (timing on)
+    Ctx& c = *cx[i];
+    if (!c.timing) continue;
+    GS_HIP(hipSetDevice(c.cfg.device));
+    GS_HIP(hipStreamSynchronize(c.stream));
+    double front = 0;
+    for (size_t q = 0; q + 1 < nev[i]; q += 2) {
+      float x = 0;
+      GS_HIP(hipEventElapsedTime(&x, c.ev_pool[q], c.ev_pool[q + 1]));
+      front += x;
+    }
+    c.stats.frontier_ms += front;
+    c.stats.relax_ms += front;
+  }
+  // completion + the lazy-gossip no-op proof of every part
+  bool ok = true;
+  for (uint32_t i = 0; i < nctx; i++) {
+    GS_HIP(hipSetDevice(cx[i]->cfg.device));
+    ok = part_lp_end(*cx[i], sinks && sinks[i].summary) && ok;
+  }
+  if (!cm->local && cx[0]->cfg.lazy_gossip) {
+    uint64_t mine = ok ? 0 : 1, all[64];
+    rank_gather(cm, *cx[0], &mine, 1, all);
+    for (uint32_t k = 0; k < P; k++) ok = ok && !all[k];
+  }
+  if (!ok) {
+    std::string why;
+    for (uint32_t i = 0; i < nctx; i++) {
+      part_abort(*cx[i]);
+      if (why.empty()) why = cx[i]->gossip_why;
+    }
+    throw Error(GS_EUNSUPPORTED, "lazy gossip can change this batch (an IHAVE lands before the last delivery; " +
+                                     (why.empty() ? std::string("another rank") : why) +
+                                     "); partitioned mode runs eager forwarding only: use gs_run");
+  }
+  for (uint32_t i = 0; i < nctx; i++) {
+    GS_HIP(hipSetDevice(cx[i]->cfg.device));
+    part_dev_finish(*cx[i], sinks ? &sinks[i] : nullptr, i0);
+  }
+  return true;
+}
+
+// One batch of the partitioned protocol over this process's parts: the list
+// pass when it can take the batch, else the push protocol (scan / routed
+// export / receive per bucket).
 void run_batch(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched, uint64_t i0, uint32_t B,
                const gs_result_sink* sinks) {
+  if (run_batch_lp(cm, cx, nctx, sched, i0, B, sinks)) return;
   const uint32_t P = cm->nranks;
   Rccl* r = cm->local ? nullptr : rccl();
   std::vector<uint64_t> key0(nctx);

@@ -85,7 +85,7 @@ extern "C" gs_status gs_create(const gs_config* cfg, gs_ctx** out) {
     }
     GS_HIP(hipSetDevice(cfg->device));
     GS_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    GS_HIP(hipHostMalloc((void**)&c->h_pinned, C_COUNT * 8, hipHostMallocDefault));
+    GS_HIP(hipHostMalloc((void**)&c->h_pinned, H_PINNED_WORDS * 8, hipHostMallocDefault));
     c->d_counters.alloc(C_COUNT);
     c->d_ctrl.alloc(4);
     GS_HIP(hipMemsetAsync(c->d_counters.p, 0, C_COUNT * 8, c->stream));

@@ -50,6 +50,8 @@ struct DevBuf {
 };
 
 // Counters written by kernels: index constants into Ctx::d_counters.
+constexpr uint32_t H_PINNED_WORDS = 32;
+
 enum : uint32_t {
   C_FD = 0, C_R = 1, C_DELIV = 2, C_LAT_SUM = 3, C_LAT_MAX = 4, C_BUCKETS = 5,
   C_R_FWD = 6, C_MESH_CHANGES = 7, C_MESH_WAKE = 8, C_ERR = 9, C_PUSH = 10, C_GOSSIP = 11, C_PASSES = 12,
@@ -159,7 +161,7 @@ struct Ctx {
   DevBuf<uint16_t> d_flane;  // [N][L] lanes of the final log
   DevBuf<uint64_t> d_counters;  // [C_COUNT]
   DevBuf<uint64_t> d_cnt_save;  // [C_COUNT] counters before a batch (gossip fallback restores them)
-  uint64_t* h_pinned = nullptr; // pinned host mirror of ctrl + counters
+  uint64_t* h_pinned = nullptr; // pinned host mirror of ctrl + counters (H_PINNED_WORDS)
   // per-message reductions of k_complete / k_pct (gs_relax.hip)
   DevBuf<uint64_t> d_mstat;     // [B][MS_COLS]
   DevBuf<uint32_t> d_hist;      // [B][GS_HIST_BINS]
@@ -177,6 +179,17 @@ struct Ctx {
   DevBuf<uint64_t> d_pcnt;      // [4] frontier groups, records, relax min key, spare
   DevBuf<uint64_t> d_dcnt, d_dpos;  // [64] records per destination part / their write cursors
   DevBuf<gs_part_record> d_pout, d_pin;  // gs_run_partitioned: records sent / received this bucket
+  // gs_run_partitioned on the list pass (gs_part.h part_lp_*): this part's rows in the list
+  // buffers above (local row indexing); every peer's records of the last pass, packed
+  bool part_lp = false;
+  uint32_t part_lpK = 0, part_lplb = 0, part_lppass = 0;
+  unsigned part_lpgrid = 0;
+  DevBuf<uint32_t> d_rcg;    // [N] records per peer (global ids)
+  DevBuf<uint64_t> d_roffg;  // [N] their offsets in d_rpk
+  DevBuf<uint64_t> d_rpk;    // every part's records of the last pass
+  DevBuf<uint64_t> d_pkout;  // this part's records, packed for the exchange
+  DevBuf<uint64_t> d_pkroff; // [own rows] their offsets in d_rpk
+  DevBuf<uint64_t> d_pkcur;  // pack cursor
 
   // stats
   gs_stats stats{};
@@ -207,6 +220,15 @@ void part_dev_relax_next(Ctx& c, const gs_part_record* in, uint64_t n);
 bool part_dev_complete(Ctx& c, bool hist);
 void part_dev_finish(Ctx& c, const gs_result_sink* sink, uint64_t row0);
 void part_abort(Ctx& c);
+// the list pass over partitioned rows (gs_part.h)
+bool part_lp_begin(Ctx& c, const gs_publish* sched, uint64_t n_msgs, uint64_t* seed_min);
+void part_lp_pass(Ctx& c);
+void part_lp_read(Ctx& c, uint64_t out[4]);  // last pass: mode, records, min pending, error word
+void part_lp_set(Ctx& c, uint64_t records, uint64_t minp);  // the combined values into the last pass's slot
+void part_lp_pack(Ctx& c, uint64_t base, uint64_t mine);
+const uint32_t* part_lp_counts(Ctx& c);  // this part's per-row record counts of the last pass
+bool part_lp_end(Ctx& c, bool hist);     // dense rows, completion, gossip proof
+void part_lp_abort(Ctx& c);
 
 // small device helpers
 void device_exclusive_scan(Ctx& c, const uint64_t* in, uint64_t* out, uint32_t n);

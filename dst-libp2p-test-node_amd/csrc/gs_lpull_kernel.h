@@ -40,8 +40,9 @@
 // a final lane's key also goes to the dense keys[N][L] table (INF-initialised
 // for such batches; no final log), and the emit step reads the key of the same
 // lane at each mesh neighbour y: y is skipped when its key time + lat(y -> w)
-// <= t (only keys final before this window can pass the test, and those are
-// stable). The skipped neighbours change the uplink positions of the others,
+// <= t. Such batches run with windows no wider than the smallest latency
+// (gs_relax.hip), so only keys final in earlier windows — written by earlier
+// passes, stable — can pass the test. The skipped neighbours change the uplink positions of the others,
 // so the record carries the 16-bit mask of every excluded mesh index (source,
 // publisher, IDONTWANT) instead of j_src / j_pub:
 //   start - window_lo (32) | hops (6) | exclusion mask (16) | lane (10);
@@ -72,6 +73,14 @@ struct LPullArgs {
   uint32_t N, B, L, S, sb, tshift, pass, K, lb, dG;  // lb = lane bits, dG = Delta in key hi-word grains
   uint32_t ls, lcap;  // list stride (max(L, 256) entries) and capacity (ls; GS_LPULL_CAP lowers it)
   uint32_t idw;       // IDONTWANT batch (k_lpull<.., true>): finals go to dense keys[N][L], no log
+  // peer-partitioned pass (k_lpull<.., .., .., true>, gs_run_partitioned): this context's rows are
+  // global peers [u0, u0 + N); every per-row array above is indexed by the local row, lrec / lcnt
+  // receive only this part's records, and the previous pass's records of EVERY peer arrive packed
+  // (rpk) with per-peer offsets (roff) and counts (rcg), exchanged by the host (gs_comm.hip)
+  uint32_t u0;
+  const uint64_t* rpk;
+  const uint64_t* roff;
+  const uint32_t* rcg;
 };
 
 constexpr uint32_t LP_FW = PULL_LMAX / 32;  // u32 final-bit words per row
@@ -98,7 +107,7 @@ struct LPullLds {
 // Record step: groups of NG = 4 neighbours, RCH = 2 chunks of 64 records each
 // per iteration (8 loads in flight per lane; 8 x 64 measured 2 % slower,
 // profiles/r03_v1/ab_record_groups.txt).
-template <int FP, uint32_t CH, bool IDW = false>
+template <int FP, uint32_t CH, bool IDW = false, bool PART = false>
 __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
   constexpr uint32_t NG = 4, RCH = 2;
   static_assert(!IDW || FP == 1, "IDONTWANT on the list pass: rows of single-fragment lanes");
@@ -134,8 +143,8 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
   const uint32_t hlo = thr[0], hspan = a.dG;  // hi words of window c: [hlo, hlo + dG)
   const size_t NL = (size_t)a.N * LL;
   const uint32_t pb = (a.pass + 1) & 1, nb = a.pass & 1;  // records read / written
-  const uint64_t* rrec = a.lrec + pb * NL;
-  const uint32_t* rcnt = a.lcnt + (size_t)pb * a.N;
+  const uint64_t* rrec = PART ? a.rpk : a.lrec + pb * NL;
+  const uint32_t* rcnt = PART ? a.rcg : a.lcnt + (size_t)pb * a.N;  // indexed by global peer id
   uint64_t* wrec = a.lrec + nb * NL;
   uint32_t* wcnt = a.lcnt + (size_t)nb * a.N;
   const uint32_t* lat = a.tables;
@@ -164,12 +173,16 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
   wave_lds_sync();
 
   const uint32_t stride = gridDim.x * PULL_WAVES;
-  uint32_t w = blockIdx.x * PULL_WAVES + wv;
+  uint32_t w = blockIdx.x * PULL_WAVES + wv;  // local row; global peer a.u0 + w
   uint32_t ej = EMPTY, cj = 0, rj = 0, sv = 0;
+  uint64_t ro = 0, ro2 = 0;  // PART: offsets of the neighbours' packed records
   if (w < a.N && lane < (int)MESH_W) {
-    ej = a.mesh[(size_t)w * MESH_W + lane];
-    rj = a.rpos[(size_t)w * MESH_W + lane];
-    if (pull && ej != EMPTY) cj = rcnt[ej & 0xFFFFFFu];
+    ej = a.mesh[(size_t)(a.u0 + w) * MESH_W + lane];
+    rj = a.rpos[(size_t)(a.u0 + w) * MESH_W + lane];
+    if (pull && ej != EMPTY) {
+      cj = rcnt[ej & 0xFFFFFFu];
+      if constexpr (PART) ro = a.roff[ej & 0xFFFFFFu];
+    }
     sv = a.st[(size_t)w * LP_SW + lane];
   }
   for (; w < a.N; w += stride) {
@@ -177,8 +190,8 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     const uint32_t w2 = w + stride;
     uint32_t ej2 = EMPTY, rj2 = 0, cj2 = 0, sv2 = 0;
     if (w2 < a.N && lane < (int)MESH_W) {  // w2 < N is wave-uniform
-      ej2 = a.mesh[(size_t)w2 * MESH_W + lane];
-      rj2 = a.rpos[(size_t)w2 * MESH_W + lane];
+      ej2 = a.mesh[(size_t)(a.u0 + w2) * MESH_W + lane];
+      rj2 = a.rpos[(size_t)(a.u0 + w2) * MESH_W + lane];
       sv2 = a.st[(size_t)w2 * LP_SW + lane];
     }
     const uint64_t cand = __ballot(cj != 0);
@@ -188,14 +201,17 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     if (cand == 0 && due == 0) {  // nothing to apply, nothing due: the pending windows stay
       if (lane == 0) wcnt[w] = 0;
       if (lane < (int)K && sv) nmh = umin32(nmh, lwhi);
-      if (pull && lane < (int)MESH_W && ej2 != EMPTY) cj2 = rcnt[ej2 & 0xFFFFFFu];
-      ej = ej2; rj = rj2; cj = cj2; sv = sv2;
+      if (pull && lane < (int)MESH_W && ej2 != EMPTY) {
+        cj2 = rcnt[ej2 & 0xFFFFFFu];
+        if constexpr (PART) ro2 = a.roff[ej2 & 0xFFFFFFu];
+      }
+      ej = ej2; rj = rj2; cj = cj2; sv = sv2; ro = ro2;
       PP_T(tS);
       PP_ADD(0, tS - tA);
       continue;
     }
     PP_ADD(7, 1);
-    const uint32_t sw = a.stage[w];
+    const uint32_t sw = a.stage[a.u0 + w];
     // final bits transposed: lane j holds bit q for lane q*64 + j (u16 per lane)
     uint32_t finT = reinterpret_cast<const uint16_t*>(a.fin + (size_t)w * LP_FW)[lane];
     // 1. the entries listed for window c (final lanes are dropped in step 3)
@@ -228,16 +244,21 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
       uint64_t cmk = cand;
       while (cmk) {
         uint32_t U[NG], R4[NG], NN[NG], SER[NG];
-        uint64_t BASE[NG];
+        uint64_t BASE[NG], RO[NG];
         uint32_t maxn = 0;
 #pragma unroll
         for (int k = 0; k < (int)NG; k++) {
-          U[k] = 0; R4[k] = 0; NN[k] = 0; SER[k] = 0; BASE[k] = 0;
+          U[k] = 0; R4[k] = 0; NN[k] = 0; SER[k] = 0; BASE[k] = 0; RO[k] = 0;
           if (cmk) {  // wave-uniform
             const int j = __builtin_ctzll(cmk);
             cmk &= cmk - 1;
             const uint32_t e = __builtin_amdgcn_readlane(ej, j);
             U[k] = e & 0xFFFFFFu;
+            if constexpr (PART)
+              RO[k] = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(ro >> 32), j) << 32) |
+                      __builtin_amdgcn_readlane((uint32_t)ro, j);
+            else
+              RO[k] = (uint64_t)U[k] * LL;
             R4[k] = __builtin_amdgcn_readlane(rj, j);
             NN[k] = __builtin_amdgcn_readlane(cj, j);
             const uint32_t su = e >> STAGE_SHIFT;
@@ -253,7 +274,7 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
 #pragma unroll
             for (int cc = 0; cc < (int)RCH; cc++) {
               const uint32_t i = i0 + cc * 64 + lane;
-              rec[k][cc] = i < NN[k] ? rrec[(size_t)U[k] * LL + i] : ~0ull;
+              rec[k][cc] = i < NN[k] ? rrec[RO[k] + i] : ~0ull;
             }
 #pragma unroll
           for (int k = 0; k < (int)NG; k++)
@@ -287,7 +308,10 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     for (int off = 32; off > 0; off >>= 1) cb |= __shfl_xor(cb, off);
     cb = __builtin_amdgcn_readfirstlane(cb);
     wave_lds_sync();
-    if (pull && lane < (int)MESH_W && ej2 != EMPTY) cj2 = rcnt[ej2 & 0xFFFFFFu];  // next row's lists
+    if (pull && lane < (int)MESH_W && ej2 != EMPTY) {  // next row's lists
+      cj2 = rcnt[ej2 & 0xFFFFFFu];
+      if constexpr (PART) ro2 = a.roff[ej2 & 0xFFFFFFu];
+    }
     // 3. classify the minima of the touched chunks: final lanes are dropped
     //    (candidates are not filtered on the way in), a minimum in window c is
     //    final now (logged, marked, its lane / group indexed from the front of
@@ -387,7 +411,7 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
         const uint32_t i = grp * FP + (lane & (FP - 1));
         const uint64_t x = gv ? CW[i] : INF64;  // final lanes were set to INF in step 3
         const uint32_t pm = gv ? a.pub[grp] : EMPTY;
-        const bool act = gv && x != INF64 && ((uint32_t)(x >> 32) - hlo) < hspan && w != pm;
+        const bool act = gv && x != INF64 && ((uint32_t)(x >> 32) - hlo) < hspan && a.u0 + w != pm;
         const uint32_t src = (uint32_t)(x & smask);
         uint32_t js = J_NONE, jp = J_NONE;  // indices of src / publisher in mesh(w)
         uint32_t xm = 0;                    // IDW: every excluded mesh index
@@ -461,7 +485,7 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     for (int q = 0; q < (int)CH; q++)
       if ((cb >> q) & 1u) CW[q * 64 + lane] = INF64;
     wave_lds_sync();
-    ej = ej2; rj = rj2; cj = cj2; sv = sv2;
+    ej = ej2; rj = rj2; cj = cj2; sv = sv2; ro = ro2;
     PP_T(tE);
     PP_ADD(6, tE - tD);
   }
@@ -511,15 +535,17 @@ __global__ void k_lpub(LPullArgs a, uint32_t Fe) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t FP = a.L / a.B;
   if (g >= a.B * Fe) return;
-  const uint32_t m = g / Fe, f = g % Fe, p = a.pub[m], i = m * FP + f;
+  const uint32_t m = g / Fe, f = g % Fe, i = m * FP + f;
+  if (a.pub[m] - a.u0 >= a.N) return;  // partitioned: another part's publisher
+  const uint32_t p = a.pub[m] - a.u0;   // local row
   const uint32_t j = i & 63, q = i >> 6;  // transposed: lane j's u16, bit q
   atomicOr(&a.fin[(size_t)p * LP_FW + (j >> 1)], 1u << (16 * (j & 1) + q));
   if (a.idw) {  // dense keys (IDONTWANT batches)
-    a.keys[(size_t)p * a.L + i] = (uint64_t)p;
+    a.keys[(size_t)p * a.L + i] = (uint64_t)(p + a.u0);
     return;
   }
   const uint32_t pos = atomicAdd(&a.st[(size_t)p * LP_SW + LP_LOG], 1u);
-  a.keys[(size_t)p * a.L + pos] = (uint64_t)p;
+  a.keys[(size_t)p * a.L + pos] = (uint64_t)(p + a.u0);
   a.flane[(size_t)p * a.L + pos] = (uint16_t)i;
 }
 
@@ -646,6 +672,53 @@ __global__ __launch_bounds__(LC_WAVES * 64) void k_lcomplete(LPullArgs a, uint64
 uint32_t lpull_chunks(uint32_t L) {
   const char* e = getenv("GS_LPULL_CH");  // per launch: A/B scripts switch it in one process
   return (L <= 512 && !(e && atoi(e) == 16)) ? 8u : 16u;
+}
+
+// Partitioned pass: this part's records of the pass (lrec[nb] / lcnt[nb], by
+// local row) packed for the exchange: out[...] holds them row after row in
+// the order rows claim space (one atomic per wave of 64 rows), and roff[r] =
+// base + the row's offset, base = this part's offset in the packed records of
+// all parts (the host knows every part's total after the pass).
+__global__ __launch_bounds__(TB) void k_lpack(const uint64_t* __restrict__ rec, const uint32_t* __restrict__ cnt,
+                                              uint32_t N, uint32_t L, uint64_t base, uint64_t* __restrict__ out,
+                                              uint64_t* __restrict__ roff, unsigned long long* cursor) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = blockIdx.x * (TB / 64) + (threadIdx.x >> 6), nw = gridDim.x * (TB / 64);
+  for (uint32_t r0 = wave * 64; r0 < N; r0 += nw * 64) {
+    const uint32_t r = r0 + lane;
+    const uint32_t n = r < N ? cnt[r] : 0;
+    uint32_t x = n;  // inclusive prefix over the wave's 64 rows
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = __shfl_up(x, off);
+      if (lane >= off) x += y;
+    }
+    const uint32_t tot = __shfl(x, 63);
+    unsigned long long b0 = 0;
+    if (lane == 0 && tot) b0 = atomicAdd(cursor, (unsigned long long)tot);
+    const uint64_t wb = ((uint64_t)__shfl((uint32_t)(b0 >> 32), 0) << 32) | __shfl((uint32_t)b0, 0);
+    const uint64_t my = wb + x - n;
+    if (r < N) roff[r] = base + my;
+    for (int j = 0; j < 64; j++) {  // copy row by row, 64 records per step
+      const uint32_t nj = __shfl(n, j);
+      const uint64_t oj = ((uint64_t)__shfl((uint32_t)(my >> 32), j) << 32) | __shfl((uint32_t)my, j);
+      for (uint32_t i = lane; i < nj; i += 64) out[oj + i] = rec[(size_t)(r0 + j) * L + i];
+    }
+  }
+}
+
+void lpull_dispatch_part(uint32_t FP, const LPullArgs& a, unsigned grid, hipStream_t s) {
+  const bool ch8 = lpull_chunks(a.L) == 8;
+#define GS_LPP(F)                                                      \
+  if (ch8) k_lpull<F, 8, false, true><<<grid, TB, 0, s>>>(a);           \
+  else k_lpull<F, 16, false, true><<<grid, TB, 0, s>>>(a);
+  switch (FP) {
+    case 1: GS_LPP(1) break;
+    case 2: GS_LPP(2) break;
+    case 4: GS_LPP(4) break;
+    case 8: GS_LPP(8) break;
+    default: GS_LPP(16) break;
+  }
+#undef GS_LPP
 }
 
 void lpull_dispatch(uint32_t FP, const LPullArgs& a, unsigned grid, hipStream_t s) {

@@ -350,7 +350,8 @@ void part_set(Ctx& c, uint32_t parts, uint32_t part) {
   c.part_un = (uint32_t)((uint64_t)(part + 1) * N / parts) - c.part_u0;
 }
 
-uint64_t part_begin(Ctx& c, const gs_publish* sched, uint64_t n_msgs) {
+// The knobs a partitioned batch accepts (both protocols).
+static uint32_t part_check(Ctx& c, const gs_publish* sched, uint64_t n_msgs) {
   if (c.part_un == 0) part_set(c, 1, 0);
   if (c.part_open) c.fail(GS_ESTATE, "a partitioned batch is in flight (gs_part_finish first)");
   if (n_msgs < 1 || n_msgs > c.cfg.batch) c.fail(GS_EINVAL, "partitioned batch needs 1..cfg.batch messages");
@@ -363,6 +364,11 @@ uint64_t part_begin(Ctx& c, const gs_publish* sched, uint64_t n_msgs) {
   if (c.traffic) c.fail(GS_EUNSUPPORTED, "per-peer traffic is not supported in partitioned mode");
   if (c.cfg.idontwant && frag_payload(c.cfg.node, sched[0].msg_size, F) >= c.cfg.idontwant)
     c.fail(GS_EUNSUPPORTED, "IDONTWANT is not supported in partitioned mode");
+  return F;
+}
+
+uint64_t part_begin(Ctx& c, const gs_publish* sched, uint64_t n_msgs) {
+  const uint32_t F = part_check(c, sched, n_msgs);
   const uint32_t FP = pow2_at_least(F), Bmax = c.cfg.batch, un = c.part_un;
   if ((uint64_t)un * Bmax * FP >= (1ull << 32)) c.fail(GS_EUNSUPPORTED, "partition needs own peers*batch*FP < 2^32");
   hipStream_t s = c.stream;
@@ -611,4 +617,170 @@ void part_finish(Ctx& c, const gs_result_sink* sink) {
   deliver(c, b, c.part_u0, c.part_un, sink, 0);
   c.stats.messages += b.B;
   collect_stats(c);
+}
+
+// ---- the list pass over partitioned rows (gs_run_partitioned) ----
+// Every part runs k_lpull<.., PART> over its own rows [u0, u0 + un) with the
+// list path's per-row buffers sized for those rows; after each pass the host
+// combines the parts' pass control (records emitted, min pending key, error
+// word), every part packs its records (k_lpack) and the packed records, the
+// per-peer counts and offsets are exchanged (gs_comm.hip), so that the next
+// pass reads any neighbour's records exactly as gs_run's pass does.
+
+static LPullArgs part_lp_args(Ctx& c) {
+  const Batch& b = c.part_b;
+  const uint32_t un = c.part_un, L = b.L;
+  LPullArgs la{};
+  la.keys = c.d_keys.p; la.flane = c.d_flane.p; la.busy = c.d_busy.p; la.blk = c.d_lblk.p;
+  la.st = c.d_lst.p; la.fin = c.d_lfin.p; la.lrec = c.d_lrec.p; la.lcnt = c.d_lcnt.p;
+  la.rpos = c.d_rpos.p; la.mesh = c.d_mesh.p; la.pub = c.d_pub.p; la.stage = c.d_stage.p;
+  la.tables = c.d_tables.p; la.ctrl = c.d_pctrl.p; la.counters = c.d_counters.p;
+  const uint64_t grain = pull_grain(b.tshift);
+  la.delta = b.delta / grain * grain;
+  la.tmax = b.tmax - grain;
+  la.N = un; la.B = b.B; la.L = L; la.S = c.S; la.sb = b.sb; la.tshift = b.tshift;
+  la.K = c.part_lpK; la.lb = c.part_lplb; la.dG = (uint32_t)(la.delta / grain);
+  la.ls = lpull_stride(b);
+  const char* cap = getenv("GS_LPULL_CAP");
+  la.lcap = cap && *cap ? (uint32_t)std::min<long>(std::max(1, atoi(cap)), (long)la.ls) : la.ls;
+  la.u0 = c.part_u0;
+  la.rpk = c.d_rpk.p; la.roff = c.d_roffg.p; la.rcg = c.d_rcg.p;
+  la.pass = c.part_lppass;
+  return la;
+}
+
+bool part_lp_begin(Ctx& c, const gs_publish* sched, uint64_t n_msgs, uint64_t* seed_min) {
+  const uint32_t F = part_check(c, sched, n_msgs);
+  (void)F;
+  const char* ve = getenv("GS_RELAX_VARIANT");  // without bit 64 (or GS_PART_PUSH) the push protocol runs
+  if ((ve && *ve && !(atoi(ve) & 64)) || getenv("GS_PART_PUSH")) return false;
+  hipStream_t s = c.stream;
+  GS_HIP(hipMemsetAsync(c.d_counters.p + C_ERR, 0, 8, s));
+  ensure_cus(c);
+  const uint32_t N = c.cfg.peers, un = c.part_un, Bmax = c.cfg.batch;
+  c.part_b = setup_batch(c, sched, 0, n_msgs);
+  const Batch& b = c.part_b;
+  if (b.L > PULL_LMAX || b.delta < pull_grain(b.tshift)) return false;
+  uint32_t lb = 0;
+  const uint64_t grain = pull_grain(b.tshift);
+  const uint32_t K = lpull_ring(c, b, b.delta / grain * grain, &lb);
+  if (!K) return false;
+  c.part_lpK = K;
+  c.part_lplb = lb;
+  c.part_lppass = 0;
+  const size_t NL = (size_t)un * b.L;
+  const uint32_t ls = lpull_stride(b);
+  c.d_keys.alloc(NL);
+  c.d_flane.alloc(NL);
+  c.d_lrec.alloc(2 * NL);
+  c.d_lcnt.alloc(2 * (size_t)un);
+  c.d_lblk.alloc((size_t)K * un * ls);
+  c.d_lst.alloc((size_t)un * LP_SW);
+  c.d_lfin.alloc((size_t)un * LP_FW);
+  c.d_pctrl.alloc(12);
+  c.d_rcg.alloc(N);
+  c.d_roffg.alloc(N);
+  c.d_rpk.alloc(1);
+  c.d_pkroff.alloc(un);
+  c.d_pkcur.alloc(1);
+  if (b.FP > 1) c.d_busy.alloc((size_t)un * Bmax);
+  c.d_tc.alloc((size_t)un * Bmax);
+  c.d_hops.alloc((size_t)un * Bmax);
+  if (!c.rpos_valid) {
+    c.d_rpos.alloc((size_t)N * MESH_W);
+    k_rpos<<<(unsigned)(((uint64_t)N * MESH_W + TB - 1) / TB), TB, 0, s>>>(c.d_mesh.p, c.d_rpos.p, N, c.d_counters.p);
+    GS_HIP(hipGetLastError());
+    if (read_counter(c, C_ERR) & ERR_MESH) c.fail(GS_ERANGE, "mesh is not symmetric");
+    c.rpos_valid = true;
+  }
+  c.keys_log = false;
+  if (b.FP > 1) GS_HIP(hipMemsetAsync(c.d_busy.p, 0, (size_t)un * b.B * 8, s));
+  GS_HIP(hipMemsetAsync(c.d_lst.p, 0, (size_t)un * LP_SW * 4, s));
+  GS_HIP(hipMemsetAsync(c.d_lfin.p, 0, (size_t)un * LP_FW * 4, s));
+  GS_HIP(hipMemsetAsync(c.d_pctrl.p, 0, 12 * 8, s));
+  for (int q = 0; q < 3; q++) GS_HIP(hipMemsetAsync(c.d_pctrl.p + q * 4 + 3, 0xFF, 8, s));
+  c.d_lp_save.alloc(C_COUNT);
+  GS_HIP(hipMemcpyAsync(c.d_lp_save.p, c.d_counters.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));
+  const uint64_t scap = (uint64_t)b.B * b.Fe * std::max<uint64_t>(c.max_degree, MESH_W);
+  c.d_skey.alloc(scap);
+  c.d_slane.alloc(scap);
+  c.d_scnt.alloc(1);
+  GS_HIP(hipMemsetAsync(c.d_scnt.p, 0, 4, s));
+  launch_seed(c, b, c.part_u0, un, c.d_pctrl.p + 2 * 4 + 3, nullptr, true);
+  const LPullArgs la = part_lp_args(c);
+  k_lseed<<<(unsigned)std::max<uint64_t>(1, std::min<uint64_t>((scap + TB - 1) / TB, (uint64_t)c.num_cus * 4)), TB, 0,
+            s>>>(la, c.d_skey.p, c.d_slane.p, c.d_scnt.p);
+  k_lpub<<<(b.B * b.Fe + 255) / 256, 256, 0, s>>>(la, b.Fe);
+  GS_HIP(hipGetLastError());
+  uint64_t auto_bpc = 4;  // as run_lpull_batch: whole blocks per CU by the rows this part owns
+  while (auto_bpc < 16 && (uint64_t)un >= (uint64_t)c.num_cus * PULL_WAVES * 32 * auto_bpc * 2) auto_bpc *= 2;
+  c.part_lpgrid = (unsigned)std::max<uint64_t>(
+      1, std::min<uint64_t>(((uint64_t)un + PULL_WAVES - 1) / PULL_WAVES, (uint64_t)c.num_cus * auto_bpc));
+  GS_HIP(hipMemcpyAsync(c.h_pinned, c.d_pctrl.p + 2 * 4 + 3, 8, hipMemcpyDeviceToHost, s));
+  GS_HIP(hipStreamSynchronize(s));
+  *seed_min = c.h_pinned[0];
+  c.part_lp = true;
+  c.part_open = true;
+  return true;
+}
+
+// The combined pass control into the slot the next pass decides from (slot of the last pass).
+void part_lp_set(Ctx& c, uint64_t records, uint64_t minp) {
+  const uint32_t slot = (c.part_lppass + 2) % 3;  // the last pass's slot (seeds: slot 2 before pass 0)
+  c.h_pinned[24] = records;
+  c.h_pinned[25] = minp;
+  GS_HIP(hipMemcpyAsync(c.d_pctrl.p + slot * 4 + 2, c.h_pinned + 24, 16, hipMemcpyHostToDevice, c.stream));
+  GS_HIP(hipStreamSynchronize(c.stream));  // the staging words are reused by the next pass
+}
+
+void part_lp_pass(Ctx& c) {
+  const LPullArgs la = part_lp_args(c);
+  lpull_dispatch_part(c.part_b.FP, la, c.part_lpgrid, c.stream);
+  GS_HIP(hipGetLastError());
+  c.part_lppass++;
+  c.stats.relax_launches++;
+}
+
+void part_lp_read(Ctx& c, uint64_t out[4]) {
+  const uint32_t slot = (c.part_lppass + 2) % 3;
+  GS_HIP(hipMemcpyAsync(c.h_pinned, c.d_pctrl.p + slot * 4, 32, hipMemcpyDeviceToHost, c.stream));
+  GS_HIP(hipMemcpyAsync(c.h_pinned + 4, c.d_counters.p + C_ERR, 8, hipMemcpyDeviceToHost, c.stream));
+  GS_HIP(hipStreamSynchronize(c.stream));
+  out[0] = c.h_pinned[1];
+  out[1] = c.h_pinned[2];
+  out[2] = c.h_pinned[3];
+  out[3] = c.h_pinned[4];
+}
+
+const uint32_t* part_lp_counts(Ctx& c) { return c.d_lcnt.p + (size_t)((c.part_lppass + 1) & 1) * c.part_un; }
+
+void part_lp_pack(Ctx& c, uint64_t base, uint64_t mine) {
+  const uint32_t un = c.part_un, L = c.part_b.L;
+  c.d_pkout.alloc(std::max<uint64_t>(mine, 1));
+  hipStream_t s = c.stream;
+  GS_HIP(hipMemsetAsync(c.d_pkcur.p, 0, 8, s));
+  const uint32_t nb = (c.part_lppass + 1) & 1;  // the last pass wrote lrec / lcnt [pass & 1]
+  const unsigned grid = (unsigned)std::max<uint64_t>(
+      1, std::min<uint64_t>(((uint64_t)un + 255) / 256, (uint64_t)c.num_cus * 8));
+  k_lpack<<<grid, TB, 0, s>>>(c.d_lrec.p + (size_t)nb * un * L, c.d_lcnt.p + (size_t)nb * un, un, L, base,
+                              c.d_pkout.p, c.d_pkroff.p, (unsigned long long*)c.d_pkcur.p);
+  GS_HIP(hipGetLastError());
+}
+
+bool part_lp_end(Ctx& c, bool hist) {
+  const LPullArgs la = part_lp_args(c);
+  k_lfinal<<<c.part_lpgrid, TB, 0, c.stream>>>(la);  // final logs -> dense rows of own peers
+  GS_HIP(hipGetLastError());
+  c.stats.list_pull_batches++;
+  c.part_lp = false;
+  return part_dev_complete(c, hist);
+}
+
+void part_lp_abort(Ctx& c) {  // the batch re-runs on the push protocol: counters as before the batch
+  if (c.part_lp) {
+    GS_HIP(hipMemcpyAsync(c.d_counters.p, c.d_lp_save.p, C_COUNT * 8, hipMemcpyDeviceToDevice, c.stream));
+    GS_HIP(hipStreamSynchronize(c.stream));
+  }
+  c.part_lp = false;
+  c.part_open = false;
 }

@@ -1229,7 +1229,13 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     // the push path with gossip. Under churn some peers never
     // complete, so the proof cannot hold and gossip runs directly.
     const bool idw_b = c.cfg.idontwant && b.payload >= c.cfg.idontwant;  // IDONTWANT active in this batch
-    const bool pull_ok = pull_any && b.delta >= pull_grain(b.tshift) && (!idw_b || (b.FP == 1 && (variant & 64)));
+    // IDONTWANT on the list pass: windows no wider than the smallest latency, so
+    // that a neighbour's key final in the same window as the sender's can never
+    // pass the test t_y + lat(y -> u) <= t_u (the sender cannot see it yet);
+    // keys of earlier windows are final and stored before the pass starts
+    Batch bw = b;
+    if (idw_b) bw.delta = std::min(b.delta, b.lat_min);
+    const bool pull_ok = pull_any && bw.delta >= pull_grain(b.tshift) && (!idw_b || (b.FP == 1 && (variant & 64)));
     bool done = false;
     if (pull_ok || (gossip && !churn)) {
       if (gossip) GS_HIP(hipMemcpyAsync(c.d_cnt_save.p, c.d_counters.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));
@@ -1239,7 +1245,7 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
         // list path for single-fragment batches; fragmented ones (FP > 1) only
         // with bit 128 (k_pull's dense rows measured 7 % faster on config #2)
         const bool lp = (variant & 64) && (b.FP == 1 || (variant & 128));
-        const uint32_t K = lp ? lpull_ring(c, b, b.delta / grain * grain, &lb) : 0u;
+        const uint32_t K = lp ? lpull_ring(c, bw, bw.delta / grain * grain, &lb) : 0u;
         reset(variant, false, K == 0 || idw_b);  // IDONTWANT: dense INF keys
         if (lp && !K && getenv("GS_REQUIRE_LPULL"))  // test knob: no silent k_pull fallback
           c.fail(GS_EUNSUPPORTED, "list pull path cannot take this batch (GS_REQUIRE_LPULL)");
@@ -1247,7 +1253,7 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
         // stream calibrates the PMC read factor (scripts/pmc_summary.py);
         // IDONTWANT batches keep their final keys dense all along
         const bool dense = !idw_b && (sink != nullptr || c.traffic || b.FP > 1 || getenv("GS_LPULL_DENSE"));
-        if (!K || !run_lpull_batch(c, b, K, lb, ev, n_ev, dev_cus, dense, idw_b)) {
+        if (!K || !run_lpull_batch(c, bw, K, lb, ev, n_ev, dev_cus, dense, idw_b)) {
           if (K && getenv("GS_REQUIRE_LPULL")) c.fail(GS_EUNSUPPORTED, "list pull overflow (GS_REQUIRE_LPULL)");
           if (idw_b) {  // k_pull has no IDONTWANT: the push path takes the batch
             push_run(variant & ~32u, false);

@@ -131,6 +131,52 @@ def test_run_partitioned_local_comm_equals_gs_run(parts, frags, batch):
     comm.close()
 
 
+@pytest.mark.parametrize("push", [False, True])
+@pytest.mark.parametrize("parts,frags,batch", [(2, 1, 64), (5, 2, 32), (8, 1, 1024)])
+def test_run_partitioned_list_pass_and_push_protocol(monkeypatch, push, parts, frags, batch):
+    """gs_run_partitioned runs each part's rows on the list pass (records
+    exchanged between passes) — or, with GS_PART_PUSH, on the push protocol —
+    bit-identical to gs_run and the oracle; uneven part sizes, fragments, rows
+    of 1024 lanes."""
+    if push:
+        monkeypatch.setenv("GS_PART_PUSH", "1")
+    N = 3001
+    p = oracle.params(peers=N, seed=65, fragments=frags)
+    sched = _sched(batch, N)
+    ref, rst = _whole(p, 5, (50, 150, 40, 130), sched, batch)
+    sims = _parts(p, 5, (50, 150, 40, 130), parts, batch)
+    comm = gossipsim.Comm(local_parts=parts)
+    res = comm.run_partitioned(sims, sched)
+    np.testing.assert_array_equal(np.concatenate([r["t_complete"] for r in res], axis=1), ref["t_complete"])
+    np.testing.assert_array_equal(np.concatenate([r["hops"] for r in res], axis=1), ref["hops"])
+    st = [s.stats() for s in sims]
+    for k in ("deliveries", "frag_deliveries", "relaxations", "latency_sum_ms"):
+        assert sum(x[k] for x in st) == rst[k], k
+    assert all((x["list_pull_batches"] > 0) != push for x in st)
+    if not push and batch <= 64:
+        ora = oracle.simulate(p, 5, (50, 150, 40, 130), sched=sched)
+        np.testing.assert_array_equal(ref["t_complete"], ora["t_complete"])
+    comm.close()
+
+
+def test_run_partitioned_list_overflow_falls_back_to_push(monkeypatch):
+    """Candidate lists capped at 2 entries: some part overflows, every part
+    restores its counters and the batch runs on the push protocol."""
+    monkeypatch.setenv("GS_LPULL_CAP", "2")
+    N = 2500
+    p = oracle.params(peers=N, seed=66)
+    sched = _sched(128, N)
+    ref, rst = _whole(p, 5, (50, 150, 40, 130), sched, 128)
+    sims = _parts(p, 5, (50, 150, 40, 130), 3, 128)
+    comm = gossipsim.Comm(local_parts=3)
+    res = comm.run_partitioned(sims, sched)
+    np.testing.assert_array_equal(np.concatenate([r["t_complete"] for r in res], axis=1), ref["t_complete"])
+    st = [s.stats() for s in sims]
+    assert sum(x["relaxations"] for x in st) == rst["relaxations"]
+    assert all(x["list_pull_batches"] == 0 for x in st)
+    comm.close()
+
+
 @pytest.mark.parametrize("N,M", [(2000, 12), (100_000, 64)])
 def test_run_partitioned_rccl_single_rank(N, M):
     """gs_comm_init over RCCL with one rank on this GPU (the N = 1 case of the
