@@ -392,8 +392,8 @@ def main():
         try:
             tj = json.load(open(args.traffic_json))
             # PMC bytes only for the very kernel this line names (one kernel, same template)
-            same_kernel = bool(tj.get("kernels")) and " + " not in kernel and \
-                all(k.startswith(kernel.split(" ")[0]) for k in tj["kernels"])
+            same_kernel = bool(tj.get("kernels")) and " + " not in kernel and args.mode == tj.get("mode", "msg") \
+                and all(k.startswith(kernel.split(" ")[0]) for k in tj["kernels"])
             if tj.get("peers") == args.peers and tj.get("batch") == args.batch and same_kernel:
                 traffic = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
