@@ -479,3 +479,34 @@ def test_churn_snapshots_invariants():
             assert (r["t_complete"][m] == np.iinfo(np.uint64).max).all()
         else:
             assert r["t_complete"][m, pub[m]] == t[m]
+
+
+@pytest.mark.parametrize("name,sub,epochs", [("uniform_n300", 1, 65), ("uniform_n300", 0, 7),
+                                             ("hetero_n400_f4", 1, 6), ("hetero_n400_f4", 0, 67)])
+def test_convergence_epochs_follow_the_prune_backoff(name, sub, epochs):
+    """Why the committed fixtures' convergence epochs moved when subscription
+    grafting was switched on (7 -> 65 uniform, 67 -> 6 heterogeneous): on
+    uniform links every subscription arrives at the same instant, so each peer
+    grafts its D_lo lowest-id connections; the low ids collect more GRAFTs than
+    D_hi, reject the peers they did not dial, and each rejection is a PRUNE with
+    the 60-heartbeat back-off (main.rs:229) — the mesh settles only after the
+    back-offs expire (> 60 epochs). On heterogeneous links the handshake order
+    spreads the grafts by latency and nothing waits for a back-off, while the
+    random heartbeat grafts of the other start do trip one."""
+    import json
+    meta = json.load(open(os.path.join(GOLDEN, "oracle_%s.json" % name)))
+    kw = dict(meta["params"], sub_graft=sub)
+    p = oracle.params(**kw)
+    S = meta["stages"]
+    lat, _ = oracle.topogen_links(S, *meta["links"])
+    stage = (np.arange(p.peers) % S).astype(np.uint8)
+    row, col, flags0 = oracle.build_topology(p)
+    _, _, _, ep = oracle.mesh_converge(p, row, col, flags0, stage, lat)
+    assert ep == epochs
+    backoff = p.backoff_ns // p.heartbeat_ns
+    assert (ep > backoff) == (epochs > 60)
+    if sub and S == 1:  # the epoch-0 grafts all go to the lowest ids
+        row = row.astype(np.int64)
+        out = set((u, int(col[e])) for u in range(p.peers) for e in range(row[u], row[u + 1]) if flags0[e] & 1)
+        mesh0 = _py_subscription_epoch(p, row, col, out, stage, lat)
+        assert max(len(m) for m in mesh0[:10]) > p.d_hi  # popular low ids hold more than D_hi before heartbeat 1
