@@ -644,6 +644,7 @@ static LPullArgs part_lp_args(Ctx& c) {
   const char* cap = getenv("GS_LPULL_CAP");
   la.lcap = cap && *cap ? (uint32_t)std::min<long>(std::max(1, atoi(cap)), (long)la.ls) : la.ls;
   la.u0 = c.part_u0;
+  la.rmax = lpull_rmax(b);
   la.rpk = c.d_rpk.p; la.roff = c.d_roffg.p; la.rcg = c.d_rcg.p;
   la.pass = c.part_lppass;
   return la;

@@ -799,6 +799,10 @@ static void run_pull_batch(Ctx& c, const Batch& b, EvFn& ev, size_t& n_ev, int d
   c.stats.relax_launches += pass;
 }
 
+// Largest arrival offset of a forward relative to its uplink start: latency +
+// downlink excess + MESH_W serialisations (the receiver's FIFO position).
+static uint64_t lpull_rmax(const Batch& b) { return b.lat_adj_max + (uint64_t)MESH_W * b.ser_max; }
+
 // Entries per candidate list: at least 256, so that rows of few lanes (small
 // batches) still hold several passes' appends of the same lanes.
 static uint32_t lpull_stride(const Batch& b) { return std::max<uint32_t>(b.L, 256); }
@@ -905,6 +909,7 @@ static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvF
   la.N = N; la.B = b.B; la.L = L; la.S = c.S; la.sb = b.sb; la.tshift = b.tshift;
   la.K = K; la.lb = lb; la.dG = (uint32_t)(la.delta / grain);
   la.idw = idw ? 1u : 0u;
+  la.rmax = lpull_rmax(b);
   const char* cap = getenv("GS_LPULL_CAP");  // test knob: small lists force the overflow re-run
   la.ls = ls;
   la.lcap = cap && *cap ? (uint32_t)std::min<long>(std::max(1, atoi(cap)), (long)ls) : ls;
