@@ -109,7 +109,7 @@ struct LPullLds {
 // Record step: groups of NG = 4 neighbours, RCH = 2 chunks of 64 records each
 // per iteration (8 loads in flight per lane; 8 x 64 measured 2 % slower,
 // profiles/r03_v1/ab_record_groups.txt).
-template <int FP, uint32_t CH, bool IDW = false, bool PART = false, bool OLDREC = false>
+template <int FP, uint32_t CH, bool IDW = false, bool PART = false>
 __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
   constexpr uint32_t NG = 4, RCH = 2;
   static_assert(!IDW || FP == 1, "IDONTWANT on the list pass: rows of single-fragment lanes");
@@ -284,49 +284,27 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
             for (int cc = 0; cc < (int)RCH; cc++) {
               const uint64_t rc = rec[k][cc];
               const uint32_t lo32 = (uint32_t)rc, r = R4[k];
-              if constexpr (OLDREC) {  // A/B reference: branch per test, time check per record
-                if (rc == ~0ull) continue;  // no record (records never have all bits set)
-                uint32_t slot, pos;
-                if constexpr (IDW) {
-                  const uint32_t xm = (lo32 >> 10) & 0xFFFFu;
-                  if ((xm >> r) & 1u) continue;
-                  slot = lo32 & 0x3FFu;
-                  pos = r + 1 - (uint32_t)__popc(xm & ((1u << r) - 1u));
-                } else {
-                  const uint32_t js = (lo32 >> 21) & 31u, jp = (lo32 >> 16) & 31u;
-                  if (js == r || jp == r) continue;
-                  slot = lo32 & 0xFFFFu;
-                  pos = r + 1 - (js < r ? 1u : 0u) - ((jp < r && jp != js) ? 1u : 0u);
-                }
-                const uint64_t arr = BASE[k] + (rc >> 32) + (uint64_t)(pos * SER[k]);
-                if (arr > a.tmax) err |= ERR_TIME;
-                const uint64_t hp1 = ((lo32 >> 26) & hmask) + 1;
-                const uint64_t nk = (arr << a.tshift) | (hp1 << a.sb) | U[k];
-                atomicMin((unsigned long long*)&CW[slot], (unsigned long long)nk);
-                cb |= 1u << (slot >> 6);
+              // one predicate per record: no record (~0, lane field all ones),
+              // or w is excluded (source / publisher / IDONTWANT); the time
+              // field cannot overflow (the sender checked start + rmax)
+              uint32_t slot, pos;
+              bool ok;
+              if constexpr (IDW) {  // exclusion mask of the sender's row
+                const uint32_t xm = (lo32 >> 10) & 0xFFFFu;
+                slot = lo32 & 0x3FFu;
+                ok = rc != ~0ull && !((xm >> r) & 1u);
+                pos = r + 1 - (uint32_t)__popc(xm & ((1u << r) - 1u));
               } else {
-                // one predicate per record: no record (~0, lane field all ones),
-                // or w is excluded (source / publisher / IDONTWANT); the time
-                // field cannot overflow (the sender checked start + rmax)
-                uint32_t slot, pos;
-                bool ok;
-                if constexpr (IDW) {  // exclusion mask of the sender's row
-                  const uint32_t xm = (lo32 >> 10) & 0xFFFFu;
-                  slot = lo32 & 0x3FFu;
-                  ok = rc != ~0ull && !((xm >> r) & 1u);
-                  pos = r + 1 - (uint32_t)__popc(xm & ((1u << r) - 1u));
-                } else {
-                  const uint32_t js = (lo32 >> 21) & 31u, jp = (lo32 >> 16) & 31u;
-                  slot = lo32 & 0xFFFFu;
-                  ok = slot != 0xFFFFu && js != r && jp != r;  // w is the source or the publisher
-                  pos = r + 1 - (js < r ? 1u : 0u) - ((jp < r && jp != js) ? 1u : 0u);
-                }
-                const uint64_t arr = BASE[k] + (rc >> 32) + (uint64_t)(pos * SER[k]);
-                const uint32_t low = ((((lo32 >> 26) & hmask) + 1) << a.sb) | U[k];  // hops + 1 | src (< 2^tshift)
-                const uint64_t nk = (arr << a.tshift) | low;
-                if (ok) atomicMin((unsigned long long*)&CW[slot], (unsigned long long)nk);
-                cb |= ok ? 1u << (slot >> 6) : 0u;
+                const uint32_t js = (lo32 >> 21) & 31u, jp = (lo32 >> 16) & 31u;
+                slot = lo32 & 0xFFFFu;
+                ok = slot != 0xFFFFu && js != r && jp != r;  // w is the source or the publisher
+                pos = r + 1 - (js < r ? 1u : 0u) - ((jp < r && jp != js) ? 1u : 0u);
               }
+              const uint64_t arr = BASE[k] + (rc >> 32) + (uint64_t)(pos * SER[k]);
+              const uint32_t low = ((((lo32 >> 26) & hmask) + 1) << a.sb) | U[k];  // hops + 1 | src (< 2^tshift)
+              const uint64_t nk = (arr << a.tshift) | low;
+              if (ok) atomicMin((unsigned long long*)&CW[slot], (unsigned long long)nk);
+              cb |= ok ? 1u << (slot >> 6) : 0u;
             }
         }
       }
@@ -748,13 +726,6 @@ void lpull_dispatch_part(uint32_t FP, const LPullArgs& a, unsigned grid, hipStre
 }
 
 void lpull_dispatch(uint32_t FP, const LPullArgs& a, unsigned grid, hipStream_t s) {
-  {
-    const char* e = getenv("GS_LPULL_OLDREC");  // A/B knob (r03): the previous record step
-    if (e && *e && atoi(e) && FP == 1 && !a.idw && lpull_chunks(a.L) == 16) {
-      k_lpull<1, 16, false, false, true><<<grid, TB, 0, s>>>(a);
-      return;
-    }
-  }
   if (a.idw) {  // FP == 1 (the host sends fragmented IDONTWANT batches to the push path)
     if (lpull_chunks(a.L) == 8) k_lpull<1, 8, true><<<grid, TB, 0, s>>>(a);
     else k_lpull<1, 16, true><<<grid, TB, 0, s>>>(a);
