@@ -384,7 +384,8 @@ def main():
     else:
         pull = st["relax_ms"] > 0 and st["scan_ms"] <= 0.01 * st["relax_ms"]
         lpull = pull and st.get("list_pull_batches", 0) > 0
-        kernel = ("k_lpull<%d>" % fpl) if lpull else ("k_pull<%d>" % fpl) if pull else \
+        ch = 8 if args.batch * fpl <= 512 else 16  # 64-lane chunks per row (gs_lpull_kernel.h lpull_chunks)
+        kernel = ("k_lpull<%d, %d>" % (fpl, ch)) if lpull else ("k_pull<%d>" % fpl) if pull else \
             "k_scan<%d,false,false> + k_frontier<%d,true,false>" % (fpl, fpl)
     achieved = st["relax_bytes_alg"] / (st["relax_ms"] / 1e3) / 1e9 if st["relax_ms"] > 0 else None
     traffic = None
@@ -392,8 +393,12 @@ def main():
         try:
             tj = json.load(open(args.traffic_json))
             # PMC bytes only for the very kernel this line names (one kernel, same template)
+            def targs(k):  # "k_lpull<1, 16u, false, false>" -> ("k_lpull", ["1", "16"])
+                name, _, rest = k.partition("<")
+                return name, [x.strip().rstrip("u") for x in rest.rstrip(">").split(",")]
+            kn, ka = targs(kernel.split(" ")[0] if " + " not in kernel else "")
             same_kernel = bool(tj.get("kernels")) and " + " not in kernel and args.mode == tj.get("mode", "msg") \
-                and all(k.startswith(kernel.split(" ")[0]) for k in tj["kernels"])
+                and all(targs(k)[0] == kn and targs(k)[1][:len(ka)] == ka for k in tj["kernels"])
             if tj.get("peers") == args.peers and tj.get("batch") == args.batch and same_kernel:
                 traffic = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):

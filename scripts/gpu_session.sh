@@ -18,7 +18,7 @@ step() {  # name seconds cmd...
   case $rc in 124|134|137|139) echo "fatal rc=$rc in $name: stopping"; exit $rc;; esac
   return 0
 }
-PROFARGS="--steps ${PROF_STEPS:-6} --warmup 2 --cpu-seconds 0 --also-peers 0 --configs 0 --gossip-check 0"
+PROFARGS="--steps ${PROF_STEPS:-6} --warmup 2 --cpu-seconds 0 --also-peers 0 --configs 0 --gossip-check 0 --output-steps 0"
 KRE="k_lpull|k_pull|k_scan|k_frontier|k_complete|k_lcomplete"
 for s in ${STEPS:-tests smoke bench prof}; do
   case $s in
