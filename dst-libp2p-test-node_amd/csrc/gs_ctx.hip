@@ -1,6 +1,7 @@
 // gs_ctx.hip — C-ABI entry points of libgossipsim (include/gossipsim.h):
 // context lifecycle, argument validation, error capture. No exception crosses
 // the ABI; every failure becomes a gs_status plus gs_last_error text.
+#include <stdio.h>
 #include <string.h>
 
 #include <algorithm>
@@ -225,6 +226,12 @@ extern "C" gs_status gs_get_stats(const gs_ctx* ctx, gs_stats* out) {
   return GS_OK;
 }
 
+extern "C" gs_status gs_get_config(const gs_ctx* ctx, gs_config* out) {
+  if (!ctx || !out) return GS_EINVAL;
+  *out = ctx->cfg;
+  return GS_OK;
+}
+
 extern "C" gs_status gs_reset_stats(gs_ctx* ctx) {
   GS_API_BEGIN(ctx)
   GS_HIP(hipSetDevice(ctx->cfg.device));
@@ -306,4 +313,158 @@ extern "C" gs_status gs_part_finish(gs_ctx* ctx, const gs_result_sink* sink) {
   GS_HIP(hipSetDevice(ctx->cfg.device));
   part_finish(*ctx, sink);
   GS_API_END(ctx)
+}
+
+// ---- checkpoint / resume (include/gossipsim.h gs_save_state) ----
+// The file holds what a later gs_run reads: the configuration, the link
+// tables, the CSR with its outbound / mesh flags, reverse entries and PRUNE
+// back-offs, the mesh ELL, the churn mesh state's epoch, the counters (host and
+// device) and the
+// per-peer traffic. Every random draw is a pure function of (seed, purpose,
+// ...), so there is no generator state to keep. Churn snapshots cached in the
+// ring are not saved: a restored context recomputes any epoch at or before the
+// saved state by a replay from epoch 0, which gives the same snapshots.
+namespace {
+const char kStateMagic[8] = {'G', 'S', 'I', 'M', 'S', 'T', '0', '1'};
+
+struct StateFile {
+  FILE* f = nullptr;
+  ~StateFile() { if (f) fclose(f); }
+};
+
+void put(FILE* f, const void* p, size_t n) {
+  if (n && fwrite(p, 1, n, f) != n) throw Error(GS_EINVAL, "cannot write the state file");
+}
+void get(FILE* f, void* p, size_t n) {
+  if (n && fread(p, 1, n, f) != n) throw Error(GS_EINVAL, "truncated state file");
+}
+template <class T>
+void put_dev(Ctx& c, FILE* f, const DevBuf<T>& b, size_t n) {
+  std::vector<T> h(n);
+  if (n) {
+    if (!b.p || b.n < n) throw Error(GS_ESTATE, "internal: state buffer missing");
+    GS_HIP(hipMemcpyAsync(h.data(), b.p, n * sizeof(T), hipMemcpyDeviceToHost, c.stream));
+    GS_HIP(hipStreamSynchronize(c.stream));
+  }
+  put(f, h.data(), n * sizeof(T));
+}
+template <class T>
+void get_dev(Ctx& c, FILE* f, DevBuf<T>& b, size_t n) {
+  std::vector<T> h(n);
+  get(f, h.data(), n * sizeof(T));
+  b.alloc(n ? n : 1);
+  if (n) GS_HIP(hipMemcpyAsync(b.p, h.data(), n * sizeof(T), hipMemcpyHostToDevice, c.stream));
+  GS_HIP(hipStreamSynchronize(c.stream));
+}
+}  // namespace
+
+extern "C" gs_status gs_save_state(gs_ctx* ctx, const char* path) {
+  GS_API_BEGIN(ctx)
+  if (!path) ctx->fail(GS_EINVAL, "null path");
+  if (!ctx->links_set || !ctx->topo_built) ctx->fail(GS_ESTATE, "gs_set_links and gs_build_topology first");
+  if (ctx->part_open) ctx->fail(GS_ESTATE, "a partitioned batch is in flight");
+  GS_HIP(hipSetDevice(ctx->cfg.device));
+  StateFile sf;
+  if (!(sf.f = fopen(path, "wb"))) ctx->fail(GS_EINVAL, std::string("cannot open ") + path);
+  FILE* f = sf.f;
+  const uint32_t abi = GS_ABI_VERSION, N = ctx->cfg.peers;
+  put(f, kStateMagic, 8);
+  put(f, &abi, 4);
+  put(f, &ctx->cfg, sizeof(gs_config));
+  const uint32_t fl[4] = {ctx->links_set, ctx->topo_built, ctx->mesh_built, ctx->traffic};
+  put(f, fl, sizeof fl);
+  put(f, &ctx->S, 4);
+  put(f, ctx->lat_ns.data(), ctx->lat_ns.size() * 8);
+  put(f, ctx->bw_up.data(), ctx->S * 8);
+  put(f, ctx->bw_dn.data(), ctx->S * 8);
+  put(f, ctx->stage_host.data(), N);
+  const uint64_t topo[3] = {ctx->k, ctx->max_degree, ctx->nnz};
+  put(f, topo, sizeof topo);
+  put_dev(*ctx, f, ctx->d_row, (size_t)N + 1);
+  put_dev(*ctx, f, ctx->d_col, ctx->nnz);
+  put_dev(*ctx, f, ctx->d_flags, ctx->nnz);
+  put_dev(*ctx, f, ctx->d_rev, ctx->nnz);
+  const uint32_t has_until = ctx->d_until.p ? 1u : 0u;
+  put(f, &has_until, 4);
+  if (has_until) put_dev(*ctx, f, ctx->d_until, ctx->nnz);
+  if (ctx->mesh_built) {
+    put_dev(*ctx, f, ctx->d_mesh, (size_t)N * MESH_W);
+    put_dev(*ctx, f, ctx->d_mcnt, N);
+  }
+  put(f, &ctx->churn_state, 8);
+  put(f, &ctx->stats, sizeof(gs_stats));
+  put_dev(*ctx, f, ctx->d_counters, C_COUNT);  // the device counters gs_stats is read from
+  if (ctx->traffic) put_dev(*ctx, f, ctx->d_traffic, (size_t)N * GS_TRAFFIC_COLS);
+  put(f, kStateMagic, 8);  // end marker
+  if (fflush(f) != 0) ctx->fail(GS_EINVAL, "cannot write the state file");
+  GS_API_END(ctx)
+}
+
+extern "C" gs_status gs_load_state(const char* path, int32_t device, gs_ctx** out) {
+  if (!path || !out) return GS_EINVAL;
+  *out = nullptr;
+  StateFile sf;
+  gs_config cfg{};
+  char magic[8];
+  uint32_t abi = 0;
+  if (!(sf.f = fopen(path, "rb"))) return GS_EINVAL;
+  if (fread(magic, 1, 8, sf.f) != 8 || memcmp(magic, kStateMagic, 8) || fread(&abi, 4, 1, sf.f) != 1 ||
+      abi != GS_ABI_VERSION || fread(&cfg, sizeof cfg, 1, sf.f) != 1)
+    return GS_EINVAL;  // not a state file of this ABI (no context to hold the message)
+  cfg.device = device;
+  gs_ctx* c = nullptr;
+  gs_status st = gs_create(&cfg, &c);
+  if (st != GS_OK) return st;
+  try {
+    FILE* f = sf.f;
+    const uint32_t N = cfg.peers;
+    uint32_t fl[4], S = 0;
+    get(f, fl, sizeof fl);
+    get(f, &S, 4);
+    if (S == 0 || S > MAX_STAGES) c->fail(GS_EINVAL, "corrupt state file (stages)");
+    std::vector<uint64_t> lat((size_t)S * S), up(S), dn(S);
+    std::vector<uint8_t> stage(N);
+    get(f, lat.data(), lat.size() * 8);
+    get(f, up.data(), S * 8);
+    get(f, dn.data(), S * 8);
+    get(f, stage.data(), N);
+    if ((st = gs_set_links(c, S, lat.data(), up.data(), dn.data(), stage.data())) != GS_OK) throw Error(st, c->last_error);
+    uint64_t topo[3];
+    get(f, topo, sizeof topo);
+    c->k = (uint32_t)topo[0];
+    c->max_degree = (uint32_t)topo[1];
+    c->nnz = topo[2];
+    get_dev(*c, f, c->d_row, (size_t)N + 1);
+    get_dev(*c, f, c->d_col, c->nnz);
+    get_dev(*c, f, c->d_flags, c->nnz);
+    get_dev(*c, f, c->d_rev, c->nnz);
+    uint32_t has_until = 0;
+    get(f, &has_until, 4);
+    if (has_until) get_dev(*c, f, c->d_until, c->nnz);
+    c->topo_built = fl[1] != 0;
+    if (fl[2]) {
+      get_dev(*c, f, c->d_mesh, (size_t)N * MESH_W);
+      get_dev(*c, f, c->d_mcnt, N);
+      c->mesh_built = true;
+    }
+    get(f, &c->churn_state, 8);
+    c->ring_lo = c->churn_state + 1;  // nothing cached: earlier epochs replay from epoch 0
+    c->ring_hi = c->churn_state;
+    get(f, &c->stats, sizeof(gs_stats));
+    get_dev(*c, f, c->d_counters, C_COUNT);
+    if (fl[3]) {
+      c->traffic = true;
+      get_dev(*c, f, c->d_traffic, (size_t)N * GS_TRAFFIC_COLS);
+    }
+    get(f, magic, 8);
+    if (memcmp(magic, kStateMagic, 8)) c->fail(GS_EINVAL, "corrupt state file (end marker)");
+  } catch (const Error& e) {
+    gs_destroy(c);
+    return e.code;
+  } catch (...) {
+    gs_destroy(c);
+    return GS_ENOMEM;
+  }
+  *out = c;
+  return GS_OK;
 }

@@ -124,6 +124,9 @@ SIGNATURES = {
     "gs_get_mesh": (i32, [ctypes.c_void_p, P(u32), P(u8)]),
     "gs_run": (i32, [ctypes.c_void_p, P(GsPublish), u64, P(GsResultSink)]),
     "gs_get_stats": (i32, [ctypes.c_void_p, P(GsStats)]),
+    "gs_get_config": (i32, [ctypes.c_void_p, P(GsConfig)]),
+    "gs_save_state": (i32, [ctypes.c_void_p, ctypes.c_char_p]),
+    "gs_load_state": (i32, [ctypes.c_char_p, i32, P(ctypes.c_void_p)]),
     "gs_reset_stats": (i32, [ctypes.c_void_p]),
     "gs_set_timing": (i32, [ctypes.c_void_p, u32]),
     "gs_set_partition": (i32, [ctypes.c_void_p, u32, u32]),
@@ -365,6 +368,25 @@ class Simulator:
             raise GossipSimError(rc, "gs_create failed")
         self.peers = self.cfg.c.peers
         self._sched = []
+
+    # ---- checkpoint / resume (gs_save_state / gs_load_state) ----
+    def save_state(self, path):
+        """Links, CSR, mesh, churn mesh state, counters and traffic into `path`."""
+        self._check(lib().gs_save_state(self.ctx, str(path).encode()))
+
+    @classmethod
+    def load_state(cls, path, device=0):
+        """A new simulator on `device` that continues where the saved one stopped."""
+        self = cls.__new__(cls)
+        self.ctx = ctypes.c_void_p()
+        rc = lib().gs_load_state(str(path).encode(), device, ctypes.byref(self.ctx))
+        if rc:
+            raise GossipSimError(rc, "gs_load_state(%s) failed" % path)
+        self.cfg = PeerConfig()
+        lib().gs_get_config(self.ctx, ctypes.byref(self.cfg.c))
+        self.peers = self.cfg.c.peers
+        self._sched = []
+        return self
 
     def _check(self, rc):
         if rc:

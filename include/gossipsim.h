@@ -353,6 +353,20 @@ gs_status gs_write_node_metrics(const gs_config* cfg, const char* path, const ui
 
 gs_status gs_create(const gs_config* cfg, struct gs_ctx** out);
 gs_status gs_destroy(struct gs_ctx* ctx);
+
+/* Checkpoint / resume (no counterpart in the reference, whose
+ * runs are single Shadow executions): gs_save_state writes the configuration,
+ * link tables, CSR + mesh flags + PRUNE back-offs, the mesh ELL, the churn
+ * mesh state's epoch, the counters and the per-peer traffic of a context to
+ * `path`; gs_load_state makes a new context on `device` from such a file. A
+ * schedule continued on the loaded context gives exactly the results and
+ * counters the saved context would have given (every random draw is a pure
+ * function of the seed: there is no generator state). GS_EINVAL for a file of
+ * another ABI version or a damaged one. */
+gs_status gs_save_state(struct gs_ctx* ctx, const char* path);
+gs_status gs_load_state(const char* path, int32_t device, struct gs_ctx** out);
+/* The configuration a context was created (or loaded) with. */
+gs_status gs_get_config(const struct gs_ctx* ctx, gs_config* out);
 const char* gs_last_error(const struct gs_ctx* ctx);
 
 /* Per-stage link model. lat_ns is S x S (sender stage row), bw arrays have S

@@ -211,3 +211,51 @@ def test_shadow_parity_harness_end_to_end(tmp_path):
             f.write("%s %d\n" % (head, int(ms) * 108 // 100))
     args[1] = str(tmp_path / "latencies2")
     assert sp.main(args) == 1
+
+
+def _stats_no_time(sim):
+    return {k: v for k, v in sim.stats().items() if not k.endswith("_ms")}
+
+
+@pytest.mark.parametrize("case", ["frozen_traffic", "churn_gossip", "churn_replay"])
+def test_checkpoint_resume(tmp_path, case):
+    """gs_save_state / gs_load_state (SURVEY §5 checkpoint/resume): a schedule
+    split at a save point and continued on a context loaded from the file (on a
+    fresh context, the saved one destroyed) gives the same results, counters and
+    per-peer traffic as the uninterrupted context; the results are also the
+    oracle's. churn_gossip resumes after the churn mesh state moved forward;
+    churn_replay's second half publishes before the saved state, so the loaded
+    context replays the churn epochs from epoch 0."""
+    N, M = 1500, 24
+    kw = dict(peers=N, seed=98)
+    if case != "frozen_traffic":
+        kw.update(churn_ppm=20000, hb_phase_ns=gossipsim.SHADOW_START_NS, lazy_gossip=1)
+    p = oracle.params(**kw)
+    t, pub, size = _sched(M, N)
+    if case == "churn_replay":  # the later half of the publishes first
+        t, pub = np.roll(t, -(M // 2)), np.roll(pub, -(M // 2))
+    ref = oracle.simulate(p, 5, (50, 150, 40, 130), sched=(t, pub, size))
+    h = M // 2
+    first, second = (t[:h], pub[:h], size[:h]), (t[h:], pub[h:], size[h:])
+    whole, _ = gpu_sim(p, 5, (50, 150, 40, 130), batch=8)
+    whole.set_traffic(True)
+    a = whole.run(first)
+    b = whole.run(second)
+    part, _ = gpu_sim(p, 5, (50, 150, 40, 130), batch=8)
+    part.set_traffic(True)
+    a2 = part.run(first)
+    part.save_state(tmp_path / "gs.state")
+    mesh0, csr0 = part.mesh(), part.csr()
+    part.close()
+    res = gossipsim.Simulator.load_state(tmp_path / "gs.state", device=0)
+    for x, y in zip(res.mesh() + res.csr(), mesh0 + csr0):
+        np.testing.assert_array_equal(x, y)
+    assert res.peers == N and res.cfg.churn_ppm == p.churn_ppm and res.cfg.batch == 8
+    b2 = res.run(second)
+    for k in ("t_complete", "hops"):
+        np.testing.assert_array_equal(a2[k], a[k])
+        np.testing.assert_array_equal(b2[k], b[k])
+        np.testing.assert_array_equal(np.concatenate([a2[k], b2[k]]), ref[k])
+    assert _stats_no_time(res) == _stats_no_time(whole)
+    assert res.stats()["deliveries"] == ref["stats"]["deliveries"]
+    np.testing.assert_array_equal(res.traffic(), whole.traffic())

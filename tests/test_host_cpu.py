@@ -458,3 +458,23 @@ def test_streaming_log_round_trips_through_summary_latency_large(tmp_path):
         want[row.t_pub_ns] = int(((tc[q][ok] - np.uint64(row.t_pub_ns)) // np.uint64(1_000_000)).max())
     assert mx == want
     assert "Total Messages Published :  %d" % len(sched) in got
+
+
+def test_load_state_rejects_foreign_files(tmp_path):
+    """gs_load_state refuses a file that is not a state file of this ABI before
+    it touches a device (GS_EINVAL; CPU only: no context is created)."""
+    import ctypes
+    import struct
+    lib = gossipsim.lib()
+    out = ctypes.c_void_p()
+    bad = tmp_path / "bad"
+    bad.write_bytes(b"NOTSTATE" + bytes(64))
+    assert lib.gs_load_state(str(bad).encode(), 0, ctypes.byref(out)) == gossipsim.GS_EINVAL
+    old = tmp_path / "old"
+    old.write_bytes(b"GSIMST01" + struct.pack("<I", gossipsim.ABI_VERSION - 1) + bytes(256))
+    assert lib.gs_load_state(str(old).encode(), 0, ctypes.byref(out)) == gossipsim.GS_EINVAL
+    short = tmp_path / "short"
+    short.write_bytes(b"GSIMST01" + struct.pack("<I", gossipsim.ABI_VERSION) + bytes(8))
+    assert lib.gs_load_state(str(short).encode(), 0, ctypes.byref(out)) == gossipsim.GS_EINVAL
+    assert lib.gs_load_state(str(tmp_path / "missing").encode(), 0, ctypes.byref(out)) == gossipsim.GS_EINVAL
+    assert not out.value
