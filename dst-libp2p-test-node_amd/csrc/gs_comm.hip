@@ -218,6 +218,160 @@ void rank_gather(gs_comm* cm, Ctx& c, const uint64_t* mine, uint32_t n, uint64_t
   memcpy(out, h.data(), h.size() * 8);
 }
 
+// Message-sharded batch: the batches the peer protocols
+// cannot take — churn (a mesh per heartbeat epoch), IDONTWANT, and lazy gossip
+// that is not a no-op (receiver-centric IWANTs read other parts' keys) — run
+// over the replicated graph instead. Part p simulates messages
+// [B*p/P, B*(p+1)/P) of the batch over all N peers with gs_run's engine, then
+// one all-to-all transposes the results: part r receives, from every part,
+// the rows of its own peers, so each sink still gets [B][own peers]. The
+// per-part memory is the same N*B/P lanes as the peer protocols'; the data
+// crossing GPUs is the results (9 B per lane), once per batch.
+void run_batch_ms(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched, uint64_t i0, uint32_t B,
+                  const gs_result_sink* sinks) {
+  const uint32_t P = cm->nranks, N = cx[0]->cfg.peers;
+  auto u0_of = [&](uint32_t p) { return (uint32_t)((uint64_t)p * N / P); };
+  auto m0_of = [&](uint32_t p) { return (uint32_t)((uint64_t)p * B / P); };
+  const uint32_t mpmax = (B + P - 1) / P;
+  // 1. every part: its share of the messages over all N peers (device-resident rows [mp][N])
+  for (uint32_t i = 0; i < nctx; i++) {
+    Ctx& c = *cx[i];
+    const uint32_t me = cm->local ? i : cm->rank, m0 = m0_of(me), mp = m0_of(me + 1) - m0;
+    GS_HIP(hipSetDevice(c.cfg.device));
+    std::string why;
+    gs_status code = GS_OK;
+    try {
+      if (c.traffic) c.fail(GS_EUNSUPPORTED, "per-peer traffic is not supported in partitioned mode");
+      if (sinks && sinks[i].summary)
+        c.fail(GS_EUNSUPPORTED, "per-message summaries of a message-sharded partitioned batch (churn, IDONTWANT or "
+                                "lazy gossip IWANTs): use gs_run");
+      c.d_ms_tc.alloc(std::max<size_t>(1, (size_t)mp * N));
+      c.d_ms_hops.alloc(std::max<size_t>(1, (size_t)mp * N));
+      const uint64_t batches = c.stats.batches;
+      if (mp) {
+        gs_result_sink ds{};
+        ds.t_complete_ns = c.d_ms_tc.p;
+        ds.hops = c.d_ms_hops.p;
+        const uint32_t batch = c.cfg.batch;
+        c.cfg.batch = mpmax;  // buffers for this part's share, not the whole batch
+        c.sink_dev = true;
+        try {
+          run_messages(c, sched + i0 + m0, mp, &ds);
+        } catch (...) {
+          c.cfg.batch = batch;
+          c.sink_dev = false;
+          throw;
+        }
+        c.cfg.batch = batch;
+        c.sink_dev = false;
+      }
+      c.stats.messages += B - mp;  // every part counts the batch, as in the peer protocols
+      c.stats.batches = batches + 1;
+      c.stats.ms_batches++;
+    } catch (const Error& e) {
+      code = e.code;
+      why = e.msg;
+    }
+    rank_status(cm, c, code != GS_OK);
+    if (code != GS_OK) throw Error(code, why);
+  }
+  // 2. the transposition: part r's peers of every part's messages into r's d_tc_t / d_hops_t [B][un_r]
+  if (cm->local) {
+    for (uint32_t i = 0; i < nctx; i++) {
+      GS_HIP(hipSetDevice(cx[i]->cfg.device));
+      GS_HIP(hipStreamSynchronize(cx[i]->stream));
+    }
+    for (uint32_t r = 0; r < nctx; r++) {
+      Ctx& d = *cx[r];
+      const uint32_t u0 = u0_of(r), un = u0_of(r + 1) - u0;
+      GS_HIP(hipSetDevice(d.cfg.device));
+      d.d_tc_t.alloc((size_t)un * B);
+      d.d_hops_t.alloc((size_t)un * B);
+      for (uint32_t p = 0; p < nctx; p++) {
+        const uint32_t m0 = m0_of(p), mp = m0_of(p + 1) - m0;
+        if (!mp) continue;
+        GS_HIP(hipMemcpy2DAsync(d.d_tc_t.p + (size_t)m0 * un, (size_t)un * 8, cx[p]->d_ms_tc.p + u0, (size_t)N * 8,
+                                (size_t)un * 8, mp, hipMemcpyDeviceToDevice, d.stream));
+        GS_HIP(hipMemcpy2DAsync(d.d_hops_t.p + (size_t)m0 * un, un, cx[p]->d_ms_hops.p + u0, N, un, mp,
+                                hipMemcpyDeviceToDevice, d.stream));
+      }
+    }
+    for (uint32_t r = 0; r < nctx; r++) {
+      GS_HIP(hipSetDevice(cx[r]->cfg.device));
+      GS_HIP(hipStreamSynchronize(cx[r]->stream));
+    }
+  } else {
+    Ctx& c = *cx[0];
+    Rccl* rc = rccl();
+    const uint32_t me = cm->rank, mme = m0_of(me + 1) - m0_of(me), u0me = u0_of(me), unme = u0_of(me + 1) - u0me;
+    GS_HIP(hipSetDevice(c.cfg.device));
+    // pack: destination r's block [mme][un_r] at offset mme * u0_r
+    c.d_ms_send.alloc(std::max<size_t>(1, (size_t)mme * N));
+    c.d_ms_sendh.alloc(std::max<size_t>(1, (size_t)mme * N));
+    if (mme)
+      for (uint32_t r = 0; r < P; r++) {
+        const uint32_t u0 = u0_of(r), un = u0_of(r + 1) - u0;
+        GS_HIP(hipMemcpy2DAsync(c.d_ms_send.p + (size_t)mme * u0, (size_t)un * 8, c.d_ms_tc.p + u0, (size_t)N * 8,
+                                (size_t)un * 8, mme, hipMemcpyDeviceToDevice, c.stream));
+        GS_HIP(hipMemcpy2DAsync(c.d_ms_sendh.p + (size_t)mme * u0, un, c.d_ms_hops.p + u0, N, un, mme,
+                                hipMemcpyDeviceToDevice, c.stream));
+      }
+    c.d_tc_t.alloc((size_t)unme * B);
+    c.d_hops_t.alloc((size_t)unme * B);
+    const uint64_t pb = rccl_piece_bytes(), p8 = std::max<uint64_t>(1, pb / 8);
+    GS_NCCL(rc->GroupStart());
+    for (uint32_t r = 0; r < P; r++) {
+      const uint64_t n = (uint64_t)mme * (u0_of(r + 1) - u0_of(r)), off = (uint64_t)mme * u0_of(r);
+      for (uint64_t k = 0; k < n; k += p8)
+        GS_NCCL(rc->Send(c.d_ms_send.p + off + k, std::min(p8, n - k), ncclUint64, (int)r, cm->nc, c.stream));
+      for (uint64_t k = 0; k < n; k += pb)
+        GS_NCCL(rc->Send(c.d_ms_sendh.p + off + k, std::min(pb, n - k), ncclUint8, (int)r, cm->nc, c.stream));
+    }
+    for (uint32_t p = 0; p < P; p++) {
+      const uint64_t n = (uint64_t)(m0_of(p + 1) - m0_of(p)) * unme, off = (uint64_t)m0_of(p) * unme;
+      for (uint64_t k = 0; k < n; k += p8)
+        GS_NCCL(rc->Recv(c.d_tc_t.p + off + k, std::min(p8, n - k), ncclUint64, (int)p, cm->nc, c.stream));
+      for (uint64_t k = 0; k < n; k += pb)
+        GS_NCCL(rc->Recv(c.d_hops_t.p + off + k, std::min(pb, n - k), ncclUint8, (int)p, cm->nc, c.stream));
+    }
+    GS_NCCL(rc->GroupEnd());
+    GS_HIP(hipStreamSynchronize(c.stream));
+  }
+  // 3. own peers' rows into the sinks
+  if (!sinks) return;
+  for (uint32_t i = 0; i < nctx; i++) {
+    Ctx& c = *cx[i];
+    const uint32_t me = cm->local ? i : cm->rank, un = u0_of(me + 1) - u0_of(me);
+    GS_HIP(hipSetDevice(c.cfg.device));
+    deliver_rows(c, B, un, &sinks[i], i0);
+    GS_HIP(hipStreamSynchronize(c.stream));
+  }
+}
+
+// Counters of every part before a batch; restored when the peer protocols'
+// eager result is discarded (lazy gossip can change the batch).
+void save_counters(Ctx** cx, uint32_t nctx) {
+  for (uint32_t i = 0; i < nctx; i++) {
+    Ctx& c = *cx[i];
+    GS_HIP(hipSetDevice(c.cfg.device));
+    c.d_cnt_save.alloc(C_COUNT);
+    GS_HIP(hipMemcpyAsync(c.d_cnt_save.p, c.d_counters.p, C_COUNT * 8, hipMemcpyDeviceToDevice, c.stream));
+  }
+}
+
+void gossip_to_ms(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched, uint64_t i0, uint32_t B,
+                  const gs_result_sink* sinks) {
+  for (uint32_t i = 0; i < nctx; i++) {
+    Ctx& c = *cx[i];
+    part_abort(c);
+    GS_HIP(hipSetDevice(c.cfg.device));
+    GS_HIP(hipMemcpyAsync(c.d_counters.p, c.d_cnt_save.p, C_COUNT * 8, hipMemcpyDeviceToDevice, c.stream));
+    GS_HIP(hipStreamSynchronize(c.stream));
+    c.stats.gossip_fallback_batches++;
+  }
+  run_batch_ms(cm, cx, nctx, sched, i0, B, sinks);
+}
+
 // The list pass over partitioned rows: every part runs the
 // window passes of gs_run over its own rows; between passes the parts agree
 // on the pass control (records emitted, min pending key, error word) and
@@ -388,15 +542,9 @@ bool run_batch_lp(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched,
     rank_gather(cm, *cx[0], &mine, 1, all);
     for (uint32_t k = 0; k < P; k++) ok = ok && !all[k];
   }
-  if (!ok) {
-    std::string why;
-    for (uint32_t i = 0; i < nctx; i++) {
-      part_abort(*cx[i]);
-      if (why.empty()) why = cx[i]->gossip_why;
-    }
-    throw Error(GS_EUNSUPPORTED, "lazy gossip can change this batch (an IHAVE lands before the last delivery; " +
-                                     (why.empty() ? std::string("another rank") : why) +
-                                     "); partitioned mode runs eager forwarding only: use gs_run");
+  if (!ok) {  // an IHAVE can land before the last delivery: the batch runs message-sharded with gossip
+    gossip_to_ms(cm, cx, nctx, sched, i0, B, sinks);
+    return true;
   }
   for (uint32_t i = 0; i < nctx; i++) {
     GS_HIP(hipSetDevice(cx[i]->cfg.device));
@@ -410,6 +558,11 @@ bool run_batch_lp(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched,
 // export / receive per bucket).
 void run_batch(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched, uint64_t i0, uint32_t B,
                const gs_result_sink* sinks) {
+  if (part_needs_ms(*cx[0], sched + i0, B)) {  // churn, IDONTWANT: the same decision on every rank
+    run_batch_ms(cm, cx, nctx, sched, i0, B, sinks);
+    return;
+  }
+  if (cx[0]->cfg.lazy_gossip) save_counters(cx, nctx);
   if (run_batch_lp(cm, cx, nctx, sched, i0, B, sinks)) return;
   const uint32_t P = cm->nranks;
   Rccl* r = cm->local ? nullptr : rccl();
@@ -594,14 +747,8 @@ void run_batch(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched, ui
     ok = c.h_pinned[0] != 0;
   }
   if (!ok) {
-    std::string why;
-    for (uint32_t i = 0; i < nctx; i++) {
-      part_abort(*cx[i]);
-      if (why.empty()) why = cx[i]->gossip_why;
-    }
-    throw Error(GS_EUNSUPPORTED, "lazy gossip can change this batch (an IHAVE lands before the last delivery; " +
-                                     (why.empty() ? std::string("another rank") : why) +
-                                     "); partitioned mode runs eager forwarding only: use gs_run");
+    gossip_to_ms(cm, cx, nctx, sched, i0, B, sinks);
+    return;
   }
   for (uint32_t i = 0; i < nctx; i++) {
     GS_HIP(hipSetDevice(cx[i]->cfg.device));

@@ -168,6 +168,11 @@ struct Ctx {
   DevBuf<uint32_t> d_pbin;      // [B][2]
   DevBuf<uint32_t> d_fine;      // [B][2][GS_HIST_MS]
   void* h_block = nullptr;      // pinned staging of streamed result blocks (gs_result_sink.on_block)
+  bool sink_dev = false;        // the sink's arrays are device memory (message-sharded partitioned batches)
+  DevBuf<uint64_t> d_ms_tc;     // message-sharded partitioned batch: this part's messages [mp][N] ...
+  DevBuf<uint8_t> d_ms_hops;
+  DevBuf<uint64_t> d_ms_send;   // ... packed per destination part (RCCL)
+  DevBuf<uint8_t> d_ms_sendh;
   size_t h_block_bytes = 0;
 
   // peer-partitioned mode (gs_part.h): this context holds keys of peers [u0, u0 + un)
@@ -207,6 +212,7 @@ void launch_topology(Ctx& c);
 uint32_t run_mesh(Ctx& c, uint32_t max_heartbeats);
 void churn_ring(Ctx& c, uint64_t h_lo, uint64_t h_hi);
 void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_result_sink* sink);
+void deliver_rows(Ctx& c, uint32_t B, uint32_t un, const gs_result_sink* sink, uint64_t sink_row0);
 void part_set(Ctx& c, uint32_t parts, uint32_t part);
 uint64_t part_begin(Ctx& c, const gs_publish* sched, uint64_t n_msgs);
 bool part_scan(Ctx& c, uint64_t bucket_key, gs_part_record* rec, uint64_t cap, uint64_t* n, uint64_t* m1);
@@ -220,6 +226,7 @@ void part_dev_relax_next(Ctx& c, const gs_part_record* in, uint64_t n);
 bool part_dev_complete(Ctx& c, bool hist);
 void part_dev_finish(Ctx& c, const gs_result_sink* sink, uint64_t row0);
 void part_abort(Ctx& c);
+bool part_needs_ms(Ctx& c, const gs_publish* sched, uint64_t n_msgs);
 // the list pass over partitioned rows (gs_part.h)
 bool part_lp_begin(Ctx& c, const gs_publish* sched, uint64_t n_msgs, uint64_t* seed_min);
 void part_lp_pass(Ctx& c);

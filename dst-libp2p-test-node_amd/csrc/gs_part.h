@@ -367,6 +367,14 @@ static uint32_t part_check(Ctx& c, const gs_publish* sched, uint64_t n_msgs) {
   return F;
 }
 
+// gs_run_partitioned: a batch the peer protocols cannot take (churn's mesh per
+// epoch, IDONTWANT) runs message-sharded over the replicated graph (gs_comm.hip).
+bool part_needs_ms(Ctx& c, const gs_publish* sched, uint64_t n_msgs) {
+  if (c.cfg.churn_ppm) return true;
+  if (!c.cfg.idontwant || !n_msgs) return false;
+  return frag_payload(c.cfg.node, sched[0].msg_size, frags_of(c, sched[0])) >= c.cfg.idontwant;
+}
+
 uint64_t part_begin(Ctx& c, const gs_publish* sched, uint64_t n_msgs) {
   const uint32_t F = part_check(c, sched, n_msgs);
   const uint32_t FP = pow2_at_least(F), Bmax = c.cfg.batch, un = c.part_un;

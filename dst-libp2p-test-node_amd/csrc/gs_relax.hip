@@ -594,6 +594,46 @@ static void fill_summary(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, gs_ms
 // Results of the batch to the caller: message-major copy into the sink
 // arrays (rows sink_row0..), or streamed in blocks through on_block; then the
 // per-message summaries.
+// Message-major rows [B][un] in d_tc_t / d_hops_t into a sink's rows
+// [row0, row0 + B): its arrays (host memory; device memory when c.sink_dev,
+// the message-sharded partitioned batches of gs_comm.hip) or on_block blocks.
+void deliver_rows(Ctx& c, uint32_t B, uint32_t un, const gs_result_sink* sink, uint64_t sink_row0) {
+  hipStream_t s = c.stream;
+  const uint32_t want = sink->want ? sink->want : (GS_WANT_T_COMPLETE | GS_WANT_HOPS);
+  const bool want_tc = sink->on_block ? (want & GS_WANT_T_COMPLETE) != 0 : sink->t_complete_ns != nullptr;
+  const bool want_h = sink->on_block ? (want & GS_WANT_HOPS) != 0 : sink->hops != nullptr;
+  if (!sink->on_block) {
+    const hipMemcpyKind kind = c.sink_dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    if (want_tc)
+      GS_HIP(hipMemcpyAsync(sink->t_complete_ns + sink_row0 * un, c.d_tc_t.p, (size_t)B * un * 8, kind, s));
+    if (want_h) GS_HIP(hipMemcpyAsync(sink->hops + sink_row0 * un, c.d_hops_t.p, (size_t)B * un, kind, s));
+    return;
+  }
+  // stream: blocks of bm messages through one pinned staging buffer
+  const uint32_t bm = std::max<uint32_t>(1, std::min<uint32_t>(sink->block_msgs ? sink->block_msgs : 64, B));
+  const size_t need = (size_t)bm * un * 9;
+  if (c.h_block_bytes < need) {
+    if (c.h_block) GS_HIP(hipHostFree(c.h_block));
+    c.h_block = nullptr;
+    c.h_block_bytes = 0;
+    GS_HIP(hipHostMalloc(&c.h_block, need, hipHostMallocDefault));
+    c.h_block_bytes = need;
+  }
+  uint64_t* htc = (uint64_t*)c.h_block;
+  uint8_t* hh = (uint8_t*)(htc + (size_t)bm * un);
+  for (uint32_t q0 = 0; q0 < B; q0 += bm) {
+    const uint32_t n = std::min(bm, B - q0);
+    if (want_tc)
+      GS_HIP(hipMemcpyAsync(htc, c.d_tc_t.p + (size_t)q0 * un, (size_t)n * un * 8, hipMemcpyDeviceToHost, s));
+    if (want_h)
+      GS_HIP(hipMemcpyAsync(hh, c.d_hops_t.p + (size_t)q0 * un, (size_t)n * un, hipMemcpyDeviceToHost, s));
+    GS_HIP(hipStreamSynchronize(s));
+    sink->on_block(sink->user, sink_row0 + q0, n, un, want_tc ? htc : nullptr, want_h ? hh : nullptr);
+  }
+}
+
+// Results of a completed batch (peer-major d_tc / d_hops of peers [u0, u0 + un))
+// into the sink: transposed to message-major, copied out, summaries.
 static void deliver(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, const gs_result_sink* sink,
                     uint64_t sink_row0) {
   if (!sink) return;
@@ -607,34 +647,7 @@ static void deliver(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, const gs_r
     dim3 tg((un + 63) / 64, (b.B + 63) / 64);
     k_transpose<<<tg, TB, 0, s>>>(c.d_tc.p, c.d_hops.p, c.d_tc_t.p, c.d_hops_t.p, un, b.B);
     GS_HIP(hipGetLastError());
-    if (!sink->on_block) {
-      if (want_tc)
-        GS_HIP(hipMemcpyAsync(sink->t_complete_ns + sink_row0 * un, c.d_tc_t.p, (size_t)b.B * un * 8,
-                              hipMemcpyDeviceToHost, s));
-      if (want_h)
-        GS_HIP(hipMemcpyAsync(sink->hops + sink_row0 * un, c.d_hops_t.p, (size_t)b.B * un, hipMemcpyDeviceToHost, s));
-    } else {  // stream: blocks of bm messages through one pinned staging buffer
-      const uint32_t bm = std::max<uint32_t>(1, std::min<uint32_t>(sink->block_msgs ? sink->block_msgs : 64, b.B));
-      const size_t need = (size_t)bm * un * 9;
-      if (c.h_block_bytes < need) {
-        if (c.h_block) GS_HIP(hipHostFree(c.h_block));
-        c.h_block = nullptr;
-        c.h_block_bytes = 0;
-        GS_HIP(hipHostMalloc(&c.h_block, need, hipHostMallocDefault));
-        c.h_block_bytes = need;
-      }
-      uint64_t* htc = (uint64_t*)c.h_block;
-      uint8_t* hh = (uint8_t*)(htc + (size_t)bm * un);
-      for (uint32_t q0 = 0; q0 < b.B; q0 += bm) {
-        const uint32_t n = std::min(bm, b.B - q0);
-        if (want_tc)
-          GS_HIP(hipMemcpyAsync(htc, c.d_tc_t.p + (size_t)q0 * un, (size_t)n * un * 8, hipMemcpyDeviceToHost, s));
-        if (want_h)
-          GS_HIP(hipMemcpyAsync(hh, c.d_hops_t.p + (size_t)q0 * un, (size_t)n * un, hipMemcpyDeviceToHost, s));
-        GS_HIP(hipStreamSynchronize(s));
-        sink->on_block(sink->user, sink_row0 + q0, n, un, want_tc ? htc : nullptr, want_h ? hh : nullptr);
-      }
-    }
+    deliver_rows(c, b.B, un, sink, sink_row0);
   }
   if (sink->summary) fill_summary(c, b, u0, un, sink->summary + sink_row0);
 }

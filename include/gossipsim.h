@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 7u
+#define GS_ABI_VERSION 8u
 
 /* Sentinel for "never delivered" in t_complete_ns. */
 #define GS_UNDELIVERED UINT64_MAX
@@ -193,6 +193,7 @@ typedef struct gs_stats {
     uint64_t batches;           /* device batches run (gs_run splits at cfg.batch, size /  */
                                 /* chunk changes and the churn snapshot ring)             */
     uint64_t list_pull_batches; /* batches whose eager passes ran on candidate lists      */
+    uint64_t ms_batches;        /* gs_run_partitioned batches run message-sharded (ABI 8) */
                                 /* (k_lpull) rather than dense rows       */
 } gs_stats;
 
@@ -480,13 +481,18 @@ gs_status gs_comm_destroy(gs_comm* comm);
 /* gs_run with the peers partitioned over the communicator's parts: ctxs are
  * this process's contexts (RCCL: nctx = 1, the rank's; local: nctx = nparts,
  * part i = ctxs[i]), all built with the same config, topology and mesh. The
- * library sets each context's partition, runs every batch's bucket protocol
- * (per bucket: own scan, records routed only to the parts owning a target
- * with grouped send/recv, relax into own peers, MIN all-reduce of the next
- * bucket key on the device; one host read of the count matrix per bucket)
- * and writes part i's peers to sinks[i] ([n_msgs][own peers]; sinks may be
- * NULL). Collective over the communicator. Results are bit-identical to
- * gs_run; lazy gossip runs as the proven no-op only (GS_EUNSUPPORTED otherwise). */
+ * library sets each context's partition, runs every batch on the list pass
+ * over own rows (records exchanged between window passes) or the bucket
+ * protocol (per bucket: own scan, records routed only to the parts owning a
+ * target with grouped send/recv, relax into own peers, MIN all-reduce of the
+ * next bucket key) and writes part i's peers to sinks[i] ([n_msgs][own peers];
+ * sinks may be NULL). Batches the peer protocols cannot take — churn,
+ * IDONTWANT, lazy gossip whose IWANTs can change the result — run
+ * message-sharded over the replicated graph (part p simulates its share of
+ * the batch's messages for all peers, one all-to-all hands every part its own
+ * peers' rows; gs_stats.ms_batches counts them). Collective over the
+ * communicator. Results are bit-identical to gs_run. GS_EUNSUPPORTED: per-peer
+ * traffic (gs_set_traffic), and sink summaries of a message-sharded batch. */
 gs_status gs_run_partitioned(struct gs_ctx* const* ctxs, uint32_t nctx, gs_comm* comm, const gs_publish* sched,
                              uint64_t n_msgs, const gs_result_sink* sinks);
 

@@ -214,11 +214,83 @@ def test_run_partitioned_rccl_many_pieces(monkeypatch, piece):
     comm.close()
 
 
-def test_run_partitioned_refuses_gossip_that_matters():
-    p = oracle.params(peers=600, seed=60, hb_phase_ns=T0 % 1_000_000_000)  # heartbeat at the publish
+def _ms_check(p, S, links, parts, sched, batch, rccl=False,
+              summed=("deliveries", "frag_deliveries", "gossip_iwant", "latency_sum_ms")):
+    """gs_run_partitioned against gs_run and the oracle on a batch the peer
+    protocols hand to the message-sharded path; counters summed over parts."""
+    ref, rst = _whole(p, S, links, sched, batch)
+    ora = oracle.simulate(p, S, links, sched=sched)
+    np.testing.assert_array_equal(ref["t_complete"], ora["t_complete"])
+    np.testing.assert_array_equal(ref["hops"], ora["hops"])
+    sims = _parts(p, S, links, 1 if rccl else parts, batch)
+    comm = (gossipsim.Comm(nranks=1, rank=0, uid=gossipsim.Comm.get_id(), device=0) if rccl
+            else gossipsim.Comm(local_parts=parts))
+    res = comm.run_partitioned(sims, sched)
+    np.testing.assert_array_equal(np.concatenate([r["t_complete"] for r in res], axis=1), ora["t_complete"])
+    np.testing.assert_array_equal(np.concatenate([r["hops"] for r in res], axis=1), ora["hops"])
+    st = [s.stats() for s in sims]
+    for k in summed:
+        assert sum(x[k] for x in st) == rst[k], k
+    assert sum(x["deliveries"] for x in st) == ora["stats"]["deliveries"]
+    assert all(x["messages"] == len(sched[0]) for x in st)
+    comm.close()
+    return st, rst
+
+
+@pytest.mark.parametrize("parts,batch", [(3, 16), (8, 8), (3, 2)])
+def test_run_partitioned_gossip_iwants_message_sharded(parts, batch):
+    """A heartbeat at the publish instant: IHAVEs land before the last
+    delivery, the peer protocols' eager result is discarded (counters restored)
+    and the batch runs message-sharded with gossip; IWANTs taken, bit-exact
+    against gs_run and the oracle (batch 2 < P = 3: parts with no messages)."""
+    N = 3000
+    p = oracle.params(peers=N, seed=60, lazy_gossip=1, hb_phase_ns=T0 % 1_000_000_000)
+    st, rst = _ms_check(p, 5, (50, 150, 40, 130), parts, _sched(16, N), batch)
+    assert rst["gossip_iwant"] > 0
+    assert all(x["ms_batches"] == 16 // batch and x["gossip_fallback_batches"] >= 16 // batch for x in st)
+
+
+@pytest.mark.parametrize("parts", [2, 8])
+def test_run_partitioned_churn_message_sharded(parts):
+    """Config #3's knobs (churn + lazy gossip, heterogeneous links) in
+    partitioned mode: every batch message-sharded over the replicated graph
+    (each part replays the churn epochs its messages need), loop-back P = 8,
+    bit-exact against the oracle."""
+    N = 4000
+    p = oracle.params(peers=N, seed=62, churn_ppm=20000, hb_phase_ns=gossipsim.SHADOW_START_NS, lazy_gossip=1)
+    st, rst = _ms_check(p, 5, (50, 150, 40, 130), parts, _sched(24, N), 8)
+    assert rst["gossip_iwant"] > 0 and all(x["ms_batches"] == 3 for x in st)
+
+
+def test_run_partitioned_idontwant_message_sharded():
+    """The go preset (IDONTWANT above 1000 B, go-test-node/main.go:153-175)
+    in partitioned mode, P = 4."""
+    N = 3000
+    p = oracle.params_for("go", peers=N, seed=63)
+    st, _ = _ms_check(p, 5, (50, 150, 40, 130), 4, _sched(12, N), 12)
+    assert all(x["ms_batches"] == 1 for x in st)
+
+
+@pytest.mark.parametrize("piece", [0, 1 << 16])
+def test_run_partitioned_rccl_message_sharded(monkeypatch, piece):
+    """The message-sharded path over RCCL (one rank: pack, grouped send/recv
+    of the result rows, in pieces with GS_RCCL_PIECE_BYTES) with churn and
+    gossip."""
+    if piece:
+        monkeypatch.setenv("GS_RCCL_PIECE_BYTES", str(piece))
+    N = 20_000
+    p = oracle.params(peers=N, seed=64, churn_ppm=20000, hb_phase_ns=gossipsim.SHADOW_START_NS, lazy_gossip=1)
+    st, _ = _ms_check(p, 5, (50, 150, 40, 130), 1, _sched(16, N), 16, rccl=True)
+    assert st[0]["ms_batches"] == 1
+
+
+def test_run_partitioned_refuses_traffic():
+    """Per-peer traffic is the one knob partitioned mode refuses."""
+    p = oracle.params(peers=600, seed=60)
     sims = _parts(p, 1, (50, 50, 50, 50), 2, 4)
+    for s in sims:
+        s.set_traffic(True)
     comm = gossipsim.Comm(local_parts=2)
     with pytest.raises(gossipsim.GossipSimError, match="GS_EUNSUPPORTED"):
         comm.run_partitioned(sims, _sched(4, 600))
-    # the contexts stay usable: an eager-only run afterwards
     comm.close()
