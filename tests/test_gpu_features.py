@@ -214,7 +214,8 @@ def test_shadow_parity_harness_end_to_end(tmp_path):
 
 
 def _stats_no_time(sim):
-    return {k: v for k, v in sim.stats().items() if not k.endswith("_ms")}
+    # pushes counts atomicMin calls past a racy pre-read filter: a diagnostic, not deterministic
+    return {k: v for k, v in sim.stats().items() if not k.endswith("_ms") and k != "pushes"}
 
 
 @pytest.mark.parametrize("case", ["frozen_traffic", "churn_gossip", "churn_replay"])
