@@ -130,6 +130,8 @@ struct Ctx {
   DevBuf<uint32_t> d_gl_idx; // lazy gossip: lanes with an IHAVE arrival in the bucket
   DevBuf<uint32_t> d_gl_cnt;
   DevBuf<uint64_t> d_gl_key; // receiver-centric gossip: the listed lane's key (saves its re-read)
+  DevBuf<uint32_t> d_gs_idx; // churn: sender-centric gossip lanes of late heartbeats (RelaxArgs::gs_switch)
+  DevBuf<uint32_t> d_gs_cnt;
   DevBuf<uint64_t> d_nonfinal;  // [3]
   DevBuf<uint64_t> d_rel0;   // [B] first heartbeat >= t_pub (relative ns)
   DevBuf<uint64_t> d_habs0;  // [B] its absolute heartbeat index

@@ -682,6 +682,10 @@ static RelaxArgs relax_args(Ctx& c, const Batch& b, bool gossip) {
     if (c.cfg.churn_ppm) {
       ra.ring_in = c.d_ring_in.p;
       ra.ring_incnt = c.d_ring_incnt.p;
+      // heartbeats of a message from index gs_switch on are decided
+      // sender-centric (exact for any value; GS_GOSSIP_SWITCH for tests / A/B)
+      const char* gsw = getenv("GS_GOSSIP_SWITCH");
+      ra.gs_switch = gsw && *gsw ? (uint32_t)atoi(gsw) : 4u;
     }
     ra.hist = c.cfg.history_gossip;
     ra.d_lazy = c.cfg.d_lazy;
@@ -1205,7 +1209,11 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
           ra.gl_cnt = c.d_gl_cnt.p;
           if (ra.ring_in) {
             c.d_gl_key.alloc(nwaves * ra.gl_cap);
+            c.d_gs_idx.alloc(nwaves * ra.gl_cap);
+            c.d_gs_cnt.alloc(nwaves);
             ra.gl_key = c.d_gl_key.p;
+            ra.gs_idx = c.d_gs_idx.p;
+            ra.gs_cnt = c.d_gs_cnt.p;
           }
           ra.nonfinal = c.d_nonfinal.p;
           if ((v & 10) == 10) {

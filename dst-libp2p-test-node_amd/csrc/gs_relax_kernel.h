@@ -67,6 +67,13 @@ struct RelaxArgs {
   const uint32_t* ring_in;
   const uint32_t* ring_incnt;  // [R][N] their number (> GT_IN: recompute)
   uint64_t* gl_key;            // receiver-centric: the listed lane's key
+  // churn + gossip: heartbeats k >= gs_switch of a message (k counted from its
+  // first heartbeat) are decided sender-centric: after the eager wave only the
+  // peers that received it within their history window gossip it, a few
+  // hundred per message, while the undelivered lanes stay ~10 % of all
+  uint32_t* gs_idx;            // sender-centric lanes of the bucket, per scan wave
+  uint32_t* gs_cnt;
+  uint32_t gs_switch;
   const uint32_t* mesh;
   const uint32_t* pub;
   const uint8_t* stage;
@@ -462,7 +469,7 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
   const size_t seg = (size_t)wave * a.seg_cap;
   const size_t gseg = (size_t)wave * a.gl_cap;
   uint64_t nmin = INF64, nonfin = 0, nscan = 0, nscan_g = 0;
-  uint32_t cnt = 0, gcnt = 0, err = 0;
+  uint32_t cnt = 0, gcnt = 0, scnt = 0, err = 0;
   const uint64_t hspan = GOSSIP ? (uint64_t)a.hist * a.hb_ns : 0;
   // Tiles are visited per wave in groups: with SKIP a group is 64 consecutive
   // tiles whose metadata every lane loads at once (one coalesced load each,
@@ -532,45 +539,56 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
       // those can fall in [lo, hi), fold the next one >= hi into nmin
       const bool fin = pending && t < hi;
       nonfin += (valid && !fin && slot % FP < a.F) ? 1u : 0u;  // padded fragments never arrive
-      bool gwork = false;
+      bool gwork = false, swork = false;  // receiver-centric entry (churn), sender-centric entry
       uint64_t gnext = INF64;
       // the first gossip heartbeat T_j0 < max(t, rel0) + hb, so a lane with
       // max(t, rel0) + hist*hb + lmax < lo is past its last IHAVE: skip it
       // before the division
       const uint32_t sv = (fin || a.ring_in) && valid ? a.stage[u] : 0, m = slot / FP;
       const uint64_t r0 = (fin || a.ring_in) && valid ? a.rel0[m] : 0;
+      // churn: heartbeat indices [0, kl] lie in the message's lifetime (none
+      // when its publisher was offline at t_pub: nobody holds it)
+      const bool alive = a.ring_in && valid && slot % FP < a.F && a.hist && a.habs0[m] <= a.q0[m] + a.horizon &&
+                         !ep_off(a, a.q0[m], a.pub[m]);
+      const uint64_t kl = alive ? a.q0[m] + a.horizon - a.habs0[m] : 0;
       if (a.ring_in) {
-        // receiver-centric (churn): a lane without a key before this bucket
-        // lists itself when an IHAVE of one of its message's heartbeats T_k
-        // can reach its peer inside [lo, hi) (T_k + min / max latency into
-        // its stage), up to the message's lifetime
-        // (a message whose publisher was offline at t_pub has no holder: skip)
-        if (valid && slot % FP < a.F && !(pending && t < lo) && a.hist && a.habs0[m] <= a.q0[m] + a.horizon &&
-            !ep_off(a, a.q0[m], a.pub[m])) {
+        // receiver-centric (churn, heartbeats k < gs_switch): a lane without a
+        // key before this bucket lists itself when an IHAVE of one of its
+        // message's heartbeats T_k can reach its peer inside [lo, hi) (T_k +
+        // min / max latency into its stage), up to the message's lifetime
+        if (alive && !(pending && t < lo) && a.gs_switch > 0) {
           const uint64_t imn = L.imin[sv], imx = L.imax[sv];
-          const uint64_t kl = a.q0[m] + a.horizon - a.habs0[m];  // last heartbeat index in the lifetime
+          const uint64_t kr = kl < a.gs_switch - 1 ? kl : a.gs_switch - 1;  // last receiver-centric heartbeat
           const uint64_t k0 = lo > r0 + imx ? udiv53(lo - r0 - imx + a.hb_ns - 1, a.hb_ns) : 0;
           // an IHAVE to a peer offline at its arrival is lost: with windows
           // shorter than a heartbeat, a window lies in the epoch of its T_k,
           // so the peer's offline epochs are skipped (its tile sleeps)
           const bool one_ep = imx < a.hb_ns;
           const uint64_t hab0 = a.habs0[m];
-          gwork = k0 <= kl && r0 + k0 * a.hb_ns + imn < hi && !(one_ep && ep_off(a, hab0 + k0, u));
+          gwork = k0 <= kr && r0 + k0 * a.hb_ns + imn < hi && !(one_ep && ep_off(a, hab0 + k0, u));
           // the next bucket that can hold one of these arrivals: the first
           // window still open at hi (a window spans several buckets) with the
           // peer online
           uint64_t k1 = hi > r0 + imx ? udiv53(hi - r0 - imx + a.hb_ns - 1, a.hb_ns) : 0;
-          if (one_ep && k1 <= kl && ep_off(a, hab0 + k1, u)) k1++;  // (one step: later ones are found then)
-          if (k1 <= kl) gnext = r0 + k1 * a.hb_ns + imn > hi ? r0 + k1 * a.hb_ns + imn : hi;
+          if (one_ep && k1 <= kr && ep_off(a, hab0 + k1, u)) k1++;  // (one step: later ones are found then)
+          if (k1 <= kr) gnext = r0 + k1 * a.hb_ns + imn > hi ? r0 + k1 * a.hb_ns + imn : hi;
         }
-      } else if (fin && a.hist && (t > r0 ? t : r0) + hspan + L.lmax[sv] >= lo) {
+      }
+      // sender-centric: a final lane gossips at its history_gossip heartbeats
+      // (under churn only those with index >= gs_switch, within the lifetime)
+      if (fin && a.hist && (!a.ring_in || alive) && (t > r0 ? t : r0) + hspan + L.lmax[sv] >= lo) {
         const uint64_t lmn = L.lmin[sv], lmx = L.lmax[sv];
         const uint64_t j0 = first_hb(t, r0, a.hb_ns);
-        const uint64_t tlast = r0 + (j0 + a.hist - 1) * a.hb_ns;
-        if (tlast + lmx >= lo) {
-          for (uint32_t k = 0; k < a.hist; k++) {
-            const uint64_t T = r0 + (j0 + k) * a.hb_ns;
-            gwork |= (T + lmx >= lo && T + lmn < hi);
+        uint64_t kb = j0, ke = j0 + a.hist;  // heartbeat indices [kb, ke)
+        if (a.ring_in) {
+          kb = kb > a.gs_switch ? kb : a.gs_switch;
+          ke = ke < kl + 1 ? ke : kl + 1;
+        }
+        const uint64_t tlast = r0 + (ke - 1) * a.hb_ns;
+        if (kb < ke && tlast + lmx >= lo) {
+          for (uint64_t k = kb; k < ke; k++) {
+            const uint64_t T = r0 + k * a.hb_ns;
+            swork |= (T + lmx >= lo && T + lmn < hi);
             if (T + lmx >= hi)
               for (uint32_t s = 0; s < a.S; s++) {
                 const uint64_t x = T + L.lat[sv * a.S + s];
@@ -578,6 +596,10 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
               }
           }
         }
+      }
+      if (!a.ring_in) {  // frozen mesh: the gossip list holds the sender-centric lanes
+        gwork = swork;
+        swork = false;
       }
       if (gnext != INF64) {
         if (gnext > a.tmax) err |= ERR_TIME;
@@ -591,6 +613,9 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
         if (a.gl_key) a.gl_key[gseg + pos] = key;
       }
       gcnt += (uint32_t)__popcll(gm);
+      const uint64_t sm = __ballot(swork);
+      if (swork) a.gs_idx[gseg + scnt + (uint32_t)__popcll(sm & ((1ull << lane) - 1))] = (uint32_t)gid;
+      scnt += (uint32_t)__popcll(sm);
       if constexpr (SKIP) {  // the tile's gossip state for later skips
         const uint64_t tg = wave_min(gnext);
         const uint32_t nf = (uint32_t)__popcll(__ballot(valid && !fin && slot % FP < a.F));
@@ -626,11 +651,12 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
     for (int off = 32; off > 0; off >>= 1) err |= __shfl_xor(err, off);
     if (lane == 0) {
       a.gl_cnt[wave] = gcnt;
+      if (a.gs_cnt) a.gs_cnt[wave] = scnt;
       if (err) atomicOr((unsigned*)&a.counters[C_ERR], err);
     }
   }
   __shared__ uint64_t s_red[TB / 64 * 5];
-  const uint64_t ws[4] = {nonfin, GOSSIP ? (uint64_t)gcnt : 0, nscan, nscan_g};
+  const uint64_t ws[4] = {nonfin, GOSSIP ? (uint64_t)gcnt + scnt : 0, nscan, nscan_g};
   unsigned long long* const ps[4] = {GOSSIP ? (unsigned long long*)&a.nonfinal[a.launch % 3] : nullptr,
                                      (unsigned long long*)&a.counters[C_GLISTED],
                                      (unsigned long long*)&a.counters[C_TSCANNED],
@@ -746,7 +772,7 @@ __device__ __forceinline__ void gossip_receiver(const RelaxArgs& a, const Bucket
   for (;; k++) {
     const uint64_t T = r0 + k * hb;
     const uint64_t hab = a.habs0[m] + k;
-    if (T + imn >= hi || hab > lim) break;
+    if (T + imn >= hi || hab > lim || k >= a.gs_switch) break;  // later heartbeats: sender-centric
     if (imx < hb && ep_off(a, hab, w)) continue;  // every IHAVE of this heartbeat reaches w offline
     auto ihave = [&](uint32_t e) {  // the IHAVE v -> w of heartbeat hab
       const uint32_t v = e & 0xFFFFFFu, sv = e >> STAGE_SHIFT;
@@ -798,6 +824,62 @@ __device__ __forceinline__ void gossip_receiver(const RelaxArgs& a, const Bucket
   }
 }
 
+// Sender-centric lazy gossip of one listed final lane (v, m, f): each of its
+// history_gossip heartbeats (index >= kmin) with an IHAVE arrival in [lo, hi)
+// re-selects v's targets; a target that has not seen (m, f) by the arrival
+// sends IWANT and v's answer is pushed into its key.
+template <int FP>
+__device__ __forceinline__ void gossip_sender(const RelaxArgs& a, const BucketLds& L, uint64_t lo, uint64_t hi,
+                                              uint64_t gid, uint64_t kmin, uint64_t& nmin, uint64_t& iw,
+                                              uint32_t& err) {
+  const uint32_t LL = a.L, S = a.S;
+  const uint64_t key = a.keys[gid];
+  const uint64_t t = key >> a.tshift;
+  const uint32_t u = row_of(gid, LL), slot = (uint32_t)(gid - (uint64_t)u * LL);
+  const uint32_t m = slot / FP, sv = a.stage[u];
+  const uint32_t hp = (uint32_t)((key >> a.sb) & ((1u << HOP_BITS) - 1));
+  const uint64_t ser = L.su[sv];
+  const uint64_t r0 = a.rel0[m];
+  const uint64_t j0 = first_hb(t, r0, a.hb_ns);
+  for (uint32_t k = 0; k < a.hist; k++) {
+    if (j0 + k < kmin) continue;
+    const uint64_t T = r0 + (j0 + k) * a.hb_ns;
+    if (T + L.lmax[sv] < lo || T + L.lmin[sv] >= hi) continue;
+    const uint64_t hab = a.habs0[m] + j0 + k;
+    auto ihave = [&](uint32_t e) {  // v's IHAVE to w; IWANT + answer if w has not seen it
+      const uint32_t w = e & 0xFFFFFFu, sw = e >> STAGE_SHIFT;
+      const uint64_t lvw = L.lat[sv * S + sw];
+      const uint64_t ti = T + lvw;
+      if (ti < lo || ti >= hi) return;
+      const uint64_t sd = L.sd[sw];
+      const uint64_t A = ti + L.lat[sw * S + sv] + ser + lvw + (sd > ser ? sd - ser : 0);
+      if (a.churn) {  // IHAVE or answer lost: epochs counted from the heartbeat's (= ev_epoch)
+        const uint64_t lim = a.q0[m] + a.horizon;
+        const uint64_t hi_ = ep_plus(hab, lvw, a.hb_ns), ha = ep_plus(hab, A - T, a.hb_ns);
+        if (hi_ > lim || ep_off(a, hi_, w) || ha > lim || ep_off(a, ha, w)) return;
+      }
+      const size_t dst = (size_t)w * LL + slot;
+      // final before this bucket (its tile's final bit from an earlier scan:
+      // key time < that bucket's end <= lo <= t_i): seen, no key read
+      if (a.tstamp && ((a.fbits[dst >> 6] >> (dst & 63)) & 1) && a.tstamp[dst >> 6] != a.launch + 1) return;
+      const uint64_t kw = a.keys[dst];
+      if (kw != INF64 && (kw >> a.tshift) <= ti) return;  // already seen: no IWANT
+      iw++;
+      if (A > a.tmax) err |= ERR_TIME;
+      if (hp + 1 >= (1u << HOP_BITS)) err |= ERR_HOPS;
+      const uint64_t nk = (A << a.tshift) | ((uint64_t)(hp + 1) << a.sb) | u;
+      if (nk < kw) {
+        atomicMin((unsigned long long*)&a.keys[dst], (unsigned long long)nk);
+        if (a.tstamp) a.touched[dst >> 6] = 1;
+        nmin = nk < nmin ? nk : nmin;
+      }
+    };
+    // v gossips only while online, within the message's lifetime
+    if (a.churn && (hab > a.q0[m] + a.horizon || ep_off(a, hab, u))) continue;
+    for_each_gossip_target(a, u, hab, ihave);
+  }
+}
+
 template <int FP>
 __global__ __launch_bounds__(TB) void k_gossip(RelaxArgs a) {
   __shared__ BucketLds L;
@@ -806,63 +888,19 @@ __global__ __launch_bounds__(TB) void k_gossip(RelaxArgs a) {
   load_tables(L, a);
   __syncthreads();
   const uint64_t lo = ((cur >> a.tshift) / a.delta) * a.delta, hi = lo + a.delta;
-  const uint32_t LL = a.L, S = a.S;
   const uint32_t wave = blockIdx.x * (TB / 64) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const uint32_t n = __builtin_amdgcn_readfirstlane(a.gl_cnt[wave]);
   const size_t seg = (size_t)wave * a.gl_cap;
   uint64_t nmin = INF64, iw = 0;
   uint32_t err = 0;
-  if (a.ring_in)
+  if (a.ring_in) {
     for (uint32_t i = lane; i < n; i += 64)
       gossip_receiver<FP>(a, L, lo, hi, a.gl_idx[seg + i], a.gl_key[seg + i], nmin, iw, err);
-  else
-  for (uint32_t i = lane; i < n; i += 64) {
-    const uint64_t gid = a.gl_idx[seg + i];
-    const uint64_t key = a.keys[gid];
-    const uint64_t t = key >> a.tshift;
-    const uint32_t u = row_of(gid, LL), slot = (uint32_t)(gid - (uint64_t)u * LL);
-    const uint32_t m = slot / FP, sv = a.stage[u];
-    const uint32_t hp = (uint32_t)((key >> a.sb) & ((1u << HOP_BITS) - 1));
-    const uint64_t ser = L.su[sv];
-    const uint64_t r0 = a.rel0[m];
-    const uint64_t j0 = first_hb(t, r0, a.hb_ns);
-    for (uint32_t k = 0; k < a.hist; k++) {
-      const uint64_t T = r0 + (j0 + k) * a.hb_ns;
-      if (T + L.lmax[sv] < lo || T + L.lmin[sv] >= hi) continue;
-      const uint64_t hab = a.habs0[m] + j0 + k;
-      auto ihave = [&](uint32_t e) {  // v's IHAVE to w; IWANT + answer if w has not seen it
-        const uint32_t w = e & 0xFFFFFFu, sw = e >> STAGE_SHIFT;
-        const uint64_t lvw = L.lat[sv * S + sw];
-        const uint64_t ti = T + lvw;
-        if (ti < lo || ti >= hi) return;
-        const uint64_t sd = L.sd[sw];
-        const uint64_t A = ti + L.lat[sw * S + sv] + ser + lvw + (sd > ser ? sd - ser : 0);
-        if (a.churn) {  // IHAVE or answer lost: epochs counted from the heartbeat's (= ev_epoch)
-          const uint64_t lim = a.q0[m] + a.horizon;
-          const uint64_t hi_ = ep_plus(hab, lvw, a.hb_ns), ha = ep_plus(hab, A - T, a.hb_ns);
-          if (hi_ > lim || ep_off(a, hi_, w) || ha > lim || ep_off(a, ha, w)) return;
-        }
-        const size_t dst = (size_t)w * LL + slot;
-        // final before this bucket (its tile's final bit from an earlier scan:
-        // key time < that bucket's end <= lo <= t_i): seen, no key read
-        if (a.tstamp && ((a.fbits[dst >> 6] >> (dst & 63)) & 1) && a.tstamp[dst >> 6] != a.launch + 1) return;
-        const uint64_t kw = a.keys[dst];
-        if (kw != INF64 && (kw >> a.tshift) <= ti) return;  // already seen: no IWANT
-        iw++;
-        if (A > a.tmax) err |= ERR_TIME;
-        if (hp + 1 >= (1u << HOP_BITS)) err |= ERR_HOPS;
-        const uint64_t nk = (A << a.tshift) | ((uint64_t)(hp + 1) << a.sb) | u;
-        if (nk < kw) {
-          atomicMin((unsigned long long*)&a.keys[dst], (unsigned long long)nk);
-          if (a.tstamp) a.touched[dst >> 6] = 1;
-          nmin = nk < nmin ? nk : nmin;
-        }
-      };
-      // v gossips only while online, within the message's lifetime
-      if (a.churn && (hab > a.q0[m] + a.horizon || ep_off(a, hab, u))) continue;
-      for_each_gossip_target(a, u, hab, ihave);
-    }
+    const uint32_t ns = __builtin_amdgcn_readfirstlane(a.gs_cnt[wave]);
+    for (uint32_t i = lane; i < ns; i += 64) gossip_sender<FP>(a, L, lo, hi, a.gs_idx[seg + i], a.gs_switch, nmin, iw, err);
+  } else {
+    for (uint32_t i = lane; i < n; i += 64) gossip_sender<FP>(a, L, lo, hi, a.gl_idx[seg + i], 0, nmin, iw, err);
   }
   nmin = wave_min(nmin);
   iw = wave_sum(iw);

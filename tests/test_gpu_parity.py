@@ -448,6 +448,22 @@ def test_churn_time_varying_mesh(frags, gossip, fast, idw):
         assert st["gossip_iwant"] > 0
 
 
+@pytest.mark.parametrize("switch", ["0", "1", "3", "1000"])
+def test_churn_gossip_sender_receiver_switch(monkeypatch, switch):
+    """Lazy gossip under churn decides a message's heartbeats k < GS_GOSSIP_SWITCH
+    receiver-centric (inverse IHAVE lists, undelivered lanes) and the later ones
+    sender-centric (holders within their history window): every split point,
+    from all-sender (0) to all-receiver (1000), is bit-exact against the oracle,
+    IWANT count included."""
+    monkeypatch.setenv("GS_GOSSIP_SWITCH", switch)
+    kw = dict(churn_ppm=20000, lazy_gossip=1, heartbeat_ns=100_000_000, hb_phase_ns=T0 - 2_000_000_000 + 37_000_000,
+              churn_down=8, churn_horizon=12)
+    p = oracle.params(peers=800, seed=52, **kw)
+    sim, res = compare(p, 5, (50, 150, 40, 130), _sched(32, 800), batch=32)
+    st = sim.stats()
+    assert 0 < st["deliveries"] < 32 * 799 and st["gossip_iwant"] > 0
+
+
 def test_churn_errors():
     p = oracle.params(peers=200, seed=3, churn_ppm=10000)  # hb_phase 0: publishes ~1e9 heartbeats later
     sim, _ = gpu_sim(p, 1, (50, 50, 50, 50))
