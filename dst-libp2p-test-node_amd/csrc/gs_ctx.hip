@@ -14,6 +14,8 @@ namespace gs {
 
 Ctx::~Ctx() {
   for (auto e : ev_pool) (void)hipEventDestroy(e);
+  for (auto e : side_ev) (void)hipEventDestroy(e);
+  if (side) (void)hipStreamDestroy(side);
   if (h_pinned) (void)hipHostFree(h_pinned);
   if (h_block) (void)hipHostFree(h_block);
   if (stream) (void)hipStreamDestroy(stream);

@@ -75,6 +75,8 @@ struct Ctx {
   gs_config cfg{};
   std::string last_error;
   hipStream_t stream = nullptr;
+  hipStream_t side = nullptr;           // second stream: churn IHAVE lists beside the epoch steps
+  std::vector<hipEvent_t> side_ev;      // its chunk events
   bool timing = false;
   bool traffic = false;        // gs_set_traffic: per-peer send/receive counters
   DevBuf<uint64_t> d_traffic;  // [N][GS_TRAFFIC_COLS]
@@ -107,6 +109,8 @@ struct Ctx {
   DevBuf<uint64_t> d_ring_off;  // [R][(N+63)/64]
   DevBuf<uint32_t> d_ring_in;     // lazy gossip: [R][N][GT_IN] senders of the IHAVEs reaching a peer per epoch
   DevBuf<uint32_t> d_ring_incnt;  // [R][N] their number (above GT_IN: k_gossip recomputes)
+  DevBuf<uint64_t> d_gout;        // scratch of ring_in_lists: IHAVE target masks over CSR rows, per (epoch, sender)
+  DevBuf<uint8_t> d_csrpos;       // [nnz] position of the row's peer in its neighbour's row (ring_in_lists)
   DevBuf<uint64_t> d_q0, d_r0;  // [B] epoch of t_pub, t_pub - start of that epoch
   uint32_t ring_R = 0;
   uint64_t churn_state = 0, ring_lo = 1, ring_hi = 0;  // mesh state epoch; valid ring epochs
@@ -130,8 +134,13 @@ struct Ctx {
   DevBuf<uint32_t> d_gl_idx; // lazy gossip: lanes with an IHAVE arrival in the bucket
   DevBuf<uint32_t> d_gl_cnt;
   DevBuf<uint64_t> d_gl_key; // receiver-centric gossip: the listed lane's key (saves its re-read)
-  DevBuf<uint32_t> d_gs_idx; // churn: sender-centric gossip lanes of late heartbeats (RelaxArgs::gs_switch)
-  DevBuf<uint32_t> d_gs_cnt;
+  DevBuf<uint32_t> d_hl_idx;  // churn + gossip: holder list (RelaxArgs::hl_*): lane, key, count, launch marks
+  DevBuf<uint64_t> d_hl_key;
+  DevBuf<uint64_t> d_hl_cnt;
+  DevBuf<uint64_t> d_hl_mark;
+  DevBuf<uint32_t> d_hs_idx;  // per scan wave scratch of the holders found (copied to the list)
+  DevBuf<uint64_t> d_hs_key;
+  DevBuf<uint64_t> d_hl_min;
   DevBuf<uint64_t> d_nonfinal;  // [3]
   DevBuf<uint64_t> d_rel0;   // [B] first heartbeat >= t_pub (relative ns)
   DevBuf<uint64_t> d_habs0;  // [B] its absolute heartbeat index

@@ -451,101 +451,149 @@ __global__ __launch_bounds__(TB) void k_extract(MeshArgs a, uint32_t* mesh, uint
 // Lazy gossip under churn: who sends IHAVEs to whom at epoch h. Peer u's
 // targets are the r smallest (rng(GOSSIP, u, h, w), w) among its online
 // connections outside its epoch-h mesh, r = max(D_lazy, factor·|non-mesh|)
-// capped at |non-mesh|. They are stored inverted, per
-// target: in[w] lists the senders v whose epoch-h IHAVEs reach w (packed
-// stage << 24 | v, at most GT_IN; incnt[w] counts all of them, so a count
-// above GT_IN tells k_gossip to recompute). The receiver side of lazy gossip
-// (k_gossip, receiver-centric under churn) then reads only the lists of the
-// lanes that have not yet received a message. One sender per thread: the
-// selection is serial compute (one rng per connection, an 8-deep sorted
-// insert in registers with static indices; the rare fan-outs above 8 rescan
-// for the next pair).
-__device__ __forceinline__ void gossip_in_scatter(const uint64_t* __restrict__ row, const uint32_t* __restrict__ col,
-                                                  const uint32_t* __restrict__ mesh, const uint64_t* __restrict__ off,
-                                                  const uint8_t* __restrict__ stage, uint64_t seed, uint32_t h,
-                                                  uint32_t d_lazy, uint32_t gf_milli, uint32_t* __restrict__ in,
-                                                  uint32_t* __restrict__ incnt, uint32_t u) {
-  if (is_off(off, u)) return;  // offline peers gossip nothing
-  uint32_t mrow[MESH_W];
-  const uint4* rp = reinterpret_cast<const uint4*>(mesh + (size_t)u * MESH_W);
-#pragma unroll
-  for (int q = 0; q < 4; q++) {
-    const uint4 x = rp[q];
-    mrow[4 * q] = x.x & 0xFFFFFFu; mrow[4 * q + 1] = x.y & 0xFFFFFFu;
-    mrow[4 * q + 2] = x.z & 0xFFFFFFu; mrow[4 * q + 3] = x.w & 0xFFFFFFu;
-  }
-  auto eligible = [&](uint32_t w) {
-    bool inm = false;
-#pragma unroll
-    for (int q = 0; q < (int)MESH_W; q++) inm |= mrow[q] == w;
-    return !inm && !is_off(off, w);
-  };
-  auto lt = [](uint64_t k1, uint32_t w1, uint64_t k2, uint32_t w2) { return k1 < k2 || (k1 == k2 && w1 < w2); };
-  const uint32_t me = ((uint32_t)stage[u] << STAGE_SHIFT) | u;
-  auto emit = [&](uint32_t w) {
-    const uint32_t pos = atomicAdd(&incnt[w], 1u);
-    if (pos < GT_IN) in[(size_t)w * GT_IN + pos] = me;
-  };
-  uint64_t kk[GT_W];
-  uint32_t ww[GT_W];
-#pragma unroll
-  for (int q = 0; q < (int)GT_W; q++) { kk[q] = INF64; ww[q] = ~0u; }
-  uint32_t nonmesh = 0;
+// capped at |non-mesh|. The receiver side of lazy gossip
+// (k_gossip, receiver-centric under churn) reads them inverted, per target:
+// in[w] lists the senders v whose epoch-h IHAVEs reach w (packed stage << 24
+// | v, at most GT_IN; incnt[w] counts them, a count above GT_IN tells k_gossip
+// to recompute). Built in two passes per chunk of epochs, without atomics:
+//  1. k_gossip_out_range: one thread per (sender, epoch) makes the selection
+//     (one rng per connection, an 8-deep sorted insert in registers with
+//     static indices; the rare fan-outs above 8 rescan for the next pair) and
+//     stores it as a bit mask over the sender's CSR row, coalesced;
+//  2. k_gossip_in_gather: one thread per (receiver, epoch) walks its CSR row
+//     and tests its own bit in each neighbour's mask (the position of w in
+//     v's row, csrpos); the masks of one epoch (8 B per peer) stay in L2/MALL.
+// Rows wider than 63 entries have no mask (GT_WIDE): their receivers get a
+// count above GT_IN, and k_gossip selects for them itself.
+constexpr uint64_t GT_WIDE = ~0ull;
+__global__ __launch_bounds__(TB) void k_gossip_out_range(const uint64_t* __restrict__ row,
+                                                         const uint32_t* __restrict__ col,
+                                                         const uint32_t* __restrict__ ring_mesh,
+                                                         const uint64_t* __restrict__ ring_off, uint32_t N, uint32_t w64,
+                                                         uint32_t R, uint64_t seed, uint64_t h0, uint32_t d_lazy,
+                                                         uint32_t gf_milli, uint64_t* __restrict__ outm) {
+  const uint32_t u = blockIdx.x * TB + threadIdx.x;
+  if (u >= N) return;
+  const uint64_t h = h0 + blockIdx.y;
+  const size_t slot = (size_t)(h % R);
+  const uint64_t* off = ring_off + slot * w64;
   const uint64_t e0 = row[u], e1 = row[u + 1];
-  for (uint64_t e = e0; e < e1; e++) {
-    const uint32_t w = col[e];
-    if (!eligible(w)) continue;
-    nonmesh++;
-    const uint64_t rk = rng(seed, P_GOSSIP, u, h, w);
-    if (!lt(rk, w, kk[GT_W - 1], ww[GT_W - 1])) continue;
+  uint64_t mask = 0;
+  if (e1 - e0 > 63) {
+    mask = GT_WIDE;
+  } else if (!is_off(off, u)) {  // offline peers gossip nothing
+    uint32_t mrow[MESH_W];
+    const uint4* rp = reinterpret_cast<const uint4*>(ring_mesh + (slot * N + u) * MESH_W);
 #pragma unroll
-    for (int q = (int)GT_W - 1; q > 0; q--) {  // insert, shifting the larger pairs up
-      if (lt(rk, w, kk[q - 1], ww[q - 1])) { kk[q] = kk[q - 1]; ww[q] = ww[q - 1]; }
-      else if (lt(rk, w, kk[q], ww[q])) { kk[q] = rk; ww[q] = w; }
+    for (int q = 0; q < 4; q++) {
+      const uint4 x = rp[q];
+      mrow[4 * q] = x.x & 0xFFFFFFu; mrow[4 * q + 1] = x.y & 0xFFFFFFu;
+      mrow[4 * q + 2] = x.z & 0xFFFFFFu; mrow[4 * q + 3] = x.w & 0xFFFFFFu;
     }
-    if (lt(rk, w, kk[0], ww[0])) { kk[0] = rk; ww[0] = w; }
-  }
-  uint32_t r = (uint32_t)(((uint64_t)nonmesh * gf_milli) / 1000);
-  if (r < d_lazy) r = d_lazy;
-  if (r > nonmesh) r = nonmesh;
+    auto eligible = [&](uint32_t w) {
+      bool inm = false;
 #pragma unroll
-  for (int q = 0; q < (int)GT_W; q++)
-    if ((uint32_t)q < r) emit(ww[q]);
-  uint64_t pk = kk[GT_W - 1];
-  uint32_t pw = ww[GT_W - 1];
-  for (uint32_t q = GT_W; q < r; q++) {  // rare: more than GT_W targets
-    uint64_t bk = ~0ull;
-    uint32_t bw = ~0u;
+      for (int q = 0; q < (int)MESH_W; q++) inm |= mrow[q] == w;
+      return !inm && !is_off(off, w);
+    };
+    auto lt = [](uint64_t k1, uint32_t w1, uint64_t k2, uint32_t w2) { return k1 < k2 || (k1 == k2 && w1 < w2); };
+    uint64_t kk[GT_W];
+    uint32_t ww[GT_W], pp[GT_W];
+#pragma unroll
+    for (int q = 0; q < (int)GT_W; q++) { kk[q] = INF64; ww[q] = ~0u; pp[q] = 0; }
+    uint32_t nonmesh = 0;
     for (uint64_t e = e0; e < e1; e++) {
       const uint32_t w = col[e];
       if (!eligible(w)) continue;
-      const uint64_t rk = rng(seed, P_GOSSIP, u, h, w);
-      if (lt(pk, pw, rk, w) && lt(rk, w, bk, bw)) { bk = rk; bw = w; }
+      nonmesh++;
+      const uint64_t rk = rng(seed, P_GOSSIP, u, (uint32_t)h, w);
+      const uint32_t pe = (uint32_t)(e - e0);
+      if (!lt(rk, w, kk[GT_W - 1], ww[GT_W - 1])) continue;
+#pragma unroll
+      for (int q = (int)GT_W - 1; q > 0; q--) {  // insert, shifting the larger pairs up
+        if (lt(rk, w, kk[q - 1], ww[q - 1])) { kk[q] = kk[q - 1]; ww[q] = ww[q - 1]; pp[q] = pp[q - 1]; }
+        else if (lt(rk, w, kk[q], ww[q])) { kk[q] = rk; ww[q] = w; pp[q] = pe; }
+      }
+      if (lt(rk, w, kk[0], ww[0])) { kk[0] = rk; ww[0] = w; pp[0] = pe; }
     }
-    emit(bw);
-    pk = bk;
-    pw = bw;
+    uint32_t r = (uint32_t)(((uint64_t)nonmesh * gf_milli) / 1000);
+    if (r < d_lazy) r = d_lazy;
+    if (r > nonmesh) r = nonmesh;
+#pragma unroll
+    for (int q = 0; q < (int)GT_W; q++)
+      if ((uint32_t)q < r) mask |= 1ull << pp[q];
+    uint64_t pk = kk[GT_W - 1];
+    uint32_t pw = ww[GT_W - 1];
+    for (uint32_t q = GT_W; q < r; q++) {  // rare: more than GT_W targets
+      uint64_t bk = ~0ull;
+      uint32_t bw = ~0u, bp = 0;
+      for (uint64_t e = e0; e < e1; e++) {
+        const uint32_t w = col[e];
+        if (!eligible(w)) continue;
+        const uint64_t rk = rng(seed, P_GOSSIP, u, (uint32_t)h, w);
+        if (lt(pk, pw, rk, w) && lt(rk, w, bk, bw)) { bk = rk; bw = w; bp = (uint32_t)(e - e0); }
+      }
+      mask |= 1ull << bp;
+      pk = bk;
+      pw = bw;
+    }
   }
+  outm[(size_t)blockIdx.y * N + u] = mask;
 }
 
-// Inverse IHAVE lists of the ring slots of epochs h0 + blockIdx.y (one launch
-// after a run of epochs: they depend only on each epoch's snapshot, so they
-// are not on the epochs' sequential path). The slots' counters are zeroed
-// before the launch.
-__global__ __launch_bounds__(TB) void k_gossip_in_range(const uint64_t* __restrict__ row,
-                                                        const uint32_t* __restrict__ col,
-                                                        const uint32_t* __restrict__ ring_mesh,
-                                                        const uint64_t* __restrict__ ring_off,
-                                                        const uint8_t* __restrict__ stage, uint32_t N, uint32_t w64,
-                                                        uint32_t R, uint64_t seed, uint64_t h0, uint32_t d_lazy,
-                                                        uint32_t gf_milli, uint32_t* __restrict__ ring_in,
-                                                        uint32_t* __restrict__ ring_incnt) {
-  const uint32_t u = blockIdx.x * TB + threadIdx.x;
+// 16 lanes per (receiver, epoch): the group loads 16 neighbours' masks at
+// once (independent loads), ballots the hits and appends them in CSR order.
+constexpr uint32_t GIN_G = 16;
+__global__ __launch_bounds__(TB) void k_gossip_in_gather(const uint64_t* __restrict__ row,
+                                                         const uint32_t* __restrict__ col,
+                                                         const uint8_t* __restrict__ csrpos,
+                                                         const uint64_t* __restrict__ ring_off,
+                                                         const uint8_t* __restrict__ stage, uint32_t N, uint32_t w64,
+                                                         uint32_t R, uint64_t h0, const uint64_t* __restrict__ outm,
+                                                         uint32_t* __restrict__ ring_in,
+                                                         uint32_t* __restrict__ ring_incnt) {
+  const uint32_t w = (blockIdx.x * TB + threadIdx.x) / GIN_G;
+  if (w >= N) return;  // group-uniform
+  const uint32_t lane = threadIdx.x & (GIN_G - 1);
   const uint64_t h = h0 + blockIdx.y;
   const size_t slot = (size_t)(h % R);
-  if (u < N)
-    gossip_in_scatter(row, col, ring_mesh + slot * N * MESH_W, ring_off + slot * w64, stage, seed, (uint32_t)h,
-                      d_lazy, gf_milli, ring_in + slot * N * GT_IN, ring_incnt + slot * N, u);
+  const uint64_t* m = outm + (size_t)blockIdx.y * N;
+  uint32_t* lst = ring_in + (slot * N + w) * GT_IN;
+  uint32_t cnt = 0;
+  bool wide = false;
+  if (!is_off(ring_off + slot * w64, w)) {  // an offline peer is nobody's target (group-uniform)
+    const uint64_t b = row[w], en = row[w + 1];
+    for (uint64_t e0 = b; e0 < en; e0 += GIN_G) {  // group-uniform
+      const uint64_t e = e0 + lane;
+      bool hit = false, wd = false;
+      uint32_t v = 0;
+      if (e < en) {
+        v = col[e];
+        const uint64_t mv = m[v];
+        const uint32_t p = csrpos[e];
+        wd = mv == GT_WIDE || p > 63;
+        hit = !wd && ((mv >> p) & 1);
+      }
+      wide |= gballot<GIN_G>(wd) != 0;
+      const uint64_t hm = gballot<GIN_G>(hit);
+      const uint32_t pos = cnt + (uint32_t)__popcll(hm & ((1ull << lane) - 1));
+      if (hit && pos < GT_IN) lst[pos] = ((uint32_t)stage[v] << STAGE_SHIFT) | v;
+      cnt += (uint32_t)__popcll(hm);
+    }
+  }
+  if (lane == 0) ring_incnt[slot * N + w] = wide && cnt <= GT_IN ? GT_IN + 1 : cnt;
+}
+
+// Position of u in the row of w = col[e], per CSR entry e (255 past 254).
+__global__ __launch_bounds__(TB) void k_csrpos(uint32_t N, const uint64_t* __restrict__ row,
+                                               const uint32_t* __restrict__ col, const uint32_t* __restrict__ rev,
+                                               uint8_t* __restrict__ pos) {
+  const uint32_t u = blockIdx.x * TB + threadIdx.x;
+  if (u >= N) return;
+  for (uint64_t e = row[u]; e < row[u + 1]; e++) {
+    const uint64_t p = rev[e] - row[col[e]];
+    pos[e] = (uint8_t)(p < 255 ? p : 255);
+  }
 }
 
 // ---- event-driven churn epochs (the default run_epochs path) ----
@@ -738,24 +786,48 @@ inline unsigned row_blocks(uint32_t N, uint32_t G) { return (unsigned)(((uint64_
     else kernel<64><<<row_blocks(N, 64), TB, 0, s>>>(__VA_ARGS__);                      \
   } while (0)
 
-// Inverse IHAVE lists of the ring snapshots of epochs [h0, h1] (h1 - h0 <
-// ring_R), when lazy gossip is on: zero the slots' counters, then one launch.
-void ring_in_lists(Ctx& c, uint64_t h0, uint64_t h1) {
-  if (!c.cfg.lazy_gossip || !c.d_ring_incnt.p) return;
+// Inverse IHAVE lists of the ring snapshots: epochs per chunk (the masks of a
+// chunk take <= 256 MB of d_gout), one chunk [h0, h0 + ny) on stream s.
+static uint64_t ring_in_chunk_epochs(uint32_t N) {
+  return std::max<uint64_t>(1, std::min<uint64_t>(64, (256ull << 20) / ((uint64_t)N * 8)));
+}
+static void ring_in_prepare(Ctx& c, uint64_t E, hipStream_t s) {
+  const uint32_t N = c.cfg.peers;
+  c.d_csrpos.alloc(c.nnz ? c.nnz : 1);
+  c.d_gout.alloc((size_t)std::min<uint64_t>(ring_in_chunk_epochs(N), E) * N);
+  k_csrpos<<<blocks(N), TB, 0, s>>>(N, c.d_row.p, c.d_col.p, c.d_rev.p, c.d_csrpos.p);
+}
+static void ring_in_chunk(Ctx& c, uint64_t h0, uint32_t ny, hipStream_t s) {
   const uint32_t N = c.cfg.peers, R = c.ring_R, w64 = (N + 63) / 64;
-  hipStream_t s = c.stream;
-  const uint64_t E = h1 - h0 + 1;
-  const uint64_t s0 = h0 % R, first = std::min<uint64_t>(E, R - s0);  // slots s0.. then 0.. on a wrap
-  GS_HIP(hipMemsetAsync(c.d_ring_incnt.p + s0 * N, 0, first * N * 4, s));
-  if (E > first) GS_HIP(hipMemsetAsync(c.d_ring_incnt.p, 0, (E - first) * N * 4, s));
-  for (uint64_t y0 = 0; y0 < E; y0 += 32768) {  // grid.y limit
-    const uint32_t ny = (uint32_t)std::min<uint64_t>(32768, E - y0);
-    k_gossip_in_range<<<dim3(blocks(N), ny), TB, 0, s>>>(c.d_row.p, c.d_col.p, c.d_ring_mesh.p, c.d_ring_off.p,
-                                                         c.d_stage.p, N, w64, R, c.cfg.seed, h0 + y0, c.cfg.d_lazy,
-                                                         c.cfg.gossip_factor_milli, c.d_ring_in.p,
-                                                         c.d_ring_incnt.p);
-  }
+  k_gossip_out_range<<<dim3(blocks(N), ny), TB, 0, s>>>(c.d_row.p, c.d_col.p, c.d_ring_mesh.p, c.d_ring_off.p, N, w64,
+                                                        R, c.cfg.seed, h0, c.cfg.d_lazy, c.cfg.gossip_factor_milli,
+                                                        c.d_gout.p);
+  k_gossip_in_gather<<<dim3(row_blocks(N, GIN_G), ny), TB, 0, s>>>(c.d_row.p, c.d_col.p, c.d_csrpos.p,
+                                                                   c.d_ring_off.p, c.d_stage.p, N, w64, R, h0,
+                                                                   c.d_gout.p, c.d_ring_in.p, c.d_ring_incnt.p);
+}
+static bool ring_in_wanted(const Ctx& c) { return c.cfg.lazy_gossip && c.d_ring_incnt.p; }
+
+// Epochs [h0, h1] (h1 - h0 < ring_R) on the context's stream: per chunk of
+// epochs, the senders' target masks, then every receiver's list
+// (k_gossip_out_range, k_gossip_in_gather).
+void ring_in_lists(Ctx& c, uint64_t h0, uint64_t h1) {
+  if (!ring_in_wanted(c)) return;
+  const uint64_t E = h1 - h0 + 1, CE = ring_in_chunk_epochs(c.cfg.peers);
+  ring_in_prepare(c, E, c.stream);
+  for (uint64_t y0 = 0; y0 < E; y0 += CE) ring_in_chunk(c, h0 + y0, (uint32_t)std::min<uint64_t>(CE, E - y0), c.stream);
   GS_HIP(hipGetLastError());
+}
+
+// Side stream + its i-th event (created on first use).
+static hipEvent_t side_event(Ctx& c, size_t i) {
+  if (!c.side) GS_HIP(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
+  while (c.side_ev.size() <= i) {
+    hipEvent_t e;
+    GS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c.side_ev.push_back(e);
+  }
+  return c.side_ev[i];
 }
 
 MeshArgs mesh_args(Ctx& c) {
@@ -833,6 +905,19 @@ void ev_epochs(Ctx& c, MeshArgs a, uint64_t h0, uint64_t h1, bool ring) {
   } while (0)
   if (G == 16) k_ev_init<16><<<grid, TB, 0, s>>>(a);
   else k_ev_init<64><<<grid, TB, 0, s>>>(a);
+  // the IHAVE lists of the ring epochs [hr, h1] run on the side stream, a
+  // chunk as soon as its epochs are stepped (compute-bound list kernels beside
+  // the latency-bound epoch steps)
+  const bool lists = ring && ring_in_wanted(c);
+  const uint64_t CE = ring_in_chunk_epochs(N);
+  uint64_t chunk0 = hr;
+  size_t nev = 0;
+  if (lists) {
+    const hipEvent_t e = side_event(c, nev++);
+    ring_in_prepare(c, h1 - hr + 1, c.side);  // (hipMalloc before the side stream waits)
+    GS_HIP(hipEventRecord(e, s));
+    GS_HIP(hipStreamWaitEvent(c.side, e, 0));
+  }
   for (uint64_t h = h0; h <= h1; h++) {
     const uint64_t y = h - h0 + 1;
     a.epoch = (uint32_t)h;
@@ -844,10 +929,21 @@ void ev_epochs(Ctx& c, MeshArgs a, uint64_t h0, uint64_t h1, bool ring) {
     GS_EVS(EV_HB, a, nullptr, nullptr);
     GS_EVS(EV_GRAFT, a, nullptr, nullptr);
     GS_EVS(EV_APPLY, a, mesh, prev);
+    if (lists && h >= hr && (h + 1 - chunk0 == CE || h == h1)) {
+      const hipEvent_t e = side_event(c, nev++);
+      GS_HIP(hipEventRecord(e, s));
+      GS_HIP(hipStreamWaitEvent(c.side, e, 0));
+      ring_in_chunk(c, chunk0, (uint32_t)(h + 1 - chunk0), c.side);
+      chunk0 = h + 1;
+    }
   }
 #undef GS_EVS
   GS_HIP(hipGetLastError());
-  if (ring) ring_in_lists(c, hr, h1);
+  if (lists) {  // the context's stream continues once every list is written
+    const hipEvent_t e = side_event(c, nev++);
+    GS_HIP(hipEventRecord(e, c.side));
+    GS_HIP(hipStreamWaitEvent(s, e, 0));
+  }
 }
 
 // Churn epochs [h0, h1] from the current mesh state (ev_epochs); `ring`:

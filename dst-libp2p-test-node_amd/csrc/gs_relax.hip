@@ -663,6 +663,10 @@ static void launch_complete(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, co
 // The batch's fields of RelaxArgs shared by the bucket launches and the
 // traffic passes: keys, graph, link tables, churn ring, and with `gossip` the
 // lazy-gossip inputs (heartbeats per message, CSR, IHAVE target ring).
+// Bucket launches one churn + gossip batch may take (the holder list's
+// per-launch marks, RelaxArgs::hl_lo / hl_end).
+constexpr uint32_t HL_LAUNCHES = 1u << 16;
+
 static RelaxArgs relax_args(Ctx& c, const Batch& b, bool gossip) {
   RelaxArgs ra{};
   set_churn_args(c, ra);
@@ -1209,11 +1213,25 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
           ra.gl_cnt = c.d_gl_cnt.p;
           if (ra.ring_in) {
             c.d_gl_key.alloc(nwaves * ra.gl_cap);
-            c.d_gs_idx.alloc(nwaves * ra.gl_cap);
-            c.d_gs_cnt.alloc(nwaves);
             ra.gl_key = c.d_gl_key.p;
-            ra.gs_idx = c.d_gs_idx.p;
-            ra.gs_cnt = c.d_gs_cnt.p;
+            // holder list (a lane is finalised once) and per-launch marks
+            c.d_hl_idx.alloc(total);
+            c.d_hl_key.alloc(total);
+            c.d_hl_cnt.alloc(1);
+            c.d_hl_mark.alloc(2 * (size_t)HL_LAUNCHES);
+            c.d_hs_idx.alloc(nwaves * ra.gl_cap);
+            c.d_hs_key.alloc(nwaves * ra.gl_cap);
+            c.d_hl_min.alloc(3);
+            GS_HIP(hipMemsetAsync(c.d_hl_cnt.p, 0, 8, s));
+            GS_HIP(hipMemsetAsync(c.d_hl_min.p, 0xFF, 3 * 8, s));
+            ra.hs_idx = c.d_hs_idx.p;
+            ra.hs_key = c.d_hs_key.p;
+            ra.hl_min = c.d_hl_min.p;
+            ra.hl_idx = c.d_hl_idx.p;
+            ra.hl_key = c.d_hl_key.p;
+            ra.hl_cnt = (unsigned long long*)c.d_hl_cnt.p;
+            ra.hl_lo = c.d_hl_mark.p;
+            ra.hl_end = c.d_hl_mark.p + HL_LAUNCHES;
           }
           ra.nonfinal = c.d_nonfinal.p;
           if ((v & 10) == 10) {
@@ -1226,6 +1244,8 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       uint32_t launch = 0;
       const uint32_t chunk = 8;
       for (;;) {
+        if (ra.hl_idx && launch + chunk > HL_LAUNCHES)
+          c.fail(GS_EUNSUPPORTED, "churn + lazy gossip batch needs more than 65536 buckets");
         for (uint32_t q = 0; q < chunk; q++) {
           ra.launch = launch++;
           if (c.timing) {  // (start, scan end, end) per bucket

@@ -71,8 +71,17 @@ struct RelaxArgs {
   // first heartbeat) are decided sender-centric: after the eager wave only the
   // peers that received it within their history window gossip it, a few
   // hundred per message, while the undelivered lanes stay ~10 % of all
-  uint32_t* gs_idx;            // sender-centric lanes of the bucket, per scan wave
-  uint32_t* gs_cnt;
+  // so the scan appends every final lane that can gossip at such a
+  // heartbeat to a holder list when it finalises it, and k_gossip walks only
+  // the entries whose history window can still reach the bucket
+  uint32_t* hs_idx;            // per scan wave: holders found by the wave (scratch, gl segments)
+  uint64_t* hs_key;
+  uint64_t* hl_min;            // [3] per launch: earliest IHAVE arrival of any holder (k_gossip walks if < hi)
+  uint32_t* hl_idx;            // holder list: lane gid
+  uint64_t* hl_key;            // its (final) key
+  unsigned long long* hl_cnt;  // entries appended
+  uint64_t* hl_lo;             // per launch: the bucket's start
+  uint64_t* hl_end;            // per launch: list length after its scan
   uint32_t gs_switch;
   const uint32_t* mesh;
   const uint32_t* pub;
@@ -192,6 +201,7 @@ struct BucketLds {
   uint32_t su[MAX_STAGES], sd[MAX_STAGES];
   uint32_t lmin[MAX_STAGES], lmax[MAX_STAGES];  // min/max latency out of each stage
   uint32_t imin[MAX_STAGES], imax[MAX_STAGES];  // min/max latency into each stage
+  uint32_t lmax_all;                             // largest latency
 };
 
 __device__ __forceinline__ void load_tables(BucketLds& L, const RelaxArgs& a) {
@@ -217,6 +227,11 @@ __device__ __forceinline__ void load_tables(BucketLds& L, const RelaxArgs& a) {
     }
     L.imin[threadIdx.x] = mn;
     L.imax[threadIdx.x] = mx;
+  }
+  if (threadIdx.x == 0) {
+    uint32_t mx = 0;
+    for (uint32_t i = 0; i < S * S; i++) mx = a.tables[i] > mx ? a.tables[i] : mx;
+    L.lmax_all = mx;
   }
 }
 
@@ -453,6 +468,7 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     a.ctrl[(a.launch + 2) % 3] = INF64;
     if (GOSSIP) a.nonfinal[(a.launch + 1) % 3] = 0;
+    if (GOSSIP && a.hl_min) a.hl_min[(a.launch + 2) % 3] = INF64;
   }
   const uint64_t cur = a.ctrl[a.launch % 3];
   if (cur == INF64) return;  // the frontier kernel exits on the same word
@@ -468,7 +484,7 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
   const uint64_t nwaves = (uint64_t)gridDim.x * (TB / 64);
   const size_t seg = (size_t)wave * a.seg_cap;
   const size_t gseg = (size_t)wave * a.gl_cap;
-  uint64_t nmin = INF64, nonfin = 0, nscan = 0, nscan_g = 0;
+  uint64_t nmin = INF64, nonfin = 0, nscan = 0, nscan_g = 0, hmin = INF64;
   uint32_t cnt = 0, gcnt = 0, scnt = 0, err = 0;
   const uint64_t hspan = GOSSIP ? (uint64_t)a.hist * a.hb_ns : 0;
   // Tiles are visited per wave in groups: with SKIP a group is 64 consecutive
@@ -574,21 +590,23 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
           if (k1 <= kr) gnext = r0 + k1 * a.hb_ns + imn > hi ? r0 + k1 * a.hb_ns + imn : hi;
         }
       }
-      // sender-centric: a final lane gossips at its history_gossip heartbeats
-      // (under churn only those with index >= gs_switch, within the lifetime)
-      if (fin && a.hist && (!a.ring_in || alive) && (t > r0 ? t : r0) + hspan + L.lmax[sv] >= lo) {
+      if (a.ring_in) {
+        // holders: a lane finalised in this bucket that gossips at a heartbeat
+        // k >= gs_switch (its first gossip heartbeat j0 >= gs_switch - hist + 1,
+        // i.e. t > T_(gs_switch - hist)) joins the holder list; so does the
+        // publisher's own lane (key 0) when gs_switch < hist
+        const bool act = pending && t >= lo && t < hi && alive;
+        swork = act && (a.gs_switch < a.hist || t > r0 + (uint64_t)(a.gs_switch - a.hist) * a.hb_ns);
+      } else if (fin && a.hist && (t > r0 ? t : r0) + hspan + L.lmax[sv] >= lo) {
+        // sender-centric (frozen mesh): a final lane gossips at its
+        // history_gossip heartbeats T_k >= t
         const uint64_t lmn = L.lmin[sv], lmx = L.lmax[sv];
         const uint64_t j0 = first_hb(t, r0, a.hb_ns);
-        uint64_t kb = j0, ke = j0 + a.hist;  // heartbeat indices [kb, ke)
-        if (a.ring_in) {
-          kb = kb > a.gs_switch ? kb : a.gs_switch;
-          ke = ke < kl + 1 ? ke : kl + 1;
-        }
-        const uint64_t tlast = r0 + (ke - 1) * a.hb_ns;
-        if (kb < ke && tlast + lmx >= lo) {
-          for (uint64_t k = kb; k < ke; k++) {
-            const uint64_t T = r0 + k * a.hb_ns;
-            swork |= (T + lmx >= lo && T + lmn < hi);
+        const uint64_t tlast = r0 + (j0 + a.hist - 1) * a.hb_ns;
+        if (tlast + lmx >= lo) {
+          for (uint32_t k = 0; k < a.hist; k++) {
+            const uint64_t T = r0 + (j0 + k) * a.hb_ns;
+            gwork |= (T + lmx >= lo && T + lmn < hi);
             if (T + lmx >= hi)
               for (uint32_t s = 0; s < a.S; s++) {
                 const uint64_t x = T + L.lat[sv * a.S + s];
@@ -596,10 +614,6 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
               }
           }
         }
-      }
-      if (!a.ring_in) {  // frozen mesh: the gossip list holds the sender-centric lanes
-        gwork = swork;
-        swork = false;
       }
       if (gnext != INF64) {
         if (gnext > a.tmax) err |= ERR_TIME;
@@ -614,7 +628,16 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
       }
       gcnt += (uint32_t)__popcll(gm);
       const uint64_t sm = __ballot(swork);
-      if (swork) a.gs_idx[gseg + scnt + (uint32_t)__popcll(sm & ((1ull << lane) - 1))] = (uint32_t)gid;
+      if (swork) {  // to this wave's scratch segment; copied to the list at the end
+        const uint32_t pos = scnt + (uint32_t)__popcll(sm & ((1ull << lane) - 1));
+        a.hs_idx[gseg + pos] = (uint32_t)gid;
+        a.hs_key[gseg + pos] = key;
+        // its first IHAVE arrival is at or after max(t, T_gs_switch) + the
+        // smallest latency out of its stage (k_gossip's walk test)
+        const uint64_t tk = r0 + (uint64_t)a.gs_switch * a.hb_ns;
+        const uint64_t lb = (t > tk ? t : tk) + L.lmin[sv];
+        hmin = lb < hmin ? lb : hmin;
+      }
       scnt += (uint32_t)__popcll(sm);
       if constexpr (SKIP) {  // the tile's gossip state for later skips
         const uint64_t tg = wave_min(gnext);
@@ -651,8 +674,30 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
     for (int off = 32; off > 0; off >>= 1) err |= __shfl_xor(err, off);
     if (lane == 0) {
       a.gl_cnt[wave] = gcnt;
-      if (a.gs_cnt) a.gs_cnt[wave] = scnt;
       if (err) atomicOr((unsigned*)&a.counters[C_ERR], err);
+    }
+    if (a.hl_idx) {  // holders: one list claim per block, waves copy their scratch
+      __shared__ uint32_t s_hn[TB / 64];
+      __shared__ uint64_t s_hm[TB / 64];
+      __shared__ unsigned long long s_base;
+      const int wv = threadIdx.x >> 6;
+      hmin = wave_min(hmin);
+      if (lane == 0) { s_hn[wv] = scnt; s_hm[wv] = hmin; }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        uint64_t mn = INF64;
+        for (int i = 0; i < TB / 64; i++) { tot += s_hn[i]; mn = s_hm[i] < mn ? s_hm[i] : mn; }
+        s_base = tot ? atomicAdd(a.hl_cnt, (unsigned long long)tot) : 0;
+        if (mn != INF64) atomicMin((unsigned long long*)&a.hl_min[a.launch % 3], (unsigned long long)mn);
+      }
+      __syncthreads();
+      uint64_t base = s_base;
+      for (int i = 0; i < wv; i++) base += s_hn[i];
+      for (uint32_t i = lane; i < scnt; i += 64) {
+        a.hl_idx[base + i] = a.hs_idx[gseg + i];
+        a.hl_key[base + i] = a.hs_key[gseg + i];
+      }
     }
   }
   __shared__ uint64_t s_red[TB / 64 * 5];
@@ -828,12 +873,13 @@ __device__ __forceinline__ void gossip_receiver(const RelaxArgs& a, const Bucket
 // history_gossip heartbeats (index >= kmin) with an IHAVE arrival in [lo, hi)
 // re-selects v's targets; a target that has not seen (m, f) by the arrival
 // sends IWANT and v's answer is pushed into its key.
+// With `next` (the holder list) the lane's next IHAVE arrival at or after hi
+// is folded into *next as well (the scan does that for listed lanes).
 template <int FP>
 __device__ __forceinline__ void gossip_sender(const RelaxArgs& a, const BucketLds& L, uint64_t lo, uint64_t hi,
-                                              uint64_t gid, uint64_t kmin, uint64_t& nmin, uint64_t& iw,
-                                              uint32_t& err) {
+                                              uint64_t gid, uint64_t key, uint64_t kmin, uint64_t* next,
+                                              uint64_t& nmin, uint64_t& iw, uint32_t& err) {
   const uint32_t LL = a.L, S = a.S;
-  const uint64_t key = a.keys[gid];
   const uint64_t t = key >> a.tshift;
   const uint32_t u = row_of(gid, LL), slot = (uint32_t)(gid - (uint64_t)u * LL);
   const uint32_t m = slot / FP, sv = a.stage[u];
@@ -844,8 +890,13 @@ __device__ __forceinline__ void gossip_sender(const RelaxArgs& a, const BucketLd
   for (uint32_t k = 0; k < a.hist; k++) {
     if (j0 + k < kmin) continue;
     const uint64_t T = r0 + (j0 + k) * a.hb_ns;
-    if (T + L.lmax[sv] < lo || T + L.lmin[sv] >= hi) continue;
     const uint64_t hab = a.habs0[m] + j0 + k;
+    if (next && T + L.lmax[sv] >= hi && !(a.churn && hab > a.q0[m] + a.horizon))
+      for (uint32_t s = 0; s < S; s++) {
+        const uint64_t x = T + L.lat[sv * S + s];
+        if (x >= hi && x < *next) *next = x;
+      }
+    if (T + L.lmax[sv] < lo || T + L.lmin[sv] >= hi) continue;
     auto ihave = [&](uint32_t e) {  // v's IHAVE to w; IWANT + answer if w has not seen it
       const uint32_t w = e & 0xFFFFFFu, sw = e >> STAGE_SHIFT;
       const uint64_t lvw = L.lat[sv * S + sw];
@@ -897,10 +948,44 @@ __global__ __launch_bounds__(TB) void k_gossip(RelaxArgs a) {
   if (a.ring_in) {
     for (uint32_t i = lane; i < n; i += 64)
       gossip_receiver<FP>(a, L, lo, hi, a.gl_idx[seg + i], a.gl_key[seg + i], nmin, iw, err);
-    const uint32_t ns = __builtin_amdgcn_readfirstlane(a.gs_cnt[wave]);
-    for (uint32_t i = lane; i < ns; i += 64) gossip_sender<FP>(a, L, lo, hi, a.gs_idx[seg + i], a.gs_switch, nmin, iw, err);
+    // holders (heartbeats >= gs_switch): the entries finalised after the last
+    // launch whose bucket ended before lo - (hist * hb + the largest latency),
+    // the earliest finalisation time whose IHAVEs can still arrive at lo
+    const uint64_t end = *a.hl_cnt;
+    const uint64_t span = (uint64_t)a.hist * a.hb_ns + L.lmax_all;
+    uint64_t start = 0;
+    if (lo > span) {
+      const uint64_t x = lo - span;
+      uint32_t l0 = 0, l1 = a.launch;  // last launch with lo_l + delta <= x: binary search on [l0, l1)
+      while (l0 < l1) {
+        const uint32_t mid = (l0 + l1) >> 1;
+        if (a.hl_lo[mid] + a.delta <= x) l0 = mid + 1; else l1 = mid;
+      }
+      start = l0 > 0 ? a.hl_end[l0 - 1] : 0;
+    }
+    const uint64_t hm = a.hl_min[a.launch % 3];
+    uint64_t hnext = INF64;
+    if (hm < hi) {
+      const uint64_t nthreads = (uint64_t)gridDim.x * TB;
+      for (uint64_t i = start + (uint64_t)blockIdx.x * TB + threadIdx.x; i < end; i += nthreads)
+        gossip_sender<FP>(a, L, lo, hi, a.hl_idx[i], a.hl_key[i], a.gs_switch, &hnext, nmin, iw, err);
+    } else if (blockIdx.x == 0 && threadIdx.x == 0) {
+      hnext = hm;  // no holder's IHAVE lands in this bucket: the bound carries over
+    }
+    hnext = wave_min(hnext);
+    if (hnext != INF64) {
+      if (hnext > a.tmax) err |= ERR_TIME;
+      const uint64_t gk = hnext << a.tshift;
+      nmin = gk < nmin ? gk : nmin;
+      if (lane == 0) atomicMin((unsigned long long*)&a.hl_min[(a.launch + 1) % 3], (unsigned long long)hnext);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      a.hl_lo[a.launch] = lo;
+      a.hl_end[a.launch] = end;
+    }
   } else {
-    for (uint32_t i = lane; i < n; i += 64) gossip_sender<FP>(a, L, lo, hi, a.gl_idx[seg + i], 0, nmin, iw, err);
+    for (uint32_t i = lane; i < n; i += 64)
+      gossip_sender<FP>(a, L, lo, hi, a.gl_idx[seg + i], a.keys[a.gl_idx[seg + i]], 0, nullptr, nmin, iw, err);
   }
   nmin = wave_min(nmin);
   iw = wave_sum(iw);
