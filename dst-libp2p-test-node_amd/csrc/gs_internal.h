@@ -144,6 +144,7 @@ struct Ctx {
   DevBuf<uint64_t> d_nonfinal;  // [3]
   DevBuf<uint64_t> d_rel0;   // [B] first heartbeat >= t_pub (relative ns)
   DevBuf<uint64_t> d_habs0;  // [B] its absolute heartbeat index
+  DevBuf<uint8_t> d_malive;  // [B] churn + gossip: the message can spread (publisher online at t_pub)
   DevBuf<uint32_t> d_pub;    // [B]
   DevBuf<uint64_t> d_tpub;   // [B]
   DevBuf<uint64_t> d_tc;     // [N * B] peer-major completion times (device result)

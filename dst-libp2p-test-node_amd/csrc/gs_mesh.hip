@@ -471,10 +471,12 @@ __global__ __launch_bounds__(TB) void k_gossip_out_range(const uint64_t* __restr
                                                          const uint32_t* __restrict__ ring_mesh,
                                                          const uint64_t* __restrict__ ring_off, uint32_t N, uint32_t w64,
                                                          uint32_t R, uint64_t seed, uint64_t h0, uint32_t d_lazy,
-                                                         uint32_t gf_milli, uint64_t* __restrict__ outm) {
-  const uint32_t u = blockIdx.x * TB + threadIdx.x;
-  if (u >= N) return;
-  const uint64_t h = h0 + blockIdx.y;
+                                                         uint32_t gf_milli, uint64_t* __restrict__ outm,
+                                                         uint32_t ny) {
+  // grid-stride over (sender, epoch): the side stream may run on a capped grid
+  for (uint64_t it = (uint64_t)blockIdx.x * TB + threadIdx.x; it < (uint64_t)N * ny; it += (uint64_t)gridDim.x * TB) {
+  const uint32_t u = (uint32_t)(it % N), y = (uint32_t)(it / N);
+  const uint64_t h = h0 + y;
   const size_t slot = (size_t)(h % R);
   const uint64_t* off = ring_off + slot * w64;
   const uint64_t e0 = row[u], e1 = row[u + 1];
@@ -538,7 +540,8 @@ __global__ __launch_bounds__(TB) void k_gossip_out_range(const uint64_t* __restr
       pw = bw;
     }
   }
-  outm[(size_t)blockIdx.y * N + u] = mask;
+  outm[(size_t)y * N + u] = mask;
+  }
 }
 
 // 16 lanes per (receiver, epoch): the group loads 16 neighbours' masks at
@@ -551,13 +554,15 @@ __global__ __launch_bounds__(TB) void k_gossip_in_gather(const uint64_t* __restr
                                                          const uint8_t* __restrict__ stage, uint32_t N, uint32_t w64,
                                                          uint32_t R, uint64_t h0, const uint64_t* __restrict__ outm,
                                                          uint32_t* __restrict__ ring_in,
-                                                         uint32_t* __restrict__ ring_incnt) {
-  const uint32_t w = (blockIdx.x * TB + threadIdx.x) / GIN_G;
-  if (w >= N) return;  // group-uniform
+                                                         uint32_t* __restrict__ ring_incnt, uint32_t ny) {
   const uint32_t lane = threadIdx.x & (GIN_G - 1);
-  const uint64_t h = h0 + blockIdx.y;
+  // grid-stride over (receiver, epoch) groups (group-uniform)
+  for (uint64_t it = ((uint64_t)blockIdx.x * TB + threadIdx.x) / GIN_G; it < (uint64_t)N * ny;
+       it += (uint64_t)gridDim.x * (TB / GIN_G)) {
+  const uint32_t w = (uint32_t)(it % N), y = (uint32_t)(it / N);
+  const uint64_t h = h0 + y;
   const size_t slot = (size_t)(h % R);
-  const uint64_t* m = outm + (size_t)blockIdx.y * N;
+  const uint64_t* m = outm + (size_t)y * N;
   uint32_t* lst = ring_in + (slot * N + w) * GT_IN;
   uint32_t cnt = 0;
   bool wide = false;
@@ -582,6 +587,7 @@ __global__ __launch_bounds__(TB) void k_gossip_in_gather(const uint64_t* __restr
     }
   }
   if (lane == 0) ring_incnt[slot * N + w] = wide && cnt <= GT_IN ? GT_IN + 1 : cnt;
+  }
 }
 
 // Position of u in the row of w = col[e], per CSR entry e (255 past 254).
@@ -797,14 +803,17 @@ static void ring_in_prepare(Ctx& c, uint64_t E, hipStream_t s) {
   c.d_gout.alloc((size_t)std::min<uint64_t>(ring_in_chunk_epochs(N), E) * N);
   k_csrpos<<<blocks(N), TB, 0, s>>>(N, c.d_row.p, c.d_col.p, c.d_rev.p, c.d_csrpos.p);
 }
-static void ring_in_chunk(Ctx& c, uint64_t h0, uint32_t ny, hipStream_t s) {
+// bpc = blocks per CU (0: one thread / group per item): beside the epoch steps
+// the lists run on a capped grid, so the steps' blocks find free slots
+static void ring_in_chunk(Ctx& c, uint64_t h0, uint32_t ny, hipStream_t s, uint32_t bpc = 0) {
   const uint32_t N = c.cfg.peers, R = c.ring_R, w64 = (N + 63) / 64;
-  k_gossip_out_range<<<dim3(blocks(N), ny), TB, 0, s>>>(c.d_row.p, c.d_col.p, c.d_ring_mesh.p, c.d_ring_off.p, N, w64,
-                                                        R, c.cfg.seed, h0, c.cfg.d_lazy, c.cfg.gossip_factor_milli,
-                                                        c.d_gout.p);
-  k_gossip_in_gather<<<dim3(row_blocks(N, GIN_G), ny), TB, 0, s>>>(c.d_row.p, c.d_col.p, c.d_csrpos.p,
-                                                                   c.d_ring_off.p, c.d_stage.p, N, w64, R, h0,
-                                                                   c.d_gout.p, c.d_ring_in.p, c.d_ring_incnt.p);
+  const uint64_t cap = bpc ? (uint64_t)std::max(c.num_cus, 1) * bpc : ~0ull;
+  const unsigned g1 = (unsigned)std::min<uint64_t>(cap, ((uint64_t)N * ny + TB - 1) / TB);
+  const unsigned g2 = (unsigned)std::min<uint64_t>(cap, ((uint64_t)N * ny * GIN_G + TB - 1) / TB);
+  k_gossip_out_range<<<g1, TB, 0, s>>>(c.d_row.p, c.d_col.p, c.d_ring_mesh.p, c.d_ring_off.p, N, w64, R, c.cfg.seed,
+                                       h0, c.cfg.d_lazy, c.cfg.gossip_factor_milli, c.d_gout.p, ny);
+  k_gossip_in_gather<<<g2, TB, 0, s>>>(c.d_row.p, c.d_col.p, c.d_csrpos.p, c.d_ring_off.p, c.d_stage.p, N, w64, R, h0,
+                                       c.d_gout.p, c.d_ring_in.p, c.d_ring_incnt.p, ny);
 }
 static bool ring_in_wanted(const Ctx& c) { return c.cfg.lazy_gossip && c.d_ring_incnt.p; }
 
@@ -821,7 +830,13 @@ void ring_in_lists(Ctx& c, uint64_t h0, uint64_t h1) {
 
 // Side stream + its i-th event (created on first use).
 static hipEvent_t side_event(Ctx& c, size_t i) {
-  if (!c.side) GS_HIP(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
+  if (!c.side) {  // lowest priority: the epoch steps' dependent chain is dispatched first
+    int lo = 0, hi = 0;
+    GS_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    const char* sp = getenv("GS_SIDE_PRIORITY");  // A/B knob: 0 = default priority
+    if (sp && *sp && atoi(sp) == 0) GS_HIP(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
+    else GS_HIP(hipStreamCreateWithPriority(&c.side, hipStreamNonBlocking, lo));
+  }
   while (c.side_ev.size() <= i) {
     hipEvent_t e;
     GS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -909,6 +924,8 @@ void ev_epochs(Ctx& c, MeshArgs a, uint64_t h0, uint64_t h1, bool ring) {
   // chunk as soon as its epochs are stepped (compute-bound list kernels beside
   // the latency-bound epoch steps)
   const bool lists = ring && ring_in_wanted(c);
+  const char* sb = getenv("GS_SIDE_BPC");  // list blocks per CU beside the steps (0: full grid)
+  const uint32_t side_bpc = sb && *sb ? (uint32_t)atoi(sb) : 2u;
   const uint64_t CE = ring_in_chunk_epochs(N);
   uint64_t chunk0 = hr;
   size_t nev = 0;
@@ -933,7 +950,7 @@ void ev_epochs(Ctx& c, MeshArgs a, uint64_t h0, uint64_t h1, bool ring) {
       const hipEvent_t e = side_event(c, nev++);
       GS_HIP(hipEventRecord(e, s));
       GS_HIP(hipStreamWaitEvent(c.side, e, 0));
-      ring_in_chunk(c, chunk0, (uint32_t)(h + 1 - chunk0), c.side);
+      ring_in_chunk(c, chunk0, (uint32_t)(h + 1 - chunk0), c.side, side_bpc);
       chunk0 = h + 1;
     }
   }

@@ -1083,6 +1083,8 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
   c.d_hops.alloc((size_t)N * Bmax);
   c.d_cnt_save.alloc(C_COUNT);
   std::vector<uint64_t> rel0(Bmax), habs0(Bmax);
+  std::vector<uint8_t> malive(Bmax);
+  uint64_t g0 = INF64;
   // Timing events come from a per-context pool: [0] run start, [1] run end,
   // then one (start, scan end, end) triple around every relaxation launch.
   size_t n_ev = 0;
@@ -1149,6 +1151,19 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       c.d_habs0.alloc(Bmax);
       GS_HIP(hipMemcpyAsync(c.d_rel0.p, rel0.data(), B * 8, hipMemcpyHostToDevice, s));
       GS_HIP(hipMemcpyAsync(c.d_habs0.p, habs0.data(), B * 8, hipMemcpyHostToDevice, s));
+      g0 = INF64;
+      if (churn) {  // per message: gossip can spread it (publisher online at t_pub, a heartbeat in its lifetime)
+        for (uint32_t q = 0; q < B; q++) {
+          malive[q] = habs0[q] <= q0v[q] + c.cfg.churn_horizon &&
+                      !offline_draw(c.cfg.seed, c.cfg.churn_ppm, c.cfg.churn_down, sched[i0 + q].publisher, q0v[q]);
+          g0 = std::min(g0, rel0[q]);
+        }
+        uint64_t lmin = INF64;
+        for (uint64_t l : c.lat_ns) lmin = std::min(lmin, l);
+        g0 += lmin;
+        c.d_malive.alloc(Bmax);
+        GS_HIP(hipMemcpyAsync(c.d_malive.p, malive.data(), B, hipMemcpyHostToDevice, s));
+      }
       GS_HIP(hipStreamSynchronize(s));  // rel0 / habs0 host vectors are rewritten by the next batch
     }
     const uint64_t total = (uint64_t)N * L;
@@ -1182,6 +1197,10 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       reset(v, with_gossip);
       launch_seed(c, b, 0, N);
       RelaxArgs ra = relax_args(c, b, with_gossip);
+      if (ra.ring_in) {
+        ra.malive = c.d_malive.p;
+        ra.g0 = g0;
+      }
       ra.busy = c.d_busy.p;
       ra.meta = reinterpret_cast<TileMeta*>(c.d_meta.p);
       ra.fbits = c.d_fbits.p;

@@ -83,6 +83,8 @@ struct RelaxArgs {
   uint64_t* hl_lo;             // per launch: the bucket's start
   uint64_t* hl_end;            // per launch: list length after its scan
   uint32_t gs_switch;
+  const uint8_t* malive;       // churn + gossip, per message: its publisher was online at t_pub (else nobody holds it)
+  uint64_t g0;                 //   and no IHAVE of the batch lands before g0 = min rel0 + the smallest latency
   const uint32_t* mesh;
   const uint32_t* pub;
   const uint8_t* stage;
@@ -564,15 +566,16 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
       const uint64_t r0 = (fin || a.ring_in) && valid ? a.rel0[m] : 0;
       // churn: heartbeat indices [0, kl] lie in the message's lifetime (none
       // when its publisher was offline at t_pub: nobody holds it)
-      const bool alive = a.ring_in && valid && slot % FP < a.F && a.hist && a.habs0[m] <= a.q0[m] + a.horizon &&
-                         !ep_off(a, a.q0[m], a.pub[m]);
+      const bool alive = a.ring_in && valid && slot % FP < a.F && a.hist && a.malive[m];
       const uint64_t kl = alive ? a.q0[m] + a.horizon - a.habs0[m] : 0;
       if (a.ring_in) {
         // receiver-centric (churn, heartbeats k < gs_switch): a lane without a
         // key before this bucket lists itself when an IHAVE of one of its
         // message's heartbeats T_k can reach its peer inside [lo, hi) (T_k +
         // min / max latency into its stage), up to the message's lifetime
-        if (alive && !(pending && t < lo) && a.gs_switch > 0) {
+        if (alive && !(pending && t < lo) && a.gs_switch > 0 && hi <= a.g0) {
+          gnext = a.g0;  // before the batch's first heartbeat + the smallest latency no IHAVE lands
+        } else if (alive && !(pending && t < lo) && a.gs_switch > 0) {
           const uint64_t imn = L.imin[sv], imx = L.imax[sv];
           const uint64_t kr = kl < a.gs_switch - 1 ? kl : a.gs_switch - 1;  // last receiver-centric heartbeat
           const uint64_t k0 = lo > r0 + imx ? udiv53(lo - r0 - imx + a.hb_ns - 1, a.hb_ns) : 0;
