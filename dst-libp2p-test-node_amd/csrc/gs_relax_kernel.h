@@ -829,7 +829,11 @@ __device__ __forceinline__ void gossip_receiver(const RelaxArgs& a, const Bucket
       if (ti < lo || ti >= hi || tw <= ti) return;  // another bucket, or w has seen it
       const uint64_t hi_ = ep_plus(hab, lvw, hb);
       if (hi_ > lim || ep_off(a, hi_, w)) return;  // IHAVE lost
-      const uint64_t kv = a.keys[(size_t)v * LL + slot];
+      // v's final bit clear: its key is >= hi > T (a tile the last scan skipped
+      // has no pending key below hi; pushes land >= hi), no key read
+      const size_t vi = (size_t)v * LL + slot;
+      if (a.tstamp && !((a.fbits[vi >> 6] >> (vi & 63)) & 1)) return;
+      const uint64_t kv = a.keys[vi];
       if (kv == INF64 || (kv >> a.tshift) > T) return;  // v does not hold it at T
       const uint64_t j0 = first_hb(kv >> a.tshift, r0, hb);
       if (k < j0 || k >= j0 + a.hist) return;  // T is not one of v's gossip heartbeats

@@ -12,7 +12,8 @@ import gossipsim  # noqa: E402
 
 N = int(os.environ.get("C3_PEERS", 100_000))
 M = int(os.environ.get("C3_MSGS", 1024))
-sim = gossipsim.Simulator(peers=N, batch=1024, fragments=1, seed=1, lazy_gossip=1, churn_ppm=10_000, churn_down=10,
+BATCH = int(os.environ.get("C3_BATCH", 1024))
+sim = gossipsim.Simulator(peers=N, batch=BATCH, fragments=1, seed=1, lazy_gossip=1, churn_ppm=10_000, churn_down=10,
                           churn_horizon=16, heartbeat_ns=1_000_000_000,
                           hb_phase_ns=gossipsim.T0_NS - 20 * 1_000_000_000 + 370_000_000)
 sim.set_topogen_links(5, 50, 150, 40, 130)
@@ -25,5 +26,5 @@ t0 = time.perf_counter()
 sim.run(gossipsim.shard_messages(1, 0, 1, M, N, 15000), collect=False)
 dt = time.perf_counter() - t0
 st = sim.stats()
-print("c3 probe: %.1f ms, %.3g deliveries/s" % (dt * 1e3, st["deliveries"] / dt))
+print("c3 probe: %.1f ms, %.3g deliveries/s, %d batches, run_ms %.1f relax_ms %.1f" % (dt * 1e3, st["deliveries"] / dt, st["batches"], st["run_ms"], st["relax_ms"]))
 print({k: v for k, v in st.items()})
