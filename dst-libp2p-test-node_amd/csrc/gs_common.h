@@ -21,6 +21,7 @@ constexpr uint32_t MAX_DIALS = 64;    // dials per peer held in registers/scratc
 constexpr uint32_t MAX_DEG = 256;     // per-row working sets of the mesh kernels
 constexpr uint32_t GT_W = 8;          // gossip target selection: pairs kept sorted in registers
 constexpr uint32_t GT_IN = 16;        // lazy gossip + churn: IHAVE senders kept per (peer, epoch)
+constexpr uint32_t GT_REDO = 0xFFFFFFFEu;  // entry 0 of such a list: more senders than it holds
 constexpr uint32_t MAX_FRAGS = 16;    // FRAGMENTS (topogen allows 1..9)
 constexpr uint32_t STAGE_SHIFT = 24;  // packed mesh entry: stage << 24 | peer
 // Subscription exchange: a connection completes HS_RTTS round

@@ -141,6 +141,7 @@ struct Ctx {
   DevBuf<uint32_t> d_hs_idx;  // per scan wave scratch of the holders found (copied to the list)
   DevBuf<uint64_t> d_hs_key;
   DevBuf<uint64_t> d_hl_min;
+  DevBuf<uint8_t> d_hwin;     // [N][L] first gossip heartbeat of each final lane (RelaxArgs::hwin)
   DevBuf<uint64_t> d_nonfinal;  // [3]
   DevBuf<uint64_t> d_rel0;   // [B] first heartbeat >= t_pub (relative ns)
   DevBuf<uint64_t> d_habs0;  // [B] its absolute heartbeat index

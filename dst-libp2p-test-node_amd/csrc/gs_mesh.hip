@@ -547,6 +547,7 @@ __global__ __launch_bounds__(TB) void k_gossip_out_range(const uint64_t* __restr
 // 16 lanes per (receiver, epoch): the group loads 16 neighbours' masks at
 // once (independent loads), ballots the hits and appends them in CSR order.
 constexpr uint32_t GIN_G = 16;
+static_assert(GIN_G == GT_IN, "k_gossip_in_gather: one lane per list entry");
 __global__ __launch_bounds__(TB) void k_gossip_in_gather(const uint64_t* __restrict__ row,
                                                          const uint32_t* __restrict__ col,
                                                          const uint8_t* __restrict__ csrpos,
@@ -586,6 +587,9 @@ __global__ __launch_bounds__(TB) void k_gossip_in_gather(const uint64_t* __restr
       cnt += (uint32_t)__popcll(hm);
     }
   }
+  // EMPTY after the senders; GT_REDO in entry 0 when k_gossip must select itself
+  if (lane >= cnt && lane < GT_IN) lst[lane] = EMPTY;
+  if (lane == 0 && (wide || cnt > GT_IN)) lst[0] = GT_REDO;
   if (lane == 0) ring_incnt[slot * N + w] = wide && cnt <= GT_IN ? GT_IN + 1 : cnt;
   }
 }

@@ -1238,6 +1238,9 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
             c.d_hl_key.alloc(total);
             c.d_hl_cnt.alloc(1);
             c.d_hl_mark.alloc(2 * (size_t)HL_LAUNCHES);
+            c.d_hwin.alloc(total);
+            GS_HIP(hipMemsetAsync(c.d_hwin.p, 0xFF, total, s));
+            ra.hwin = c.d_hwin.p;
             c.d_hs_idx.alloc(nwaves * ra.gl_cap);
             c.d_hs_key.alloc(nwaves * ra.gl_cap);
             c.d_hl_min.alloc(3);

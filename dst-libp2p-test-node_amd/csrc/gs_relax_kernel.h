@@ -83,6 +83,7 @@ struct RelaxArgs {
   uint64_t* hl_lo;             // per launch: the bucket's start
   uint64_t* hl_end;            // per launch: list length after its scan
   uint32_t gs_switch;
+  uint8_t* hwin;               // per lane: first gossip heartbeat index of its final key (255: none yet)
   const uint8_t* malive;       // churn + gossip, per message: its publisher was online at t_pub (else nobody holds it)
   uint64_t g0;                 //   and no IHAVE of the batch lands before g0 = min rel0 + the smallest latency
   const uint32_t* mesh;
@@ -593,6 +594,10 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
           if (k1 <= kr) gnext = r0 + k1 * a.hb_ns + imn > hi ? r0 + k1 * a.hb_ns + imn : hi;
         }
       }
+      if (a.hwin && pending && t >= lo && t < hi) {  // receiver-centric gossip reads it for senders
+        const uint64_t j = t <= r0 ? 0 : t <= r0 + a.hb_ns ? 1 : first_hb(t, r0, a.hb_ns);
+        a.hwin[gid] = (uint8_t)(j < 254 ? j : 254);
+      }
       if (a.ring_in) {
         // holders: a lane finalised in this bucket that gossips at a heartbeat
         // k >= gs_switch (its first gossip heartbeat j0 >= gs_switch - hist + 1,
@@ -635,11 +640,14 @@ __global__ __launch_bounds__(TB) void k_scan(RelaxArgs a) {
         const uint32_t pos = scnt + (uint32_t)__popcll(sm & ((1ull << lane) - 1));
         a.hs_idx[gseg + pos] = (uint32_t)gid;
         a.hs_key[gseg + pos] = key;
-        // its first IHAVE arrival is at or after max(t, T_gs_switch) + the
-        // smallest latency out of its stage (k_gossip's walk test)
-        const uint64_t tk = r0 + (uint64_t)a.gs_switch * a.hb_ns;
-        const uint64_t lb = (t > tk ? t : tk) + L.lmin[sv];
-        hmin = lb < hmin ? lb : hmin;
+        // its first IHAVE arrival: heartbeat max(j0, gs_switch) + the smallest
+        // latency out of its stage (k_gossip's walk test)
+        const uint64_t j0 = first_hb(t, r0, a.hb_ns);
+        const uint64_t k = j0 > a.gs_switch ? j0 : a.gs_switch;
+        if (k < j0 + a.hist && k <= kl) {
+          const uint64_t lb = r0 + k * a.hb_ns + L.lmin[sv];
+          hmin = lb < hmin ? lb : hmin;
+        }
       }
       scnt += (uint32_t)__popcll(sm);
       if constexpr (SKIP) {  // the tile's gossip state for later skips
@@ -832,32 +840,52 @@ __device__ __forceinline__ void gossip_receiver(const RelaxArgs& a, const Bucket
       // v's final bit clear: its key is >= hi > T (a tile the last scan skipped
       // has no pending key below hi; pushes land >= hi), no key read
       const size_t vi = (size_t)v * LL + slot;
-      if (a.tstamp && !((a.fbits[vi >> 6] >> (vi & 63)) & 1)) return;
-      const uint64_t kv = a.keys[vi];
-      if (kv == INF64 || (kv >> a.tshift) > T) return;  // v does not hold it at T
-      const uint64_t j0 = first_hb(kv >> a.tshift, r0, hb);
+      if (!a.hwin && a.tstamp && !((a.fbits[vi >> 6] >> (vi & 63)) & 1)) return;
+      // v holds (m, f) at T and T is one of its gossip heartbeats: j0 <= k <
+      // j0 + hist, j0 = the first heartbeat at or after its final key time
+      // (hwin, written when the scan finalised it; else from the key)
+      uint64_t kv = INF64, j0;
+      if (a.hwin) {
+        j0 = a.hwin[vi];
+        if (j0 == 255) return;  // not final: does not hold it
+      } else {
+        kv = a.keys[vi];
+        if (kv == INF64 || (kv >> a.tshift) > T) return;  // v does not hold it at T
+        j0 = first_hb(kv >> a.tshift, r0, hb);
+      }
       if (k < j0 || k >= j0 + a.hist) return;  // T is not one of v's gossip heartbeats
       const uint64_t ser = L.su[sv];
       const uint64_t A = ti + L.lat[sw * S + sv] + ser + lvw + (sdw > ser ? sdw - ser : 0);
       const uint64_t ha = ep_plus(hab, A - T, hb);
       if (ha > lim || ep_off(a, ha, w)) return;  // answer lost
-      const uint32_t hp = (uint32_t)((kv >> a.sb) & ((1u << HOP_BITS) - 1));
       iw++;
       if (A > a.tmax) err |= ERR_TIME;
+      // the answer's key needs v's hops only if its time can beat (or tie) the
+      // best answer so far and w's own key
+      const uint64_t cur = best < kw ? best : kw;
+      if (cur != INF64 && A > (cur >> a.tshift)) return;
+      if (kv == INF64) kv = a.keys[vi];
+      const uint32_t hp = (uint32_t)((kv >> a.sb) & ((1u << HOP_BITS) - 1));
       if (hp + 1 >= (1u << HOP_BITS)) err |= ERR_HOPS;
       const uint64_t nk = (A << a.tshift) | ((uint64_t)(hp + 1) << a.sb) | v;
       best = nk < best ? nk : best;
     };
     const size_t li = (size_t)((uint32_t)hab % a.ring_R) * a.N + w;
-    const uint32_t cnt = a.ring_incnt[li];
-    if (cnt <= GT_IN) {
-      const uint4* lp = reinterpret_cast<const uint4*>(a.ring_in + li * GT_IN);
-      for (uint32_t q0 = 0; q0 < cnt; q0 += 4) {
-        const uint4 x = lp[q0 / 4];
+    // the list: senders first, EMPTY after them; GT_REDO in entry 0: more
+    // senders than it holds (k_gossip_in_gather)
+    const uint4* lp = reinterpret_cast<const uint4*>(a.ring_in + li * GT_IN);
+    const uint4 x0 = lp[0];
+    if (x0.x != GT_REDO) {
+      for (uint32_t q0 = 0; q0 < GT_IN; q0 += 4) {
+        const uint4 x = q0 ? lp[q0 / 4] : x0;
+        if (x.x == EMPTY) break;
         ihave(x.x);
-        if (q0 + 1 < cnt) ihave(x.y);
-        if (q0 + 2 < cnt) ihave(x.z);
-        if (q0 + 3 < cnt) ihave(x.w);
+        if (x.y == EMPTY) break;
+        ihave(x.y);
+        if (x.z == EMPTY) break;
+        ihave(x.z);
+        if (x.w == EMPTY) break;
+        ihave(x.w);
       }
     } else {  // more senders than the list holds (rare): w's online non-mesh neighbours that pick w
       for (uint64_t e = a.row[w]; e < a.row[w + 1]; e++) {
