@@ -44,6 +44,7 @@ struct MeshArgs {
   uint8_t* pst;              // [PS_PLANES][N]
   const uint64_t* off_prev;  // offline bitsets of the previous and the next epoch
   const uint64_t* off_next;  // (nullptr: the last epoch of the run)
+  unsigned long long* dbg;   // GS_DEBUG_EV: [3][4] active rows per step (+ for HB: leaving, nbr-off, propd, hungry)
 };
 
 // Planes of MeshArgs::pst. A row runs the heavy per-row code of an epoch step
@@ -737,6 +738,23 @@ __global__ __launch_bounds__(TB) void k_ev_step(MeshArgs a, uint32_t* mesh, cons
     const uint64_t bm = __ballot(on);
     if (on) act[__popcll(bm & ((1ull << threadIdx.x) - 1))] = u;
     if (threadIdx.x == 0) nact = (uint32_t)__popcll(bm);
+    if (a.dbg) {  // diagnostic counts (GS_DEBUG_EV)
+      uint32_t c[4] = {(uint32_t)__popcll(bm), 0, 0, 0};
+      if (STEP == EV_HB && u < N) {
+        const bool off = is_off(a.off, u);
+        const uint32_t mc = P[(size_t)PS_MC * N + u], oc = P[(size_t)PS_OC * N + u];
+        c[1] = (uint32_t)__popcll(__ballot(off && !is_off(a.off_prev, u)));
+        c[2] = (uint32_t)__popcll(__ballot(P[(size_t)PS_NBROFF * N + u] != 0));
+        c[3] = (uint32_t)__popcll(__ballot(!off && (mc < a.d_lo || mc > a.d_hi || oc < a.d_out)));
+      } else if (STEP == EV_HB) {
+        c[1] = (uint32_t)__popcll(__ballot(false));
+        c[2] = (uint32_t)__popcll(__ballot(false));
+        c[3] = (uint32_t)__popcll(__ballot(false));
+      }
+      if (threadIdx.x == 0)
+        for (int q = 0; q < 4; q++)
+          if (c[q]) atomicAdd(&a.dbg[STEP * 4 + q], (unsigned long long)c[q]);
+    }
   }
   __syncthreads();  // also orders the ELL copy before the re-extracted rows
   const int lane = threadIdx.x & (G - 1);
@@ -907,6 +925,13 @@ void ev_epochs(Ctx& c, MeshArgs a, uint64_t h0, uint64_t h1, bool ring) {
   GS_HIP(hipMemsetAsync(c.d_prop.p, 0, c.nnz ? c.nnz : 1, s));
   const uint64_t* lin = c.d_offlin.p;  // lin[y] = epoch h0 - 1 + y
   a.pst = c.d_pst.p;
+  static const bool dbg_ev = getenv("GS_DEBUG_EV") != nullptr;
+  DevBuf<uint64_t> dbg;
+  if (dbg_ev) {
+    dbg.alloc(12);
+    GS_HIP(hipMemsetAsync(dbg.p, 0, 12 * 8, s));
+    a.dbg = (unsigned long long*)dbg.p;
+  }
   a.off = lin + w64;
   a.off_prev = lin;
   a.off_next = nullptr;
@@ -964,6 +989,14 @@ void ev_epochs(Ctx& c, MeshArgs a, uint64_t h0, uint64_t h1, bool ring) {
     const hipEvent_t e = side_event(c, nev++);
     GS_HIP(hipEventRecord(e, c.side));
     GS_HIP(hipStreamWaitEvent(s, e, 0));
+  }
+  if (dbg_ev) {
+    uint64_t h[12];
+    GS_HIP(hipMemcpyAsync(h, dbg.p, sizeof h, hipMemcpyDeviceToHost, s));
+    GS_HIP(hipStreamSynchronize(s));
+    fprintf(stderr, "[gs] epochs %llu: active rows hb %llu (leaving %llu nbr-off %llu hungry %llu) graft %llu apply %llu\n",
+            (unsigned long long)E, (unsigned long long)h[0], (unsigned long long)h[1], (unsigned long long)h[2],
+            (unsigned long long)h[3], (unsigned long long)h[4], (unsigned long long)h[8]);
   }
 }
 
