@@ -396,7 +396,9 @@ def main():
             def targs(k):  # "k_lpull<1, 16u, false, false>" -> ("k_lpull", ["1", "16"])
                 name, _, rest = k.partition("<")
                 return name, [x.strip().rstrip("u") for x in rest.rstrip(">").split(",")]
-            kn, ka = targs(kernel.split(" ")[0] if " + " not in kernel else "")
+            # the template id, without a descriptive suffix ("k_lpull<1> over each part's rows ...")
+            kid = kernel[:kernel.find(">") + 1] if "<" in kernel else kernel.split(" ")[0]
+            kn, ka = targs(kid if " + " not in kernel else "")
             same_kernel = bool(tj.get("kernels")) and " + " not in kernel and args.mode == tj.get("mode", "msg") \
                 and all(targs(k)[0] == kn and targs(k)[1][:len(ka)] == ka for k in tj["kernels"])
             if tj.get("peers") == args.peers and tj.get("batch") == args.batch and same_kernel:
