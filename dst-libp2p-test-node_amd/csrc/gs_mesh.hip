@@ -308,7 +308,7 @@ __device__ __forceinline__ bool row_handle_graft(const MeshArgs& a, uint32_t w) 
   const uint64_t b = a.row[w], en = a.row[w + 1];
   const uint32_t deg = (uint32_t)(en - b);
   const uint32_t sw = a.stage[w];
-  uint32_t f[HB_PER_LANE], p[HB_PER_LANE], r[HB_PER_LANE];
+  uint32_t f[HB_PER_LANE], p[HB_PER_LANE], r[HB_PER_LANE], un[HB_PER_LANE];
   uint64_t lvl[HB_PER_LANE];  // latency u->w of a proposing neighbour u, else INF64
   uint32_t c = 0;
 #pragma unroll
@@ -317,11 +317,13 @@ __device__ __forceinline__ bool row_handle_graft(const MeshArgs& a, uint32_t w) 
     f[k] = 0;
     p[k] = 0;
     r[k] = 0;
+    un[k] = 0;
     lvl[k] = INF64;
     if (i < deg) {
       f[k] = a.flags[b + i];
       p[k] = a.prop[b + i];
       r[k] = a.rev[b + i];
+      un[k] = a.until[b + i];  // loaded with the row: the GRAFT loop below is serial
       if (a.prop[r[k]] & PR_GRAFT) {  // arrival order: latency u->w (heartbeat), handshake (subscription)
         const uint32_t su = a.stage[a.col[b + i]];
         lvl[k] = a.sub ? (uint64_t)(a.sub + 1) * (a.lat[su * a.S + sw] + a.lat[sw * a.S + su])
@@ -343,7 +345,11 @@ __device__ __forceinline__ bool row_handle_graft(const MeshArgs& a, uint32_t w) 
     const uint32_t fs = ((uint32_t)__shfl(fpack, src) >> sh) & 0xFFu, ps = ((uint32_t)__shfl(ppack, src) >> sh) & 0xFFu;
     const bool in_mesh = ((fs & F_MESH) && !(ps & PR_PRUNE)) || (ps & PR_GRAFT);
     const uint64_t e = b + sel;
-    const uint32_t us = a.until[e];  // every lane, before the owner writes
+    uint32_t uo = 0;  // the owner lane's preloaded back-off of entry sel (written only below, once)
+#pragma unroll
+    for (int k = 0; k < HB_PER_LANE; k++)
+      if ((uint32_t)k == (sel / G)) uo = un[k];
+    const uint32_t us = (uint32_t)__shfl((int)uo, src);
     const bool rej = !in_mesh && (a.epoch < us || (c >= a.d_hi && !(fs & F_OUT)));
     if ((int)(threadIdx.x & 63) == src) {
       drop_key<G>(lvl, sel);
@@ -700,6 +706,88 @@ __global__ __launch_bounds__(TB) void k_ev_init(MeshArgs a) {
   }
 }
 
+// The apply step of an event-driven epoch for one row, in one pass over it:
+// row_apply (when the row proposed or was pruned), then, when its mesh may
+// have changed, the recount, the ELL re-extraction and (departing next epoch)
+// the neighbour flags — every load of the row issued together (flags, props,
+// reverse entries, ids, then the neighbours' props and stages), the new flags
+// kept in registers instead of re-read. Same results as row_apply +
+// row_counts + row_extract + mark_departure.
+template <int G>
+__device__ __forceinline__ void row_apply_ev(const MeshArgs& a, uint32_t u, bool need, bool dirty, bool depart,
+                                             uint32_t* mesh) {
+  const int lane = threadIdx.x & (G - 1);
+  uint8_t* P = a.pst;
+  const uint32_t N = a.N;
+  const uint64_t b = a.row[u];
+  const uint32_t deg = (uint32_t)(a.row[u + 1] - b);
+  uint32_t f[HB_PER_LANE], pp[HB_PER_LANE], rv[HB_PER_LANE], cw[HB_PER_LANE], pr[HB_PER_LANE], sg[HB_PER_LANE];
+#pragma unroll
+  for (int k = 0; k < HB_PER_LANE; k++) {
+    const uint32_t i = (uint32_t)(k * G + lane);
+    const bool v = i < deg;
+    f[k] = v ? a.flags[b + i] : 0u;
+    pp[k] = v && need ? a.prop[b + i] : 0u;
+    rv[k] = v && need ? a.rev[b + i] : 0u;
+    cw[k] = v && (dirty || depart) ? a.col[b + i] : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < HB_PER_LANE; k++) {
+    const uint32_t i = (uint32_t)(k * G + lane);
+    const bool v = i < deg;
+    pr[k] = v && need ? a.prop[rv[k]] : 0u;
+    sg[k] = v && dirty && mesh ? a.stage[cw[k]] : 0u;
+  }
+  if (need) {  // row_apply
+#pragma unroll
+    for (int k = 0; k < HB_PER_LANE; k++) {
+      const uint32_t i = (uint32_t)(k * G + lane);
+      if (i >= deg) continue;
+      const uint64_t e = b + i;
+      const uint32_t p = pp[k];
+      uint32_t fk = f[k];
+      bool bo = false;
+      if (p & PR_GRAFT) {
+        if (p & PR_ACCEPT) fk |= F_MESH;
+        else { fk &= ~(uint32_t)F_MESH; bo = true; }
+      }
+      if (p & PR_PRUNE) { fk &= ~(uint32_t)F_MESH; bo = true; }
+      if (pr[k] & PR_PRUNE) { fk &= ~(uint32_t)F_MESH; bo = true; }
+      if (bo) a.until[e] = a.epoch + a.bo;
+      a.flags[e] = (uint8_t)fk;
+      f[k] = fk;
+    }
+  }
+  if (dirty) {  // row_counts + row_extract on the new flags
+    uint32_t m = 0, o = 0;
+#pragma unroll
+    for (int k = 0; k < HB_PER_LANE; k++) {
+      const bool in = (f[k] & F_MESH) != 0;
+      const uint64_t bm = gballot<G>(in);
+      if (mesh && in) {
+        const uint32_t pos = m + (uint32_t)__popcll(bm & ((1ull << lane) - 1));
+        if (pos < MESH_W) mesh[(size_t)u * MESH_W + pos] = (sg[k] << STAGE_SHIFT) | cw[k];
+      }
+      m += (uint32_t)__popcll(bm);
+      o += (uint32_t)__popcll(gballot<G>(in && (f[k] & F_OUT)));
+    }
+    if (mesh) {
+      if (m > MESH_W && lane == 0) atomicOr((unsigned*)&a.counters[C_ERR], ERR_MESH);
+      if ((uint32_t)lane >= m && lane < (int)MESH_W) mesh[(size_t)u * MESH_W + lane] = EMPTY;
+    }
+    if (lane == 0) {
+      P[(size_t)PS_MC * N + u] = (uint8_t)(m < 255 ? m : 255);
+      P[(size_t)PS_OC * N + u] = (uint8_t)(o < 255 ? o : 255);
+      P[(size_t)PS_DIRTY * N + u] = 0;
+      P[(size_t)PS_PRUNED * N + u] = 0;
+    }
+  }
+  if (depart)  // u goes offline at the next epoch: flag its mesh neighbours
+#pragma unroll
+    for (int k = 0; k < HB_PER_LANE; k++)
+      if ((uint32_t)(k * G + lane) < deg && (f[k] & F_MESH)) P[(size_t)PS_NBROFF * N + cw[k]] = 1;
+}
+
 // One step of an event-driven epoch. A block owns EV_ROWS consecutive rows:
 // its first wave tests them one thread per row and compacts the rows the step
 // can change into LDS; then every group of G lanes takes active rows (most
@@ -779,20 +867,9 @@ __global__ __launch_bounds__(TB) void k_ev_step(MeshArgs a, uint32_t* mesh, cons
     } else {
       const bool need = P[(size_t)PS_PROPD * N + u] || P[(size_t)PS_PRUNED * N + u];
       const bool dirty = need || P[(size_t)PS_DIRTY * N + u] || (mesh && !mesh_prev);
-      if (need) row_apply<G>(a, u);
-      if (dirty) {
-        uint32_t m, o;
-        row_counts<G>(a, u, m, o);
-        if (lane == 0) {
-          P[(size_t)PS_MC * N + u] = (uint8_t)(m < 255 ? m : 255);
-          P[(size_t)PS_OC * N + u] = (uint8_t)(o < 255 ? o : 255);
-          P[(size_t)PS_DIRTY * N + u] = 0;
-          P[(size_t)PS_PRUNED * N + u] = 0;
-        }
-        if (mesh) row_extract<G>(a, u, mesh);
-      }
       // the departures of the next epoch flag their mesh neighbours
-      if (a.off_next && !is_off(a.off, u) && is_off(a.off_next, u)) mark_departure<G>(a, u);
+      const bool depart = a.off_next && !is_off(a.off, u) && is_off(a.off_next, u);
+      row_apply_ev<G>(a, u, need, dirty, depart, mesh);
     }
   }
 }
