@@ -108,7 +108,6 @@ struct Ctx {
   DevBuf<uint32_t> d_ring_mesh; // [R][N][MESH_W]
   DevBuf<uint64_t> d_ring_off;  // [R][(N+63)/64]
   DevBuf<uint32_t> d_ring_in;     // lazy gossip: [R][N][GT_IN] senders of the IHAVEs reaching a peer per epoch
-  DevBuf<uint32_t> d_ring_incnt;  // [R][N] their number (above GT_IN: k_gossip recomputes)
   DevBuf<uint64_t> d_gout;        // scratch of ring_in_lists: IHAVE target masks over CSR rows, per (epoch, sender)
   DevBuf<uint8_t> d_csrpos;       // [nnz] position of the row's peer in its neighbour's row (ring_in_lists)
   DevBuf<uint64_t> d_q0, d_r0;  // [B] epoch of t_pub, t_pub - start of that epoch

@@ -562,7 +562,7 @@ __global__ __launch_bounds__(TB) void k_gossip_in_gather(const uint64_t* __restr
                                                          const uint8_t* __restrict__ stage, uint32_t N, uint32_t w64,
                                                          uint32_t R, uint64_t h0, const uint64_t* __restrict__ outm,
                                                          uint32_t* __restrict__ ring_in,
-                                                         uint32_t* __restrict__ ring_incnt, uint32_t ny) {
+                                                         uint32_t ny) {
   const uint32_t lane = threadIdx.x & (GIN_G - 1);
   // grid-stride over (receiver, epoch) groups (group-uniform)
   for (uint64_t it = ((uint64_t)blockIdx.x * TB + threadIdx.x) / GIN_G; it < (uint64_t)N * ny;
@@ -597,7 +597,6 @@ __global__ __launch_bounds__(TB) void k_gossip_in_gather(const uint64_t* __restr
   // EMPTY after the senders; GT_REDO in entry 0 when k_gossip must select itself
   if (lane >= cnt && lane < GT_IN) lst[lane] = EMPTY;
   if (lane == 0 && (wide || cnt > GT_IN)) lst[0] = GT_REDO;
-  if (lane == 0) ring_incnt[slot * N + w] = wide && cnt <= GT_IN ? GT_IN + 1 : cnt;
   }
 }
 
@@ -912,9 +911,9 @@ static void ring_in_chunk(Ctx& c, uint64_t h0, uint32_t ny, hipStream_t s, uint3
   k_gossip_out_range<<<g1, TB, 0, s>>>(c.d_row.p, c.d_col.p, c.d_ring_mesh.p, c.d_ring_off.p, N, w64, R, c.cfg.seed,
                                        h0, c.cfg.d_lazy, c.cfg.gossip_factor_milli, c.d_gout.p, ny);
   k_gossip_in_gather<<<g2, TB, 0, s>>>(c.d_row.p, c.d_col.p, c.d_csrpos.p, c.d_ring_off.p, c.d_stage.p, N, w64, R, h0,
-                                       c.d_gout.p, c.d_ring_in.p, c.d_ring_incnt.p, ny);
+                                       c.d_gout.p, c.d_ring_in.p, ny);
 }
-static bool ring_in_wanted(const Ctx& c) { return c.cfg.lazy_gossip && c.d_ring_incnt.p; }
+static bool ring_in_wanted(const Ctx& c) { return c.cfg.lazy_gossip && c.d_ring_in.p; }
 
 // Epochs [h0, h1] (h1 - h0 < ring_R) on the context's stream: per chunk of
 // epochs, the senders' target masks, then every receiver's list

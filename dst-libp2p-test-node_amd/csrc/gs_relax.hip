@@ -685,7 +685,6 @@ static RelaxArgs relax_args(Ctx& c, const Batch& b, bool gossip) {
     ra.gossip = 1;
     if (c.cfg.churn_ppm) {
       ra.ring_in = c.d_ring_in.p;
-      ra.ring_incnt = c.d_ring_incnt.p;
       // heartbeats of a message from index gs_switch on are decided
       // sender-centric (exact for any value; GS_GOSSIP_SWITCH for tests / A/B)
       const char* gsw = getenv("GS_GOSSIP_SWITCH");
@@ -1070,7 +1069,6 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       c.d_ring_off.alloc((size_t)c.ring_R * w64);
       if (gossip) {  // inverse IHAVE lists per (peer, epoch) beside the snapshots (k_gossip_in_range)
         c.d_ring_in.alloc((size_t)c.ring_R * N * GT_IN);
-        c.d_ring_incnt.alloc((size_t)c.ring_R * N);
       }
     }
   }

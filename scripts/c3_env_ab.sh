@@ -6,7 +6,8 @@ OUT=${OUT:-gpurun_out/c3env}
 mkdir -p "$OUT"
 for r in 1 2; do
   for e in ${ENVS}; do
-    env $e timeout -k 10 300 python -u scripts/c3_probe.py > "$OUT/probe_${e}_$r.log" 2>&1 || exit $?
-    echo "$e (round $r): $(grep 'c3 probe' $OUT/probe_${e}_$r.log)"
+    f="$OUT/probe_$(echo "$e" | tr '/=' '__')_$r.log"
+    env $e timeout -k 10 300 python -u scripts/c3_probe.py > "$f" 2>&1 || exit $?
+    echo "$e (round $r): $(grep 'c3 probe' "$f")"
   done
 done
