@@ -265,7 +265,12 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
             NN[k] = __builtin_amdgcn_readlane(cj, j);
             const uint32_t su = e >> STAGE_SHIFT;
             SER[k] = sup[su];
-            BASE[k] = lo + lat[su * S + sw] + (sd > SER[k] ? sd - SER[k] : 0);
+            // the candidate key less its record-dependent parts: (arrival base
+            // << tshift) + (hops 1 | src); a record adds (start offset + FIFO
+            // position * ser) << tshift and its hops << sb (no carries: the low
+            // fields stay below 2^tshift, the sender checked the time field)
+            BASE[k] = ((lo + lat[su * S + sw] + (sd > SER[k] ? sd - SER[k] : 0)) << a.tshift) +
+                      ((1ull << a.sb) | U[k]);
             maxn = NN[k] > maxn ? NN[k] : maxn;
           }
         }
@@ -300,11 +305,10 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
                 ok = slot != 0xFFFFu && js != r && jp != r;  // w is the source or the publisher
                 pos = r + 1 - (js < r ? 1u : 0u) - ((jp < r && jp != js) ? 1u : 0u);
               }
-              const uint64_t arr = BASE[k] + (rc >> 32) + (uint64_t)(pos * SER[k]);
-              const uint32_t low = ((((lo32 >> 26) & hmask) + 1) << a.sb) | U[k];  // hops + 1 | src (< 2^tshift)
-              const uint64_t nk = (arr << a.tshift) | low;
+              const uint64_t off = (uint64_t)pos * SER[k] + (rc >> 32);
+              const uint64_t nk = BASE[k] + (off << a.tshift) + ((uint64_t)((lo32 >> 26) & hmask) << a.sb);
               if (ok) atomicMin((unsigned long long*)&CW[slot], (unsigned long long)nk);
-              cb |= ok ? 1u << (slot >> 6) : 0u;
+              cb |= 1u << ((slot >> 6) & 31u);  // an excluded record's chunk is classified for nothing
             }
         }
       }
