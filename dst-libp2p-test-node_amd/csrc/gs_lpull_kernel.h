@@ -365,17 +365,11 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     PP_ADD(3, tC - tR);
     // 3b. the pending minima -> the lists of their windows c + r (r = 1..K-1),
     //     appended after the entries already there
-    uint32_t ncnt[LP_KMAX], base[LP_KMAX];
-#pragma unroll
-    for (uint32_t k = 0; k < LP_KMAX; k++) {
-      ncnt[k] = 0;
-      base[k] = 0;
-    }
+    // lane j < K: entries appended to list slot j in this pass (lane-held, so
+    // each group of 64 visits only the destination windows present in it)
+    uint32_t addl = 0;
     if (!pull && npend) err |= ERR_RING;  // an EMIT pass's minima all lie in window c
     if (pull && npend) {
-#pragma unroll
-      for (uint32_t k = 1; k < LP_KMAX; k++)
-        if (k < K) base[k] = (uint32_t)__builtin_amdgcn_readlane(sv, (cslot + k) % K);
       const uint32_t lmax = a.lcap;
       for (uint32_t j0 = 0; j0 < npend; j0 += 64) {
         const bool jv = j0 + lane < npend;
@@ -383,18 +377,24 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
         const uint64_t x = jv ? CW[li] : INF64;
         const uint32_t r = jv ? lp_rof((uint32_t)(x >> 32), thr, K) : 0u;
         if (jv && r >= K) err |= ERR_RING;
+        const bool ap = jv && r > 0 && r < K;
+        uint32_t rm = ap ? 1u << r : 0u;  // the window offsets present
+        for (int off = 32; off > 0; off >>= 1) rm |= (uint32_t)__shfl_xor((int)rm, off);
+        rm = __builtin_amdgcn_readfirstlane(rm);
         uint32_t pos = 0, slot = 0;
-#pragma unroll
-        for (uint32_t k = 1; k < LP_KMAX; k++) {
-          if (k >= K) continue;
-          const uint64_t bm = __ballot(jv && r == k);
-          if (r == k) {
-            pos = base[k] + ncnt[k] + (uint32_t)__popcll(bm & lanelt);
-            slot = (cslot + k) % K;
+        while (rm) {  // wave-uniform
+          const uint32_t k = (uint32_t)__builtin_ctz(rm);
+          rm &= rm - 1;
+          const uint32_t sl = (cslot + k) % K;
+          const uint64_t bm = __ballot(ap && r == k);
+          const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane(sv + addl, sl);
+          if (ap && r == k) {
+            pos = b0 + (uint32_t)__popcll(bm & lanelt);
+            slot = sl;
           }
-          ncnt[k] += (uint32_t)__popcll(bm);
+          addl += lane == (int)sl ? (uint32_t)__popcll(bm) : 0u;
         }
-        if (jv && r > 0 && r < K) {
+        if (ap) {
           if (pos >= lmax) err |= ERR_LIST;
           else {
             const uint64_t toff = (x >> a.tshift) - (wlo + (uint64_t)r * a.delta);
@@ -477,11 +477,8 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     // 5. row state: final bits, pending list lengths, log length
     if (nfin) reinterpret_cast<uint16_t*>(a.fin + (size_t)w * LP_FW)[lane] = (uint16_t)finT;
     {
-      uint32_t add = 0;  // lane j < K: slot j stands for window c + lwin
-#pragma unroll
-      for (uint32_t k = 1; k < LP_KMAX; k++) add += (lwin == k) ? ncnt[k] : 0u;
-      uint32_t nv = sv;
-      if (lane < (int)K) nv = lane == (int)cslot ? 0u : sv + add;
+      uint32_t nv = sv;  // lane j < K: slot j (window c + lwin), emptied if it is window c's
+      if (lane < (int)K) nv = lane == (int)cslot ? 0u : sv + addl;
       if (lane == (int)LP_LOG) nv = logc;
       if (lane <= (int)LP_LOG) a.st[(size_t)w * LP_SW + lane] = nv;
       if (lane < (int)K && nv) nmh = umin32(nmh, lwhi);
