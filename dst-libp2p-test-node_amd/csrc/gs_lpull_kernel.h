@@ -143,6 +143,10 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
 #pragma unroll
   for (uint32_t k = 0; k <= LP_KMAX; k++) thr[k] = sat32(hlo64 + (uint64_t)k * a.dG);
   const uint32_t hlo = thr[0], hspan = a.dG;  // hi words of window c: [hlo, hlo + dG)
+  // window offsets of pending minima by division when no threshold of the
+  // ring saturates (lp_rof's count of thr[k] <= hx is then floor((hx - hlo) / dG))
+  const bool rdiv = hlo64 + (uint64_t)(K + 1) * a.dG < 0xFFFFFFFFull;
+  const float rinv = 1.0f / (float)a.dG;
   const size_t NL = (size_t)a.N * LL;
   const uint32_t pb = (a.pass + 1) & 1, nb = a.pass & 1;  // records read / written
   const uint64_t* rrec = PART ? a.rpk : a.lrec + pb * NL;
@@ -220,7 +224,10 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     uint32_t cb = 0;
     if (due) {
       const uint64_t* lst = a.blk + ((size_t)cslot * a.N + w) * a.ls;
-      const uint32_t lmask = (1u << a.lb) - 1, tsh = a.tshift + a.lb;
+      // entry = toff << (tshift + lb) | low << lb | lane, so key = (wlo +
+      // toff) << tshift | low = (wlo << tshift) + (entry >> lb)
+      const uint32_t lmask = (1u << a.lb) - 1;
+      const uint64_t wlok = wlo << a.tshift;
       for (uint32_t f0 = 0; f0 < due; f0 += 256) {
         uint64_t e[4];
 #pragma unroll
@@ -232,7 +239,7 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
         for (int u = 0; u < 4; u++) {
           if (e[u] == ~0ull) continue;
           const uint32_t li = (uint32_t)e[u] & lmask;
-          const uint64_t key = ((wlo + (e[u] >> tsh)) << a.tshift) | ((e[u] >> a.lb) & lowmask);
+          const uint64_t key = wlok + (e[u] >> a.lb);
           atomicMin((unsigned long long*)&CW[li], (unsigned long long)key);
           cb |= 1u << (li >> 6);
         }
@@ -375,7 +382,18 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
         const bool jv = j0 + lane < npend;
         const uint32_t li = jv ? LST[LMAX - 1 - (j0 + lane)] : 0u;
         const uint64_t x = jv ? CW[li] : INF64;
-        const uint32_t r = jv ? lp_rof((uint32_t)(x >> 32), thr, K) : 0u;
+        uint32_t r = 0;
+        if (jv) {
+          if (rdiv) {  // floor((hx - hlo) / dG) capped at K: the float quotient is within 1
+            const uint32_t d = (uint32_t)(x >> 32) - hlo;
+            uint32_t q = (uint32_t)((float)d * rinv);
+            if ((uint64_t)q * hspan > d) q--;
+            else if ((uint64_t)(q + 1) * hspan <= d) q++;
+            r = q < K ? q : K;
+          } else {
+            r = lp_rof((uint32_t)(x >> 32), thr, K);
+          }
+        }
         if (jv && r >= K) err |= ERR_RING;
         const bool ap = jv && r > 0 && r < K;
         uint32_t rm = ap ? 1u << r : 0u;  // the window offsets present
