@@ -252,12 +252,12 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
       const uint32_t sd = sdn[sw];
       uint64_t cmk = cand;
       while (cmk) {
-        uint32_t U[NG], R4[NG], NN[NG], SER[NG];
+        uint32_t U[NG], R4[NG], NN[NG], SER[NG], ltm[NG];
         uint64_t BASE[NG], RO[NG];
         uint32_t maxn = 0;
 #pragma unroll
         for (int k = 0; k < (int)NG; k++) {
-          U[k] = 0; R4[k] = 0; NN[k] = 0; SER[k] = 0; BASE[k] = 0; RO[k] = 0;
+          U[k] = 0; R4[k] = 0; NN[k] = 0; SER[k] = 0; BASE[k] = 0; RO[k] = 0; ltm[k] = 0;
           if (cmk) {  // wave-uniform
             const int j = __builtin_ctzll(cmk);
             cmk &= cmk - 1;
@@ -269,6 +269,7 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
             else
               RO[k] = (uint64_t)U[k] * LL;
             R4[k] = __builtin_amdgcn_readlane(rj, j);
+            ltm[k] = (1u << R4[k]) - 1u;
             NN[k] = __builtin_amdgcn_readlane(cj, j);
             const uint32_t su = e >> STAGE_SHIFT;
             SER[k] = sup[su];
@@ -310,7 +311,8 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
                 const uint32_t js = (lo32 >> 21) & 31u, jp = (lo32 >> 16) & 31u;
                 slot = lo32 & 0xFFFFu;
                 ok = slot != 0xFFFFu && js != r && jp != r;  // w is the source or the publisher
-                pos = r + 1 - (js < r ? 1u : 0u) - ((jp < r && jp != js) ? 1u : 0u);
+                // ltm = (1 << r) - 1: bit j set iff j < r (J_NONE = 31 > r)
+                pos = r + 1 - ((ltm[k] >> js) & 1u) - (((ltm[k] >> jp) & 1u) & (jp != js ? 1u : 0u));
               }
               const uint64_t off = (uint64_t)pos * SER[k] + (rc >> 32);
               const uint64_t nk = BASE[k] + (off << a.tshift) + ((uint64_t)((lo32 >> 26) & hmask) << a.sb);
@@ -340,13 +342,13 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     for (int q = 0; q < (int)CH; q++) {
       if (!((cb >> q) & 1u)) continue;  // wave-uniform
       const uint32_t i = q * 64 + lane;
-      uint64_t x = CW[i];
-      if (x != INF64 && ((finT >> q) & 1u)) {  // final in an earlier window
-        x = INF64;
-        CW[i] = INF64;
-      }
-      const bool act = x != INF64 && ((uint32_t)(x >> 32) - hlo) < hspan;
-      const bool pend = x != INF64 && !act;
+      const uint64_t x = CW[i];
+      const bool fe = (finT >> q) & 1u;  // final in an earlier window: dropped
+      // (a fragment group's step 4 re-reads every lane of a final group)
+      if (FP > 1 && fe && x != INF64) CW[i] = INF64;
+      const bool live = !fe && x != INF64;
+      const bool act = live && ((uint32_t)(x >> 32) - hlo) < hspan;
+      const bool pend = live && !act;
       const uint64_t pm = __ballot(pend);
       if (pend) LST[LMAX - 1 - (npend + (uint32_t)__popcll(pm & lanelt))] = (uint16_t)i;
       npend += (uint32_t)__popcll(pm);
