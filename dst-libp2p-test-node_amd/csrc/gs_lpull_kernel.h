@@ -398,15 +398,13 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
         }
         if (jv && r >= K) err |= ERR_RING;
         const bool ap = jv && r > 0 && r < K;
-        uint32_t rm = ap ? 1u << r : 0u;  // the window offsets present
-        for (int off = 32; off > 0; off >>= 1) rm |= (uint32_t)__shfl_xor((int)rm, off);
-        rm = __builtin_amdgcn_readfirstlane(rm);
         uint32_t pos = 0, slot = 0;
-        while (rm) {  // wave-uniform
-          const uint32_t k = (uint32_t)__builtin_ctz(rm);
-          rm &= rm - 1;
+        uint64_t rem = __ballot(ap);  // the window offsets present: one pass each,
+        while (rem) {                 // read from the lowest lane still waiting (wave-uniform)
+          const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)r, (int)__builtin_ctzll(rem));
           const uint32_t sl = (cslot + k) % K;
           const uint64_t bm = __ballot(ap && r == k);
+          rem &= ~bm;
           const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane(sv + addl, sl);
           if (ap && r == k) {
             pos = b0 + (uint32_t)__popcll(bm & lanelt);
@@ -439,7 +437,9 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
         const uint32_t i = grp * FP + (lane & (FP - 1));
         const uint64_t x = gv ? CW[i] : INF64;  // final lanes were set to INF in step 3
         const uint32_t pm = gv ? a.pub[grp] : EMPTY;
-        const bool act = gv && x != INF64 && ((uint32_t)(x >> 32) - hlo) < hspan && a.u0 + w != pm;
+        // FP == 1: LST holds only lanes final in window c; a fragment group's
+        // other lanes are re-checked
+        const bool act = gv && (FP == 1 || (x != INF64 && ((uint32_t)(x >> 32) - hlo) < hspan)) && a.u0 + w != pm;
         const uint32_t src = (uint32_t)(x & smask);
         uint32_t js = J_NONE, jp = J_NONE;  // indices of src / publisher in mesh(w)
         uint32_t xm = 0;                    // IDW: every excluded mesh index
