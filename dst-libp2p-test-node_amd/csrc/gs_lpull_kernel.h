@@ -282,14 +282,22 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
             maxn = NN[k] > maxn ? NN[k] : maxn;
           }
         }
+        __amdgpu_buffer_rsrc_t RS[NG];  // wave-uniform: base = the neighbour's records, NN[k] of them
+#pragma unroll
+        for (int k = 0; k < (int)NG; k++)
+          RS[k] = __builtin_amdgcn_make_buffer_rsrc((void*)(rrec + RO[k]), (short)0, (int)(NN[k] * 8u), 0x00020000);
         for (uint32_t i0 = 0; i0 < maxn; i0 += 64 * RCH) {
           uint64_t rec[NG][RCH];
 #pragma unroll
           for (int k = 0; k < (int)NG; k++)
 #pragma unroll
             for (int cc = 0; cc < (int)RCH; cc++) {
+              // bounds-checked buffer load, 32-bit offset: past the
+              // neighbour's NN records it reads 0, which no record is (a
+              // forwarding sender has hops >= 1)
               const uint32_t i = i0 + cc * 64 + lane;
-              rec[k][cc] = i < NN[k] ? rrec[RO[k] + i] : ~0ull;
+              const auto v = __builtin_amdgcn_raw_buffer_load_b64(RS[k], i * 8u, 0, 0);
+              rec[k][cc] = ((uint64_t)v[1] << 32) | v[0];
             }
 #pragma unroll
           for (int k = 0; k < (int)NG; k++)
@@ -305,12 +313,12 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
               if constexpr (IDW) {  // exclusion mask of the sender's row
                 const uint32_t xm = (lo32 >> 10) & 0xFFFFu;
                 slot = lo32 & 0x3FFu;
-                ok = rc != ~0ull && !((xm >> r) & 1u);
+                ok = rc != 0 && !((xm >> r) & 1u);
                 pos = r + 1 - (uint32_t)__popc(xm & ((1u << r) - 1u));
               } else {
                 const uint32_t js = (lo32 >> 21) & 31u, jp = (lo32 >> 16) & 31u;
                 slot = lo32 & 0xFFFFu;
-                ok = slot != 0xFFFFu && js != r && jp != r;  // w is the source or the publisher
+                ok = rc != 0 && js != r && jp != r;  // no record, or w is the source or the publisher
                 // ltm = (1 << r) - 1: bit j set iff j < r (J_NONE = 31 > r)
                 pos = r + 1 - ((ltm[k] >> js) & 1u) - (((ltm[k] >> jp) & 1u) & (jp != js ? 1u : 0u));
               }
