@@ -461,7 +461,7 @@ __global__ __launch_bounds__(TB) void k_extract(MeshArgs a, uint32_t* mesh, uint
 // capped at |non-mesh|. The receiver side of lazy gossip
 // (k_gossip, receiver-centric under churn) reads them inverted, per target:
 // in[w] lists the senders v whose epoch-h IHAVEs reach w (packed stage << 24
-// | v, at most GT_IN; incnt[w] counts them, a count above GT_IN tells k_gossip
+// | v, at most GT_IN, EMPTY after the last; GT_REDO in entry 0 tells k_gossip
 // to recompute). Built in two passes per chunk of epochs, without atomics:
 //  1. k_gossip_out_range: one thread per (sender, epoch) makes the selection
 //     (one rng per connection, an 8-deep sorted insert in registers with
@@ -626,7 +626,8 @@ __global__ __launch_bounds__(TB) void k_csrpos(uint32_t N, const uint64_t* __res
 //  apply: proposers and PRUNEd rows; rows whose mesh changed are recounted
 //    and re-extracted into the ring slot, the others copy their previous row.
 // Offline bitsets and IHAVE targets do not depend on the epoch sequence and
-// run batched over the whole range (k_offline_range, k_gossip_in_range).
+// run batched over the whole range (k_offline_range; the IHAVE lists per
+// chunk of epochs on the side stream, ring_in_lists).
 
 // ELL row of u from its CSR flags (packed stage<<24 | peer, ascending ids).
 template <int G>

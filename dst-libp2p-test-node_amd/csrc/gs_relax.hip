@@ -1067,7 +1067,7 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       c.ring_R = (uint32_t)std::min<uint64_t>(want, std::max<uint64_t>(c.cfg.churn_horizon + 2, budget / per_slot));
       c.d_ring_mesh.alloc((size_t)c.ring_R * N * MESH_W);
       c.d_ring_off.alloc((size_t)c.ring_R * w64);
-      if (gossip) {  // inverse IHAVE lists per (peer, epoch) beside the snapshots (k_gossip_in_range)
+      if (gossip) {  // inverse IHAVE lists per (peer, epoch) beside the snapshots (ring_in_lists)
         c.d_ring_in.alloc((size_t)c.ring_R * N * GT_IN);
       }
     }

@@ -63,7 +63,8 @@ struct RelaxArgs {
   const uint64_t* r0;         // [B] t_pub - start of that epoch
   uint32_t churn, ring_R, w64, horizon;
   // churn + gossip: receiver-centric lazy gossip over the inverse IHAVE lists
-  // of each epoch (k_gossip_in_range): [R][N][GT_IN] senders (stage<<24 | id)
+  // of each epoch (k_gossip_out_range + k_gossip_in_gather): [R][N][GT_IN]
+  // senders (stage<<24 | id), EMPTY after the last, GT_REDO: recompute
   const uint32_t* ring_in;
   uint64_t* gl_key;            // receiver-centric: the listed lane's key
   // churn + gossip: heartbeats k >= gs_switch of a message (k counted from its
