@@ -5,17 +5,23 @@ roofline fraction and the CPU oracle's rate on a bounded sample.
 
 One step = one batch of B messages disseminated over a frozen 1M-peer mesh
 (publish -> flood -> mesh forwarding -> reassembly), inputs resident in HBM.
-Multi-GPU: one process per GPU (torchrun), each simulating its own message
-shard (weak scaling; no data-path collective). `--mode peer`
-instead partitions the peers across ranks and exchanges each bucket's records
-over RCCL (strong scaling of one batch, config #4).
+Multi-GPU: one process per GPU, each simulating its own message shard (weak
+scaling; no data-path collective). Under torchrun the ranks come
+from the environment; `python bench.py --gpus N` without it starts the N rank
+processes itself (launch_ranks) before anything touches a GPU and relays rank
+0's line. `--mode peer` instead partitions the peers across ranks and
+exchanges each pass's records over RCCL (strong scaling of one batch, config
+#4).
 
     python bench.py --gpus 1 --steps 20 --warmup 3
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -64,6 +70,66 @@ def parse():
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="per-launch HBM bytes of the relax kernel from a rocprofv3 --pmc pass")
     return ap.parse_args()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv, cmd=None, env=None, out=None):
+    """`bench.py --gpus N` started without torchrun (no WORLD_SIZE): start N
+    rank processes of this script with RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_ADDR / MASTER_PORT set (rendezvous on 127.0.0.1), one per GPU. This
+    process makes no GPU call (gossipsim is loaded lazily; nothing here touches
+    HIP), so the ranks own their devices. Rank 0's stdout is collected and its
+    JSON line relayed to `out`; the other ranks' stdout goes to stderr. If a
+    rank fails, the others are terminated and its exit code is returned (a CPU
+    box fails here, for want of a device, instead of timing one rank).
+    `cmd` replaces the worker command (tests use a stub)."""
+    out = out or sys.stdout
+    cmd = cmd or [sys.executable, "-u", os.path.abspath(__file__)] + list(argv)
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        e = dict(os.environ if env is None else env)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(cmd, env=e, stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno(),
+                                      text=True))
+    lines = []
+    drain = threading.Thread(target=lambda: lines.extend(procs[0].stdout), daemon=True)
+    drain.start()
+    rc = 0
+    live = list(range(n))
+    while live:
+        for r in list(live):
+            code = procs[r].poll()
+            if code is None:
+                continue
+            live.remove(r)
+            if code != 0 and rc == 0:
+                rc = code
+                print("bench.py: rank %d of %d exited with status %d; stopping the others" % (r, n, code),
+                      file=sys.stderr, flush=True)
+                for q in live:
+                    procs[q].terminate()
+        time.sleep(0.05)
+    drain.join(timeout=10)
+    js = [ln for ln in lines if ln.lstrip().startswith("{")]
+    for ln in lines:
+        if ln not in js:
+            sys.stderr.write(ln)
+    if rc == 0 and not js:
+        print("bench.py: rank 0 printed no result line", file=sys.stderr, flush=True)
+        rc = 1
+    if rc == 0:
+        out.write(js[-1] if js[-1].endswith("\n") else js[-1] + "\n")
+        out.flush()
+    return rc
 
 
 def dist_setup():
@@ -355,7 +421,11 @@ def config_rates(args, local):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:  # no torchrun: be the launcher
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world, rank, local, torch, dist = dist_setup()
+    if args.gpus != world:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE is %d" % (args.gpus, world))
     S, bl, bh, ll, lh = [int(x) for x in args.links.split(",")]
     links = (bl, bh, ll, lh)
     sim, epochs, t_setup = make_sim(args, args.peers, S, links, local)

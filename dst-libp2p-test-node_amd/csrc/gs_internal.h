@@ -64,6 +64,8 @@ enum : uint32_t {
 struct Batch {
   uint32_t B = 0, L = 0, F = 0, FP = 1, sb = 0, tshift = 0, Fe = 1;
   uint64_t lat_min = 0;  // smallest latency between used link classes (lazy-gossip no-op proof)
+  uint64_t lat_max = 0;  // largest latency between used link classes (IHAVE travel bound)
+  uint64_t ans_max = 0;  // largest IHAVE-arrival -> IWANT-answer-arrival time (lat + ser + lat + dn)
   uint64_t ser_max = 0;      // largest uplink serialisation of a used link class
   uint64_t lat_adj_max = 0;  // largest lat(x->y) + max(0, ser_dn(y) - ser_up(x)) over used classes
   bool collide = false;
@@ -109,7 +111,8 @@ struct Ctx {
   DevBuf<uint64_t> d_ring_off;  // [R][(N+63)/64]
   DevBuf<uint32_t> d_ring_in;     // lazy gossip: [R][N][GT_IN] senders of the IHAVEs reaching a peer per epoch
   DevBuf<uint64_t> d_gout;        // scratch of ring_in_lists: IHAVE target masks over CSR rows, per (epoch, sender)
-  DevBuf<uint8_t> d_csrpos;       // [nnz] position of the row's peer in its neighbour's row (ring_in_lists)
+  DevBuf<uint8_t> d_csrpos;       // [nnz] position of the row's peer in its neighbour's row (ring_in_lists, GOS)
+  bool csrpos_valid = false;      // d_csrpos is of the current CSR
   DevBuf<uint64_t> d_q0, d_r0;  // [B] epoch of t_pub, t_pub - start of that epoch
   uint32_t ring_R = 0;
   uint64_t churn_state = 0, ring_lo = 1, ring_hi = 0;  // mesh state epoch; valid ring epochs
@@ -207,6 +210,12 @@ struct Ctx {
   DevBuf<uint64_t> d_pkout;  // this part's records, packed for the exchange
   DevBuf<uint64_t> d_pkroff; // [own rows] their offsets in d_rpk
   DevBuf<uint64_t> d_pkcur;  // pack cursor
+  // lazy gossip inside the list pass (gs_lpull_kernel.h, GOS batches)
+  DevBuf<uint32_t> d_gpl;      // [N][32] sender planes of the built heartbeat
+  DevBuf<uint64_t> d_gse;      // [N][L] their entries
+  DevBuf<uint32_t> d_rowdone;  // [(N + 31) / 32]
+  DevBuf<uint64_t> d_gctl;     // [GC_WORDS]
+  bool glp_prefer = false;     // the last eager no-op proof failed: run gossip batches on the list pass first
 
   // stats
   gs_stats stats{};
@@ -223,6 +232,7 @@ struct Ctx {
 void launch_topology(Ctx& c);
 uint32_t run_mesh(Ctx& c, uint32_t max_heartbeats);
 void churn_ring(Ctx& c, uint64_t h_lo, uint64_t h_hi);
+void ensure_csrpos(Ctx& c);
 void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_result_sink* sink);
 void deliver_rows(Ctx& c, uint32_t B, uint32_t un, const gs_result_sink* sink, uint64_t sink_row0);
 void part_set(Ctx& c, uint32_t parts, uint32_t part);

@@ -49,6 +49,13 @@
 // the receiver at index r of the sender's row is skipped if bit r is set,
 // else its position is r + 1 - popcount(mask below r).
 
+// The record step reads through raw buffer resources whose word 3 (0x00020000:
+// DATA_FORMAT 32, no swizzle, bounds check on) is the gfx9 / CDNA layout; its
+// out-of-range reads return 0, which the step relies on.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "k_lpull's buffer resource layout is gfx950's (CDNA4); build with --offload-arch=gfx950"
+#endif
+
 constexpr uint32_t LP_KMAX = 12;  // ring of destination-window lists
 constexpr uint32_t LP_SW = 16;    // u32 words of per-row state: list lengths [0..11] (slot = window % K), log length
 constexpr uint32_t LP_LOG = 15;   // state word holding the final-log length
@@ -83,7 +90,39 @@ struct LPullArgs {
   const uint64_t* rpk;
   const uint64_t* roff;
   const uint32_t* rcg;
+  // lazy gossip inside the passes (k_lpull<.., GOS>, k_lctl, k_gsend):
+  // a lockstep batch (every message's heartbeat k at the same relative time
+  // grel0 + k * ghb) on the frozen mesh, rows of single-fragment lanes
+  uint64_t grel0, ghb;        // heartbeats, relative to every t_pub
+  uint64_t glat_min, glat_max;  // IHAVE travel time bounds over the used link classes
+  uint64_t gnf;               // non-publisher lanes of the batch, B * (N - 1)
+  uint64_t gseed;
+  uint32_t ghist, gd_lazy, ggf;  // history_gossip, D_lazy, gossip factor x 1000
+  uint64_t* gctl;             // [GC_WORDS] pass and heartbeat control (k_lctl)
+  uint32_t* gpl;              // [N][LP_FW] sender planes of the built heartbeat (fin's transposed layout)
+  uint64_t* gse;              // [N][L] their entries in rank order: target mask | sender hops << 58
+  uint32_t* rowdone;          // [(N + 31) / 32] rows whose every lane is final
+  const uint64_t* row;        // CSR (non-mesh connections are the IHAVE peers)
+  const uint32_t* col;
+  const uint8_t* flags;
+  const uint8_t* csrpos;      // position of the row's peer in its neighbour's row
+  const uint64_t* habs0;      // [B] absolute index of each message's heartbeat 0
 };
+
+// gctl words (k_lctl writes them between passes; k_gsend / k_lpull only read,
+// except GC_TLAST, which the passes raise with atomicMax)
+enum : uint32_t {
+  GC_FD0 = 0,    // counters[C_FD] at the start of the batch
+  GC_TLAST = 1,  // largest final key time so far (relative ns)
+  GC_E = 2,      // end of the last emitted window
+  GC_DONE = 3,   // the batch's passes are over
+  GC_GB = 4,     // next heartbeat whose senders are not yet known final
+  GC_BK = 5,     // heartbeat + 1 whose sender planes are built (0: none)
+  GC_BUILD = 6,  // heartbeat + 1 to build before this pass (0: none)
+  GC_GW = 7,     // this pass's window holds IHAVE arrivals of heartbeat GC_BK - 1
+  GC_WORDS = 8
+};
+constexpr uint32_t GSE_HOPS = 58;  // entry bits [0, 58): target mask over the sender's CSR row
 
 constexpr uint32_t LP_FW = PULL_LMAX / 32;  // u32 final-bit words per row
 
@@ -106,30 +145,162 @@ struct LPullLds {
   uint16_t lst[PULL_WAVES][CH * 64];
 };
 
+// ---- lazy gossip inside the passes (GOS batches) ----
+//
+// IHAVE rules (libp2p-gossipsub emit_gossip / handle_ihave / handle_iwant,
+// upstream; gossip_lazy / gossip_factor at rust-test-node/src/main.rs:230,235;
+// the oracle's sched_gossip): a peer v that first received m at t_v gossips
+// it at the history_gossip heartbeats R_k >= t_v to the r smallest
+// rng(GOSSIP, v, h, x) of its non-mesh connections x; the IHAVE reaches w at
+// t_i = R_k + lat(v -> w); unless w holds m by t_i, w sends IWANT and v's
+// answer arrives lat(w -> v) + ser_up(v) + lat(v -> w) + dn later with v's
+// hops + 1 and src v. In a lockstep batch R_k is one relative time for every
+// message, windows are no wider than the smallest latency (t_i never shares a
+// window with R_k), so before the first pass that can see heartbeat k's IHAVEs
+// every sender of k is final: k_gsend writes each row's sender plane (which
+// lanes v gossips at k) and its entries (the lane's target mask over v's CSR
+// row, v's hops), and the passes decide the IHAVEs receiver-side (glp_ihave).
+
+// IHAVE targets of v at heartbeat h among its non-mesh connections (bit e of
+// nmm: CSR entry e, held by lane e in x): the r smallest (rng, id) pairs, as a
+// mask over v's CSR row. The CSR walk is wave-uniform, h is the lane's own.
+__device__ __forceinline__ uint64_t glp_targets(uint64_t seed, uint32_t v, uint32_t h, uint32_t x, uint64_t nmm,
+                                                uint32_t deg, uint32_t r) {
+  auto lt = [](uint64_t k1, uint32_t w1, uint64_t k2, uint32_t w2) { return k1 < k2 || (k1 == k2 && w1 < w2); };
+  uint64_t kk[GT_W];
+  uint32_t ww[GT_W], pp[GT_W];
+#pragma unroll
+  for (int q = 0; q < (int)GT_W; q++) { kk[q] = INF64; ww[q] = ~0u; pp[q] = 0; }
+  for (uint32_t e = 0; e < deg; e++) {
+    if (!((nmm >> e) & 1)) continue;  // wave-uniform
+    const uint32_t w = __builtin_amdgcn_readlane(x, e);
+    const uint64_t rk = rng(seed, P_GOSSIP, v, h, w);
+    if (!lt(rk, w, kk[GT_W - 1], ww[GT_W - 1])) continue;
+#pragma unroll
+    for (int q = (int)GT_W - 1; q > 0; q--) {  // insert, shifting the larger pairs up
+      if (lt(rk, w, kk[q - 1], ww[q - 1])) { kk[q] = kk[q - 1]; ww[q] = ww[q - 1]; pp[q] = pp[q - 1]; }
+      else if (lt(rk, w, kk[q], ww[q])) { kk[q] = rk; ww[q] = w; pp[q] = e; }
+    }
+    if (lt(rk, w, kk[0], ww[0])) { kk[0] = rk; ww[0] = w; pp[0] = e; }
+  }
+  uint64_t mask = 0;
+#pragma unroll
+  for (int q = 0; q < (int)GT_W; q++)
+    if ((uint32_t)q < r) mask |= 1ull << pp[q];
+  uint64_t pk = kk[GT_W - 1];
+  uint32_t pw = ww[GT_W - 1];
+  for (uint32_t q = GT_W; q < r; q++) {  // rare: more than GT_W targets, the next pair by a rescan
+    uint64_t bk = INF64;
+    uint32_t bw = ~0u, bp = 0;
+    for (uint32_t e = 0; e < deg; e++) {
+      if (!((nmm >> e) & 1)) continue;
+      const uint32_t w = __builtin_amdgcn_readlane(x, e);
+      const uint64_t rk = rng(seed, P_GOSSIP, v, h, w);
+      if (lt(pk, pw, rk, w) && lt(rk, w, bk, bw)) { bk = rk; bw = w; bp = e; }
+    }
+    mask |= 1ull << bp;
+    pk = bk;
+    pw = bw;
+  }
+  return mask;
+}
+
+// Receiver side, row w in a window c = [wlo, wlo + Delta) holding IHAVE
+// arrivals of heartbeat k (at gR): every non-mesh connection v whose t_i =
+// gR + lat(v -> w) lies in c offers the lanes of its plane; for a lane of w
+// not final before c that v targets, CW (the window's entries and records)
+// says whether w has the message by t_i — if not, IWANT, and v's answer goes
+// into CW as a candidate (it lands after window c).
+__device__ __forceinline__ void glp_ihave(const LPullArgs& a, uint64_t* CW, uint32_t w, uint32_t sw, uint32_t finT,
+                                          uint64_t wlo, uint64_t gR, const uint32_t* lat, const uint32_t* sup,
+                                          const uint32_t* sdn, uint32_t& cb, uint64_t& niw, uint32_t& err) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t S = a.S;
+  wave_lds_sync();  // the window's entries and records are in CW
+  const uint64_t rb = a.row[w], deg = a.row[w + 1] - rb;  // the host checked deg <= GSE_HOPS
+  uint32_t vx = 0, cp = 0, tio = 0, aoff = 0;
+  bool ok = false;
+  if ((uint64_t)lane < deg) {
+    vx = a.col[rb + lane];
+    const uint8_t fl = a.flags[rb + lane];
+    cp = a.csrpos[rb + lane];
+    const uint32_t sv = a.stage[vx];
+    tio = lat[sv * S + sw];  // t_i - R_k
+    const uint64_t ti = gR + tio;
+    ok = !(fl & F_MESH) && ti >= wlo && ti < wlo + a.delta;
+    const uint32_t su = sup[sv], sd = sdn[sw];
+    aoff = lat[sw * S + sv] + su + tio + (sd > su ? sd - su : 0u);  // IWANT + answer: t_i -> arrival
+  }
+  uint64_t gm = __ballot(ok);
+  const uint32_t nfl = ~finT & 0xFFFFu;  // lanes not final before window c
+  while (gm) {  // wave-uniform: one IHAVE sender at a time
+    const int e = __builtin_ctzll(gm);
+    gm &= gm - 1;
+    const uint32_t v = __builtin_amdgcn_readlane(vx, e);
+    const uint32_t p = __builtin_amdgcn_readlane(cp, e);
+    const uint64_t ti = gR + (uint32_t)__builtin_amdgcn_readlane(tio, e);
+    const uint64_t A = ti + (uint32_t)__builtin_amdgcn_readlane(aoff, e);
+    const uint32_t plj = reinterpret_cast<const uint16_t*>(a.gpl + (size_t)v * LP_FW)[lane];
+    uint32_t c = plj & nfl;
+    if (__ballot(c != 0) == 0) continue;
+    // rank of (lane j, bit q) among v's entries: the lanes below j first, then q ascending
+    const uint32_t own = (uint32_t)__popc(plj);
+    uint32_t pre = own;
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = __shfl_up(pre, off);
+      if (lane >= off) pre += y;
+    }
+    pre -= own;
+    const uint64_t* ge = a.gse + (size_t)v * a.L;
+    const uint64_t kb = (A << a.tshift) | v;
+    const bool tbad = A > a.tmax;
+    while (c) {
+      const int q = __builtin_ctz(c);
+      c &= c - 1;
+      const uint64_t en = ge[pre + (uint32_t)__popc(plj & ((1u << q) - 1u))];
+      if (!((en >> p) & 1)) continue;  // w is not among v's targets at heartbeat k
+      const uint32_t i = (uint32_t)q * 64 + lane;
+      const uint64_t x = CW[i];
+      if (x != INF64 && (x >> a.tshift) <= ti) continue;  // w has it by t_i (arrivals first at equal time)
+      niw++;
+      const uint32_t hv = (uint32_t)(en >> GSE_HOPS) + 1;
+      if (hv >= (1u << HOP_BITS)) err |= ERR_HOPS;
+      if (tbad) err |= ERR_TIME;
+      atomicMin((unsigned long long*)&CW[i], (unsigned long long)(kb | ((uint64_t)hv << a.sb)));
+      cb |= 1u << q;
+    }
+  }
+}
+
 // Record step: groups of NG = 4 neighbours, RCH = 2 chunks of 64 records each
 // per iteration (8 loads in flight per lane; 8 x 64 measured 2 % slower,
 // profiles/r03_v1/ab_record_groups.txt).
-template <int FP, uint32_t CH, bool IDW = false, bool PART = false>
+template <int FP, uint32_t CH, bool IDW = false, bool PART = false, bool GOS = false>
 __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
   constexpr uint32_t NG = 4, RCH = 2;
   static_assert(!IDW || FP == 1, "IDONTWANT on the list pass: rows of single-fragment lanes");
+  static_assert(!GOS || (FP == 1 && !IDW && !PART), "gossip on the list pass: gs_run's single-fragment rows");
   constexpr uint32_t LMAX = CH * 64;
   __shared__ LPullLds<CH> Ls;
-  // ---- decide this pass from the previous slot (grid-uniform; k_pull's rule) ----
-  const uint64_t* pv = a.ctrl + ((a.pass + 2) % 3) * 4;
-  uint64_t lo, mode;
-  if (pv[1] != PM_DONE && pv[2]) { mode = PM_PULL; lo = pv[1] == PM_PULL ? pv[0] + a.delta : pv[0]; }
-  else if (pv[3] != INF64) { mode = PM_EMIT; lo = ((pv[3] >> a.tshift) / a.delta) * a.delta; }
-  else { mode = PM_DONE; lo = pv[0]; }
   uint64_t* me = a.ctrl + (a.pass % 3) * 4;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    me[0] = lo;
-    me[1] = mode;
-    uint64_t* nx = a.ctrl + ((a.pass + 1) % 3) * 4;
-    nx[2] = 0;
-    nx[3] = INF64;
-    if (mode != PM_DONE) atomicAdd((unsigned long long*)&a.counters[C_PASSES], 1ull);
-    if (mode == PM_PULL) atomicAdd((unsigned long long*)&a.counters[C_BUCKETS], 1ull);
+  uint64_t lo, mode;
+  if constexpr (GOS) {  // k_lctl decided this pass (gossip windows need the heartbeat state)
+    lo = me[0];
+    mode = me[1];
+  } else {  // ---- decide this pass from the previous slot (grid-uniform; k_pull's rule) ----
+    const uint64_t* pv = a.ctrl + ((a.pass + 2) % 3) * 4;
+    if (pv[1] != PM_DONE && pv[2]) { mode = PM_PULL; lo = pv[1] == PM_PULL ? pv[0] + a.delta : pv[0]; }
+    else if (pv[3] != INF64) { mode = PM_EMIT; lo = ((pv[3] >> a.tshift) / a.delta) * a.delta; }
+    else { mode = PM_DONE; lo = pv[0]; }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      me[0] = lo;
+      me[1] = mode;
+      uint64_t* nx = a.ctrl + ((a.pass + 1) % 3) * 4;
+      nx[2] = 0;
+      nx[3] = INF64;
+      if (mode != PM_DONE) atomicAdd((unsigned long long*)&a.counters[C_PASSES], 1ull);
+      if (mode == PM_PULL) atomicAdd((unsigned long long*)&a.counters[C_BUCKETS], 1ull);
+    }
   }
   if (mode == PM_DONE) return;
 
@@ -156,6 +327,14 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
   const uint32_t* lat = a.tables;
   const uint32_t* sup = a.tables + S * S;
   const uint32_t* sdn = a.tables + S * S + S;
+  // lazy gossip: does this window hold IHAVE arrivals of the built heartbeat (k_lctl)?
+  bool gw = false;
+  uint64_t gR = 0;  // that heartbeat, relative to every t_pub
+  if constexpr (GOS) {
+    gw = a.gctl[GC_GW] != 0;
+    gR = a.grel0 + (a.gctl[GC_BK] - 1) * a.ghb;
+  }
+  uint64_t niw = 0, tfin = 0;  // IWANTs sent; largest final time of the pass
 
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint64_t* CW = Ls.cw[wv];
@@ -191,27 +370,32 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     }
     sv = a.st[(size_t)w * LP_SW + lane];
   }
+  uint32_t dw = 0;  // gossip windows: the row-done word of row w (every lane reads it)
+  if (GOS && gw && w < a.N) dw = a.rowdone[w >> 5];
   for (; w < a.N; w += stride) {
     PP_T(tA);
     const uint32_t w2 = w + stride;
-    uint32_t ej2 = EMPTY, rj2 = 0, cj2 = 0, sv2 = 0;
+    uint32_t ej2 = EMPTY, rj2 = 0, cj2 = 0, sv2 = 0, dw2 = 0;
     if (w2 < a.N && lane < (int)MESH_W) {  // w2 < N is wave-uniform
       ej2 = a.mesh[(size_t)(a.u0 + w2) * MESH_W + lane];
       rj2 = a.rpos[(size_t)(a.u0 + w2) * MESH_W + lane];
       sv2 = a.st[(size_t)w2 * LP_SW + lane];
     }
+    if (GOS && gw && w2 < a.N) dw2 = a.rowdone[w2 >> 5];
     const uint64_t cand = __ballot(cj != 0);
     // entries destined to window c; a count past the capacity means entries were
     // dropped (ERR_LIST, the batch re-runs on k_pull): read only what was written
     const uint32_t due = umin32(__builtin_amdgcn_readlane(sv, cslot), a.lcap);
-    if (cand == 0 && due == 0) {  // nothing to apply, nothing due: the pending windows stay
+    // gossip windows: a row with a lane not yet final may take IWANT answers
+    const bool gossip_row = GOS && gw && !((dw >> (w & 31)) & 1u);
+    if (cand == 0 && due == 0 && !gossip_row) {  // nothing to apply, nothing due: the pending windows stay
       if (lane == 0) wcnt[w] = 0;
       if (lane < (int)K && sv) nmh = umin32(nmh, lwhi);
       if (pull && lane < (int)MESH_W && ej2 != EMPTY) {
         cj2 = rcnt[ej2 & 0xFFFFFFu];
         if constexpr (PART) ro2 = a.roff[ej2 & 0xFFFFFFu];
       }
-      ej = ej2; rj = rj2; cj = cj2; sv = sv2; ro = ro2;
+      ej = ej2; rj = rj2; cj = cj2; sv = sv2; ro = ro2; dw = dw2;
       PP_T(tS);
       PP_ADD(0, tS - tA);
       continue;
@@ -330,6 +514,14 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
         }
       }
     }
+    // 2b. lazy gossip (GOS): IHAVEs of the built heartbeat k landing in window c
+    //     from the row's non-mesh connections v. Every entry and record of the
+    //     window is in CW now, so w has the message by the IHAVE's arrival t_i
+    //     iff CW holds a time <= t_i there; else w sends IWANT and v's answer
+    //     (its key's hops + 1, src v) is one more candidate, after window c.
+    if constexpr (GOS) {
+      if (gossip_row) glp_ihave(a, CW, w, sw, finT, wlo, gR, lat, sup, sdn, cb, niw, err);
+    }
     for (int off = 32; off > 0; off >>= 1) cb |= __shfl_xor(cb, off);
     cb = __builtin_amdgcn_readfirstlane(cb);
     wave_lds_sync();
@@ -385,8 +577,9 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     // lane j < K: entries appended to list slot j in this pass (lane-held, so
     // each group of 64 visits only the destination windows present in it)
     uint32_t addl = 0;
-    if (!pull && npend) err |= ERR_RING;  // an EMIT pass's minima all lie in window c
-    if (pull && npend) {
+    // an EMIT pass's minima all lie in window c, except IWANT answers (GOS)
+    if (!pull && !GOS && npend) err |= ERR_RING;
+    if ((pull || GOS) && npend) {
       const uint32_t lmax = a.lcap;
       for (uint32_t j0 = 0; j0 < npend; j0 += 64) {
         const bool jv = j0 + lane < npend;
@@ -398,7 +591,7 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
             const uint32_t d = (uint32_t)(x >> 32) - hlo;
             uint32_t q = (uint32_t)((float)d * rinv);
             if ((uint64_t)q * hspan > d) q--;
-            else if ((uint64_t)(q + 1) * hspan <= d) q++;
+            else if (((uint64_t)q + 1) * hspan <= d) q++;  // widened first: q may be 0xFFFFFFFF
             r = q < K ? q : K;
           } else {
             r = lp_rof((uint32_t)(x >> 32), thr, K);
@@ -477,6 +670,7 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
         if (act) {
           fd++;
           nr += n;
+          if constexpr (GOS) tfin = (x >> a.tshift) > tfin ? (x >> a.tshift) : tfin;
           if (n && hp + 1 >= (1u << HOP_BITS)) err |= ERR_HOPS;
           if (start - wlo >= (1ull << 32) || (n && start + a.rmax > a.tmax)) err |= ERR_TIME;
         }
@@ -504,6 +698,10 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     PP_ADD(5, tD - tP);
     // 5. row state: final bits, pending list lengths, log length
     if (nfin) reinterpret_cast<uint16_t*>(a.fin + (size_t)w * LP_FW)[lane] = (uint16_t)finT;
+    if constexpr (GOS) {  // every lane final: no IHAVE can matter to this row any more
+      if (nfin && wave_sum((uint64_t)__popc(finT & 0xFFFFu)) == a.B && lane == 0)
+        atomicOr(&a.rowdone[w >> 5], 1u << (w & 31));
+    }
     {
       uint32_t nv = sv;  // lane j < K: slot j (window c + lwin), emptied if it is window c's
       if (lane < (int)K) nv = lane == (int)cslot ? 0u : sv + addl;
@@ -518,7 +716,7 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     for (int q = 0; q < (int)CH; q++)
       if ((cb >> q) & 1u) CW[q * 64 + lane] = INF64;
     wave_lds_sync();
-    ej = ej2; rj = rj2; cj = cj2; sv = sv2; ro = ro2;
+    ej = ej2; rj = rj2; cj = cj2; sv = sv2; ro = ro2; dw = dw2;
     PP_T(tE);
     PP_ADD(6, tE - tD);
   }
@@ -538,6 +736,176 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     if (nr) atomicAdd((unsigned long long*)&a.counters[C_R_FWD], (unsigned long long)nr);
     if (np) atomicAdd((unsigned long long*)&a.counters[C_PUSH], (unsigned long long)np);
     if (err) atomicOr((unsigned*)&a.counters[C_ERR], err);
+  }
+  if constexpr (GOS) {
+    niw = wave_sum(niw);
+    for (int off = 32; off > 0; off >>= 1) {
+      const uint64_t y = __shfl_xor(tfin, off);
+      tfin = y > tfin ? y : tfin;
+    }
+    if (lane == 0) {
+      if (niw) atomicAdd((unsigned long long*)&a.counters[C_GOSSIP], (unsigned long long)niw);
+      atomicMax((unsigned long long*)&a.gctl[GC_TLAST], (unsigned long long)tfin);
+    }
+  }
+}
+
+// Pass control of a GOS batch (one thread, before every pass): k_pull's rule
+// (PULL the window whose records were just emitted, else EMIT the window of
+// the min pending key, else DONE), where an EMIT also stops at the first
+// window that can hold IHAVE arrivals while some lane is not final and some
+// final lane still gossips (its first heartbeat + history_gossip - 1); then
+// the heartbeats whose senders are all final now (R_k below the window):
+// the one whose IHAVEs are still to come gets its planes built before the
+// pass (k_gsend), and the pass learns whether its window holds its IHAVEs.
+__global__ void k_lctl(LPullArgs a) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint64_t* g = a.gctl;
+  const uint64_t* pv = a.ctrl + ((a.pass + 2) % 3) * 4;
+  uint64_t* me = a.ctrl + (a.pass % 3) * 4;
+  uint64_t* nx = a.ctrl + ((a.pass + 1) % 3) * 4;
+  const uint64_t D = a.delta, hb = a.ghb, r0 = a.grel0;
+  const uint64_t nf = a.gnf - (a.counters[C_FD] - g[GC_FD0]);  // lanes not final yet
+  const uint64_t tl = g[GC_TLAST];
+  const uint64_t kmax = (tl <= r0 ? 0 : (tl - r0 + hb - 1) / hb) + a.ghist - 1;  // last heartbeat with a sender
+  const bool gos = nf && a.ghist;
+  uint64_t lo, mode;
+  if (g[GC_DONE]) {
+    mode = PM_DONE;
+    lo = pv[0];
+  } else if (pv[1] != PM_DONE && pv[2]) {
+    mode = PM_PULL;
+    lo = pv[1] == PM_PULL ? pv[0] + D : pv[0];
+  } else {
+    uint64_t e = pv[3] != INF64 ? ((pv[3] >> a.tshift) / D) * D : INF64;
+    if (gos) {  // the next window with IHAVE arrivals: [R_k + lat_min, R_k + lat_max] from E on
+      const uint64_t E = g[GC_E];
+      const uint64_t k = E <= r0 + a.glat_max ? 0 : (E - r0 - a.glat_max + hb - 1) / hb;
+      if (k <= kmax) {
+        const uint64_t s = r0 + k * hb + a.glat_min;
+        const uint64_t ws = s >= E ? (s / D) * D : E;  // E is a window boundary
+        e = ws < e ? ws : e;
+      }
+    }
+    if (e == INF64) {
+      mode = PM_DONE;
+      lo = pv[0];
+      g[GC_DONE] = 1;
+    } else {
+      mode = PM_EMIT;
+      lo = e;
+    }
+  }
+  me[0] = lo;
+  me[1] = mode;
+  nx[2] = 0;
+  nx[3] = INF64;
+  g[GC_BUILD] = 0;
+  g[GC_GW] = 0;
+  if (mode == PM_DONE) return;
+  atomicAdd((unsigned long long*)&a.counters[C_PASSES], 1ull);
+  if (mode == PM_PULL) atomicAdd((unsigned long long*)&a.counters[C_BUCKETS], 1ull);
+  const uint64_t wl = mode == PM_PULL ? lo + D : lo;  // the window this pass emits
+  g[GC_E] = wl + D;
+  for (uint64_t k = g[GC_GB]; r0 + k * hb < wl; k++) {  // every t_v <= R_k is final now
+    if (gos && k <= kmax && r0 + k * hb + a.glat_max >= wl) {
+      g[GC_BUILD] = k + 1;
+      g[GC_BK] = k + 1;
+    }
+    g[GC_GB] = k + 1;
+  }
+  if (g[GC_BK] && gos) {
+    const uint64_t R = r0 + (g[GC_BK] - 1) * hb;
+    if (wl <= R + a.glat_max && wl + D > R + a.glat_min) g[GC_GW] = 1;
+  }
+}
+
+// Sender planes of heartbeat k = GC_BUILD - 1, before the pass that first
+// needs them. One wave per row v reads its final log (emission order: the
+// entries with t <= R_k come first), keeps the lanes v gossips at k (first
+// received in (R_(k - hist), R_k]), selects each one's IHAVE targets
+// (glp_targets at heartbeat habs0[m] + k, the oracle's gossip_targets) and
+// writes the plane and the entries (target mask | hops << 58) in rank order.
+// A row none of whose non-mesh connections has a lane left to finalise is
+// skipped: no pass reads its plane (row-done bits never clear within a batch).
+template <uint32_t CH>
+__global__ __launch_bounds__(TB) void k_gsend(LPullArgs a) {
+  const uint64_t bk = a.gctl[GC_BUILD];
+  if (!bk) return;  // grid-uniform: nothing to build before this pass
+  __shared__ uint64_t ent[PULL_WAVES][CH * 64];
+  __shared__ uint32_t sel[PULL_WAVES][CH * 64];
+  __shared__ uint32_t pl[PULL_WAVES][LP_FW];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t lanelt = (1ull << lane) - 1;
+  const uint64_t k = bk - 1, Rk = a.grel0 + k * a.ghb;
+  const bool haslo = k >= a.ghist;
+  const uint64_t Rlo = haslo ? a.grel0 + (k - a.ghist) * a.ghb : 0;
+  const uint32_t hmask = (1u << HOP_BITS) - 1;
+  for (uint32_t v = blockIdx.x * PULL_WAVES + wv; v < a.N; v += gridDim.x * PULL_WAVES) {
+    const uint64_t rb = a.row[v];
+    const uint32_t deg = (uint32_t)(a.row[v + 1] - rb);
+    uint32_t x = EMPTY;
+    bool nm = false;
+    if ((uint32_t)lane < deg) {
+      x = a.col[rb + lane];
+      nm = !(a.flags[rb + lane] & F_MESH);
+    }
+    bool need = false;
+    if (nm) need = !((a.rowdone[x >> 5] >> (x & 31)) & 1u);
+    if (__ballot(need) == 0) continue;  // wave-uniform
+    if (lane < (int)LP_FW) pl[wv][lane] = 0;
+    const uint64_t nmm = __ballot(nm);
+    const uint32_t nonmesh = (uint32_t)__popcll(nmm);
+    uint32_t r = (uint32_t)(((uint64_t)nonmesh * a.ggf) / 1000);
+    if (r < a.gd_lazy) r = a.gd_lazy;
+    if (r > nonmesh) r = nonmesh;
+    // 1. the senders of k from the log: lane | hops << 16
+    const uint32_t n = a.st[(size_t)v * LP_SW + LP_LOG];
+    uint32_t ns = 0;
+    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+      const uint32_t i = i0 + lane;
+      const uint64_t key = i < n ? a.keys[(size_t)v * a.L + i] : INF64;
+      const uint64_t t = key >> a.tshift;
+      const bool s = i < n && t <= Rk && (!haslo || t > Rlo);
+      const uint64_t sm = __ballot(s);
+      if (s)
+        sel[wv][ns + (uint32_t)__popcll(sm & lanelt)] =
+            (uint32_t)a.flane[(size_t)v * a.L + i] | ((uint32_t)(key >> a.sb) & hmask) << 16;
+      ns += (uint32_t)__popcll(sm);
+      // entries of later windows have t > R_k: stop after a chunk with none at or below R_k + Delta
+      if (__ballot(i < n && t <= Rk + a.delta) == 0) break;
+    }
+    wave_lds_sync();
+    // 2. each sender lane's targets at its message's heartbeat habs0[m] + k
+    for (uint32_t j0 = 0; j0 < ns; j0 += 64) {
+      const bool jv = j0 + lane < ns;
+      const uint32_t s = jv ? sel[wv][j0 + lane] : 0u;
+      const uint32_t m = s & 0xFFFFu;
+      const uint32_t h = jv ? (uint32_t)(a.habs0[m] + k) : 0u;
+      const uint64_t mask = glp_targets(a.gseed, v, h, x, nmm, deg, r);
+      if (jv) {
+        ent[wv][m] = mask | ((uint64_t)(s >> 16) << GSE_HOPS);
+        atomicOr(&pl[wv][(m & 63) >> 1], 1u << (16 * (m & 1) + (m >> 6)));
+      }
+    }
+    wave_lds_sync();
+    // 3. the plane, and the entries in rank order (lane j's bits q ascending after the lanes below j)
+    if (lane < (int)LP_FW) a.gpl[(size_t)v * LP_FW + lane] = pl[wv][lane];
+    const uint32_t plj = (pl[wv][lane >> 1] >> (16 * (lane & 1))) & 0xFFFFu;
+    const uint32_t own = (uint32_t)__popc(plj);
+    uint32_t pre = own;
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = __shfl_up(pre, off);
+      if (lane >= off) pre += y;
+    }
+    pre -= own;
+    uint32_t c = plj;
+    while (c) {
+      const int q = __builtin_ctz(c);
+      c &= c - 1;
+      a.gse[(size_t)v * a.L + pre++] = ent[wv][q * 64 + lane];
+    }
+    wave_lds_sync();
   }
 }
 
@@ -752,6 +1120,19 @@ void lpull_dispatch_part(uint32_t FP, const LPullArgs& a, unsigned grid, hipStre
     default: GS_LPP(16) break;
   }
 #undef GS_LPP
+}
+
+// One pass of a GOS batch: its control, the sender planes when a heartbeat's
+// senders just became final, the pass itself (rows of one fragment).
+void lpull_dispatch_gos(const LPullArgs& a, unsigned grid, hipStream_t s) {
+  k_lctl<<<1, 64, 0, s>>>(a);
+  if (lpull_chunks(a.L) == 8) {
+    k_gsend<8><<<grid, TB, 0, s>>>(a);
+    k_lpull<1, 8, false, false, true><<<grid, TB, 0, s>>>(a);
+  } else {
+    k_gsend<16><<<grid, TB, 0, s>>>(a);
+    k_lpull<1, 16, false, false, true><<<grid, TB, 0, s>>>(a);
+  }
 }
 
 void lpull_dispatch(uint32_t FP, const LPullArgs& a, unsigned grid, hipStream_t s) {

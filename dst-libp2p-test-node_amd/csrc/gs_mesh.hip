@@ -1120,6 +1120,16 @@ void churn_ring(Ctx& c, uint64_t h_lo, uint64_t h_hi) {
   if (c.h_pinned[0] & ERR_MESH) c.fail(GS_ERANGE, "mesh row exceeds GS_MESH_W entries");
 }
 
+// Position of each row's peer in its neighbour's row (k_csrpos), once per CSR:
+// the IHAVE receivers of the list pass test their bit in the sender's target mask.
+void ensure_csrpos(Ctx& c) {
+  if (c.csrpos_valid) return;
+  c.d_csrpos.alloc(c.nnz ? c.nnz : 1);
+  k_csrpos<<<blocks(c.cfg.peers), TB, 0, c.stream>>>(c.cfg.peers, c.d_row.p, c.d_col.p, c.d_rev.p, c.d_csrpos.p);
+  GS_HIP(hipGetLastError());
+  c.csrpos_valid = true;
+}
+
 uint32_t run_mesh(Ctx& c, uint32_t max_hb) {
   const uint32_t N = c.cfg.peers;
   hipStream_t s = c.stream;

@@ -400,6 +400,14 @@ static Batch setup_batch(Ctx& c, const gs_publish* sched, uint64_t i0, uint64_t 
     }
   }
   b.lat_min = min_lat;
+  for (uint32_t x = 0; x < S; x++)  // IHAVE x -> y, IWANT y -> x, answer x -> y (uplink of x, downlink of y)
+    for (uint32_t y = 0; y < S; y++) {
+      if (!c.stage_used[x] || !c.stage_used[y]) continue;
+      const uint64_t up = tab[(size_t)S * S + x], dn = tab[(size_t)S * S + S + y];
+      b.lat_max = std::max<uint64_t>(b.lat_max, tab[(size_t)x * S + y]);
+      b.ans_max = std::max<uint64_t>(b.ans_max, (uint64_t)tab[(size_t)y * S + x] + up + tab[(size_t)x * S + y] +
+                                                    (dn > up ? dn - up : 0));
+    }
   b.tpub.resize(b.B);
   for (uint32_t q = 0; q < b.B; q++) { pub[q] = sched[i0 + q].publisher; b.tpub[q] = sched[i0 + q].t_pub_ns; }
   c.d_pub.alloc(c.cfg.batch);
@@ -689,6 +697,10 @@ static RelaxArgs relax_args(Ctx& c, const Batch& b, bool gossip) {
       // sender-centric (exact for any value; GS_GOSSIP_SWITCH for tests / A/B)
       const char* gsw = getenv("GS_GOSSIP_SWITCH");
       ra.gs_switch = gsw && *gsw ? (uint32_t)atoi(gsw) : 4u;
+      // the per-lane first gossip heartbeat (RelaxArgs::hwin) saturates at 254:
+      // the receiver-centric test k < j0 needs gs_switch <= 254 to stay exact
+      // (a larger switch puts every heartbeat of a 16-epoch lifetime on that side anyway)
+      if (ra.gs_switch > 254) ra.gs_switch = 254;
     }
     ra.hist = c.cfg.history_gossip;
     ra.d_lazy = c.cfg.d_lazy;
@@ -834,7 +846,7 @@ static uint32_t lpull_stride(const Batch& b) { return std::max<uint32_t>(b.L, 25
 // destination is at most K - 1 windows after the emitted one; the entry
 // packs (t - window start) | hops | src | lane into 64 bits; the seed list
 // packs row << 11 | lane (N < 2^21); the lists must fit the device memory left.
-static uint32_t lpull_ring(Ctx& c, const Batch& b, uint64_t delta, uint32_t* lb) {
+static uint32_t lpull_ring(Ctx& c, const Batch& b, uint64_t delta, uint32_t* lb, bool gos = false) {
   if (!c.mesh_dmax) {  // widest mesh row, once per mesh
     std::vector<uint32_t> m((size_t)c.cfg.peers * MESH_W);
     GS_HIP(hipMemcpyAsync(m.data(), c.d_mesh.p, m.size() * 4, hipMemcpyDeviceToHost, c.stream));
@@ -858,6 +870,8 @@ static uint32_t lpull_ring(Ctx& c, const Batch& b, uint64_t delta, uint32_t* lb)
   const uint64_t sdeg = c.cfg.flood_publish ? std::max<uint64_t>(c.max_degree, 1) : dm;
   const uint64_t seed_span = (uint64_t)b.FP * sdeg * b.ser_max + b.lat_adj_max;
   uint64_t K = std::max(span / delta + 2, seed_span / delta + 1);
+  // GOS: an IWANT answer is appended from the window of its IHAVE's arrival
+  if (gos) K = std::max<uint64_t>(K, (delta + b.ans_max) / delta + 2);
   if (K > LP_KMAX) return 0;
   // test knob: a ring smaller than the bound forces ERR_RING and the k_pull re-run
   const char* kf = getenv("GS_LPULL_K");  // per batch: tests set it between runs
@@ -867,8 +881,12 @@ static uint32_t lpull_ring(Ctx& c, const Batch& b, uint64_t delta, uint32_t* lb)
   *lb = bits_for(b.L);
   if (tb + b.tshift + *lb > 64) return 0;
   const uint32_t N = c.cfg.peers;
-  const uint64_t need = (uint64_t)K * N * lpull_stride(b) * 8 + (uint64_t)N * b.L * 2 + (uint64_t)N * (LP_SW + LP_FW) * 4;
-  const uint64_t have = (uint64_t)c.d_lblk.n * 8 + (uint64_t)c.d_flane.n * 2 + (uint64_t)(c.d_lst.n + c.d_lfin.n) * 4;
+  uint64_t need = (uint64_t)K * N * lpull_stride(b) * 8 + (uint64_t)N * b.L * 2 + (uint64_t)N * (LP_SW + LP_FW) * 4;
+  uint64_t have = (uint64_t)c.d_lblk.n * 8 + (uint64_t)c.d_flane.n * 2 + (uint64_t)(c.d_lst.n + c.d_lfin.n) * 4;
+  if (gos) {  // sender planes and entries
+    need += (uint64_t)N * b.L * 8 + (uint64_t)N * LP_FW * 4;
+    have += (uint64_t)c.d_gse.n * 8 + (uint64_t)c.d_gpl.n * 4;
+  }
   if (need > have) {
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess || need - have + (4ull << 30) > fr) return 0;
@@ -883,9 +901,15 @@ static uint32_t lpull_ring(Ctx& c, const Batch& b, uint64_t delta, uint32_t* lb)
 // caller needs dense rows (k_lfinal).
 // Returns false (counters restored) when a list overflowed: the caller re-runs
 // the batch on k_pull.
+// Lazy gossip inside the passes (GOS): the batch's heartbeats relative to
+// every t_pub (lockstep) and the IHAVE travel bounds.
+struct GosRun {
+  uint64_t rel0, hb;
+};
+
 template <class EvFn>
 static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvFn& ev, size_t& n_ev, int dev_cus,
-                            bool dense, bool idw) {
+                            bool dense, bool idw, const GosRun* gos = nullptr) {
   const uint32_t N = c.cfg.peers, L = b.L;
   hipStream_t s = c.stream;
   const size_t NL = (size_t)N * L;
@@ -951,6 +975,38 @@ static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvF
       la, c.d_skey.p, c.d_slane.p, c.d_scnt.p);
   k_lpub<<<(b.B * b.Fe + 255) / 256, 256, 0, s>>>(la, b.Fe);
   GS_HIP(hipGetLastError());
+  if (gos) {  // GOS: sender planes, row-done bits, heartbeat control (gs_lpull_kernel.h)
+    ensure_csrpos(c);
+    c.d_gpl.alloc((size_t)N * LP_FW);
+    c.d_gse.alloc(NL);
+    c.d_rowdone.alloc(((size_t)N + 31) / 32);
+    c.d_gctl.alloc(GC_WORDS);
+    GS_HIP(hipMemsetAsync(c.d_rowdone.p, 0, ((size_t)N + 31) / 32 * 4, s));
+    GS_HIP(hipMemsetAsync(c.d_gctl.p, 0, GC_WORDS * 8, s));
+    GS_HIP(hipMemcpyAsync(c.d_gctl.p + GC_FD0, c.d_counters.p + C_FD, 8, hipMemcpyDeviceToDevice, s));
+    la.grel0 = gos->rel0;
+    la.ghb = gos->hb;
+    la.glat_min = b.lat_min;
+    la.glat_max = b.lat_max;
+    la.gnf = (uint64_t)b.B * (N - 1);
+    la.gseed = c.cfg.seed;
+    la.ghist = c.cfg.history_gossip;
+    la.gd_lazy = c.cfg.d_lazy;
+    la.ggf = c.cfg.gossip_factor_milli;
+    la.gctl = c.d_gctl.p;
+    la.gpl = c.d_gpl.p;
+    la.gse = c.d_gse.p;
+    la.rowdone = c.d_rowdone.p;
+    la.row = c.d_row.p;
+    la.col = c.d_col.p;
+    la.flags = c.d_flags.p;
+    la.csrpos = c.d_csrpos.p;
+    la.habs0 = c.d_habs0.p;
+  }
+  auto dispatch = [&] {
+    if (gos) lpull_dispatch_gos(la, grid, s);
+    else lpull_dispatch(b.FP, la, grid, s);
+  };
   uint32_t pass = 0;
   for (;;) {
     for (uint32_t q = 0; q < 8; q++) {
@@ -958,11 +1014,11 @@ static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvF
       if (c.timing) {  // (start, mid, end): the whole pass is frontier time
         GS_HIP(hipEventRecord(ev(n_ev), s));
         GS_HIP(hipEventRecord(ev(n_ev + 1), s));
-        lpull_dispatch(b.FP, la, grid, s);
+        dispatch();
         GS_HIP(hipEventRecord(ev(n_ev + 2), s));
         n_ev += 3;
       } else {
-        lpull_dispatch(b.FP, la, grid, s);
+        dispatch();
       }
     }
     GS_HIP(hipGetLastError());
@@ -1302,8 +1358,43 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     Batch bw = b;
     if (idw_b) bw.delta = std::min(b.delta, b.lat_min);
     const bool pull_ok = pull_any && bw.delta >= pull_grain(b.tshift) && (!idw_b || (b.FP == 1 && (variant & 64)));
+    // Lazy gossip inside the list pass (GOS, gs_lpull_kernel.h): rows of one
+    // fragment without IDONTWANT on the frozen mesh, every message's heartbeats
+    // the same time after its publish (lockstep), CSR rows narrow enough for a
+    // 58-bit target mask, windows no wider than the smallest latency (an IHAVE
+    // never shares a window with its heartbeat) and heartbeats farther apart
+    // than an IHAVE travels. GS_GOSSIP_LIST=0 keeps such batches on the eager
+    // pass + no-op proof, with the push path behind it.
+    bool lockstep = gossip && B > 0;
+    for (uint32_t q = 1; q < B && lockstep; q++) lockstep = rel0[q] == rel0[0];
+    Batch bg = b;
+    bg.delta = std::min(b.delta, b.lat_min);
+    const uint64_t ggr = pull_grain(b.tshift);
+    const char* glp_env = getenv("GS_GOSSIP_LIST");
+    const bool glp = gossip && !churn && pull_ok && !idw_b && b.FP == 1 && (variant & 64) && lockstep &&
+                     !(glp_env && *glp_env && atoi(glp_env) == 0) && c.max_degree <= GSE_HOPS && bg.delta >= ggr &&
+                     c.cfg.heartbeat_ns > b.lat_max + bg.delta;
+    bool glp_tried = false;
+    auto run_glp = [&]() -> bool {
+      glp_tried = true;
+      uint32_t lb = 0;
+      const uint32_t K = lpull_ring(c, bg, bg.delta / ggr * ggr, &lb, true);
+      if (!K) return false;
+      reset(variant, false, false);
+      const uint64_t iw0 = read_counter(c, C_GOSSIP);
+      const GosRun gr{rel0[0], c.cfg.heartbeat_ns};
+      const bool dense = sink != nullptr || c.traffic || getenv("GS_LPULL_DENSE");
+      if (!run_lpull_batch(c, bg, K, lb, ev, n_ev, dev_cus, dense, false, &gr)) return false;
+      c.stats.gossip_list_batches++;
+      // IWANTs taken: the next batch comes here directly (no eager run first)
+      c.glp_prefer = read_counter(c, C_GOSSIP) != iw0;
+      if (c.traffic) launch_traffic(c, b);
+      launch_complete(c, b, 0, N, sink, i0);
+      return true;
+    };
     bool done = false;
-    if (pull_ok || (gossip && !churn)) {
+    if (glp && c.glp_prefer) done = run_glp();
+    if (!done && (pull_ok || (gossip && !churn))) {
       if (gossip) GS_HIP(hipMemcpyAsync(c.d_cnt_save.p, c.d_counters.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));
       if (pull_ok) {
         const uint64_t grain = pull_grain(b.tshift);
@@ -1348,6 +1439,10 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
         } else {  // gossip can change this batch: discard the eager run's counters
           GS_HIP(hipMemcpyAsync(c.d_counters.p, c.d_cnt_save.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));
           c.stats.gossip_fallback_batches++;
+          if (glp && !glp_tried) {  // re-run with the gossip inside the passes
+            c.glp_prefer = true;
+            done = run_glp();
+          }
         }
       }
     }

@@ -26,7 +26,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GOSSIPSIM_LIB", os.path.join(HERE, "libgossipsim.so"))
-ABI_VERSION = 8
+ABI_VERSION = 9
 MESH_W = 16
 UNDELIVERED = np.uint64(0xFFFFFFFFFFFFFFFF)
 MUXERS = {"yamux": 0, "quic": 1, "mplex": 2}
@@ -78,7 +78,7 @@ class GsStats(ctypes.Structure):
         ("relax_ms", ctypes.c_double), ("run_ms", ctypes.c_double), ("relax_bytes_alg", u64),
         ("pushes", u64), ("scan_ms", ctypes.c_double), ("frontier_ms", ctypes.c_double),
         ("gossip_iwant", u64), ("gossip_noop_msgs", u64), ("gossip_fallback_batches", u64), ("batches", u64),
-        ("list_pull_batches", u64), ("ms_batches", u64)]
+        ("list_pull_batches", u64), ("ms_batches", u64), ("gossip_list_batches", u64)]
 
 
 class GsInjector(ctypes.Structure):

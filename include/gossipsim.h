@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 8u
+#define GS_ABI_VERSION 9u
 
 /* Sentinel for "never delivered" in t_complete_ns. */
 #define GS_UNDELIVERED UINT64_MAX
@@ -193,8 +193,10 @@ typedef struct gs_stats {
     uint64_t batches;           /* device batches run (gs_run splits at cfg.batch, size /  */
                                 /* chunk changes and the churn snapshot ring)             */
     uint64_t list_pull_batches; /* batches whose eager passes ran on candidate lists      */
+                                /* (k_lpull, DESIGN.md §4.3) rather than dense rows       */
     uint64_t ms_batches;        /* gs_run_partitioned batches run message-sharded (ABI 8) */
-                                /* (k_lpull, DESIGN.md §4.5) rather than dense rows       */
+    uint64_t gossip_list_batches; /* batches whose lazy gossip ran inside the list pass    */
+                                /* (IHAVE / IWANT decided per window, ABI 9; §2.7)        */
 } gs_stats;
 
 /* ---- host-only helpers (no device work) ---------------------------------- */

@@ -48,10 +48,13 @@ def test_lazy_gossip_noop_proof_on_pull_path():
 
 
 @pytest.mark.parametrize("phase_ms", [0, 120])
-def test_lazy_gossip_fallback_to_push_path(phase_ms):
+def test_lazy_gossip_fallback_to_push_path(monkeypatch, phase_ms):
     """A heartbeat at (or shortly after) the publish instant: IHAVEs can land
     before the last delivery, the batch is re-run with gossip on the push path
-    and the eager run's counters are discarded (bit-exact, IWANTs taken)."""
+    and the eager run's counters are discarded (bit-exact, IWANTs taken).
+    GS_GOSSIP_LIST=0 keeps these batches off the list pass's own gossip
+    (tests/test_gpu_gossip_list.py), the push path being the one tested here."""
+    monkeypatch.setenv("GS_GOSSIP_LIST", "0")
     p = oracle.params(peers=2000, seed=93, lazy_gossip=1,
                       hb_phase_ns=(T0 + phase_ms * 1_000_000) % 1_000_000_000)
     sim, _ = compare(p, 5, (50, 150, 40, 130), _sched(24, 2000), batch=8)
