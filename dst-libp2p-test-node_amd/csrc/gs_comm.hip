@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "gs_internal.h"
+#include "gs_layout.h"
 
 struct gs_ctx : gs::Ctx {};
 
@@ -230,13 +231,12 @@ void rank_gather(gs_comm* cm, Ctx& c, const uint64_t* mine, uint32_t n, uint64_t
 void run_batch_ms(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched, uint64_t i0, uint32_t B,
                   const gs_result_sink* sinks) {
   const uint32_t P = cm->nranks, N = cx[0]->cfg.peers;
-  auto u0_of = [&](uint32_t p) { return (uint32_t)((uint64_t)p * N / P); };
-  auto m0_of = [&](uint32_t p) { return (uint32_t)((uint64_t)p * B / P); };
-  const uint32_t mpmax = (B + P - 1) / P;
+  const PartLayout lay{P, N, B};
+  const uint32_t mpmax = lay.mmax();
   // 1. every part: its share of the messages over all N peers (device-resident rows [mp][N])
   for (uint32_t i = 0; i < nctx; i++) {
     Ctx& c = *cx[i];
-    const uint32_t me = cm->local ? i : cm->rank, m0 = m0_of(me), mp = m0_of(me + 1) - m0;
+    const uint32_t me = cm->local ? i : cm->rank, m0 = lay.m0(me), mp = lay.mn(me);
     GS_HIP(hipSetDevice(c.cfg.device));
     std::string why;
     gs_status code = GS_OK;
@@ -283,16 +283,16 @@ void run_batch_ms(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched,
     }
     for (uint32_t r = 0; r < nctx; r++) {
       Ctx& d = *cx[r];
-      const uint32_t u0 = u0_of(r), un = u0_of(r + 1) - u0;
+      const uint32_t u0 = lay.u0(r), un = lay.un(r);
       GS_HIP(hipSetDevice(d.cfg.device));
       d.d_tc_t.alloc((size_t)un * B);
       d.d_hops_t.alloc((size_t)un * B);
-      for (uint32_t p = 0; p < nctx; p++) {
-        const uint32_t m0 = m0_of(p), mp = m0_of(p + 1) - m0;
+      for (uint32_t p = 0; p < nctx; p++) {  // part p's block of r's peers, straight from p's rows
+        const uint32_t mp = lay.mn(p);
         if (!mp) continue;
-        GS_HIP(hipMemcpy2DAsync(d.d_tc_t.p + (size_t)m0 * un, (size_t)un * 8, cx[p]->d_ms_tc.p + u0, (size_t)N * 8,
-                                (size_t)un * 8, mp, hipMemcpyDeviceToDevice, d.stream));
-        GS_HIP(hipMemcpy2DAsync(d.d_hops_t.p + (size_t)m0 * un, un, cx[p]->d_ms_hops.p + u0, N, un, mp,
+        GS_HIP(hipMemcpy2DAsync(d.d_tc_t.p + lay.ms_recv_off(p, r), (size_t)un * 8, cx[p]->d_ms_tc.p + u0,
+                                (size_t)N * 8, (size_t)un * 8, mp, hipMemcpyDeviceToDevice, d.stream));
+        GS_HIP(hipMemcpy2DAsync(d.d_hops_t.p + lay.ms_recv_off(p, r), un, cx[p]->d_ms_hops.p + u0, N, un, mp,
                                 hipMemcpyDeviceToDevice, d.stream));
       }
     }
@@ -303,17 +303,17 @@ void run_batch_ms(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched,
   } else {
     Ctx& c = *cx[0];
     Rccl* rc = rccl();
-    const uint32_t me = cm->rank, mme = m0_of(me + 1) - m0_of(me), u0me = u0_of(me), unme = u0_of(me + 1) - u0me;
+    const uint32_t me = cm->rank, mme = lay.mn(me), unme = lay.un(me);
     GS_HIP(hipSetDevice(c.cfg.device));
-    // pack: destination r's block [mme][un_r] at offset mme * u0_r
+    // pack: destination r's block [mme][un_r] at lay.ms_send_off(me, r)
     c.d_ms_send.alloc(std::max<size_t>(1, (size_t)mme * N));
     c.d_ms_sendh.alloc(std::max<size_t>(1, (size_t)mme * N));
     if (mme)
       for (uint32_t r = 0; r < P; r++) {
-        const uint32_t u0 = u0_of(r), un = u0_of(r + 1) - u0;
-        GS_HIP(hipMemcpy2DAsync(c.d_ms_send.p + (size_t)mme * u0, (size_t)un * 8, c.d_ms_tc.p + u0, (size_t)N * 8,
-                                (size_t)un * 8, mme, hipMemcpyDeviceToDevice, c.stream));
-        GS_HIP(hipMemcpy2DAsync(c.d_ms_sendh.p + (size_t)mme * u0, un, c.d_ms_hops.p + u0, N, un, mme,
+        const uint32_t u0 = lay.u0(r), un = lay.un(r);
+        GS_HIP(hipMemcpy2DAsync(c.d_ms_send.p + lay.ms_send_off(me, r), (size_t)un * 8, c.d_ms_tc.p + u0,
+                                (size_t)N * 8, (size_t)un * 8, mme, hipMemcpyDeviceToDevice, c.stream));
+        GS_HIP(hipMemcpy2DAsync(c.d_ms_sendh.p + lay.ms_send_off(me, r), un, c.d_ms_hops.p + u0, N, un, mme,
                                 hipMemcpyDeviceToDevice, c.stream));
       }
     c.d_tc_t.alloc((size_t)unme * B);
@@ -321,14 +321,14 @@ void run_batch_ms(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched,
     const uint64_t pb = rccl_piece_bytes(), p8 = std::max<uint64_t>(1, pb / 8);
     GS_NCCL(rc->GroupStart());
     for (uint32_t r = 0; r < P; r++) {
-      const uint64_t n = (uint64_t)mme * (u0_of(r + 1) - u0_of(r)), off = (uint64_t)mme * u0_of(r);
+      const uint64_t n = lay.ms_count(me, r), off = lay.ms_send_off(me, r);
       for (uint64_t k = 0; k < n; k += p8)
         GS_NCCL(rc->Send(c.d_ms_send.p + off + k, std::min(p8, n - k), ncclUint64, (int)r, cm->nc, c.stream));
       for (uint64_t k = 0; k < n; k += pb)
         GS_NCCL(rc->Send(c.d_ms_sendh.p + off + k, std::min(pb, n - k), ncclUint8, (int)r, cm->nc, c.stream));
     }
     for (uint32_t p = 0; p < P; p++) {
-      const uint64_t n = (uint64_t)(m0_of(p + 1) - m0_of(p)) * unme, off = (uint64_t)m0_of(p) * unme;
+      const uint64_t n = lay.ms_count(p, me), off = lay.ms_recv_off(p, me);
       for (uint64_t k = 0; k < n; k += p8)
         GS_NCCL(rc->Recv(c.d_tc_t.p + off + k, std::min(p8, n - k), ncclUint64, (int)p, cm->nc, c.stream));
       for (uint64_t k = 0; k < n; k += pb)
@@ -341,7 +341,7 @@ void run_batch_ms(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched,
   if (!sinks) return;
   for (uint32_t i = 0; i < nctx; i++) {
     Ctx& c = *cx[i];
-    const uint32_t me = cm->local ? i : cm->rank, un = u0_of(me + 1) - u0_of(me);
+    const uint32_t me = cm->local ? i : cm->rank, un = lay.un(me);
     GS_HIP(hipSetDevice(c.cfg.device));
     deliver_rows(c, B, un, &sinks[i], i0);
     GS_HIP(hipStreamSynchronize(c.stream));
@@ -433,7 +433,7 @@ bool run_batch_lp(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched,
     }
     GS_HIP(hipEventRecord(c.ev_pool[nev[i]++], c.stream));
   };
-  auto u0_of = [&](uint32_t p) { return (uint32_t)((uint64_t)p * N / P); };
+  const PartLayout lay{P, N, B};
   const size_t RB = 8;  // bytes per record
   std::vector<uint64_t> st((size_t)P * 4);  // per part: mode, records, min pending, error word
   for (;;) {
@@ -473,8 +473,9 @@ bool run_batch_lp(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched,
     }
     if (!recs) continue;  // the next pass emits a window: it reads no records
     // pack (each part knows its offset in the packed records of all parts)
-    std::vector<uint64_t> base(P + 1, 0);
-    for (uint32_t p = 0; p < P; p++) base[p + 1] = base[p] + st[(size_t)p * 4 + 1];
+    std::vector<uint64_t> base(P + 1, 0), cnt(P);
+    for (uint32_t p = 0; p < P; p++) cnt[p] = st[(size_t)p * 4 + 1];
+    lp_bases(cnt.data(), P, base.data());
     for (uint32_t i = 0; i < nctx; i++) {
       const uint32_t me = cm->local ? i : cm->rank;
       GS_HIP(hipSetDevice(cx[i]->cfg.device));
@@ -488,7 +489,7 @@ bool run_batch_lp(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched,
         GS_HIP(hipSetDevice(d.cfg.device));
         for (uint32_t p = 0; p < nctx; p++) {
           Ctx& src = *cx[p];
-          const uint64_t n = st[(size_t)p * 4 + 1], u0 = u0_of(p), un = u0_of(p + 1) - u0;
+          const uint64_t n = cnt[p], u0 = lay.u0(p), un = lay.un(p);
           if (n) GS_HIP(hipMemcpyAsync(d.d_rpk.p + base[p], src.d_pkout.p, n * RB, hipMemcpyDeviceToDevice, d.stream));
           GS_HIP(hipMemcpyAsync(d.d_rcg.p + u0, part_lp_counts(src), un * 4, hipMemcpyDeviceToDevice, d.stream));
           GS_HIP(hipMemcpyAsync(d.d_roffg.p + u0, src.d_pkroff.p, un * 8, hipMemcpyDeviceToDevice, d.stream));
@@ -499,7 +500,7 @@ bool run_batch_lp(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched,
       Ctx& c = *cx[0];
       const uint32_t me = cm->rank;
       const uint64_t piece = std::max<uint64_t>(1, rccl_piece_bytes() / RB);
-      const uint64_t myn = st[(size_t)me * 4 + 1], my0 = u0_of(me), myun = u0_of(me + 1) - my0;
+      const uint64_t myn = cnt[me], myun = lay.un(me);
       GS_NCCL(r->GroupStart());
       for (uint32_t d = 0; d < P; d++) {
         for (uint64_t k = 0; k < myn; k += piece)
@@ -508,7 +509,7 @@ bool run_batch_lp(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched,
         GS_NCCL(r->Send(c.d_pkroff.p, myun, ncclUint64, (int)d, cm->nc, c.stream));
       }
       for (uint32_t sr = 0; sr < P; sr++) {
-        const uint64_t n = st[(size_t)sr * 4 + 1], u0 = u0_of(sr), un = u0_of(sr + 1) - u0;
+        const uint64_t n = cnt[sr], u0 = lay.u0(sr), un = lay.un(sr);
         for (uint64_t k = 0; k < n; k += piece)
           GS_NCCL(r->Recv(c.d_rpk.p + base[sr] + k, std::min(piece, n - k), ncclUint64, (int)sr, cm->nc, c.stream));
         GS_NCCL(r->Recv(c.d_rcg.p + u0, un, ncclUint32, (int)sr, cm->nc, c.stream));
@@ -767,6 +768,9 @@ extern "C" gs_status gs_run_partitioned(gs_ctx* const* ctxs, uint32_t nctx, gs_c
   try {
     if (comm->local ? nctx != comm->nranks : nctx != 1)
       c0->fail(GS_EINVAL, "gs_run_partitioned: pass one context per part (local) or this rank's context (RCCL)");
+    for (uint32_t i = 0; sinks && i < nctx; i++)
+      if (sinks[i].on_lat || (sinks[i].want & GS_WANT_LAT_MS))
+        c0->fail(GS_EUNSUPPORTED, "gs_run_partitioned: the u16 latency stream (on_lat) is gs_run's");
     std::vector<Ctx*> cx(nctx);
     for (uint32_t i = 0; i < nctx; i++) {
       cx[i] = ctxs[i];

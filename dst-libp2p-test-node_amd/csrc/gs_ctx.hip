@@ -15,6 +15,8 @@ namespace gs {
 Ctx::~Ctx() {
   for (auto e : ev_pool) (void)hipEventDestroy(e);
   for (auto e : side_ev) (void)hipEventDestroy(e);
+  for (auto e : blk_ev)
+    if (e) (void)hipEventDestroy(e);
   if (side) (void)hipStreamDestroy(side);
   if (h_pinned) (void)hipHostFree(h_pinned);
   if (h_block) (void)hipHostFree(h_block);
@@ -216,8 +218,10 @@ extern "C" gs_status gs_run(gs_ctx* ctx, const gs_publish* sched, uint64_t n_msg
   if (sink && sink->on_block && (sink->t_complete_ns || sink->hops))
     ctx->fail(GS_EINVAL, "gs_result_sink: with on_block, t_complete_ns and hops must be NULL (select outputs "
                          "with want, ABI 7)");
-  if (sink && (sink->want & ~(uint32_t)(GS_WANT_T_COMPLETE | GS_WANT_HOPS)))
+  if (sink && (sink->want & ~(uint32_t)(GS_WANT_T_COMPLETE | GS_WANT_HOPS | GS_WANT_LAT_MS)))
     ctx->fail(GS_EINVAL, "gs_result_sink.want: unknown bits");
+  if (sink && (sink->on_lat != nullptr) != ((sink->want & GS_WANT_LAT_MS) != 0))
+    ctx->fail(GS_EINVAL, "gs_result_sink: on_lat and GS_WANT_LAT_MS go together");
   GS_HIP(hipSetDevice(ctx->cfg.device));
   if (n_msgs) run_messages(*ctx, sched, n_msgs, sink);
   GS_API_END(ctx)

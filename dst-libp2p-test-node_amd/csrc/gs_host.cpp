@@ -709,14 +709,16 @@ namespace {
 uint64_t nim_msg_id(const gs_config* cfg, const gs_publish& p) {  // msgId = rand(high(int64)) (main.nim:162)
   return gs::rng(cfg->seed, gs::P_MSGID, p.publisher, (uint32_t)(p.t_pub_ns >> 32), (uint32_t)p.t_pub_ns) >> 1;
 }
-void log_line(FILE* f, const gs_config* cfg, uint32_t u, uint64_t line, const gs_publish& p, uint64_t t) {
-  const int64_t ms = ((int64_t)t - (int64_t)p.t_pub_ns) / 1000000;  // i64 division, main.rs:91-93
+void log_line_ms(FILE* f, const gs_config* cfg, uint32_t u, uint64_t line, const gs_publish& p, int64_t ms) {
   if (cfg->node == GS_NODE_NIM)
     fprintf(f, "shadow.data/hosts/peer%u/main.1000.stdout:%llu:%llu milliseconds: %lld\n", u,
             (unsigned long long)line, (unsigned long long)nim_msg_id(cfg, p), (long long)ms);
   else
     fprintf(f, "shadow.data/hosts/peer%u/main.1000.stdout:%llu:%lld milliseconds: %lld\n", u,
             (unsigned long long)line, (long long)p.t_pub_ns, (long long)ms);
+}
+void log_line(FILE* f, const gs_config* cfg, uint32_t u, uint64_t line, const gs_publish& p, uint64_t t) {
+  log_line_ms(f, cfg, u, line, p, ((int64_t)t - (int64_t)p.t_pub_ns) / 1000000);  // i64 division, main.rs:91-93
 }
 }  // namespace
 
@@ -750,6 +752,20 @@ extern "C" gs_status gs_log_write(gs_log* L, const gs_publish* sched, uint32_t n
       const uint64_t t = tc[(size_t)m * N + u];
       if (t == GS_UNDELIVERED || (u == sched[m].publisher && !L->cfg.self_log)) continue;
       log_line(L->f, &L->cfg, u, ++L->line[u], sched[m], t);
+    }
+  return ferror(L->f) ? GS_EINVAL : GS_OK;
+}
+
+// The same lines from the u16 latency stream (gs_result_sink.on_lat): the
+// value is the log line's ms already, GS_LAT_NONE where nothing is logged.
+extern "C" gs_status gs_log_write_lat(gs_log* L, const gs_publish* sched, uint32_t n_msgs, const uint16_t* lat_ms) {
+  if (!L || (!sched && n_msgs) || (!lat_ms && n_msgs)) return GS_EINVAL;
+  const uint32_t N = L->cfg.peers;
+  for (uint32_t m = 0; m < n_msgs; m++)
+    for (uint32_t u = 0; u < N; u++) {
+      const uint16_t v = lat_ms[(size_t)m * N + u];
+      if (v == GS_LAT_NONE) continue;
+      log_line_ms(L->f, &L->cfg, u, ++L->line[u], sched[m], (int64_t)v);
     }
   return ferror(L->f) ? GS_EINVAL : GS_OK;
 }

@@ -27,7 +27,8 @@ struct Error {
 // Device-side error word bits (set by kernels, checked by the host).
 // ERR_LIST: a list pull candidate list overflowed; ERR_RING: a list pull candidate
 // fell outside the K-window ring the host bound promised. Both re-run the batch on k_pull.
-enum : uint32_t { ERR_TIME = 1, ERR_HOPS = 2, ERR_MESH = 4, ERR_DEG = 8, ERR_LIST = 16, ERR_RING = 32 };
+// ERR_LAT16: a logged latency of 65535 ms or more for the u16 stream (GS_WANT_LAT_MS).
+enum : uint32_t { ERR_TIME = 1, ERR_HOPS = 2, ERR_MESH = 4, ERR_DEG = 8, ERR_LIST = 16, ERR_RING = 32, ERR_LAT16 = 64 };
 
 // Device buffer owned by a context.
 template <class T>
@@ -154,6 +155,9 @@ struct Ctx {
   DevBuf<uint8_t> d_hops;    // [N * B]
   DevBuf<uint64_t> d_tc_t;   // [B * N] message-major staging for the caller's sink
   DevBuf<uint8_t> d_hops_t;
+  DevBuf<uint16_t> d_lat;    // [N * B] peer-major logged latency in ms (GS_WANT_LAT_MS)
+  DevBuf<uint16_t> d_lat_t;  // [B * N] message-major staging of it
+  hipEvent_t blk_ev[2] = {nullptr, nullptr};  // double-buffered streaming: D2H of block k done
   DevBuf<uint32_t> d_tables; // lat[S*S] | ser_up[S] | ser_dn[S] (u32 ns)
   DevBuf<uint64_t> d_ctrl;   // [4] triple-buffered next-min keys + spare
   // owner-computes pull path (gs_pull_kernel.h)

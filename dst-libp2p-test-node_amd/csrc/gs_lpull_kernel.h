@@ -80,6 +80,7 @@ struct LPullArgs {
   uint32_t N, B, L, S, sb, tshift, pass, K, lb, dG;  // lb = lane bits, dG = Delta in key hi-word grains
   uint32_t ls, lcap;  // list stride (max(L, 256) entries) and capacity (ls; GS_LPULL_CAP lowers it)
   uint32_t idw;       // IDONTWANT batch (k_lpull<.., true>): finals go to dense keys[N][L], no log
+  uint32_t self_log;  // k_lcomplete's latency stream: the publisher logs its own message
   uint64_t rmax;      // largest arrival offset of a forward after its uplink start (lat + dn + MESH_W ser):
                       // the emit step checks start + rmax <= tmax, so receivers need no time check
   // peer-partitioned pass (k_lpull<.., .., .., true>, gs_run_partitioned): this context's rows are
@@ -987,7 +988,9 @@ __global__ __launch_bounds__(TB) void k_lfinal(LPullArgs a) {
 // log entry is a delivery unless the row is the message's publisher); one
 // flush per block through LDS.
 constexpr uint32_t LC_WAVES = 16;
-__global__ __launch_bounds__(LC_WAVES * 64) void k_lcomplete(LPullArgs a, uint64_t* mstat) {
+// With `lat` it also writes each row's logged latencies ([N][B] u16, the
+// GS_WANT_LAT_MS stream; GS_LAT_NONE where nothing is logged).
+__global__ __launch_bounds__(LC_WAVES * 64) void k_lcomplete(LPullArgs a, uint64_t* mstat, uint16_t* lat) {
   __shared__ uint64_t R[LC_WAVES][PULL_LMAX];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t B = a.B, stride = gridDim.x * LC_WAVES;
@@ -1021,6 +1024,25 @@ __global__ __launch_bounds__(LC_WAVES * 64) void k_lcomplete(LPullArgs a, uint64
         if (k4[u] != INF64) Rw[l4[u]] = k4[u];
     }
     wave_lds_sync();
+    if (lat) {  // block-uniform
+      bool big = false;
+#pragma unroll
+      for (int j = 0; j < (int)PULL_CH; j++) {
+        const uint32_t m = j * 64 + lane;
+        if (m >= B) continue;
+        const uint64_t x = Rw[m];
+        uint32_t v = GS_LAT_NONE;
+        if (pm[j] == w) {
+          if (a.self_log && x != INF64) v = 0;
+        } else if (x != INF64) {
+          const uint64_t ms = (x >> a.tshift) / 1000000ull;
+          big |= ms >= 0xFFFF;
+          v = ms < 0xFFFF ? (uint32_t)ms : 0xFFFEu;
+        }
+        lat[(size_t)w * B + m] = (uint16_t)v;
+      }
+      if (big) atomicOr((unsigned*)&a.counters[C_ERR], ERR_LAT16);
+    }
 #pragma unroll
     for (int j = 0; j < (int)PULL_CH; j++) {
       const uint32_t m = j * 64 + lane;

@@ -346,8 +346,9 @@ void part_set(Ctx& c, uint32_t parts, uint32_t part) {
   if (parts < 1 || part >= parts || parts > N) c.fail(GS_EINVAL, "need 1 <= parts <= peers and part < parts");
   c.part_parts = parts;
   c.part_idx = part;
-  c.part_u0 = (uint32_t)((uint64_t)part * N / parts);
-  c.part_un = (uint32_t)((uint64_t)(part + 1) * N / parts) - c.part_u0;
+  const PartLayout lay{parts, N, 0};
+  c.part_u0 = lay.u0(part);
+  c.part_un = lay.un(part);
 }
 
 // The knobs a partitioned batch accepts (both protocols).

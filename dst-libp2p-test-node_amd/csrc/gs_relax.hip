@@ -22,6 +22,7 @@
 #include <algorithm>
 
 #include "gs_internal.h"
+#include "gs_layout.h"
 
 namespace gs {
 namespace {
@@ -138,6 +139,7 @@ struct CompArgs {
   const uint64_t* tpub;
   uint64_t* tc;     // [N][B] peer-major, like the keys
   uint8_t* hops;    // [N][B]
+  uint16_t* lat;    // [N][B] logged latency in ms (GS_WANT_LAT_MS), else nullptr
   uint64_t* counters;
   uint64_t* mstat;  // [B][MS_COLS] per-message reductions (k_complete / k_pct)
   uint32_t* hist;   // [B][GS_HIST_BINS] 100 ms latency bins (summary requested), else nullptr
@@ -248,6 +250,10 @@ __global__ __launch_bounds__(TB) void k_complete(CompArgs a) {
       a.tc[i] = tc;
       a.hops[i] = h;
     }
+    if (a.lat) {  // the log line's value (main.rs:93), GS_LAT_NONE where nothing is logged
+      if (lms >= 0xFFFF) atomicOr((unsigned*)&a.counters[C_ERR], ERR_LAT16);
+      a.lat[i] = lms < 0 ? (uint16_t)GS_LAT_NONE : (uint16_t)(lms < 0xFFFF ? lms : 0xFFFE);
+    }
   }
   {
     const uint64_t d = wave_sum(deliv), s = wave_sum(lsum);
@@ -303,6 +309,24 @@ __global__ __launch_bounds__(TB) void k_pct(CompArgs a) {
   for (uint32_t i = threadIdx.x; i < a.MT * 2 * GS_HIST_MS; i += TB) {
     const uint32_t mm = m0 + i / (2 * GS_HIST_MS);
     if (sf[i] && mm < a.B) atomicAdd(&a.fine[(size_t)mm * 2 * GS_HIST_MS + i % (2 * GS_HIST_MS)], sf[i]);
+  }
+}
+
+// The logged latency [N][B] u16 -> [B][N] through a 64x64 LDS tile (the
+// message-major GS_WANT_LAT_MS stream).
+__global__ __launch_bounds__(TB) void k_transpose16(const uint16_t* __restrict__ lat, uint16_t* __restrict__ lat_t,
+                                                    uint32_t N, uint32_t B) {
+  __shared__ uint16_t s[64][66];
+  const uint32_t u0 = blockIdx.x * 64, m0 = blockIdx.y * 64;
+  const uint32_t nu = min(64u, N - u0), nm = min(64u, B - m0);
+  for (uint32_t i = threadIdx.x; i < 64 * 64; i += TB) {
+    const uint32_t pu = i >> 6, qm = i & 63;
+    if (pu < nu && qm < nm) s[qm][pu] = lat[(size_t)(u0 + pu) * B + m0 + qm];
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < 64 * 64; i += TB) {
+    const uint32_t qm = i >> 6, pu = i & 63;
+    if (pu < nu && qm < nm) lat_t[(size_t)(m0 + qm) * N + u0 + pu] = s[qm][pu];
   }
 }
 
@@ -461,27 +485,31 @@ static void launch_seed(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, uint64
 // 100 ms histograms of gs_msg_summary.
 // store: write d_tc / d_hops (results go to a sink); without it only the
 // counters and reductions are produced (a device-resident run).
+// lat: also the logged latencies [un][B] u16 into d_lat (GS_WANT_LAT_MS).
 static void run_complete(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, bool mstat, bool hist,
-                         bool store = true) {
+                         bool store = true, bool lat = false) {
   hipStream_t s = c.stream;
+  if (lat) c.d_lat.alloc((size_t)un * c.cfg.batch);
   if (c.keys_log) {  // list pull path, results on the device: reduce the final logs
     if (hist || store || u0 || un != c.cfg.peers || b.FP != 1) c.fail(GS_EINVAL, "internal: final logs need k_lfinal");
     LPullArgs la{};
     la.keys = c.d_keys.p; la.flane = c.d_flane.p; la.st = c.d_lst.p; la.pub = c.d_pub.p;
     la.counters = c.d_counters.p; la.N = un; la.B = b.B; la.L = b.L; la.tshift = b.tshift;
+    la.self_log = c.cfg.self_log;
     if (mstat) {
       c.d_mstat.alloc((size_t)c.cfg.batch * MS_COLS);
       GS_HIP(hipMemsetAsync(c.d_mstat.p, 0, (size_t)b.B * MS_COLS * 8, s));
     }
     const unsigned grid = (unsigned)std::max<uint64_t>(
         1, std::min<uint64_t>(((uint64_t)un + LC_WAVES - 1) / LC_WAVES, (uint64_t)std::max(1, c.num_cus)));
-    k_lcomplete<<<grid, LC_WAVES * 64, 0, s>>>(la, mstat ? c.d_mstat.p : nullptr);
+    k_lcomplete<<<grid, LC_WAVES * 64, 0, s>>>(la, mstat ? c.d_mstat.p : nullptr, lat ? c.d_lat.p : nullptr);
     GS_HIP(hipGetLastError());
     return;
   }
   CompArgs ca{};
   ca.keys = c.d_keys.p; ca.pub = c.d_pub.p; ca.tpub = c.d_tpub.p; ca.tc = store ? c.d_tc.p : nullptr;
   ca.hops = c.d_hops.p; ca.counters = c.d_counters.p; ca.N = un; ca.B = b.B; ca.F = b.F;
+  ca.lat = lat ? c.d_lat.p : nullptr;
   ca.FP = b.FP; ca.L = b.L; ca.sb = b.sb; ca.tshift = b.tshift; ca.collide = b.collide ? 1 : 0;
   ca.u0 = u0;
   ca.self_log = c.cfg.self_log;
@@ -599,72 +627,126 @@ static void fill_summary(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, gs_ms
   }
 }
 
-// Results of the batch to the caller: message-major copy into the sink
-// arrays (rows sink_row0..), or streamed in blocks through on_block; then the
-// per-message summaries.
-// Message-major rows [B][un] in d_tc_t / d_hops_t into a sink's rows
-// [row0, row0 + B): its arrays (host memory; device memory when c.sink_dev,
-// the message-sharded partitioned batches of gs_comm.hip) or on_block blocks.
+// What a sink takes from a batch (include/gossipsim.h gs_result_sink): with
+// on_block the want bits select t_complete / hops (neither = both), without
+// it the non-NULL arrays do; on_lat takes the logged latency (GS_WANT_LAT_MS).
+struct SinkWants {
+  bool tc = false, h = false, lat = false, summary = false;
+  bool rows() const { return tc || h; }
+};
+static SinkWants sink_wants(const gs_result_sink* sink) {
+  SinkWants w;
+  if (!sink) return w;
+  if (sink->on_block) {
+    uint32_t th = sink->want & (GS_WANT_T_COMPLETE | GS_WANT_HOPS);
+    if (!th) th = GS_WANT_T_COMPLETE | GS_WANT_HOPS;
+    w.tc = (th & GS_WANT_T_COMPLETE) != 0;
+    w.h = (th & GS_WANT_HOPS) != 0;
+  } else {
+    w.tc = sink->t_complete_ns != nullptr;
+    w.h = sink->hops != nullptr;
+  }
+  w.lat = sink->on_lat != nullptr;
+  w.summary = sink->summary != nullptr;
+  return w;
+}
+
+// Message-major rows of the batch — [B][un] in d_tc_t / d_hops_t, and the
+// latency in d_lat_t — into a sink's rows [row0, row0 + B): its arrays (host
+// memory; device memory when c.sink_dev, the message-sharded partitioned
+// batches of gs_comm.hip), and the on_block / on_lat streams in blocks of
+// block_msgs messages through two pinned staging halves (the copy of block k
+// runs while the caller's callbacks consume block k - 1).
 void deliver_rows(Ctx& c, uint32_t B, uint32_t un, const gs_result_sink* sink, uint64_t sink_row0) {
   hipStream_t s = c.stream;
-  const uint32_t want = sink->want ? sink->want : (GS_WANT_T_COMPLETE | GS_WANT_HOPS);
-  const bool want_tc = sink->on_block ? (want & GS_WANT_T_COMPLETE) != 0 : sink->t_complete_ns != nullptr;
-  const bool want_h = sink->on_block ? (want & GS_WANT_HOPS) != 0 : sink->hops != nullptr;
-  if (!sink->on_block) {
+  const SinkWants w = sink_wants(sink);
+  if (!sink->on_block && w.rows()) {
     const hipMemcpyKind kind = c.sink_dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
-    if (want_tc)
-      GS_HIP(hipMemcpyAsync(sink->t_complete_ns + sink_row0 * un, c.d_tc_t.p, (size_t)B * un * 8, kind, s));
-    if (want_h) GS_HIP(hipMemcpyAsync(sink->hops + sink_row0 * un, c.d_hops_t.p, (size_t)B * un, kind, s));
-    return;
+    if (w.tc) GS_HIP(hipMemcpyAsync(sink->t_complete_ns + sink_row0 * un, c.d_tc_t.p, (size_t)B * un * 8, kind, s));
+    if (w.h) GS_HIP(hipMemcpyAsync(sink->hops + sink_row0 * un, c.d_hops_t.p, (size_t)B * un, kind, s));
   }
-  // stream: blocks of bm messages through one pinned staging buffer
+  const bool st_rows = sink->on_block != nullptr, st_lat = w.lat;
+  if (!st_rows && !st_lat) return;
   const uint32_t bm = std::max<uint32_t>(1, std::min<uint32_t>(sink->block_msgs ? sink->block_msgs : 64, B));
-  const size_t need = (size_t)bm * un * 9;
-  if (c.h_block_bytes < need) {
+  const size_t cell = (st_rows && w.tc ? 8 : 0) + (st_lat ? 2 : 0) + (st_rows && w.h ? 1 : 0);
+  const size_t half = ((size_t)bm * un * cell + 255) & ~(size_t)255;
+  if (c.h_block_bytes < 2 * half) {
     if (c.h_block) GS_HIP(hipHostFree(c.h_block));
     c.h_block = nullptr;
     c.h_block_bytes = 0;
-    GS_HIP(hipHostMalloc(&c.h_block, need, hipHostMallocDefault));
-    c.h_block_bytes = need;
+    GS_HIP(hipHostMalloc(&c.h_block, 2 * half, hipHostMallocDefault));
+    c.h_block_bytes = 2 * half;
   }
-  uint64_t* htc = (uint64_t*)c.h_block;
-  uint8_t* hh = (uint8_t*)(htc + (size_t)bm * un);
-  for (uint32_t q0 = 0; q0 < B; q0 += bm) {
+  for (int k = 0; k < 2; k++)
+    if (!c.blk_ev[k]) GS_HIP(hipEventCreateWithFlags(&c.blk_ev[k], hipEventDisableTiming));
+  struct Part { uint64_t* tc; uint16_t* lat; uint8_t* h; };
+  auto part = [&](int k) {  // [t_complete u64][latency u16][hops u8] of one half
+    uint8_t* p = (uint8_t*)c.h_block + (size_t)k * half;
+    Part q{nullptr, nullptr, nullptr};
+    if (st_rows && w.tc) { q.tc = (uint64_t*)p; p += (size_t)bm * un * 8; }
+    if (st_lat) { q.lat = (uint16_t*)p; p += (size_t)bm * un * 2; }
+    if (st_rows && w.h) q.h = p;
+    return q;
+  };
+  auto hand_over = [&](int k, uint32_t q0, uint32_t n) {
+    GS_HIP(hipEventSynchronize(c.blk_ev[k]));
+    const Part q = part(k);
+    if (st_rows) sink->on_block(sink->user, sink_row0 + q0, n, un, q.tc, q.h);
+    if (st_lat) sink->on_lat(sink->user, sink_row0 + q0, n, un, q.lat);
+  };
+  int prev = -1;
+  uint32_t pq0 = 0, pn = 0;
+  for (uint32_t q0 = 0, k = 0; q0 < B; q0 += bm, k ^= 1) {
     const uint32_t n = std::min(bm, B - q0);
-    if (want_tc)
-      GS_HIP(hipMemcpyAsync(htc, c.d_tc_t.p + (size_t)q0 * un, (size_t)n * un * 8, hipMemcpyDeviceToHost, s));
-    if (want_h)
-      GS_HIP(hipMemcpyAsync(hh, c.d_hops_t.p + (size_t)q0 * un, (size_t)n * un, hipMemcpyDeviceToHost, s));
-    GS_HIP(hipStreamSynchronize(s));
-    sink->on_block(sink->user, sink_row0 + q0, n, un, want_tc ? htc : nullptr, want_h ? hh : nullptr);
+    const Part q = part((int)k);
+    if (q.tc) GS_HIP(hipMemcpyAsync(q.tc, c.d_tc_t.p + (size_t)q0 * un, (size_t)n * un * 8, hipMemcpyDeviceToHost, s));
+    if (q.lat)
+      GS_HIP(hipMemcpyAsync(q.lat, c.d_lat_t.p + (size_t)q0 * un, (size_t)n * un * 2, hipMemcpyDeviceToHost, s));
+    if (q.h) GS_HIP(hipMemcpyAsync(q.h, c.d_hops_t.p + (size_t)q0 * un, (size_t)n * un, hipMemcpyDeviceToHost, s));
+    GS_HIP(hipEventRecord(c.blk_ev[k], s));
+    if (prev >= 0) hand_over(prev, pq0, pn);  // block k - 1 while block k is copied
+    prev = (int)k;
+    pq0 = q0;
+    pn = n;
   }
+  hand_over(prev, pq0, pn);
 }
 
-// Results of a completed batch (peer-major d_tc / d_hops of peers [u0, u0 + un))
-// into the sink: transposed to message-major, copied out, summaries.
+// Results of a completed batch (peer-major d_tc / d_hops / d_lat of peers
+// [u0, u0 + un)) into the sink: transposed to message-major, copied out,
+// summaries.
 static void deliver(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, const gs_result_sink* sink,
                     uint64_t sink_row0) {
   if (!sink) return;
   hipStream_t s = c.stream;
-  const uint32_t want = sink->want ? sink->want : (GS_WANT_T_COMPLETE | GS_WANT_HOPS);
-  const bool want_tc = sink->on_block ? (want & GS_WANT_T_COMPLETE) != 0 : sink->t_complete_ns != nullptr;
-  const bool want_h = sink->on_block ? (want & GS_WANT_HOPS) != 0 : sink->hops != nullptr;
-  if (want_tc || want_h) {
+  const SinkWants w = sink_wants(sink);
+  if (w.rows()) {
     c.d_tc_t.alloc((size_t)un * c.cfg.batch);
     c.d_hops_t.alloc((size_t)un * c.cfg.batch);
     dim3 tg((un + 63) / 64, (b.B + 63) / 64);
     k_transpose<<<tg, TB, 0, s>>>(c.d_tc.p, c.d_hops.p, c.d_tc_t.p, c.d_hops_t.p, un, b.B);
     GS_HIP(hipGetLastError());
-    deliver_rows(c, b.B, un, sink, sink_row0);
   }
-  if (sink->summary) fill_summary(c, b, u0, un, sink->summary + sink_row0);
+  if (w.lat) {
+    c.d_lat_t.alloc((size_t)un * c.cfg.batch);
+    dim3 tg((un + 63) / 64, (b.B + 63) / 64);
+    k_transpose16<<<tg, TB, 0, s>>>(c.d_lat.p, c.d_lat_t.p, un, b.B);
+    GS_HIP(hipGetLastError());
+    GS_HIP(hipMemcpyAsync(c.h_pinned, c.d_counters.p + C_ERR, 8, hipMemcpyDeviceToHost, s));
+    GS_HIP(hipStreamSynchronize(s));
+    if (c.h_pinned[0] & ERR_LAT16) c.fail(GS_ERANGE, "a logged latency of 65535 ms or more does not fit the u16 "
+                                                     "stream (GS_WANT_LAT_MS)");
+  }
+  if (w.rows() || w.lat) deliver_rows(c, b.B, un, sink, sink_row0);
+  if (w.summary) fill_summary(c, b, u0, un, sink->summary + sink_row0);
 }
 
 // Completion + delivery of a finished batch.
 static void launch_complete(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, const gs_result_sink* sink,
                             uint64_t sink_row0) {
   const bool hist = sink && sink->summary;
-  run_complete(c, b, u0, un, hist, hist, sink != nullptr);
+  const SinkWants w = sink_wants(sink);
+  run_complete(c, b, u0, un, hist, hist, w.rows(), w.lat);
   deliver(c, b, u0, un, sink, sink_row0);
 }
 
@@ -1383,7 +1465,8 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       reset(variant, false, false);
       const uint64_t iw0 = read_counter(c, C_GOSSIP);
       const GosRun gr{rel0[0], c.cfg.heartbeat_ns};
-      const bool dense = sink != nullptr || c.traffic || getenv("GS_LPULL_DENSE");
+      const SinkWants sw = sink_wants(sink);
+      const bool dense = sw.rows() || sw.summary || c.traffic || getenv("GS_LPULL_DENSE");
       if (!run_lpull_batch(c, bg, K, lb, ev, n_ev, dev_cus, dense, false, &gr)) return false;
       c.stats.gossip_list_batches++;
       // IWANTs taken: the next batch comes here directly (no eager run first)
@@ -1409,7 +1492,8 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
         // GS_LPULL_DENSE (diagnostic): dense rows + k_complete, whose known key
         // stream calibrates the PMC read factor (scripts/pmc_summary.py);
         // IDONTWANT batches keep their final keys dense all along
-        const bool dense = !idw_b && (sink != nullptr || c.traffic || b.FP > 1 || getenv("GS_LPULL_DENSE"));
+        const SinkWants sw = sink_wants(sink);
+        const bool dense = !idw_b && (sw.rows() || sw.summary || c.traffic || b.FP > 1 || getenv("GS_LPULL_DENSE"));
         if (!K || !run_lpull_batch(c, bw, K, lb, ev, n_ev, dev_cus, dense, idw_b)) {
           if (K && getenv("GS_REQUIRE_LPULL")) c.fail(GS_EUNSUPPORTED, "list pull overflow (GS_REQUIRE_LPULL)");
           if (idw_b) {  // k_pull has no IDONTWANT: the push path takes the batch
@@ -1427,7 +1511,7 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
         launch_complete(c, b, 0, N, sink, i0);
         done = true;
       } else {  // keep the eager result only if gossip provably changes nothing
-        run_complete(c, b, 0, N, true, sink && sink->summary, sink != nullptr);
+        run_complete(c, b, 0, N, true, sink && sink->summary, sink_wants(sink).rows(), sink_wants(sink).lat);
         std::vector<uint64_t> ms((size_t)B * MS_COLS);
         GS_HIP(hipMemcpyAsync(ms.data(), c.d_mstat.p, ms.size() * 8, hipMemcpyDeviceToHost, s));
         GS_HIP(hipStreamSynchronize(s));

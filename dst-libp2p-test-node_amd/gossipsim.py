@@ -61,14 +61,16 @@ class GsMsgSummary(ctypes.Structure):
 
 
 BLOCK_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, u64, u32, u32, P(u64), P(u8))
+LAT_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, u64, u32, u32, P(ctypes.c_uint16))
 
 
 class GsResultSink(ctypes.Structure):
     _fields_ = [("t_complete_ns", P(u64)), ("hops", P(u8)), ("on_block", BLOCK_FN), ("user", ctypes.c_void_p),
-                ("block_msgs", u32), ("want", u32), ("summary", P(GsMsgSummary))]
+                ("block_msgs", u32), ("want", u32), ("summary", P(GsMsgSummary)), ("on_lat", LAT_FN)]
 
 
-WANT_T_COMPLETE, WANT_HOPS = 1, 2  # gs_result_sink.want (GS_WANT_*)
+WANT_T_COMPLETE, WANT_HOPS, WANT_LAT_MS = 1, 2, 4  # gs_result_sink.want (GS_WANT_*)
+LAT_NONE = 0xFFFF  # GS_LAT_NONE: the peer logs nothing for the message
 
 
 class GsStats(ctypes.Structure):
@@ -97,6 +99,7 @@ SIGNATURES = {
     "gs_write_node_log": (i32, [P(GsConfig), ctypes.c_char_p, P(GsPublish), u64, P(u64)]),
     "gs_log_open": (i32, [P(GsConfig), ctypes.c_char_p, P(ctypes.c_void_p)]),
     "gs_log_write": (i32, [ctypes.c_void_p, P(GsPublish), u32, P(u64)]),
+    "gs_log_write_lat": (i32, [ctypes.c_void_p, P(GsPublish), u32, P(ctypes.c_uint16)]),
     "gs_log_close": (i32, [ctypes.c_void_p]),
     "gs_config_from_env": (i32, [P(GsConfig), ctypes.c_char_p, ctypes.c_size_t]),
     "gs_wire_bytes": (u64, [u64, u32, u32]),
@@ -485,19 +488,32 @@ class Simulator:
         return schedule
 
     def run(self, schedule=None, collect=True, summary=False, on_block=None, block_msgs=0,
-            want=WANT_T_COMPLETE | WANT_HOPS):
+            want=WANT_T_COMPLETE | WANT_HOPS, on_lat=None):
         """Simulate the queued publishes (or `schedule`); returns t_complete/hops [M, N].
 
         summary: also return the device's per-message latency reductions
         (gs_msg_summary: delivered, lat_sum_ms, p50/p95/max ms, 100 ms histogram).
         on_block(first_msg, t_complete[n, N], hops[n, N]): stream the results in
         blocks of `block_msgs` messages instead of returning [M, N] arrays;
-        `want` (WANT_* bits) selects which of the two it receives (None if not)."""
+        `want` (WANT_* bits) selects which of the two it receives (None if not).
+        on_lat(first_msg, lat_ms[n, N] uint16): the logged latency stream
+        (GS_WANT_LAT_MS: (t_complete - tx_time) // 1e6 as main.rs:93 logs it,
+        LAT_NONE where nothing is logged), in the same blocks; it may be used
+        alone or beside on_block."""
         schedule = self._schedule(schedule)
         M = len(schedule)
         res = {"schedule": schedule}
         sink = GsResultSink()
         keep = []
+        if on_lat is not None:
+            def _lcb(user, first, n, peers, lat):
+                on_lat(int(first), np.ctypeslib.as_array(lat, (n, peers)))
+
+            lcb = LAT_FN(_lcb)
+            keep.append(lcb)
+            sink.on_lat = lcb
+            sink.block_msgs = block_msgs
+            sink.want = WANT_LAT_MS | (want & (WANT_T_COMPLETE | WANT_HOPS) if on_block is not None else 0)
         if on_block is not None:
             N = self.peers
 
@@ -508,10 +524,10 @@ class Simulator:
 
             cb = BLOCK_FN(_cb)
             keep.append(cb)
-            sink.want = want
+            sink.want = want | (WANT_LAT_MS if on_lat is not None else 0)
             sink.on_block = cb
             sink.block_msgs = block_msgs
-        elif collect:
+        elif collect and on_lat is None:
             tc = np.zeros(M * self.peers, np.uint64)
             hops = np.zeros(M * self.peers, np.uint8)
             sink.t_complete_ns = _ptr(tc, u64)
@@ -522,7 +538,7 @@ class Simulator:
             sm = (GsMsgSummary * M)()
             sink.summary = ctypes.cast(sm, P(GsMsgSummary))
             keep.append(sm)
-        use_sink = on_block is not None or collect or summary
+        use_sink = on_block is not None or on_lat is not None or collect or summary
         self._check(lib().gs_run(self.ctx, schedule, M, ctypes.byref(sink) if use_sink else None))
         if summary:
             res["summary"] = {
@@ -634,6 +650,15 @@ class LogStream:
         rc = lib().gs_log_write(self.h, rows, n, _ptr(tc, u64))
         if rc:
             raise GossipSimError(rc, "gs_log_write failed")
+
+    def write_lat(self, sched_rows, lat_ms):
+        """The same lines from a block of the u16 latency stream (run(on_lat=...))."""
+        lat = np.ascontiguousarray(lat_ms, np.uint16)
+        n = lat.shape[0]
+        rows = (GsPublish * n)(*sched_rows[:n]) if not isinstance(sched_rows, ctypes.Array) else sched_rows
+        rc = lib().gs_log_write_lat(self.h, rows, n, _ptr(lat, ctypes.c_uint16))
+        if rc:
+            raise GossipSimError(rc, "gs_log_write_lat failed")
 
     def close(self):
         if self.h:

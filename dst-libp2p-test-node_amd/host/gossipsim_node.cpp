@@ -30,29 +30,26 @@ void usage() {
           "     GS_DEVICE\n");
 }
 
-// Results arrive in message-major blocks (gs_result_sink.on_block): the log is
-// streamed through gs_log_* and the latencies folded into a 1 ms histogram, so
-// no [messages][peers] host array is held.
+// Results arrive as the logged latency, message-major blocks of u16 ms
+// (gs_result_sink.on_lat, GS_WANT_LAT_MS: 2 bytes per (peer, message), the
+// value main.rs:93 prints): the log is streamed through gs_log_write_lat and
+// the latencies folded into a 1 ms histogram, so no [messages][peers] host
+// array is held.
 struct Stream {
   gs_log* log = nullptr;
   const gs_publish* sched = nullptr;
-  uint32_t self_log = 0;
   gs_status st = GS_OK;
   std::vector<uint64_t> hist_ms;
 };
 
-void on_block(void* user, uint64_t first, uint32_t n, uint32_t peers, const uint64_t* tc, const uint8_t*) {
+void on_lat(void* user, uint64_t first, uint32_t n, uint32_t peers, const uint16_t* lat) {
   Stream* S = (Stream*)user;
-  if (S->log && S->st == GS_OK) S->st = gs_log_write(S->log, S->sched + first, n, tc);
-  for (uint32_t m = 0; m < n; m++) {
-    const gs_publish& p = S->sched[first + m];
-    for (uint32_t u = 0; u < peers; u++) {
-      const uint64_t t = tc[(size_t)m * peers + u];
-      if (t == GS_UNDELIVERED || (u == p.publisher && !S->self_log)) continue;
-      const uint64_t ms = (t - p.t_pub_ns) / 1000000ull;
-      if (ms >= S->hist_ms.size()) S->hist_ms.resize(ms + 1, 0);
-      S->hist_ms[ms]++;
-    }
+  if (S->log && S->st == GS_OK) S->st = gs_log_write_lat(S->log, S->sched + first, n, lat);
+  for (size_t i = 0; i < (size_t)n * peers; i++) {
+    const uint16_t ms = lat[i];
+    if (ms == GS_LAT_NONE) continue;  // undelivered, or the publisher without SELFTRIGGER
+    if (ms >= S->hist_ms.size()) S->hist_ms.resize((size_t)ms + 1, 0);
+    S->hist_ms[ms]++;
   }
 }
 
@@ -176,12 +173,11 @@ int main(int argc, char** argv) {
   }
   Stream strm;
   strm.sched = sched.data();
-  strm.self_log = cfg.self_log;
   if (!latencies.empty() && (st = gs_log_open(&cfg, latencies.c_str(), &strm.log)) != GS_OK)
     return die(ctx, st, "gs_log_open");
   gs_result_sink sink{};
-  sink.want = GS_WANT_T_COMPLETE;  // streamed through on_block
-  sink.on_block = on_block;
+  sink.want = GS_WANT_LAT_MS;  // the logged latency, streamed through on_lat
+  sink.on_lat = on_lat;
   sink.user = &strm;
   sink.block_msgs = 16;
   if ((st = gs_run(ctx, sched.data(), n_msgs, &sink)) != GS_OK) return die(ctx, st, "gs_run");

@@ -145,8 +145,18 @@ typedef struct gs_msg_summary {
 typedef void (*gs_block_fn)(void* user, uint64_t first_msg, uint32_t n_msgs, uint32_t peers,
                             const uint64_t* t_complete_ns, const uint8_t* hops);
 
-/* Outputs an on_block sink streams (gs_result_sink.want). */
-enum { GS_WANT_T_COMPLETE = 1u, GS_WANT_HOPS = 2u };
+/* Streaming receiver of the logged latency (GS_WANT_LAT_MS, ABI 9): the
+ * value each peer's log line carries, (t_complete - tx_time) / 1e6 truncated
+ * (rust-test-node/src/main.rs:91-93), message-major [n_msgs][peers] u16;
+ * GS_LAT_NONE where the peer logs nothing (undelivered; the publisher unless
+ * cfg.self_log). 2 bytes per (peer, message) instead of the 9 of
+ * t_complete + hops. A latency of 65535 ms or more fails the run (GS_ERANGE). */
+typedef void (*gs_lat_fn)(void* user, uint64_t first_msg, uint32_t n_msgs, uint32_t peers, const uint16_t* lat_ms);
+#define GS_LAT_NONE 0xFFFFu
+
+/* Outputs a streaming sink delivers (gs_result_sink.want): t_complete and
+ * hops through on_block, the logged latency through on_lat. */
+enum { GS_WANT_T_COMPLETE = 1u, GS_WANT_HOPS = 2u, GS_WANT_LAT_MS = 4u };
 
 /* Where gs_run puts results. Every member may be NULL / 0.
  *  - t_complete_ns / hops: caller arrays, message-major [n_msgs][peers];
@@ -156,15 +166,20 @@ enum { GS_WANT_T_COMPLETE = 1u, GS_WANT_HOPS = 2u };
  *    host array is needed for large N); `want` selects what it receives
  *    (GS_WANT_* bits, 0 = both); ABI 7 (ABI 6 used non-NULL array pointers
  *    as the selection flags);
- *  - summary: [n_msgs] per-message latency reductions. */
+ *  - summary: [n_msgs] per-message latency reductions;
+ *  - on_lat: the logged latency in ms, u16, streamed in the same blocks; set
+ *    iff want has GS_WANT_LAT_MS (ABI 9). gs_run only (gs_run_partitioned
+ *    returns GS_EUNSUPPORTED). */
 typedef struct gs_result_sink {
     uint64_t* t_complete_ns;  /* completion time of message m at peer u (GS_UNDELIVERED if never) */
     uint8_t*  hops;           /* hop count of the completing fragment (0 at the publisher)        */
     gs_block_fn on_block;
     void*     user;
     uint32_t  block_msgs;     /* messages per on_block call; 0 = 64                               */
-    uint32_t  want;           /* on_block only: GS_WANT_T_COMPLETE | GS_WANT_HOPS; 0 = both       */
+    uint32_t  want;           /* GS_WANT_T_COMPLETE | GS_WANT_HOPS (on_block; neither = both)     */
+                              /* | GS_WANT_LAT_MS (on_lat)                                        */
     gs_msg_summary* summary;
+    gs_lat_fn on_lat;         /* ABI 9: the logged latency stream (GS_WANT_LAT_MS)                */
 } gs_result_sink;
 
 /* Counters accumulated since gs_create / gs_reset_stats. */
@@ -304,6 +319,9 @@ typedef struct gs_log gs_log;
 gs_status gs_log_open(const gs_config* cfg, const char* path, gs_log** out);
 /* sched = the block's n_msgs schedule rows, t_complete_ns = [n_msgs][peers]. */
 gs_status gs_log_write(gs_log* log, const gs_publish* sched, uint32_t n_msgs, const uint64_t* t_complete_ns);
+/* The same from the u16 latency stream (gs_result_sink.on_lat, ABI 9):
+ * lat_ms = [n_msgs][peers], GS_LAT_NONE where no line is written. */
+gs_status gs_log_write_lat(gs_log* log, const gs_publish* sched, uint32_t n_msgs, const uint16_t* lat_ms);
 gs_status gs_log_close(gs_log* log);
 
 /* Packets and header bytes of one fragment send in the same model as

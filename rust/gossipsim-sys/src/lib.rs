@@ -42,13 +42,17 @@ pub struct gs_msg_summary {
 }
 pub type gs_block_fn = Option<unsafe extern "C" fn(user: *mut c_void, first_msg: u64, n_msgs: u32, peers: u32,
                                                    t_complete_ns: *const u64, hops: *const u8)>;
+pub type gs_lat_fn = Option<unsafe extern "C" fn(user: *mut c_void, first_msg: u64, n_msgs: u32, peers: u32,
+                                                 lat_ms: *const u16)>;
 #[repr(C)]
 pub struct gs_result_sink {
     pub t_complete_ns: *mut u64, pub hops: *mut u8, pub on_block: gs_block_fn, pub user: *mut c_void,
-    pub block_msgs: u32, pub want: u32, pub summary: *mut gs_msg_summary,
+    pub block_msgs: u32, pub want: u32, pub summary: *mut gs_msg_summary, pub on_lat: gs_lat_fn,
 }
 pub const GS_WANT_T_COMPLETE: u32 = 1;
 pub const GS_WANT_HOPS: u32 = 2;
+pub const GS_WANT_LAT_MS: u32 = 4;
+pub const GS_LAT_NONE: u16 = 0xFFFF;
 #[repr(C)] #[derive(Default)]
 pub struct gs_stats {
     pub messages: u64, pub deliveries: u64, pub frag_deliveries: u64, pub relaxations: u64,
@@ -94,6 +98,8 @@ extern "C" {
     pub fn gs_log_open(cfg: *const gs_config, path: *const c_char, out: *mut *mut gs_log) -> gs_status;
     pub fn gs_log_write(log: *mut gs_log, sched: *const gs_publish, n_msgs: u32, t_complete_ns: *const u64)
                         -> gs_status;
+    pub fn gs_log_write_lat(log: *mut gs_log, sched: *const gs_publish, n_msgs: u32, lat_ms: *const u16)
+                            -> gs_status;
     pub fn gs_log_close(log: *mut gs_log) -> gs_status;
     pub fn gs_write_shadow_heartbeat(path: *const c_char, peers: u32, traffic: *const u64, sim_seconds: u64)
                                      -> gs_status;

@@ -183,6 +183,74 @@ def test_streaming_sink_want_bits():
     assert rc == gossipsim.GS_EINVAL and b"want" in lib.gs_last_error(sim.ctx)
 
 
+def _logged_ms(tc, sched, self_log):
+    """The oracle side of GS_WANT_LAT_MS: (t_complete - tx_time) // 1e6 where a
+    line is logged (main.rs:91-93), LAT_NONE elsewhere."""
+    tx = np.asarray(sched[0], np.uint64)[:, None]
+    ok = tc != UND
+    if not self_log:
+        ok[np.arange(tc.shape[0]), np.asarray(sched[1])] = False
+    out = np.full(tc.shape, gossipsim.LAT_NONE, np.uint16)
+    out[ok] = ((tc - tx) // np.uint64(1_000_000))[ok].astype(np.uint16)
+    return out
+
+
+@pytest.mark.parametrize("case", ["rust", "nim_self_log", "churn", "frags3", "gossip_370"])
+@pytest.mark.parametrize("with_rows", [False, True])
+def test_latency_ms_stream(case, with_rows):
+    """ABI 9's u16 latency stream (gs_result_sink.on_lat, GS_WANT_LAT_MS):
+    exactly the ms each peer's log line carries (main.rs:91-93), GS_LAT_NONE
+    for the undelivered and the publisher (unless SELFTRIGGER), against the
+    oracle; alone (the list pass's final logs, k_lcomplete) and beside the
+    t_complete / hops stream (dense rows, k_complete)."""
+    N, M = 1400, 20
+    kw = dict(peers=N, seed=98)
+    if case == "churn":
+        kw.update(churn_ppm=30000, hb_phase_ns=gossipsim.SHADOW_START_NS)
+    elif case == "frags3":
+        kw.update(fragments=3)
+    elif case == "gossip_370":
+        kw.update(hb_phase_ns=(T0 + 370_000_000) % 1_000_000_000)
+    p = oracle.params_for("nim", **kw) if case == "nim_self_log" else oracle.params(**kw)
+    sched = _sched(M, N)
+    ref = oracle.simulate(p, 5, (50, 150, 40, 130), sched=sched)
+    sim, _ = gpu_sim(p, 5, (50, 150, 40, 130), batch=8)
+    lat, rows = {}, {}
+
+    def on_lat(first, v):
+        lat[first] = v.copy()
+
+    def on_block(first, tc, hp):
+        rows[first] = tc.copy()
+
+    sim.run(sched, on_lat=on_lat, on_block=on_block if with_rows else None, block_msgs=6,
+            want=gossipsim.WANT_T_COMPLETE)
+    assert sorted(lat) == [0, 6, 12, 16]  # blocks of 6 within batches of 8
+    got = np.concatenate([lat[k] for k in sorted(lat)])
+    np.testing.assert_array_equal(got, _logged_ms(ref["t_complete"], sched, p.self_log))
+    if with_rows:
+        np.testing.assert_array_equal(np.concatenate([rows[k] for k in sorted(rows)]), ref["t_complete"])
+    st = sim.stats()
+    assert st["deliveries"] == ref["stats"]["deliveries"]
+
+
+def test_latency_ms_stream_writes_the_log(tmp_path):
+    """gs_log_write_lat over the u16 stream writes the same lines as the
+    grouped writer over t_complete (the C++ CLI streams this way)."""
+    N, M = 900, 10
+    p = oracle.params(peers=N, seed=99)
+    sched = _sched(M, N)
+    sim, _ = gpu_sim(p, 5, (50, 150, 40, 130), batch=8)
+    whole = sim.run(sched)
+    a, b = tmp_path / "grouped", tmp_path / "stream"
+    sim.write_latency_log(str(a), whole)
+    log = gossipsim.LogStream(sim.cfg, str(b))
+    rows = sim._schedule(sched)
+    sim.run(sched, on_lat=lambda first, v: log.write_lat(rows[first:first + v.shape[0]], v), block_msgs=4)
+    log.close()
+    assert sorted(open(a).read().splitlines()) == sorted(open(b).read().splitlines())
+
+
 def test_shadow_parity_harness_end_to_end(tmp_path):
     """shadow_parity.py end to end on the GPU: a synthetic Shadow `latencies1`
     (an oracle run written in the grep format run.sh:61 produces) -> schedule

@@ -478,3 +478,102 @@ def test_load_state_rejects_foreign_files(tmp_path):
     assert lib.gs_load_state(str(short).encode(), 0, ctypes.byref(out)) == gossipsim.GS_EINVAL
     assert lib.gs_load_state(str(tmp_path / "missing").encode(), 0, ctypes.byref(out)) == gossipsim.GS_EINVAL
     assert not out.value
+
+
+LAYOUT_CHECK = r"""
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include "gs_layout.h"
+using namespace gs;
+static uint64_t code(uint64_t m, uint64_t u) { return (m << 32) | u; }
+int main() {
+  const uint32_t Ns[] = {7, 97, 1000, 4099};
+  const uint32_t Bs[] = {1, 2, 3, 5, 16, 17, 1024};
+  unsigned long long checks = 0;
+  for (uint32_t P = 1; P <= 8; P++)
+    for (uint32_t N : Ns)
+      for (uint32_t B : Bs) {
+        if (P > N) continue;
+        const PartLayout L{P, N, B};
+        // peers and messages: contiguous covers
+        if (L.u0(0) != 0 || L.u0(P) != N || L.m0(0) != 0 || L.m0(P) != B) { puts("cover"); return 1; }
+        for (uint32_t p = 0; p < P; p++)
+          if (L.u0(p + 1) < L.u0(p) || L.m0(p + 1) < L.m0(p) || L.mn(p) > L.mmax()) { puts("order"); return 1; }
+        // message-sharded all-to-all, RCCL form: pack per destination, one send / recv per pair
+        std::vector<std::vector<uint64_t>> res(P), send(P), recv(P), loop(P);
+        for (uint32_t s = 0; s < P; s++) {
+          res[s].resize((size_t)L.mn(s) * N);
+          for (uint32_t i = 0; i < L.mn(s); i++)
+            for (uint32_t u = 0; u < N; u++) res[s][(size_t)i * N + u] = code(L.m0(s) + i, u);
+          send[s].assign((size_t)L.mn(s) * N, ~0ull);
+          uint64_t packed = 0;
+          for (uint32_t d = 0; d < P; d++) {
+            if (L.ms_send_off(s, d) != packed) { puts("send tiling"); return 1; }
+            for (uint32_t i = 0; i < L.mn(s); i++)
+              for (uint32_t j = 0; j < L.un(d); j++)
+                send[s][L.ms_send_off(s, d) + (size_t)i * L.un(d) + j] = res[s][(size_t)i * N + L.u0(d) + j];
+            packed += L.ms_count(s, d);
+          }
+          if (packed != (uint64_t)L.mn(s) * N) { puts("send size"); return 1; }
+        }
+        for (uint32_t d = 0; d < P; d++) {
+          recv[d].assign((size_t)B * L.un(d), ~0ull);
+          loop[d].assign((size_t)B * L.un(d), ~0ull);
+          uint64_t got = 0;
+          for (uint32_t s = 0; s < P; s++) {
+            if (L.ms_recv_off(s, d) != got) { puts("recv tiling"); return 1; }
+            for (uint64_t k = 0; k < L.ms_count(s, d); k++)
+              recv[d][L.ms_recv_off(s, d) + k] = send[s][L.ms_send_off(s, d) + k];
+            // loop-back form: a 2-D copy straight from s's rows
+            for (uint32_t i = 0; i < L.mn(s); i++)
+              for (uint32_t j = 0; j < L.un(d); j++)
+                loop[d][L.ms_recv_off(s, d) + (size_t)i * L.un(d) + j] = res[s][(size_t)i * N + L.u0(d) + j];
+            got += L.ms_count(s, d);
+          }
+          if (got != (uint64_t)B * L.un(d)) { puts("recv size"); return 1; }
+          for (uint32_t m = 0; m < B; m++)
+            for (uint32_t j = 0; j < L.un(d); j++) {
+              const uint64_t want = code(m, L.u0(d) + j);
+              if (recv[d][(size_t)m * L.un(d) + j] != want || loop[d][(size_t)m * L.un(d) + j] != want) {
+                printf("ms P=%u N=%u B=%u d=%u m=%u j=%u\n", P, N, B, d, m, j);
+                return 1;
+              }
+              checks++;
+            }
+        }
+        // list-pass record exchange: part p's records at base[p] of every gathered buffer
+        std::vector<uint64_t> cnt(P), base(P + 1);
+        for (uint32_t p = 0; p < P; p++) cnt[p] = (p * 7919u + N + B) % 13;
+        const uint64_t tot = lp_bases(cnt.data(), P, base.data());
+        std::vector<uint64_t> all(tot, ~0ull);
+        for (uint32_t p = 0; p < P; p++)
+          for (uint64_t k = 0; k < cnt[p]; k++) all[base[p] + k] = code(p, k);
+        uint64_t q = 0;
+        for (uint32_t p = 0; p < P; p++)
+          for (uint64_t k = 0; k < cnt[p]; k++, q++)
+            if (all[q] != code(p, k)) { puts("records"); return 1; }
+      }
+  printf("ok %llu\n", checks);
+  return 0;
+}
+"""
+
+
+def test_partition_layout_exchanges(tmp_path):
+    """gs_run_partitioned's block arithmetic (csrc/gs_layout.h, used by both
+    the loop-back and the RCCL branches of gs_comm.hip): for P = 1..8 with
+    uneven peer splits and batches smaller than P, the message-sharded
+    all-to-all (pack per destination, one send / recv per pair, and the
+    loop-back 2-D copies) hands every part exactly its peers' rows of every
+    message, and the list pass's packed records tile the gathered buffer.
+    RCCL with more than one rank never ran here (one GPU per box); this pins
+    its offsets on the CPU."""
+    src = tmp_path / "layout.cpp"
+    src.write_text(LAYOUT_CHECK)
+    exe = tmp_path / "layout"
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-I", os.path.join(ROOT, "dst-libp2p-test-node_amd", "csrc"),
+                           str(src), "-o", str(exe)])
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout
+    assert out.stdout.startswith("ok ") and int(out.stdout.split()[1]) > 100000

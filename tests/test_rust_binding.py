@@ -15,8 +15,9 @@ STRUCTS = ["gs_config", "gs_publish", "gs_msg_summary", "gs_result_sink", "gs_st
            "gs_part_record"]
 
 C_TYPES = {"uint64_t": "u64", "uint32_t": "u32", "int32_t": "i32", "uint8_t": "u8", "double": "f64",
-           "gs_block_fn": "fnptr"}
-R_TYPES = {"u64": "u64", "u32": "u32", "i32": "i32", "u8": "u8", "f64": "f64", "gs_block_fn": "fnptr"}
+           "gs_block_fn": "fnptr", "gs_lat_fn": "fnptr"}
+R_TYPES = {"u64": "u64", "u32": "u32", "i32": "i32", "u8": "u8", "f64": "f64", "gs_block_fn": "fnptr",
+           "gs_lat_fn": "fnptr"}
 
 
 def _strip_c(src):
