@@ -110,18 +110,18 @@ struct LPullArgs {
   const uint64_t* habs0;      // [B] absolute index of each message's heartbeat 0
 };
 
-// gctl words (k_lctl writes them between passes; k_gsend / k_lpull only read,
-// except GC_TLAST, which the passes raise with atomicMax)
+// gctl words (k_lctl writes them between passes; k_gsend / k_lpull only read)
 enum : uint32_t {
   GC_FD0 = 0,    // counters[C_FD] at the start of the batch
-  GC_TLAST = 1,  // largest final key time so far (relative ns)
+  GC_TLAST = 1,  // bound on the latest final time: the end of the last window that finalised a lane
   GC_E = 2,      // end of the last emitted window
   GC_DONE = 3,   // the batch's passes are over
   GC_GB = 4,     // next heartbeat whose senders are not yet known final
   GC_BK = 5,     // heartbeat + 1 whose sender planes are built (0: none)
   GC_BUILD = 6,  // heartbeat + 1 to build before this pass (0: none)
   GC_GW = 7,     // this pass's window holds IHAVE arrivals of heartbeat GC_BK - 1
-  GC_WORDS = 8
+  GC_FDP = 8,    // counters[C_FD] at the previous decision
+  GC_WORDS = 9
 };
 constexpr uint32_t GSE_HOPS = 58;  // entry bits [0, 58): target mask over the sender's CSR row
 
@@ -335,7 +335,7 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     gw = a.gctl[GC_GW] != 0;
     gR = a.grel0 + (a.gctl[GC_BK] - 1) * a.ghb;
   }
-  uint64_t niw = 0, tfin = 0;  // IWANTs sent; largest final time of the pass
+  uint64_t niw = 0;  // IWANTs sent
 
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint64_t* CW = Ls.cw[wv];
@@ -441,31 +441,34 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
         uint64_t BASE[NG], RO[NG];
         uint32_t maxn = 0;
 #pragma unroll
+        // wave-uniform and branch-free (a missing neighbour has NN = 0): with
+        // the assignments under `if (cmk)` the compiler kept the descriptors of
+        // neighbours 1-3 in VGPRs and wrapped each of their buffer loads in a
+        // readfirstlane waterfall loop (35 -> 11 v_readfirstlane, 118 -> 110
+        // VGPRs for k_lpull<1, 16>)
         for (int k = 0; k < (int)NG; k++) {
-          U[k] = 0; R4[k] = 0; NN[k] = 0; SER[k] = 0; BASE[k] = 0; RO[k] = 0; ltm[k] = 0;
-          if (cmk) {  // wave-uniform
-            const int j = __builtin_ctzll(cmk);
-            cmk &= cmk - 1;
-            const uint32_t e = __builtin_amdgcn_readlane(ej, j);
-            U[k] = e & 0xFFFFFFu;
-            if constexpr (PART)
-              RO[k] = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(ro >> 32), j) << 32) |
-                      __builtin_amdgcn_readlane((uint32_t)ro, j);
-            else
-              RO[k] = (uint64_t)U[k] * LL;
-            R4[k] = __builtin_amdgcn_readlane(rj, j);
-            ltm[k] = (1u << R4[k]) - 1u;
-            NN[k] = __builtin_amdgcn_readlane(cj, j);
-            const uint32_t su = e >> STAGE_SHIFT;
-            SER[k] = sup[su];
-            // the candidate key less its record-dependent parts: (arrival base
-            // << tshift) + (hops 1 | src); a record adds (start offset + FIFO
-            // position * ser) << tshift and its hops << sb (no carries: the low
-            // fields stay below 2^tshift, the sender checked the time field)
-            BASE[k] = ((lo + lat[su * S + sw] + (sd > SER[k] ? sd - SER[k] : 0)) << a.tshift) +
-                      ((1ull << a.sb) | U[k]);
-            maxn = NN[k] > maxn ? NN[k] : maxn;
-          }
+          const uint64_t bit = cmk & (~cmk + 1);
+          cmk ^= bit;
+          const int j = bit ? (int)__builtin_ctzll(bit) : 0;
+          const uint32_t e = __builtin_amdgcn_readlane(ej, j);
+          U[k] = e & 0xFFFFFFu;
+          if constexpr (PART)
+            RO[k] = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(ro >> 32), j) << 32) |
+                    __builtin_amdgcn_readlane((uint32_t)ro, j);
+          else
+            RO[k] = (uint64_t)U[k] * LL;
+          R4[k] = __builtin_amdgcn_readlane(rj, j);
+          ltm[k] = (1u << R4[k]) - 1u;
+          NN[k] = bit ? (uint32_t)__builtin_amdgcn_readlane(cj, j) : 0u;
+          const uint32_t su0 = e >> STAGE_SHIFT, su = su0 < S ? su0 : 0u;  // a missing neighbour's EMPTY: class 0
+          SER[k] = sup[su];
+          // the candidate key less its record-dependent parts: (arrival base
+          // << tshift) + (hops 1 | src); a record adds (start offset + FIFO
+          // position * ser) << tshift and its hops << sb (no carries: the low
+          // fields stay below 2^tshift, the sender checked the time field)
+          BASE[k] = ((lo + lat[su * S + sw] + (sd > SER[k] ? sd - SER[k] : 0)) << a.tshift) +
+                    ((1ull << a.sb) | U[k]);
+          maxn = NN[k] > maxn ? NN[k] : maxn;
         }
         __amdgpu_buffer_rsrc_t RS[NG];  // wave-uniform: base = the neighbour's records, NN[k] of them
 #pragma unroll
@@ -671,7 +674,6 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
         if (act) {
           fd++;
           nr += n;
-          if constexpr (GOS) tfin = (x >> a.tshift) > tfin ? (x >> a.tshift) : tfin;
           if (n && hp + 1 >= (1u << HOP_BITS)) err |= ERR_HOPS;
           if (start - wlo >= (1ull << 32) || (n && start + a.rmax > a.tmax)) err |= ERR_TIME;
         }
@@ -740,14 +742,7 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
   }
   if constexpr (GOS) {
     niw = wave_sum(niw);
-    for (int off = 32; off > 0; off >>= 1) {
-      const uint64_t y = __shfl_xor(tfin, off);
-      tfin = y > tfin ? y : tfin;
-    }
-    if (lane == 0) {
-      if (niw) atomicAdd((unsigned long long*)&a.counters[C_GOSSIP], (unsigned long long)niw);
-      atomicMax((unsigned long long*)&a.gctl[GC_TLAST], (unsigned long long)tfin);
-    }
+    if (lane == 0 && niw) atomicAdd((unsigned long long*)&a.counters[C_GOSSIP], (unsigned long long)niw);
   }
 }
 
@@ -766,7 +761,12 @@ __global__ void k_lctl(LPullArgs a) {
   uint64_t* me = a.ctrl + (a.pass % 3) * 4;
   uint64_t* nx = a.ctrl + ((a.pass + 1) % 3) * 4;
   const uint64_t D = a.delta, hb = a.ghb, r0 = a.grel0;
-  const uint64_t nf = a.gnf - (a.counters[C_FD] - g[GC_FD0]);  // lanes not final yet
+  const uint64_t fd = a.counters[C_FD];
+  const uint64_t nf = a.gnf - (fd - g[GC_FD0]);  // lanes not final yet
+  if (fd != g[GC_FDP]) {  // the last pass finalised lanes: all before the end of its window
+    g[GC_TLAST] = g[GC_E];
+    g[GC_FDP] = fd;
+  }
   const uint64_t tl = g[GC_TLAST];
   const uint64_t kmax = (tl <= r0 ? 0 : (tl - r0 + hb - 1) / hb) + a.ghist - 1;  // last heartbeat with a sender
   const bool gos = nf && a.ghist;

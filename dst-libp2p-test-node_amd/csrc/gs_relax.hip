@@ -1066,6 +1066,7 @@ static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvF
     GS_HIP(hipMemsetAsync(c.d_rowdone.p, 0, ((size_t)N + 31) / 32 * 4, s));
     GS_HIP(hipMemsetAsync(c.d_gctl.p, 0, GC_WORDS * 8, s));
     GS_HIP(hipMemcpyAsync(c.d_gctl.p + GC_FD0, c.d_counters.p + C_FD, 8, hipMemcpyDeviceToDevice, s));
+    GS_HIP(hipMemcpyAsync(c.d_gctl.p + GC_FDP, c.d_counters.p + C_FD, 8, hipMemcpyDeviceToDevice, s));
     la.grel0 = gos->rel0;
     la.ghb = gos->hb;
     la.glat_min = b.lat_min;
