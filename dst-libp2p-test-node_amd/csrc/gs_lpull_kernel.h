@@ -714,7 +714,11 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     }
     if (lane == 0) wcnt[w] = ecnt;
     nrec += ecnt;
-    // 6. LDS back to INF for the next row: the touched chunks
+    // 6. LDS back to INF for the next row: the touched chunks. cb passes
+    //    through an empty asm so that the chunk tests are recomputed here from
+    //    the scalar word (else the compiler keeps step 3's 16 chunk masks alive
+    //    across the row: 32 SGPR spills to VGPR lanes and back per row)
+    asm volatile("" : "+s"(cb));
 #pragma unroll
     for (int q = 0; q < (int)CH; q++)
       if ((cb >> q) & 1u) CW[q * 64 + lane] = INF64;
