@@ -746,7 +746,7 @@ static void launch_complete(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, co
                             uint64_t sink_row0) {
   const bool hist = sink && sink->summary;
   const SinkWants w = sink_wants(sink);
-  run_complete(c, b, u0, un, hist, hist, w.rows(), w.lat);
+  run_complete(c, b, u0, un, hist, hist, w.rows() || w.summary, w.lat);  // k_pct reads d_tc
   deliver(c, b, u0, un, sink, sink_row0);
 }
 
@@ -1464,14 +1464,11 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       const uint32_t K = lpull_ring(c, bg, bg.delta / ggr * ggr, &lb, true);
       if (!K) return false;
       reset(variant, false, false);
-      const uint64_t iw0 = read_counter(c, C_GOSSIP);
       const GosRun gr{rel0[0], c.cfg.heartbeat_ns};
       const SinkWants sw = sink_wants(sink);
       const bool dense = sw.rows() || sw.summary || c.traffic || getenv("GS_LPULL_DENSE");
       if (!run_lpull_batch(c, bg, K, lb, ev, n_ev, dev_cus, dense, false, &gr)) return false;
       c.stats.gossip_list_batches++;
-      // IWANTs taken: the next batch comes here directly (no eager run first)
-      c.glp_prefer = read_counter(c, C_GOSSIP) != iw0;
       if (c.traffic) launch_traffic(c, b);
       launch_complete(c, b, 0, N, sink, i0);
       return true;
@@ -1512,7 +1509,8 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
         launch_complete(c, b, 0, N, sink, i0);
         done = true;
       } else {  // keep the eager result only if gossip provably changes nothing
-        run_complete(c, b, 0, N, true, sink && sink->summary, sink_wants(sink).rows(), sink_wants(sink).lat);
+        const SinkWants sw = sink_wants(sink);
+        run_complete(c, b, 0, N, true, sw.summary, sw.rows() || sw.summary, sw.lat);
         std::vector<uint64_t> ms((size_t)B * MS_COLS);
         GS_HIP(hipMemcpyAsync(ms.data(), c.d_mstat.p, ms.size() * 8, hipMemcpyDeviceToHost, s));
         GS_HIP(hipStreamSynchronize(s));
@@ -1524,8 +1522,8 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
         } else {  // gossip can change this batch: discard the eager run's counters
           GS_HIP(hipMemcpyAsync(c.d_counters.p, c.d_cnt_save.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));
           c.stats.gossip_fallback_batches++;
-          if (glp && !glp_tried) {  // re-run with the gossip inside the passes
-            c.glp_prefer = true;
+          if (glp && !glp_tried) {  // re-run with the gossip inside the passes; the context's
+            c.glp_prefer = true;      // later batches go there directly (no eager run first)
             done = run_glp();
           }
         }

@@ -225,7 +225,7 @@ def test_latency_ms_stream(case, with_rows):
 
     sim.run(sched, on_lat=on_lat, on_block=on_block if with_rows else None, block_msgs=6,
             want=gossipsim.WANT_T_COMPLETE)
-    assert sorted(lat) == [0, 6, 12, 16]  # blocks of 6 within batches of 8
+    assert sorted(lat) == [0, 6, 8, 14, 16]  # blocks of 6 inside each batch of 8
     got = np.concatenate([lat[k] for k in sorted(lat)])
     np.testing.assert_array_equal(got, _logged_ms(ref["t_complete"], sched, p.self_log))
     if with_rows:
