@@ -275,10 +275,16 @@ __device__ __forceinline__ void glp_ihave(const LPullArgs& a, uint64_t* CW, uint
 
 // Record step: groups of NG = 4 neighbours, RCH = 2 chunks of 64 records each
 // per iteration (8 loads in flight per lane; 8 x 64 measured 2 % slower,
-// profiles/r03_v1/ab_record_groups.txt).
+// profiles/r03_v1/ab_record_groups.txt). GS_LP_NG / GS_LP_RCH: A/B builds.
+#ifndef GS_LP_NG
+#define GS_LP_NG 4
+#endif
+#ifndef GS_LP_RCH
+#define GS_LP_RCH 2
+#endif
 template <int FP, uint32_t CH, bool IDW = false, bool PART = false, bool GOS = false>
 __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
-  constexpr uint32_t NG = 4, RCH = 2;
+  constexpr uint32_t NG = GS_LP_NG, RCH = GS_LP_RCH;
   static_assert(!IDW || FP == 1, "IDONTWANT on the list pass: rows of single-fragment lanes");
   static_assert(!GOS || (FP == 1 && !IDW && !PART), "gossip on the list pass: gs_run's single-fragment rows");
   constexpr uint32_t LMAX = CH * 64;
@@ -358,8 +364,64 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
   for (int q = 0; q < (int)CH; q++) CW[q * 64 + lane] = INF64;
   wave_lds_sync();
 
+  // The wave's rows are w0 + k * stride (local row; global peer a.u0 + w), taken
+  // 64 at a time: step 0 finds, one row per lane, the rows with something to do
+  // in this pass, and the wave visits only those (the near-empty first and last
+  // passes of a batch would otherwise walk every row header one row at a time).
   const uint32_t stride = gridDim.x * PULL_WAVES;
-  uint32_t w = blockIdx.x * PULL_WAVES + wv;  // local row; global peer a.u0 + w
+  for (uint32_t base = blockIdx.x * PULL_WAVES + wv; base < a.N; base += 64 * stride) {
+  // 0. lane l: row base + l * stride is active if a neighbour sent records
+  //    (PULL), entries are due in window c, or it may take IHAVEs (a gossip
+  //    window, a lane not final); an inactive row is only booked: no records
+  //    from it next pass, its pending windows into nmh
+  uint64_t am;
+  {
+    const uint32_t wl = base + (uint32_t)lane * stride;
+    bool act = false;
+    if (wl < a.N) {
+      const uint4* sp = reinterpret_cast<const uint4*>(a.st + (size_t)wl * LP_SW);
+      uint32_t s4[LP_KMAX];
+#pragma unroll
+      for (int k = 0; k < (int)LP_KMAX / 4; k++) {
+        const uint4 v = sp[k];
+        s4[k * 4] = v.x; s4[k * 4 + 1] = v.y; s4[k * 4 + 2] = v.z; s4[k * 4 + 3] = v.w;
+      }
+      // the nearest pending window; cs passes through an empty asm so that the
+      // per-slot offsets are computed here, not hoisted out of the row loop
+      // (12 more scalars live across every row: SGPR spills)
+      uint32_t cs = cslot, mo = ~0u;
+      asm volatile("" : "+s"(cs));
+#pragma unroll
+      for (uint32_t j = 0; j < LP_KMAX; j++) {
+        if (j >= K || !s4[j]) continue;
+        act |= j == cs;
+        mo = umin32(mo, j >= cs ? j - cs : j + K - cs);
+      }
+      const uint32_t mh = mo == ~0u ? ~0u : sat32(hlo64 + (uint64_t)mo * a.dG);
+      if (GOS && gw) act |= !((a.rowdone[wl >> 5] >> (wl & 31)) & 1u);
+      if (pull && !act) {
+        const uint4* mp = reinterpret_cast<const uint4*>(a.mesh + (size_t)(a.u0 + wl) * MESH_W);
+#pragma unroll
+        for (int k = 0; k < (int)MESH_W / 4; k++) {
+          const uint4 m = mp[k];
+          const uint32_t e[4] = {m.x, m.y, m.z, m.w};
+#pragma unroll
+          for (int u = 0; u < 4; u++)
+            if (e[u] != EMPTY) act |= rcnt[e[u] & 0xFFFFFFu] != 0;
+        }
+      }
+      if (!act) {
+        wcnt[wl] = 0;
+        nmh = umin32(nmh, mh);
+      }
+    }
+    am = __ballot(act);
+  }
+  uint32_t w = a.N, wn = a.N;
+  if (am) {
+    w = base + (uint32_t)__builtin_ctzll(am) * stride;
+    am &= am - 1;
+  }
   uint32_t ej = EMPTY, cj = 0, rj = 0, sv = 0;
   uint64_t ro = 0, ro2 = 0;  // PART: offsets of the neighbours' packed records
   if (w < a.N && lane < (int)MESH_W) {
@@ -373,9 +435,11 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
   }
   uint32_t dw = 0;  // gossip windows: the row-done word of row w (every lane reads it)
   if (GOS && gw && w < a.N) dw = a.rowdone[w >> 5];
-  for (; w < a.N; w += stride) {
+  for (; w < a.N; w = wn) {
     PP_T(tA);
-    const uint32_t w2 = w + stride;
+    wn = am ? base + (uint32_t)__builtin_ctzll(am) * stride : a.N;  // the next active row
+    am &= am - 1;
+    const uint32_t w2 = wn;
     uint32_t ej2 = EMPTY, rj2 = 0, cj2 = 0, sv2 = 0, dw2 = 0;
     if (w2 < a.N && lane < (int)MESH_W) {  // w2 < N is wave-uniform
       ej2 = a.mesh[(size_t)(a.u0 + w2) * MESH_W + lane];
@@ -726,6 +790,7 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     ej = ej2; rj = rj2; cj = cj2; sv = sv2; ro = ro2; dw = dw2;
     PP_T(tE);
     PP_ADD(6, tE - tD);
+  }
   }
 #ifdef GS_PULL_PROF
   if (lane == 0 && a.pass < 32)
