@@ -42,12 +42,14 @@
 // lane at each mesh neighbour y: y is skipped when its key time + lat(y -> w)
 // <= t. Such batches run with windows no wider than the smallest latency
 // (gs_relax.hip), so only keys final in earlier windows — written by earlier
-// passes, stable — can pass the test. The skipped neighbours change the uplink positions of the others,
-// so the record carries the 16-bit mask of every excluded mesh index (source,
-// publisher, IDONTWANT) instead of j_src / j_pub:
-//   start - window_lo (32) | hops (6) | exclusion mask (16) | lane (10);
-// the receiver at index r of the sender's row is skipped if bit r is set,
-// else its position is r + 1 - popcount(mask below r).
+// passes, stable — can pass the test.
+//
+// Arrival record (every batch): the sender's row lists which of its mesh
+// entries receive the lane (all but the source and the publisher, and for
+// IDONTWANT the peers that said they have it) as a 16-bit inclusion mask:
+//   start - window_lo (32) | hops (6) | inclusion mask (16) | lane (10);
+// the receiver at index r of the sender's row takes it iff bit r is set, at
+// FIFO position 1 + popcount(mask below r). A missing record reads 0: no bit.
 
 // The record step reads through raw buffer resources whose word 3 (0x00020000:
 // DATA_FORMAT 32, no swizzle, bounds check on) is the gfx9 / CDNA layout; its
@@ -59,6 +61,10 @@
 constexpr uint32_t LP_KMAX = 12;  // ring of destination-window lists
 constexpr uint32_t LP_SW = 16;    // u32 words of per-row state: list lengths [0..11] (slot = window % K), log length
 constexpr uint32_t LP_LOG = 15;   // state word holding the final-log length
+// arrival record (u64): start - window_lo (32) | hops (6) | inclusion mask (16) | lane (10)
+constexpr uint32_t LP_IM_SHIFT = 10, LP_HOP_SHIFT = 26, LP_LANE_MASK = (1u << LP_IM_SHIFT) - 1;
+static_assert(MESH_W <= LP_HOP_SHIFT - LP_IM_SHIFT && PULL_LMAX <= (1u << LP_IM_SHIFT) && HOP_BITS == 32 - LP_HOP_SHIFT,
+              "record fields");
 
 struct LPullArgs {
   uint64_t* keys;       // [N][L] final log during the passes; dense again after k_lfinal
@@ -501,7 +507,7 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
       const uint32_t sd = sdn[sw];
       uint64_t cmk = cand;
       while (cmk) {
-        uint32_t U[NG], R4[NG], NN[NG], SER[NG], ltm[NG];
+        uint32_t U[NG], NN[NG], SER[NG], IB[NG], LB[NG];
         uint64_t BASE[NG], RO[NG];
         uint32_t maxn = 0;
 #pragma unroll
@@ -521,8 +527,10 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
                     __builtin_amdgcn_readlane((uint32_t)ro, j);
           else
             RO[k] = (uint64_t)U[k] * LL;
-          R4[k] = __builtin_amdgcn_readlane(rj, j);
-          ltm[k] = (1u << R4[k]) - 1u;
+          // w's bit in the record's inclusion mask, and the bits below it
+          const uint32_t r = __builtin_amdgcn_readlane(rj, j);
+          IB[k] = 1u << (LP_IM_SHIFT + r);
+          LB[k] = ((1u << r) - 1u) << LP_IM_SHIFT;
           NN[k] = bit ? (uint32_t)__builtin_amdgcn_readlane(cj, j) : 0u;
           const uint32_t su0 = e >> STAGE_SHIFT, su = su0 < S ? su0 : 0u;  // a missing neighbour's EMPTY: class 0
           SER[k] = sup[su];
@@ -556,28 +564,21 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
 #pragma unroll
             for (int cc = 0; cc < (int)RCH; cc++) {
               const uint64_t rc = rec[k][cc];
-              const uint32_t lo32 = (uint32_t)rc, r = R4[k];
-              // one predicate per record: no record (~0, lane field all ones),
-              // or w is excluded (source / publisher / IDONTWANT); the time
-              // field cannot overflow (the sender checked start + rmax)
-              uint32_t slot, pos;
-              bool ok;
-              if constexpr (IDW) {  // exclusion mask of the sender's row
-                const uint32_t xm = (lo32 >> 10) & 0xFFFFu;
-                slot = lo32 & 0x3FFu;
-                ok = rc != 0 && !((xm >> r) & 1u);
-                pos = r + 1 - (uint32_t)__popc(xm & ((1u << r) - 1u));
-              } else {
-                const uint32_t js = (lo32 >> 21) & 31u, jp = (lo32 >> 16) & 31u;
-                slot = lo32 & 0xFFFFu;
-                ok = rc != 0 && js != r && jp != r;  // no record, or w is the source or the publisher
-                // ltm = (1 << r) - 1: bit j set iff j < r (J_NONE = 31 > r)
-                pos = r + 1 - ((ltm[k] >> js) & 1u) - (((ltm[k] >> jp) & 1u) & (jp != js ? 1u : 0u));
-              }
+              const uint32_t lo32 = (uint32_t)rc;
+              // w receives it iff its bit of the inclusion mask is set (no
+              // record reads 0: no bit), at FIFO position 1 + the receivers
+              // before it; the time field cannot overflow (the sender checked
+              // start + rmax)
+              const bool ok = (lo32 & IB[k]) != 0;
+              const uint32_t slot = lo32 & LP_LANE_MASK;
+              const uint32_t pos = (uint32_t)__popc(lo32 & LB[k]) + 1u;
               const uint64_t off = (uint64_t)pos * SER[k] + (rc >> 32);
-              const uint64_t nk = BASE[k] + (off << a.tshift) + ((uint64_t)((lo32 >> 26) & hmask) << a.sb);
-              if (ok) atomicMin((unsigned long long*)&CW[slot], (unsigned long long)nk);
-              cb |= 1u << ((slot >> 6) & 31u);  // an excluded record's chunk is classified for nothing
+              // tshift = sb + HOP_BITS: time and hops are one field above src
+              const uint64_t nk = BASE[k] + (((off << HOP_BITS) | (lo32 >> LP_HOP_SHIFT)) << a.sb);
+              if (ok) {
+                atomicMin((unsigned long long*)&CW[slot], (unsigned long long)nk);
+                cb |= 1u << (slot >> 6);
+              }
             }
         }
       }
@@ -710,8 +711,7 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
         // other lanes are re-checked
         const bool act = gv && (FP == 1 || (x != INF64 && ((uint32_t)(x >> 32) - hlo) < hspan)) && a.u0 + w != pm;
         const uint32_t src = (uint32_t)(x & smask);
-        uint32_t js = J_NONE, jp = J_NONE;  // indices of src / publisher in mesh(w)
-        uint32_t xm = 0;                    // IDW: every excluded mesh index
+        uint32_t xm = 0;  // excluded mesh indices: source, publisher (IDW: and IDONTWANT)
         if constexpr (IDW) {
           const uint64_t tw = x >> a.tshift;
           for (uint32_t k = 0; k < deg; k++) {  // wave-uniform: entry k from lane k
@@ -727,12 +727,11 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
         } else {
           for (uint32_t k = 0; k < deg; k++) {  // wave-uniform: entry k from lane k
             const uint32_t y = __builtin_amdgcn_readlane(ej, k) & 0xFFFFFFu;
-            js = y == src ? k : js;
-            jp = y == pm ? k : jp;
+            xm |= (y == src || y == pm) ? 1u << k : 0u;
           }
         }
-        const uint32_t n = !act ? 0u : IDW ? deg - (uint32_t)__popc(xm)
-                                           : deg - (js != J_NONE ? 1u : 0u) - ((jp != J_NONE && jp != js) ? 1u : 0u);
+        const uint32_t im = ((1u << deg) - 1u) & ~xm;  // the receivers (deg <= MESH_W = 16)
+        const uint32_t n = act ? (uint32_t)__popc(im) : 0u;
         const uint64_t start = uplink_start<FP>(a.busy, (size_t)w * a.B + grp, act, x, n, serw, a.tshift);
         const uint32_t hp = (uint32_t)(x >> a.sb) & hmask;
         if (act) {
@@ -755,8 +754,8 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
         const bool want = act && n != 0;
         const uint64_t wm = __ballot(want);
         if (want) {
-          const uint64_t low = IDW ? (((uint64_t)xm << 10) | i) : (((uint64_t)js << 21) | ((uint64_t)jp << 16) | i);
-          wrec[(size_t)w * LL + ecnt + (uint32_t)__popcll(wm & lanelt)] = ((start - wlo) << 32) | ((uint64_t)hp << 26) | low;
+          wrec[(size_t)w * LL + ecnt + (uint32_t)__popcll(wm & lanelt)] =
+              ((start - wlo) << 32) | ((uint64_t)hp << LP_HOP_SHIFT) | ((uint64_t)im << LP_IM_SHIFT) | i;
         }
         ecnt += (uint32_t)__popcll(wm);
       }
