@@ -484,15 +484,17 @@ bool run_batch_lp(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched,
     }
     if (cm->local) {
       for (uint32_t i = 0; i < nctx; i++) GS_HIP(hipStreamSynchronize(cx[i]->stream));  // every pack done
-      for (uint32_t q = 0; q < nctx; q++) {
+      for (uint32_t q = 0; q < nctx; q++) {  // every other part's range (each packed its own in place)
         Ctx& d = *cx[q];
         GS_HIP(hipSetDevice(d.cfg.device));
         for (uint32_t p = 0; p < nctx; p++) {
+          if (p == q) continue;
           Ctx& src = *cx[p];
           const uint64_t n = cnt[p], u0 = lay.u0(p), un = lay.un(p);
-          if (n) GS_HIP(hipMemcpyAsync(d.d_rpk.p + base[p], src.d_pkout.p, n * RB, hipMemcpyDeviceToDevice, d.stream));
-          GS_HIP(hipMemcpyAsync(d.d_rcg.p + u0, part_lp_counts(src), un * 4, hipMemcpyDeviceToDevice, d.stream));
-          GS_HIP(hipMemcpyAsync(d.d_roffg.p + u0, src.d_pkroff.p, un * 8, hipMemcpyDeviceToDevice, d.stream));
+          if (n) GS_HIP(hipMemcpyAsync(d.d_rpk.p + base[p], src.d_rpk.p + base[p], n * RB, hipMemcpyDeviceToDevice,
+                                       d.stream));
+          GS_HIP(hipMemcpyAsync(d.d_rcg.p + u0, src.d_rcg.p + u0, un * 4, hipMemcpyDeviceToDevice, d.stream));
+          GS_HIP(hipMemcpyAsync(d.d_roffg.p + u0, src.d_roffg.p + u0, un * 8, hipMemcpyDeviceToDevice, d.stream));
         }
       }
       for (uint32_t q = 0; q < nctx; q++) GS_HIP(hipStreamSynchronize(cx[q]->stream));  // sources reused next pass
@@ -500,15 +502,18 @@ bool run_batch_lp(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched,
       Ctx& c = *cx[0];
       const uint32_t me = cm->rank;
       const uint64_t piece = std::max<uint64_t>(1, rccl_piece_bytes() / RB);
-      const uint64_t myn = cnt[me], myun = lay.un(me);
+      const uint64_t myn = cnt[me], myu0 = lay.u0(me), myun = lay.un(me);
+      const uint64_t* mine = c.d_rpk.p + base[me];  // packed in place (part_lp_pack): the own range stays
       GS_NCCL(r->GroupStart());
       for (uint32_t d = 0; d < P; d++) {
+        if (d == me) continue;
         for (uint64_t k = 0; k < myn; k += piece)
-          GS_NCCL(r->Send(c.d_pkout.p + k, std::min(piece, myn - k), ncclUint64, (int)d, cm->nc, c.stream));
-        GS_NCCL(r->Send(part_lp_counts(c), myun, ncclUint32, (int)d, cm->nc, c.stream));
-        GS_NCCL(r->Send(c.d_pkroff.p, myun, ncclUint64, (int)d, cm->nc, c.stream));
+          GS_NCCL(r->Send(mine + k, std::min(piece, myn - k), ncclUint64, (int)d, cm->nc, c.stream));
+        GS_NCCL(r->Send(c.d_rcg.p + myu0, myun, ncclUint32, (int)d, cm->nc, c.stream));
+        GS_NCCL(r->Send(c.d_roffg.p + myu0, myun, ncclUint64, (int)d, cm->nc, c.stream));
       }
       for (uint32_t sr = 0; sr < P; sr++) {
+        if (sr == me) continue;
         const uint64_t n = cnt[sr], u0 = lay.u0(sr), un = lay.un(sr);
         for (uint64_t k = 0; k < n; k += piece)
           GS_NCCL(r->Recv(c.d_rpk.p + base[sr] + k, std::min(piece, n - k), ncclUint64, (int)sr, cm->nc, c.stream));
@@ -536,7 +541,7 @@ bool run_batch_lp(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched,
   bool ok = true;
   for (uint32_t i = 0; i < nctx; i++) {
     GS_HIP(hipSetDevice(cx[i]->cfg.device));
-    ok = part_lp_end(*cx[i], sinks && sinks[i].summary) && ok;
+    ok = part_lp_end(*cx[i], sinks ? &sinks[i] : nullptr) && ok;
   }
   if (!cm->local && cx[0]->cfg.lazy_gossip) {
     uint64_t mine = ok ? 0 : 1, all[64];

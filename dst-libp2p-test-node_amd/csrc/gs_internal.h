@@ -211,8 +211,6 @@ struct Ctx {
   DevBuf<uint32_t> d_rcg;    // [N] records per peer (global ids)
   DevBuf<uint64_t> d_roffg;  // [N] their offsets in d_rpk
   DevBuf<uint64_t> d_rpk;    // every part's records of the last pass
-  DevBuf<uint64_t> d_pkout;  // this part's records, packed for the exchange
-  DevBuf<uint64_t> d_pkroff; // [own rows] their offsets in d_rpk
   DevBuf<uint64_t> d_pkcur;  // pack cursor
   // lazy gossip inside the list pass (gs_lpull_kernel.h, GOS batches)
   DevBuf<uint32_t> d_gpl;      // [N][32] sender planes of the built heartbeat
@@ -249,7 +247,7 @@ void part_dev_bucket(Ctx& c, uint32_t parts);
 void part_dev_scan_count(Ctx& c, uint32_t parts);
 void part_dev_export(Ctx& c, uint32_t parts, gs_part_record* out);
 void part_dev_relax_next(Ctx& c, const gs_part_record* in, uint64_t n);
-bool part_dev_complete(Ctx& c, bool hist);
+bool part_dev_complete(Ctx& c, bool hist, bool store = true);
 void part_dev_finish(Ctx& c, const gs_result_sink* sink, uint64_t row0);
 void part_abort(Ctx& c);
 bool part_needs_ms(Ctx& c, const gs_publish* sched, uint64_t n_msgs);
@@ -259,8 +257,7 @@ void part_lp_pass(Ctx& c);
 void part_lp_read(Ctx& c, uint64_t out[4]);  // last pass: mode, records, min pending, error word
 void part_lp_set(Ctx& c, uint64_t records, uint64_t minp);  // the combined values into the last pass's slot
 void part_lp_pack(Ctx& c, uint64_t base, uint64_t mine);
-const uint32_t* part_lp_counts(Ctx& c);  // this part's per-row record counts of the last pass
-bool part_lp_end(Ctx& c, bool hist);     // dense rows, completion, gossip proof
+bool part_lp_end(Ctx& c, const gs_result_sink* sink);  // completion (final logs or dense rows), gossip proof
 void part_lp_abort(Ctx& c);
 
 // small device helpers

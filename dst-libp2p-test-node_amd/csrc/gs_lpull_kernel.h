@@ -1100,7 +1100,7 @@ __global__ __launch_bounds__(LC_WAVES * 64) void k_lcomplete(LPullArgs a, uint64
         if (m >= B) continue;
         const uint64_t x = Rw[m];
         uint32_t v = GS_LAT_NONE;
-        if (pm[j] == w) {
+        if (pm[j] == a.u0 + w) {
           if (a.self_log && x != INF64) v = 0;
         } else if (x != INF64) {
           const uint64_t ms = (x >> a.tshift) / 1000000ull;
@@ -1114,7 +1114,7 @@ __global__ __launch_bounds__(LC_WAVES * 64) void k_lcomplete(LPullArgs a, uint64
 #pragma unroll
     for (int j = 0; j < (int)PULL_CH; j++) {
       const uint32_t m = j * 64 + lane;
-      if (m >= B || pm[j] == w) continue;  // the publisher's own key is no delivery
+      if (m >= B || pm[j] == a.u0 + w) continue;  // the publisher's own key is no delivery
       const uint64_t x = Rw[m];
       if (x == INF64) { ud[j]++; continue; }
       const uint64_t trel = x >> a.tshift, ms = trel / 1000000ull;
@@ -1166,13 +1166,16 @@ uint32_t lpull_chunks(uint32_t L) {
 }
 
 // Partitioned pass: this part's records of the pass (lrec[nb] / lcnt[nb], by
-// local row) packed for the exchange: out[...] holds them row after row in
-// the order rows claim space (one atomic per wave of 64 rows), and roff[r] =
-// base + the row's offset, base = this part's offset in the packed records of
-// all parts (the host knows every part's total after the pass).
+// local row) packed straight into its own range of the next pass's packed
+// records of all parts: out = rpk + base (base = this part's offset there, the
+// host knows every part's total after the pass) holds them row after row in
+// the order rows claim space (one atomic per wave of 64 rows); roff[r] = base +
+// the row's offset and rcg[r] = its count go to the own rows of the global
+// offset / count tables. Only the other parts' ranges are then exchanged.
 __global__ __launch_bounds__(TB) void k_lpack(const uint64_t* __restrict__ rec, const uint32_t* __restrict__ cnt,
                                               uint32_t N, uint32_t L, uint64_t base, uint64_t* __restrict__ out,
-                                              uint64_t* __restrict__ roff, unsigned long long* cursor) {
+                                              uint64_t* __restrict__ roff, uint32_t* __restrict__ rcg,
+                                              unsigned long long* cursor) {
   const int lane = threadIdx.x & 63;
   const uint32_t wave = blockIdx.x * (TB / 64) + (threadIdx.x >> 6), nw = gridDim.x * (TB / 64);
   for (uint32_t r0 = wave * 64; r0 < N; r0 += nw * 64) {
@@ -1188,7 +1191,10 @@ __global__ __launch_bounds__(TB) void k_lpack(const uint64_t* __restrict__ rec, 
     if (lane == 0 && tot) b0 = atomicAdd(cursor, (unsigned long long)tot);
     const uint64_t wb = ((uint64_t)__shfl((uint32_t)(b0 >> 32), 0) << 32) | __shfl((uint32_t)b0, 0);
     const uint64_t my = wb + x - n;
-    if (r < N) roff[r] = base + my;
+    if (r < N) {
+      roff[r] = base + my;
+      rcg[r] = n;
+    }
     for (int j = 0; j < 64; j++) {  // copy row by row, 64 records per step
       const uint32_t nj = __shfl(n, j);
       const uint64_t oj = ((uint64_t)__shfl((uint32_t)(my >> 32), j) << 32) | __shfl((uint32_t)my, j);

@@ -562,9 +562,9 @@ void part_dev_relax_next(Ctx& c, const gs_part_record* in, uint64_t n) {
 // when a summary is wanted) and, with lazy gossip, this part's half of the
 // no-op proof (gossip_noop over its own peers; the batch stands iff every
 // part's holds). Returns true without lazy gossip.
-bool part_dev_complete(Ctx& c, bool hist) {
+bool part_dev_complete(Ctx& c, bool hist, bool store) {
   const Batch& b = c.part_b;
-  run_complete(c, b, c.part_u0, c.part_un, true, hist);
+  run_complete(c, b, c.part_u0, c.part_un, true, hist, store);
   if (!c.cfg.lazy_gossip) return true;
   std::vector<uint64_t> ms((size_t)b.B * MS_COLS), rel0(b.B);
   GS_HIP(hipMemcpyAsync(ms.data(), c.d_mstat.p, ms.size() * 8, hipMemcpyDeviceToHost, c.stream));
@@ -691,7 +691,6 @@ bool part_lp_begin(Ctx& c, const gs_publish* sched, uint64_t n_msgs, uint64_t* s
   c.d_rcg.alloc(N);
   c.d_roffg.alloc(N);
   c.d_rpk.alloc(1);
-  c.d_pkroff.alloc(un);
   c.d_pkcur.alloc(1);
   if (b.FP > 1) c.d_busy.alloc((size_t)un * Bmax);
   c.d_tc.alloc((size_t)un * Bmax);
@@ -762,28 +761,36 @@ void part_lp_read(Ctx& c, uint64_t out[4]) {
   out[3] = c.h_pinned[4];
 }
 
-const uint32_t* part_lp_counts(Ctx& c) { return c.d_lcnt.p + (size_t)((c.part_lppass + 1) & 1) * c.part_un; }
-
 void part_lp_pack(Ctx& c, uint64_t base, uint64_t mine) {
   const uint32_t un = c.part_un, L = c.part_b.L;
-  c.d_pkout.alloc(std::max<uint64_t>(mine, 1));
+  (void)mine;  // the caller sized d_rpk for every part's records
   hipStream_t s = c.stream;
   GS_HIP(hipMemsetAsync(c.d_pkcur.p, 0, 8, s));
   const uint32_t nb = (c.part_lppass + 1) & 1;  // the last pass wrote lrec / lcnt [pass & 1]
   const unsigned grid = (unsigned)std::max<uint64_t>(
       1, std::min<uint64_t>(((uint64_t)un + 255) / 256, (uint64_t)c.num_cus * 8));
   k_lpack<<<grid, TB, 0, s>>>(c.d_lrec.p + (size_t)nb * un * L, c.d_lcnt.p + (size_t)nb * un, un, L, base,
-                              c.d_pkout.p, c.d_pkroff.p, (unsigned long long*)c.d_pkcur.p);
+                              c.d_rpk.p + base, c.d_roffg.p + c.part_u0, c.d_rcg.p + c.part_u0,
+                              (unsigned long long*)c.d_pkcur.p);
   GS_HIP(hipGetLastError());
 }
 
-bool part_lp_end(Ctx& c, bool hist) {
-  const LPullArgs la = part_lp_args(c);
-  k_lfinal<<<c.part_lpgrid, TB, 0, c.stream>>>(la);  // final logs -> dense rows of own peers
-  GS_HIP(hipGetLastError());
+// As gs_run's list pass: completion reads the final logs (k_lcomplete) unless
+// the sink takes rows or a summary, or the rows hold fragment groups (k_lfinal
+// -> dense rows -> k_complete).
+bool part_lp_end(Ctx& c, const gs_result_sink* sink) {
+  const SinkWants w = sink_wants(sink);
+  const bool dense = w.rows() || w.summary || c.part_b.FP > 1 || getenv("GS_LPULL_DENSE");
+  if (dense) {
+    const LPullArgs la = part_lp_args(c);
+    k_lfinal<<<c.part_lpgrid, TB, 0, c.stream>>>(la);  // final logs -> dense rows of own peers
+    GS_HIP(hipGetLastError());
+  } else {
+    c.keys_log = true;
+  }
   c.stats.list_pull_batches++;
   c.part_lp = false;
-  return part_dev_complete(c, hist);
+  return part_dev_complete(c, w.summary, dense);
 }
 
 void part_lp_abort(Ctx& c) {  // the batch re-runs on the push protocol: counters as before the batch

@@ -491,8 +491,9 @@ static void run_complete(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, bool 
   hipStream_t s = c.stream;
   if (lat) c.d_lat.alloc((size_t)un * c.cfg.batch);
   if (c.keys_log) {  // list pull path, results on the device: reduce the final logs
-    if (hist || store || u0 || un != c.cfg.peers || b.FP != 1) c.fail(GS_EINVAL, "internal: final logs need k_lfinal");
+    if (hist || store || b.FP != 1) c.fail(GS_EINVAL, "internal: final logs need k_lfinal");
     LPullArgs la{};
+    la.u0 = u0;  // rows [0, un) are global peers u0 + row (a part of gs_run_partitioned)
     la.keys = c.d_keys.p; la.flane = c.d_flane.p; la.st = c.d_lst.p; la.pub = c.d_pub.p;
     la.counters = c.d_counters.p; la.N = un; la.B = b.B; la.L = b.L; la.tshift = b.tshift;
     la.self_log = c.cfg.self_log;
@@ -527,8 +528,11 @@ static void run_complete(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, bool 
   const uint32_t tiles = (b.B + ca.MT - 1) / ca.MT;
   const uint64_t rows_per_block = (TB / 64) * (64 / ca.MT);
   const uint64_t want = std::max<uint64_t>(1, (uint64_t)c.num_cus * 16 / tiles);
-  dim3 grid((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((un + rows_per_block - 1) / rows_per_block, want)),
-            tiles);
+  // >= 16 rows per lane: every block ends in one atomic per message and column,
+  // and a grid of thin blocks serialises on them (config #2, 10k rows x 2 message
+  // tiles: 2048 blocks per tile, 595 us per batch, profiles/r04_v3)
+  const uint64_t thick = (un + rows_per_block * 16 - 1) / (rows_per_block * 16);
+  dim3 grid((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(thick, want)), tiles);
 #define GS_COMPLETE(FPV)                                                      \
   if (hist) k_complete<FPV, true><<<grid, TB, 0, s>>>(ca);                    \
   else k_complete<FPV, false><<<grid, TB, 0, s>>>(ca);

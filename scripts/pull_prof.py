@@ -16,15 +16,16 @@ gossipsim.LIB_PATH = os.path.join(ROOT, "prof_build", "libgossipsim.so")
 peers = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
 L = gossipsim.lib()
 L.gs_debug_pull_prof.argtypes = [ctypes.c_void_p]
-sim = gossipsim.Simulator(peers=peers, batch=1024, fragments=1, seed=1, device=0)
+B = int(os.environ.get("BATCH", 1024))  # config #2: PEERS=10000 BATCH=128 FRAGS=8
+sim = gossipsim.Simulator(peers=peers, batch=B, fragments=int(os.environ.get("FRAGS", 1)), seed=1, device=0)
 sim.set_topogen_links(5, 50, 150, 40, 130)
 sim.connect_gossipsub_peers()
 sim.mesh_converge(400)
-sim.run(gossipsim.shard_messages(0, 0, 1, 1024, peers, 15000), collect=False)
+sim.run(gossipsim.shard_messages(0, 0, 1, B, peers, 15000), collect=False)
 buf = np.zeros(32 * 8, dtype=np.uint64)
 L.gs_debug_pull_prof(buf.ctypes.data)
 sim.set_timing(True)
-sim.run(gossipsim.shard_messages(1, 0, 1, 1024, peers, 15000), collect=False)
+sim.run(gossipsim.shard_messages(1, 0, 1, B, peers, 15000), collect=False)
 L.gs_debug_pull_prof(buf.ctypes.data)
 b = buf.reshape(32, 8).astype(np.float64)
 print("pass  skip%  load+rec%  dense%  sparse%  cmin%  active_rows  Gclk")
