@@ -412,6 +412,20 @@ def config_rates(args, local):
             d = time.perf_counter() - t0
             dt = d if dt is None else min(dt, d)
         st = sim.stats()
+        # one more repeat with HIP events around every window pass / bucket: the
+        # config's roofline on SURVEY 8(d)'s algorithmic bytes (kernel time only)
+        sim.reset_stats()
+        sim.set_timing(True)
+        sim.run(sched, collect=False)
+        sim.set_timing(False)
+        tst = sim.stats()
+        roof = None
+        if tst["relax_ms"] > 0 and tst["relax_launches"]:
+            ach = tst["relax_bytes_alg"] / (tst["relax_ms"] / 1e3) / 1e9
+            roof = {"bound": "hbm", "achieved": ach, "peak": 8000.0, "unit": "GB/s", "frac": ach / 8000.0,
+                    "alg_bytes_per_launch": tst["relax_bytes_alg"] / tst["relax_launches"],
+                    "avg_launch_us": tst["relax_ms"] * 1e3 / tst["relax_launches"],
+                    "launches": int(tst["relax_launches"]), "pass_ms": tst["relax_ms"]}
         push = c["knobs"].get("churn_ppm") or (st["gossip_fallback_batches"] and not st["gossip_list_batches"]) or \
             (st["list_pull_batches"] == 0 and sim.cfg.c.idontwant)
         out[name] = {"value": st["deliveries"] / dt, "unit": "deliveries/s", "msgs": c["msgs"], "best_of": c.get("reps", 1),
@@ -422,7 +436,8 @@ def config_rates(args, local):
                      "list_pull_batches": int(st["list_pull_batches"]),
                      "kernel_path": "push (k_scan+k_frontier+k_gossip)" if push else
                      "pull (k_lpull, IHAVE/IWANT inside the passes)" if st["gossip_list_batches"] else
-                     "pull (k_lpull)" if st["list_pull_batches"] else "pull (k_pull)"}
+                     "pull (k_lpull)" if st["list_pull_batches"] else "pull (k_pull)",
+                     "roofline": roof}
         sim.close()
     return out
 

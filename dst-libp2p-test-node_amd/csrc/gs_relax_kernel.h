@@ -254,6 +254,11 @@ __device__ __forceinline__ uint64_t first_hb(uint64_t t, uint64_t rel0, uint64_t
 // max(t_f, busy) + n_f * ser in (key, fragment) order (gossip answers bypass
 // the FIFO, so two fragments can carry equal keys; the index breaks the tie)
 // and stores the new FIFO end in busy[bi]. Returns the lane's uplink start.
+// Closed form of the fold instead of FP sequential selection rounds (FP^2
+// compares): with P_f = the sends queued before fragment f in that order,
+//   start_f = max(busy + P_f, max over g <= f of t_g + P_f - P_g),
+//   end     = max(busy + P, max over g of t_g + P - P_g),  P = all sends
+// (O(FP) per lane; scripts/fifo_check.cpp compares it with the fold).
 // Every lane of the wave must call this.
 template <int FP>
 __device__ __forceinline__ uint64_t uplink_start(uint64_t* busy, size_t bi, bool active, uint64_t key,
@@ -261,39 +266,34 @@ __device__ __forceinline__ uint64_t uplink_start(uint64_t* busy, size_t bi, bool
   uint64_t start = key >> tshift;
   if constexpr (FP > 1) {
     const int lane = threadIdx.x & 63;
-    const int gb = lane & ~(FP - 1);
+    const int gb = lane & ~(FP - 1), me = lane - gb;
     const uint64_t ka = active ? key : INF64;
-    uint64_t kk[FP];
-    uint32_t nn[FP];
-#pragma unroll
-    for (int g = 0; g < FP; g++) { kk[g] = __shfl(ka, gb + g); nn[g] = __shfl(n, gb + g); }
+    // the group's keys are re-read by shuffle in each loop (no per-fragment
+    // arrays live across the function: k_pull<8> spilled 187 VGPRs with them)
+    uint64_t P = 0, tot = 0;  // sends before mine, all sends
     int first = -1;
-#pragma unroll
-    for (int g = FP - 1; g >= 0; g--) if (kk[g] != INF64) first = g;
-    if (first >= 0) {
-      uint64_t cb = busy ? busy[bi] : 0;  // no busy array: the FIFO starts empty (gs_traffic.h)
-      uint64_t pk = 0;
-      int pg = -1;
-#pragma unroll
-      for (int it = 0; it < FP; it++) {
-        uint64_t bk = INF64;
-        int bg = FP;
-        uint32_t bn = 0;
-#pragma unroll
-        for (int g = 0; g < FP; g++) {
-          const bool after = kk[g] > pk || (kk[g] == pk && g > pg);
-          const bool better = kk[g] < bk || (kk[g] == bk && g < bg);
-          if (kk[g] != INF64 && after && better) { bk = kk[g]; bg = g; bn = nn[g]; }
-        }
-        if (bg == FP) continue;  // nothing left (kept unrollable: no break)
-        const uint64_t tb = bk >> tshift;
-        const uint64_t s = tb > cb ? tb : cb;
-        if (active && bg == lane - gb) start = s;
-        cb = s + (uint64_t)bn * ser;
-        pk = bk;
-        pg = bg;
-      }
-      if (busy && lane - gb == first) busy[bi] = cb;
+#pragma unroll 8
+    for (int g = FP - 1; g >= 0; g--) {
+      const uint64_t kg = __shfl(ka, gb + g);
+      const bool v = kg != INF64;
+      if (v) first = g;
+      const uint64_t d = (uint64_t)(uint32_t)__shfl((int)n, gb + g) * ser;
+      tot += v ? d : 0;
+      P += (v && (kg < ka || (kg == ka && g < me))) ? d : 0;
+    }
+    uint64_t s = 0, e = 0;
+#pragma unroll 8
+    for (int g = 0; g < FP; g++) {
+      const uint64_t kg = __shfl(ka, gb + g), pg = __shfl(P, gb + g);
+      if (kg == INF64) continue;
+      const uint64_t tg = kg >> tshift;
+      if (kg < ka || (kg == ka && g <= me)) s = max(s, tg + P - pg);
+      e = max(e, tg + tot - pg);
+    }
+    if (first >= 0) {  // group-uniform
+      const uint64_t cb = busy ? busy[bi] : 0;  // no busy array: the FIFO starts empty (gs_traffic.h)
+      if (active) start = max(s, cb + P);
+      if (busy && me == first) busy[bi] = max(e, cb + tot);
     }
   }
   return start;

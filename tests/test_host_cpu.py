@@ -577,3 +577,13 @@ def test_partition_layout_exchanges(tmp_path):
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stdout
     assert out.stdout.startswith("ok ") and int(out.stdout.split()[1]) > 100000
+
+
+def test_uplink_fifo_closed_form(tmp_path):
+    """uplink_start's prefix-sum form of the fragment FIFO (gs_relax_kernel.h)
+    equals the sequential (key, fragment) fold it replaced, on 2M random
+    groups of 2-16 fragments with ties, missing fragments and busy uplinks."""
+    exe = tmp_path / "fifo_check"
+    subprocess.run(["g++", "-O2", "-o", str(exe), os.path.join(ROOT, "scripts", "fifo_check.cpp")], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and out.stdout.strip() == "ok", out.stdout
