@@ -288,6 +288,9 @@ __device__ __forceinline__ void glp_ihave(const LPullArgs& a, uint64_t* CW, uint
 #ifndef GS_LP_RCH
 #define GS_LP_RCH 2
 #endif
+#ifndef GS_LP_CLS2
+#define GS_LP_CLS2 0
+#endif
 template <int FP, uint32_t CH, bool IDW = false, bool PART = false, bool GOS = false>
 __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
   constexpr uint32_t NG = GS_LP_NG, RCH = GS_LP_RCH;
@@ -612,9 +615,23 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
       if (!((cb >> q) & 1u)) continue;  // wave-uniform
       const uint32_t i = q * 64 + lane;
       const uint64_t x = CW[i];
-      const bool fe = (finT >> q) & 1u;  // final in an earlier window: dropped
+      const bool fe = (finT & (1u << q)) != 0;  // final in an earlier window: dropped
       // (a fragment group's step 4 re-reads every lane of a final group)
       if (FP > 1 && fe && x != INF64) CW[i] = INF64;
+#if GS_LP_CLS2
+      // the wave's masks from three single compares (a ballot of a compound
+      // predicate cost a select + compare each), lane positions by mbcnt
+      const bool inf = x == INF64, inw = ((uint32_t)(x >> 32) - hlo) < hspan;
+      // llvm.amdgcn.icmp: the compare's lane mask as is (32 EQ, 33 NE, 36 ULT)
+      const uint64_t dead = __builtin_amdgcn_uicmp(finT & (1u << q), 0u, 33) | __builtin_amdgcn_uicmpl(x, INF64, 32);
+      const uint64_t bw = __builtin_amdgcn_uicmp((uint32_t)(x >> 32) - hlo, hspan, 36);
+      const uint64_t am = bw & ~dead, pm = ~(bw | dead);
+      const bool act = !fe && !inf && inw, pend = !fe && !inf && !inw;
+      if (pend)
+        LST[LMAX - 1 - (npend + __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u)))] =
+            (uint16_t)i;
+      npend += (uint32_t)__popcll(pm);
+#else
       const bool live = !fe && x != INF64;
       const bool act = live && ((uint32_t)(x >> 32) - hlo) < hspan;
       const bool pend = live && !act;
@@ -622,11 +639,18 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
       if (pend) LST[LMAX - 1 - (npend + (uint32_t)__popcll(pm & lanelt))] = (uint16_t)i;
       npend += (uint32_t)__popcll(pm);
       const uint64_t am = __ballot(act);
+#endif
       if (am) {  // wave-uniform
         finT |= act ? 1u << q : 0u;
         nfin = 1;
         if constexpr (FP == 1) {
+#if GS_LP_CLS2
+          if (act)
+            LST[cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(am >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0u))] =
+                (uint16_t)i;
+#else
           if (act) LST[cnt + (uint32_t)__popcll(am & lanelt)] = (uint16_t)i;
+#endif
           cnt += (uint32_t)__popcll(am);
         } else {
           constexpr uint64_t gmask = (FP == 64) ? ~0ull : ((1ull << FP) - 1);
@@ -669,15 +693,27 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
         if (jv && r >= K) err |= ERR_RING;
         const bool ap = jv && r > 0 && r < K;
         uint32_t pos = 0, slot = 0;
+#if GS_LP_CLS2
+        uint64_t rem = __builtin_amdgcn_uicmp(r - 1u, K - 1u, 36);  // ap: r in [1, K) (r = 0 off the list)
+#else
         uint64_t rem = __ballot(ap);  // the window offsets present: one pass each,
+#endif
         while (rem) {                 // read from the lowest lane still waiting (wave-uniform)
           const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)r, (int)__builtin_ctzll(rem));
           const uint32_t sl = (cslot + k) % K;
+#if GS_LP_CLS2
+          const uint64_t bm = __builtin_amdgcn_uicmp(r, k, 32);  // k >= 1: only listed lanes
+#else
           const uint64_t bm = __ballot(ap && r == k);
+#endif
           rem &= ~bm;
           const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane(sv + addl, sl);
           if (ap && r == k) {
+#if GS_LP_CLS2
+            pos = b0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+#else
             pos = b0 + (uint32_t)__popcll(bm & lanelt);
+#endif
             slot = sl;
           }
           addl += lane == (int)sl ? (uint32_t)__popcll(bm) : 0u;
@@ -740,21 +776,39 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
           if (n && hp + 1 >= (1u << HOP_BITS)) err |= ERR_HOPS;
           if (start - wlo >= (1ull << 32) || (n && start + a.rmax > a.tmax)) err |= ERR_TIME;
         }
+#if GS_LP_CLS2
+        // act as lane masks: listed (gi < cnt) and not the message's publisher
+        const uint64_t fm = FP == 1 ? (__builtin_amdgcn_uicmp(gi, cnt, 36) & __builtin_amdgcn_uicmp(pm, a.u0 + w, 33))
+                                    : __ballot(act);  // final log: 64 entries per store
+#else
         const uint64_t fm = __ballot(act);  // final log: 64 entries per store
+#endif
         if constexpr (IDW) {
           if (act) a.keys[(size_t)w * LL + i] = x;  // dense: the neighbours' IDONTWANT tests read it
         } else {
           if (act) {
+#if GS_LP_CLS2
+            const uint32_t p =
+                logc + __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
+#else
             const uint32_t p = logc + (uint32_t)__popcll(fm & lanelt);
+#endif
             a.keys[(size_t)w * LL + p] = x;
             a.flane[(size_t)w * LL + p] = (uint16_t)i;
           }
           logc += (uint32_t)__popcll(fm);
         }
         const bool want = act && n != 0;
+#if GS_LP_CLS2
+        const uint64_t wm = fm & __builtin_amdgcn_uicmp(n, 0u, 33);
+        if (want) {
+          wrec[(size_t)w * LL + ecnt +
+               __builtin_amdgcn_mbcnt_hi((uint32_t)(wm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wm, 0u))] =
+#else
         const uint64_t wm = __ballot(want);
         if (want) {
           wrec[(size_t)w * LL + ecnt + (uint32_t)__popcll(wm & lanelt)] =
+#endif
               ((start - wlo) << 32) | ((uint64_t)hp << LP_HOP_SHIFT) | ((uint64_t)im << LP_IM_SHIFT) | i;
         }
         ecnt += (uint32_t)__popcll(wm);
