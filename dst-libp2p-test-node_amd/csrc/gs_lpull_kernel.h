@@ -135,11 +135,12 @@ constexpr uint32_t LP_FW = PULL_LMAX / 32;  // u32 final-bit words per row
 
 __device__ __forceinline__ uint32_t sat32(uint64_t x) { return x > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)x; }
 
-// Offset of key hi word hx from the emitted window (thr[k] = start of window c + k).
-__device__ __forceinline__ uint32_t lp_rof(uint32_t hx, const uint32_t (&thr)[LP_KMAX + 1], uint32_t K) {
+// Offset of key hi word hx from the emitted window c (window c + k starts at
+// hi word sat32(hlo64 + k * dG)); for the saturated end of the time range only,
+// where the division of the pass does not apply.
+__device__ __forceinline__ uint32_t lp_rof(uint32_t hx, uint64_t hlo64, uint32_t dG, uint32_t K) {
   uint32_t r = 0;
-#pragma unroll
-  for (uint32_t k = 1; k <= LP_KMAX; k++) r += (k <= K && hx >= thr[k]) ? 1u : 0u;
+  for (uint32_t k = 1; k <= K; k++) r += hx >= sat32(hlo64 + (uint64_t)k * dG) ? 1u : 0u;
   return r;  // r == K: beyond the ring (an error the host bound rules out)
 }
 
@@ -288,9 +289,6 @@ __device__ __forceinline__ void glp_ihave(const LPullArgs& a, uint64_t* CW, uint
 #ifndef GS_LP_RCH
 #define GS_LP_RCH 2
 #endif
-#ifndef GS_LP_CLS2
-#define GS_LP_CLS2 0
-#endif
 template <int FP, uint32_t CH, bool IDW = false, bool PART = false, bool GOS = false>
 __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
   constexpr uint32_t NG = GS_LP_NG, RCH = GS_LP_RCH;
@@ -326,12 +324,9 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
   const uint32_t K = a.K, LL = a.L, S = a.S;
   const uint32_t cslot = (uint32_t)(c % K);
   const uint64_t hlo64 = c * a.dG;
-  uint32_t thr[LP_KMAX + 1];
-#pragma unroll
-  for (uint32_t k = 0; k <= LP_KMAX; k++) thr[k] = sat32(hlo64 + (uint64_t)k * a.dG);
-  const uint32_t hlo = thr[0], hspan = a.dG;  // hi words of window c: [hlo, hlo + dG)
+  const uint32_t hlo = sat32(hlo64), hspan = a.dG;  // hi words of window c: [hlo, hlo + dG)
   // window offsets of pending minima by division when no threshold of the
-  // ring saturates (lp_rof's count of thr[k] <= hx is then floor((hx - hlo) / dG))
+  // ring saturates (lp_rof's count of window starts <= hx is then floor((hx - hlo) / dG))
   const bool rdiv = hlo64 + (uint64_t)(K + 1) * a.dG < 0xFFFFFFFFull;
   const float rinv = 1.0f / (float)a.dG;
   const size_t NL = (size_t)a.N * LL;
@@ -395,16 +390,16 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
         const uint4 v = sp[k];
         s4[k * 4] = v.x; s4[k * 4 + 1] = v.y; s4[k * 4 + 2] = v.z; s4[k * 4 + 3] = v.w;
       }
-      // the nearest pending window; cs passes through an empty asm so that the
-      // per-slot offsets are computed here, not hoisted out of the row loop
-      // (12 more scalars live across every row: SGPR spills)
-      uint32_t cs = cslot, mo = ~0u;
-      asm volatile("" : "+s"(cs));
+      // the nearest pending window; cs and kk pass through an empty asm so that
+      // the per-slot offsets and tests are computed here, not hoisted out of the
+      // row loop (24 more scalars live across every row: SGPR spills)
+      uint32_t cs = cslot, kk = K, mo = ~0u;
+      asm volatile("" : "+s"(cs), "+s"(kk));
 #pragma unroll
       for (uint32_t j = 0; j < LP_KMAX; j++) {
-        if (j >= K || !s4[j]) continue;
+        if (j >= kk || !s4[j]) continue;
         act |= j == cs;
-        mo = umin32(mo, j >= cs ? j - cs : j + K - cs);
+        mo = umin32(mo, j >= cs ? j - cs : j + kk - cs);
       }
       const uint32_t mh = mo == ~0u ? ~0u : sat32(hlo64 + (uint64_t)mo * a.dG);
       if (GOS && gw) act |= !((a.rowdone[wl >> 5] >> (wl & 31)) & 1u);
@@ -618,7 +613,6 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
       const bool fe = (finT & (1u << q)) != 0;  // final in an earlier window: dropped
       // (a fragment group's step 4 re-reads every lane of a final group)
       if (FP > 1 && fe && x != INF64) CW[i] = INF64;
-#if GS_LP_CLS2
       // the wave's masks from three single compares (a ballot of a compound
       // predicate cost a select + compare each), lane positions by mbcnt
       const bool inf = x == INF64, inw = ((uint32_t)(x >> 32) - hlo) < hspan;
@@ -631,26 +625,13 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
         LST[LMAX - 1 - (npend + __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u)))] =
             (uint16_t)i;
       npend += (uint32_t)__popcll(pm);
-#else
-      const bool live = !fe && x != INF64;
-      const bool act = live && ((uint32_t)(x >> 32) - hlo) < hspan;
-      const bool pend = live && !act;
-      const uint64_t pm = __ballot(pend);
-      if (pend) LST[LMAX - 1 - (npend + (uint32_t)__popcll(pm & lanelt))] = (uint16_t)i;
-      npend += (uint32_t)__popcll(pm);
-      const uint64_t am = __ballot(act);
-#endif
       if (am) {  // wave-uniform
         finT |= act ? 1u << q : 0u;
         nfin = 1;
         if constexpr (FP == 1) {
-#if GS_LP_CLS2
           if (act)
             LST[cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(am >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0u))] =
                 (uint16_t)i;
-#else
-          if (act) LST[cnt + (uint32_t)__popcll(am & lanelt)] = (uint16_t)i;
-#endif
           cnt += (uint32_t)__popcll(am);
         } else {
           constexpr uint64_t gmask = (FP == 64) ? ~0ull : ((1ull << FP) - 1);
@@ -687,33 +668,21 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
             else if (((uint64_t)q + 1) * hspan <= d) q++;  // widened first: q may be 0xFFFFFFFF
             r = q < K ? q : K;
           } else {
-            r = lp_rof((uint32_t)(x >> 32), thr, K);
+            r = lp_rof((uint32_t)(x >> 32), hlo64, a.dG, K);
           }
         }
         if (jv && r >= K) err |= ERR_RING;
         const bool ap = jv && r > 0 && r < K;
         uint32_t pos = 0, slot = 0;
-#if GS_LP_CLS2
         uint64_t rem = __builtin_amdgcn_uicmp(r - 1u, K - 1u, 36);  // ap: r in [1, K) (r = 0 off the list)
-#else
-        uint64_t rem = __ballot(ap);  // the window offsets present: one pass each,
-#endif
         while (rem) {                 // read from the lowest lane still waiting (wave-uniform)
           const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)r, (int)__builtin_ctzll(rem));
           const uint32_t sl = (cslot + k) % K;
-#if GS_LP_CLS2
           const uint64_t bm = __builtin_amdgcn_uicmp(r, k, 32);  // k >= 1: only listed lanes
-#else
-          const uint64_t bm = __ballot(ap && r == k);
-#endif
           rem &= ~bm;
           const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane(sv + addl, sl);
           if (ap && r == k) {
-#if GS_LP_CLS2
             pos = b0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
-#else
-            pos = b0 + (uint32_t)__popcll(bm & lanelt);
-#endif
             slot = sl;
           }
           addl += lane == (int)sl ? (uint32_t)__popcll(bm) : 0u;
@@ -776,39 +745,25 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
           if (n && hp + 1 >= (1u << HOP_BITS)) err |= ERR_HOPS;
           if (start - wlo >= (1ull << 32) || (n && start + a.rmax > a.tmax)) err |= ERR_TIME;
         }
-#if GS_LP_CLS2
         // act as lane masks: listed (gi < cnt) and not the message's publisher
         const uint64_t fm = FP == 1 ? (__builtin_amdgcn_uicmp(gi, cnt, 36) & __builtin_amdgcn_uicmp(pm, a.u0 + w, 33))
                                     : __ballot(act);  // final log: 64 entries per store
-#else
-        const uint64_t fm = __ballot(act);  // final log: 64 entries per store
-#endif
         if constexpr (IDW) {
           if (act) a.keys[(size_t)w * LL + i] = x;  // dense: the neighbours' IDONTWANT tests read it
         } else {
           if (act) {
-#if GS_LP_CLS2
             const uint32_t p =
                 logc + __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
-#else
-            const uint32_t p = logc + (uint32_t)__popcll(fm & lanelt);
-#endif
             a.keys[(size_t)w * LL + p] = x;
             a.flane[(size_t)w * LL + p] = (uint16_t)i;
           }
           logc += (uint32_t)__popcll(fm);
         }
         const bool want = act && n != 0;
-#if GS_LP_CLS2
         const uint64_t wm = fm & __builtin_amdgcn_uicmp(n, 0u, 33);
         if (want) {
           wrec[(size_t)w * LL + ecnt +
                __builtin_amdgcn_mbcnt_hi((uint32_t)(wm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wm, 0u))] =
-#else
-        const uint64_t wm = __ballot(want);
-        if (want) {
-          wrec[(size_t)w * LL + ecnt + (uint32_t)__popcll(wm & lanelt)] =
-#endif
               ((start - wlo) << 32) | ((uint64_t)hp << LP_HOP_SHIFT) | ((uint64_t)im << LP_IM_SHIFT) | i;
         }
         ecnt += (uint32_t)__popcll(wm);
