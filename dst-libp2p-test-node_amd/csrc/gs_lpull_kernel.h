@@ -153,6 +153,19 @@ struct LPullLds {
   uint16_t lst[PULL_WAVES][CH * 64];
 };
 
+// Listed entries e[0..3] (entry = toff << (tshift + lb) | low << lb | lane, so
+// key = (wlo << tshift) + (entry >> lb)) into the row's candidate minima.
+__device__ __forceinline__ void lp_apply_entries(uint64_t* CW, const uint64_t (&e)[4], uint32_t lmask, uint32_t lb,
+                                                 uint64_t wlok, uint32_t& cb) {
+#pragma unroll
+  for (int u = 0; u < 4; u++) {
+    if (e[u] == ~0ull) continue;
+    const uint32_t li = (uint32_t)e[u] & lmask;
+    atomicMin((unsigned long long*)&CW[li], (unsigned long long)(wlok + (e[u] >> lb)));
+    cb |= 1u << (li >> 6);
+  }
+}
+
 // ---- lazy gossip inside the passes (GOS batches) ----
 //
 // IHAVE rules (libp2p-gossipsub emit_gossip / handle_ihave / handle_iwant,
@@ -473,33 +486,22 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     const uint32_t sw = a.stage[a.u0 + w];
     // final bits transposed: lane j holds bit q for lane q*64 + j (u16 per lane)
     uint32_t finT = reinterpret_cast<const uint16_t*>(a.fin + (size_t)w * LP_FW)[lane];
-    // 1. the entries listed for window c (final lanes are dropped in step 3)
+    // 1 + 2. the entries listed for window c and this pass's candidates from
+    //    the neighbours' records of window lo, min-reduced per lane in CW (final
+    //    lanes are dropped in step 3). The first 256 entries are applied after
+    //    the first neighbour group's record loads are issued: one memory round
+    //    trip for both instead of two in a row.
     uint32_t cb = 0;
-    if (due) {
-      const uint64_t* lst = a.blk + ((size_t)cslot * a.N + w) * a.ls;
-      // entry = toff << (tshift + lb) | low << lb | lane, so key = (wlo +
-      // toff) << tshift | low = (wlo << tshift) + (entry >> lb)
-      const uint32_t lmask = (1u << a.lb) - 1;
-      const uint64_t wlok = wlo << a.tshift;
-      for (uint32_t f0 = 0; f0 < due; f0 += 256) {
-        uint64_t e[4];
+    const uint64_t* lst = a.blk + ((size_t)cslot * a.N + w) * a.ls;
+    const uint32_t lmask = (1u << a.lb) - 1;
+    const uint64_t wlok = wlo << a.tshift;
+    uint64_t e[4];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-          const uint32_t f = f0 + u * 64 + lane;
-          e[u] = f < due ? lst[f] : ~0ull;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-          if (e[u] == ~0ull) continue;
-          const uint32_t li = (uint32_t)e[u] & lmask;
-          const uint64_t key = wlok + (e[u] >> a.lb);
-          atomicMin((unsigned long long*)&CW[li], (unsigned long long)key);
-          cb |= 1u << (li >> 6);
-        }
-      }
+    for (int u = 0; u < 4; u++) {
+      const uint32_t f = u * 64 + lane;
+      e[u] = f < due ? lst[f] : ~0ull;
     }
-    PP_T(tG);
-    PP_ADD(1, tG - tA);
+    bool ent = true;  // wave-uniform: the first entries still to apply
     // 2. this pass's candidates from the neighbours' records of window lo
     if (pull) {
       const uint32_t sd = sdn[sw];
@@ -557,6 +559,10 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
               const auto v = __builtin_amdgcn_raw_buffer_load_b64(RS[k], i * 8u, 0, 0);
               rec[k][cc] = ((uint64_t)v[1] << 32) | v[0];
             }
+          if (ent) {  // the listed entries while the records are in flight
+            ent = false;
+            lp_apply_entries(CW, e, lmask, a.lb, wlok, cb);
+          }
 #pragma unroll
           for (int k = 0; k < (int)NG; k++)
 #pragma unroll
@@ -581,6 +587,17 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
         }
       }
     }
+    if (ent) lp_apply_entries(CW, e, lmask, a.lb, wlok, cb);  // no records
+    for (uint32_t f0 = 256; f0 < due; f0 += 256) {  // more than 256 entries (rare)
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const uint32_t f = f0 + u * 64 + lane;
+        e[u] = f < due ? lst[f] : ~0ull;
+      }
+      lp_apply_entries(CW, e, lmask, a.lb, wlok, cb);
+    }
+    PP_T(tG);
+    PP_ADD(1, tG - tA);
     // 2b. lazy gossip (GOS): IHAVEs of the built heartbeat k landing in window c
     //     from the row's non-mesh connections v. Every entry and record of the
     //     window is in CW now, so w has the message by the IHAVE's arrival t_i
