@@ -132,6 +132,9 @@ def launch_ranks(n, argv, cmd=None, env=None, out=None):
     return rc
 
 
+DIST = {}  # the torch.distributed backend of this run (dist_setup)
+
+
 def dist_setup():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -143,17 +146,26 @@ def dist_setup():
     except ImportError:
         pass
     if world > 1:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # one GPU per rank over RCCL; ranks sharing a GPU (a rehearsal of the
+        # N-rank path on a box with fewer GPUs: RCCL refuses two ranks on one
+        # device) reduce their few timing / counter scalars over gloo instead
+        # (message sharding has no data-path collective either way)
+        ndev = torch.cuda.device_count() if torch is not None else 0
+        shared = ndev > 0 and ndev < int(os.environ.get("LOCAL_WORLD_SIZE", world))
+        backend = os.environ.get("GS_BENCH_BACKEND") or ("nccl" if ndev and not shared else "gloo")
+        if ndev:
+            local = local % ndev
         if backend == "nccl":
             torch.cuda.set_device(local)
         dist.init_process_group(backend)
+        DIST.update(backend=backend, ranks=world, ranks_share_gpus=bool(shared))
     return world, rank, local, torch, dist
 
 
 def allreduce(torch, dist, world, vals, op):
     if world == 1:
         return vals
-    dev = "cuda" if torch.cuda.is_available() else "cpu"
+    dev = "cuda" if DIST.get("backend") == "nccl" else "cpu"
     t = torch.tensor(vals, dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=op)
     return t.tolist()
@@ -557,6 +569,7 @@ def main():
             "frag_deliveries": int(tot[1]),
             "relaxations": int(tot[2]),
             "bytes_alg": int(tot[3]),
+            "dist": DIST or None,
             "setup_s": t_setup,
             "mesh_epochs": epochs,
             "buckets_per_step": st["buckets"] / max(1, args.steps),
