@@ -1173,10 +1173,11 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
   for (uint64_t i = 0; i < n_msgs; i++) Fmax = std::max(Fmax, frags_of(c, sched[i]));
   const uint32_t FPmax = pow2_at_least(Fmax);
   const char* var_env = getenv("GS_RELAX_VARIANT");
-  // default: owner-computes pull over candidate lists (64 | 32; + 128: fragmented batches
-  // too; k_pull's dense rows without 64);
-  // without 32 the push path: split (8) + final bitset (4) + read filter (1)
-  uint32_t variant = var_env && *var_env ? (uint32_t)atoi(var_env) : 109u;
+  // default: owner-computes pull over candidate lists (64 | 32), fragmented batches
+  // too (128; config #2 7.2e8 against 6.7e8/s on k_pull's dense rows, round 4);
+  // k_pull's dense rows without 64; without 32 the push path: split (8) + final
+  // bitset (4) + read filter (1)
+  uint32_t variant = var_env && *var_env ? (uint32_t)atoi(var_env) : 237u;
   const bool lanes32 = (uint64_t)N * Bmax * FPmax < (1ull << 32);  // frontier indices are u32
   if (!lanes32) variant &= ~8u;
   const bool gossip = c.cfg.lazy_gossip != 0;
@@ -1484,8 +1485,8 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       if (pull_ok) {
         const uint64_t grain = pull_grain(b.tshift);
         uint32_t lb = 0;
-        // list path for single-fragment batches; fragmented ones (FP > 1) only
-        // with bit 128 (k_pull's dense rows measured 7 % faster on config #2)
+        // list path for single-fragment batches; fragmented ones (FP > 1) with
+        // bit 128 (the default)
         const bool lp = (variant & 64) && (b.FP == 1 || (variant & 128));
         const uint32_t K = lp ? lpull_ring(c, bw, bw.delta / grain * grain, &lb) : 0u;
         reset(variant, false, K == 0 || idw_b);  // IDONTWANT: dense INF keys
