@@ -216,7 +216,6 @@ struct Ctx {
   DevBuf<uint32_t> d_gpl;      // [N][32] sender planes of the built heartbeat
   DevBuf<uint64_t> d_gse;      // [N][L] their entries
   DevBuf<uint32_t> d_rowdone;  // [(N + 31) / 32]
-  DevBuf<uint64_t> d_ispub;    // [(N + 63) / 64] the batch's publishers (list pass)
   DevBuf<uint64_t> d_gctl;     // [GC_WORDS]
   bool glp_prefer = false;     // the last eager no-op proof failed: run gossip batches on the list pass first
 

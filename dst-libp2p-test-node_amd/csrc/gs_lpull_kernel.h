@@ -114,15 +114,7 @@ struct LPullArgs {
   const uint8_t* flags;
   const uint8_t* csrpos;      // position of the row's peer in its neighbour's row
   const uint64_t* habs0;      // [B] absolute index of each message's heartbeat 0
-  const uint64_t* ispub;      // [(peers + 63) / 64] peers publishing in this batch (global ids)
 };
-
-// Bit 8 of a row's rpos lane j: mesh neighbour j publishes a message of the
-// batch (the emit step then needs the lanes' publishers to exclude it).
-__device__ __forceinline__ uint32_t lp_pubbit(const uint64_t* ispub, uint32_t e) {
-  const uint32_t u = e & 0xFFFFFFu;
-  return (uint32_t)((ispub[u >> 6] >> (u & 63)) & 1u) << 8;
-}
 
 // gctl words (k_lctl writes them between passes; k_gsend / k_lpull only read)
 enum : uint32_t {
@@ -456,7 +448,6 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
       cj = rcnt[ej & 0xFFFFFFu];
       if constexpr (PART) ro = a.roff[ej & 0xFFFFFFu];
     }
-    if (FP == 1 && ej != EMPTY) rj |= lp_pubbit(a.ispub, ej);
     sv = a.st[(size_t)w * LP_SW + lane];
   }
   uint32_t dw = 0;  // gossip windows: the row-done word of row w (every lane reads it)
@@ -486,7 +477,6 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
         cj2 = rcnt[ej2 & 0xFFFFFFu];
         if constexpr (PART) ro2 = a.roff[ej2 & 0xFFFFFFu];
       }
-      if (FP == 1 && lane < (int)MESH_W && ej2 != EMPTY) rj2 |= lp_pubbit(a.ispub, ej2);
       ej = ej2; rj = rj2; cj = cj2; sv = sv2; ro = ro2; dw = dw2;
       PP_T(tS);
       PP_ADD(0, tS - tA);
@@ -538,7 +528,7 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
           else
             RO[k] = (uint64_t)U[k] * LL;
           // w's bit in the record's inclusion mask, and the bits below it
-          const uint32_t r = __builtin_amdgcn_readlane(rj, j) & 0xFFu;
+          const uint32_t r = __builtin_amdgcn_readlane(rj, j);
           IB[k] = 1u << (LP_IM_SHIFT + r);
           LB[k] = ((1u << r) - 1u) << LP_IM_SHIFT;
           NN[k] = bit ? (uint32_t)__builtin_amdgcn_readlane(cj, j) : 0u;
@@ -623,7 +613,6 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
       cj2 = rcnt[ej2 & 0xFFFFFFu];
       if constexpr (PART) ro2 = a.roff[ej2 & 0xFFFFFFu];
     }
-    if (FP == 1 && lane < (int)MESH_W && ej2 != EMPTY) rj2 |= lp_pubbit(a.ispub, ej2);
     // 3. classify the minima of the touched chunks: final lanes are dropped
     //    (candidates are not filtered on the way in), a minimum in window c is
     //    final now (logged, marked, its lane / group indexed from the front of
@@ -731,10 +720,6 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     uint32_t ecnt = 0;
     if (cnt) {
       const uint32_t deg = (uint32_t)__popcll(__ballot(ej != EMPTY));  // rows are packed
-      // the lanes' publishers only matter when one of them is in the mesh row
-      // (rows of one fragment: < 1 % of rows at 1M peers x 1024 messages); a
-      // load here would also wait for the append step's stores
-      const bool anypub = FP > 1 || __builtin_amdgcn_uicmp(rj & 0x100u, 0u, 33) != 0;
       const uint32_t serw = sup[sw];
       constexpr uint32_t GPW = 64 / FP;
       for (uint32_t g0 = 0; g0 < cnt; g0 += GPW) {
@@ -743,7 +728,7 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
         const uint32_t grp = gv ? LST[gi] : 0;
         const uint32_t i = grp * FP + (lane & (FP - 1));
         const uint64_t x = gv ? CW[i] : INF64;  // final lanes were set to INF in step 3
-        const uint32_t pm = gv && anypub ? a.pub[grp] : EMPTY;
+        const uint32_t pm = gv ? a.pub[grp] : EMPTY;
         // FP == 1: LST holds only lanes final in window c; a fragment group's
         // other lanes are re-checked
         const bool act = gv && (FP == 1 || (x != INF64 && ((uint32_t)(x >> 32) - hlo) < hspan)) && a.u0 + w != pm;
@@ -1058,12 +1043,6 @@ __global__ void k_lpub(LPullArgs a, uint32_t Fe) {
   const uint32_t pos = atomicAdd(&a.st[(size_t)p * LP_SW + LP_LOG], 1u);
   a.keys[(size_t)p * a.L + pos] = (uint64_t)(p + a.u0);
   a.flane[(size_t)p * a.L + pos] = (uint16_t)i;
-}
-
-// The batch's publishers as a bitset over the global peer ids (LPullArgs::ispub).
-__global__ void k_pubbits(const uint32_t* __restrict__ pub, uint32_t B, uint64_t* __restrict__ bits) {
-  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
-  if (m < B) atomicOr((unsigned long long*)&bits[pub[m] >> 6], 1ull << (pub[m] & 63));
 }
 
 // Final logs -> dense [N][L] key rows (INF where nothing arrived), in place:

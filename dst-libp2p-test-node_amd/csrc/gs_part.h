@@ -655,7 +655,6 @@ static LPullArgs part_lp_args(Ctx& c) {
   la.u0 = c.part_u0;
   la.rmax = lpull_rmax(b);
   la.rpk = c.d_rpk.p; la.roff = c.d_roffg.p; la.rcg = c.d_rcg.p;
-  la.ispub = c.d_ispub.p;
   la.pass = c.part_lppass;
   return la;
 }
@@ -721,10 +720,6 @@ bool part_lp_begin(Ctx& c, const gs_publish* sched, uint64_t n_msgs, uint64_t* s
   k_lseed<<<(unsigned)std::max<uint64_t>(1, std::min<uint64_t>((scap + TB - 1) / TB, (uint64_t)c.num_cus * 4)), TB, 0,
             s>>>(la, c.d_skey.p, c.d_slane.p, c.d_scnt.p);
   k_lpub<<<(b.B * b.Fe + 255) / 256, 256, 0, s>>>(la, b.Fe);
-  GS_HIP(hipGetLastError());
-  c.d_ispub.alloc(((size_t)N + 63) / 64);  // the batch's publishers over the global ids (k_lpull's emit step)
-  GS_HIP(hipMemsetAsync(c.d_ispub.p, 0, ((size_t)N + 63) / 64 * 8, s));
-  k_pubbits<<<(b.B + 255) / 256, 256, 0, s>>>(c.d_pub.p, b.B, c.d_ispub.p);
   GS_HIP(hipGetLastError());
   uint64_t auto_bpc = 4;  // as run_lpull_batch: whole blocks per CU by the rows this part owns
   while (auto_bpc < 16 && (uint64_t)un >= (uint64_t)c.num_cus * PULL_WAVES * 32 * auto_bpc * 2) auto_bpc *= 2;

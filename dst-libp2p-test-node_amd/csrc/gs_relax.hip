@@ -1060,10 +1060,6 @@ static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvF
   k_lseed<<<(unsigned)std::max<uint64_t>(1, std::min<uint64_t>((scap + TB - 1) / TB, (uint64_t)dev_cus * 4)), TB, 0, s>>>(
       la, c.d_skey.p, c.d_slane.p, c.d_scnt.p);
   k_lpub<<<(b.B * b.Fe + 255) / 256, 256, 0, s>>>(la, b.Fe);
-  c.d_ispub.alloc(((size_t)N + 63) / 64);
-  GS_HIP(hipMemsetAsync(c.d_ispub.p, 0, ((size_t)N + 63) / 64 * 8, s));
-  k_pubbits<<<(b.B + 255) / 256, 256, 0, s>>>(c.d_pub.p, b.B, c.d_ispub.p);
-  la.ispub = c.d_ispub.p;
   GS_HIP(hipGetLastError());
   if (gos) {  // GOS: sender planes, row-done bits, heartbeat control (gs_lpull_kernel.h)
     ensure_csrpos(c);
