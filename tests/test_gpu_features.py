@@ -331,3 +331,27 @@ def test_checkpoint_resume(tmp_path, case):
     assert _stats_no_time(res) == _stats_no_time(whole)
     assert res.stats()["deliveries"] == ref["stats"]["deliveries"]
     np.testing.assert_array_equal(res.traffic(), whole.traffic())
+
+
+@pytest.mark.parametrize("case", ["rust", "nim_self_log", "gossip_370", "gossip_55", "not_lockstep"])
+def test_completion_counted_by_the_passes(case):
+    """Results left on the device (nothing streamed out, the bench's path): the
+    counters come from the list pass's final logs (k_lcomplete) and the lazy
+    gossip no-op proof from its per-message reductions; lockstep or not, with
+    gossip proven a no-op or taken inside the passes, they equal the oracle's."""
+    N, M = 1400, 24
+    kw = dict(peers=N, seed=77)
+    if case.startswith("gossip"):
+        kw.update(hb_phase_ns=(T0 + int(case.split("_")[1]) * 1_000_000) % 1_000_000_000)
+    p = oracle.params_for("nim", **kw) if case == "nim_self_log" else oracle.params(**kw)
+    sched = _sched(M, N)
+    if case == "not_lockstep":  # publish times off the heartbeat grid by different amounts
+        t = np.asarray(sched[0], np.uint64) + (np.arange(M, dtype=np.uint64) * np.uint64(7_777_777))
+        sched = (t, sched[1], sched[2])
+    ref = oracle.simulate(p, 5, (50, 150, 40, 130), sched=sched)
+    sim, _ = gpu_sim(p, 5, (50, 150, 40, 130), batch=8)
+    sim.run(sched, collect=False)
+    st = sim.stats()
+    for k in ("deliveries", "relaxations", "gossip_iwant", "latency_sum_ms", "latency_max_ms"):
+        assert st[k] == ref["stats"][k], k
+    assert st["list_pull_batches"] >= 1
