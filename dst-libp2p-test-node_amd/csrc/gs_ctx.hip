@@ -157,6 +157,7 @@ extern "C" gs_status gs_build_topology(gs_ctx* ctx) {
   if (ctx->max_degree > MAX_DEG) ctx->fail(GS_EUNSUPPORTED, "peer degree exceeds 256");
   ctx->topo_built = true;
   ctx->csrpos_valid = false;
+  ctx->cell_valid = false;
   ctx->mesh_built = false;
   GS_API_END(ctx)
 }
@@ -450,6 +451,7 @@ extern "C" gs_status gs_load_state(const char* path, int32_t device, gs_ctx** ou
     if (has_until) get_dev(*c, f, c->d_until, c->nnz);
     c->topo_built = fl[1] != 0;
     c->csrpos_valid = false;
+    c->cell_valid = false;
     if (fl[2]) {
       get_dev(*c, f, c->d_mesh, (size_t)N * MESH_W);
       get_dev(*c, f, c->d_mcnt, N);

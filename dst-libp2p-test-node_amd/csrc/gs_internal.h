@@ -114,6 +114,9 @@ struct Ctx {
   DevBuf<uint64_t> d_gout;        // scratch of ring_in_lists: IHAVE target masks over CSR rows, per (epoch, sender)
   DevBuf<uint8_t> d_csrpos;       // [nnz] position of the row's peer in its neighbour's row (ring_in_lists, GOS)
   bool csrpos_valid = false;      // d_csrpos is of the current CSR
+  DevBuf<uint64_t> d_ring_mm;     // [R][N] mesh of each epoch as a mask over the CSR row (max_degree <= 64)
+  std::vector<uint64_t> ring_in_tag;  // [R] epoch whose inverse IHAVE lists a slot holds (~0: none)
+  bool ring_in_defer = false;         // the churn list pass takes the batch: no inverse lists beside the epochs
   DevBuf<uint64_t> d_q0, d_r0;  // [B] epoch of t_pub, t_pub - start of that epoch
   uint32_t ring_R = 0;
   uint64_t churn_state = 0, ring_lo = 1, ring_hi = 0;  // mesh state epoch; valid ring epochs
@@ -218,6 +221,17 @@ struct Ctx {
   DevBuf<uint32_t> d_rowdone;  // [(N + 31) / 32]
   DevBuf<uint64_t> d_gctl;     // [GC_WORDS]
   bool glp_prefer = false;     // the last eager no-op proof failed: run gossip batches on the list pass first
+  // churn on the list pass (gs_cpull.h, k_lpull<.., CHN>): the CSR rows as 64-wide ELL rows (once
+  // per topology), per batch the per-epoch mesh / IHAVE-eligible masks of every row over the
+  // batch's epochs, each peer's offline epochs, and the offline lanes per relative epoch
+  DevBuf<uint32_t> d_ccol;     // [N][64] stage << 24 | peer, ascending, EMPTY padded
+  DevBuf<uint8_t> d_cpos;      // [N][64] position of the row's peer in that neighbour's row
+  bool cell_valid = false;
+  DevBuf<uint64_t> d_cmm, d_cge;  // [N][cE]
+  DevBuf<uint64_t> d_offe;     // [N][cW] offline bit per epoch of the batch range
+  DevBuf<uint32_t> d_coff;     // [H + 2][N][32] offline lanes per relative epoch (transposed like the final bits)
+  DevBuf<uint32_t> d_cq;       // [B] epoch of t_pub - first epoch of the range
+  DevBuf<uint8_t> d_pubok;     // [B] the publisher was online at t_pub
 
   // stats
   gs_stats stats{};
@@ -235,6 +249,7 @@ void launch_topology(Ctx& c);
 uint32_t run_mesh(Ctx& c, uint32_t max_heartbeats);
 void churn_ring(Ctx& c, uint64_t h_lo, uint64_t h_hi);
 void ensure_csrpos(Ctx& c);
+void ensure_in_lists(Ctx& c, uint64_t h0, uint64_t h1);
 void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_result_sink* sink);
 void deliver_rows(Ctx& c, uint32_t B, uint32_t un, const gs_result_sink* sink, uint64_t sink_row0);
 void part_set(Ctx& c, uint32_t parts, uint32_t part);

@@ -114,6 +114,19 @@ struct LPullArgs {
   const uint8_t* flags;
   const uint8_t* csrpos;      // position of the row's peer in its neighbour's row
   const uint64_t* habs0;      // [B] absolute index of each message's heartbeat 0
+  // churn on the list pass (k_lpull<1, CH, false, false, GOS, true>; gs_cpull.h): a lockstep
+  // batch whose lane m at relative time t is in epoch E0 + cq[m] + k(t), k(t) = floor((cr0 + t) / chb)
+  const uint32_t* ccol;  // [N][64] CSR rows, stage << 24 | peer, EMPTY padded (the row header)
+  const uint8_t* cpos;   // [N][64] position of the row's peer in that neighbour's CSR row
+  const uint64_t* cmm;   // [N][cE] mesh of each epoch as a mask over the row's CSR entries
+  const uint64_t* cge;   // [N][cE] IHAVE-eligible entries per epoch (online, outside the mesh; 0: offline)
+  const uint32_t* coff;  // [chz + 2][N][LP_FW] offline lanes per relative epoch (fin's layout)
+  const uint32_t* cq;    // [B]
+  const uint8_t* pubok;  // [B] the publisher was online at t_pub (k_lpub; nullptr: all)
+  uint64_t cr0, chb;
+  uint32_t cE, chz;      // epochs per row of cmm / cge; the lifetime in epochs (churn_horizon)
+  uint32_t ghoff;        // GOS: relative epoch of heartbeat 0 (habs0 - q0: 0 or 1)
+  uint32_t ghk;          // GOS: last heartbeat index whose IHAVEs are inside the lifetime (~0u: no cap)
 };
 
 // gctl words (k_lctl writes them between passes; k_gsend / k_lpull only read)
@@ -132,6 +145,9 @@ enum : uint32_t {
 constexpr uint32_t GSE_HOPS = 58;  // entry bits [0, 58): target mask over the sender's CSR row
 
 constexpr uint32_t LP_FW = PULL_LMAX / 32;  // u32 final-bit words per row
+constexpr uint32_t CELL_W = 64;             // churn: CSR entries per 64-wide ELL row header (the mask width)
+// churn records (CHN) are 16 B: the word above with the 16 mask bits unused, then
+// the sender's 64-bit receiver mask over its CSR row
 
 __device__ __forceinline__ uint32_t sat32(uint64_t x) { return x > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)x; }
 
@@ -293,6 +309,72 @@ __device__ __forceinline__ void glp_ihave(const LPullArgs& a, uint64_t* CW, uint
   }
 }
 
+// Receiver side under churn (CHN): the epoch's mesh differs per lane, so every
+// CSR neighbour v (lane e of the row header: ej / rj) may send IHAVEs; v's entry
+// says whether w is a target (targets are online connections outside v's mesh
+// at the heartbeat's epoch kh), lanes where w is offline at kh get none (offh),
+// and an answer landing at or after gB1 (the start of epoch kh + 1) is lost
+// where w is offline then or past the lifetime (offa): no IWANT is counted for
+// it (the oracle's lost_a).
+__device__ __forceinline__ void glp_ihave_chn(const LPullArgs& a, uint64_t* CW, uint32_t sw, uint32_t finT, uint64_t wlo,
+                                              uint64_t gR, uint32_t ej, uint32_t rj, uint32_t offh, uint32_t offa,
+                                              uint64_t gB1, const uint32_t* lat, const uint32_t* sup,
+                                              const uint32_t* sdn, uint32_t& cb, uint64_t& niw, uint32_t& err) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t S = a.S;
+  wave_lds_sync();  // the window's entries and records are in CW
+  uint32_t tio = 0, aoff = 0;
+  bool ok = false;
+  if (ej != EMPTY) {
+    const uint32_t sv = ej >> STAGE_SHIFT;
+    tio = lat[sv * S + sw];  // t_i - R_k
+    const uint64_t ti = gR + tio;
+    ok = ti >= wlo && ti < wlo + a.delta;
+    const uint32_t su = sup[sv], sd = sdn[sw];
+    aoff = lat[sw * S + sv] + su + tio + (sd > su ? sd - su : 0u);  // IWANT + answer: t_i -> arrival
+  }
+  uint64_t gm = __ballot(ok);
+  const uint32_t nfl = ~finT & ~offh & 0xFFFFu;  // not final before window c, online at kh
+  while (gm) {  // wave-uniform: one IHAVE sender at a time
+    const int e = __builtin_ctzll(gm);
+    gm &= gm - 1;
+    const uint32_t v = __builtin_amdgcn_readlane(ej, e) & 0xFFFFFFu;
+    const uint32_t p = __builtin_amdgcn_readlane(rj, e);
+    const uint64_t ti = gR + (uint32_t)__builtin_amdgcn_readlane(tio, e);
+    const uint64_t A = ti + (uint32_t)__builtin_amdgcn_readlane(aoff, e);
+    const uint32_t plj = reinterpret_cast<const uint16_t*>(a.gpl + (size_t)v * LP_FW)[lane];
+    uint32_t c = plj & nfl;
+    if (__ballot(c != 0) == 0) continue;
+    const uint32_t lost = A >= gB1 ? offa : 0u;  // lanes whose answer is lost
+    const uint32_t own = (uint32_t)__popc(plj);
+    uint32_t pre = own;
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = __shfl_up(pre, off);
+      if (lane >= off) pre += y;
+    }
+    pre -= own;
+    const uint64_t* ge = a.gse + (size_t)v * a.L;
+    const uint64_t kb = (A << a.tshift) | v;
+    const bool tbad = A > a.tmax;
+    while (c) {
+      const int q = __builtin_ctz(c);
+      c &= c - 1;
+      const uint64_t en = ge[pre + (uint32_t)__popc(plj & ((1u << q) - 1u))];
+      if (!((en >> p) & 1)) continue;  // w is not among v's targets at heartbeat k
+      if ((lost >> q) & 1) continue;   // the answer reaches w offline / past the lifetime
+      const uint32_t i = (uint32_t)q * 64 + lane;
+      const uint64_t x = CW[i];
+      if (x != INF64 && (x >> a.tshift) <= ti) continue;  // w has it by t_i (arrivals first at equal time)
+      niw++;
+      const uint32_t hv = (uint32_t)(en >> GSE_HOPS) + 1;
+      if (hv >= (1u << HOP_BITS)) err |= ERR_HOPS;
+      if (tbad) err |= ERR_TIME;
+      atomicMin((unsigned long long*)&CW[i], (unsigned long long)(kb | ((uint64_t)hv << a.sb)));
+      cb |= 1u << q;
+    }
+  }
+}
+
 // Record step: groups of NG = 4 neighbours, RCH = 2 chunks of 64 records each
 // per iteration (8 loads in flight per lane; 8 x 64 measured 2 % slower,
 // profiles/r03_v1/ab_record_groups.txt). GS_LP_NG / GS_LP_RCH: A/B builds.
@@ -302,11 +384,15 @@ __device__ __forceinline__ void glp_ihave(const LPullArgs& a, uint64_t* CW, uint
 #ifndef GS_LP_RCH
 #define GS_LP_RCH 2
 #endif
-template <int FP, uint32_t CH, bool IDW = false, bool PART = false, bool GOS = false>
+template <int FP, uint32_t CH, bool IDW = false, bool PART = false, bool GOS = false, bool CHN = false>
 __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
   constexpr uint32_t NG = GS_LP_NG, RCH = GS_LP_RCH;
   static_assert(!IDW || FP == 1, "IDONTWANT on the list pass: rows of single-fragment lanes");
   static_assert(!GOS || (FP == 1 && !IDW && !PART), "gossip on the list pass: gs_run's single-fragment rows");
+  static_assert(!CHN || (FP == 1 && !IDW && !PART), "churn on the list pass: gs_run's single-fragment rows");
+  // row header: the mesh row (frozen mesh) or, under churn, the CSR row (the
+  // mesh of a lane's epoch is a mask over it)
+  constexpr uint32_t HW = CHN ? CELL_W : MESH_W;
   constexpr uint32_t LMAX = CH * 64;
   __shared__ LPullLds<CH> Ls;
   uint64_t* me = a.ctrl + (a.pass % 3) * 4;
@@ -344,9 +430,10 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
   const float rinv = 1.0f / (float)a.dG;
   const size_t NL = (size_t)a.N * LL;
   const uint32_t pb = (a.pass + 1) & 1, nb = a.pass & 1;  // records read / written
-  const uint64_t* rrec = PART ? a.rpk : a.lrec + pb * NL;
+  constexpr uint32_t RW = CHN ? 2 : 1;  // u64 words per record
+  const uint64_t* rrec = PART ? a.rpk : a.lrec + pb * NL * RW;
   const uint32_t* rcnt = PART ? a.rcg : a.lcnt + (size_t)pb * a.N;  // indexed by global peer id
-  uint64_t* wrec = a.lrec + nb * NL;
+  uint64_t* wrec = a.lrec + nb * NL * RW;
   uint32_t* wcnt = a.lcnt + (size_t)nb * a.N;
   const uint32_t* lat = a.tables;
   const uint32_t* sup = a.tables + S * S;
@@ -359,6 +446,33 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     gR = a.grel0 + (a.gctl[GC_BK] - 1) * a.ghb;
   }
   uint64_t niw = 0;  // IWANTs sent
+  // churn (CHN): the epoch boundaries the pass can meet. A record whose sender
+  // started before xBs (time) arrives in the sender's epoch ks unless it lands
+  // at or after xBs: then it is lost where the receiver is offline in ks + 1
+  // (offn; the sender's mesh of ks held only peers online in ks). Window c
+  // starts in relative epoch kc and, when it straddles a boundary, its lanes
+  // final at or after eBc forward with the mesh of kc + 1.
+  uint64_t xBs = INF64, eBc = INF64;
+  uint32_t xBoff = 0, kc = 0;
+  const uint32_t* offn = nullptr;
+  uint32_t gkh = 0;     // GOS + CHN: relative epoch of the built heartbeat
+  uint64_t gB1 = INF64;  // its next epoch's start (relative time)
+  if constexpr (CHN) {
+    const uint64_t ks = udiv53(a.cr0 + lo, a.chb), Bs = (ks + 1) * a.chb - a.cr0;
+    if (pull && Bs < lo + a.delta + a.rmax) {
+      xBs = Bs << a.tshift;
+      xBoff = (uint32_t)(Bs - lo);
+      offn = a.coff + (size_t)(ks + 1 <= a.chz + 1 ? ks + 1 : a.chz + 1) * a.N * LP_FW;
+    }
+    kc = (uint32_t)udiv53(a.cr0 + wlo, a.chb);
+    const uint64_t Bc = ((uint64_t)kc + 1) * a.chb - a.cr0;
+    if (Bc < wlo + a.delta) eBc = Bc;
+    if constexpr (GOS) {
+      gkh = a.ghoff + (uint32_t)(a.gctl[GC_BK] ? a.gctl[GC_BK] - 1 : 0);
+      if (gkh > a.chz) gkh = a.chz;
+      gB1 = ((uint64_t)gkh + 1) * a.chb - a.cr0;
+    }
+  }
 
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint64_t* CW = Ls.cw[wv];
@@ -417,14 +531,30 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
       const uint32_t mh = mo == ~0u ? ~0u : sat32(hlo64 + (uint64_t)mo * a.dG);
       if (GOS && gw) act |= !((a.rowdone[wl >> 5] >> (wl & 31)) & 1u);
       if (pull && !act) {
-        const uint4* mp = reinterpret_cast<const uint4*>(a.mesh + (size_t)(a.u0 + wl) * MESH_W);
+        if constexpr (CHN) {  // CSR rows, 16 entries at a time until the padding
+          const uint4* mp = reinterpret_cast<const uint4*>(a.ccol + (size_t)wl * CELL_W);
+          for (int g = 0; g < (int)CELL_W / 16 && !act; g++) {
+            uint32_t e[16];
 #pragma unroll
-        for (int k = 0; k < (int)MESH_W / 4; k++) {
-          const uint4 m = mp[k];
-          const uint32_t e[4] = {m.x, m.y, m.z, m.w};
+            for (int k = 0; k < 4; k++) {
+              const uint4 m = mp[g * 4 + k];
+              e[4 * k] = m.x; e[4 * k + 1] = m.y; e[4 * k + 2] = m.z; e[4 * k + 3] = m.w;
+            }
 #pragma unroll
-          for (int u = 0; u < 4; u++)
-            if (e[u] != EMPTY) act |= rcnt[e[u] & 0xFFFFFFu] != 0;
+            for (int u = 0; u < 16; u++)
+              if (e[u] != EMPTY) act |= rcnt[e[u] & 0xFFFFFFu] != 0;
+            if (e[15] == EMPTY) break;
+          }
+        } else {
+          const uint4* mp = reinterpret_cast<const uint4*>(a.mesh + (size_t)(a.u0 + wl) * MESH_W);
+#pragma unroll
+          for (int k = 0; k < (int)MESH_W / 4; k++) {
+            const uint4 m = mp[k];
+            const uint32_t e[4] = {m.x, m.y, m.z, m.w};
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+              if (e[u] != EMPTY) act |= rcnt[e[u] & 0xFFFFFFu] != 0;
+          }
         }
       }
       if (!act) {
@@ -441,7 +571,14 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
   }
   uint32_t ej = EMPTY, cj = 0, rj = 0, sv = 0;
   uint64_t ro = 0, ro2 = 0;  // PART: offsets of the neighbours' packed records
-  if (w < a.N && lane < (int)MESH_W) {
+  if constexpr (CHN) {
+    if (w < a.N) {
+      ej = a.ccol[(size_t)w * CELL_W + lane];
+      rj = a.cpos[(size_t)w * CELL_W + lane];
+      if (pull && ej != EMPTY) cj = rcnt[ej & 0xFFFFFFu];
+      if (lane < (int)LP_SW) sv = a.st[(size_t)w * LP_SW + lane];
+    }
+  } else if (w < a.N && lane < (int)MESH_W) {
     ej = a.mesh[(size_t)(a.u0 + w) * MESH_W + lane];
     rj = a.rpos[(size_t)(a.u0 + w) * MESH_W + lane];
     if (pull && ej != EMPTY) {
@@ -458,7 +595,13 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     am &= am - 1;
     const uint32_t w2 = wn;
     uint32_t ej2 = EMPTY, rj2 = 0, cj2 = 0, sv2 = 0, dw2 = 0;
-    if (w2 < a.N && lane < (int)MESH_W) {  // w2 < N is wave-uniform
+    if constexpr (CHN) {
+      if (w2 < a.N) {
+        ej2 = a.ccol[(size_t)w2 * CELL_W + lane];
+        rj2 = a.cpos[(size_t)w2 * CELL_W + lane];
+        if (lane < (int)LP_SW) sv2 = a.st[(size_t)w2 * LP_SW + lane];
+      }
+    } else if (w2 < a.N && lane < (int)MESH_W) {  // w2 < N is wave-uniform
       ej2 = a.mesh[(size_t)(a.u0 + w2) * MESH_W + lane];
       rj2 = a.rpos[(size_t)(a.u0 + w2) * MESH_W + lane];
       sv2 = a.st[(size_t)w2 * LP_SW + lane];
@@ -473,7 +616,7 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     if (cand == 0 && due == 0 && !gossip_row) {  // nothing to apply, nothing due: the pending windows stay
       if (lane == 0) wcnt[w] = 0;
       if (lane < (int)K && sv) nmh = umin32(nmh, lwhi);
-      if (pull && lane < (int)MESH_W && ej2 != EMPTY) {
+      if (pull && lane < (int)HW && ej2 != EMPTY) {
         cj2 = rcnt[ej2 & 0xFFFFFFu];
         if constexpr (PART) ro2 = a.roff[ej2 & 0xFFFFFFu];
       }
@@ -486,6 +629,11 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     const uint32_t sw = a.stage[a.u0 + w];
     // final bits transposed: lane j holds bit q for lane q*64 + j (u16 per lane)
     uint32_t finT = reinterpret_cast<const uint16_t*>(a.fin + (size_t)w * LP_FW)[lane];
+    // churn: the row's lanes offline in the records' next epoch (crossing records)
+    uint32_t onl = 0;
+    if constexpr (CHN) {
+      if (offn) onl = reinterpret_cast<const uint16_t*>(offn + (size_t)w * LP_FW)[lane];
+    }
     // 1 + 2. the entries listed for window c and this pass's candidates from
     //    the neighbours' records of window lo, min-reduced per lane in CW (final
     //    lanes are dropped in step 3). The first 256 entries are applied after
@@ -502,8 +650,77 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
       e[u] = f < due ? lst[f] : ~0ull;
     }
     bool ent = true;  // wave-uniform: the first entries still to apply
+    // 2 (churn). 16-B records from the CSR neighbours: w's bit at its position
+    //    p in the sender's row (rj), FIFO position 1 + the receivers below p; a
+    //    record that crosses into the next epoch is dropped where w is offline
+    //    there (onl; lane `slot`'s bit fetched from lane slot & 63)
+    if constexpr (CHN) {
+      if (pull) {
+        const uint32_t sd = sdn[sw];
+        uint64_t cmk = cand;
+        while (cmk) {
+          uint32_t U[NG], NN[NG], SER[NG], IB0[NG], IB1[NG], LM0[NG], LM1[NG];
+          uint64_t BASE[NG];
+          uint32_t maxn = 0;
+#pragma unroll
+          for (int k = 0; k < (int)NG; k++) {
+            const uint64_t bit = cmk & (~cmk + 1);
+            cmk ^= bit;
+            const int j = bit ? (int)__builtin_ctzll(bit) : 0;
+            const uint32_t e = __builtin_amdgcn_readlane(ej, j);
+            U[k] = e & 0xFFFFFFu;
+            const uint32_t r = __builtin_amdgcn_readlane(rj, j) & 63u;
+            IB0[k] = r < 32 ? 1u << r : 0u;
+            IB1[k] = r < 32 ? 0u : 1u << (r - 32);
+            LM0[k] = r < 32 ? (1u << r) - 1u : ~0u;
+            LM1[k] = r < 32 ? 0u : (1u << (r - 32)) - 1u;
+            NN[k] = bit ? (uint32_t)__builtin_amdgcn_readlane(cj, j) : 0u;
+            const uint32_t su0 = e >> STAGE_SHIFT, su = su0 < S ? su0 : 0u;
+            SER[k] = sup[su];
+            BASE[k] = ((lo + lat[su * S + sw] + (sd > SER[k] ? sd - SER[k] : 0)) << a.tshift) +
+                      ((1ull << a.sb) | U[k]);
+            maxn = NN[k] > maxn ? NN[k] : maxn;
+          }
+          __amdgpu_buffer_rsrc_t RS[NG];
+#pragma unroll
+          for (int k = 0; k < (int)NG; k++)
+            RS[k] = __builtin_amdgcn_make_buffer_rsrc((void*)(rrec + (size_t)U[k] * LL * 2), (short)0,
+                                                      (int)(NN[k] * 16u), 0x00020000);
+          for (uint32_t i0 = 0; i0 < maxn; i0 += 64) {
+            uint32_t rv[NG][4];
+#pragma unroll
+            for (int k = 0; k < (int)NG; k++) {
+              const uint32_t i = i0 + lane;
+              const auto v = __builtin_amdgcn_raw_buffer_load_b128(RS[k], i * 16u, 0, 0);
+              rv[k][0] = v[0]; rv[k][1] = v[1]; rv[k][2] = v[2]; rv[k][3] = v[3];
+            }
+            if (ent) {
+              ent = false;
+              lp_apply_entries(CW, e, lmask, a.lb, wlok, cb);
+            }
+#pragma unroll
+            for (int k = 0; k < (int)NG; k++) {
+              const uint32_t lo32 = rv[k][0], so = rv[k][1];
+              bool ok = ((rv[k][2] & IB0[k]) | (rv[k][3] & IB1[k])) != 0;
+              const uint32_t slot = lo32 & LP_LANE_MASK;
+              const uint32_t pos = (uint32_t)__popc(rv[k][2] & LM0[k]) + (uint32_t)__popc(rv[k][3] & LM1[k]) + 1u;
+              const uint64_t off = (uint64_t)pos * SER[k] + so;
+              const uint64_t nk = BASE[k] + (((off << HOP_BITS) | (lo32 >> LP_HOP_SHIFT)) << a.sb);
+              if (offn) {  // wave-uniform: a record may cross into epoch ks + 1
+                const uint32_t ob = (uint32_t)__shfl((int)onl, (int)(slot & 63u));
+                if (so < xBoff && nk >= xBs && ((ob >> (slot >> 6)) & 1u)) ok = false;
+              }
+              if (ok) {
+                atomicMin((unsigned long long*)&CW[slot], (unsigned long long)nk);
+                cb |= 1u << (slot >> 6);
+              }
+            }
+          }
+        }
+      }
+    }
     // 2. this pass's candidates from the neighbours' records of window lo
-    if (pull) {
+    if (!CHN && pull) {
       const uint32_t sd = sdn[sw];
       uint64_t cmk = cand;
       while (cmk) {
@@ -523,8 +740,8 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
           const uint32_t e = __builtin_amdgcn_readlane(ej, j);
           U[k] = e & 0xFFFFFFu;
           if constexpr (PART)
-            RO[k] = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(ro >> 32), j) << 32) |
-                    __builtin_amdgcn_readlane((uint32_t)ro, j);
+            RO[k] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(ro >> 32), j) << 32) |
+                    (uint32_t)__builtin_amdgcn_readlane((uint32_t)ro, j);
           else
             RO[k] = (uint64_t)U[k] * LL;
           // w's bit in the record's inclusion mask, and the bits below it
@@ -603,13 +820,19 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     //     window is in CW now, so w has the message by the IHAVE's arrival t_i
     //     iff CW holds a time <= t_i there; else w sends IWANT and v's answer
     //     (its key's hops + 1, src v) is one more candidate, after window c.
-    if constexpr (GOS) {
+    if constexpr (GOS && CHN) {
+      if (gossip_row) {
+        const uint32_t offh = reinterpret_cast<const uint16_t*>(a.coff + ((size_t)gkh * a.N + w) * LP_FW)[lane];
+        const uint32_t offa = reinterpret_cast<const uint16_t*>(a.coff + ((size_t)(gkh + 1) * a.N + w) * LP_FW)[lane];
+        glp_ihave_chn(a, CW, sw, finT, wlo, gR, ej, rj, offh, offa, gB1, lat, sup, sdn, cb, niw, err);
+      }
+    } else if constexpr (GOS) {
       if (gossip_row) glp_ihave(a, CW, w, sw, finT, wlo, gR, lat, sup, sdn, cb, niw, err);
     }
     for (int off = 32; off > 0; off >>= 1) cb |= __shfl_xor(cb, off);
     cb = __builtin_amdgcn_readfirstlane(cb);
     wave_lds_sync();
-    if (pull && lane < (int)MESH_W && ej2 != EMPTY) {  // next row's lists
+    if (pull && lane < (int)HW && ej2 != EMPTY) {  // next row's lists
       cj2 = rcnt[ej2 & 0xFFFFFFu];
       if constexpr (PART) ro2 = a.roff[ej2 & 0xFFFFFFu];
     }
@@ -734,7 +957,17 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
         const bool act = gv && (FP == 1 || (x != INF64 && ((uint32_t)(x >> 32) - hlo) < hspan)) && a.u0 + w != pm;
         const uint32_t src = (uint32_t)(x & smask);
         uint32_t xm = 0;  // excluded mesh indices: source, publisher (IDW: and IDONTWANT)
-        if constexpr (IDW) {
+        uint64_t im64 = 0;  // churn: the receivers as a mask over the CSR row
+        if constexpr (CHN) {  // the mesh of the epoch the lane was received in, less source and publisher
+          const uint32_t kk = kc + ((x >> a.tshift) >= eBc ? 1u : 0u);
+          const uint64_t mmv = act ? a.cmm[(size_t)w * a.cE + a.cq[grp] + kk] : 0ull;
+          uint64_t xm64 = 0;
+          for (uint32_t k = 0; k < deg; k++) {  // wave-uniform: entry k from lane k
+            const uint32_t y = __builtin_amdgcn_readlane(ej, k) & 0xFFFFFFu;
+            xm64 |= (y == src || y == pm) ? 1ull << k : 0ull;
+          }
+          im64 = mmv & ~xm64;
+        } else if constexpr (IDW) {
           const uint64_t tw = x >> a.tshift;
           for (uint32_t k = 0; k < deg; k++) {  // wave-uniform: entry k from lane k
             const uint32_t e = __builtin_amdgcn_readlane(ej, k);
@@ -752,8 +985,8 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
             xm |= (y == src || y == pm) ? 1u << k : 0u;
           }
         }
-        const uint32_t im = ((1u << deg) - 1u) & ~xm;  // the receivers (deg <= MESH_W = 16)
-        const uint32_t n = act ? (uint32_t)__popc(im) : 0u;
+        const uint32_t im = CHN ? 0u : ((1u << deg) - 1u) & ~xm;  // the receivers (deg <= MESH_W = 16)
+        const uint32_t n = act ? (CHN ? (uint32_t)__popcll(im64) : (uint32_t)__popc(im)) : 0u;
         const uint64_t start = uplink_start<FP>(a.busy, (size_t)w * a.B + grp, act, x, n, serw, a.tshift);
         const uint32_t hp = (uint32_t)(x >> a.sb) & hmask;
         if (act) {
@@ -779,9 +1012,15 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
         const bool want = act && n != 0;
         const uint64_t wm = fm & __builtin_amdgcn_uicmp(n, 0u, 33);
         if (want) {
-          wrec[(size_t)w * LL + ecnt +
-               __builtin_amdgcn_mbcnt_hi((uint32_t)(wm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wm, 0u))] =
-              ((start - wlo) << 32) | ((uint64_t)hp << LP_HOP_SHIFT) | ((uint64_t)im << LP_IM_SHIFT) | i;
+          const size_t ri = (size_t)w * LL + ecnt +
+                            __builtin_amdgcn_mbcnt_hi((uint32_t)(wm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wm, 0u));
+          if constexpr (CHN) {
+            const uint64_t r0 = ((start - wlo) << 32) | ((uint64_t)hp << LP_HOP_SHIFT) | i;
+            *reinterpret_cast<uint4*>(wrec + ri * 2) =
+                make_uint4((uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)im64, (uint32_t)(im64 >> 32));
+          } else {
+            wrec[ri] = ((start - wlo) << 32) | ((uint64_t)hp << LP_HOP_SHIFT) | ((uint64_t)im << LP_IM_SHIFT) | i;
+          }
         }
         ecnt += (uint32_t)__popcll(wm);
       }
@@ -862,7 +1101,8 @@ __global__ void k_lctl(LPullArgs a) {
     g[GC_FDP] = fd;
   }
   const uint64_t tl = g[GC_TLAST];
-  const uint64_t kmax = (tl <= r0 ? 0 : (tl - r0 + hb - 1) / hb) + a.ghist - 1;  // last heartbeat with a sender
+  uint64_t kmax = (tl <= r0 ? 0 : (tl - r0 + hb - 1) / hb) + a.ghist - 1;  // last heartbeat with a sender
+  if (kmax > a.ghk) kmax = a.ghk;  // churn: no IHAVE past the messages' lifetime
   const bool gos = nf && a.ghist;
   uint64_t lo, mode;
   if (g[GC_DONE]) {
@@ -923,7 +1163,11 @@ __global__ void k_lctl(LPullArgs a) {
 // writes the plane and the entries (target mask | hops << 58) in rank order.
 // A row none of whose non-mesh connections has a lane left to finalise is
 // skipped: no pass reads its plane (row-done bits never clear within a batch).
-template <uint32_t CH>
+// Churn (CHN): a lane's epoch is E0 + cq[m] + kh (kh = ghoff + k, the
+// heartbeat's relative epoch), its IHAVE-eligible entries cge[v][..] (0 when v
+// is offline then), and nothing past the lifetime (kh > chz); lanes with no
+// target get no plane bit.
+template <uint32_t CH, bool CHN = false>
 __global__ __launch_bounds__(TB) void k_gsend(LPullArgs a) {
   const uint64_t bk = a.gctl[GC_BUILD];
   if (!bk) return;  // grid-uniform: nothing to build before this pass
@@ -937,13 +1181,20 @@ __global__ __launch_bounds__(TB) void k_gsend(LPullArgs a) {
   const uint64_t Rlo = haslo ? a.grel0 + (k - a.ghist) * a.ghb : 0;
   const uint32_t hmask = (1u << HOP_BITS) - 1;
   for (uint32_t v = blockIdx.x * PULL_WAVES + wv; v < a.N; v += gridDim.x * PULL_WAVES) {
-    const uint64_t rb = a.row[v];
-    const uint32_t deg = (uint32_t)(a.row[v + 1] - rb);
-    uint32_t x = EMPTY;
+    uint32_t deg, x = EMPTY;
     bool nm = false;
-    if ((uint32_t)lane < deg) {
-      x = a.col[rb + lane];
-      nm = !(a.flags[rb + lane] & F_MESH);
+    if constexpr (CHN) {
+      const uint32_t xe = a.ccol[(size_t)v * CELL_W + lane];
+      nm = xe != EMPTY;  // any connection may be outside the lane's epoch mesh
+      x = nm ? xe & 0xFFFFFFu : EMPTY;
+      deg = (uint32_t)__popcll(__ballot(nm));
+    } else {
+      const uint64_t rb = a.row[v];
+      deg = (uint32_t)(a.row[v + 1] - rb);
+      if ((uint32_t)lane < deg) {
+        x = a.col[rb + lane];
+        nm = !(a.flags[rb + lane] & F_MESH);
+      }
     }
     bool need = false;
     if (nm) need = !((a.rowdone[x >> 5] >> (x & 31)) & 1u);
@@ -977,8 +1228,18 @@ __global__ __launch_bounds__(TB) void k_gsend(LPullArgs a) {
       const uint32_t s = jv ? sel[wv][j0 + lane] : 0u;
       const uint32_t m = s & 0xFFFFu;
       const uint32_t h = jv ? (uint32_t)(a.habs0[m] + k) : 0u;
-      const uint64_t mask = glp_targets(a.gseed, v, h, x, nmm, deg, r);
-      if (jv) {
+      uint64_t lm = nmm;
+      uint32_t lr = r;
+      if constexpr (CHN) {  // the lane's epoch: its eligible set and fan-out
+        const uint32_t kh = a.ghoff + (uint32_t)k;
+        lm = jv && kh <= a.chz ? a.cge[(size_t)v * a.cE + a.cq[m] + kh] : 0ull;
+        const uint32_t nn = (uint32_t)__popcll(lm);
+        lr = (uint32_t)(((uint64_t)nn * a.ggf) / 1000);
+        if (lr < a.gd_lazy) lr = a.gd_lazy;
+        if (lr > nn) lr = nn;
+      }
+      const uint64_t mask = glp_targets(a.gseed, v, h, x, lm, deg, lr);
+      if (jv && (!CHN || mask)) {
         ent[wv][m] = mask | ((uint64_t)(s >> 16) << GSE_HOPS);
         atomicOr(&pl[wv][(m & 63) >> 1], 1u << (16 * (m & 1) + (m >> 6)));
       }
@@ -1033,6 +1294,7 @@ __global__ void k_lpub(LPullArgs a, uint32_t Fe) {
   if (g >= a.B * Fe) return;
   const uint32_t m = g / Fe, f = g % Fe, i = m * FP + f;
   if (a.pub[m] - a.u0 >= a.N) return;  // partitioned: another part's publisher
+  if (a.pubok && !a.pubok[m]) return;   // churn: an offline publisher publishes nothing
   const uint32_t p = a.pub[m] - a.u0;   // local row
   const uint32_t j = i & 63, q = i >> 6;  // transposed: lane j's u16, bit q
   atomicOr(&a.fin[(size_t)p * LP_FW + (j >> 1)], 1u << (16 * (j & 1) + q));
@@ -1248,6 +1510,16 @@ void lpull_dispatch_part(uint32_t FP, const LPullArgs& a, unsigned grid, hipStre
 // senders just became final, the pass itself (rows of one fragment).
 void lpull_dispatch_gos(const LPullArgs& a, unsigned grid, hipStream_t s) {
   k_lctl<<<1, 64, 0, s>>>(a);
+  if (a.ccol) {  // churn
+    if (lpull_chunks(a.L) == 8) {
+      k_gsend<8, true><<<grid, TB, 0, s>>>(a);
+      k_lpull<1, 8, false, false, true, true><<<grid, TB, 0, s>>>(a);
+    } else {
+      k_gsend<16, true><<<grid, TB, 0, s>>>(a);
+      k_lpull<1, 16, false, false, true, true><<<grid, TB, 0, s>>>(a);
+    }
+    return;
+  }
   if (lpull_chunks(a.L) == 8) {
     k_gsend<8><<<grid, TB, 0, s>>>(a);
     k_lpull<1, 8, false, false, true><<<grid, TB, 0, s>>>(a);
@@ -1258,6 +1530,11 @@ void lpull_dispatch_gos(const LPullArgs& a, unsigned grid, hipStream_t s) {
 }
 
 void lpull_dispatch(uint32_t FP, const LPullArgs& a, unsigned grid, hipStream_t s) {
+  if (a.ccol) {  // churn without lazy gossip (FP == 1)
+    if (lpull_chunks(a.L) == 8) k_lpull<1, 8, false, false, false, true><<<grid, TB, 0, s>>>(a);
+    else k_lpull<1, 16, false, false, false, true><<<grid, TB, 0, s>>>(a);
+    return;
+  }
   if (a.idw) {  // FP == 1 (the host sends fragmented IDONTWANT batches to the push path)
     if (lpull_chunks(a.L) == 8) k_lpull<1, 8, true><<<grid, TB, 0, s>>>(a);
     else k_lpull<1, 16, true><<<grid, TB, 0, s>>>(a);

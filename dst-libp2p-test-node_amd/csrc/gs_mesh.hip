@@ -45,6 +45,11 @@ struct MeshArgs {
   const uint64_t* off_prev;  // offline bitsets of the previous and the next epoch
   const uint64_t* off_next;  // (nullptr: the last epoch of the run)
   unsigned long long* dbg;   // GS_DEBUG_EV: [3][4] active rows per step (+ for HB: leaving, nbr-off, propd, hungry)
+  // churn ring of mesh masks (the churn list pass, gs_lpull_kernel.h): bit e of
+  // mm_out[u] = CSR entry e of u is in the epoch's mesh; rows the apply step does
+  // not re-extract copy mm_prev (nullptr: no mask ring)
+  uint64_t* mm_out;
+  const uint64_t* mm_prev;
 };
 
 // Planes of MeshArgs::pst. A row runs the heavy per-row code of an epoch step
@@ -445,6 +450,12 @@ __global__ __launch_bounds__(TB) void k_extract(MeshArgs a, uint32_t* mesh, uint
   const uint32_t u = blockIdx.x * TB + threadIdx.x;
   if (u >= a.N) return;
   uint32_t c = 0;
+  if (a.mm_out) {  // the mask ring's slot (rows of <= 64 entries)
+    uint64_t mm = 0;
+    for (uint64_t e = a.row[u]; e < a.row[u + 1] && e - a.row[u] < 64; e++)
+      if (a.flags[e] & F_MESH) mm |= 1ull << (e - a.row[u]);
+    a.mm_out[u] = mm;
+  }
   for (uint64_t e = a.row[u]; e < a.row[u + 1]; e++)
     if (a.flags[e] & F_MESH) {
       if (c == MESH_W) { atomicOr((unsigned*)&a.counters[C_ERR], ERR_MESH); break; }
@@ -716,6 +727,7 @@ __global__ __launch_bounds__(TB) void k_ev_init(MeshArgs a) {
 template <int G>
 __device__ __forceinline__ void row_apply_ev(const MeshArgs& a, uint32_t u, bool need, bool dirty, bool depart,
                                              uint32_t* mesh) {
+  uint64_t mmask = 0;  // the new mesh as a mask over the CSR row (entries < 64)
   const int lane = threadIdx.x & (G - 1);
   uint8_t* P = a.pst;
   const uint32_t N = a.N;
@@ -768,9 +780,11 @@ __device__ __forceinline__ void row_apply_ev(const MeshArgs& a, uint32_t u, bool
         const uint32_t pos = m + (uint32_t)__popcll(bm & ((1ull << lane) - 1));
         if (pos < MESH_W) mesh[(size_t)u * MESH_W + pos] = (sg[k] << STAGE_SHIFT) | cw[k];
       }
+      if (k * G < 64) mmask |= bm << (k * G);
       m += (uint32_t)__popcll(bm);
       o += (uint32_t)__popcll(gballot<G>(in && (f[k] & F_OUT)));
     }
+    if (a.mm_out && lane == 0) a.mm_out[u] = mmask;
     if (mesh) {
       if (m > MESH_W && lane == 0) atomicOr((unsigned*)&a.counters[C_ERR], ERR_MESH);
       if ((uint32_t)lane >= m && lane < (int)MESH_W) mesh[(size_t)u * MESH_W + lane] = EMPTY;
@@ -806,6 +820,8 @@ __global__ __launch_bounds__(TB) void k_ev_step(MeshArgs a, uint32_t* mesh, cons
     const uint4* src = reinterpret_cast<const uint4*>(mesh_prev + (size_t)base * MESH_W);
     uint4* dst = reinterpret_cast<uint4*>(mesh + (size_t)base * MESH_W);
     for (uint32_t i = threadIdx.x; i < nrow * (MESH_W / 4); i += TB) dst[i] = src[i];
+    if (a.mm_out && a.mm_prev)
+      for (uint32_t i = threadIdx.x; i < nrow; i += TB) a.mm_out[base + i] = a.mm_prev[base + i];
   }
   if (threadIdx.x < 64) {
     const uint32_t u = base + threadIdx.x;
@@ -906,6 +922,8 @@ static void ring_in_prepare(Ctx& c, uint64_t E, hipStream_t s) {
 // the lists run on a capped grid, so the steps' blocks find free slots
 static void ring_in_chunk(Ctx& c, uint64_t h0, uint32_t ny, hipStream_t s, uint32_t bpc = 0) {
   const uint32_t N = c.cfg.peers, R = c.ring_R, w64 = (N + 63) / 64;
+  if (c.ring_in_tag.size() != R) c.ring_in_tag.assign(R, ~0ull);
+  for (uint64_t h = h0; h < h0 + ny; h++) c.ring_in_tag[h % R] = h;
   const uint64_t cap = bpc ? (uint64_t)std::max(c.num_cus, 1) * bpc : ~0ull;
   const unsigned g1 = (unsigned)std::min<uint64_t>(cap, ((uint64_t)N * ny + TB - 1) / TB);
   const unsigned g2 = (unsigned)std::min<uint64_t>(cap, ((uint64_t)N * ny * GIN_G + TB - 1) / TB);
@@ -914,7 +932,9 @@ static void ring_in_chunk(Ctx& c, uint64_t h0, uint32_t ny, hipStream_t s, uint3
   k_gossip_in_gather<<<g2, TB, 0, s>>>(c.d_row.p, c.d_col.p, c.d_csrpos.p, c.d_ring_off.p, c.d_stage.p, N, w64, R, h0,
                                        c.d_gout.p, c.d_ring_in.p, ny);
 }
-static bool ring_in_wanted(const Ctx& c) { return c.cfg.lazy_gossip && c.d_ring_in.p; }
+// (deferred while the churn list pass takes the batches: it decides IHAVEs from
+// the mask ring; ensure_in_lists builds them when a batch falls back to the push path)
+static bool ring_in_wanted(const Ctx& c) { return c.cfg.lazy_gossip && c.d_ring_in.p && !c.ring_in_defer; }
 
 // Epochs [h0, h1] (h1 - h0 < ring_R) on the context's stream: per chunk of
 // epochs, the senders' target masks, then every receiver's list
@@ -1049,8 +1069,14 @@ void ev_epochs(Ctx& c, MeshArgs a, uint64_t h0, uint64_t h1, bool ring) {
     a.off_next = h < h1 ? lin + (y + 1) * w64 : nullptr;
     uint32_t* mesh = ring ? c.d_ring_mesh.p + (size_t)(h % c.ring_R) * N * MESH_W : nullptr;
     const uint32_t* prev = ring && h > h0 ? c.d_ring_mesh.p + (size_t)((h - 1) % c.ring_R) * N * MESH_W : nullptr;
-    GS_EVS(EV_HB, a, nullptr, nullptr);
-    GS_EVS(EV_GRAFT, a, nullptr, nullptr);
+    const bool mmr = ring && c.d_ring_mm.p;
+    a.mm_out = mmr ? c.d_ring_mm.p + (size_t)(h % c.ring_R) * N : nullptr;
+    a.mm_prev = mmr && h > h0 ? c.d_ring_mm.p + (size_t)((h - 1) % c.ring_R) * N : nullptr;
+    MeshArgs an = a;  // the mask ring is written by the apply step only
+    an.mm_out = nullptr;
+    an.mm_prev = nullptr;
+    GS_EVS(EV_HB, an, nullptr, nullptr);
+    GS_EVS(EV_GRAFT, an, nullptr, nullptr);
     GS_EVS(EV_APPLY, a, mesh, prev);
     if (lists && h >= hr && (h + 1 - chunk0 == CE || h == h1)) {
       const hipEvent_t e = side_event(c, nev++);
@@ -1083,6 +1109,26 @@ void run_epochs(Ctx& c, MeshArgs a, uint64_t h0, uint64_t h1, bool ring) { ev_ep
 
 }  // namespace
 
+// The inverse IHAVE lists of ring epochs [h0, h1] that were deferred (the push
+// path's receiver-centric gossip reads them), on the context's stream.
+void ensure_in_lists(Ctx& c, uint64_t h0, uint64_t h1) {
+  if (!c.cfg.lazy_gossip || !c.d_ring_in.p) return;
+  const uint32_t R = c.ring_R;
+  if (c.ring_in_tag.size() != R) c.ring_in_tag.assign(R, ~0ull);
+  const uint64_t CE = ring_in_chunk_epochs(c.cfg.peers);
+  bool prepared = false;
+  for (uint64_t h = h0; h <= h1;) {
+    if (c.ring_in_tag[h % R] == h) { h++; continue; }
+    uint64_t e = h;  // a run of epochs without lists, at most one chunk
+    while (e + 1 <= h1 && e + 1 - h < CE && c.ring_in_tag[(e + 1) % R] != e + 1) e++;
+    if (!prepared) ring_in_prepare(c, std::min<uint64_t>(CE, h1 - h0 + 1), c.stream);
+    prepared = true;
+    ring_in_chunk(c, h, (uint32_t)(e - h + 1), c.stream);
+    h = e + 1;
+  }
+  GS_HIP(hipGetLastError());
+}
+
 // Make the churn ring hold the snapshots of epochs [h_lo, h_hi] (h_hi - h_lo
 // < ring_R): replay from the empty mesh when h_lo has left the ring, else run
 // the epochs after the current mesh state. Snapshot h = mesh after heartbeat h
@@ -1101,7 +1147,9 @@ void churn_ring(Ctx& c, uint64_t h_lo, uint64_t h_hi) {
     c.ring_lo = 1;
     if (h_lo == 0) {  // slot 0: the mesh after the subscription exchange (empty without it); a
       // row may be wider than the ELL before heartbeat 1 prunes it (GS_ERANGE below)
-      k_extract<<<blocks(N), TB, 0, s>>>(a, c.d_ring_mesh.p, nullptr);
+      MeshArgs a0 = a;
+      a0.mm_out = c.d_ring_mm.p;  // slot 0 (nullptr: no mask ring)
+      k_extract<<<blocks(N), TB, 0, s>>>(a0, c.d_ring_mesh.p, nullptr);
       GS_HIP(hipMemsetAsync(c.d_ring_off.p, 0, w64 * 8, s));
       ring_in_lists(c, 0, 0);
       c.ring_lo = 0;
@@ -1136,6 +1184,7 @@ uint32_t run_mesh(Ctx& c, uint32_t max_hb) {
   MeshArgs a = mesh_args(c);
   if (c.nnz) k_clear_mesh<<<blocks(c.nnz), TB, 0, s>>>(c.nnz, c.d_flags.p, c.d_until.p);
   GS_HIP(hipMemsetAsync(c.d_counters.p + C_ERR, 0, 8, s));
+  c.ring_in_tag.assign(c.ring_in_tag.size(), ~0ull);  // a new mesh: the churn ring restarts
   sub_epoch(c, a);
   uint32_t epoch = 1, last = 0;
   uint64_t* h = c.h_pinned;

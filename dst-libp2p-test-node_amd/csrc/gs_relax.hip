@@ -359,6 +359,7 @@ __global__ __launch_bounds__(TB) void k_transpose(const uint64_t* __restrict__ t
 }
 
 #include "gs_lpull_kernel.h"
+#include "gs_cpull.h"
 
 uint32_t pow2_at_least(uint32_t x) { uint32_t p = 1; while (p < x) p <<= 1; return p; }
 
@@ -932,7 +933,7 @@ static uint32_t lpull_stride(const Batch& b) { return std::max<uint32_t>(b.L, 25
 // destination is at most K - 1 windows after the emitted one; the entry
 // packs (t - window start) | hops | src | lane into 64 bits; the seed list
 // packs row << 11 | lane (N < 2^21); the lists must fit the device memory left.
-static uint32_t lpull_ring(Ctx& c, const Batch& b, uint64_t delta, uint32_t* lb, bool gos = false) {
+static uint32_t lpull_ring(Ctx& c, const Batch& b, uint64_t delta, uint32_t* lb, bool gos = false, bool chn = false) {
   if (!c.mesh_dmax) {  // widest mesh row, once per mesh
     std::vector<uint32_t> m((size_t)c.cfg.peers * MESH_W);
     GS_HIP(hipMemcpyAsync(m.data(), c.d_mesh.p, m.size() * 4, hipMemcpyDeviceToHost, c.stream));
@@ -948,7 +949,8 @@ static uint32_t lpull_ring(Ctx& c, const Batch& b, uint64_t delta, uint32_t* lb,
   if (b.tshift >= 32 || b.L > PULL_LMAX || delta < 2 || c.cfg.peers >= (1u << 21)) return 0;  // seed list: row << 11
   // a fragment waits behind at most the other FP - 1 fragments' sends to the
   // row's mesh peers (c.mesh_dmax, the widest mesh row)
-  const uint64_t dm = c.mesh_dmax ? c.mesh_dmax : MESH_W;
+  // (churn: each epoch has its own mesh, bounded by the ELL width)
+  const uint64_t dm = chn ? MESH_W : c.mesh_dmax ? c.mesh_dmax : MESH_W;
   const uint64_t fifo = (uint64_t)(b.FP - 1) * dm * b.ser_max;
   const uint64_t span = delta + fifo + b.lat_adj_max + dm * b.ser_max;
   // k_seed's first sends (every fragment to every mesh peer, or to every
@@ -992,14 +994,20 @@ static uint32_t lpull_ring(Ctx& c, const Batch& b, uint64_t delta, uint32_t* lb,
 struct GosRun {
   uint64_t rel0, hb;
 };
+// Churn on the list pass (gs_cpull.h): the batch's first epoch and epoch count,
+// the common offset of its publishes into their epochs, heartbeat 0's relative epoch.
+struct ChnRun {
+  uint64_t E0, r0;
+  uint32_t cE, ghoff;
+};
 
 template <class EvFn>
 static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvFn& ev, size_t& n_ev, int dev_cus,
-                            bool dense, bool idw, const GosRun* gos = nullptr) {
+                            bool dense, bool idw, const GosRun* gos = nullptr, const ChnRun* chn = nullptr) {
   const uint32_t N = c.cfg.peers, L = b.L;
   hipStream_t s = c.stream;
   const size_t NL = (size_t)N * L;
-  c.d_lrec.alloc(2 * NL);
+  c.d_lrec.alloc((chn ? 4 : 2) * NL);  // churn records are 16 B
   c.d_lcnt.alloc(2 * (size_t)N);
   c.d_pctrl.alloc(12);
   const uint32_t ls = lpull_stride(b);
@@ -1040,6 +1048,22 @@ static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvF
   la.K = K; la.lb = lb; la.dG = (uint32_t)(la.delta / grain);
   la.idw = idw ? 1u : 0u;
   la.rmax = lpull_rmax(b);
+  la.ghk = ~0u;
+  if (chn) {  // churn (gs_cpull.h): the tables k_cprep built for this batch
+    la.ccol = c.d_ccol.p;
+    la.cpos = c.d_cpos.p;
+    la.cmm = c.d_cmm.p;
+    la.cge = c.d_cge.p;
+    la.coff = c.d_coff.p;
+    la.cq = c.d_cq.p;
+    la.pubok = c.d_pubok.p;
+    la.cr0 = chn->r0;
+    la.chb = c.cfg.heartbeat_ns;
+    la.cE = chn->cE;
+    la.chz = c.cfg.churn_horizon;
+    la.ghoff = chn->ghoff;
+    la.ghk = c.cfg.churn_horizon - chn->ghoff;
+  }
   const char* cap = getenv("GS_LPULL_CAP");  // test knob: small lists force the overflow re-run
   la.ls = ls;
   la.lcap = cap && *cap ? (uint32_t)std::min<long>(std::max(1, atoi(cap)), (long)ls) : ls;
@@ -1163,6 +1187,77 @@ static bool gossip_noop(const Batch& b, const uint64_t* ms, const std::vector<ui
   return true;
 }
 
+// The churn list pass's per-batch tables (gs_cpull.h) for epochs [E0, E0 + cE)
+// and the batch's publish epochs q0 (lanes), after the epoch chain filled the ring.
+static void chn_prepare(Ctx& c, uint64_t E0, uint32_t cE, const uint64_t* q0, const gs_publish* sched, uint32_t B) {
+  const uint32_t N = c.cfg.peers, H = c.cfg.churn_horizon, R = c.ring_R;
+  const uint32_t cW = (cE + 63) / 64, w64 = (N + 63) / 64;
+  hipStream_t s = c.stream;
+  if (!c.cell_valid) {
+    c.d_ccol.alloc((size_t)N * CELL_W);
+    c.d_cpos.alloc((size_t)N * CELL_W);
+    k_cell<<<(unsigned)(((uint64_t)N * CELL_W + TB - 1) / TB), TB, 0, s>>>(N, c.d_row.p, c.d_col.p, c.d_rev.p,
+                                                                          c.d_stage.p, c.d_ccol.p, c.d_cpos.p);
+    GS_HIP(hipGetLastError());
+    c.cell_valid = true;
+  }
+  std::vector<uint32_t> cq(B);
+  std::vector<uint8_t> ok(B);
+  for (uint32_t q = 0; q < B; q++) {
+    cq[q] = (uint32_t)(q0[q] - E0);
+    ok[q] = !offline_draw(c.cfg.seed, c.cfg.churn_ppm, c.cfg.churn_down, sched[q].publisher, q0[q]);
+  }
+  c.d_cq.alloc(c.cfg.batch);
+  c.d_pubok.alloc(c.cfg.batch);
+  GS_HIP(hipMemcpyAsync(c.d_cq.p, cq.data(), B * 4, hipMemcpyHostToDevice, s));
+  GS_HIP(hipMemcpyAsync(c.d_pubok.p, ok.data(), B, hipMemcpyHostToDevice, s));
+  c.d_offe.alloc((size_t)N * cW);
+  c.d_cmm.alloc((size_t)N * cE);
+  c.d_cge.alloc((size_t)N * cE);
+  c.d_coff.alloc((size_t)(H + 2) * N * LP_FW);
+  k_offe<<<dim3(w64, cW), 64, 0, s>>>(N, c.d_ring_off.p, w64, R, E0, cE, cW, c.d_offe.p);
+  CPrepArgs pa{};
+  pa.ccol = c.d_ccol.p; pa.ring_mm = c.d_ring_mm.p; pa.offe = c.d_offe.p; pa.cq = c.d_cq.p;
+  pa.cmm = c.d_cmm.p; pa.cge = c.d_cge.p; pa.coff = c.d_coff.p;
+  pa.E0 = E0; pa.N = N; pa.R = R; pa.cE = cE; pa.cW = cW; pa.B = B; pa.H = H;
+  const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((N + 3) / 4, (uint64_t)std::max(c.num_cus, 1) * 8));
+  k_cprep<<<grid, TB, 0, s>>>(pa);
+  GS_HIP(hipGetLastError());
+  GS_HIP(hipStreamSynchronize(s));  // cq / ok die here
+  if (getenv("GS_DEBUG_CHN")) {  // diagnostic: the tables against the ELL ring and offline_draw
+    std::vector<uint64_t> row(N + 1), cmm((size_t)N * cE), cge((size_t)N * cE);
+    std::vector<uint32_t> col(c.nnz), ell((size_t)R * N * MESH_W);
+    GS_HIP(hipMemcpy(row.data(), c.d_row.p, (N + 1) * 8, hipMemcpyDeviceToHost));
+    GS_HIP(hipMemcpy(col.data(), c.d_col.p, c.nnz * 4, hipMemcpyDeviceToHost));
+    GS_HIP(hipMemcpy(cmm.data(), c.d_cmm.p, cmm.size() * 8, hipMemcpyDeviceToHost));
+    GS_HIP(hipMemcpy(cge.data(), c.d_cge.p, cge.size() * 8, hipMemcpyDeviceToHost));
+    GS_HIP(hipMemcpy(ell.data(), c.d_ring_mesh.p, ell.size() * 4, hipMemcpyDeviceToHost));
+    uint64_t bad_mm = 0, bad_ge = 0;
+    for (uint32_t w = 0; w < N; w++)
+      for (uint32_t e = 0; e < cE; e++) {
+        const uint64_t E = E0 + e;
+        const uint32_t* er = &ell[((size_t)(E % R) * N + w) * MESH_W];
+        uint64_t mm = 0, ge = 0;
+        const bool woff = offline_draw(c.cfg.seed, c.cfg.churn_ppm, c.cfg.churn_down, w, E);
+        for (uint64_t x = row[w]; x < row[w + 1]; x++) {
+          bool in = false;
+          for (uint32_t j = 0; j < MESH_W; j++) in |= er[j] != EMPTY && (er[j] & 0xFFFFFFu) == col[x];
+          if (in) mm |= 1ull << (x - row[w]);
+          else if (!woff && !offline_draw(c.cfg.seed, c.cfg.churn_ppm, c.cfg.churn_down, col[x], E))
+            ge |= 1ull << (x - row[w]);
+        }
+        if (mm != cmm[(size_t)w * cE + e] && bad_mm++ < 5)
+          fprintf(stderr, "[chn] mm w %u E %llu dev %llx host %llx\n", w, (unsigned long long)E,
+                  (unsigned long long)cmm[(size_t)w * cE + e], (unsigned long long)mm);
+        if (ge != cge[(size_t)w * cE + e] && bad_ge++ < 5)
+          fprintf(stderr, "[chn] ge w %u E %llu dev %llx host %llx\n", w, (unsigned long long)E,
+                  (unsigned long long)cge[(size_t)w * cE + e], (unsigned long long)ge);
+      }
+    fprintf(stderr, "[chn] E0 %llu cE %u: mm mismatches %llu, ge mismatches %llu\n", (unsigned long long)E0, cE,
+            (unsigned long long)bad_mm, (unsigned long long)bad_ge);
+  }
+}
+
 void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_result_sink* sink) {
   const uint32_t N = c.cfg.peers;
   const uint32_t Bmax = c.cfg.batch;
@@ -1188,6 +1283,12 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
   // proves it a no-op (gossip_noop), else the batch is re-run on the push path.
   const bool churn = c.cfg.churn_ppm != 0;  // per-epoch mesh lookups live on the push path
   const bool pull_any = (variant & 32) && !churn;
+  // churn on the list pass (gs_cpull.h): lockstep single-fragment batches without
+  // IDONTWANT, CSR rows of <= 64 entries (<= 58 with lazy gossip: the IHAVE entry's
+  // target mask); GS_CHURN_LIST=0 keeps them on the push path
+  const char* chl_env = getenv("GS_CHURN_LIST");
+  const bool chn_any = churn && (variant & 32) && (variant & 64) && !(chl_env && *chl_env && atoi(chl_env) == 0) &&
+                       c.max_degree <= (gossip ? GSE_HOPS : CELL_W) && N < (1u << 21);
   // the push path with gossip or churn runs split, without tile skip
   // the push path with gossip or churn runs split + tile skip (its long tail of
   // IHAVE and churn buckets touches few tiles); GS_RELAX_VARIANT can turn the skip off
@@ -1204,13 +1305,15 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     }
     if (!c.ring_R) {
       const uint64_t w64 = ((uint64_t)N + 63) / 64;
-      const uint64_t per_slot = (uint64_t)N * MESH_W * 4 + w64 * 8 + (gossip ? (uint64_t)N * (GT_IN * 4 + 4) : 0);
+      const uint64_t per_slot = (uint64_t)N * MESH_W * 4 + w64 * 8 + (gossip ? (uint64_t)N * (GT_IN * 4 + 4) : 0) +
+                                (uint64_t)N * 8;
       const char* rb = getenv("GS_RING_BUDGET_MB");  // test knob: force batch cuts at the ring size
       const uint64_t budget = rb && *rb ? (uint64_t)atoll(rb) << 20 : 16ull << 30;
       const uint64_t want = (uint64_t)Bmax + c.cfg.churn_horizon + 1;
       c.ring_R = (uint32_t)std::min<uint64_t>(want, std::max<uint64_t>(c.cfg.churn_horizon + 2, budget / per_slot));
       c.d_ring_mesh.alloc((size_t)c.ring_R * N * MESH_W);
       c.d_ring_off.alloc((size_t)c.ring_R * w64);
+      if (c.max_degree <= CELL_W) c.d_ring_mm.alloc((size_t)c.ring_R * N);  // the churn list pass's meshes
       if (gossip) {  // inverse IHAVE lists per (peer, epoch) beside the snapshots (ring_in_lists)
         c.d_ring_in.alloc((size_t)c.ring_R * N * GT_IN);
       }
@@ -1251,8 +1354,9 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     // tables and the lane layout are per batch); the pull path holds a row in
     // registers, so its batch is capped at PULL_LMAX / FP messages
     const uint32_t F0 = frags_of(c, sched[i0]);
-    const uint32_t Bcap = pull_any ? std::max<uint32_t>(1, std::min<uint32_t>(Bmax, PULL_LMAX / pow2_at_least(F0)))
-                                   : Bmax;
+    const uint32_t Bcap = pull_any || (chn_any && F0 == 1)
+                              ? std::max<uint32_t>(1, std::min<uint32_t>(Bmax, PULL_LMAX / pow2_at_least(F0)))
+                              : Bmax;
     uint64_t i1 = i0 + 1;
     uint64_t h_lo = churn ? ep[i0] : 0, h_hi = churn ? ep[i0] : 0;  // churn: publish epochs of the batch
     while (i1 < n_msgs && i1 - i0 < Bcap && sched[i1].msg_size == sched[i0].msg_size &&
@@ -1267,13 +1371,26 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     }
     const Batch b = setup_batch(c, sched, i0, i1);
     const uint32_t FP = b.FP;
+    bool chn = false;  // this batch runs on the churn list pass
     if (churn) {
-      churn_ring(c, h_lo, h_hi + c.cfg.churn_horizon);
       const uint64_t hb = c.cfg.heartbeat_ns, ph = c.cfg.hb_phase_ns;
       for (uint32_t q = 0; q < b.B; q++) {
         q0v[q] = ep[i0 + q];
         r0v[q] = b.tpub[q] - ph - q0v[q] * hb;
       }
+      if (chn_any && b.FP == 1 && !b.collide && c.d_ring_mm.p) {
+        const bool idw = c.cfg.idontwant && b.payload >= c.cfg.idontwant;
+        bool lock = true;
+        for (uint32_t q = 1; q < b.B && lock; q++) lock = r0v[q] == r0v[0];
+        const uint64_t dl = gossip ? std::min(b.delta, b.lat_min) : b.delta;
+        const uint64_t cE = h_hi + c.cfg.churn_horizon - h_lo + 1;
+        chn = !idw && lock && cE <= 4096 && dl >= pull_grain(b.tshift) && hb > lpull_rmax(b) + 2 * dl &&
+              (!gossip || hb > b.lat_max + dl);
+      }
+      c.ring_in_defer = chn;  // the push path's inverse IHAVE lists are not needed
+      churn_ring(c, h_lo, h_hi + c.cfg.churn_horizon);
+      c.ring_in_defer = false;
+      if (chn) chn_prepare(c, h_lo, (uint32_t)(h_hi + c.cfg.churn_horizon - h_lo + 1), q0v.data(), sched + i0, b.B);
       c.d_q0.alloc(Bmax);
       c.d_r0.alloc(Bmax);
       GS_HIP(hipMemcpyAsync(c.d_q0.p, q0v.data(), b.B * 8, hipMemcpyHostToDevice, s));
@@ -1479,6 +1596,29 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       return true;
     };
     bool done = false;
+    if (chn) {  // churn on the list pass; a list overflow falls back to the push path
+      uint32_t lb = 0;
+      Batch bc = b;
+      if (gossip) bc.delta = std::min(b.delta, b.lat_min);
+      const uint64_t grain = pull_grain(b.tshift);
+      const uint32_t K = lpull_ring(c, bc, bc.delta / grain * grain, &lb, gossip, true);
+      if (K) {
+        reset(variant, false, false);
+        const GosRun gr{rel0[0], c.cfg.heartbeat_ns};
+        const ChnRun cr{h_lo, r0v[0], (uint32_t)(h_hi + c.cfg.churn_horizon - h_lo + 1),
+                        gossip ? (uint32_t)(habs0[0] - q0v[0]) : 0u};
+        const SinkWants sw = sink_wants(sink);
+        const bool dense = sw.rows() || sw.summary || c.traffic || getenv("GS_LPULL_DENSE");
+        if (run_lpull_batch(c, bc, K, lb, ev, n_ev, dev_cus, dense, false, gossip ? &gr : nullptr, &cr)) {
+          if (gossip) c.stats.gossip_list_batches++;
+          if (c.traffic) launch_traffic(c, b);
+          launch_complete(c, b, 0, N, sink, i0);
+          done = true;
+        }
+      }
+      if (!done && getenv("GS_REQUIRE_LPULL")) c.fail(GS_EUNSUPPORTED, "churn list pass cannot take this batch (GS_REQUIRE_LPULL)");
+      if (!done && gossip) ensure_in_lists(c, h_lo, h_hi + c.cfg.churn_horizon);
+    }
     if (glp && c.glp_prefer) done = run_glp();
     if (!done && (pull_ok || (gossip && !churn))) {
       if (gossip) GS_HIP(hipMemcpyAsync(c.d_cnt_save.p, c.d_counters.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));

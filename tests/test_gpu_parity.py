@@ -464,6 +464,59 @@ def test_churn_gossip_sender_receiver_switch(monkeypatch, switch):
     assert 0 < st["deliveries"] < 32 * 799 and st["gossip_iwant"] > 0
 
 
+@pytest.mark.parametrize("gossip,hb_ms,phase_ms,frags", [(0, 1000, 370, 1), (1, 1000, 370, 1), (1, 400, 150, 1),
+                                                           (0, 400, 330, 1), (1, 300, 20, 1), (1, 400, 150, 2)])
+def test_churn_list_pass(monkeypatch, gossip, hb_ms, phase_ms, frags):
+    """Churn on the owner-computes list pass (gs_cpull.h, k_lpull<.., CHN>):
+    per-lane epoch meshes as CSR masks, 16-B records, forwards that cross an
+    epoch boundary into a receiver's offline epoch, IWANT answers lost the same
+    way, the lifetime cut; heartbeats short enough that several boundaries fall
+    inside a dissemination. Bit-exact against the oracle, IWANTs included; the
+    single-fragment batches must take the list pass (GS_REQUIRE_LPULL), the
+    fragmented one the push path."""
+    if frags == 1:
+        monkeypatch.setenv("GS_REQUIRE_LPULL", "1")
+    hb = hb_ms * 1_000_000
+    kw = dict(churn_ppm=30000, lazy_gossip=gossip, fragments=frags, heartbeat_ns=hb, churn_down=6,
+              churn_horizon=10, hb_phase_ns=T0 - 30 * hb + phase_ms * 1_000_000)
+    p = oracle.params(peers=900, seed=57, **kw)
+    t = T0 + np.arange(40, dtype=np.uint64) * np.uint64(hb)  # lockstep: one publish per heartbeat
+    sched = (t, (6 + np.arange(40)) % 900, np.full(40, 15000))
+    sim, res = compare(p, 5, (50, 150, 40, 130), sched, batch=40)
+    st = sim.stats()
+    assert 0 < st["deliveries"] < 40 * 899
+    if frags == 1:
+        assert st["list_pull_batches"] == 1
+        if gossip:
+            assert st["gossip_list_batches"] == 1 and st["gossip_iwant"] > 0
+    else:
+        assert st["list_pull_batches"] == 0
+
+
+def test_churn_list_pass_equals_push_path_at_10k(monkeypatch):
+    """The churn list pass against the push path on a 10k-peer, 256-message
+    config #3-shaped batch (heterogeneous links, lazy gossip, 1 % churn,
+    heartbeats 370 ms after each publish): every completion time, hop count and
+    counter equal."""
+    p = oracle.params(peers=10_000, seed=3, lazy_gossip=1, churn_ppm=10_000, churn_down=10, churn_horizon=16,
+                      hb_phase_ns=T0 - 20 * 1_000_000_000 + 370_000_000)
+    sched = _sched(256, 10_000)
+    out = []
+    for chl in ("1", "0"):
+        monkeypatch.setenv("GS_CHURN_LIST", chl)
+        sim, _ = gpu_sim(p, 5, (50, 150, 40, 130), batch=256)
+        res = sim.run(sched)
+        out.append((res, sim.stats()))
+        sim.close()
+    (a, sa), (b, sb) = out
+    assert sa["list_pull_batches"] == 1 and sb["list_pull_batches"] == 0
+    np.testing.assert_array_equal(a["t_complete"], b["t_complete"])
+    np.testing.assert_array_equal(a["hops"], b["hops"])
+    for k in ("deliveries", "frag_deliveries", "relaxations", "gossip_iwant", "latency_sum_ms"):
+        assert sa[k] == sb[k], k
+    assert sa["gossip_iwant"] > 0
+
+
 def test_churn_errors():
     p = oracle.params(peers=200, seed=3, churn_ppm=10000)  # hb_phase 0: publishes ~1e9 heartbeats later
     sim, _ = gpu_sim(p, 1, (50, 50, 50, 50))
