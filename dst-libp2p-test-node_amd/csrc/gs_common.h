@@ -49,6 +49,14 @@ GS_HD uint64_t rng(uint64_t seed, uint32_t purpose, uint32_t a, uint32_t b, uint
   h = mix64(h ^ ((((uint64_t)b) << 32) | c) ^ 0xD6E8FEB86659FD93ull);
   return h;
 }
+// The same draw in two parts: rng_fin(rng_pre(seed, purpose, a), b, c) ==
+// rng(seed, purpose, a, b, c); a loop over (b, c) of one `a` mixes once per draw.
+GS_HD uint64_t rng_pre(uint64_t seed, uint32_t purpose, uint32_t a) {
+  return mix64(mix64(seed + 0x9E3779B97F4A7C15ull * (uint64_t)(purpose + 1u)) ^ ((uint64_t)a + 0x9E3779B97F4A7C15ull));
+}
+GS_HD uint64_t rng_fin(uint64_t pre, uint32_t b, uint32_t c) {
+  return mix64(pre ^ ((((uint64_t)b) << 32) | c) ^ 0xD6E8FEB86659FD93ull);
+}
 GS_HD uint64_t mulhi64(uint64_t a, uint64_t b) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return __umul64hi(a, b);

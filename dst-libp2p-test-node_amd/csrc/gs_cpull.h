@@ -20,8 +20,8 @@
 //  k_offe   each peer's offline bits over the batch's epochs, from the ring's
 //           offline bitsets (a 64 x 64 bit transpose by ballots);
 //  k_cprep  per row and epoch: the mesh mask (from the chain's mask ring) and
-//           the IHAVE-eligible mask (online connections outside the mesh; 0 when
-//           the row is offline), and per relative epoch k the offline lanes in
+//           the IHAVE targets (selected among the online connections outside
+//           the mesh; none when the row is offline), and per relative epoch k the offline lanes in
 //           the final bits' transposed layout (all lanes at k = horizon + 1:
 //           past the message's lifetime nothing is delivered).
 
@@ -69,17 +69,19 @@ struct CPrepArgs {
   const uint64_t* offe;     // [N][cW]
   const uint32_t* cq;       // [B]
   uint64_t* cmm;            // [N][cE]
-  uint64_t* cge;
+  uint64_t* cgt;            // lazy gossip: IHAVE targets per (row, epoch) (nullptr: no gossip)
   uint32_t* coff;           // [H + 2][N][LP_FW]
-  uint64_t E0;
-  uint32_t N, R, cE, cW, B, H;
+  uint64_t E0, seed;
+  uint32_t N, R, cE, cW, B, H, d_lazy, gf_milli;
+  uint32_t c0, c1;  // k_cprep: the chunks of 64 epochs [c0, c1) (their epochs are in the ring)
 };
 
 // One wave per row w: lane e holds CSR entry e (neighbour x). Per chunk of 64
 // epochs, lane j loads the mesh mask of epoch E0 + 64c + j; then for each epoch
 // of the chunk the IHAVE-eligible mask is the row's entries outside that mesh
-// whose neighbour is online (a ballot of the neighbours' offline bits). The
-// offline lanes per relative epoch come from the row's own offline bits.
+// whose neighbour is online (a ballot of the neighbours' offline bits), and lane
+// j selects epoch j's targets. Launched per range of chunks on the side stream
+// while the epoch chain fills the ring (gs_relax.hip chn_prepare).
 __global__ __launch_bounds__(TB) void k_cprep(CPrepArgs a) {
   const int lane = threadIdx.x & 63;
   const uint32_t wv = blockIdx.x * (TB / 64) + (threadIdx.x >> 6), nw = gridDim.x * (TB / 64);
@@ -88,8 +90,10 @@ __global__ __launch_bounds__(TB) void k_cprep(CPrepArgs a) {
     const bool valid = xe != EMPTY;
     const uint32_t xc = xe & 0xFFFFFFu;
     const uint64_t cm = __ballot(valid);
+    const uint32_t deg = (uint32_t)__popcll(cm);
+    const uint64_t pre = rng_pre(a.seed, P_GOSSIP, w);
     const uint64_t* ownp = a.offe + (size_t)w * a.cW;
-    for (uint32_t c = 0; c < a.cW; c++) {
+    for (uint32_t c = a.c0; c < a.c1; c++) {
       const uint32_t e = c * 64 + (uint32_t)lane;
       const uint64_t mml =
           e < a.cE ? a.ring_mm[(size_t)((uint32_t)((a.E0 + e) % a.R)) * a.N + w] & cm : 0;
@@ -104,14 +108,27 @@ __global__ __launch_bounds__(TB) void k_cprep(CPrepArgs a) {
         const uint64_t ge = ((own >> j) & 1) ? 0 : (cm & ~mmj & ~offn);
         if ((uint32_t)lane == j) gel = ge;
       }
-      if (e < a.cE) {
-        a.cmm[(size_t)w * a.cE + e] = mml;
-        a.cge[(size_t)w * a.cE + e] = gel;
+      if (e < a.cE) a.cmm[(size_t)w * a.cE + e] = mml;
+      if (a.cgt) {  // lane j: the IHAVE targets of epoch E0 + 64c + j (glp_targets, the oracle's gossip_targets)
+        const uint32_t nn = (uint32_t)__popcll(gel);
+        uint32_t r = (uint32_t)(((uint64_t)nn * a.gf_milli) / 1000);
+        if (r < a.d_lazy) r = a.d_lazy;
+        if (r > nn) r = nn;
+        const uint64_t tg = glp_targets(pre, (uint32_t)(a.E0 + e), valid ? xc : EMPTY, gel, deg, r);
+        if (e < a.cE) a.cgt[(size_t)w * a.cE + e] = tg;
       }
     }
-    // offline lanes per relative epoch k (lane m: epoch E0 + cq[m] + k); lane j
-    // builds its u16 (bit q = lane q*64 + j); the row's own bits are fetched
-    // from lane (index >> 6), which holds word index >> 6 of ownp
+  }
+}
+
+// The offline lanes per relative epoch k (lane m: epoch E0 + cq[m] + k), one
+// wave per row: lane j builds its u16 (bit q = lane q*64 + j); the row's own
+// bits are fetched from lane (index >> 6), which holds word index >> 6.
+__global__ __launch_bounds__(TB) void k_coff(CPrepArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t wv = blockIdx.x * (TB / 64) + (threadIdx.x >> 6), nw = gridDim.x * (TB / 64);
+  for (uint32_t w = wv; w < a.N; w += nw) {
+    const uint64_t* ownp = a.offe + (size_t)w * a.cW;
     const uint64_t ownl = (uint32_t)lane < a.cW ? ownp[lane] : 0;
     uint32_t cql[PULL_CH];
 #pragma unroll

@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -117,6 +118,11 @@ struct Ctx {
   DevBuf<uint64_t> d_ring_mm;     // [R][N] mesh of each epoch as a mask over the CSR row (max_degree <= 64)
   std::vector<uint64_t> ring_in_tag;  // [R] epoch whose inverse IHAVE lists a slot holds (~0: none)
   bool ring_in_defer = false;         // the churn list pass takes the batch: no inverse lists beside the epochs
+  // called by the epoch chain after it enqueued epoch h on the context's stream (and once with
+  // h0 - 1 when the run's offline bits are written): the churn list pass's tables of the epochs
+  // done so far go to the side stream (gs_relax.hip chn_chunks)
+  std::function<void(uint64_t)> epoch_hook;
+  std::vector<hipEvent_t> cp_ev;      // their events
   DevBuf<uint64_t> d_q0, d_r0;  // [B] epoch of t_pub, t_pub - start of that epoch
   uint32_t ring_R = 0;
   uint64_t churn_state = 0, ring_lo = 1, ring_hi = 0;  // mesh state epoch; valid ring epochs
@@ -227,11 +233,16 @@ struct Ctx {
   DevBuf<uint32_t> d_ccol;     // [N][64] stage << 24 | peer, ascending, EMPTY padded
   DevBuf<uint8_t> d_cpos;      // [N][64] position of the row's peer in that neighbour's row
   bool cell_valid = false;
-  DevBuf<uint64_t> d_cmm, d_cge;  // [N][cE]
+  DevBuf<uint64_t> d_cmm, d_cgt;  // [N][cE]
   DevBuf<uint64_t> d_offe;     // [N][cW] offline bit per epoch of the batch range
   DevBuf<uint32_t> d_coff;     // [H + 2][N][32] offline lanes per relative epoch (transposed like the final bits)
   DevBuf<uint32_t> d_cq;       // [B] epoch of t_pub - first epoch of the range
   DevBuf<uint8_t> d_pubok;     // [B] the publisher was online at t_pub
+  DevBuf<uint8_t> d_gnz;       // [N] the row's IHAVE plane of the built heartbeat is not empty
+  DevBuf<uint32_t> d_calive;   // [32] published lanes in the final bits' transposed layout
+  DevBuf<uint16_t> d_gtag;     // [N] the built heartbeat (GC_BK) whose IHAVEs the row takes by scanning planes
+  DevBuf<uint32_t> d_gpc;      // [N] IHAVE entries pushed to the row per heartbeat (bk << 16 | count)
+  DevBuf<uint64_t> d_luni;     // [2][N] per pass: OR of the receiver masks of a row's records
 
   // stats
   gs_stats stats{};
@@ -250,6 +261,7 @@ uint32_t run_mesh(Ctx& c, uint32_t max_heartbeats);
 void churn_ring(Ctx& c, uint64_t h_lo, uint64_t h_hi);
 void ensure_csrpos(Ctx& c);
 void ensure_in_lists(Ctx& c, uint64_t h0, uint64_t h1);
+hipStream_t side_stream(Ctx& c);
 void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_result_sink* sink);
 void deliver_rows(Ctx& c, uint32_t B, uint32_t un, const gs_result_sink* sink, uint64_t sink_row0);
 void part_set(Ctx& c, uint32_t parts, uint32_t part);

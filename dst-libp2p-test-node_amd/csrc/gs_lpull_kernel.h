@@ -119,12 +119,21 @@ struct LPullArgs {
   const uint32_t* ccol;  // [N][64] CSR rows, stage << 24 | peer, EMPTY padded (the row header)
   const uint8_t* cpos;   // [N][64] position of the row's peer in that neighbour's CSR row
   const uint64_t* cmm;   // [N][cE] mesh of each epoch as a mask over the row's CSR entries
-  const uint64_t* cge;   // [N][cE] IHAVE-eligible entries per epoch (online, outside the mesh; 0: offline)
+  const uint64_t* cgt;   // [N][cE] IHAVE targets per epoch, a mask over the CSR row (lazy gossip)
   const uint32_t* coff;  // [chz + 2][N][LP_FW] offline lanes per relative epoch (fin's layout)
   const uint32_t* cq;    // [B]
   const uint8_t* pubok;  // [B] the publisher was online at t_pub (k_lpub; nullptr: all)
+  uint8_t* gnz;          // [N] GOS: the row's plane of the built heartbeat has a lane (k_gsend)
+  uint16_t* gtag;        // [N] GOS: = GC_BK when a plane of the built heartbeat targets the row
+  uint32_t gsw;          // CHN + GOS: heartbeats k >= gsw push their IHAVEs into the targets' lists
+                         // (k_gsend: only those a target may still need, per-target cap); k < gsw:
+                         // every target scans the planes
+  uint32_t* gpc;         // [N] CHN + GOS: IHAVE entries pushed to the row this heartbeat, bk << 16 | count
+  const uint32_t* calive;  // [LP_FW] churn: the published lanes (publisher online at t_pub), fin's layout
+  uint64_t* luni;        // [2][N] per pass: OR of the receiver masks of a row's records (a receiver
+                         // reads a neighbour's records only when its own bit is set)
   uint64_t cr0, chb;
-  uint32_t cE, chz;      // epochs per row of cmm / cge; the lifetime in epochs (churn_horizon)
+  uint32_t cE, chz;      // epochs per row of cmm / cgt; the lifetime in epochs (churn_horizon)
   uint32_t ghoff;        // GOS: relative epoch of heartbeat 0 (habs0 - q0: 0 or 1)
   uint32_t ghk;          // GOS: last heartbeat index whose IHAVEs are inside the lifetime (~0u: no cap)
 };
@@ -170,12 +179,14 @@ struct LPullLds {
 };
 
 // Listed entries e[0..3] (entry = toff << (tshift + lb) | low << lb | lane, so
-// key = (wlo << tshift) + (entry >> lb)) into the row's candidate minima.
+// key = (wlo << tshift) + (entry >> lb)) into the row's candidate minima. Bit 63
+// marks an IHAVE entry (churn + lazy gossip, heartbeats >= gsw: glp_ihave_ent),
+// not a candidate; the host keeps every entry below bit 63.
 __device__ __forceinline__ void lp_apply_entries(uint64_t* CW, const uint64_t (&e)[4], uint32_t lmask, uint32_t lb,
                                                  uint64_t wlok, uint32_t& cb) {
 #pragma unroll
   for (int u = 0; u < 4; u++) {
-    if (e[u] == ~0ull) continue;
+    if (e[u] >> 63) continue;  // no entry (~0) or an IHAVE entry
     const uint32_t li = (uint32_t)e[u] & lmask;
     atomicMin((unsigned long long*)&CW[li], (unsigned long long)(wlok + (e[u] >> lb)));
     cb |= 1u << (li >> 6);
@@ -201,8 +212,9 @@ __device__ __forceinline__ void lp_apply_entries(uint64_t* CW, const uint64_t (&
 // IHAVE targets of v at heartbeat h among its non-mesh connections (bit e of
 // nmm: CSR entry e, held by lane e in x): the r smallest (rng, id) pairs, as a
 // mask over v's CSR row. The CSR walk is wave-uniform, h is the lane's own.
-__device__ __forceinline__ uint64_t glp_targets(uint64_t seed, uint32_t v, uint32_t h, uint32_t x, uint64_t nmm,
-                                                uint32_t deg, uint32_t r) {
+// pre = rng_pre(seed, P_GOSSIP, v): one mix per candidate.
+__device__ __forceinline__ uint64_t glp_targets(uint64_t pre, uint32_t h, uint32_t x, uint64_t nmm, uint32_t deg,
+                                                uint32_t r) {
   auto lt = [](uint64_t k1, uint32_t w1, uint64_t k2, uint32_t w2) { return k1 < k2 || (k1 == k2 && w1 < w2); };
   uint64_t kk[GT_W];
   uint32_t ww[GT_W], pp[GT_W];
@@ -211,7 +223,7 @@ __device__ __forceinline__ uint64_t glp_targets(uint64_t seed, uint32_t v, uint3
   for (uint32_t e = 0; e < deg; e++) {
     if (!((nmm >> e) & 1)) continue;  // wave-uniform
     const uint32_t w = __builtin_amdgcn_readlane(x, e);
-    const uint64_t rk = rng(seed, P_GOSSIP, v, h, w);
+    const uint64_t rk = rng_fin(pre, h, w);
     if (!lt(rk, w, kk[GT_W - 1], ww[GT_W - 1])) continue;
 #pragma unroll
     for (int q = (int)GT_W - 1; q > 0; q--) {  // insert, shifting the larger pairs up
@@ -232,7 +244,7 @@ __device__ __forceinline__ uint64_t glp_targets(uint64_t seed, uint32_t v, uint3
     for (uint32_t e = 0; e < deg; e++) {
       if (!((nmm >> e) & 1)) continue;
       const uint32_t w = __builtin_amdgcn_readlane(x, e);
-      const uint64_t rk = rng(seed, P_GOSSIP, v, h, w);
+      const uint64_t rk = rng_fin(pre, h, w);
       if (lt(pk, pw, rk, w) && lt(rk, w, bk, bw)) { bk = rk; bw = w; bp = e; }
     }
     mask |= 1ull << bp;
@@ -316,8 +328,8 @@ __device__ __forceinline__ void glp_ihave(const LPullArgs& a, uint64_t* CW, uint
 // and an answer landing at or after gB1 (the start of epoch kh + 1) is lost
 // where w is offline then or past the lifetime (offa): no IWANT is counted for
 // it (the oracle's lost_a).
-__device__ __forceinline__ void glp_ihave_chn(const LPullArgs& a, uint64_t* CW, uint32_t sw, uint32_t finT, uint64_t wlo,
-                                              uint64_t gR, uint32_t ej, uint32_t rj, uint32_t offh, uint32_t offa,
+__device__ __forceinline__ void glp_ihave_chn(const LPullArgs& a, uint64_t* CW, uint32_t sw, uint32_t nfl, uint64_t wlo,
+                                              uint64_t gR, uint32_t ej, uint32_t rj, uint32_t offa,
                                               uint64_t gB1, const uint32_t* lat, const uint32_t* sup,
                                               const uint32_t* sdn, uint32_t& cb, uint64_t& niw, uint32_t& err) {
   const int lane = threadIdx.x & 63;
@@ -329,49 +341,113 @@ __device__ __forceinline__ void glp_ihave_chn(const LPullArgs& a, uint64_t* CW, 
     const uint32_t sv = ej >> STAGE_SHIFT;
     tio = lat[sv * S + sw];  // t_i - R_k
     const uint64_t ti = gR + tio;
-    ok = ti >= wlo && ti < wlo + a.delta;
+    // a sender whose plane is empty (k_gsend's gnz) offers nothing
+    ok = ti >= wlo && ti < wlo + a.delta && a.gnz[ej & 0xFFFFFFu];
     const uint32_t su = sup[sv], sd = sdn[sw];
     aoff = lat[sw * S + sv] + su + tio + (sd > su ? sd - su : 0u);  // IWANT + answer: t_i -> arrival
   }
   uint64_t gm = __ballot(ok);
-  const uint32_t nfl = ~finT & ~offh & 0xFFFFu;  // not final before window c, online at kh
-  while (gm) {  // wave-uniform: one IHAVE sender at a time
-    const int e = __builtin_ctzll(gm);
-    gm &= gm - 1;
-    const uint32_t v = __builtin_amdgcn_readlane(ej, e) & 0xFFFFFFu;
-    const uint32_t p = __builtin_amdgcn_readlane(rj, e);
-    const uint64_t ti = gR + (uint32_t)__builtin_amdgcn_readlane(tio, e);
-    const uint64_t A = ti + (uint32_t)__builtin_amdgcn_readlane(aoff, e);
-    const uint32_t plj = reinterpret_cast<const uint16_t*>(a.gpl + (size_t)v * LP_FW)[lane];
-    uint32_t c = plj & nfl;
-    if (__ballot(c != 0) == 0) continue;
-    const uint32_t lost = A >= gB1 ? offa : 0u;  // lanes whose answer is lost
-    const uint32_t own = (uint32_t)__popc(plj);
-    uint32_t pre = own;
-    for (int off = 1; off < 64; off <<= 1) {
-      const uint32_t y = __shfl_up(pre, off);
-      if (lane >= off) pre += y;
+  constexpr int GV = 8;  // senders whose plane loads are in flight together
+  while (gm) {  // wave-uniform
+    uint32_t V[GV], P[GV], PL[GV];
+    int E[GV];
+    int nv = 0;
+#pragma unroll
+    for (int q = 0; q < GV; q++) {
+      E[q] = gm ? __builtin_ctzll(gm) : 0;
+      if (gm) { gm &= gm - 1; nv = q + 1; }
+      V[q] = __builtin_amdgcn_readlane(ej, E[q]) & 0xFFFFFFu;
+      P[q] = __builtin_amdgcn_readlane(rj, E[q]);
     }
-    pre -= own;
-    const uint64_t* ge = a.gse + (size_t)v * a.L;
-    const uint64_t kb = (A << a.tshift) | v;
-    const bool tbad = A > a.tmax;
-    while (c) {
-      const int q = __builtin_ctz(c);
-      c &= c - 1;
-      const uint64_t en = ge[pre + (uint32_t)__popc(plj & ((1u << q) - 1u))];
-      if (!((en >> p) & 1)) continue;  // w is not among v's targets at heartbeat k
-      if ((lost >> q) & 1) continue;   // the answer reaches w offline / past the lifetime
-      const uint32_t i = (uint32_t)q * 64 + lane;
-      const uint64_t x = CW[i];
-      if (x != INF64 && (x >> a.tshift) <= ti) continue;  // w has it by t_i (arrivals first at equal time)
-      niw++;
-      const uint32_t hv = (uint32_t)(en >> GSE_HOPS) + 1;
-      if (hv >= (1u << HOP_BITS)) err |= ERR_HOPS;
-      if (tbad) err |= ERR_TIME;
-      atomicMin((unsigned long long*)&CW[i], (unsigned long long)(kb | ((uint64_t)hv << a.sb)));
-      cb |= 1u << q;
+#pragma unroll
+    for (int q = 0; q < GV; q++)
+      PL[q] = q < nv ? reinterpret_cast<const uint16_t*>(a.gpl + (size_t)V[q] * LP_FW)[lane] : 0u;
+#pragma unroll
+    for (int q = 0; q < GV; q++) {
+      const uint32_t plj = PL[q];
+      uint32_t c = plj & nfl;
+      if (__ballot(c != 0) == 0) continue;  // wave-uniform (also q >= nv)
+      const uint32_t v = V[q], p = P[q];
+      const uint64_t ti = gR + (uint32_t)__builtin_amdgcn_readlane(tio, E[q]);
+      const uint64_t A = ti + (uint32_t)__builtin_amdgcn_readlane(aoff, E[q]);
+      c &= ~(A >= gB1 ? offa : 0u);  // lanes whose answer reaches w offline / past the lifetime
+      const uint64_t* ge = a.gse + (size_t)v * a.L + lane;  // v's entry of lane q*64 + lane: ge[q * 64]
+      const uint64_t kb = (A << a.tshift) | v;
+      const bool tbad = A > a.tmax;
+      while (c) {  // four of the lane's entries per round trip
+        int qv[4];
+        uint64_t en[4];
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+          qv[t] = c ? __builtin_ctz(c) : -1;
+          c &= c ? c - 1 : 0u;
+          en[t] = qv[t] >= 0 ? ge[(size_t)qv[t] * 64] : 0ull;
+        }
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+          if (qv[t] < 0 || !((en[t] >> p) & 1)) continue;  // w is not among v's targets at heartbeat k
+          const uint32_t i = (uint32_t)qv[t] * 64 + lane;
+          const uint64_t x = CW[i];
+          if (x != INF64 && (x >> a.tshift) <= ti) continue;  // w has it by t_i (arrivals first at equal time)
+          niw++;
+          const uint32_t hv = (uint32_t)(en[t] >> GSE_HOPS) + 1;
+          if (hv >= (1u << HOP_BITS)) err |= ERR_HOPS;
+          if (tbad) err |= ERR_TIME;
+          atomicMin((unsigned long long*)&CW[i], (unsigned long long)(kb | ((uint64_t)hv << a.sb)));
+          cb |= 1u << qv[t];
+        }
+      }
     }
+  }
+}
+
+// Pushed IHAVE entries (churn, heartbeats k >= gsw): k_gsend appended, for
+// every (sender v, lane m, target w), an entry t_i | hops + 1 | v | m flagged
+// by bit 63 to w's list of the window holding t_i. With the window's entries
+// and records in CW, w decides as glp_ihave does: no IWANT when the lane is
+// final before the window or CW holds a time <= t_i; else IWANT (counted
+// unless the answer lands in the next epoch where w is offline, or past the
+// lifetime), and v's answer at t_i + lat(w -> v) + ser_up(v) + lat(v -> w) + dn
+// is one more candidate.
+__device__ __forceinline__ void glp_ihave_ent(const LPullArgs& a, uint64_t* CW, uint32_t w, uint32_t sw, uint32_t finT,
+                                              const uint64_t* lst, uint32_t due, uint64_t wlok, const uint32_t* lat,
+                                              const uint32_t* sup, const uint32_t* sdn, uint32_t& cb, uint64_t& niw,
+                                              uint32_t& err) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t S = a.S, lmask = (1u << a.lb) - 1;
+  const uint64_t smask = (1ull << a.sb) - 1;
+  // a row the pushes of the built heartbeat overflowed scans its neighbours'
+  // planes instead (glp_ihave_chn): its pushed entries of that heartbeat are
+  // left to the scan (pushed entries are taken while GC_BK is their heartbeat's)
+  if (a.gtag[w] == (uint16_t)a.gctl[GC_BK]) return;
+  wave_lds_sync();
+  for (uint32_t f0 = 0; f0 < due; f0 += 64) {
+    const uint32_t f = f0 + lane;
+    const uint64_t en = f < due ? lst[f] : 0ull;
+    const bool ih = (en >> 63) != 0;
+    if (__ballot(ih) == 0) continue;
+    const uint32_t li = ih ? (uint32_t)en & lmask : 0u;
+    // lane li's final bit lives in lane li & 63 (bit li >> 6)
+    const uint32_t fb = (uint32_t)__shfl((int)finT, (int)(li & 63u));
+    if (!ih || ((fb >> (li >> 6)) & 1u)) continue;  // final before window c: w has it
+    const uint64_t key = wlok + ((en & ~(1ull << 63)) >> a.lb);
+    const uint64_t ti = key >> a.tshift;
+    const uint64_t x = CW[li];
+    if (x != INF64 && (x >> a.tshift) <= ti) continue;  // w has it by t_i
+    const uint32_t v = (uint32_t)(key & smask), hv = (uint32_t)(key >> a.sb) & ((1u << HOP_BITS) - 1);
+    const uint32_t sv = a.stage[v];
+    const uint32_t su = sup[sv], sd = sdn[sw];
+    const uint64_t A = ti + lat[sw * S + sv] + su + lat[sv * S + sw] + (sd > su ? sd - su : 0u);
+    const uint64_t kt = udiv53(a.cr0 + ti, a.chb), B1 = (kt + 1) * a.chb - a.cr0;
+    if (A >= B1) {  // the answer lands in epoch kt + 1: lost where w is offline then (or past the lifetime)
+      const uint32_t ko = kt + 1 <= a.chz + 1 ? (uint32_t)kt + 1 : a.chz + 1;
+      const uint32_t ob = reinterpret_cast<const uint16_t*>(a.coff + ((size_t)ko * a.N + w) * LP_FW)[li & 63u];
+      if ((ob >> (li >> 6)) & 1u) continue;
+    }
+    niw++;
+    if (A > a.tmax) err |= ERR_TIME;
+    atomicMin((unsigned long long*)&CW[li], (unsigned long long)((A << a.tshift) | ((uint64_t)hv << a.sb) | v));
+    cb |= 1u << (li >> 6);
   }
 }
 
@@ -434,6 +510,8 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
   const uint64_t* rrec = PART ? a.rpk : a.lrec + pb * NL * RW;
   const uint32_t* rcnt = PART ? a.rcg : a.lcnt + (size_t)pb * a.N;  // indexed by global peer id
   uint64_t* wrec = a.lrec + nb * NL * RW;
+  const uint64_t* runi = CHN ? a.luni + (size_t)pb * a.N : nullptr;
+  uint64_t* wuni = CHN ? a.luni + (size_t)nb * a.N : nullptr;
   uint32_t* wcnt = a.lcnt + (size_t)nb * a.N;
   const uint32_t* lat = a.tables;
   const uint32_t* sup = a.tables + S * S;
@@ -441,9 +519,11 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
   // lazy gossip: does this window hold IHAVE arrivals of the built heartbeat (k_lctl)?
   bool gw = false;
   uint64_t gR = 0;  // that heartbeat, relative to every t_pub
+  uint16_t gbk = 0;  // CHN: the gtag of rows the built heartbeat's planes target
   if constexpr (GOS) {
     gw = a.gctl[GC_GW] != 0;
     gR = a.grel0 + (a.gctl[GC_BK] - 1) * a.ghb;
+    gbk = (uint16_t)a.gctl[GC_BK];
   }
   uint64_t niw = 0;  // IWANTs sent
   // churn (CHN): the epoch boundaries the pass can meet. A record whose sender
@@ -456,6 +536,7 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
   uint32_t xBoff = 0, kc = 0;
   const uint32_t* offn = nullptr;
   uint32_t gkh = 0;     // GOS + CHN: relative epoch of the built heartbeat
+  uint32_t calT = 0;    // GOS + CHN: the published lanes (lane j: bit q = lane q*64 + j)
   uint64_t gB1 = INF64;  // its next epoch's start (relative time)
   if constexpr (CHN) {
     const uint64_t ks = udiv53(a.cr0 + lo, a.chb), Bs = (ks + 1) * a.chb - a.cr0;
@@ -468,6 +549,7 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     const uint64_t Bc = ((uint64_t)kc + 1) * a.chb - a.cr0;
     if (Bc < wlo + a.delta) eBc = Bc;
     if constexpr (GOS) {
+      calT = reinterpret_cast<const uint16_t*>(a.calive)[threadIdx.x & 63];
       gkh = a.ghoff + (uint32_t)(a.gctl[GC_BK] ? a.gctl[GC_BK] - 1 : 0);
       if (gkh > a.chz) gkh = a.chz;
       gB1 = ((uint64_t)gkh + 1) * a.chb - a.cr0;
@@ -529,7 +611,7 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
         mo = umin32(mo, j >= cs ? j - cs : j + kk - cs);
       }
       const uint32_t mh = mo == ~0u ? ~0u : sat32(hlo64 + (uint64_t)mo * a.dG);
-      if (GOS && gw) act |= !((a.rowdone[wl >> 5] >> (wl & 31)) & 1u);
+      if (GOS && gw) act |= !((a.rowdone[wl >> 5] >> (wl & 31)) & 1u) && (!CHN || a.gtag[wl] == gbk);
       if (pull && !act) {
         if constexpr (CHN) {  // CSR rows, 16 entries at a time until the padding
           const uint4* mp = reinterpret_cast<const uint4*>(a.ccol + (size_t)wl * CELL_W);
@@ -575,7 +657,10 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     if (w < a.N) {
       ej = a.ccol[(size_t)w * CELL_W + lane];
       rj = a.cpos[(size_t)w * CELL_W + lane];
-      if (pull && ej != EMPTY) cj = rcnt[ej & 0xFFFFFFu];
+      if (pull && ej != EMPTY) {
+        cj = rcnt[ej & 0xFFFFFFu];
+        if (!((runi[ej & 0xFFFFFFu] >> (rj & 63u)) & 1)) cj = 0;  // no record of it is for w
+      }
       if (lane < (int)LP_SW) sv = a.st[(size_t)w * LP_SW + lane];
     }
   } else if (w < a.N && lane < (int)MESH_W) {
@@ -612,13 +697,26 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     // dropped (ERR_LIST, the batch re-runs on k_pull): read only what was written
     const uint32_t due = umin32(__builtin_amdgcn_readlane(sv, cslot), a.lcap);
     // gossip windows: a row with a lane not yet final may take IWANT answers
-    const bool gossip_row = GOS && gw && !((dw >> (w & 31)) & 1u);
+    bool gossip_row = GOS && gw && !((dw >> (w & 31)) & 1u) && (!CHN || a.gtag[w] == gbk);
+    uint32_t gnfl = 0, goffa = 0;  // CHN: lanes that may take an IHAVE (not final, online at kh, published)
+    if constexpr (GOS && CHN) {
+      if (gossip_row) {
+        const uint32_t fT = reinterpret_cast<const uint16_t*>(a.fin + (size_t)w * LP_FW)[lane];
+        const uint32_t offh = reinterpret_cast<const uint16_t*>(a.coff + ((size_t)gkh * a.N + w) * LP_FW)[lane];
+        goffa = reinterpret_cast<const uint16_t*>(a.coff + ((size_t)(gkh + 1) * a.N + w) * LP_FW)[lane];
+        gnfl = ~fT & ~offh & calT & 0xFFFFu;
+        gossip_row = __ballot(gnfl != 0) != 0;
+      }
+    }
     if (cand == 0 && due == 0 && !gossip_row) {  // nothing to apply, nothing due: the pending windows stay
       if (lane == 0) wcnt[w] = 0;
       if (lane < (int)K && sv) nmh = umin32(nmh, lwhi);
       if (pull && lane < (int)HW && ej2 != EMPTY) {
         cj2 = rcnt[ej2 & 0xFFFFFFu];
         if constexpr (PART) ro2 = a.roff[ej2 & 0xFFFFFFu];
+        if constexpr (CHN) {
+          if (!((runi[ej2 & 0xFFFFFFu] >> (rj2 & 63u)) & 1)) cj2 = 0;
+        }
       }
       ej = ej2; rj = rj2; cj = cj2; sv = sv2; ro = ro2; dw = dw2;
       PP_T(tS);
@@ -821,11 +919,8 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     //     iff CW holds a time <= t_i there; else w sends IWANT and v's answer
     //     (its key's hops + 1, src v) is one more candidate, after window c.
     if constexpr (GOS && CHN) {
-      if (gossip_row) {
-        const uint32_t offh = reinterpret_cast<const uint16_t*>(a.coff + ((size_t)gkh * a.N + w) * LP_FW)[lane];
-        const uint32_t offa = reinterpret_cast<const uint16_t*>(a.coff + ((size_t)(gkh + 1) * a.N + w) * LP_FW)[lane];
-        glp_ihave_chn(a, CW, sw, finT, wlo, gR, ej, rj, offh, offa, gB1, lat, sup, sdn, cb, niw, err);
-      }
+      if (gossip_row) glp_ihave_chn(a, CW, sw, gnfl, wlo, gR, ej, rj, goffa, gB1, lat, sup, sdn, cb, niw, err);
+      if (due) glp_ihave_ent(a, CW, w, sw, finT, lst, due, wlok, lat, sup, sdn, cb, niw, err);
     } else if constexpr (GOS) {
       if (gossip_row) glp_ihave(a, CW, w, sw, finT, wlo, gR, lat, sup, sdn, cb, niw, err);
     }
@@ -835,6 +930,9 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     if (pull && lane < (int)HW && ej2 != EMPTY) {  // next row's lists
       cj2 = rcnt[ej2 & 0xFFFFFFu];
       if constexpr (PART) ro2 = a.roff[ej2 & 0xFFFFFFu];
+      if constexpr (CHN) {
+        if (!((runi[ej2 & 0xFFFFFFu] >> (rj2 & 63u)) & 1)) cj2 = 0;
+      }
     }
     // 3. classify the minima of the touched chunks: final lanes are dropped
     //    (candidates are not filtered on the way in), a minimum in window c is
@@ -941,6 +1039,7 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     PP_ADD(4, tP - tC);
     // 4. sparse: forward targets, uplink FIFO and one record per arrival (k_pull's step 4)
     uint32_t ecnt = 0;
+    uint64_t uni = 0;  // churn: the receivers of any of the row's records
     if (cnt) {
       const uint32_t deg = (uint32_t)__popcll(__ballot(ej != EMPTY));  // rows are packed
       const uint32_t serw = sup[sw];
@@ -1015,6 +1114,7 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
           const size_t ri = (size_t)w * LL + ecnt +
                             __builtin_amdgcn_mbcnt_hi((uint32_t)(wm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wm, 0u));
           if constexpr (CHN) {
+            uni |= im64;
             const uint64_t r0 = ((start - wlo) << 32) | ((uint64_t)hp << LP_HOP_SHIFT) | i;
             *reinterpret_cast<uint4*>(wrec + ri * 2) =
                 make_uint4((uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)im64, (uint32_t)(im64 >> 32));
@@ -1040,6 +1140,10 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
       if (lane <= (int)LP_LOG) a.st[(size_t)w * LP_SW + lane] = nv;
       if (lane < (int)K && nv) nmh = umin32(nmh, lwhi);
     }
+    if constexpr (CHN) {
+      for (int off = 32; off > 0; off >>= 1) uni |= __shfl_xor(uni, off);
+      if (lane == 0) wuni[w] = uni;
+    }
     if (lane == 0) wcnt[w] = ecnt;
     nrec += ecnt;
     // 6. LDS back to INF for the next row: the touched chunks. cb passes
@@ -1057,8 +1161,8 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
   }
   }
 #ifdef GS_PULL_PROF
-  if (lane == 0 && a.pass < 32)
-    for (int k = 0; k < 8; k++) atomicAdd(&g_pull_prof[a.pass][k], (unsigned long long)pp[k]);
+  if (lane == 0)
+    for (int k = 0; k < 8; k++) atomicAdd(&g_pull_prof[a.pass < 31 ? a.pass : 31][k], (unsigned long long)pp[k]);
 #endif
   for (int off = 32; off > 0; off >>= 1) nmh = umin32(nmh, __shfl_xor(nmh, off));
   const uint64_t nmin = nmh == ~0u ? INF64 : (uint64_t)nmh << 32;
@@ -1163,10 +1267,113 @@ __global__ void k_lctl(LPullArgs a) {
 // writes the plane and the entries (target mask | hops << 58) in rank order.
 // A row none of whose non-mesh connections has a lane left to finalise is
 // skipped: no pass reads its plane (row-done bits never clear within a batch).
+// Pushed IHAVEs of sender row v at heartbeat k (churn, k >= gsw). Lane j holds
+// the entries eq[q] (target mask | hops << 58) of v's lanes q*64 + j it gossips.
+// For each connection t = ccx[e] (wave-uniform), the lanes whose targets
+// include t and that t has not finalised yet (its final bits; most IHAVEs reach
+// a peer that has the message, those are dropped here) become flagged entries
+// t_i | hops + 1 | v | lane in t's list of the window holding t_i = R_k +
+// lat(v -> t). A target that collects more than GP_CAP of them this heartbeat
+// scans the planes instead (gtag; glp_ihave_ent then ignores its entries).
+constexpr uint32_t GP_CAP = 192;
+template <uint32_t CH>
+__device__ __forceinline__ void glp_push(const LPullArgs& a, uint32_t v, uint64_t bk, uint64_t Rk, uint64_t wcur,
+                                         const uint32_t* ccx, uint32_t deg, uint32_t plj, const uint64_t* eq,
+                                         uint32_t calT, uint32_t& err) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t S = a.S, sv = a.stage[v];
+  const uint64_t dcur = udiv53(wcur, a.delta);  // the window the coming pass emits
+  // connections whose targets include any offered lane, eight final-bit rows in flight at once
+  uint64_t ce = 0;
+  for (uint32_t e = 0; e < deg; e++) {  // wave-uniform
+    uint32_t off = 0;
+#pragma unroll
+    for (int q = 0; q < (int)CH; q++) off |= (uint32_t)((eq[q] >> e) & 1) << q;
+    if (__ballot((off & plj) != 0)) ce |= 1ull << e;
+  }
+  while (ce) {
+    constexpr int GT = 8;
+    uint32_t E[GT], FT[GT];
+    int nt = 0;
+#pragma unroll
+    for (int g = 0; g < GT; g++) {
+      E[g] = ce ? (uint32_t)__builtin_ctzll(ce) : 0u;
+      if (ce) { ce &= ce - 1; nt = g + 1; }
+    }
+#pragma unroll
+    for (int g = 0; g < GT; g++)
+      FT[g] = g < nt ? reinterpret_cast<const uint16_t*>(a.fin + (size_t)(ccx[E[g]] & 0xFFFFFFu) * LP_FW)[lane] : 0xFFFFu;
+    auto one = [&](uint32_t e, uint32_t ftg) {
+
+    uint32_t off = 0;  // lane j: chunks q whose lane targets t
+#pragma unroll
+    for (int q = 0; q < (int)CH; q++) off |= (uint32_t)((eq[q] >> e) & 1) << q;
+    off &= plj;
+    const uint32_t xe = ccx[e], t = xe & 0xFFFFFFu;
+    const uint32_t pj = off & ~ftg & calT;
+    const uint32_t cj = (uint32_t)__popc(pj);
+    uint32_t n = cj;
+    for (int o = 32; o > 0; o >>= 1) n += (uint32_t)__shfl_xor((int)n, o);
+    if (n == 0) return;
+    uint32_t ok = 0, pos0 = 0, slot = 0;
+    uint64_t toff = 0;
+    if (lane == 0) {
+      uint32_t old = a.gpc[t], nw;
+      for (;;) {  // count the row's pushes of heartbeat bk (a stale tag restarts the count)
+        const uint32_t cnt = (old >> 16) == (uint32_t)bk ? (old & 0xFFFFu) : 0u;
+        nw = ((uint32_t)bk << 16) | (cnt + n < 0xFFFFu ? cnt + n : 0xFFFFu);
+        const uint32_t o2 = atomicCAS(&a.gpc[t], old, nw);
+        if (o2 == old) break;
+        old = o2;
+      }
+      if ((nw & 0xFFFFu) > GP_CAP) {
+        a.gtag[t] = (uint16_t)bk;  // t scans the planes of this heartbeat
+      } else {
+        const uint64_t ti = Rk + a.tables[sv * S + (xe >> STAGE_SHIFT)];
+        const uint64_t d = udiv53(ti, a.delta);  // the window of t_i
+        if (d < dcur || d >= dcur + a.K) {
+          err |= ERR_RING;  // (k_lctl builds before the first window that can hold an IHAVE)
+        } else {
+          slot = (uint32_t)(d % a.K);
+          toff = ti - d * a.delta;
+          pos0 = atomicAdd(&a.st[(size_t)t * LP_SW + slot], n);
+          ok = 1;
+        }
+      }
+    }
+    if (!__shfl((int)ok, 0)) return;
+    pos0 = (uint32_t)__shfl((int)pos0, 0);
+    slot = (uint32_t)__shfl((int)slot, 0);
+    toff = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(toff >> 32), 0) << 32) | (uint32_t)__shfl((int)(uint32_t)toff, 0);
+    uint32_t pre = cj;  // exclusive prefix of the lanes' counts
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)pre, o);
+      if (lane >= o) pre += y;
+    }
+    pre -= cj;
+    uint64_t* lst = a.blk + ((size_t)slot * a.N + t) * a.ls;
+    uint32_t c = pj;
+    while (c) {
+      const int q = __builtin_ctz(c);
+      c &= c - 1;
+      const uint32_t pos = pos0 + pre++;
+      if (pos >= a.lcap) { err |= ERR_LIST; continue; }
+      const uint32_t hv = (uint32_t)(eq[q] >> GSE_HOPS) + 1;
+      if (hv >= (1u << HOP_BITS)) { err |= ERR_HOPS; continue; }
+      lst[pos] = (1ull << 63) | (toff << (a.tshift + a.lb)) | ((((uint64_t)hv << a.sb) | v) << a.lb) |
+                 ((uint32_t)q * 64 + lane);
+    }
+    };
+#pragma unroll
+    for (int g = 0; g < GT; g++)
+      if (g < nt) one(E[g], FT[g]);  // wave-uniform
+  }
+}
+
 // Churn (CHN): a lane's epoch is E0 + cq[m] + kh (kh = ghoff + k, the
-// heartbeat's relative epoch), its IHAVE-eligible entries cge[v][..] (0 when v
-// is offline then), and nothing past the lifetime (kh > chz); lanes with no
-// target get no plane bit.
+// heartbeat's relative epoch), its targets the ones k_cprep selected for (v,
+// that epoch) (none when v is offline then), and nothing past the lifetime
+// (kh > chz); lanes with no target get no plane bit.
 template <uint32_t CH, bool CHN = false>
 __global__ __launch_bounds__(TB) void k_gsend(LPullArgs a) {
   const uint64_t bk = a.gctl[GC_BUILD];
@@ -1174,17 +1381,22 @@ __global__ __launch_bounds__(TB) void k_gsend(LPullArgs a) {
   __shared__ uint64_t ent[PULL_WAVES][CH * 64];
   __shared__ uint32_t sel[PULL_WAVES][CH * 64];
   __shared__ uint32_t pl[PULL_WAVES][LP_FW];
+  __shared__ uint32_t cxs[PULL_WAVES][CHN ? CELL_W : 1];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint64_t lanelt = (1ull << lane) - 1;
   const uint64_t k = bk - 1, Rk = a.grel0 + k * a.ghb;
+  const uint64_t wcur = a.gctl[GC_E] - a.delta;  // start of the window the coming pass emits
+  const uint32_t calT = CHN ? reinterpret_cast<const uint16_t*>(a.calive)[threadIdx.x & 63] : 0u;
   const bool haslo = k >= a.ghist;
   const uint64_t Rlo = haslo ? a.grel0 + (k - a.ghist) * a.ghb : 0;
   const uint32_t hmask = (1u << HOP_BITS) - 1;
   for (uint32_t v = blockIdx.x * PULL_WAVES + wv; v < a.N; v += gridDim.x * PULL_WAVES) {
     uint32_t deg, x = EMPTY;
     bool nm = false;
+    uint32_t* ccx = cxs[wv];  // CHN: the row's CSR entries (stage << 24 | peer) for glp_push
     if constexpr (CHN) {
       const uint32_t xe = a.ccol[(size_t)v * CELL_W + lane];
+      ccx[lane] = xe;
       nm = xe != EMPTY;  // any connection may be outside the lane's epoch mesh
       x = nm ? xe & 0xFFFFFFu : EMPTY;
       deg = (uint32_t)__popcll(__ballot(nm));
@@ -1198,9 +1410,13 @@ __global__ __launch_bounds__(TB) void k_gsend(LPullArgs a) {
     }
     bool need = false;
     if (nm) need = !((a.rowdone[x >> 5] >> (x & 31)) & 1u);
-    if (__ballot(need) == 0) continue;  // wave-uniform
+    if (__ballot(need) == 0) {  // wave-uniform
+      if (CHN && lane == 0) a.gnz[v] = 0;
+      continue;
+    }
     if (lane < (int)LP_FW) pl[wv][lane] = 0;
     const uint64_t nmm = __ballot(nm);
+    const uint64_t rpre = rng_pre(a.gseed, P_GOSSIP, v);
     const uint32_t nonmesh = (uint32_t)__popcll(nmm);
     uint32_t r = (uint32_t)(((uint64_t)nonmesh * a.ggf) / 1000);
     if (r < a.gd_lazy) r = a.gd_lazy;
@@ -1208,7 +1424,18 @@ __global__ __launch_bounds__(TB) void k_gsend(LPullArgs a) {
     // 1. the senders of k from the log: lane | hops << 16
     const uint32_t n = a.st[(size_t)v * LP_SW + LP_LOG];
     uint32_t ns = 0;
-    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+    // the log is in window order: entries before the first one whose window
+    // holds R_(k - hist) or later are not senders of k; 64 samples locate it
+    uint32_t i_start = 0;
+    if (haslo && n > 64) {
+      const uint32_t stride = (n + 63) / 64, ip = (uint32_t)lane * stride;
+      const uint64_t T = (Rlo / a.delta) * a.delta;
+      const uint64_t sk = ip < n ? a.keys[(size_t)v * a.L + ip] : INF64;
+      const uint64_t sm = __ballot(ip >= n || (sk >> a.tshift) >= T);
+      const uint32_t J = sm ? (uint32_t)__builtin_ctzll(sm) : 64u;
+      i_start = J == 0 ? 0u : (J - 1) * stride + 1;
+    }
+    for (uint32_t i0 = i_start; i0 < n; i0 += 64) {
       const uint32_t i = i0 + lane;
       const uint64_t key = i < n ? a.keys[(size_t)v * a.L + i] : INF64;
       const uint64_t t = key >> a.tshift;
@@ -1223,24 +1450,26 @@ __global__ __launch_bounds__(TB) void k_gsend(LPullArgs a) {
     }
     wave_lds_sync();
     // 2. each sender lane's targets at its message's heartbeat habs0[m] + k
+    uint64_t tu = 0;  // CHN: every target of the row's planes
     for (uint32_t j0 = 0; j0 < ns; j0 += 64) {
       const bool jv = j0 + lane < ns;
       const uint32_t s = jv ? sel[wv][j0 + lane] : 0u;
       const uint32_t m = s & 0xFFFFu;
       const uint32_t h = jv ? (uint32_t)(a.habs0[m] + k) : 0u;
-      uint64_t lm = nmm;
-      uint32_t lr = r;
-      if constexpr (CHN) {  // the lane's epoch: its eligible set and fan-out
+      uint64_t mask;
+      if constexpr (CHN) {  // the targets k_cprep selected for (v, the lane's epoch)
         const uint32_t kh = a.ghoff + (uint32_t)k;
-        lm = jv && kh <= a.chz ? a.cge[(size_t)v * a.cE + a.cq[m] + kh] : 0ull;
-        const uint32_t nn = (uint32_t)__popcll(lm);
-        lr = (uint32_t)(((uint64_t)nn * a.ggf) / 1000);
-        if (lr < a.gd_lazy) lr = a.gd_lazy;
-        if (lr > nn) lr = nn;
+        mask = jv && kh <= a.chz ? a.cgt[(size_t)v * a.cE + a.cq[m] + kh] : 0ull;
+      } else {
+        mask = glp_targets(rpre, h, x, nmm, deg, r);
       }
-      const uint64_t mask = glp_targets(a.gseed, v, h, x, lm, deg, lr);
       if (jv && (!CHN || mask)) {
-        ent[wv][m] = mask | ((uint64_t)(s >> 16) << GSE_HOPS);
+        const uint64_t en = mask | ((uint64_t)(s >> 16) << GSE_HOPS);
+        if constexpr (CHN) {  // churn: entries at their lane's position
+          a.gse[(size_t)v * a.L + m] = en;
+          tu |= mask;
+        }
+        ent[wv][m] = en;
         atomicOr(&pl[wv][(m & 63) >> 1], 1u << (16 * (m & 1) + (m >> 6)));
       }
     }
@@ -1248,6 +1477,23 @@ __global__ __launch_bounds__(TB) void k_gsend(LPullArgs a) {
     // 3. the plane, and the entries in rank order (lane j's bits q ascending after the lanes below j)
     if (lane < (int)LP_FW) a.gpl[(size_t)v * LP_FW + lane] = pl[wv][lane];
     const uint32_t plj = (pl[wv][lane >> 1] >> (16 * (lane & 1))) & 0xFFFFu;
+    if constexpr (CHN) {
+      const bool nz = __ballot(plj != 0) != 0;
+      if (lane == 0) a.gnz[v] = nz ? 1 : 0;
+      if (nz && k < a.gsw) {  // every target of an early heartbeat scans the planes
+        for (int off = 32; off > 0; off >>= 1) tu |= __shfl_xor(tu, off);
+        if ((uint32_t)lane < deg && ((tu >> lane) & 1)) a.gtag[x] = (uint16_t)bk;
+      } else if (nz) {  // later heartbeats push what a target may still need
+        uint64_t eq[CH];
+#pragma unroll
+        for (int q = 0; q < (int)CH; q++) eq[q] = ((plj >> q) & 1) ? ent[wv][q * 64 + lane] : 0ull;
+        uint32_t err = 0;
+        glp_push<CH>(a, v, bk, Rk, wcur, ccx, deg, plj, eq, calT, err);
+        if (err) atomicOr((unsigned*)&a.counters[C_ERR], err);
+      }
+      wave_lds_sync();
+      continue;  // (entries are in place)
+    }
     const uint32_t own = (uint32_t)__popc(plj);
     uint32_t pre = own;
     for (int off = 1; off < 64; off <<= 1) {

@@ -147,32 +147,15 @@ __device__ __forceinline__ void drop_key(uint64_t (&key)[HB_PER_LANE], uint32_t 
     if ((uint32_t)k == (sel / G)) key[k] = INF64;
 }
 
+// The decisions of row_heartbeat on the row's loaded entries (f, w, elig) and
+// its mesh / outbound counts m, o.
 template <int G>
-__device__ __forceinline__ void row_heartbeat(const MeshArgs& a, uint32_t u) {
+__device__ __forceinline__ void row_heartbeat_rest(const MeshArgs& a, uint32_t u, uint64_t b, uint32_t deg,
+                                                   const uint32_t (&f)[HB_PER_LANE], const uint32_t (&w)[HB_PER_LANE],
+                                                   const bool (&elig)[HB_PER_LANE], uint32_t m, uint32_t o) {
   const int lane = threadIdx.x & (G - 1);
   const int gbase = (threadIdx.x & 63) & ~(G - 1);
   (void)gbase;
-  if (is_off(a.off, u)) return;  // wave-uniform
-  const uint64_t b = a.row[u], en = a.row[u + 1];
-  const uint32_t deg = (uint32_t)(en - b);
-  uint32_t f[HB_PER_LANE], w[HB_PER_LANE];
-  bool elig[HB_PER_LANE];  // not in mesh, back-off over, neighbour online
-  uint32_t m = 0, o = 0;
-#pragma unroll
-  for (int k = 0; k < HB_PER_LANE; k++) {
-    const uint32_t i = (uint32_t)(k * G + lane);
-    f[k] = 0;
-    w[k] = 0;
-    elig[k] = false;
-    if (k * G >= (int)deg) continue;  // wave-uniform
-    if (i < deg) {
-      f[k] = a.flags[b + i];
-      w[k] = a.col[b + i];
-      elig[k] = !(f[k] & F_MESH) && a.epoch > a.until[b + i] && !is_off(a.off, w[k]);
-    }
-    m += (uint32_t)__popcll(gballot<G>(f[k] & F_MESH));
-    o += (uint32_t)__popcll(gballot<G>((f[k] & F_MESH) && (f[k] & F_OUT)));
-  }
   const int fpack = (int)(f[0] | (f[1] << 8) | (f[2] << 16) | (f[3] << 24));
   auto flag_of = [&](uint32_t sel) {  // flags of entry sel, from the lane holding it
     return ((uint32_t)__shfl(fpack, gbase + (int)(sel % G)) >> (8 * (sel / G))) & 0xFFu;
@@ -295,6 +278,84 @@ __device__ __forceinline__ void row_heartbeat(const MeshArgs& a, uint32_t u) {
   }
 }
 
+
+template <int G>
+__device__ __forceinline__ void row_heartbeat(const MeshArgs& a, uint32_t u) {
+  const int lane = threadIdx.x & (G - 1);
+  const int gbase = (threadIdx.x & 63) & ~(G - 1);
+  (void)gbase;
+  if (is_off(a.off, u)) return;  // wave-uniform
+  const uint64_t b = a.row[u], en = a.row[u + 1];
+  const uint32_t deg = (uint32_t)(en - b);
+  uint32_t f[HB_PER_LANE], w[HB_PER_LANE];
+  bool elig[HB_PER_LANE];  // not in mesh, back-off over, neighbour online
+  uint32_t m = 0, o = 0;
+#pragma unroll
+  for (int k = 0; k < HB_PER_LANE; k++) {
+    const uint32_t i = (uint32_t)(k * G + lane);
+    f[k] = 0;
+    w[k] = 0;
+    elig[k] = false;
+    if (k * G >= (int)deg) continue;  // wave-uniform
+    if (i < deg) {
+      f[k] = a.flags[b + i];
+      w[k] = a.col[b + i];
+      elig[k] = !(f[k] & F_MESH) && a.epoch > a.until[b + i] && !is_off(a.off, w[k]);
+    }
+    m += (uint32_t)__popcll(gballot<G>(f[k] & F_MESH));
+    o += (uint32_t)__popcll(gballot<G>((f[k] & F_MESH) && (f[k] & F_OUT)));
+  }
+  row_heartbeat_rest<G>(a, u, b, deg, f, w, elig, m, o);
+}
+
+// Heartbeat step of an event-driven epoch for one row (row base b, degree deg
+// from the block's activity scan), every load issued once: last epoch's
+// proposals cleared (propd), links to offline peers dropped (the disconnect),
+// then the heartbeat decisions on the same registers — the results of the
+// prop clear + row_disconnect + row_heartbeat sequence. Returns (group-uniform)
+// whether the disconnect dropped a mesh link.
+template <int G>
+__device__ __forceinline__ bool row_hb_ev(const MeshArgs& a, uint32_t u, uint64_t b, uint32_t deg, bool propd,
+                                          bool ou) {
+  const int lane = threadIdx.x & (G - 1);
+  uint32_t f[HB_PER_LANE], w[HB_PER_LANE], un[HB_PER_LANE];
+  bool elig[HB_PER_LANE];
+#pragma unroll
+  for (int k = 0; k < HB_PER_LANE; k++) {
+    const uint32_t i = (uint32_t)(k * G + lane);
+    const bool v = i < deg;
+    f[k] = v ? a.flags[b + i] : 0u;
+    w[k] = v ? a.col[b + i] : 0u;
+    un[k] = v ? a.until[b + i] : 0u;
+  }
+  if (propd)  // last epoch's proposals (read by the neighbours until its apply step)
+#pragma unroll
+    for (int k = 0; k < HB_PER_LANE; k++)
+      if ((uint32_t)(k * G + lane) < deg) a.prop[b + k * G + lane] = 0;
+  bool ch = false;
+#pragma unroll
+  for (int k = 0; k < HB_PER_LANE; k++) {
+    const uint32_t i = (uint32_t)(k * G + lane);
+    const bool offw = i < deg && is_off(a.off, w[k]);
+    if (i < deg && (f[k] & F_MESH) && (ou || offw)) {  // disconnect: no back-off
+      f[k] &= ~(uint32_t)F_MESH;
+      a.flags[b + i] = (uint8_t)f[k];
+      ch = true;
+    }
+    elig[k] = i < deg && !(f[k] & F_MESH) && a.epoch > un[k] && !offw;
+  }
+  const bool dirty = gballot<G>(ch) != 0;
+  if (ou) return dirty;  // offline: the heartbeat decides nothing
+  uint32_t m = 0, o = 0;
+#pragma unroll
+  for (int k = 0; k < HB_PER_LANE; k++) {
+    m += (uint32_t)__popcll(gballot<G>(f[k] & F_MESH));
+    o += (uint32_t)__popcll(gballot<G>((f[k] & F_MESH) && (f[k] & F_OUT)));
+  }
+  row_heartbeat_rest<G>(a, u, b, deg, f, w, elig, m, o);
+  return dirty;
+}
+
 template <int G>
 __global__ __launch_bounds__(TB) void k_heartbeat(MeshArgs a) {
   const uint32_t u = (blockIdx.x * TB + threadIdx.x) / G;
@@ -306,12 +367,10 @@ __global__ __launch_bounds__(TB) void k_heartbeat(MeshArgs a) {
 // order — (latency u->w, id), by wave argmin — with the running mesh size c.
 // Returns (group-uniform) whether a GRAFT was accepted (w's mesh changed).
 template <int G>
-__device__ __forceinline__ bool row_handle_graft(const MeshArgs& a, uint32_t w) {
+__device__ __forceinline__ bool row_handle_graft(const MeshArgs& a, uint32_t w, uint64_t b, uint32_t deg) {
   const int lane = threadIdx.x & (G - 1);
   const int gbase = (threadIdx.x & 63) & ~(G - 1);
   (void)gbase;
-  const uint64_t b = a.row[w], en = a.row[w + 1];
-  const uint32_t deg = (uint32_t)(en - b);
   const uint32_t sw = a.stage[w];
   uint32_t f[HB_PER_LANE], p[HB_PER_LANE], r[HB_PER_LANE], un[HB_PER_LANE];
   uint64_t lvl[HB_PER_LANE];  // latency u->w of a proposing neighbour u, else INF64
@@ -376,7 +435,7 @@ __device__ __forceinline__ bool row_handle_graft(const MeshArgs& a, uint32_t w) 
 template <int G>
 __global__ __launch_bounds__(TB) void k_handle_graft(MeshArgs a) {
   const uint32_t w = (blockIdx.x * TB + threadIdx.x) / G;
-  if (w < a.N) row_handle_graft<G>(a, w);  // group-uniform
+  if (w < a.N) row_handle_graft<G>(a, w, a.row[w], (uint32_t)(a.row[w + 1] - a.row[w]));  // group-uniform
 }
 
 // Apply the epoch's decisions, one peer per wave (lane per entry). The change
@@ -725,14 +784,12 @@ __global__ __launch_bounds__(TB) void k_ev_init(MeshArgs a) {
 // kept in registers instead of re-read. Same results as row_apply +
 // row_counts + row_extract + mark_departure.
 template <int G>
-__device__ __forceinline__ void row_apply_ev(const MeshArgs& a, uint32_t u, bool need, bool dirty, bool depart,
-                                             uint32_t* mesh) {
+__device__ __forceinline__ void row_apply_ev(const MeshArgs& a, uint32_t u, uint64_t b, uint32_t deg, bool need,
+                                             bool dirty, bool depart, uint32_t* mesh) {
   uint64_t mmask = 0;  // the new mesh as a mask over the CSR row (entries < 64)
   const int lane = threadIdx.x & (G - 1);
   uint8_t* P = a.pst;
   const uint32_t N = a.N;
-  const uint64_t b = a.row[u];
-  const uint32_t deg = (uint32_t)(a.row[u + 1] - b);
   uint32_t f[HB_PER_LANE], pp[HB_PER_LANE], rv[HB_PER_LANE], cw[HB_PER_LANE], pr[HB_PER_LANE], sg[HB_PER_LANE];
 #pragma unroll
   for (int k = 0; k < HB_PER_LANE; k++) {
@@ -810,7 +867,11 @@ enum : int { EV_HB = 0, EV_GRAFT = 1, EV_APPLY = 2 };
 constexpr uint32_t EV_ROWS = 64;
 template <int G, int STEP>
 __global__ __launch_bounds__(TB) void k_ev_step(MeshArgs a, uint32_t* mesh, const uint32_t* mesh_prev) {
-  __shared__ uint32_t act[EV_ROWS];
+  // per active row: id, CSR base, degree, the step's flags (loaded by the scan,
+  // so a row's own work starts with its entries)
+  __shared__ uint32_t act[EV_ROWS], actd[EV_ROWS];
+  __shared__ uint64_t actb[EV_ROWS];
+  __shared__ uint8_t actf[EV_ROWS];
   __shared__ uint32_t nact;
   uint8_t* P = a.pst;
   const uint32_t N = a.N;
@@ -826,21 +887,35 @@ __global__ __launch_bounds__(TB) void k_ev_step(MeshArgs a, uint32_t* mesh, cons
   if (threadIdx.x < 64) {
     const uint32_t u = base + threadIdx.x;
     bool on = false;
+    uint32_t fl = 0;
+    uint64_t rb = 0, re = 0;
     if (u < N) {
+      rb = a.row[u];
+      re = a.row[u + 1];
       if (STEP == EV_HB) {
         const bool off = is_off(a.off, u), leaving = off && !is_off(a.off_prev, u);
         const uint32_t mc = P[(size_t)PS_MC * N + u], oc = P[(size_t)PS_OC * N + u];
-        on = leaving || P[(size_t)PS_NBROFF * N + u] || P[(size_t)PS_PROPD * N + u] ||
-             (!off && (mc < a.d_lo || mc > a.d_hi || oc < a.d_out));
+        const bool propd = P[(size_t)PS_PROPD * N + u] != 0;
+        on = leaving || P[(size_t)PS_NBROFF * N + u] || propd || (!off && (mc < a.d_lo || mc > a.d_hi || oc < a.d_out));
+        fl = (propd ? 1u : 0u) | (off ? 2u : 0u);
       } else if (STEP == EV_GRAFT) {
         on = P[(size_t)PS_INBOX * N + u];
       } else {
-        on = P[(size_t)PS_PROPD * N + u] || P[(size_t)PS_PRUNED * N + u] || P[(size_t)PS_DIRTY * N + u] ||
-             (a.off_next && !is_off(a.off, u) && is_off(a.off_next, u)) || (mesh && !mesh_prev);
+        const bool need = P[(size_t)PS_PROPD * N + u] || P[(size_t)PS_PRUNED * N + u];
+        const bool dirty = need || P[(size_t)PS_DIRTY * N + u] || (mesh && !mesh_prev);
+        const bool depart = a.off_next && !is_off(a.off, u) && is_off(a.off_next, u);
+        on = dirty || depart;
+        fl = (need ? 1u : 0u) | (dirty ? 2u : 0u) | (depart ? 4u : 0u);
       }
     }
     const uint64_t bm = __ballot(on);
-    if (on) act[__popcll(bm & ((1ull << threadIdx.x) - 1))] = u;
+    if (on) {
+      const uint32_t q = (uint32_t)__popcll(bm & ((1ull << threadIdx.x) - 1));
+      act[q] = u;
+      actb[q] = rb;
+      actd[q] = (uint32_t)(re - rb);
+      actf[q] = (uint8_t)fl;
+    }
     if (threadIdx.x == 0) nact = (uint32_t)__popcll(bm);
     if (a.dbg) {  // diagnostic counts (GS_DEBUG_EV)
       uint32_t c[4] = {(uint32_t)__popcll(bm), 0, 0, 0};
@@ -864,28 +939,23 @@ __global__ __launch_bounds__(TB) void k_ev_step(MeshArgs a, uint32_t* mesh, cons
   const int lane = threadIdx.x & (G - 1);
   const uint32_t n = nact;
   for (uint32_t i = threadIdx.x / G; i < n; i += TB / G) {  // group-uniform
-    const uint32_t u = act[i];
+    const uint32_t u = act[i], deg = actd[i], fl = actf[i];
+    const uint64_t b = actb[i];
     if (STEP == EV_HB) {
-      if (P[(size_t)PS_PROPD * N + u])  // last epoch's proposals (read by the neighbours until its apply step)
-        for (uint64_t e = a.row[u] + lane; e < a.row[u + 1]; e += G) a.prop[e] = 0;
       if (lane == 0) {
         P[(size_t)PS_PROPD * N + u] = 0;
         P[(size_t)PS_NBROFF * N + u] = 0;
       }
-      if (row_disconnect<G>(a, u) && lane == 0) P[(size_t)PS_DIRTY * N + u] = 1;
-      row_heartbeat<G>(a, u);
+      if (row_hb_ev<G>(a, u, b, deg, (fl & 1u) != 0, (fl & 2u) != 0) && lane == 0) P[(size_t)PS_DIRTY * N + u] = 1;
     } else if (STEP == EV_GRAFT) {
-      const bool acc = row_handle_graft<G>(a, u);
+      const bool acc = row_handle_graft<G>(a, u, b, deg);
       if (lane == 0) {
         P[(size_t)PS_INBOX * N + u] = 0;
         if (acc) P[(size_t)PS_DIRTY * N + u] = 1;
       }
     } else {
-      const bool need = P[(size_t)PS_PROPD * N + u] || P[(size_t)PS_PRUNED * N + u];
-      const bool dirty = need || P[(size_t)PS_DIRTY * N + u] || (mesh && !mesh_prev);
-      // the departures of the next epoch flag their mesh neighbours
-      const bool depart = a.off_next && !is_off(a.off, u) && is_off(a.off_next, u);
-      row_apply_ev<G>(a, u, need, dirty, depart, mesh);
+      // (depart: the departures of the next epoch flag their mesh neighbours)
+      row_apply_ev<G>(a, u, b, deg, (fl & 1u) != 0, (fl & 2u) != 0, (fl & 4u) != 0, mesh);
     }
   }
 }
@@ -1046,6 +1116,7 @@ void ev_epochs(Ctx& c, MeshArgs a, uint64_t h0, uint64_t h1, bool ring) {
   } while (0)
   if (G == 16) k_ev_init<16><<<grid, TB, 0, s>>>(a);
   else k_ev_init<64><<<grid, TB, 0, s>>>(a);
+  if (c.epoch_hook && ring) c.epoch_hook(h0 - 1);
   // the IHAVE lists of the ring epochs [hr, h1] run on the side stream, a
   // chunk as soon as its epochs are stepped (compute-bound list kernels beside
   // the latency-bound epoch steps)
@@ -1078,6 +1149,7 @@ void ev_epochs(Ctx& c, MeshArgs a, uint64_t h0, uint64_t h1, bool ring) {
     GS_EVS(EV_HB, an, nullptr, nullptr);
     GS_EVS(EV_GRAFT, an, nullptr, nullptr);
     GS_EVS(EV_APPLY, a, mesh, prev);
+    if (c.epoch_hook && ring) c.epoch_hook(h);
     if (lists && h >= hr && (h + 1 - chunk0 == CE || h == h1)) {
       const hipEvent_t e = side_event(c, nev++);
       GS_HIP(hipEventRecord(e, s));
@@ -1108,6 +1180,11 @@ void ev_epochs(Ctx& c, MeshArgs a, uint64_t h0, uint64_t h1, bool ring) {
 void run_epochs(Ctx& c, MeshArgs a, uint64_t h0, uint64_t h1, bool ring) { ev_epochs(c, a, h0, h1, ring); }
 
 }  // namespace
+
+hipStream_t side_stream(Ctx& c) {
+  (void)side_event(c, 0);
+  return c.side;
+}
 
 // The inverse IHAVE lists of ring epochs [h0, h1] that were deferred (the push
 // path's receiver-centric gossip reads them), on the context's stream.

@@ -967,7 +967,7 @@ static uint32_t lpull_ring(Ctx& c, const Batch& b, uint64_t delta, uint32_t* lb,
   uint32_t tb = 0;
   while ((1ull << tb) < delta) tb++;
   *lb = bits_for(b.L);
-  if (tb + b.tshift + *lb > 64) return 0;
+  if (tb + b.tshift + *lb > 63) return 0;  // bit 63 of an entry marks a pushed IHAVE (gs_lpull_kernel.h)
   const uint32_t N = c.cfg.peers;
   uint64_t need = (uint64_t)K * N * lpull_stride(b) * 8 + (uint64_t)N * b.L * 2 + (uint64_t)N * (LP_SW + LP_FW) * 4;
   uint64_t have = (uint64_t)c.d_lblk.n * 8 + (uint64_t)c.d_flane.n * 2 + (uint64_t)(c.d_lst.n + c.d_lfin.n) * 4;
@@ -1049,20 +1049,38 @@ static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvF
   la.idw = idw ? 1u : 0u;
   la.rmax = lpull_rmax(b);
   la.ghk = ~0u;
+  la.gsw = ~0u;  // (frozen mesh: every heartbeat's IHAVEs are decided by the receivers)
   if (chn) {  // churn (gs_cpull.h): the tables k_cprep built for this batch
     la.ccol = c.d_ccol.p;
     la.cpos = c.d_cpos.p;
     la.cmm = c.d_cmm.p;
-    la.cge = c.d_cge.p;
+    la.cgt = c.d_cgt.p;
     la.coff = c.d_coff.p;
     la.cq = c.d_cq.p;
     la.pubok = c.d_pubok.p;
+    la.calive = c.d_calive.p;
+    c.d_luni.alloc(2 * (size_t)N);
+    la.luni = c.d_luni.p;
+    c.d_gnz.alloc(N);
+    la.gnz = c.d_gnz.p;
+    c.d_gtag.alloc(N);
+    GS_HIP(hipMemsetAsync(c.d_gtag.p, 0, (size_t)N * 2, s));  // GC_BK counts from 1 per batch
+    la.gtag = c.d_gtag.p;
+    c.d_gpc.alloc(N);
+    GS_HIP(hipMemsetAsync(c.d_gpc.p, 0, (size_t)N * 4, s));
+    la.gpc = c.d_gpc.p;
     la.cr0 = chn->r0;
     la.chb = c.cfg.heartbeat_ns;
     la.cE = chn->cE;
     la.chz = c.cfg.churn_horizon;
     la.ghoff = chn->ghoff;
     la.ghk = c.cfg.churn_horizon - chn->ghoff;
+    // heartbeats from gsw on push their IHAVEs to the targets that may still need
+    // them (GS_GOSSIP_SWITCH, any value is exact). Off by default: at config #3's
+    // shape the pushes cost more in k_gsend than the plane scans they replace
+    // (121 ms per batch without, 129 ms from heartbeat 4 on, 193 ms from 1 on)
+    const char* gsw = getenv("GS_GOSSIP_SWITCH");
+    la.gsw = gsw && *gsw ? (uint32_t)atoi(gsw) : ~0u;
   }
   const char* cap = getenv("GS_LPULL_CAP");  // test knob: small lists force the overflow re-run
   la.ls = ls;
@@ -1188,10 +1206,31 @@ static bool gossip_noop(const Batch& b, const uint64_t* ms, const std::vector<ui
 }
 
 // The churn list pass's per-batch tables (gs_cpull.h) for epochs [E0, E0 + cE)
-// and the batch's publish epochs q0 (lanes), after the epoch chain filled the ring.
-static void chn_prepare(Ctx& c, uint64_t E0, uint32_t cE, const uint64_t* q0, const gs_publish* sched, uint32_t B) {
+// and the batch's publish epochs q0 (lanes). chn_begin before the epoch chain
+// runs; chn_chunks then puts k_cprep of every chunk of 64 epochs whose epochs
+// the chain has enqueued on the side stream (the chain is latency-bound, the
+// target selection compute-bound: they overlap), chn_end the rest, the
+// offline lanes per relative epoch (k_coff) and the join.
+struct ChnPrep {
+  uint64_t E0 = 0;
+  uint32_t cE = 0, cW = 0, next = 0;
+  bool offe = false;
+  size_t nev = 0;
+  CPrepArgs pa{};
+  unsigned grid = 1;
+};
+static hipEvent_t cp_event(Ctx& c, size_t i) {
+  while (c.cp_ev.size() <= i) {
+    hipEvent_t e;
+    GS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c.cp_ev.push_back(e);
+  }
+  return c.cp_ev[i];
+}
+static void chn_begin(Ctx& c, ChnPrep& cp, uint64_t E0, uint32_t cE, const uint64_t* q0, const gs_publish* sched,
+                      uint32_t B) {
   const uint32_t N = c.cfg.peers, H = c.cfg.churn_horizon, R = c.ring_R;
-  const uint32_t cW = (cE + 63) / 64, w64 = (N + 63) / 64;
+  const uint32_t cW = (cE + 63) / 64;
   hipStream_t s = c.stream;
   if (!c.cell_valid) {
     c.d_ccol.alloc((size_t)N * CELL_W);
@@ -1207,30 +1246,73 @@ static void chn_prepare(Ctx& c, uint64_t E0, uint32_t cE, const uint64_t* q0, co
     cq[q] = (uint32_t)(q0[q] - E0);
     ok[q] = !offline_draw(c.cfg.seed, c.cfg.churn_ppm, c.cfg.churn_down, sched[q].publisher, q0[q]);
   }
+  std::vector<uint16_t> alive(64, 0);  // lane j: bit q = lane q*64 + j published
+  for (uint32_t q = 0; q < B; q++)
+    if (ok[q]) alive[q & 63] |= (uint16_t)(1u << (q >> 6));
   c.d_cq.alloc(c.cfg.batch);
   c.d_pubok.alloc(c.cfg.batch);
+  c.d_calive.alloc(LP_FW);
   GS_HIP(hipMemcpyAsync(c.d_cq.p, cq.data(), B * 4, hipMemcpyHostToDevice, s));
   GS_HIP(hipMemcpyAsync(c.d_pubok.p, ok.data(), B, hipMemcpyHostToDevice, s));
+  GS_HIP(hipMemcpyAsync(c.d_calive.p, alive.data(), 128, hipMemcpyHostToDevice, s));
   c.d_offe.alloc((size_t)N * cW);
   c.d_cmm.alloc((size_t)N * cE);
-  c.d_cge.alloc((size_t)N * cE);
+  c.d_cgt.alloc((size_t)N * cE);
   c.d_coff.alloc((size_t)(H + 2) * N * LP_FW);
-  k_offe<<<dim3(w64, cW), 64, 0, s>>>(N, c.d_ring_off.p, w64, R, E0, cE, cW, c.d_offe.p);
-  CPrepArgs pa{};
+  GS_HIP(hipStreamSynchronize(s));  // cq / ok / alive die here
+  cp.E0 = E0;
+  cp.cE = cE;
+  cp.cW = cW;
+  cp.next = 0;
+  cp.offe = false;
+  cp.nev = 0;
+  CPrepArgs& pa = cp.pa;
+  pa = CPrepArgs{};
   pa.ccol = c.d_ccol.p; pa.ring_mm = c.d_ring_mm.p; pa.offe = c.d_offe.p; pa.cq = c.d_cq.p;
-  pa.cmm = c.d_cmm.p; pa.cge = c.d_cge.p; pa.coff = c.d_coff.p;
+  pa.cmm = c.d_cmm.p; pa.cgt = c.cfg.lazy_gossip ? c.d_cgt.p : nullptr; pa.coff = c.d_coff.p;
   pa.E0 = E0; pa.N = N; pa.R = R; pa.cE = cE; pa.cW = cW; pa.B = B; pa.H = H;
-  const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((N + 3) / 4, (uint64_t)std::max(c.num_cus, 1) * 8));
-  k_cprep<<<grid, TB, 0, s>>>(pa);
+  pa.seed = c.cfg.seed; pa.d_lazy = c.cfg.d_lazy; pa.gf_milli = c.cfg.gossip_factor_milli;
+  ensure_cus(c);
+  cp.grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((N + 3) / 4, (uint64_t)std::max(c.num_cus, 1) * 8));
+}
+// The chunks whose epochs are all <= h_done (every remaining one with `all`).
+static void chn_chunks(Ctx& c, ChnPrep& cp, uint64_t h_done, bool all) {
+  uint32_t c1 = cp.next;
+  while (c1 < cp.cW && (all || cp.E0 + std::min<uint64_t>(64ull * (c1 + 1), cp.cE) - 1 <= h_done)) c1++;
+  if (c1 == cp.next) return;
+  const uint32_t N = c.cfg.peers, w64 = (N + 63) / 64;
+  hipStream_t side = side_stream(c);
+  const hipEvent_t e = cp_event(c, cp.nev++);
+  GS_HIP(hipEventRecord(e, c.stream));
+  GS_HIP(hipStreamWaitEvent(side, e, 0));
+  if (!cp.offe) {  // every epoch's offline bits are in the ring once the chain's run started
+    k_offe<<<dim3(w64, cp.cW), 64, 0, side>>>(N, c.d_ring_off.p, w64, c.ring_R, cp.E0, cp.cE, cp.cW, c.d_offe.p);
+    cp.offe = true;
+  }
+  cp.pa.c0 = cp.next;
+  cp.pa.c1 = c1;
+  k_cprep<<<cp.grid, TB, 0, side>>>(cp.pa);
   GS_HIP(hipGetLastError());
-  GS_HIP(hipStreamSynchronize(s));  // cq / ok die here
+  cp.next = c1;
+}
+static void chn_end(Ctx& c, ChnPrep& cp) {
+  chn_chunks(c, cp, 0, true);
+  const hipEvent_t e = cp_event(c, cp.nev++);
+  GS_HIP(hipEventRecord(e, side_stream(c)));
+  GS_HIP(hipStreamWaitEvent(c.stream, e, 0));
+  k_coff<<<cp.grid, TB, 0, c.stream>>>(cp.pa);
+  GS_HIP(hipGetLastError());
+  const uint32_t N = c.cfg.peers, R = c.ring_R, cE = cp.cE;
+  const uint64_t E0 = cp.E0;
+  hipStream_t s = c.stream;
+  GS_HIP(hipStreamSynchronize(s));
   if (getenv("GS_DEBUG_CHN")) {  // diagnostic: the tables against the ELL ring and offline_draw
     std::vector<uint64_t> row(N + 1), cmm((size_t)N * cE), cge((size_t)N * cE);
     std::vector<uint32_t> col(c.nnz), ell((size_t)R * N * MESH_W);
     GS_HIP(hipMemcpy(row.data(), c.d_row.p, (N + 1) * 8, hipMemcpyDeviceToHost));
     GS_HIP(hipMemcpy(col.data(), c.d_col.p, c.nnz * 4, hipMemcpyDeviceToHost));
     GS_HIP(hipMemcpy(cmm.data(), c.d_cmm.p, cmm.size() * 8, hipMemcpyDeviceToHost));
-    GS_HIP(hipMemcpy(cge.data(), c.d_cge.p, cge.size() * 8, hipMemcpyDeviceToHost));
+    GS_HIP(hipMemcpy(cge.data(), c.d_cgt.p, cge.size() * 8, hipMemcpyDeviceToHost));
     GS_HIP(hipMemcpy(ell.data(), c.d_ring_mesh.p, ell.size() * 4, hipMemcpyDeviceToHost));
     uint64_t bad_mm = 0, bad_ge = 0;
     for (uint32_t w = 0; w < N; w++)
@@ -1239,13 +1321,22 @@ static void chn_prepare(Ctx& c, uint64_t E0, uint32_t cE, const uint64_t* q0, co
         const uint32_t* er = &ell[((size_t)(E % R) * N + w) * MESH_W];
         uint64_t mm = 0, ge = 0;
         const bool woff = offline_draw(c.cfg.seed, c.cfg.churn_ppm, c.cfg.churn_down, w, E);
+        std::vector<std::pair<uint64_t, uint32_t>> cand;
         for (uint64_t x = row[w]; x < row[w + 1]; x++) {
           bool in = false;
           for (uint32_t j = 0; j < MESH_W; j++) in |= er[j] != EMPTY && (er[j] & 0xFFFFFFu) == col[x];
           if (in) mm |= 1ull << (x - row[w]);
           else if (!woff && !offline_draw(c.cfg.seed, c.cfg.churn_ppm, c.cfg.churn_down, col[x], E))
-            ge |= 1ull << (x - row[w]);
+            cand.push_back({rng(c.cfg.seed, P_GOSSIP, w, (uint32_t)E, col[x]), (uint32_t)(x - row[w])});
         }
+        std::sort(cand.begin(), cand.end(), [&](const std::pair<uint64_t, uint32_t>& p1, const std::pair<uint64_t, uint32_t>& p2) {
+          return p1.first < p2.first || (p1.first == p2.first && col[row[w] + p1.second] < col[row[w] + p2.second]);
+        });
+        uint32_t r = (uint32_t)(((uint64_t)cand.size() * c.cfg.gossip_factor_milli) / 1000);
+        if (r < c.cfg.d_lazy) r = c.cfg.d_lazy;
+        if (r > cand.size()) r = (uint32_t)cand.size();
+        for (uint32_t q = 0; q < r; q++) ge |= 1ull << cand[q].second;
+        if (!c.cfg.lazy_gossip) ge = 0;
         if (mm != cmm[(size_t)w * cE + e] && bad_mm++ < 5)
           fprintf(stderr, "[chn] mm w %u E %llu dev %llx host %llx\n", w, (unsigned long long)E,
                   (unsigned long long)cmm[(size_t)w * cE + e], (unsigned long long)mm);
@@ -1388,9 +1479,21 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
               (!gossip || hb > b.lat_max + dl);
       }
       c.ring_in_defer = chn;  // the push path's inverse IHAVE lists are not needed
-      churn_ring(c, h_lo, h_hi + c.cfg.churn_horizon);
+      ChnPrep cp;
+      if (chn) {
+        chn_begin(c, cp, h_lo, (uint32_t)(h_hi + c.cfg.churn_horizon - h_lo + 1), q0v.data(), sched + i0, b.B);
+        c.epoch_hook = [&](uint64_t h) { chn_chunks(c, cp, h, false); };
+      }
+      try {
+        churn_ring(c, h_lo, h_hi + c.cfg.churn_horizon);
+      } catch (...) {
+        c.epoch_hook = nullptr;
+        c.ring_in_defer = false;
+        throw;
+      }
+      c.epoch_hook = nullptr;
       c.ring_in_defer = false;
-      if (chn) chn_prepare(c, h_lo, (uint32_t)(h_hi + c.cfg.churn_horizon - h_lo + 1), q0v.data(), sched + i0, b.B);
+      if (chn) chn_end(c, cp);
       c.d_q0.alloc(Bmax);
       c.d_r0.alloc(Bmax);
       GS_HIP(hipMemcpyAsync(c.d_q0.p, q0v.data(), b.B * 8, hipMemcpyHostToDevice, s));

@@ -34,12 +34,15 @@ void usage() {
 // (gs_result_sink.on_lat, GS_WANT_LAT_MS: 2 bytes per (peer, message), the
 // value main.rs:93 prints): the log is streamed through gs_log_write_lat and
 // the latencies folded into a 1 ms histogram, so no [messages][peers] host
-// array is held.
+// array is held. A run with a latency of 65535 ms or more (which the u16
+// stream cannot carry: gs_run fails with GS_ERANGE) is delivered again as
+// completion times (on_block, gs_log_write), the log rewritten from the start.
 struct Stream {
   gs_log* log = nullptr;
   const gs_publish* sched = nullptr;
   gs_status st = GS_OK;
   std::vector<uint64_t> hist_ms;
+  bool self_log = false;
 };
 
 void on_lat(void* user, uint64_t first, uint32_t n, uint32_t peers, const uint16_t* lat) {
@@ -50,6 +53,24 @@ void on_lat(void* user, uint64_t first, uint32_t n, uint32_t peers, const uint16
     if (ms == GS_LAT_NONE) continue;  // undelivered, or the publisher without SELFTRIGGER
     if (ms >= S->hist_ms.size()) S->hist_ms.resize((size_t)ms + 1, 0);
     S->hist_ms[ms]++;
+  }
+}
+
+// The same from completion times (the u64 fallback): the lines main.rs:93
+// prints, (t_complete - tx_time) / 1e6 truncated; the publisher logs only with
+// SELFTRIGGER (cfg.self_log).
+void on_block(void* user, uint64_t first, uint32_t n, uint32_t peers, const uint64_t* tc, const uint8_t*) {
+  Stream* S = (Stream*)user;
+  if (S->log && S->st == GS_OK) S->st = gs_log_write(S->log, S->sched + first, n, tc);
+  for (uint32_t q = 0; q < n; q++) {
+    const gs_publish& p = S->sched[first + q];
+    for (uint32_t u = 0; u < peers; u++) {
+      const uint64_t t = tc[(size_t)q * peers + u];
+      if (t == GS_UNDELIVERED || (u == p.publisher && !S->self_log)) continue;
+      const uint64_t ms = (t - p.t_pub_ns) / 1000000ull;
+      if (ms >= S->hist_ms.size()) S->hist_ms.resize((size_t)ms + 1, 0);
+      S->hist_ms[ms]++;
+    }
   }
 }
 
@@ -173,6 +194,7 @@ int main(int argc, char** argv) {
   }
   Stream strm;
   strm.sched = sched.data();
+  strm.self_log = cfg.self_log != 0;
   if (!latencies.empty() && (st = gs_log_open(&cfg, latencies.c_str(), &strm.log)) != GS_OK)
     return die(ctx, st, "gs_log_open");
   gs_result_sink sink{};
@@ -180,7 +202,25 @@ int main(int argc, char** argv) {
   sink.on_lat = on_lat;
   sink.user = &strm;
   sink.block_msgs = 16;
-  if ((st = gs_run(ctx, sched.data(), n_msgs, &sink)) != GS_OK) return die(ctx, st, "gs_run");
+  st = gs_run(ctx, sched.data(), n_msgs, &sink);
+  if (st == GS_ERANGE && strstr(gs_last_error(ctx), "GS_WANT_LAT_MS")) {
+    // a latency the u16 stream cannot carry: the same run again (it is
+    // deterministic) through the u64 completion times, the log from the start
+    if (strm.log) gs_log_close(strm.log);
+    strm.log = nullptr;
+    strm.st = GS_OK;
+    strm.hist_ms.clear();
+    if (!latencies.empty() && (st = gs_log_open(&cfg, latencies.c_str(), &strm.log)) != GS_OK)
+      return die(ctx, st, "gs_log_open");
+    gs_reset_stats(ctx);  // (also restarts the per-peer traffic counters)
+    gs_result_sink wide{};
+    wide.want = GS_WANT_T_COMPLETE;
+    wide.on_block = on_block;
+    wide.user = &strm;
+    wide.block_msgs = 16;
+    st = gs_run(ctx, sched.data(), n_msgs, &wide);
+  }
+  if (st != GS_OK) return die(ctx, st, "gs_run");
   if (strm.log && ((st = gs_log_close(strm.log)) != GS_OK || (st = strm.st) != GS_OK))
     return die(ctx, st, "gs_log_write");
   gs_stats s;

@@ -318,6 +318,34 @@ def test_cli_injector_args_and_schedule_file(tmp_path):
     assert sorted(open(str(tmp_path / "c")).read().splitlines()) == sorted(open(str(tmp_path / "d")).read().splitlines())
 
 
+def test_cli_latency_past_u16(tmp_path):
+    """A logged latency of 65535 ms or more (70 s heartbeats: a peer offline
+    during the eager spread gets the message by IWANT one heartbeat later) does
+    not fit the CLI's u16 latency stream: gossipsim-node re-delivers the run as
+    completion times and writes the whole log, equal to the oracle's."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(gossipsim.LIB_PATH), "gossipsim-node")
+    hb = 70_000_000_000
+    t0 = (946684800 + 500) * 1_000_000_000
+    phase = t0 - 10 * hb + 20_000_000_000
+    env = dict(os.environ, PEERS="300", CONNECTTO="10", FRAGMENTS="1", GS_SEED="5", GS_CHURN_PPM="150000",
+               GS_CHURN_DOWN="1", GS_CHURN_HORIZON="4", GOSSIPSUB_HEARTBEAT_MS=str(hb // 1_000_000),
+               GS_HB_PHASE_NS=str(phase), GS_LAZY_GOSSIP="1")
+    subprocess.run([exe, "-st", "5", "-bl", "50", "-bh", "150", "-ll", "40", "-lh", "130", "-m", "6", "-s", "15000",
+                    "--latencies", str(tmp_path / "a")], env=env, check=True, timeout=120)
+    p = oracle.params(peers=300, seed=5, churn_ppm=150000, churn_down=1, churn_horizon=4, heartbeat_ns=hb,
+                      hb_phase_ns=phase, lazy_gossip=1)
+    sched = gossipsim.schedule_runsh(6, 300, 6, 1, t0 + gossipsim.HTTP_TRANSIT_NS, 1_000_000_000, 15000)
+    cols = (np.array([r.t_pub_ns for r in sched], dtype=np.uint64), np.array([r.publisher for r in sched]),
+            np.array([r.msg_size for r in sched]))
+    ref = oracle.simulate(p, 5, (50, 150, 40, 130), sched=cols)
+    sim = gossipsim.Simulator(**_knobs(p))
+    sim.write_latency_log(str(tmp_path / "b"), {"schedule": sched, "t_complete": ref["t_complete"]})
+    a = open(str(tmp_path / "a")).read().splitlines()
+    assert sorted(a) == sorted(open(str(tmp_path / "b")).read().splitlines())
+    assert max(int(x.rsplit(" ", 1)[1]) for x in a) >= 65535
+
+
 def test_fragment_collision_defect_d8():
     p = oracle.params(peers=100, fragments=4)
     sim, res = compare(p, 1, (50, 50, 50, 50), _sched(2, 100, size=40))
@@ -464,16 +492,19 @@ def test_churn_gossip_sender_receiver_switch(monkeypatch, switch):
     assert 0 < st["deliveries"] < 32 * 799 and st["gossip_iwant"] > 0
 
 
-@pytest.mark.parametrize("gossip,hb_ms,phase_ms,frags", [(0, 1000, 370, 1), (1, 1000, 370, 1), (1, 400, 150, 1),
-                                                           (0, 400, 330, 1), (1, 300, 20, 1), (1, 400, 150, 2)])
-def test_churn_list_pass(monkeypatch, gossip, hb_ms, phase_ms, frags):
+@pytest.mark.parametrize("gossip,hb_ms,phase_ms,frags,switch", [(0, 1000, 370, 1, 3), (1, 1000, 370, 1, 3), (1, 1000, 370, 1, 0), (1, 1000, 370, 1, 1000), (1, 400, 150, 1, 3), (1, 400, 150, 1, 1),
+                                                                  (0, 400, 330, 1, 3), (1, 300, 20, 1, 3),
+                                                                  (1, 400, 150, 2, 3)])
+def test_churn_list_pass(monkeypatch, gossip, hb_ms, phase_ms, frags, switch):
     """Churn on the owner-computes list pass (gs_cpull.h, k_lpull<.., CHN>):
     per-lane epoch meshes as CSR masks, 16-B records, forwards that cross an
     epoch boundary into a receiver's offline epoch, IWANT answers lost the same
     way, the lifetime cut; heartbeats short enough that several boundaries fall
-    inside a dissemination. Bit-exact against the oracle, IWANTs included; the
-    single-fragment batches must take the list pass (GS_REQUIRE_LPULL), the
-    fragmented one the push path."""
+    inside a dissemination; heartbeats from GS_GOSSIP_SWITCH on may push their
+    IHAVEs into the targets' lists (1000: none). Bit-exact against the
+    oracle, IWANTs included; the single-fragment batches must take the list
+    pass (GS_REQUIRE_LPULL), the fragmented one the push path."""
+    monkeypatch.setenv("GS_GOSSIP_SWITCH", str(switch))
     if frags == 1:
         monkeypatch.setenv("GS_REQUIRE_LPULL", "1")
     hb = hb_ms * 1_000_000
