@@ -56,7 +56,7 @@ def parse():
     ap.add_argument("--max-heartbeats", type=int, default=400)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU oracle sample budget (0=off)")
     ap.add_argument("--cpu-gossip", type=int, default=0, help="also time the oracle with lazy gossip on (slow)")
-    ap.add_argument("--output-steps", type=int, default=2,
+    ap.add_argument("--output-steps", type=int, default=4,
                     help="with_output: steps timed with the results streamed to host memory (0=off)")
     ap.add_argument("--configs", type=int, default=1, help="also time BASELINE configs #1-#3 (1 GPU runs)")
     ap.add_argument("--mode", choices=("msg", "peer"), default="msg",
@@ -298,21 +298,23 @@ def with_output(args, sim, rank, world):
     def on_lat(first, lat):
         blocks[0] += 1
 
-    sim.run(gossipsim.shard_messages(0, rank, world, args.batch, args.peers, args.msg_size), on_lat=on_lat,
-            block_msgs=64)  # warm-up: pinned staging buffers, transposes
+    def steps(first, n):  # n batches' messages as one run (the batches' results stream beside the next passes)
+        sh = [gossipsim.shard_messages(first + i, rank, world, args.batch, args.peers, args.msg_size) for i in range(n)]
+        return tuple(np.concatenate([x[k] for x in sh]) for k in range(3))
+
+    sim.run(steps(0, 2), on_lat=on_lat, block_msgs=64)  # warm-up: both pinned staging halves, transposes
     sim.reset_stats()
     blocks[0] = 0
     t0 = time.perf_counter()
-    for i in range(args.output_steps):
-        sim.run(gossipsim.shard_messages(args.warmup + i, rank, world, args.batch, args.peers, args.msg_size),
-                on_lat=on_lat, block_msgs=64)
+    sim.run(steps(args.warmup, args.output_steps), on_lat=on_lat, block_msgs=64)
     dt = time.perf_counter() - t0
     st = sim.stats()
     return {"value": st["deliveries"] / dt, "unit": "deliveries/s", "steps": args.output_steps,
             "ms_per_step": dt * 1e3 / args.output_steps, "blocks": blocks[0],
             "bytes_to_host_per_step": args.batch * args.peers * 2,
             "sink": "on_lat: the logged latency (u16 ms, main.rs:93's value) of every (peer, message), 64-message "
-                    "blocks; completion from the final logs, device transpose, D2H through two pinned halves"}
+                    "blocks; the steps as one gs_run of %d batches: completion from the final logs, device transpose, "
+                    "each batch's D2H on a copy stream beside the next batch's passes" % args.output_steps}
 
 
 def make_sim(args, peers, S, links, local):
@@ -438,8 +440,9 @@ def config_rates(args, local):
                     "alg_bytes_per_launch": tst["relax_bytes_alg"] / tst["relax_launches"],
                     "avg_launch_us": tst["relax_ms"] * 1e3 / tst["relax_launches"],
                     "launches": int(tst["relax_launches"]), "pass_ms": tst["relax_ms"]}
-        push = c["knobs"].get("churn_ppm") or (st["gossip_fallback_batches"] and not st["gossip_list_batches"]) or \
-            (st["list_pull_batches"] == 0 and sim.cfg.c.idontwant)
+        push = st["list_pull_batches"] < st["batches"] and (
+            (st["gossip_fallback_batches"] and not st["gossip_list_batches"]) or
+            (st["list_pull_batches"] == 0 and (sim.cfg.c.idontwant or c["knobs"].get("churn_ppm"))))
         out[name] = {"value": st["deliveries"] / dt, "unit": "deliveries/s", "msgs": c["msgs"], "best_of": c.get("reps", 1),
                      "ms": dt * 1e3, "deliveries": int(st["deliveries"]), "batches": int(st["batches"]),
                      "gossip_iwant": int(st["gossip_iwant"]), "gossip_noop_msgs": int(st["gossip_noop_msgs"]),
@@ -447,6 +450,8 @@ def config_rates(args, local):
                      "gossip_fallback_batches": int(st["gossip_fallback_batches"]),
                      "list_pull_batches": int(st["list_pull_batches"]),
                      "kernel_path": "push (k_scan+k_frontier+k_gossip)" if push else
+                     "pull (k_lpull churn: per-epoch meshes, IHAVE/IWANT inside the passes)"
+                     if c["knobs"].get("churn_ppm") and st["list_pull_batches"] else
                      "pull (k_lpull, IHAVE/IWANT inside the passes)" if st["gossip_list_batches"] else
                      "pull (k_lpull)" if st["list_pull_batches"] else "pull (k_pull)",
                      "roofline": roof}
@@ -459,8 +464,11 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:  # no torchrun: be the launcher
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world, rank, local, torch, dist = dist_setup()
-    if args.gpus != world:
-        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE is %d" % (args.gpus, world))
+    if args.gpus != world:  # under torchrun the launcher's WORLD_SIZE is the GPU count
+        if rank == 0:
+            print("bench.py: --gpus %d but WORLD_SIZE is %d: running on %d GPUs" % (args.gpus, world, world),
+                  file=sys.stderr)
+        args.gpus = world
     S, bl, bh, ll, lh = [int(x) for x in args.links.split(",")]
     links = (bl, bh, ll, lh)
     sim, epochs, t_setup = make_sim(args, args.peers, S, links, local)

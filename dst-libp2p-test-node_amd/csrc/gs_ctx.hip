@@ -18,6 +18,14 @@ Ctx::~Ctx() {
   for (auto e : blk_ev)
     if (e) (void)hipEventDestroy(e);
   if (side) (void)hipStreamDestroy(side);
+  for (int k = 0; k < 2; k++) {
+    if (lat_src[k]) (void)hipEventDestroy(lat_src[k]);
+    if (lat_done[k]) (void)hipEventDestroy(lat_done[k]);
+    if (h_lat[k]) (void)hipHostFree(h_lat[k]);
+  }
+  for (auto e : cp_ev) (void)hipEventDestroy(e);
+  if (h_laterr) (void)hipHostFree(h_laterr);
+  if (copy) (void)hipStreamDestroy(copy);
   if (h_pinned) (void)hipHostFree(h_pinned);
   if (h_block) (void)hipHostFree(h_block);
   if (stream) (void)hipStreamDestroy(stream);
@@ -159,6 +167,7 @@ extern "C" gs_status gs_build_topology(gs_ctx* ctx) {
   ctx->csrpos_valid = false;
   ctx->cell_valid = false;
   ctx->mesh_built = false;
+  ctx->glp_prefer = false;
   GS_API_END(ctx)
 }
 
@@ -248,6 +257,7 @@ extern "C" gs_status gs_reset_stats(gs_ctx* ctx) {
     GS_HIP(hipMemsetAsync(ctx->d_traffic.p, 0, (size_t)ctx->cfg.peers * GS_TRAFFIC_COLS * 8, ctx->stream));
   GS_HIP(hipStreamSynchronize(ctx->stream));
   memset(&ctx->stats, 0, sizeof(ctx->stats));
+  ctx->glp_prefer = false;  // the next gossip batch tries the eager pass + no-op proof first
   GS_API_END(ctx)
 }
 

@@ -53,6 +53,7 @@ struct DevBuf {
 
 // Counters written by kernels: index constants into Ctx::d_counters.
 constexpr uint32_t H_PINNED_WORDS = 32;
+constexpr uint32_t GLP_QUIET = 8;  // see run_messages run_glp
 
 enum : uint32_t {
   C_FD = 0, C_R = 1, C_DELIV = 2, C_LAT_SUM = 3, C_LAT_MAX = 4, C_BUCKETS = 5,
@@ -167,6 +168,24 @@ struct Ctx {
   DevBuf<uint16_t> d_lat;    // [N * B] peer-major logged latency in ms (GS_WANT_LAT_MS)
   DevBuf<uint16_t> d_lat_t;  // [B * N] message-major staging of it
   hipEvent_t blk_ev[2] = {nullptr, nullptr};  // double-buffered streaming: D2H of block k done
+  // latency-only sinks inside gs_run (gs_relax.hip deliver_lat_async): a finished
+  // batch's u16 latencies leave on the copy stream into a whole-batch pinned
+  // buffer while the next batch's passes run; its callbacks run at the next
+  // batch's delivery or at the end of the run (message order kept)
+  bool lat_async = false;
+  hipStream_t copy = nullptr;
+  DevBuf<uint16_t> d_lat_t2;                  // the other parity's message-major staging
+  uint16_t* h_lat[2] = {nullptr, nullptr};    // pinned [B][un] per parity
+  size_t h_lat_bytes[2] = {0, 0};
+  uint64_t* h_laterr = nullptr;               // pinned: the error word after each parity's batch
+  hipEvent_t lat_src[2] = {nullptr, nullptr}, lat_done[2] = {nullptr, nullptr};
+  struct LatPending {
+    bool on = false;
+    uint32_t par = 0, B = 0, un = 0, bm = 64;
+    uint64_t row0 = 0;
+    const gs_result_sink* sink = nullptr;
+  } lat_pend;
+  uint32_t lat_par = 0;
   DevBuf<uint32_t> d_tables; // lat[S*S] | ser_up[S] | ser_dn[S] (u32 ns)
   DevBuf<uint64_t> d_ctrl;   // [4] triple-buffered next-min keys + spare
   // owner-computes pull path (gs_pull_kernel.h)
@@ -227,6 +246,7 @@ struct Ctx {
   DevBuf<uint32_t> d_rowdone;  // [(N + 31) / 32]
   DevBuf<uint64_t> d_gctl;     // [GC_WORDS]
   bool glp_prefer = false;     // the last eager no-op proof failed: run gossip batches on the list pass first
+  uint32_t glp_quiet = 0;      // list-pass gossip batches in a row without an IWANT (GLP_QUIET clears glp_prefer)
   // churn on the list pass (gs_cpull.h, k_lpull<.., CHN>): the CSR rows as 64-wide ELL rows (once
   // per topology), per batch the per-epoch mesh / IHAVE-eligible masks of every row over the
   // batch's epochs, each peer's offline epochs, and the offline lanes per relative epoch

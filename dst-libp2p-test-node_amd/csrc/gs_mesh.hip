@@ -1262,6 +1262,7 @@ uint32_t run_mesh(Ctx& c, uint32_t max_hb) {
   if (c.nnz) k_clear_mesh<<<blocks(c.nnz), TB, 0, s>>>(c.nnz, c.d_flags.p, c.d_until.p);
   GS_HIP(hipMemsetAsync(c.d_counters.p + C_ERR, 0, 8, s));
   c.ring_in_tag.assign(c.ring_in_tag.size(), ~0ull);  // a new mesh: the churn ring restarts
+  c.glp_prefer = false;  // and gossip batches try the eager pass + no-op proof first again
   sub_epoch(c, a);
   uint32_t epoch = 1, last = 0;
   uint64_t* h = c.h_pinned;

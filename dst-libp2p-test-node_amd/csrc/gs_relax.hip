@@ -717,6 +717,67 @@ void deliver_rows(Ctx& c, uint32_t B, uint32_t un, const gs_result_sink* sink, u
   hand_over(prev, pq0, pn);
 }
 
+// The pending latency-only delivery of the previous batch (deliver_lat_async):
+// wait for its copy, check the error word it carried (a latency the u16 stream
+// cannot hold fails the run before any of that batch's lines are handed out),
+// then its callbacks block by block.
+static void lat_flush(Ctx& c) {
+  Ctx::LatPending& p = c.lat_pend;
+  if (!p.on) return;
+  p.on = false;
+  GS_HIP(hipEventSynchronize(c.lat_done[p.par]));
+  if (c.h_laterr[p.par] & ERR_LAT16)
+    c.fail(GS_ERANGE, "a logged latency of 65535 ms or more does not fit the u16 stream (GS_WANT_LAT_MS)");
+  for (uint32_t q0 = 0; q0 < p.B; q0 += p.bm) {
+    const uint32_t n = std::min(p.bm, p.B - q0);
+    p.sink->on_lat(p.sink->user, p.row0 + q0, n, p.un, c.h_lat[p.par] + (size_t)q0 * p.un);
+  }
+}
+
+// A latency-only sink inside gs_run (on_lat, no rows, no summary): the batch's
+// transposed u16 latencies leave on the copy stream into a whole-batch pinned
+// buffer of this batch's parity while the next batch's passes run; the
+// previous batch's callbacks run now (its copy had this batch's passes to
+// finish), this batch's at the next delivery or at the end of the run.
+static void deliver_lat_async(Ctx& c, const Batch& b, uint32_t un, const gs_result_sink* sink, uint64_t sink_row0) {
+  hipStream_t s = c.stream;
+  const uint32_t par = c.lat_par;
+  c.lat_par ^= 1u;
+  DevBuf<uint16_t>& lt = par ? c.d_lat_t2 : c.d_lat_t;
+  lt.alloc((size_t)un * c.cfg.batch);
+  dim3 tg((un + 63) / 64, (b.B + 63) / 64);
+  k_transpose16<<<tg, TB, 0, s>>>(c.d_lat.p, lt.p, un, b.B);
+  GS_HIP(hipGetLastError());
+  const size_t bytes = (size_t)b.B * un * 2;
+  if (c.h_lat_bytes[par] < bytes) {
+    if (c.h_lat[par]) GS_HIP(hipHostFree(c.h_lat[par]));
+    c.h_lat[par] = nullptr;
+    c.h_lat_bytes[par] = 0;
+    GS_HIP(hipHostMalloc((void**)&c.h_lat[par], bytes, hipHostMallocDefault));
+    c.h_lat_bytes[par] = bytes;
+  }
+  if (!c.h_laterr) GS_HIP(hipHostMalloc((void**)&c.h_laterr, 2 * 8, hipHostMallocDefault));
+  if (!c.copy) GS_HIP(hipStreamCreateWithFlags(&c.copy, hipStreamNonBlocking));
+  for (int k = 0; k < 2; k++) {
+    if (!c.lat_src[k]) GS_HIP(hipEventCreateWithFlags(&c.lat_src[k], hipEventDisableTiming));
+    if (!c.lat_done[k]) GS_HIP(hipEventCreateWithFlags(&c.lat_done[k], hipEventDisableTiming));
+  }
+  GS_HIP(hipEventRecord(c.lat_src[par], s));
+  GS_HIP(hipStreamWaitEvent(c.copy, c.lat_src[par], 0));
+  GS_HIP(hipMemcpyAsync(c.h_lat[par], lt.p, bytes, hipMemcpyDeviceToHost, c.copy));
+  GS_HIP(hipMemcpyAsync(c.h_laterr + par, c.d_counters.p + C_ERR, 8, hipMemcpyDeviceToHost, c.copy));
+  GS_HIP(hipEventRecord(c.lat_done[par], c.copy));
+  lat_flush(c);  // the previous batch, in message order
+  Ctx::LatPending& p = c.lat_pend;
+  p.on = true;
+  p.par = par;
+  p.B = b.B;
+  p.un = un;
+  p.bm = std::max<uint32_t>(1, std::min<uint32_t>(sink->block_msgs ? sink->block_msgs : 64, b.B));
+  p.row0 = sink_row0;
+  p.sink = sink;
+}
+
 // Results of a completed batch (peer-major d_tc / d_hops / d_lat of peers
 // [u0, u0 + un)) into the sink: transposed to message-major, copied out,
 // summaries.
@@ -725,6 +786,11 @@ static void deliver(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, const gs_r
   if (!sink) return;
   hipStream_t s = c.stream;
   const SinkWants w = sink_wants(sink);
+  if (c.lat_async && w.lat && !w.rows() && !w.summary && sink->on_lat) {
+    deliver_lat_async(c, b, un, sink, sink_row0);
+    return;
+  }
+  lat_flush(c);  // (a pending batch is delivered before this one)
   if (w.rows()) {
     c.d_tc_t.alloc((size_t)un * c.cfg.batch);
     c.d_hops_t.alloc((size_t)un * c.cfg.batch);
@@ -1353,6 +1419,15 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
   const uint32_t N = c.cfg.peers;
   const uint32_t Bmax = c.cfg.batch;
   hipStream_t s = c.stream;
+  if (c.lat_pend.on) {  // left by a run that failed: its lines are not handed out
+    GS_HIP(hipStreamSynchronize(c.copy));
+    c.lat_pend.on = false;
+  }
+  c.lat_async = true;
+  struct AsyncOff {
+    Ctx& c;
+    ~AsyncOff() { c.lat_async = false; }
+  } async_off{c};
   GS_HIP(hipMemsetAsync(c.d_counters.p + C_ERR, 0, 8, s));
   check_schedule(c, sched, n_msgs);
   uint32_t Fmax = 1;
@@ -1692,8 +1767,15 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       const GosRun gr{rel0[0], c.cfg.heartbeat_ns};
       const SinkWants sw = sink_wants(sink);
       const bool dense = sw.rows() || sw.summary || c.traffic || getenv("GS_LPULL_DENSE");
+      const uint64_t iw0 = read_counter(c, C_GOSSIP);
       if (!run_lpull_batch(c, bg, K, lb, ev, n_ev, dev_cus, dense, false, &gr)) return false;
       c.stats.gossip_list_batches++;
+      // GLP_QUIET batches in a row whose gossip sent no IWANT: the next one tries the
+      // eager pass and its no-op proof first again (glp_prefer was never
+      // cleared). Not after one: batches alternating with and without IWANTs (a
+      // heartbeat late in the dissemination) would pay a failed proof every other batch.
+      if (read_counter(c, C_GOSSIP) != iw0) c.glp_quiet = 0;
+      else if (++c.glp_quiet >= GLP_QUIET) c.glp_prefer = false;
       if (c.traffic) launch_traffic(c, b);
       launch_complete(c, b, 0, N, sink, i0);
       return true;
@@ -1772,6 +1854,7 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
           c.stats.gossip_fallback_batches++;
           if (glp && !glp_tried) {  // re-run with the gossip inside the passes; the context's
             c.glp_prefer = true;      // later batches go there directly (no eager run first)
+            c.glp_quiet = 0;
             done = run_glp();
           }
         }
@@ -1789,6 +1872,7 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     c.stats.batches++;
     i0 = i1;
   }
+  lat_flush(c);  // the last batch's latencies
   if (c.timing) GS_HIP(hipEventRecord(ev(1), s));
   collect_stats(c);
   if (c.timing) {
