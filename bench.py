@@ -408,6 +408,7 @@ CONFIGS = {
 
 def config_rates(args, local):
     out = {}
+    mark = os.environ.get("GS_CFG_MARK") == "1"
     for name, c in CONFIGS.items():
         sim = gossipsim.Simulator(peers=c["peers"], batch=c["batch"], fragments=c["fragments"], seed=args.seed,
                                   device=local, **c["knobs"])
@@ -421,9 +422,11 @@ def config_rates(args, local):
         for _ in range(c.get("reps", 1)):
             sim.reset_stats()
             sched = gossipsim.shard_messages(1, 0, 1, c["msgs"], c["peers"], args.msg_size)  # after the warm-up's
-            t0 = time.perf_counter()
+            t0, m0 = time.perf_counter(), time.monotonic_ns()
             sim.run(sched, collect=False)
             d = time.perf_counter() - t0
+            if mark and dt is None:  # the first timed run's clock span (scripts/config_traffic.py)
+                print(json.dumps({"mark": name, "t0_ns": m0, "t1_ns": time.monotonic_ns()}), file=sys.stderr)
             dt = d if dt is None else min(dt, d)
         st = sim.stats()
         # one more repeat with HIP events around every window pass / bucket: the
@@ -445,6 +448,7 @@ def config_rates(args, local):
             (st["list_pull_batches"] == 0 and (sim.cfg.c.idontwant or c["knobs"].get("churn_ppm"))))
         out[name] = {"value": st["deliveries"] / dt, "unit": "deliveries/s", "msgs": c["msgs"], "best_of": c.get("reps", 1),
                      "ms": dt * 1e3, "deliveries": int(st["deliveries"]), "batches": int(st["batches"]),
+                     "alg_bytes_per_batch": st["bytes_alg"] / max(1, st["batches"]),
                      "gossip_iwant": int(st["gossip_iwant"]), "gossip_noop_msgs": int(st["gossip_noop_msgs"]),
                      "gossip_list_batches": int(st["gossip_list_batches"]),
                      "gossip_fallback_batches": int(st["gossip_fallback_batches"]),

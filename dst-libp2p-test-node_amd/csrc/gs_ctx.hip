@@ -28,6 +28,7 @@ Ctx::~Ctx() {
   if (copy) (void)hipStreamDestroy(copy);
   if (h_pinned) (void)hipHostFree(h_pinned);
   if (h_block) (void)hipHostFree(h_block);
+  if (h_slms) (void)hipHostFree(h_slms);
   if (stream) (void)hipStreamDestroy(stream);
 }
 

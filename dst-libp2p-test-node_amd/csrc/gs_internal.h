@@ -193,6 +193,17 @@ struct Ctx {
   DevBuf<uint64_t> d_lrec;   // [2][N][L] per-row arrival records (gs_pull_kernel.h)
   DevBuf<uint32_t> d_lcnt;   // [2][N]
   DevBuf<uint8_t> d_rpos;    // [N][MESH_W] index of w in mesh(mesh[w][j])
+  // batch slices (gs_relax.hip run_slices): S copies of the graph's mesh rows, reverse
+  // positions and stages; the slices' publishers as slice rows and as peers
+  DevBuf<uint32_t> d_smesh;  // [S * N][MESH_W]
+  DevBuf<uint8_t> d_srpos;
+  DevBuf<uint8_t> d_sstage;  // [S * N]
+  DevBuf<uint32_t> d_spub;   // [S][B]
+  DevBuf<uint32_t> d_lpub;
+  DevBuf<uint64_t> d_cnt_save2;  // [C_COUNT] counters around a slice group's repeated completions
+  DevBuf<uint64_t> d_stpub;  // [S][B] the slices' publish times
+  uint64_t* h_slms = nullptr;  // pinned [S][B][MS_COLS]: every slice's reductions for the gossip no-op proof
+  size_t h_slms_bytes = 0;
   bool rpos_valid = false;
   bool keys_log = false;       // keys hold the list pull path's final logs (not dense rows): k_lcomplete
   uint32_t mesh_dmax = 0;      // widest frozen-mesh row (list pull ring bound); 0 = not known

@@ -61,6 +61,10 @@
 constexpr uint32_t LP_KMAX = 12;  // ring of destination-window lists
 constexpr uint32_t LP_SW = 16;    // u32 words of per-row state: list lengths [0..11] (slot = window % K), log length
 constexpr uint32_t LP_LOG = 15;   // state word holding the final-log length
+// state word set (k_lpubnb) on every batch publisher and its mesh (churn: CSR)
+// neighbours: only those rows' emit step needs the publishers (LPullArgs::pubw)
+constexpr uint32_t LP_PUB = 12;
+static_assert(LP_KMAX <= LP_PUB && LP_PUB < LP_LOG, "row state words");
 // arrival record (u64): start - window_lo (32) | hops (6) | inclusion mask (16) | lane (10)
 constexpr uint32_t LP_IM_SHIFT = 10, LP_HOP_SHIFT = 26, LP_LANE_MASK = (1u << LP_IM_SHIFT) - 1;
 static_assert(MESH_W <= LP_HOP_SHIFT - LP_IM_SHIFT && PULL_LMAX <= (1u << LP_IM_SHIFT) && HOP_BITS == 32 - LP_HOP_SHIFT,
@@ -94,6 +98,11 @@ struct LPullArgs {
   // receive only this part's records, and the previous pass's records of EVERY peer arrive packed
   // (rpk) with per-peer offsets (roff) and counts (rcg), exchanged by the host (gs_comm.hip)
   uint32_t u0;
+  // batch slices (gs_relax.hip run_slices): rows [j * rN, (j + 1) * rN) are slice j, a
+  // whole batch of its own over a copy of the graph (ids + j * rN); pub holds the
+  // slices' publishers [S][B] as such row ids. 0: one batch
+  uint32_t rN;
+  uint32_t pubw;  // the LP_PUB state words are set (k_lpubnb): a row without it skips the publisher load
   const uint64_t* rpk;
   const uint64_t* roff;
   const uint32_t* rcg;
@@ -1042,6 +1051,8 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     uint64_t uni = 0;  // churn: the receivers of any of the row's records
     if (cnt) {
       const uint32_t deg = (uint32_t)__popcll(__ballot(ej != EMPTY));  // rows are packed
+      const uint32_t psl = a.rN ? (w / a.rN) * a.B : 0u;  // batch slices: this row's publishers
+      const bool needp = !a.pubw || __builtin_amdgcn_readlane(sv, LP_PUB) != 0;
       const uint32_t serw = sup[sw];
       constexpr uint32_t GPW = 64 / FP;
       for (uint32_t g0 = 0; g0 < cnt; g0 += GPW) {
@@ -1050,7 +1061,10 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
         const uint32_t grp = gv ? LST[gi] : 0;
         const uint32_t i = grp * FP + (lane & (FP - 1));
         const uint64_t x = gv ? CW[i] : INF64;  // final lanes were set to INF in step 3
-        const uint32_t pm = gv ? a.pub[grp] : EMPTY;
+        // the message's publisher (excluded from the receivers); a row that is
+        // no publisher nor a publisher's neighbour needs none (no load)
+        uint32_t pm = EMPTY;
+        if (needp) pm = gv ? a.pub[psl + grp] : EMPTY;
         // FP == 1: LST holds only lanes final in window c; a fragment group's
         // other lanes are re-checked
         const bool act = gv && (FP == 1 || (x != INF64 && ((uint32_t)(x >> 32) - hlo) < hspan)) && a.u0 + w != pm;
@@ -1531,6 +1545,24 @@ __global__ __launch_bounds__(TB) void k_lseed(LPullArgs a, const uint64_t* __res
     a.blk[((size_t)slot * a.N + w) * a.ls + pos] = (toff << (a.tshift + a.lb)) | ((key & lowmask) << a.lb) | l;
   }
   if (err) atomicOr((unsigned*)&a.counters[C_ERR], err);
+}
+
+// LP_PUB of every publisher of the batch and of its mesh neighbours (churn:
+// its CSR neighbours, the emit step's receivers): one thread per (message,
+// entry); entry `width` is the publisher itself. nmsg: the pub entries (slices: S x B).
+__global__ __launch_bounds__(TB) void k_lpubnb(LPullArgs a, uint32_t nmsg) {
+  const uint32_t width = a.ccol ? CELL_W : MESH_W;
+  const uint64_t g = (uint64_t)blockIdx.x * TB + threadIdx.x;
+  if (g >= (uint64_t)nmsg * (width + 1)) return;
+  const uint32_t m = (uint32_t)(g / (width + 1)), k = (uint32_t)(g % (width + 1));
+  const uint32_t p = a.pub[m];
+  uint32_t x = p;
+  if (k < width) {
+    const uint32_t e = a.ccol ? a.ccol[(size_t)p * CELL_W + k] : a.mesh[(size_t)p * MESH_W + k];
+    if (e == EMPTY) return;
+    x = e & 0xFFFFFFu;
+  }
+  a.st[(size_t)x * LP_SW + LP_PUB] = 1u;
 }
 
 // The publishers' own lanes: final at time 0 (k_seed's key p), logged first.

@@ -431,6 +431,23 @@ __global__ __launch_bounds__(TB) void k_rpos(const uint32_t* __restrict__ mesh, 
   rpos[g] = r;
 }
 
+// Batch slices (gs_relax.hip run_slices): S copies of the mesh rows, reverse
+// positions and stages, copy j's peer ids shifted by j * N. One thread per
+// (copy, row, entry).
+__global__ __launch_bounds__(TB) void k_srep(uint32_t N, uint32_t S, const uint32_t* __restrict__ mesh,
+                                             const uint8_t* __restrict__ rpos, const uint8_t* __restrict__ stage,
+                                             uint32_t* __restrict__ smesh, uint8_t* __restrict__ srpos,
+                                             uint8_t* __restrict__ sstage) {
+  const uint64_t g = (uint64_t)blockIdx.x * TB + threadIdx.x, per = (uint64_t)N * MESH_W;
+  if (g >= per * S) return;
+  const uint32_t j = (uint32_t)(g / per);
+  const uint64_t i = g - (uint64_t)j * per;
+  const uint32_t e = mesh[i];
+  smesh[g] = e == EMPTY ? EMPTY : e + j * N;  // (stage bits above the id: no carry, S * N < 2^21)
+  srpos[g] = rpos[i];
+  if (i % MESH_W == 0) sstage[(size_t)j * N + i / MESH_W] = stage[i / MESH_W];
+}
+
 // Window grain of the pull path: one unit of the key's high 32-bit word.
 inline uint64_t pull_grain(uint32_t tshift) { return tshift >= 32 ? 1ull : 1ull << (32 - tshift); }
 

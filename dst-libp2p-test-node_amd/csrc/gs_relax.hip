@@ -53,6 +53,7 @@ struct SeedArgs {
   uint64_t tmax;
   uint32_t L, FP, Fe, S, sb, tshift, flood;
   uint32_t u0, un;  // keys held for peers [u0, u0 + un) (the whole graph unless partitioned)
+  uint32_t soff;    // batch slice (run_slices): its rows are soff + peer (list seeds and key sources)
   // churn: see RelaxArgs
   const uint32_t* ring_mesh;
   const uint64_t* ring_off;
@@ -109,13 +110,13 @@ __global__ __launch_bounds__(TB) void k_seed(SeedArgs a) {
     const uint64_t sd = a.tables[S * S + S + sw];
     const uint64_t arr = ((uint64_t)f * deg + j + 1) * ser + a.tables[sp * S + sw] + (sd > ser ? sd - ser : 0);
     if (arr > a.tmax) err |= ERR_TIME;
-    const uint64_t nk = (arr << a.tshift) | (1ull << a.sb) | p;
+    const uint64_t nk = (arr << a.tshift) | (1ull << a.sb) | (p + a.soff);
     if (w - a.u0 >= a.un) continue;
     if (a.churn && ev_lost(a, m, arr, w)) continue;
     if (a.skey) {  // one send per (target, fragment): no duplicates to reduce
       const uint32_t q = atomicAdd(a.scnt, 1u);
       a.skey[q] = nk;
-      a.slane[q] = ((w - a.u0) << 11) | (m * a.FP + f);
+      a.slane[q] = ((w - a.u0 + a.soff) << 11) | (m * a.FP + f);
       nmin = nk < nmin ? nk : nmin;
       continue;
     }
@@ -382,7 +383,8 @@ static void check_schedule(Ctx& c, const gs_publish* sched, uint64_t n_msgs) {
 
 // Upload pub/tpub/link tables for messages [i0, i1) (equal msg_size) and
 // compute the bucket width Delta = min latency + min serialisation.
-static Batch setup_batch(Ctx& c, const gs_publish* sched, uint64_t i0, uint64_t i1) {
+// upload = false: only the host fields (a batch slice after the first: same shape and tables)
+static Batch setup_batch(Ctx& c, const gs_publish* sched, uint64_t i0, uint64_t i1, bool upload = true) {
   Batch b;
   const uint32_t N = c.cfg.peers, S = c.S;
   b.F = frags_of(c, sched[i0]);
@@ -435,6 +437,7 @@ static Batch setup_batch(Ctx& c, const gs_publish* sched, uint64_t i0, uint64_t 
     }
   b.tpub.resize(b.B);
   for (uint32_t q = 0; q < b.B; q++) { pub[q] = sched[i0 + q].publisher; b.tpub[q] = sched[i0 + q].t_pub_ns; }
+  if (!upload) return b;
   c.d_pub.alloc(c.cfg.batch);
   c.d_tpub.alloc(c.cfg.batch);
   c.d_tables.alloc((size_t)S * S + 2 * S);
@@ -463,7 +466,8 @@ static void set_churn_args(Ctx& c, A& a) {
 }
 
 static void launch_seed(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, uint64_t* seed_min = nullptr,
-                        uint32_t* chunkmin = nullptr, bool to_list = false) {
+                        uint32_t* chunkmin = nullptr, bool to_list = false, const uint32_t* pub = nullptr,
+                        uint32_t soff = 0) {
   SeedArgs sa{};
   if (to_list) {
     sa.skey = c.d_skey.p;
@@ -472,7 +476,8 @@ static void launch_seed(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, uint64
   }
   set_churn_args(c, sa);
   sa.keys = c.d_keys.p; sa.row = c.d_row.p; sa.col = c.d_col.p; sa.mesh = c.d_mesh.p;
-  sa.pub = c.d_pub.p; sa.stage = c.d_stage.p; sa.tables = c.d_tables.p;
+  sa.pub = pub ? pub : c.d_pub.p; sa.stage = c.d_stage.p; sa.tables = c.d_tables.p;
+  sa.soff = soff;
   sa.ctrl = seed_min ? seed_min : c.d_ctrl.p; sa.chunkmin = chunkmin;
   sa.counters = c.d_counters.p; sa.tmax = b.tmax; sa.L = b.L; sa.FP = b.FP; sa.Fe = b.Fe;
   sa.S = c.S; sa.sb = b.sb; sa.tshift = b.tshift; sa.flood = c.cfg.flood_publish;
@@ -487,15 +492,21 @@ static void launch_seed(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, uint64
 // store: write d_tc / d_hops (results go to a sink); without it only the
 // counters and reductions are produced (a device-resident run).
 // lat: also the logged latencies [un][B] u16 into d_lat (GS_WANT_LAT_MS).
+// r0: the batch's rows start at row r0 of the key / log buffers (a batch slice, run_slices)
+// pub / tpub: the batch's publishers and publish times (default d_pub / d_tpub)
 static void run_complete(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, bool mstat, bool hist,
-                         bool store = true, bool lat = false) {
+                         bool store = true, bool lat = false, size_t r0 = 0, const uint32_t* pub = nullptr,
+                         const uint64_t* tpub = nullptr) {
+  if (!pub) pub = c.d_pub.p;
+  if (!tpub) tpub = c.d_tpub.p;
   hipStream_t s = c.stream;
   if (lat) c.d_lat.alloc((size_t)un * c.cfg.batch);
   if (c.keys_log) {  // list pull path, results on the device: reduce the final logs
     if (hist || store || b.FP != 1) c.fail(GS_EINVAL, "internal: final logs need k_lfinal");
     LPullArgs la{};
     la.u0 = u0;  // rows [0, un) are global peers u0 + row (a part of gs_run_partitioned)
-    la.keys = c.d_keys.p; la.flane = c.d_flane.p; la.st = c.d_lst.p; la.pub = c.d_pub.p;
+    la.keys = c.d_keys.p + r0 * b.L; la.flane = c.d_flane.p + r0 * b.L; la.st = c.d_lst.p + r0 * LP_SW;
+    la.pub = pub;
     la.counters = c.d_counters.p; la.N = un; la.B = b.B; la.L = b.L; la.tshift = b.tshift;
     la.self_log = c.cfg.self_log;
     if (mstat) {
@@ -509,7 +520,7 @@ static void run_complete(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, bool 
     return;
   }
   CompArgs ca{};
-  ca.keys = c.d_keys.p; ca.pub = c.d_pub.p; ca.tpub = c.d_tpub.p; ca.tc = store ? c.d_tc.p : nullptr;
+  ca.keys = c.d_keys.p + r0 * b.L; ca.pub = pub; ca.tpub = tpub; ca.tc = store ? c.d_tc.p : nullptr;
   ca.hops = c.d_hops.p; ca.counters = c.d_counters.p; ca.N = un; ca.B = b.B; ca.F = b.F;
   ca.lat = lat ? c.d_lat.p : nullptr;
   ca.FP = b.FP; ca.L = b.L; ca.sb = b.sb; ca.tshift = b.tshift; ca.collide = b.collide ? 1 : 0;
@@ -814,10 +825,10 @@ static void deliver(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, const gs_r
 
 // Completion + delivery of a finished batch.
 static void launch_complete(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, const gs_result_sink* sink,
-                            uint64_t sink_row0) {
+                            uint64_t sink_row0, size_t r0 = 0) {
   const bool hist = sink && sink->summary;
   const SinkWants w = sink_wants(sink);
-  run_complete(c, b, u0, un, hist, hist, w.rows() || w.summary, w.lat);  // k_pct reads d_tc
+  run_complete(c, b, u0, un, hist, hist, w.rows() || w.summary, w.lat, r0);  // k_pct reads d_tc
   deliver(c, b, u0, un, sink, sink_row0);
 }
 
@@ -999,7 +1010,9 @@ static uint32_t lpull_stride(const Batch& b) { return std::max<uint32_t>(b.L, 25
 // destination is at most K - 1 windows after the emitted one; the entry
 // packs (t - window start) | hops | src | lane into 64 bits; the seed list
 // packs row << 11 | lane (N < 2^21); the lists must fit the device memory left.
-static uint32_t lpull_ring(Ctx& c, const Batch& b, uint64_t delta, uint32_t* lb, bool gos = false, bool chn = false) {
+// rows: the pass's rows (batch slices: slices x peers)
+static uint32_t lpull_ring(Ctx& c, const Batch& b, uint64_t delta, uint32_t* lb, bool gos = false, bool chn = false,
+                           uint32_t rows = 0) {
   if (!c.mesh_dmax) {  // widest mesh row, once per mesh
     std::vector<uint32_t> m((size_t)c.cfg.peers * MESH_W);
     GS_HIP(hipMemcpyAsync(m.data(), c.d_mesh.p, m.size() * 4, hipMemcpyDeviceToHost, c.stream));
@@ -1012,7 +1025,8 @@ static uint32_t lpull_ring(Ctx& c, const Batch& b, uint64_t delta, uint32_t* lb,
     }
     c.mesh_dmax = dmax;
   }
-  if (b.tshift >= 32 || b.L > PULL_LMAX || delta < 2 || c.cfg.peers >= (1u << 21)) return 0;  // seed list: row << 11
+  const uint32_t N = rows ? rows : c.cfg.peers;
+  if (b.tshift >= 32 || b.L > PULL_LMAX || delta < 2 || N >= (1u << 21)) return 0;  // seed list: row << 11
   // a fragment waits behind at most the other FP - 1 fragments' sends to the
   // row's mesh peers (c.mesh_dmax, the widest mesh row)
   // (churn: each epoch has its own mesh, bounded by the ELL width)
@@ -1034,7 +1048,6 @@ static uint32_t lpull_ring(Ctx& c, const Batch& b, uint64_t delta, uint32_t* lb,
   while ((1ull << tb) < delta) tb++;
   *lb = bits_for(b.L);
   if (tb + b.tshift + *lb > 63) return 0;  // bit 63 of an entry marks a pushed IHAVE (gs_lpull_kernel.h)
-  const uint32_t N = c.cfg.peers;
   uint64_t need = (uint64_t)K * N * lpull_stride(b) * 8 + (uint64_t)N * b.L * 2 + (uint64_t)N * (LP_SW + LP_FW) * 4;
   uint64_t have = (uint64_t)c.d_lblk.n * 8 + (uint64_t)c.d_flane.n * 2 + (uint64_t)(c.d_lst.n + c.d_lfin.n) * 4;
   if (gos) {  // sender planes and entries
@@ -1067,10 +1080,22 @@ struct ChnRun {
   uint32_t cE, ghoff;
 };
 
+// Batch slices (run_slices): S batches of the same shape as one pass over S
+// copies of the graph, slice j's rows j * N1 + peer; the copies' mesh rows,
+// reverse positions and stages (d_smesh, d_srpos, d_sstage), the publishers
+// as slice rows (spub, k_lpull / k_lpub) and as peers (lpub, k_seed).
+struct Slices {
+  uint32_t S, N1;
+  const uint32_t* spub;
+  const uint32_t* lpub;
+};
+
 template <class EvFn>
 static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvFn& ev, size_t& n_ev, int dev_cus,
-                            bool dense, bool idw, const GosRun* gos = nullptr, const ChnRun* chn = nullptr) {
-  const uint32_t N = c.cfg.peers, L = b.L;
+                            bool dense, bool idw, const GosRun* gos = nullptr, const ChnRun* chn = nullptr,
+                            const Slices* sl = nullptr) {
+  const uint32_t N0 = c.cfg.peers, L = b.L;
+  const uint32_t N = sl ? sl->S * N0 : N0;  // the pass's rows
   hipStream_t s = c.stream;
   const size_t NL = (size_t)N * L;
   c.d_lrec.alloc((chn ? 4 : 2) * NL);  // churn records are 16 B
@@ -1082,12 +1107,20 @@ static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvF
   c.d_lfin.alloc((size_t)N * LP_FW);
   c.d_flane.alloc(NL);
   if (!c.rpos_valid) {
-    c.d_rpos.alloc((size_t)N * MESH_W);
+    c.d_rpos.alloc((size_t)N0 * MESH_W);
     GS_HIP(hipMemsetAsync(c.d_counters.p + C_ERR, 0, 8, s));
-    k_rpos<<<(unsigned)(((uint64_t)N * MESH_W + TB - 1) / TB), TB, 0, s>>>(c.d_mesh.p, c.d_rpos.p, N, c.d_counters.p);
+    k_rpos<<<(unsigned)(((uint64_t)N0 * MESH_W + TB - 1) / TB), TB, 0, s>>>(c.d_mesh.p, c.d_rpos.p, N0, c.d_counters.p);
     GS_HIP(hipGetLastError());
     if (read_counter(c, C_ERR) & ERR_MESH) c.fail(GS_ERANGE, "mesh is not symmetric");
     c.rpos_valid = true;
+  }
+  if (sl) {  // the graph copies of the slices (rebuilt per group: a few MB)
+    c.d_smesh.alloc((size_t)N * MESH_W);
+    c.d_srpos.alloc((size_t)N * MESH_W);
+    c.d_sstage.alloc(N);
+    k_srep<<<(unsigned)(((uint64_t)N * MESH_W + TB - 1) / TB), TB, 0, s>>>(
+        N0, sl->S, c.d_mesh.p, c.d_rpos.p, c.d_stage.p, c.d_smesh.p, c.d_srpos.p, c.d_sstage.p);
+    GS_HIP(hipGetLastError());
   }
   GS_HIP(hipMemsetAsync(c.d_lst.p, 0, (size_t)N * LP_SW * 4, s));
   GS_HIP(hipMemsetAsync(c.d_lfin.p, 0, (size_t)N * LP_FW * 4, s));
@@ -1096,17 +1129,28 @@ static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvF
   c.d_lp_save.alloc(C_COUNT);
   GS_HIP(hipMemcpyAsync(c.d_lp_save.p, c.d_counters.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));
   // seeds: one entry per (target, fragment) of every publish (flood: every connection)
-  const uint64_t scap = (uint64_t)b.B * b.Fe * std::max<uint64_t>(c.max_degree, MESH_W);
+  const uint64_t scap = (uint64_t)(sl ? sl->S : 1) * b.B * b.Fe * std::max<uint64_t>(c.max_degree, MESH_W);
   c.d_skey.alloc(scap);
   c.d_slane.alloc(scap);
   c.d_scnt.alloc(1);
   GS_HIP(hipMemsetAsync(c.d_scnt.p, 0, 4, s));
-  launch_seed(c, b, 0, N, c.d_pctrl.p + 2 * 4 + 3, nullptr, true);
+  if (sl)
+    for (uint32_t j = 0; j < sl->S; j++)
+      launch_seed(c, b, 0, N0, c.d_pctrl.p + 2 * 4 + 3, nullptr, true, sl->lpub + (size_t)j * b.B, j * N0);
+  else
+    launch_seed(c, b, 0, N, c.d_pctrl.p + 2 * 4 + 3, nullptr, true);
   LPullArgs la{};
   la.keys = c.d_keys.p; la.flane = c.d_flane.p; la.busy = c.d_busy.p; la.blk = c.d_lblk.p;
   la.st = c.d_lst.p; la.fin = c.d_lfin.p;
   la.lrec = c.d_lrec.p; la.lcnt = c.d_lcnt.p; la.rpos = c.d_rpos.p;
   la.mesh = c.d_mesh.p; la.pub = c.d_pub.p; la.stage = c.d_stage.p; la.tables = c.d_tables.p;
+  if (sl) {
+    la.mesh = c.d_smesh.p;
+    la.rpos = c.d_srpos.p;
+    la.stage = c.d_sstage.p;
+    la.pub = sl->spub;
+    la.rN = N0;
+  }
   const uint64_t grain = pull_grain(b.tshift);
   la.ctrl = c.d_pctrl.p; la.counters = c.d_counters.p; la.delta = b.delta / grain * grain;
   la.tmax = b.tmax - grain;
@@ -1167,7 +1211,17 @@ static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvF
   unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(((uint64_t)N + PULL_WAVES - 1) / PULL_WAVES, want));
   k_lseed<<<(unsigned)std::max<uint64_t>(1, std::min<uint64_t>((scap + TB - 1) / TB, (uint64_t)dev_cus * 4)), TB, 0, s>>>(
       la, c.d_skey.p, c.d_slane.p, c.d_scnt.p);
-  k_lpub<<<(b.B * b.Fe + 255) / 256, 256, 0, s>>>(la, b.Fe);
+  {  // the rows whose emit step needs the publishers (LP_PUB); GS_LPULL_PUBW=0: every row loads them
+    const char* pw = getenv("GS_LPULL_PUBW");  // per batch: A/B scripts switch it in one process
+    la.pubw = pw && *pw && atoi(pw) == 0 ? 0u : 1u;
+    const uint64_t nm = (uint64_t)(sl ? sl->S : 1u) * b.B, width = (chn ? CELL_W : MESH_W) + 1;
+    if (la.pubw) k_lpubnb<<<(unsigned)((nm * width + TB - 1) / TB), TB, 0, s>>>(la, (uint32_t)nm);
+  }
+  for (uint32_t j = 0; j < (sl ? sl->S : 1u); j++) {  // (a slice's publishers are its rows)
+    LPullArgs lj = la;
+    if (sl) lj.pub = sl->spub + (size_t)j * b.B;
+    k_lpub<<<(b.B * b.Fe + 255) / 256, 256, 0, s>>>(lj, b.Fe);
+  }
   GS_HIP(hipGetLastError());
   if (gos) {  // GOS: sender planes, row-done bits, heartbeat control (gs_lpull_kernel.h)
     ensure_csrpos(c);
@@ -1514,8 +1568,152 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
   }
   ensure_cus(c);
   const int dev_cus = c.num_cus;
+  // Batch slices: consecutive full batches of one shape on a small graph run as
+  // one list pass over S copies of the graph (run_lpull_batch's Slices), so that
+  // a launch has S x N rows instead of N: a pass of a few rows per resident wave
+  // is mostly latency (config #2's 10k-peer F = 8 rows: 98 us per pass at 10k
+  // rows, 340 us at 80k; scripts/c2_probe.py). Frozen mesh, no IDONTWANT, no
+  // per-peer traffic; lazy gossip through the eager pass's no-op proof, per slice
+  // (a group that fails it runs again as single batches). GS_SLICES=0 turns
+  // them off, GS_SLICES=n caps a group at n slices.
+  const char* sl_env = getenv("GS_SLICES");
+  const uint32_t sl_max = sl_env && *sl_env ? (uint32_t)std::max(0, atoi(sl_env)) : 64u;
+  constexpr uint64_t SL_ROWS = 1ull << 19;  // rows per pass a group aims at (memory: ~S x N x L x 40 B)
+  uint64_t slice_skip = 0;                  // messages before it run as single batches
+  auto try_slices = [&](uint64_t i0, uint64_t& i_end) -> bool {
+    if (sl_max < 2 || !pull_any || !(variant & 64) || c.traffic || (gossip && c.glp_prefer) ||
+        (uint64_t)N * 2 >= (1u << 21))
+      return false;
+    const uint32_t F0 = frags_of(c, sched[i0]), FP0 = pow2_at_least(F0);
+    if (FP0 > 1 && !(variant & 128)) return false;
+    const uint32_t Bc = std::min<uint32_t>(Bmax, PULL_LMAX / FP0);
+    const uint64_t s_cap = std::min<uint64_t>({(uint64_t)sl_max, std::max<uint64_t>(1, SL_ROWS / N), ((1ull << 21) - 1) / N});
+    uint64_t n_same = 1;  // messages of this shape from i0 (as far as a group can take)
+    while (n_same < s_cap * Bc && i0 + n_same < n_msgs && sched[i0 + n_same].msg_size == sched[i0].msg_size &&
+           frags_of(c, sched[i0 + n_same]) == F0)
+      n_same++;
+    const uint32_t S = (uint32_t)std::min<uint64_t>(n_same / Bc, s_cap);
+    if (S < 2) return false;
+    slice_skip = i0 + (uint64_t)S * Bc;  // unless the group completes below
+    std::vector<Batch> bs(S);
+    std::vector<uint32_t> spub((size_t)S * Bc), lpub((size_t)S * Bc);
+    for (uint32_t j = 0; j < S; j++) {
+      const uint64_t q0 = i0 + (uint64_t)j * Bc;
+      bs[j] = setup_batch(c, sched, q0, q0 + Bc, j == 0);
+      for (uint32_t q = 0; q < Bc; q++) {
+        lpub[(size_t)j * Bc + q] = sched[q0 + q].publisher;
+        spub[(size_t)j * Bc + q] = sched[q0 + q].publisher + j * N;
+      }
+    }
+    Batch g = bs[0];  // the slices' keys: the source field holds slice rows (S x N ids)
+    g.sb = bits_for(S * N);
+    g.tshift = g.sb + HOP_BITS;
+    g.tmax = g.tshift >= 64 ? 0 : (INF64 >> g.tshift);
+    for (Batch& bj : bs) {
+      bj.sb = g.sb;
+      bj.tshift = g.tshift;
+      bj.tmax = g.tmax;
+    }
+    if (c.cfg.idontwant && g.payload >= c.cfg.idontwant) return false;
+    const uint64_t grain = pull_grain(g.tshift);
+    if (g.delta < grain) return false;
+    uint32_t lb = 0;
+    const uint32_t K = lpull_ring(c, g, g.delta / grain * grain, &lb, false, false, S * N);
+    if (!K) return false;
+    const size_t NR = (size_t)S * N;
+    std::vector<uint64_t> stp((size_t)S * Bc);
+    for (uint32_t j = 0; j < S; j++) std::copy(bs[j].tpub.begin(), bs[j].tpub.end(), stp.begin() + (size_t)j * Bc);
+    c.d_spub.alloc(spub.size());
+    c.d_lpub.alloc(lpub.size());
+    c.d_stpub.alloc(stp.size());
+    GS_HIP(hipMemcpyAsync(c.d_spub.p, spub.data(), spub.size() * 4, hipMemcpyHostToDevice, s));
+    GS_HIP(hipMemcpyAsync(c.d_lpub.p, lpub.data(), lpub.size() * 4, hipMemcpyHostToDevice, s));
+    GS_HIP(hipMemcpyAsync(c.d_stpub.p, stp.data(), stp.size() * 8, hipMemcpyHostToDevice, s));
+    c.d_keys.alloc(NR * g.L);
+    if (g.FP > 1) {
+      c.d_busy.alloc(NR * Bc);
+      GS_HIP(hipMemsetAsync(c.d_busy.p, 0, NR * Bc * 8, s));
+    }
+    c.keys_log = false;
+    if (gossip) GS_HIP(hipMemcpyAsync(c.d_cnt_save.p, c.d_counters.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));
+    const SinkWants sw = sink_wants(sink);
+    const bool dense = sw.rows() || sw.summary || g.FP > 1 || getenv("GS_LPULL_DENSE");
+    const Slices sl{S, N, c.d_spub.p, c.d_lpub.p};
+    if (!run_lpull_batch(c, g, K, lb, ev, n_ev, dev_cus, dense, false, nullptr, nullptr, &sl))
+      return false;  // (a list overflowed: counters restored; single batches take the messages)
+    c.stats.list_pull_batches += S - 1;
+    auto slice_in = [&](uint32_t j) {  // slice j's publishers and publish times where completion reads them
+      GS_HIP(hipMemcpyAsync(c.d_pub.p, lpub.data() + (size_t)j * Bc, Bc * 4, hipMemcpyHostToDevice, s));
+      GS_HIP(hipMemcpyAsync(c.d_tpub.p, bs[j].tpub.data(), Bc * 8, hipMemcpyHostToDevice, s));
+    };
+    const bool wants = sw.rows() || sw.lat || sw.summary;
+    if (gossip) {  // the eager result stands only if gossip is a no-op in every slice
+      // every slice's reductions into one pinned buffer, one wait
+      const size_t msb = (size_t)S * Bc * MS_COLS * 8;
+      if (c.h_slms_bytes < msb) {
+        if (c.h_slms) GS_HIP(hipHostFree(c.h_slms));
+        c.h_slms = nullptr;
+        c.h_slms_bytes = 0;
+        GS_HIP(hipHostMalloc((void**)&c.h_slms, msb, hipHostMallocDefault));
+        c.h_slms_bytes = msb;
+      }
+      for (uint32_t j = 0; j < S; j++) {
+        run_complete(c, bs[j], 0, N, true, false, false, false, (size_t)j * N, c.d_lpub.p + (size_t)j * Bc,
+                     c.d_stpub.p + (size_t)j * Bc);
+        GS_HIP(hipMemcpyAsync(c.h_slms + (size_t)j * Bc * MS_COLS, c.d_mstat.p, (size_t)Bc * MS_COLS * 8,
+                              hipMemcpyDeviceToHost, s));
+      }
+      GS_HIP(hipStreamSynchronize(s));
+      std::vector<uint64_t> r0(Bc);
+      const uint64_t hb = c.cfg.heartbeat_ns, ph = c.cfg.hb_phase_ns;
+      bool noop = true;
+      for (uint32_t j = 0; j < S && noop; j++) {
+        for (uint32_t q = 0; q < Bc; q++) {
+          const uint64_t tp = bs[j].tpub[q], h0 = tp <= ph ? 0 : (tp - ph + hb - 1) / hb;
+          r0[q] = ph + h0 * hb - tp;
+        }
+        noop = gossip_noop(bs[j], c.h_slms + (size_t)j * Bc * MS_COLS, r0);
+      }
+      if (!noop) {  // discard the group; its batches run one by one (eager + proof, then the gossip paths)
+        GS_HIP(hipMemcpyAsync(c.d_counters.p, c.d_cnt_save.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));
+        c.stats.list_pull_batches -= S;
+        return false;
+      }
+      c.stats.gossip_noop_msgs += (uint64_t)S * Bc;
+      if (wants) {  // the sink's results: completion again per slice, its counters not counted twice
+        c.d_cnt_save2.alloc(C_COUNT);
+        GS_HIP(hipMemcpyAsync(c.d_cnt_save2.p, c.d_counters.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));
+        for (uint32_t j = 0; j < S; j++) {
+          slice_in(j);
+          launch_complete(c, bs[j], 0, N, sink, i0 + (uint64_t)j * Bc, (size_t)j * N);
+        }
+        GS_HIP(hipMemcpyAsync(c.d_counters.p, c.d_cnt_save2.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));
+      }
+    } else if (!wants) {  // device-resident results: the counters only
+      for (uint32_t j = 0; j < S; j++)
+        run_complete(c, bs[j], 0, N, false, false, false, false, (size_t)j * N, c.d_lpub.p + (size_t)j * Bc,
+                     c.d_stpub.p + (size_t)j * Bc);
+    } else {
+      for (uint32_t j = 0; j < S; j++) {
+        slice_in(j);
+        launch_complete(c, bs[j], 0, N, sink, i0 + (uint64_t)j * Bc, (size_t)j * N);
+      }
+    }
+    GS_HIP(hipStreamSynchronize(s));  // (lpub / tpub host copies die here)
+    c.stats.messages += (uint64_t)S * Bc;
+    c.stats.batches += S;
+    i_end = i0 + (uint64_t)S * Bc;
+    return true;
+  };
   uint64_t i0 = 0;
   while (i0 < n_msgs) {
+    if (i0 >= slice_skip) {
+      uint64_t ie = 0;
+      if (try_slices(i0, ie)) {
+        i0 = ie;
+        continue;
+      }
+    }
     // a batch: up to B messages of equal size and chunk count (serialisation
     // tables and the lane layout are per batch); the pull path holds a row in
     // registers, so its batch is capped at PULL_LMAX / FP messages
