@@ -103,6 +103,7 @@ struct LPullArgs {
   // slices' publishers [S][B] as such row ids. 0: one batch
   uint32_t rN;
   uint32_t pubw;  // the LP_PUB state words are set (k_lpubnb): a row without it skips the publisher load
+  uint32_t F, collide;  // k_lcomplete: fragments per message, defect D8 (no fragment group completes)
   const uint64_t* rpk;
   const uint64_t* roff;
   const uint32_t* rcg;
@@ -1615,19 +1616,26 @@ __global__ __launch_bounds__(TB) void k_lfinal(LPullArgs a) {
   }
 }
 
-// Completion from the final logs (FP == 1, results kept on the device): the
-// counters and per-message reductions of k_complete<1, false> without dense
-// rows. One wave per row scatters the row's log into LDS; lane j keeps the
-// reductions of messages j, j + 64, ... in registers over all its rows (a
-// log entry is a delivery unless the row is the message's publisher); one
-// flush per block through LDS.
+// Completion from the final logs (results kept on the device): the counters
+// and per-message reductions of k_complete<FP, false> without dense rows. One
+// wave per row scatters the row's log into LDS; lane j keeps the reductions
+// of messages j, j + 64, ... in registers over all its rows. A message's key
+// at a row is the latest of its F fragments' keys (reassembly, main.rs:79-99:
+// none unless all F arrived; never with colliding fragments, defect D8); at a
+// non-publisher row it is a delivery; one flush per block through LDS.
+// Batch slices (gs_relax.hip run_slices): block row y = slice y, whose rows
+// are y * N + w of the key / log buffers, its publishers pub[y * B ..] (peer
+// ids) and its reductions mstat[y * B ..].
 constexpr uint32_t LC_WAVES = 16;
 // With `lat` it also writes each row's logged latencies ([N][B] u16, the
-// GS_WANT_LAT_MS stream; GS_LAT_NONE where nothing is logged).
+// GS_WANT_LAT_MS stream; GS_LAT_NONE where nothing is logged; one slice).
 __global__ __launch_bounds__(LC_WAVES * 64) void k_lcomplete(LPullArgs a, uint64_t* mstat, uint16_t* lat) {
   __shared__ uint64_t R[LC_WAVES][PULL_LMAX];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const uint32_t B = a.B, stride = gridDim.x * LC_WAVES;
+  const uint32_t B = a.B, stride = gridDim.x * LC_WAVES, FP = a.L / a.B, F = a.F;
+  const size_t rbase = (size_t)blockIdx.y * a.N;
+  const uint32_t* pub = a.pub + (size_t)blockIdx.y * B;
+  if (mstat) mstat += (size_t)blockIdx.y * B * MS_COLS;
   uint64_t tm[PULL_CH];
   uint32_t ud[PULL_CH], pm[PULL_CH];
 #pragma unroll
@@ -1635,23 +1643,36 @@ __global__ __launch_bounds__(LC_WAVES * 64) void k_lcomplete(LPullArgs a, uint64
     const uint32_t m = j * 64 + lane;
     tm[j] = 0;
     ud[j] = 0;
-    pm[j] = m < B ? a.pub[m] : EMPTY;
+    pm[j] = m < B ? pub[m] : EMPTY;
   }
   uint64_t deliv = 0, lsum = 0, lmax = 0;
   uint64_t* Rw = R[wv];
+  // message m's key at this row (own: the publisher's own key, fragment 0)
+  auto mkey = [&](uint32_t m, bool own) -> uint64_t {
+    if (FP == 1 || own) return Rw[m * FP];
+    if (a.collide) return INF64;
+    uint64_t mk = 0;
+    for (uint32_t f = 0; f < F; f++) {
+      const uint64_t x = Rw[m * FP + f];
+      if (x == INF64) return INF64;
+      mk = x > mk ? x : mk;
+    }
+    return mk;
+  };
   for (uint32_t w = blockIdx.x * LC_WAVES + wv; w < a.N; w += stride) {
+    const size_t wr = rbase + w;
 #pragma unroll
     for (int j = 0; j < (int)PULL_CH; j++) Rw[j * 64 + lane] = INF64;
     wave_lds_sync();
-    const uint32_t n = a.st[(size_t)w * LP_SW + LP_LOG];
+    const uint32_t n = a.st[wr * LP_SW + LP_LOG];
     for (uint32_t i0 = 0; i0 < n; i0 += 256) {
       uint64_t k4[4];
       uint32_t l4[4];
 #pragma unroll
       for (int u = 0; u < 4; u++) {
         const uint32_t i = i0 + u * 64 + lane;
-        k4[u] = i < n ? a.keys[(size_t)w * a.L + i] : INF64;
-        l4[u] = i < n ? a.flane[(size_t)w * a.L + i] : 0u;
+        k4[u] = i < n ? a.keys[wr * a.L + i] : INF64;
+        l4[u] = i < n ? a.flane[wr * a.L + i] : 0u;
       }
 #pragma unroll
       for (int u = 0; u < 4; u++)
@@ -1664,9 +1685,10 @@ __global__ __launch_bounds__(LC_WAVES * 64) void k_lcomplete(LPullArgs a, uint64
       for (int j = 0; j < (int)PULL_CH; j++) {
         const uint32_t m = j * 64 + lane;
         if (m >= B) continue;
-        const uint64_t x = Rw[m];
+        const bool own = pm[j] == a.u0 + w;
+        const uint64_t x = mkey(m, own);
         uint32_t v = GS_LAT_NONE;
-        if (pm[j] == a.u0 + w) {
+        if (own) {
           if (a.self_log && x != INF64) v = 0;
         } else if (x != INF64) {
           const uint64_t ms = (x >> a.tshift) / 1000000ull;
@@ -1681,7 +1703,7 @@ __global__ __launch_bounds__(LC_WAVES * 64) void k_lcomplete(LPullArgs a, uint64
     for (int j = 0; j < (int)PULL_CH; j++) {
       const uint32_t m = j * 64 + lane;
       if (m >= B || pm[j] == a.u0 + w) continue;  // the publisher's own key is no delivery
-      const uint64_t x = Rw[m];
+      const uint64_t x = mkey(m, false);
       if (x == INF64) { ud[j]++; continue; }
       const uint64_t trel = x >> a.tshift, ms = trel / 1000000ull;
       deliv++;

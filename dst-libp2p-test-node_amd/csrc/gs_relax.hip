@@ -496,26 +496,29 @@ static void launch_seed(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, uint64
 // pub / tpub: the batch's publishers and publish times (default d_pub / d_tpub)
 static void run_complete(Ctx& c, const Batch& b, uint32_t u0, uint32_t un, bool mstat, bool hist,
                          bool store = true, bool lat = false, size_t r0 = 0, const uint32_t* pub = nullptr,
-                         const uint64_t* tpub = nullptr) {
+                         const uint64_t* tpub = nullptr, uint32_t nsl = 1) {
   if (!pub) pub = c.d_pub.p;
   if (!tpub) tpub = c.d_tpub.p;
   hipStream_t s = c.stream;
   if (lat) c.d_lat.alloc((size_t)un * c.cfg.batch);
   if (c.keys_log) {  // list pull path, results on the device: reduce the final logs
-    if (hist || store || b.FP != 1) c.fail(GS_EINVAL, "internal: final logs need k_lfinal");
+    // (nsl batch slices of un rows each, one launch: block row y = slice y, run_slices)
+    if (hist || store || (lat && nsl > 1)) c.fail(GS_EINVAL, "internal: final logs need k_lfinal");
     LPullArgs la{};
     la.u0 = u0;  // rows [0, un) are global peers u0 + row (a part of gs_run_partitioned)
     la.keys = c.d_keys.p + r0 * b.L; la.flane = c.d_flane.p + r0 * b.L; la.st = c.d_lst.p + r0 * LP_SW;
     la.pub = pub;
     la.counters = c.d_counters.p; la.N = un; la.B = b.B; la.L = b.L; la.tshift = b.tshift;
+    la.F = b.F; la.collide = b.collide ? 1u : 0u;
     la.self_log = c.cfg.self_log;
     if (mstat) {
-      c.d_mstat.alloc((size_t)c.cfg.batch * MS_COLS);
-      GS_HIP(hipMemsetAsync(c.d_mstat.p, 0, (size_t)b.B * MS_COLS * 8, s));
+      c.d_mstat.alloc((size_t)std::max(c.cfg.batch, nsl * b.B) * MS_COLS);
+      GS_HIP(hipMemsetAsync(c.d_mstat.p, 0, (size_t)nsl * b.B * MS_COLS * 8, s));
     }
     const unsigned grid = (unsigned)std::max<uint64_t>(
-        1, std::min<uint64_t>(((uint64_t)un + LC_WAVES - 1) / LC_WAVES, (uint64_t)std::max(1, c.num_cus)));
-    k_lcomplete<<<grid, LC_WAVES * 64, 0, s>>>(la, mstat ? c.d_mstat.p : nullptr, lat ? c.d_lat.p : nullptr);
+        1, std::min<uint64_t>(((uint64_t)un + LC_WAVES - 1) / LC_WAVES,
+                              std::max<uint64_t>(1, (uint64_t)std::max(1, c.num_cus) / nsl)));
+    k_lcomplete<<<dim3(grid, nsl), LC_WAVES * 64, 0, s>>>(la, mstat ? c.d_mstat.p : nullptr, lat ? c.d_lat.p : nullptr);
     GS_HIP(hipGetLastError());
     return;
   }
@@ -1637,7 +1640,7 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     c.keys_log = false;
     if (gossip) GS_HIP(hipMemcpyAsync(c.d_cnt_save.p, c.d_counters.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));
     const SinkWants sw = sink_wants(sink);
-    const bool dense = sw.rows() || sw.summary || g.FP > 1 || getenv("GS_LPULL_DENSE");
+    const bool dense = sw.rows() || sw.summary || getenv("GS_LPULL_DENSE");
     const Slices sl{S, N, c.d_spub.p, c.d_lpub.p};
     if (!run_lpull_batch(c, g, K, lb, ev, n_ev, dev_cus, dense, false, nullptr, nullptr, &sl))
       return false;  // (a list overflowed: counters restored; single batches take the messages)
@@ -1657,11 +1660,16 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
         GS_HIP(hipHostMalloc((void**)&c.h_slms, msb, hipHostMallocDefault));
         c.h_slms_bytes = msb;
       }
-      for (uint32_t j = 0; j < S; j++) {
-        run_complete(c, bs[j], 0, N, true, false, false, false, (size_t)j * N, c.d_lpub.p + (size_t)j * Bc,
-                     c.d_stpub.p + (size_t)j * Bc);
-        GS_HIP(hipMemcpyAsync(c.h_slms + (size_t)j * Bc * MS_COLS, c.d_mstat.p, (size_t)Bc * MS_COLS * 8,
-                              hipMemcpyDeviceToHost, s));
+      if (c.keys_log) {  // every slice in one launch
+        run_complete(c, bs[0], 0, N, true, false, false, false, 0, c.d_lpub.p, c.d_stpub.p, S);
+        GS_HIP(hipMemcpyAsync(c.h_slms, c.d_mstat.p, msb, hipMemcpyDeviceToHost, s));
+      } else {
+        for (uint32_t j = 0; j < S; j++) {
+          run_complete(c, bs[j], 0, N, true, false, false, false, (size_t)j * N, c.d_lpub.p + (size_t)j * Bc,
+                       c.d_stpub.p + (size_t)j * Bc);
+          GS_HIP(hipMemcpyAsync(c.h_slms + (size_t)j * Bc * MS_COLS, c.d_mstat.p, (size_t)Bc * MS_COLS * 8,
+                                hipMemcpyDeviceToHost, s));
+        }
       }
       GS_HIP(hipStreamSynchronize(s));
       std::vector<uint64_t> r0(Bc);
@@ -1690,9 +1698,11 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
         GS_HIP(hipMemcpyAsync(c.d_counters.p, c.d_cnt_save2.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));
       }
     } else if (!wants) {  // device-resident results: the counters only
-      for (uint32_t j = 0; j < S; j++)
-        run_complete(c, bs[j], 0, N, false, false, false, false, (size_t)j * N, c.d_lpub.p + (size_t)j * Bc,
-                     c.d_stpub.p + (size_t)j * Bc);
+      if (c.keys_log) run_complete(c, bs[0], 0, N, false, false, false, false, 0, c.d_lpub.p, c.d_stpub.p, S);
+      else
+        for (uint32_t j = 0; j < S; j++)
+          run_complete(c, bs[j], 0, N, false, false, false, false, (size_t)j * N, c.d_lpub.p + (size_t)j * Bc,
+                       c.d_stpub.p + (size_t)j * Bc);
     } else {
       for (uint32_t j = 0; j < S; j++) {
         slice_in(j);
@@ -2019,7 +2029,7 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
         // stream calibrates the PMC read factor (scripts/pmc_summary.py);
         // IDONTWANT batches keep their final keys dense all along
         const SinkWants sw = sink_wants(sink);
-        const bool dense = !idw_b && (sw.rows() || sw.summary || c.traffic || b.FP > 1 || getenv("GS_LPULL_DENSE"));
+        const bool dense = !idw_b && (sw.rows() || sw.summary || c.traffic || getenv("GS_LPULL_DENSE"));
         if (!K || !run_lpull_batch(c, bw, K, lb, ev, n_ev, dev_cus, dense, idw_b)) {
           if (K && getenv("GS_REQUIRE_LPULL")) c.fail(GS_EUNSUPPORTED, "list pull overflow (GS_REQUIRE_LPULL)");
           if (idw_b) {  // k_pull has no IDONTWANT: the push path takes the batch

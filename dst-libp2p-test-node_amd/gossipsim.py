@@ -480,11 +480,17 @@ class Simulator:
             self._sched = []
         elif not isinstance(schedule, ctypes.Array):
             t, p, s = schedule[:3]
-            fr = schedule[3] if len(schedule) > 3 else np.zeros(len(t), np.uint32)
-            arr = (GsPublish * len(t))()
-            for i in range(len(t)):
-                arr[i] = GsPublish(int(t[i]), int(p[i]), int(s[i]), int(fr[i]), 0)
-            schedule = arr
+            fr = schedule[3] if len(schedule) > 3 else 0
+            # one vectorised fill of the gs_publish layout (a per-element struct loop cost
+            # ~0.7 ms per 1024 messages, most of a config #1 run)
+            rec = np.zeros(len(t), np.dtype([("t_pub_ns", "<u8"), ("publisher", "<u4"), ("msg_size", "<u4"),
+                                             ("frags", "<u4"), ("reserved", "<u4")]))
+            assert rec.dtype.itemsize == ctypes.sizeof(GsPublish)
+            rec["t_pub_ns"] = np.asarray(t, np.uint64)
+            rec["publisher"] = np.asarray(p, np.uint32)
+            rec["msg_size"] = np.asarray(s, np.uint32)
+            rec["frags"] = np.asarray(fr, np.uint32)
+            schedule = (GsPublish * len(t)).from_buffer_copy(rec.tobytes())
         return schedule
 
     def run(self, schedule=None, collect=True, summary=False, on_block=None, block_msgs=0,

@@ -113,3 +113,24 @@ def test_slices_c2_shape_bench_path(monkeypatch):
     for k in KEYS:
         assert sa[k] == sb[k], k
     assert sa["gossip_noop_msgs"] == 256
+
+
+@pytest.mark.parametrize("frags,slices", [(2, "0"), (8, "0"), (8, ""), (3, "")])
+def test_fragment_groups_complete_from_logs(monkeypatch, frags, slices):
+    """Fragmented batches complete from the final logs (k_lcomplete reduces each
+    message's F fragment lanes: reassembly) unless a sink takes rows: the
+    counters, the gossip no-op proof and the u16 latency stream equal the dense
+    rows' k_complete (GS_LPULL_DENSE=1)."""
+    p = oracle.params(peers=1300, seed=340 + frags, fragments=frags)
+    sched = _sched(64, 1300)
+    out = {}
+    for dense in ("", "1"):
+        monkeypatch.setenv("GS_LPULL_DENSE", dense)
+        o, st = _run(monkeypatch, slices, p, sched, 16, "lat")
+        _, st2 = _run(monkeypatch, slices, p, sched, 16, "none")
+        out[dense] = (o["lat"], st, st2)
+    np.testing.assert_array_equal(out[""][0], out["1"][0])
+    for k in KEYS + ("gossip_noop_msgs",):
+        assert out[""][1][k] == out["1"][1][k], k
+        assert out[""][2][k] == out["1"][2][k], k
+    assert out[""][2]["gossip_noop_msgs"] == 64
