@@ -67,6 +67,8 @@ def parse():
                     help="second graph size reported beside the headline (metric names 100k & 1M; 0=off)")
     ap.add_argument("--gossip-check", type=int, default=64,
                     help="messages of the 1M-peer gossip-on vs eager-only delivery comparison (0=off)")
+    ap.add_argument("--config-traffic-json", default=os.path.join(ROOT, "profiles", "config_traffic_latest.json"),
+                    help="per-config HBM bytes from rocprofv3 --pmc passes (scripts/config_pmc.sh + config_traffic.py)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="per-launch HBM bytes of the relax kernel from a rocprofv3 --pmc pass")
     return ap.parse_args()
@@ -399,6 +401,10 @@ CONFIGS = {
     # forwards (0.7 % of completions change), the gossip runs inside the list pass
     "c4_1m_gossip_370ms": dict(peers=1_000_000, links=(5, 50, 150, 40, 130), fragments=1, batch=1024, msgs=1024,
                                reps=2, knobs=dict(hb_phase_ns=(gossipsim.T0_NS + 370_000_000) % 1_000_000_000)),
+    # config #2's shape with heartbeats 370 ms after every publish: fragment rows with IHAVE/IWANT
+    # inside the list pass (every fragment gossiped on its own)
+    "c2_10k_F8_gossip_370ms": dict(peers=10_000, links=(5, 50, 150, 40, 130), fragments=8, batch=128, msgs=1024,
+                                   reps=3, knobs=dict(hb_phase_ns=(gossipsim.T0_NS + 370_000_000) % 1_000_000_000)),
     "c3_100k_gossip_churn": dict(
         peers=100_000, links=(5, 50, 150, 40, 130), fragments=1, batch=1024, msgs=1024,
         knobs=dict(lazy_gossip=1, churn_ppm=10_000, churn_down=10, churn_horizon=16,
@@ -406,8 +412,17 @@ CONFIGS = {
 }
 
 
+def config_traffic(args):
+    """{config: PMC entry} of --config-traffic-json (empty when absent or unreadable)"""
+    try:
+        return json.load(open(args.config_traffic_json)).get("configs", {})
+    except (OSError, ValueError, AttributeError):
+        return {}
+
+
 def config_rates(args, local):
     out = {}
+    ctraffic = config_traffic(args)
     mark = os.environ.get("GS_CFG_MARK") == "1"
     for name, c in CONFIGS.items():
         sim = gossipsim.Simulator(peers=c["peers"], batch=c["batch"], fragments=c["fragments"], seed=args.seed,
@@ -459,6 +474,14 @@ def config_rates(args, local):
                      "pull (k_lpull, IHAVE/IWANT inside the passes)" if st["gossip_list_batches"] else
                      "pull (k_lpull)" if st["list_pull_batches"] else "pull (k_pull)",
                      "roofline": roof}
+        pmc = ctraffic.get(name)
+        # PMC bytes of the same window-pass kernel family as this run's path (k_lpull / k_pull)
+        if roof and pmc and pmc.get("hbm_bytes_per_launch") and pmc.get("pass_kernels") and \
+                all(k.split("<")[0] in out[name]["kernel_path"] for k in pmc["pass_kernels"]):
+            roof["traffic"] = pmc["hbm_bytes_per_launch"]
+            roof["traffic_ratio"] = pmc["hbm_bytes_per_launch"] / roof["alg_bytes_per_launch"]
+            out[name]["hbm_bytes_per_batch_all_kernels"] = pmc.get("hbm_bytes_per_batch_all_kernels")
+            out[name]["traffic_source"] = pmc.get("source")
         sim.close()
     return out
 

@@ -258,7 +258,8 @@ extern "C" gs_status gs_reset_stats(gs_ctx* ctx) {
     GS_HIP(hipMemsetAsync(ctx->d_traffic.p, 0, (size_t)ctx->cfg.peers * GS_TRAFFIC_COLS * 8, ctx->stream));
   GS_HIP(hipStreamSynchronize(ctx->stream));
   memset(&ctx->stats, 0, sizeof(ctx->stats));
-  ctx->glp_prefer = false;  // the next gossip batch tries the eager pass + no-op proof first
+  // (glp_prefer, the path choice learnt from a failed no-op proof, is no statistic: it
+  // stays until the mesh changes or GLP_QUIET IWANT-free batches clear it)
   GS_API_END(ctx)
 }
 

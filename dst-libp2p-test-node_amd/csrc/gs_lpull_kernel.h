@@ -474,7 +474,7 @@ template <int FP, uint32_t CH, bool IDW = false, bool PART = false, bool GOS = f
 __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
   constexpr uint32_t NG = GS_LP_NG, RCH = GS_LP_RCH;
   static_assert(!IDW || FP == 1, "IDONTWANT on the list pass: rows of single-fragment lanes");
-  static_assert(!GOS || (FP == 1 && !IDW && !PART), "gossip on the list pass: gs_run's single-fragment rows");
+  static_assert(!GOS || (!IDW && !PART), "gossip on the list pass: gs_run's rows without IDONTWANT");
   static_assert(!CHN || (FP == 1 && !IDW && !PART), "churn on the list pass: gs_run's single-fragment rows");
   // row header: the mesh row (frozen mesh) or, under churn, the CSR row (the
   // mesh of a lane's epoch is a mask over it)
@@ -1145,7 +1145,8 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     // 5. row state: final bits, pending list lengths, log length
     if (nfin) reinterpret_cast<uint16_t*>(a.fin + (size_t)w * LP_FW)[lane] = (uint16_t)finT;
     if constexpr (GOS) {  // every lane final: no IHAVE can matter to this row any more
-      if (nfin && wave_sum((uint64_t)__popc(finT & 0xFFFFu)) == a.B && lane == 0)
+      // (the lanes that can be final: F per message, one under defect D8; padding lanes never are)
+      if (nfin && wave_sum((uint64_t)__popc(finT & 0xFFFFu)) == a.B * (a.collide ? 1u : a.F) && lane == 0)
         atomicOr(&a.rowdone[w >> 5], 1u << (w & 31));
     }
     {
@@ -1469,8 +1470,9 @@ __global__ __launch_bounds__(TB) void k_gsend(LPullArgs a) {
     for (uint32_t j0 = 0; j0 < ns; j0 += 64) {
       const bool jv = j0 + lane < ns;
       const uint32_t s = jv ? sel[wv][j0 + lane] : 0u;
-      const uint32_t m = s & 0xFFFFu;
-      const uint32_t h = jv ? (uint32_t)(a.habs0[m] + k) : 0u;
+      const uint32_t m = s & 0xFFFFu;  // the lane (fragment lanes: message m / FP; every fragment is
+                                       // gossiped on its own, at its message's heartbeats)
+      const uint32_t h = jv ? (uint32_t)(a.habs0[m / (a.L / a.B)] + k) : 0u;
       uint64_t mask;
       if constexpr (CHN) {  // the targets k_cprep selected for (v, the lane's epoch)
         const uint32_t kh = a.ghoff + (uint32_t)k;
@@ -1820,12 +1822,25 @@ void lpull_dispatch_gos(const LPullArgs& a, unsigned grid, hipStream_t s) {
     }
     return;
   }
+  const uint32_t FP = a.L / a.B;  // fragment lanes per message (rows of fragment groups: one lane per fragment)
   if (lpull_chunks(a.L) == 8) {
     k_gsend<8><<<grid, TB, 0, s>>>(a);
-    k_lpull<1, 8, false, false, true><<<grid, TB, 0, s>>>(a);
+    switch (FP) {
+      case 1: k_lpull<1, 8, false, false, true><<<grid, TB, 0, s>>>(a); break;
+      case 2: k_lpull<2, 8, false, false, true><<<grid, TB, 0, s>>>(a); break;
+      case 4: k_lpull<4, 8, false, false, true><<<grid, TB, 0, s>>>(a); break;
+      case 8: k_lpull<8, 8, false, false, true><<<grid, TB, 0, s>>>(a); break;
+      default: k_lpull<16, 8, false, false, true><<<grid, TB, 0, s>>>(a); break;
+    }
   } else {
     k_gsend<16><<<grid, TB, 0, s>>>(a);
-    k_lpull<1, 16, false, false, true><<<grid, TB, 0, s>>>(a);
+    switch (FP) {
+      case 1: k_lpull<1, 16, false, false, true><<<grid, TB, 0, s>>>(a); break;
+      case 2: k_lpull<2, 16, false, false, true><<<grid, TB, 0, s>>>(a); break;
+      case 4: k_lpull<4, 16, false, false, true><<<grid, TB, 0, s>>>(a); break;
+      case 8: k_lpull<8, 16, false, false, true><<<grid, TB, 0, s>>>(a); break;
+      default: k_lpull<16, 16, false, false, true><<<grid, TB, 0, s>>>(a); break;
+    }
   }
 }
 

@@ -1240,7 +1240,9 @@ static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvF
     la.ghb = gos->hb;
     la.glat_min = b.lat_min;
     la.glat_max = b.lat_max;
-    la.gnf = (uint64_t)b.B * (N - 1);
+    la.gnf = (uint64_t)b.B * b.Fe * (N - 1);  // fragment lanes that can be final, less the publishers'
+    la.F = b.F;
+    la.collide = b.collide ? 1u : 0u;
     la.gseed = c.cfg.seed;
     la.ghist = c.cfg.history_gossip;
     la.gd_lazy = c.cfg.d_lazy;
@@ -1949,8 +1951,9 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     Batch bw = b;
     if (idw_b) bw.delta = std::min(b.delta, b.lat_min);
     const bool pull_ok = pull_any && bw.delta >= pull_grain(b.tshift) && (!idw_b || (b.FP == 1 && (variant & 64)));
-    // Lazy gossip inside the list pass (GOS, gs_lpull_kernel.h): rows of one
-    // fragment without IDONTWANT on the frozen mesh, every message's heartbeats
+    // Lazy gossip inside the list pass (GOS, gs_lpull_kernel.h): rows without
+    // IDONTWANT (fragment groups too: every fragment is gossiped on its own at its
+    // message's heartbeats, as the oracle's sched_gossip) on the frozen mesh, every message's heartbeats
     // the same time after its publish (lockstep), CSR rows narrow enough for a
     // 58-bit target mask, windows no wider than the smallest latency (an IHAVE
     // never shares a window with its heartbeat) and heartbeats farther apart
@@ -1962,7 +1965,7 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     bg.delta = std::min(b.delta, b.lat_min);
     const uint64_t ggr = pull_grain(b.tshift);
     const char* glp_env = getenv("GS_GOSSIP_LIST");
-    const bool glp = gossip && !churn && pull_ok && !idw_b && b.FP == 1 && (variant & 64) && lockstep &&
+    const bool glp = gossip && !churn && pull_ok && !idw_b && (b.FP == 1 || (variant & 128)) && (variant & 64) && lockstep &&
                      !(glp_env && *glp_env && atoi(glp_env) == 0) && c.max_degree <= GSE_HOPS && bg.delta >= ggr &&
                      c.cfg.heartbeat_ns > b.lat_max + bg.delta;
     bool glp_tried = false;

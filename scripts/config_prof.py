@@ -12,6 +12,8 @@ class Args:
     seed = 1
     max_heartbeats = 400
     msg_size = 15000
+    config_traffic_json = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
+                                       "config_traffic_latest.json")
 
 
 bench.CONFIGS = {k: v for k, v in bench.CONFIGS.items() if k in sys.argv[1:]}

@@ -89,7 +89,7 @@ def main():
         log = os.path.join(a.dir, "%s_FETCH_SIZE.log" % name)
         alg = None
         try:
-            line = [x for x in open(log) if x.startswith("{")][-1]
+            line = [x for x in open(log) if x.startswith("{") and not x.startswith('{"mark"')][-1]
             alg = json.loads(line)[name].get("alg_bytes_per_batch")
         except (OSError, IndexError, ValueError, KeyError):
             pass

@@ -209,3 +209,31 @@ def test_gossip_active_1m_x_1024_heartbeat_370ms(monkeypatch):
         sums[path] = (got, s2["relaxations"], s2["gossip_iwant"], s2["deliveries"])
     assert sums["list"] == sums["push"]
     sim.close()
+
+
+@pytest.mark.parametrize("frags,phase_ms", [(2, 120), (3, 55), (8, 0), (8, 120)])
+def test_gossip_in_list_pass_fragment_groups(frags, phase_ms):
+    """Fragmented messages with gossip-active heartbeats: every fragment is
+    gossiped on its own (the oracle's sched_gossip per (peer, fragment)); after
+    the first batch's failed no-op proof the batches' IHAVE/IWANT run inside
+    the list pass of fragment-group rows — bit-exact with the oracle."""
+    p = oracle.params(peers=2200, seed=250 + frags, fragments=frags, hb_phase_ns=_phase(phase_ms))
+    sim, _ = compare(p, 5, LINKS, _sched(32, 2200), batch=8)
+    st = sim.stats()
+    assert st["gossip_iwant"] > 0
+    assert st["gossip_fallback_batches"] <= 1 and st["gossip_list_batches"] >= 3
+
+
+@pytest.mark.parametrize("path", ["list", "push"])
+def test_gossip_fragment_groups_list_equals_push(monkeypatch, path):
+    """F = 8 gossip-active batches on the list pass and (GS_GOSSIP_LIST=0) on
+    the push path: both equal the oracle."""
+    if path == "push":
+        monkeypatch.setenv("GS_GOSSIP_LIST", "0")
+    p = oracle.params(peers=1800, seed=96, fragments=8, hb_phase_ns=_phase(0))
+    sim, _ = compare(p, 5, LINKS, _sched(24, 1800), batch=8)
+    st = sim.stats()
+    if path == "list":
+        assert st["gossip_fallback_batches"] == 1 and st["gossip_list_batches"] == 3
+    else:
+        assert st["gossip_fallback_batches"] == 3 and st["gossip_list_batches"] == 0
