@@ -397,6 +397,10 @@ CONFIGS = {
     # unsigned, own message logged) at 100k peers, the IDONTWANT list pass
     "go_100k_idontwant": dict(peers=100_000, knobs=dict(node="go"), links=(5, 50, 150, 40, 130), fragments=1,
                               batch=1024, msgs=1024, reps=2),
+    # the go preset gossip-active: IDONTWANT and IHAVE / IWANT in the same list pass
+    "go_100k_idontwant_gossip_370ms": dict(peers=100_000, links=(5, 50, 150, 40, 130), fragments=1, batch=1024,
+                                           msgs=1024, reps=2, knobs=dict(
+                                               node="go", hb_phase_ns=(gossipsim.T0_NS + 370_000_000) % 1_000_000_000)),
     # the headline graph with heartbeats 370 ms after every publish: IWANT answers overtake eager
     # forwards (0.7 % of completions change), the gossip runs inside the list pass
     "c4_1m_gossip_370ms": dict(peers=1_000_000, links=(5, 50, 150, 40, 130), fragments=1, batch=1024, msgs=1024,

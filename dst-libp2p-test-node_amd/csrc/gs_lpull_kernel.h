@@ -474,7 +474,7 @@ template <int FP, uint32_t CH, bool IDW = false, bool PART = false, bool GOS = f
 __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
   constexpr uint32_t NG = GS_LP_NG, RCH = GS_LP_RCH;
   static_assert(!IDW || FP == 1, "IDONTWANT on the list pass: rows of single-fragment lanes");
-  static_assert(!GOS || (!IDW && !PART), "gossip on the list pass: gs_run's rows without IDONTWANT");
+  static_assert(!GOS || !PART, "gossip on the list pass: gs_run's rows");
   static_assert(!CHN || (FP == 1 && !IDW && !PART), "churn on the list pass: gs_run's single-fragment rows");
   // row header: the mesh row (frozen mesh) or, under churn, the CSR row (the
   // mesh of a lane's epoch is a mask over it)
@@ -1437,13 +1437,14 @@ __global__ __launch_bounds__(TB) void k_gsend(LPullArgs a) {
     uint32_t r = (uint32_t)(((uint64_t)nonmesh * a.ggf) / 1000);
     if (r < a.gd_lazy) r = a.gd_lazy;
     if (r > nonmesh) r = nonmesh;
-    // 1. the senders of k from the log: lane | hops << 16
-    const uint32_t n = a.st[(size_t)v * LP_SW + LP_LOG];
+    // 1. the senders of k from the log: lane | hops << 16 (IDONTWANT batches keep
+    //    dense final keys instead of a log: every lane of the row is looked at)
+    const uint32_t n = a.idw ? a.L : a.st[(size_t)v * LP_SW + LP_LOG];
     uint32_t ns = 0;
     // the log is in window order: entries before the first one whose window
     // holds R_(k - hist) or later are not senders of k; 64 samples locate it
     uint32_t i_start = 0;
-    if (haslo && n > 64) {
+    if (haslo && n > 64 && !a.idw) {
       const uint32_t stride = (n + 63) / 64, ip = (uint32_t)lane * stride;
       const uint64_t T = (Rlo / a.delta) * a.delta;
       const uint64_t sk = ip < n ? a.keys[(size_t)v * a.L + ip] : INF64;
@@ -1455,14 +1456,14 @@ __global__ __launch_bounds__(TB) void k_gsend(LPullArgs a) {
       const uint32_t i = i0 + lane;
       const uint64_t key = i < n ? a.keys[(size_t)v * a.L + i] : INF64;
       const uint64_t t = key >> a.tshift;
-      const bool s = i < n && t <= Rk && (!haslo || t > Rlo);
+      const bool s = i < n && key != INF64 && t <= Rk && (!haslo || t > Rlo);
       const uint64_t sm = __ballot(s);
       if (s)
         sel[wv][ns + (uint32_t)__popcll(sm & lanelt)] =
-            (uint32_t)a.flane[(size_t)v * a.L + i] | ((uint32_t)(key >> a.sb) & hmask) << 16;
+            (a.idw ? i : (uint32_t)a.flane[(size_t)v * a.L + i]) | ((uint32_t)(key >> a.sb) & hmask) << 16;
       ns += (uint32_t)__popcll(sm);
-      // entries of later windows have t > R_k: stop after a chunk with none at or below R_k + Delta
-      if (__ballot(i < n && t <= Rk + a.delta) == 0) break;
+      // log entries of later windows have t > R_k: stop after a chunk with none at or below R_k + Delta
+      if (!a.idw && __ballot(i < n && t <= Rk + a.delta) == 0) break;
     }
     wave_lds_sync();
     // 2. each sender lane's targets at its message's heartbeat habs0[m] + k
@@ -1823,6 +1824,16 @@ void lpull_dispatch_gos(const LPullArgs& a, unsigned grid, hipStream_t s) {
     return;
   }
   const uint32_t FP = a.L / a.B;  // fragment lanes per message (rows of fragment groups: one lane per fragment)
+  if (a.idw) {  // IDONTWANT (FP == 1: the host sends fragmented IDONTWANT batches to the push path)
+    if (lpull_chunks(a.L) == 8) {
+      k_gsend<8><<<grid, TB, 0, s>>>(a);
+      k_lpull<1, 8, true, false, true><<<grid, TB, 0, s>>>(a);
+    } else {
+      k_gsend<16><<<grid, TB, 0, s>>>(a);
+      k_lpull<1, 16, true, false, true><<<grid, TB, 0, s>>>(a);
+    }
+    return;
+  }
   if (lpull_chunks(a.L) == 8) {
     k_gsend<8><<<grid, TB, 0, s>>>(a);
     switch (FP) {

@@ -1965,7 +1965,7 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     bg.delta = std::min(b.delta, b.lat_min);
     const uint64_t ggr = pull_grain(b.tshift);
     const char* glp_env = getenv("GS_GOSSIP_LIST");
-    const bool glp = gossip && !churn && pull_ok && !idw_b && (b.FP == 1 || (variant & 128)) && (variant & 64) && lockstep &&
+    const bool glp = gossip && !churn && pull_ok && (b.FP == 1 || (variant & 128)) && (variant & 64) && lockstep &&
                      !(glp_env && *glp_env && atoi(glp_env) == 0) && c.max_degree <= GSE_HOPS && bg.delta >= ggr &&
                      c.cfg.heartbeat_ns > b.lat_max + bg.delta;
     bool glp_tried = false;
@@ -1974,12 +1974,12 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       uint32_t lb = 0;
       const uint32_t K = lpull_ring(c, bg, bg.delta / ggr * ggr, &lb, true);
       if (!K) return false;
-      reset(variant, false, false);
+      reset(variant, false, idw_b);  // IDONTWANT: dense INF keys (the finals stay dense rows)
       const GosRun gr{rel0[0], c.cfg.heartbeat_ns};
       const SinkWants sw = sink_wants(sink);
       const bool dense = sw.rows() || sw.summary || c.traffic || getenv("GS_LPULL_DENSE");
       const uint64_t iw0 = read_counter(c, C_GOSSIP);
-      if (!run_lpull_batch(c, bg, K, lb, ev, n_ev, dev_cus, dense, false, &gr)) return false;
+      if (!run_lpull_batch(c, bg, K, lb, ev, n_ev, dev_cus, dense, idw_b, &gr)) return false;
       c.stats.gossip_list_batches++;
       // GLP_QUIET batches in a row whose gossip sent no IWANT: the next one tries the
       // eager pass and its no-op proof first again (glp_prefer was never

@@ -237,3 +237,16 @@ def test_gossip_fragment_groups_list_equals_push(monkeypatch, path):
         assert st["gossip_fallback_batches"] == 1 and st["gossip_list_batches"] == 3
     else:
         assert st["gossip_fallback_batches"] == 3 and st["gossip_list_batches"] == 0
+
+
+@pytest.mark.parametrize("phase_ms", [55, 120])
+def test_gossip_in_list_pass_idontwant(phase_ms):
+    """The go preset (IDONTWANT >= 1000 B, go-test-node/main.go:165) with
+    gossip-active heartbeats: the IDONTWANT list pass (dense final keys, the
+    neighbours' IDONTWANTs read in the emit step) takes the IHAVE / IWANT too —
+    the sender planes come from the dense rows — bit-exact with the oracle."""
+    p = oracle.params_for("go", peers=2400, seed=260 + phase_ms, hb_phase_ns=_phase(phase_ms))
+    sim, _ = compare(p, 5, LINKS, _sched(32, 2400), batch=8)
+    st = sim.stats()
+    assert st["gossip_iwant"] > 0
+    assert st["gossip_fallback_batches"] <= 1 and st["gossip_list_batches"] >= 3
