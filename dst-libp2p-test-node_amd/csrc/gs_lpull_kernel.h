@@ -276,7 +276,9 @@ __device__ __forceinline__ void glp_ihave(const LPullArgs& a, uint64_t* CW, uint
   const int lane = threadIdx.x & 63;
   const uint32_t S = a.S;
   wave_lds_sync();  // the window's entries and records are in CW
-  const uint64_t rb = a.row[w], deg = a.row[w + 1] - rb;  // the host checked deg <= GSE_HOPS
+  // batch slices: the CSR by the peer (w - soff), the senders' planes by their slice rows
+  const uint32_t soff = a.rN ? (w / a.rN) * a.rN : 0u;
+  const uint64_t rb = a.row[w - soff], deg = a.row[w - soff + 1] - rb;  // the host checked deg <= GSE_HOPS
   uint32_t vx = 0, cp = 0, tio = 0, aoff = 0;
   bool ok = false;
   if ((uint64_t)lane < deg) {
@@ -295,7 +297,7 @@ __device__ __forceinline__ void glp_ihave(const LPullArgs& a, uint64_t* CW, uint
   while (gm) {  // wave-uniform: one IHAVE sender at a time
     const int e = __builtin_ctzll(gm);
     gm &= gm - 1;
-    const uint32_t v = __builtin_amdgcn_readlane(vx, e);
+    const uint32_t v = __builtin_amdgcn_readlane(vx, e) + soff;
     const uint32_t p = __builtin_amdgcn_readlane(cp, e);
     const uint64_t ti = gR + (uint32_t)__builtin_amdgcn_readlane(tio, e);
     const uint64_t A = ti + (uint32_t)__builtin_amdgcn_readlane(aoff, e);
@@ -1407,6 +1409,7 @@ __global__ __launch_bounds__(TB) void k_gsend(LPullArgs a) {
   const uint64_t Rlo = haslo ? a.grel0 + (k - a.ghist) * a.ghb : 0;
   const uint32_t hmask = (1u << HOP_BITS) - 1;
   for (uint32_t v = blockIdx.x * PULL_WAVES + wv; v < a.N; v += gridDim.x * PULL_WAVES) {
+    const uint32_t soff = a.rN ? (v / a.rN) * a.rN : 0u;  // batch slices: the slice's first row
     uint32_t deg, x = EMPTY;
     bool nm = false;
     uint32_t* ccx = cxs[wv];  // CHN: the row's CSR entries (stage << 24 | peer) for glp_push
@@ -1416,23 +1419,23 @@ __global__ __launch_bounds__(TB) void k_gsend(LPullArgs a) {
       nm = xe != EMPTY;  // any connection may be outside the lane's epoch mesh
       x = nm ? xe & 0xFFFFFFu : EMPTY;
       deg = (uint32_t)__popcll(__ballot(nm));
-    } else {
-      const uint64_t rb = a.row[v];
-      deg = (uint32_t)(a.row[v + 1] - rb);
+    } else {  // batch slices: the CSR and the rng by the peer, per-row arrays by the slice row
+      const uint64_t rb = a.row[v - soff];
+      deg = (uint32_t)(a.row[v - soff + 1] - rb);
       if ((uint32_t)lane < deg) {
         x = a.col[rb + lane];
         nm = !(a.flags[rb + lane] & F_MESH);
       }
     }
     bool need = false;
-    if (nm) need = !((a.rowdone[x >> 5] >> (x & 31)) & 1u);
+    if (nm) need = !((a.rowdone[(x + soff) >> 5] >> ((x + soff) & 31)) & 1u);
     if (__ballot(need) == 0) {  // wave-uniform
       if (CHN && lane == 0) a.gnz[v] = 0;
       continue;
     }
     if (lane < (int)LP_FW) pl[wv][lane] = 0;
     const uint64_t nmm = __ballot(nm);
-    const uint64_t rpre = rng_pre(a.gseed, P_GOSSIP, v);
+    const uint64_t rpre = rng_pre(a.gseed, P_GOSSIP, v - soff);
     const uint32_t nonmesh = (uint32_t)__popcll(nmm);
     uint32_t r = (uint32_t)(((uint64_t)nonmesh * a.ggf) / 1000);
     if (r < a.gd_lazy) r = a.gd_lazy;
@@ -1473,7 +1476,7 @@ __global__ __launch_bounds__(TB) void k_gsend(LPullArgs a) {
       const uint32_t s = jv ? sel[wv][j0 + lane] : 0u;
       const uint32_t m = s & 0xFFFFu;  // the lane (fragment lanes: message m / FP; every fragment is
                                        // gossiped on its own, at its message's heartbeats)
-      const uint32_t h = jv ? (uint32_t)(a.habs0[m / (a.L / a.B)] + k) : 0u;
+      const uint32_t h = jv ? (uint32_t)(a.habs0[(a.rN ? (v / a.rN) * a.B : 0u) + m / (a.L / a.B)] + k) : 0u;
       uint64_t mask;
       if constexpr (CHN) {  // the targets k_cprep selected for (v, the lane's epoch)
         const uint32_t kh = a.ghoff + (uint32_t)k;

@@ -1240,7 +1240,7 @@ static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvF
     la.ghb = gos->hb;
     la.glat_min = b.lat_min;
     la.glat_max = b.lat_max;
-    la.gnf = (uint64_t)b.B * b.Fe * (N - 1);  // fragment lanes that can be final, less the publishers'
+    la.gnf = (uint64_t)(sl ? sl->S : 1u) * b.B * b.Fe * (N0 - 1);  // lanes that can be final, less the publishers'
     la.F = b.F;
     la.collide = b.collide ? 1u : 0u;
     la.gseed = c.cfg.seed;
@@ -1578,17 +1578,16 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
   // a launch has S x N rows instead of N: a pass of a few rows per resident wave
   // is mostly latency (config #2's 10k-peer F = 8 rows: 98 us per pass at 10k
   // rows, 340 us at 80k; scripts/c2_probe.py). Frozen mesh, no IDONTWANT, no
-  // per-peer traffic; lazy gossip through the eager pass's no-op proof, per slice
-  // (a group that fails it runs again as single batches). GS_SLICES=0 turns
-  // them off, GS_SLICES=n caps a group at n slices.
+  // per-peer traffic; lazy gossip through the eager pass's no-op proof, per slice,
+  // and when that fails (or failed before: glp_prefer) inside the group's passes
+  // as run_glp does, if the whole group is lockstep (else single batches take
+  // it). GS_SLICES=0 turns them off, GS_SLICES=n caps a group at n slices.
   const char* sl_env = getenv("GS_SLICES");
   const uint32_t sl_max = sl_env && *sl_env ? (uint32_t)std::max(0, atoi(sl_env)) : 64u;
   constexpr uint64_t SL_ROWS = 1ull << 19;  // rows per pass a group aims at (memory: ~S x N x L x 40 B)
   uint64_t slice_skip = 0;                  // messages before it run as single batches
   auto try_slices = [&](uint64_t i0, uint64_t& i_end) -> bool {
-    if (sl_max < 2 || !pull_any || !(variant & 64) || c.traffic || (gossip && c.glp_prefer) ||
-        (uint64_t)N * 2 >= (1u << 21))
-      return false;
+    if (sl_max < 2 || !pull_any || !(variant & 64) || c.traffic || (uint64_t)N * 2 >= (1u << 21)) return false;
     const uint32_t F0 = frags_of(c, sched[i0]), FP0 = pow2_at_least(F0);
     if (FP0 > 1 && !(variant & 128)) return false;
     const uint32_t Bc = std::min<uint32_t>(Bmax, PULL_LMAX / FP0);
@@ -1622,12 +1621,28 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     if (c.cfg.idontwant && g.payload >= c.cfg.idontwant) return false;
     const uint64_t grain = pull_grain(g.tshift);
     if (g.delta < grain) return false;
-    uint32_t lb = 0;
-    const uint32_t K = lpull_ring(c, g, g.delta / grain * grain, &lb, false, false, S * N);
-    if (!K) return false;
-    const size_t NR = (size_t)S * N;
     std::vector<uint64_t> stp((size_t)S * Bc);
     for (uint32_t j = 0; j < S; j++) std::copy(bs[j].tpub.begin(), bs[j].tpub.end(), stp.begin() + (size_t)j * Bc);
+    // lazy gossip inside the passes (the group's IHAVE / IWANT as run_glp's): every
+    // message of the group has its heartbeats at the same time after its publish
+    std::vector<uint64_t> rel(stp.size()), hab(stp.size());
+    bool lock = gossip;
+    if (gossip) {
+      const uint64_t hb = c.cfg.heartbeat_ns, ph = c.cfg.hb_phase_ns;
+      for (size_t q = 0; q < stp.size(); q++) {
+        const uint64_t tp = stp[q], h0 = tp <= ph ? 0 : (tp - ph + hb - 1) / hb;
+        rel[q] = ph + h0 * hb - tp;
+        hab[q] = h0;
+        lock = lock && rel[q] == rel[0];
+      }
+    }
+    const char* glp_env = getenv("GS_GOSSIP_LIST");
+    Batch gg = g;
+    gg.delta = std::min(g.delta, g.lat_min);
+    const bool glp_ok = lock && !(glp_env && *glp_env && atoi(glp_env) == 0) && c.max_degree <= GSE_HOPS &&
+                        gg.delta >= grain && c.cfg.heartbeat_ns > g.lat_max + gg.delta;
+    if (gossip && c.glp_prefer && !glp_ok) return false;  // single batches (the push path)
+    const size_t NR = (size_t)S * N;
     c.d_spub.alloc(spub.size());
     c.d_lpub.alloc(lpub.size());
     c.d_stpub.alloc(stp.size());
@@ -1635,83 +1650,118 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     GS_HIP(hipMemcpyAsync(c.d_lpub.p, lpub.data(), lpub.size() * 4, hipMemcpyHostToDevice, s));
     GS_HIP(hipMemcpyAsync(c.d_stpub.p, stp.data(), stp.size() * 8, hipMemcpyHostToDevice, s));
     c.d_keys.alloc(NR * g.L);
-    if (g.FP > 1) {
-      c.d_busy.alloc(NR * Bc);
-      GS_HIP(hipMemsetAsync(c.d_busy.p, 0, NR * Bc * 8, s));
-    }
-    c.keys_log = false;
-    if (gossip) GS_HIP(hipMemcpyAsync(c.d_cnt_save.p, c.d_counters.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));
+    if (g.FP > 1) c.d_busy.alloc(NR * Bc);
+    auto fresh = [&] {  // per-run state of the group's pass
+      c.keys_log = false;
+      if (g.FP > 1) GS_HIP(hipMemsetAsync(c.d_busy.p, 0, NR * Bc * 8, s));
+    };
     const SinkWants sw = sink_wants(sink);
     const bool dense = sw.rows() || sw.summary || getenv("GS_LPULL_DENSE");
+    const bool wants = sw.rows() || sw.lat || sw.summary;
     const Slices sl{S, N, c.d_spub.p, c.d_lpub.p};
-    if (!run_lpull_batch(c, g, K, lb, ev, n_ev, dev_cus, dense, false, nullptr, nullptr, &sl))
-      return false;  // (a list overflowed: counters restored; single batches take the messages)
-    c.stats.list_pull_batches += S - 1;
     auto slice_in = [&](uint32_t j) {  // slice j's publishers and publish times where completion reads them
       GS_HIP(hipMemcpyAsync(c.d_pub.p, lpub.data() + (size_t)j * Bc, Bc * 4, hipMemcpyHostToDevice, s));
       GS_HIP(hipMemcpyAsync(c.d_tpub.p, bs[j].tpub.data(), Bc * 8, hipMemcpyHostToDevice, s));
     };
-    const bool wants = sw.rows() || sw.lat || sw.summary;
-    if (gossip) {  // the eager result stands only if gossip is a no-op in every slice
-      // every slice's reductions into one pinned buffer, one wait
-      const size_t msb = (size_t)S * Bc * MS_COLS * 8;
-      if (c.h_slms_bytes < msb) {
-        if (c.h_slms) GS_HIP(hipHostFree(c.h_slms));
-        c.h_slms = nullptr;
-        c.h_slms_bytes = 0;
-        GS_HIP(hipHostMalloc((void**)&c.h_slms, msb, hipHostMallocDefault));
-        c.h_slms_bytes = msb;
-      }
-      if (c.keys_log) {  // every slice in one launch
-        run_complete(c, bs[0], 0, N, true, false, false, false, 0, c.d_lpub.p, c.d_stpub.p, S);
-        GS_HIP(hipMemcpyAsync(c.h_slms, c.d_mstat.p, msb, hipMemcpyDeviceToHost, s));
+    auto finish = [&] {  // completion of a group whose keys stand
+      if (!wants) {  // device-resident results: the counters only
+        if (c.keys_log) run_complete(c, bs[0], 0, N, false, false, false, false, 0, c.d_lpub.p, c.d_stpub.p, S);
+        else
+          for (uint32_t j = 0; j < S; j++)
+            run_complete(c, bs[j], 0, N, false, false, false, false, (size_t)j * N, c.d_lpub.p + (size_t)j * Bc,
+                         c.d_stpub.p + (size_t)j * Bc);
       } else {
-        for (uint32_t j = 0; j < S; j++) {
-          run_complete(c, bs[j], 0, N, true, false, false, false, (size_t)j * N, c.d_lpub.p + (size_t)j * Bc,
-                       c.d_stpub.p + (size_t)j * Bc);
-          GS_HIP(hipMemcpyAsync(c.h_slms + (size_t)j * Bc * MS_COLS, c.d_mstat.p, (size_t)Bc * MS_COLS * 8,
-                                hipMemcpyDeviceToHost, s));
-        }
-      }
-      GS_HIP(hipStreamSynchronize(s));
-      std::vector<uint64_t> r0(Bc);
-      const uint64_t hb = c.cfg.heartbeat_ns, ph = c.cfg.hb_phase_ns;
-      bool noop = true;
-      for (uint32_t j = 0; j < S && noop; j++) {
-        for (uint32_t q = 0; q < Bc; q++) {
-          const uint64_t tp = bs[j].tpub[q], h0 = tp <= ph ? 0 : (tp - ph + hb - 1) / hb;
-          r0[q] = ph + h0 * hb - tp;
-        }
-        noop = gossip_noop(bs[j], c.h_slms + (size_t)j * Bc * MS_COLS, r0);
-      }
-      if (!noop) {  // discard the group; its batches run one by one (eager + proof, then the gossip paths)
-        GS_HIP(hipMemcpyAsync(c.d_counters.p, c.d_cnt_save.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));
-        c.stats.list_pull_batches -= S;
-        return false;
-      }
-      c.stats.gossip_noop_msgs += (uint64_t)S * Bc;
-      if (wants) {  // the sink's results: completion again per slice, its counters not counted twice
-        c.d_cnt_save2.alloc(C_COUNT);
-        GS_HIP(hipMemcpyAsync(c.d_cnt_save2.p, c.d_counters.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));
         for (uint32_t j = 0; j < S; j++) {
           slice_in(j);
           launch_complete(c, bs[j], 0, N, sink, i0 + (uint64_t)j * Bc, (size_t)j * N);
         }
-        GS_HIP(hipMemcpyAsync(c.d_counters.p, c.d_cnt_save2.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));
       }
-    } else if (!wants) {  // device-resident results: the counters only
-      if (c.keys_log) run_complete(c, bs[0], 0, N, false, false, false, false, 0, c.d_lpub.p, c.d_stpub.p, S);
-      else
-        for (uint32_t j = 0; j < S; j++)
-          run_complete(c, bs[j], 0, N, false, false, false, false, (size_t)j * N, c.d_lpub.p + (size_t)j * Bc,
-                       c.d_stpub.p + (size_t)j * Bc);
+    };
+    auto run_glp_group = [&]() -> bool {  // the gossip inside the group's passes
+      uint32_t lbg = 0;
+      const uint32_t Kg = lpull_ring(c, gg, gg.delta / grain * grain, &lbg, true, false, S * N);
+      if (!Kg) return false;
+      fresh();
+      c.d_habs0.alloc(std::max<size_t>(Bmax, hab.size()));
+      GS_HIP(hipMemcpyAsync(c.d_habs0.p, hab.data(), hab.size() * 8, hipMemcpyHostToDevice, s));
+      const GosRun gr{rel[0], c.cfg.heartbeat_ns};
+      const uint64_t iw0 = read_counter(c, C_GOSSIP);
+      if (!run_lpull_batch(c, gg, Kg, lbg, ev, n_ev, dev_cus, dense, false, &gr, nullptr, &sl)) return false;
+      c.stats.list_pull_batches += S - 1;
+      c.stats.gossip_list_batches += S;
+      if (read_counter(c, C_GOSSIP) != iw0) c.glp_quiet = 0;  // (run_glp's rule, per batch of the group)
+      else if ((c.glp_quiet += S) >= GLP_QUIET) c.glp_prefer = false;
+      finish();
+      return true;
+    };
+    bool ok = false;
+    if (gossip && c.glp_prefer) {
+      ok = run_glp_group();
     } else {
-      for (uint32_t j = 0; j < S; j++) {
-        slice_in(j);
-        launch_complete(c, bs[j], 0, N, sink, i0 + (uint64_t)j * Bc, (size_t)j * N);
+      uint32_t lb = 0;
+      const uint32_t K = lpull_ring(c, g, g.delta / grain * grain, &lb, false, false, S * N);
+      if (!K) return false;
+      fresh();
+      if (gossip) GS_HIP(hipMemcpyAsync(c.d_cnt_save.p, c.d_counters.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));
+      if (!run_lpull_batch(c, g, K, lb, ev, n_ev, dev_cus, dense, false, nullptr, nullptr, &sl))
+        return false;  // (a list overflowed: counters restored; single batches take the messages)
+      c.stats.list_pull_batches += S - 1;
+      if (!gossip) {
+        finish();
+        ok = true;
+      } else {  // the eager result stands only if gossip is a no-op in every slice
+        // every slice's reductions into one pinned buffer, one wait
+        const size_t msb = (size_t)S * Bc * MS_COLS * 8;
+        if (c.h_slms_bytes < msb) {
+          if (c.h_slms) GS_HIP(hipHostFree(c.h_slms));
+          c.h_slms = nullptr;
+          c.h_slms_bytes = 0;
+          GS_HIP(hipHostMalloc((void**)&c.h_slms, msb, hipHostMallocDefault));
+          c.h_slms_bytes = msb;
+        }
+        if (c.keys_log) {  // every slice in one launch
+          run_complete(c, bs[0], 0, N, true, false, false, false, 0, c.d_lpub.p, c.d_stpub.p, S);
+          GS_HIP(hipMemcpyAsync(c.h_slms, c.d_mstat.p, msb, hipMemcpyDeviceToHost, s));
+        } else {
+          for (uint32_t j = 0; j < S; j++) {
+            run_complete(c, bs[j], 0, N, true, false, false, false, (size_t)j * N, c.d_lpub.p + (size_t)j * Bc,
+                         c.d_stpub.p + (size_t)j * Bc);
+            GS_HIP(hipMemcpyAsync(c.h_slms + (size_t)j * Bc * MS_COLS, c.d_mstat.p, (size_t)Bc * MS_COLS * 8,
+                                  hipMemcpyDeviceToHost, s));
+          }
+        }
+        GS_HIP(hipStreamSynchronize(s));
+        bool noop = true;
+        for (uint32_t j = 0; j < S && noop; j++) {
+          const std::vector<uint64_t> r0(rel.begin() + (size_t)j * Bc, rel.begin() + (size_t)(j + 1) * Bc);
+          noop = gossip_noop(bs[j], c.h_slms + (size_t)j * Bc * MS_COLS, r0);
+        }
+        if (noop) {
+          c.stats.gossip_noop_msgs += (uint64_t)S * Bc;
+          if (wants) {  // the sink's results: completion again per slice, its counters not counted twice
+            c.d_cnt_save2.alloc(C_COUNT);
+            GS_HIP(hipMemcpyAsync(c.d_cnt_save2.p, c.d_counters.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));
+            for (uint32_t j = 0; j < S; j++) {
+              slice_in(j);
+              launch_complete(c, bs[j], 0, N, sink, i0 + (uint64_t)j * Bc, (size_t)j * N);
+            }
+            GS_HIP(hipMemcpyAsync(c.d_counters.p, c.d_cnt_save2.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));
+          }
+          ok = true;
+        } else {  // gossip changes the group: discard the eager run; the gossip inside the passes takes it
+          GS_HIP(hipMemcpyAsync(c.d_counters.p, c.d_cnt_save.p, C_COUNT * 8, hipMemcpyDeviceToDevice, s));
+          c.stats.list_pull_batches -= S;
+          if (glp_ok) {  // (without the in-pass gossip the single batches take it: they count their own)
+            c.stats.gossip_fallback_batches++;
+            c.glp_prefer = true;
+            c.glp_quiet = 0;
+            ok = run_glp_group();
+          }
+        }
       }
     }
-    GS_HIP(hipStreamSynchronize(s));  // (lpub / tpub host copies die here)
+    if (!ok) return false;
+    GS_HIP(hipStreamSynchronize(s));  // (lpub / tpub / habs0 host copies die here)
     c.stats.messages += (uint64_t)S * Bc;
     c.stats.batches += S;
     i_end = i0 + (uint64_t)S * Bc;

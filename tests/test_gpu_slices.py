@@ -90,9 +90,9 @@ def test_slices_against_oracle(monkeypatch, frags):
 
 def test_slices_gossip_phase_falls_back_exactly(monkeypatch):
     """Heartbeats 120 ms after every publish: IWANTs change the result, the
-    group's no-op proof fails, its batches re-run one by one (the in-pass
-    gossip path takes them) — still the oracle's result, and the discarded
-    group counts nothing."""
+    group's no-op proof fails and the group runs again with the IHAVE / IWANT
+    inside its passes — still the oracle's result; the discarded eager run
+    counts once as a fallback."""
     monkeypatch.setenv("GS_SLICES", "")
     p = oracle.params(peers=1200, seed=330, hb_phase_ns=(T0 + 120_000_000) % HB)
     sim, _ = compare(p, 5, LINKS, _sched(32, 1200), batch=8)
@@ -134,3 +134,29 @@ def test_fragment_groups_complete_from_logs(monkeypatch, frags, slices):
         assert out[""][1][k] == out["1"][1][k], k
         assert out[""][2][k] == out["1"][2][k], k
     assert out[""][2]["gossip_noop_msgs"] == 64
+
+
+@pytest.mark.parametrize("frags,phase_ms", [(1, 55), (1, 30), (4, 120)])
+def test_slices_gossip_active_equal_single_batches(monkeypatch, frags, phase_ms):
+    """Gossip-active groups (the in-pass IHAVE / IWANT over slice rows: CSR and
+    rng by the peer, planes and row-done bits by the slice row, each slice's
+    heartbeat indices) equal the same batches run one at a time."""
+    p = oracle.params(peers=1400, seed=350 + phase_ms, fragments=frags, hb_phase_ns=(T0 + phase_ms * 1_000_000) % HB)
+    sched = _sched(96, 1400)
+    a, sa = _run(monkeypatch, "", p, sched, 16, "rows")
+    b, sb = _run(monkeypatch, "0", p, sched, 16, "rows")
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    # (which batches take the in-pass gossip may differ: a single batch can prove its gossip a no-op)
+    for k in ("deliveries", "frag_deliveries", "relaxations", "latency_sum_ms", "latency_max_ms", "messages",
+              "batches", "gossip_iwant"):
+        assert sa[k] == sb[k], k
+    assert sa["gossip_iwant"] > 0 and sa["gossip_list_batches"] >= 5
+
+
+def test_slices_gossip_active_against_oracle(monkeypatch):
+    monkeypatch.setenv("GS_SLICES", "")
+    p = oracle.params(peers=1100, seed=360, fragments=2, hb_phase_ns=(T0 + 90_000_000) % HB)
+    sim, _ = compare(p, 5, LINKS, _sched(40, 1100), batch=8)
+    st = sim.stats()
+    assert st["gossip_iwant"] > 0 and st["gossip_list_batches"] == 5
