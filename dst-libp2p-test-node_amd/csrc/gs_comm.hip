@@ -436,6 +436,10 @@ bool run_batch_lp(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched,
   const PartLayout lay{P, N, B};
   const size_t RB = 8;  // bytes per record
   std::vector<uint64_t> st((size_t)P * 4);  // per part: mode, records, min pending, error word
+  // the record exchange: routed per destination part (GS_PART_ROUTE=1; at most
+  // PART_ROUTE_PMAX parts), or every part's records to every part (the default)
+  const char* rte = getenv("GS_PART_ROUTE");
+  const bool routed = P <= PART_ROUTE_PMAX && rte && *rte && atoi(rte) != 0;
   for (;;) {
     for (uint32_t i = 0; i < nctx; i++) {
       GS_HIP(hipSetDevice(cx[i]->cfg.device));
@@ -472,9 +476,75 @@ bool run_batch_lp(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched,
       part_lp_set(*cx[i], recs, minp);
     }
     if (!recs) continue;  // the next pass emits a window: it reads no records
-    // pack (each part knows its offset in the packed records of all parts)
     std::vector<uint64_t> base(P + 1, 0), cnt(P);
     for (uint32_t p = 0; p < P; p++) cnt[p] = st[(size_t)p * 4 + 1];
+    if (routed) {  // each part receives only the records with a receiver it owns (gs_layout.h lp_route_bases)
+      std::vector<uint64_t> route((size_t)P * P), bq(P);
+      for (uint32_t i = 0; i < nctx; i++) {
+        const uint32_t me = cm->local ? i : cm->rank;
+        GS_HIP(hipSetDevice(cx[i]->cfg.device));
+        cx[i]->d_rpk.alloc(recs);
+        part_lp_pack_route(*cx[i], P, me, cnt[me]);
+      }
+      if (cm->local) {
+        for (uint32_t i = 0; i < nctx; i++) {
+          GS_HIP(hipSetDevice(cx[i]->cfg.device));
+          part_lp_route_read(*cx[i], P, &route[(size_t)i * P]);  // (every pack done)
+        }
+        for (uint32_t q = 0; q < nctx; q++) {
+          Ctx& d = *cx[q];
+          GS_HIP(hipSetDevice(d.cfg.device));
+          lp_route_bases(route.data(), P, q, bq.data());
+          for (uint32_t p = 0; p < nctx; p++) {
+            if (p == q) continue;
+            Ctx& src = *cx[p];
+            const uint64_t n = route[(size_t)p * P + q], cap = std::max<uint64_t>(cnt[p], 1);
+            const uint32_t u0 = lay.u0(p), un = lay.un(p);
+            if (n) GS_HIP(hipMemcpyAsync(d.d_rpk.p + bq[p], src.d_rsend.p + (size_t)q * cap, n * RB,
+                                         hipMemcpyDeviceToDevice, d.stream));
+            GS_HIP(hipMemcpyAsync(d.d_rcg.p + u0, src.d_rrcg.p + (size_t)q * un, un * 4, hipMemcpyDeviceToDevice,
+                                  d.stream));
+            GS_HIP(hipMemcpyAsync(d.d_roffg.p + u0, src.d_rroff.p + (size_t)q * un, un * 8, hipMemcpyDeviceToDevice,
+                                  d.stream));
+          }
+          part_lp_route_fix(d, P, q, bq.data());
+        }
+        for (uint32_t q = 0; q < nctx; q++) GS_HIP(hipStreamSynchronize(cx[q]->stream));  // sources reused next pass
+      } else {
+        Ctx& c = *cx[0];
+        const uint32_t me = cm->rank;
+        GS_NCCL(r->AllGather(c.d_pkcur.p, cm->d_scratch, P, ncclUint64, cm->nc, c.stream));  // row p: p's counts
+        GS_HIP(hipMemcpyAsync(route.data(), cm->d_scratch, (size_t)P * P * 8, hipMemcpyDeviceToHost, c.stream));
+        GS_HIP(hipStreamSynchronize(c.stream));
+        lp_route_bases(route.data(), P, me, bq.data());
+        const uint64_t piece = std::max<uint64_t>(1, rccl_piece_bytes() / RB);
+        const uint64_t mycap = std::max<uint64_t>(cnt[me], 1);
+        const uint32_t myun = lay.un(me);
+        GS_NCCL(r->GroupStart());
+        for (uint32_t d = 0; d < P; d++) {
+          if (d == me) continue;
+          const uint64_t n = route[(size_t)me * P + d];
+          const uint64_t* src = c.d_rsend.p + (size_t)d * mycap;
+          for (uint64_t k = 0; k < n; k += piece)
+            GS_NCCL(r->Send(src + k, std::min(piece, n - k), ncclUint64, (int)d, cm->nc, c.stream));
+          GS_NCCL(r->Send(c.d_rrcg.p + (size_t)d * myun, myun, ncclUint32, (int)d, cm->nc, c.stream));
+          GS_NCCL(r->Send(c.d_rroff.p + (size_t)d * myun, myun, ncclUint64, (int)d, cm->nc, c.stream));
+        }
+        for (uint32_t sr = 0; sr < P; sr++) {
+          if (sr == me) continue;
+          const uint64_t n = route[(size_t)sr * P + me];
+          const uint32_t u0 = lay.u0(sr), un = lay.un(sr);
+          for (uint64_t k = 0; k < n; k += piece)
+            GS_NCCL(r->Recv(c.d_rpk.p + bq[sr] + k, std::min(piece, n - k), ncclUint64, (int)sr, cm->nc, c.stream));
+          GS_NCCL(r->Recv(c.d_rcg.p + u0, un, ncclUint32, (int)sr, cm->nc, c.stream));
+          GS_NCCL(r->Recv(c.d_roffg.p + u0, un, ncclUint64, (int)sr, cm->nc, c.stream));
+        }
+        GS_NCCL(r->GroupEnd());
+        part_lp_route_fix(c, P, me, bq.data());
+      }
+      continue;
+    }
+    // gathered: every part's whole record range to every part
     lp_bases(cnt.data(), P, base.data());
     for (uint32_t i = 0; i < nctx; i++) {
       const uint32_t me = cm->local ? i : cm->rank;

@@ -250,7 +250,12 @@ struct Ctx {
   DevBuf<uint32_t> d_rcg;    // [N] records per peer (global ids)
   DevBuf<uint64_t> d_roffg;  // [N] their offsets in d_rpk
   DevBuf<uint64_t> d_rpk;    // every part's records of the last pass
-  DevBuf<uint64_t> d_pkcur;  // pack cursor
+  DevBuf<uint64_t> d_pkcur;  // pack cursor (routed: one per destination part)
+  // routed exchange (k_lpack_route): the records for each other part [P][cap] and
+  // this part's per-peer offsets / counts for each destination [P][un]
+  DevBuf<uint64_t> d_rsend;
+  DevBuf<uint64_t> d_rroff;
+  DevBuf<uint32_t> d_rrcg;
   // lazy gossip inside the list pass (gs_lpull_kernel.h, GOS batches)
   DevBuf<uint32_t> d_gpl;      // [N][32] sender planes of the built heartbeat
   DevBuf<uint64_t> d_gse;      // [N][L] their entries
@@ -315,6 +320,9 @@ void part_lp_pass(Ctx& c);
 void part_lp_read(Ctx& c, uint64_t out[4]);  // last pass: mode, records, min pending, error word
 void part_lp_set(Ctx& c, uint64_t records, uint64_t minp);  // the combined values into the last pass's slot
 void part_lp_pack(Ctx& c, uint64_t base, uint64_t mine);
+void part_lp_pack_route(Ctx& c, uint32_t P, uint32_t me, uint64_t mine);
+void part_lp_route_read(Ctx& c, uint32_t P, uint64_t* counts);
+void part_lp_route_fix(Ctx& c, uint32_t P, uint32_t me, const uint64_t* base);
 bool part_lp_end(Ctx& c, const gs_result_sink* sink);  // completion (final logs or dense rows), gossip proof
 void part_lp_abort(Ctx& c);
 

@@ -1797,6 +1797,155 @@ __global__ __launch_bounds__(TB) void k_lpack(const uint64_t* __restrict__ rec, 
   }
 }
 
+// Routed record packing (gs_run_partitioned's default exchange, DESIGN.md
+// §5.2; gs_layout.h lp_route_bases): this part's records of a pass, for every
+// destination part q the records with a receiver q owns (a bit of the
+// record's inclusion mask at a mesh position whose peer is in q; the own part
+// gets every record), each row's records contiguous and in emission order.
+// Pass 1 counts per (row, destination); one claim per wave and destination
+// reserves the space (cursor[q]); pass 2 copies. Own part: into the gathered
+// buffer at base 0 (out_own) with the global offset tables at its peers
+// (roff_own / rcg_own); other parts: out[q * cap ..] with per-destination
+// tables roff[q * un + r] (relative to the segment) / rcg[q * un + r]. One
+// wave per 64 rows, P <= LP_PMAX.
+constexpr uint32_t LP_PMAX = 16;
+__global__ __launch_bounds__(TB) void k_lpack_route(const uint64_t* __restrict__ rec, const uint32_t* __restrict__ cnt,
+                                                    const uint32_t* __restrict__ mesh, uint32_t u0, uint32_t un,
+                                                    uint32_t L, uint32_t N, uint32_t P, uint32_t me, uint64_t cap,
+                                                    uint64_t* __restrict__ out, uint64_t* __restrict__ out_own,
+                                                    uint64_t* __restrict__ roff, uint32_t* __restrict__ rcg,
+                                                    uint64_t* __restrict__ roff_own, uint32_t* __restrict__ rcg_own,
+                                                    unsigned long long* cursor) {
+  __shared__ uint32_t smq[TB / 64][64][LP_PMAX];  // per row: the inclusion-mask bits of each part's receivers
+  __shared__ uint32_t sco[TB / 64][64][LP_PMAX];  // per row and destination: count, then next write position
+  __shared__ uint32_t spre[TB / 64][65];          // exclusive prefix of the rows' record counts
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t wave = blockIdx.x * (TB / 64) + wv, nw = gridDim.x * (TB / 64);
+  constexpr uint32_t IM = ((1u << MESH_W) - 1u) << LP_IM_SHIFT;
+  for (uint32_t r0 = wave * 64; r0 < un; r0 += nw * 64) {
+    // lane j: row r0 + j — its record count, and each part's receivers as mask bits
+    const uint32_t r = r0 + (uint32_t)lane;
+    const bool rv = r < un;
+    const uint32_t n = rv ? cnt[r] : 0u;
+    uint32_t e[MESH_W];
+    {
+      const uint4* mp = reinterpret_cast<const uint4*>(mesh + (size_t)(u0 + (rv ? r : 0u)) * MESH_W);
+#pragma unroll
+      for (int k = 0; k < (int)MESH_W / 4; k++) {
+        const uint4 m = rv ? mp[k] : make_uint4(EMPTY, EMPTY, EMPTY, EMPTY);
+        e[4 * k] = m.x; e[4 * k + 1] = m.y; e[4 * k + 2] = m.z; e[4 * k + 3] = m.w;
+      }
+    }
+    for (uint32_t q = 0; q < P; q++) {
+      uint32_t m = 0;
+#pragma unroll
+      for (int k = 0; k < (int)MESH_W; k++) {
+        const uint32_t pe = e[k] == EMPTY ? ~0u : (uint32_t)((((uint64_t)(e[k] & 0xFFFFFFu) + 1) * P - 1) / N);
+        m |= pe == q ? 1u << (LP_IM_SHIFT + k) : 0u;
+      }
+      smq[wv][lane][q] = m;
+      sco[wv][lane][q] = 0;
+    }
+    uint32_t x = n;  // inclusive prefix over the 64 rows
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = __shfl_up(x, off);
+      if (lane >= off) x += y;
+    }
+    spre[wv][lane] = x - n;
+    const uint32_t T = __shfl(x, 63);
+    if (lane == 63) spre[wv][64] = T;
+    wave_lds_sync();
+    // the records of the 64 rows as one sequence, 64 at a time: lane -> (row, index)
+    auto locate = [&](uint32_t t, uint32_t& j) {  // the row holding sequence position t (largest pre <= t)
+      uint32_t lo = 0, hi = 63;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (spre[wv][mid] <= t) lo = mid; else hi = mid - 1;
+      }
+      j = lo;
+    };
+    // 1. counts per (row, destination)
+    for (uint32_t t0 = 0; t0 < T; t0 += 64) {
+      const uint32_t t = t0 + (uint32_t)lane;
+      if (t < T) {
+        uint32_t j;
+        locate(t, j);
+        const uint32_t im = (uint32_t)rec[(size_t)(r0 + j) * L + (t - spre[wv][j])] & IM;
+        for (uint32_t q = 0; q < P; q++)
+          if (q == me || (im & smq[wv][j][q])) atomicAdd(&sco[wv][j][q], 1u);
+      }
+    }
+    wave_lds_sync();
+    // 2. offsets: one claim per destination; sco becomes each (row, destination)'s write position
+    for (uint32_t q = 0; q < P; q++) {
+      const uint32_t c = sco[wv][lane][q];
+      uint32_t y = c;
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t z = __shfl_up(y, off);
+        if (lane >= off) y += z;
+      }
+      const uint32_t tot = __shfl(y, 63);
+      unsigned long long b0 = 0;
+      if (lane == 0 && tot) b0 = atomicAdd(&cursor[q], (unsigned long long)tot);
+      const uint64_t off = (((uint64_t)__shfl((uint32_t)(b0 >> 32), 0) << 32) | __shfl((uint32_t)b0, 0)) + y - c;
+      sco[wv][lane][q] = (uint32_t)off;  // (< cap < 2^32)
+      if (rv) {
+        if (q == me) {
+          roff_own[r] = off;
+          rcg_own[r] = c;
+        } else {
+          roff[(size_t)q * un + r] = off;
+          rcg[(size_t)q * un + r] = c;
+        }
+      }
+    }
+    wave_lds_sync();
+    // 3. copy in emission order: within a chunk a row's records are a run of
+    //    lanes [s, e); the lanes of that run before this one, for destination q,
+    //    come first; the run's last lane advances the row's position
+    for (uint32_t t0 = 0; t0 < T; t0 += 64) {
+      const uint32_t t = t0 + (uint32_t)lane;
+      const bool v = t < T;
+      uint32_t j = 0, im = 0;
+      uint64_t xr = 0;
+      if (v) {
+        locate(t, j);
+        xr = rec[(size_t)(r0 + j) * L + (t - spre[wv][j])];
+        im = (uint32_t)xr & IM;
+      }
+      const uint32_t s0 = spre[wv][j] > t0 ? spre[wv][j] - t0 : 0u;             // the run's first lane
+      const uint32_t e0 = spre[wv][j + 1] - t0 < 64 ? spre[wv][j + 1] - t0 : 64u;  // one past its last
+      const uint64_t below = ((1ull << lane) - 1) & ~((1ull << s0) - 1);
+      for (uint32_t q = 0; q < P; q++) {
+        const bool sel = v && (q == me || (im & smq[wv][j][q]));
+        const uint64_t bm = __ballot(sel);
+        const uint32_t base = v ? sco[wv][j][q] : 0u;
+        if (sel) (q == me ? out_own : out + (size_t)q * cap)[(uint64_t)base + (uint32_t)__popcll(bm & below)] = xr;
+        wave_lds_sync();  // (every lane read the position before the run's last lane moves it)
+        if (v && (uint32_t)lane + 1 == e0) {
+          const uint64_t run = e0 >= 64 ? ~0ull & ~((1ull << s0) - 1) : ((1ull << e0) - 1) & ~((1ull << s0) - 1);
+          sco[wv][j][q] = base + (uint32_t)__popcll(bm & run);
+        }
+        wave_lds_sync();
+      }
+    }
+    wave_lds_sync();
+  }
+}
+
+// The receiver's offsets of the routed records: a foreign peer's offset is
+// relative to its part's segment; add the segment's base in the gathered buffer.
+struct RouteBases {
+  uint64_t b[LP_PMAX];
+};
+__global__ __launch_bounds__(TB) void k_roff_fix(uint64_t* __restrict__ roff, uint32_t N, uint32_t P, uint32_t me,
+                                                 RouteBases rb) {
+  const uint32_t x = blockIdx.x * TB + threadIdx.x;
+  if (x >= N) return;
+  const uint32_t p = (uint32_t)((((uint64_t)x + 1) * P - 1) / N);  // gs_layout.h part_of
+  if (p != me) roff[x] += rb.b[p];
+}
+
 void lpull_dispatch_part(uint32_t FP, const LPullArgs& a, unsigned grid, hipStream_t s) {
   const bool ch8 = lpull_chunks(a.L) == 8;
 #define GS_LPP(F)                                                      \

@@ -775,6 +775,44 @@ void part_lp_pack(Ctx& c, uint64_t base, uint64_t mine) {
   GS_HIP(hipGetLastError());
 }
 
+// Routed pack (k_lpack_route): this part's records of the last pass for each
+// destination part (own: into d_rpk at base 0, with the global offset tables
+// at its peers; others: d_rsend[q * mine] with the tables d_rroff / d_rrcg[q * un]).
+void part_lp_pack_route(Ctx& c, uint32_t P, uint32_t me, uint64_t mine) {
+  const uint32_t un = c.part_un, L = c.part_b.L;
+  hipStream_t s = c.stream;
+  const uint64_t cap = std::max<uint64_t>(mine, 1);
+  c.d_pkcur.alloc(P);
+  c.d_rsend.alloc((size_t)P * cap);
+  c.d_rroff.alloc((size_t)P * un);
+  c.d_rrcg.alloc((size_t)P * un);
+  GS_HIP(hipMemsetAsync(c.d_pkcur.p, 0, (size_t)P * 8, s));
+  const uint32_t nb = (c.part_lppass + 1) & 1;  // the last pass wrote lrec / lcnt [pass & 1]
+  const unsigned grid = (unsigned)std::max<uint64_t>(
+      1, std::min<uint64_t>(((uint64_t)un + 255) / 256, (uint64_t)c.num_cus * 8));
+  k_lpack_route<<<grid, TB, 0, s>>>(c.d_lrec.p + (size_t)nb * un * L, c.d_lcnt.p + (size_t)nb * un, c.d_mesh.p,
+                                    c.part_u0, un, L, c.cfg.peers, P, me, cap, c.d_rsend.p, c.d_rpk.p, c.d_rroff.p,
+                                    c.d_rrcg.p, c.d_roffg.p + c.part_u0, c.d_rcg.p + c.part_u0,
+                                    (unsigned long long*)c.d_pkcur.p);
+  GS_HIP(hipGetLastError());
+}
+
+// The routed records per destination (counts[q]) of the last pack.
+void part_lp_route_read(Ctx& c, uint32_t P, uint64_t* counts) {
+  GS_HIP(hipMemcpyAsync(c.h_pinned, c.d_pkcur.p, (size_t)P * 8, hipMemcpyDeviceToHost, c.stream));
+  GS_HIP(hipStreamSynchronize(c.stream));
+  memcpy(counts, c.h_pinned, (size_t)P * 8);
+}
+
+// After the routed exchange: the foreign peers' offsets by their segment's base.
+void part_lp_route_fix(Ctx& c, uint32_t P, uint32_t me, const uint64_t* base) {
+  RouteBases rb{};
+  for (uint32_t p = 0; p < P; p++) rb.b[p] = base[p];
+  k_roff_fix<<<(unsigned)(((uint64_t)c.cfg.peers + TB - 1) / TB), TB, 0, c.stream>>>(c.d_roffg.p, c.cfg.peers, P, me,
+                                                                                       rb);
+  GS_HIP(hipGetLastError());
+}
+
 // As gs_run's list pass: completion reads the final logs (k_lcomplete) unless
 // the sink takes rows or a summary, or the rows hold fragment groups (k_lfinal
 // -> dense rows -> k_complete).

@@ -559,6 +559,106 @@ int main() {
 }
 """
 
+ROUTE_CHECK = r"""
+#include <cstdio>
+#include <vector>
+#include <random>
+#include "gs_layout.h"
+using namespace gs;
+// The routed list-pass exchange simulated on the CPU: random mesh rows (<= 16
+// entries, ids of any part), each row's records with random inclusion masks;
+// sender p packs, per destination q, the records with a receiver in q (q = p:
+// all) with per-peer offsets relative to the segment; receiver q lays the
+// segments out by lp_route_bases and adds base[p] to p's offsets. Every
+// receiver must then read, for each mesh neighbour, exactly the neighbour's
+// records that include it, in emission order (what k_lpull<.., PART> reads).
+int main() {
+  std::mt19937_64 rng(7);
+  unsigned long long checks = 0;
+  const uint32_t Ns[] = {5, 37, 1000, 3001};
+  for (uint32_t P = 1; P <= 16; P++)
+    for (uint32_t N : Ns) {
+      if (P > N) continue;
+      const PartLayout L{P, N, 1};
+      for (uint32_t p = 0; p < P; p++)
+        for (uint32_t x = L.u0(p); x < L.u0(p + 1); x++)
+          if (L.part_of(x) != p) { printf("part_of P=%u N=%u x=%u\n", P, N, x); return 1; }
+      std::vector<std::vector<uint32_t>> mesh(N);
+      std::vector<std::vector<uint32_t>> recs(N);  // record = emission index << 16 | inclusion mask
+      for (uint32_t u = 0; u < N; u++) {
+        const uint32_t d = (uint32_t)(rng() % 17);
+        for (uint32_t k = 0; k < d; k++) mesh[u].push_back((uint32_t)(rng() % N));
+        const uint32_t n = (uint32_t)(rng() % 9);
+        for (uint32_t i = 0; i < n; i++) recs[u].push_back((i << 16) | (uint32_t)(rng() & ((1u << d) - 1)));
+      }
+      // sender side
+      std::vector<std::vector<std::vector<uint32_t>>> seg(P, std::vector<std::vector<uint32_t>>(P));
+      std::vector<std::vector<uint64_t>> roff(P, std::vector<uint64_t>(N)), rcg(P, std::vector<uint64_t>(N));
+      std::vector<uint64_t> route((size_t)P * P);
+      for (uint32_t p = 0; p < P; p++)
+        for (uint32_t q = 0; q < P; q++) {
+          uint32_t mq = 0;
+          for (uint32_t u = L.u0(p); u < L.u0(p + 1); u++) {
+            mq = 0;
+            for (uint32_t k = 0; k < mesh[u].size(); k++) mq |= L.part_of(mesh[u][k]) == q ? 1u << k : 0u;
+            roff[q][u] = seg[p][q].size();  // (tables per destination; u is p's own peer)
+            for (uint32_t r : recs[u])
+              if (q == p || (r & 0xFFFFu & mq)) seg[p][q].push_back(r);
+            rcg[q][u] = seg[p][q].size() - roff[q][u];
+          }
+          route[(size_t)p * P + q] = seg[p][q].size();
+        }
+      // receiver side
+      for (uint32_t q = 0; q < P; q++) {
+        std::vector<uint64_t> base(P);
+        const uint64_t tot = lp_route_bases(route.data(), P, q, base.data());
+        std::vector<uint32_t> buf(tot, ~0u);
+        std::vector<uint64_t> groff(N), grcg(N);
+        for (uint32_t p = 0; p < P; p++) {
+          for (size_t k = 0; k < seg[p][q].size(); k++) buf[base[p] + k] = seg[p][q][k];
+          for (uint32_t u = L.u0(p); u < L.u0(p + 1); u++) {
+            groff[u] = roff[q][u] + base[p];
+            grcg[u] = rcg[q][u];
+          }
+        }
+        for (uint32_t x : buf)
+          if (x == ~0u) { puts("hole"); return 1; }
+        for (uint32_t w = L.u0(q); w < L.u0(q + 1); w++)  // every own receiver w and neighbour entry
+          for (uint32_t v = 0; v < N; v++)
+            for (uint32_t k = 0; k < mesh[v].size(); k++) {
+              if (mesh[v][k] != w) continue;
+              std::vector<uint32_t> want, got;
+              for (uint32_t r : recs[v])
+                if ((r >> k) & 1u) want.push_back(r);
+              for (uint64_t i = 0; i < grcg[v]; i++)
+                if ((buf[groff[v] + i] >> k) & 1u) got.push_back(buf[groff[v] + i]);
+              if (want != got) { printf("route P=%u N=%u q=%u w=%u v=%u\n", P, N, q, w, v); return 1; }
+              checks++;
+            }
+      }
+    }
+  printf("ok %llu\n", checks);
+  return 0;
+}
+"""
+
+
+def test_partition_routed_record_exchange(tmp_path):
+    """The routed list-pass record exchange (csrc/gs_layout.h part_of /
+    lp_route_bases, packed by k_lpack_route): for P = 1..16 with uneven peer
+    splits, a part receives from every other part only the records with a
+    receiver it owns, laid out after its own records, and every receiver reads
+    through the offset tables exactly its neighbours' records that include it,
+    in order (SURVEY.md §8e's per-destination exchange)."""
+    src = tmp_path / "route.cpp"
+    src.write_text(ROUTE_CHECK)
+    exe = tmp_path / "route"
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-I", os.path.join(ROOT, "dst-libp2p-test-node_amd", "csrc"),
+                           str(src), "-o", str(exe)])
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout
+    assert out.stdout.startswith("ok ") and int(out.stdout.split()[1]) > 10000
+
 
 def test_partition_layout_exchanges(tmp_path):
     """gs_run_partitioned's block arithmetic (csrc/gs_layout.h, used by both
