@@ -131,15 +131,19 @@ def test_run_partitioned_local_comm_equals_gs_run(parts, frags, batch):
     comm.close()
 
 
-@pytest.mark.parametrize("push", [False, True])
+@pytest.mark.parametrize("mode", ["gather", "route", "push"])
 @pytest.mark.parametrize("parts,frags,batch", [(2, 1, 64), (5, 2, 32), (8, 1, 1024)])
-def test_run_partitioned_list_pass_and_push_protocol(monkeypatch, push, parts, frags, batch):
+def test_run_partitioned_list_pass_and_push_protocol(monkeypatch, mode, parts, frags, batch):
     """gs_run_partitioned runs each part's rows on the list pass (records
-    exchanged between passes) — or, with GS_PART_PUSH, on the push protocol —
-    bit-identical to gs_run and the oracle; uneven part sizes, fragments, rows
-    of 1024 lanes."""
+    exchanged between passes: every part's to every part, or with
+    GS_PART_ROUTE routed to the parts owning a receiver) — or, with
+    GS_PART_PUSH, on the push protocol — bit-identical to gs_run and the
+    oracle; uneven part sizes, fragments, rows of 1024 lanes."""
+    push = mode == "push"
     if push:
         monkeypatch.setenv("GS_PART_PUSH", "1")
+    if mode == "route":
+        monkeypatch.setenv("GS_PART_ROUTE", "1")
     N = 3001
     p = oracle.params(peers=N, seed=65, fragments=frags)
     sched = _sched(batch, N)
@@ -177,11 +181,15 @@ def test_run_partitioned_list_overflow_falls_back_to_push(monkeypatch):
     comm.close()
 
 
+@pytest.mark.parametrize("route", [False, True])
 @pytest.mark.parametrize("N,M", [(2000, 12), (100_000, 64)])
-def test_run_partitioned_rccl_single_rank(N, M):
+def test_run_partitioned_rccl_single_rank(monkeypatch, N, M, route):
     """gs_comm_init over RCCL with one rank on this GPU (the N = 1 case of the
     multi-GPU bench): the same protocol through RCCL's all-gather, grouped
-    send/recv and MIN all-reduce, bit-identical to gs_run."""
+    send/recv and MIN all-reduce (and the routed exchange's count matrix),
+    bit-identical to gs_run."""
+    if route:
+        monkeypatch.setenv("GS_PART_ROUTE", "1")
     p = oracle.params(peers=N, seed=59)
     sched = _sched(M, N)
     ref, _ = _whole(p, 5, (50, 150, 40, 130), sched, M)
