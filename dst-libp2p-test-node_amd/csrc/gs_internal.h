@@ -119,6 +119,11 @@ struct Ctx {
   DevBuf<uint64_t> d_ring_mm;     // [R][N] mesh of each epoch as a mask over the CSR row (max_degree <= 64)
   std::vector<uint64_t> ring_in_tag;  // [R] epoch whose inverse IHAVE lists a slot holds (~0: none)
   bool ring_in_defer = false;         // the churn list pass takes the batch: no inverse lists beside the epochs
+  // the ELL snapshots too: a churn list-pass batch reads only the mask ring, so the
+  // epochs skip the ELL copy and ensure_ring_ell rebuilds a slot from its mask when
+  // another reader needs it (push-path fallback, non-flood seeds, traffic)
+  std::vector<uint64_t> ring_ell_tag;  // [R] epoch whose ELL snapshot a slot holds (~0: none)
+  bool ring_ell_defer = false;
   // called by the epoch chain after it enqueued epoch h on the context's stream (and once with
   // h0 - 1 when the run's offline bits are written): the churn list pass's tables of the epochs
   // done so far go to the side stream (gs_relax.hip chn_chunks)
@@ -297,6 +302,7 @@ uint32_t run_mesh(Ctx& c, uint32_t max_heartbeats);
 void churn_ring(Ctx& c, uint64_t h_lo, uint64_t h_hi);
 void ensure_csrpos(Ctx& c);
 void ensure_in_lists(Ctx& c, uint64_t h0, uint64_t h1);
+void ensure_ring_ell(Ctx& c, uint64_t h0, uint64_t h1);
 hipStream_t side_stream(Ctx& c);
 void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_result_sink* sink);
 void deliver_rows(Ctx& c, uint32_t B, uint32_t un, const gs_result_sink* sink, uint64_t sink_row0);

@@ -876,11 +876,13 @@ __global__ __launch_bounds__(TB) void k_ev_step(MeshArgs a, uint32_t* mesh, cons
   uint8_t* P = a.pst;
   const uint32_t N = a.N;
   const uint32_t base = blockIdx.x * EV_ROWS;
-  if (STEP == EV_APPLY && mesh && mesh_prev) {  // unchanged rows keep their ELL row: copy the block's rows
+  if (STEP == EV_APPLY) {  // unchanged rows keep their ELL row / mesh mask: copy the block's rows
     const uint32_t nrow = base + EV_ROWS <= N ? EV_ROWS : N - base;
-    const uint4* src = reinterpret_cast<const uint4*>(mesh_prev + (size_t)base * MESH_W);
-    uint4* dst = reinterpret_cast<uint4*>(mesh + (size_t)base * MESH_W);
-    for (uint32_t i = threadIdx.x; i < nrow * (MESH_W / 4); i += TB) dst[i] = src[i];
+    if (mesh && mesh_prev) {
+      const uint4* src = reinterpret_cast<const uint4*>(mesh_prev + (size_t)base * MESH_W);
+      uint4* dst = reinterpret_cast<uint4*>(mesh + (size_t)base * MESH_W);
+      for (uint32_t i = threadIdx.x; i < nrow * (MESH_W / 4); i += TB) dst[i] = src[i];
+    }
     if (a.mm_out && a.mm_prev)
       for (uint32_t i = threadIdx.x; i < nrow; i += TB) a.mm_out[base + i] = a.mm_prev[base + i];
   }
@@ -902,7 +904,8 @@ __global__ __launch_bounds__(TB) void k_ev_step(MeshArgs a, uint32_t* mesh, cons
         on = P[(size_t)PS_INBOX * N + u];
       } else {
         const bool need = P[(size_t)PS_PROPD * N + u] || P[(size_t)PS_PRUNED * N + u];
-        const bool dirty = need || P[(size_t)PS_DIRTY * N + u] || (mesh && !mesh_prev);
+        // (the first epoch of a run writes every row: no previous snapshot to copy)
+        const bool dirty = need || P[(size_t)PS_DIRTY * N + u] || (mesh && !mesh_prev) || (a.mm_out && !a.mm_prev);
         const bool depart = a.off_next && !is_off(a.off, u) && is_off(a.off_next, u);
         on = dirty || depart;
         fl = (need ? 1u : 0u) | (dirty ? 2u : 0u) | (depart ? 4u : 0u);
@@ -1138,8 +1141,13 @@ void ev_epochs(Ctx& c, MeshArgs a, uint64_t h0, uint64_t h1, bool ring) {
     a.off = lin + y * w64;
     a.off_prev = lin + (y - 1) * w64;
     a.off_next = h < h1 ? lin + (y + 1) * w64 : nullptr;
-    uint32_t* mesh = ring ? c.d_ring_mesh.p + (size_t)(h % c.ring_R) * N * MESH_W : nullptr;
-    const uint32_t* prev = ring && h > h0 ? c.d_ring_mesh.p + (size_t)((h - 1) % c.ring_R) * N * MESH_W : nullptr;
+    const bool ell = ring && !(c.ring_ell_defer && c.d_ring_mm.p);  // (deferred: the mask ring only)
+    uint32_t* mesh = ell ? c.d_ring_mesh.p + (size_t)(h % c.ring_R) * N * MESH_W : nullptr;
+    const uint32_t* prev = ell && h > h0 ? c.d_ring_mesh.p + (size_t)((h - 1) % c.ring_R) * N * MESH_W : nullptr;
+    if (ring) {
+      if (c.ring_ell_tag.size() != c.ring_R) c.ring_ell_tag.assign(c.ring_R, ~0ull);
+      c.ring_ell_tag[h % c.ring_R] = ell ? h : ~0ull;
+    }
     const bool mmr = ring && c.d_ring_mm.p;
     a.mm_out = mmr ? c.d_ring_mm.p + (size_t)(h % c.ring_R) * N : nullptr;
     a.mm_prev = mmr && h > h0 ? c.d_ring_mm.p + (size_t)((h - 1) % c.ring_R) * N : nullptr;
@@ -1227,6 +1235,8 @@ void churn_ring(Ctx& c, uint64_t h_lo, uint64_t h_hi) {
       MeshArgs a0 = a;
       a0.mm_out = c.d_ring_mm.p;  // slot 0 (nullptr: no mask ring)
       k_extract<<<blocks(N), TB, 0, s>>>(a0, c.d_ring_mesh.p, nullptr);
+      if (c.ring_ell_tag.size() != R) c.ring_ell_tag.assign(R, ~0ull);
+      c.ring_ell_tag[0] = 0;
       GS_HIP(hipMemsetAsync(c.d_ring_off.p, 0, w64 * 8, s));
       ring_in_lists(c, 0, 0);
       c.ring_lo = 0;
@@ -1243,6 +1253,44 @@ void churn_ring(Ctx& c, uint64_t h_lo, uint64_t h_hi) {
   GS_HIP(hipMemcpyAsync(c.h_pinned, c.d_counters.p + C_ERR, 8, hipMemcpyDeviceToHost, s));
   GS_HIP(hipStreamSynchronize(s));
   if (c.h_pinned[0] & ERR_MESH) c.fail(GS_ERANGE, "mesh row exceeds GS_MESH_W entries");
+}
+
+// ELL snapshots of ring epochs [h0, h0 + gridDim.y) rebuilt from the mask ring:
+// row u's mesh = its CSR entries (ccol: stage << 24 | peer, ascending, the ELL
+// order) whose bit is set. One wave per row.
+__global__ __launch_bounds__(TB) void k_mm2ell(const uint32_t* __restrict__ ccol, const uint64_t* __restrict__ ring_mm,
+                                               uint32_t* __restrict__ ring_mesh, uint32_t N, uint32_t R, uint64_t h0,
+                                               uint64_t* counters) {
+  const uint32_t lane = threadIdx.x & 63, u = blockIdx.x * (TB / 64) + (threadIdx.x >> 6);
+  if (u >= N) return;
+  const size_t slot = (size_t)((h0 + blockIdx.y) % R);
+  const uint64_t m = ring_mm[slot * N + u];
+  const uint32_t x = ccol[(size_t)u * 64 + lane];
+  const bool in = (m >> lane) & 1ull;
+  const uint64_t bm = __ballot(in);
+  const uint32_t pos = (uint32_t)__popcll(bm & ((1ull << lane) - 1)), cnt = (uint32_t)__popcll(bm);
+  uint32_t* row = ring_mesh + (slot * N + u) * MESH_W;
+  if (in && pos < MESH_W) row[pos] = x;
+  if (lane >= cnt && lane < MESH_W) row[lane] = EMPTY;
+  if (cnt > MESH_W && lane == 0) atomicOr((unsigned*)&counters[C_ERR], ERR_MESH);
+}
+
+// The ELL snapshots of ring epochs [h0, h1] the epochs skipped (ring_ell_defer),
+// on the context's stream (the mask ring and the 64-wide CSR rows hold them).
+void ensure_ring_ell(Ctx& c, uint64_t h0, uint64_t h1) {
+  if (!c.d_ring_mm.p || !c.cell_valid) return;  // (no mask ring: every epoch wrote its ELL)
+  const uint32_t R = c.ring_R, N = c.cfg.peers;
+  if (c.ring_ell_tag.size() != R) c.ring_ell_tag.assign(R, ~0ull);
+  for (uint64_t h = h0; h <= h1;) {
+    if (c.ring_ell_tag[h % R] == h) { h++; continue; }
+    uint64_t e = h;
+    while (e + 1 <= h1 && e + 1 - h < 32768 && c.ring_ell_tag[(e + 1) % R] != e + 1) e++;
+    k_mm2ell<<<dim3((N + TB / 64 - 1) / (TB / 64), (unsigned)(e - h + 1)), TB, 0, c.stream>>>(
+        c.d_ccol.p, c.d_ring_mm.p, c.d_ring_mesh.p, N, R, h, c.d_counters.p);
+    for (uint64_t k = h; k <= e; k++) c.ring_ell_tag[k % R] = k;
+    h = e + 1;
+  }
+  GS_HIP(hipGetLastError());
 }
 
 // Position of each row's peer in its neighbour's row (k_csrpos), once per CSR:
@@ -1262,6 +1310,7 @@ uint32_t run_mesh(Ctx& c, uint32_t max_hb) {
   if (c.nnz) k_clear_mesh<<<blocks(c.nnz), TB, 0, s>>>(c.nnz, c.d_flags.p, c.d_until.p);
   GS_HIP(hipMemsetAsync(c.d_counters.p + C_ERR, 0, 8, s));
   c.ring_in_tag.assign(c.ring_in_tag.size(), ~0ull);  // a new mesh: the churn ring restarts
+  c.ring_ell_tag.assign(c.ring_ell_tag.size(), ~0ull);
   c.glp_prefer = false;  // and gossip batches try the eager pass + no-op proof first again
   sub_epoch(c, a);
   uint32_t epoch = 1, last = 0;

@@ -1814,6 +1814,7 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
               (!gossip || hb > b.lat_max + dl);
       }
       c.ring_in_defer = chn;  // the push path's inverse IHAVE lists are not needed
+      c.ring_ell_defer = chn;  // nor the ELL snapshots (the pass reads the mask ring)
       ChnPrep cp;
       if (chn) {
         chn_begin(c, cp, h_lo, (uint32_t)(h_hi + c.cfg.churn_horizon - h_lo + 1), q0v.data(), sched + i0, b.B);
@@ -1824,10 +1825,16 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       } catch (...) {
         c.epoch_hook = nullptr;
         c.ring_in_defer = false;
+        c.ring_ell_defer = false;
         throw;
       }
       c.epoch_hook = nullptr;
       c.ring_in_defer = false;
+      c.ring_ell_defer = false;
+      // readers of the ELL snapshots beside the list pass: seeds to the mesh (no flood
+      // publish), the per-peer traffic pass, the GS_DEBUG_CHN check
+      if (chn && (!c.cfg.flood_publish || c.traffic || getenv("GS_DEBUG_CHN")))
+        ensure_ring_ell(c, h_lo, h_hi + c.cfg.churn_horizon);
       if (chn) chn_end(c, cp);
       c.d_q0.alloc(Bmax);
       c.d_r0.alloc(Bmax);
@@ -2063,6 +2070,7 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
         }
       }
       if (!done && getenv("GS_REQUIRE_LPULL")) c.fail(GS_EUNSUPPORTED, "churn list pass cannot take this batch (GS_REQUIRE_LPULL)");
+      if (!done) ensure_ring_ell(c, h_lo, h_hi + c.cfg.churn_horizon);  // the push path reads the ELL ring
       if (!done && gossip) ensure_in_lists(c, h_lo, h_hi + c.cfg.churn_horizon);
     }
     if (glp && c.glp_prefer) done = run_glp();
