@@ -372,9 +372,11 @@ __device__ __forceinline__ bool row_handle_graft(const MeshArgs& a, uint32_t w, 
   const int gbase = (threadIdx.x & 63) & ~(G - 1);
   (void)gbase;
   const uint32_t sw = a.stage[w];
-  uint32_t f[HB_PER_LANE], p[HB_PER_LANE], r[HB_PER_LANE], un[HB_PER_LANE];
+  uint32_t f[HB_PER_LANE], p[HB_PER_LANE], r[HB_PER_LANE], un[HB_PER_LANE], cl[HB_PER_LANE];
   uint64_t lvl[HB_PER_LANE];  // latency u->w of a proposing neighbour u, else INF64
   uint32_t c = 0;
+  // the row's entries first (ids too), then the neighbours' proposals and stages
+  // together: two dependent round trips instead of three (rev -> prop -> col -> stage)
 #pragma unroll
   for (int k = 0; k < HB_PER_LANE; k++) {
     const uint32_t i = (uint32_t)(k * G + lane);
@@ -382,17 +384,24 @@ __device__ __forceinline__ bool row_handle_graft(const MeshArgs& a, uint32_t w, 
     p[k] = 0;
     r[k] = 0;
     un[k] = 0;
-    lvl[k] = INF64;
+    cl[k] = 0;
     if (i < deg) {
       f[k] = a.flags[b + i];
       p[k] = a.prop[b + i];
       r[k] = a.rev[b + i];
       un[k] = a.until[b + i];  // loaded with the row: the GRAFT loop below is serial
-      if (a.prop[r[k]] & PR_GRAFT) {  // arrival order: latency u->w (heartbeat), handshake (subscription)
-        const uint32_t su = a.stage[a.col[b + i]];
+      cl[k] = a.col[b + i];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < HB_PER_LANE; k++) {
+    const uint32_t i = (uint32_t)(k * G + lane);
+    lvl[k] = INF64;
+    if (i < deg) {
+      const uint32_t pr = a.prop[r[k]], su = a.stage[cl[k]];
+      if (pr & PR_GRAFT)  // arrival order: latency u->w (heartbeat), handshake (subscription)
         lvl[k] = a.sub ? (uint64_t)(a.sub + 1) * (a.lat[su * a.S + sw] + a.lat[sw * a.S + su])
                        : a.lat[su * a.S + sw];
-      }
     }
     c += (uint32_t)__popcll(gballot<G>(((f[k] & F_MESH) && !(p[k] & PR_PRUNE)) || (p[k] & PR_GRAFT)));
   }
