@@ -469,6 +469,12 @@ __device__ __forceinline__ void glp_ihave_ent(const LPullArgs& a, uint64_t* CW, 
 #ifndef GS_LP_NG
 #define GS_LP_NG 4
 #endif
+#ifndef GS_LP_NT  // nontemporal stores of the final log (A/B: -DGS_LP_NT=0)
+#define GS_LP_NT 1
+#endif
+#ifndef GS_LP_NTR  // nontemporal stores of the records (A/B variant; off)
+#define GS_LP_NTR 0
+#endif
 #ifndef GS_LP_RCH
 #define GS_LP_RCH 2
 #endif
@@ -1120,8 +1126,13 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
           if (act) {
             const uint32_t p =
                 logc + __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
-            a.keys[(size_t)w * LL + p] = x;
-            a.flane[(size_t)w * LL + p] = (uint16_t)i;
+            if (GS_LP_NT) {  // the final log is read after the passes (completion): stream it past the caches
+              __builtin_nontemporal_store(x, &a.keys[(size_t)w * LL + p]);
+              __builtin_nontemporal_store((uint16_t)i, &a.flane[(size_t)w * LL + p]);
+            } else {
+              a.keys[(size_t)w * LL + p] = x;
+              a.flane[(size_t)w * LL + p] = (uint16_t)i;
+            }
           }
           logc += (uint32_t)__popcll(fm);
         }
@@ -1136,7 +1147,9 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
             *reinterpret_cast<uint4*>(wrec + ri * 2) =
                 make_uint4((uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)im64, (uint32_t)(im64 >> 32));
           } else {
-            wrec[ri] = ((start - wlo) << 32) | ((uint64_t)hp << LP_HOP_SHIFT) | ((uint64_t)im << LP_IM_SHIFT) | i;
+            const uint64_t rv = ((start - wlo) << 32) | ((uint64_t)hp << LP_HOP_SHIFT) | ((uint64_t)im << LP_IM_SHIFT) | i;
+            if (GS_LP_NTR) __builtin_nontemporal_store(rv, &wrec[ri]);
+            else wrec[ri] = rv;
           }
         }
         ecnt += (uint32_t)__popcll(wm);
