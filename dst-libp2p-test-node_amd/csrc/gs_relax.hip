@@ -1412,6 +1412,7 @@ static void chn_chunks(Ctx& c, ChnPrep& cp, uint64_t h_done, bool all) {
   GS_HIP(hipStreamWaitEvent(side, e, 0));
   if (!cp.offe) {  // every epoch's offline bits are in the ring once the chain's run started
     k_offe<<<dim3(w64, cp.cW), 64, 0, side>>>(N, c.d_ring_off.p, w64, c.ring_R, cp.E0, cp.cE, cp.cW, c.d_offe.p);
+    k_coff<<<cp.grid, TB, 0, side>>>(cp.pa);  // the offline lanes need no mesh: beside the chain too
     cp.offe = true;
   }
   cp.pa.c0 = cp.next;
@@ -1425,7 +1426,6 @@ static void chn_end(Ctx& c, ChnPrep& cp) {
   const hipEvent_t e = cp_event(c, cp.nev++);
   GS_HIP(hipEventRecord(e, side_stream(c)));
   GS_HIP(hipStreamWaitEvent(c.stream, e, 0));
-  k_coff<<<cp.grid, TB, 0, c.stream>>>(cp.pa);
   GS_HIP(hipGetLastError());
   const uint32_t N = c.cfg.peers, R = c.ring_R, cE = cp.cE;
   const uint64_t E0 = cp.E0;
