@@ -199,10 +199,11 @@ __device__ __forceinline__ void row_heartbeat_rest(const MeshArgs& a, uint32_t u
   uint32_t mm = m, oo = o;
   uint32_t graft = 0;  // bit k: entry k*64 + lane grafted this epoch
   if (m < a.d_lo) {  // graft mesh_n - |mesh| random eligible peers
+    const uint64_t pre = rng_pre(a.seed, P_GRAFT, u);
 #pragma unroll
     for (int k = 0; k < HB_PER_LANE; k++) {
       key[k] = INF64;
-      if (k * G < (int)deg && elig[k]) key[k] = rng(a.seed, P_GRAFT, u, a.epoch, w[k]);
+      if (k * G < (int)deg && elig[k]) key[k] = rng_fin(pre, a.epoch, w[k]);
     }
     for (uint32_t q = 0; q < a.d - m; q++) {
       uint64_t bk;
@@ -225,10 +226,11 @@ __device__ __forceinline__ void row_heartbeat_rest(const MeshArgs& a, uint32_t u
     // walk the (start-of-epoch) mesh in ascending (key, entry) order
     const uint32_t excess = mm - a.d;
     uint32_t removed = 0;
+    const uint64_t pre = rng_pre(a.seed, P_PRUNE, u);
 #pragma unroll
     for (int k = 0; k < HB_PER_LANE; k++) {
       key[k] = INF64;
-      if (k * G < (int)deg && (f[k] & F_MESH)) key[k] = rng(a.seed, P_PRUNE, u, a.epoch, w[k]);
+      if (k * G < (int)deg && (f[k] & F_MESH)) key[k] = rng_fin(pre, a.epoch, w[k]);
     }
     for (uint32_t q = 0; q < m && removed < excess; q++) {
       uint64_t bk;
@@ -251,12 +253,13 @@ __device__ __forceinline__ void row_heartbeat_rest(const MeshArgs& a, uint32_t u
     }
   }
   if (mm >= a.d_lo && oo < a.d_out) {  // graft outbound peers
+    const uint64_t pre = rng_pre(a.seed, P_OUT_GRAFT, u);
 #pragma unroll
     for (int k = 0; k < HB_PER_LANE; k++)
     {
       key[k] = INF64;
       if (k * G < (int)deg && elig[k] && (f[k] & F_OUT) && !((graft >> k) & 1u))
-        key[k] = rng(a.seed, P_OUT_GRAFT, u, a.epoch, w[k]);
+        key[k] = rng_fin(pre, a.epoch, w[k]);
     }
     for (uint32_t q = 0; q < a.d_out - oo; q++) {
       uint64_t bk;
@@ -590,11 +593,12 @@ __global__ __launch_bounds__(TB) void k_gossip_out_range(const uint64_t* __restr
 #pragma unroll
     for (int q = 0; q < (int)GT_W; q++) { kk[q] = INF64; ww[q] = ~0u; pp[q] = 0; }
     uint32_t nonmesh = 0;
+    const uint64_t pre = rng_pre(seed, P_GOSSIP, u);
     for (uint64_t e = e0; e < e1; e++) {
       const uint32_t w = col[e];
       if (!eligible(w)) continue;
       nonmesh++;
-      const uint64_t rk = rng(seed, P_GOSSIP, u, (uint32_t)h, w);
+      const uint64_t rk = rng_fin(pre, (uint32_t)h, w);
       const uint32_t pe = (uint32_t)(e - e0);
       if (!lt(rk, w, kk[GT_W - 1], ww[GT_W - 1])) continue;
 #pragma unroll
@@ -618,7 +622,7 @@ __global__ __launch_bounds__(TB) void k_gossip_out_range(const uint64_t* __restr
       for (uint64_t e = e0; e < e1; e++) {
         const uint32_t w = col[e];
         if (!eligible(w)) continue;
-        const uint64_t rk = rng(seed, P_GOSSIP, u, (uint32_t)h, w);
+        const uint64_t rk = rng_fin(pre, (uint32_t)h, w);
         if (lt(pk, pw, rk, w) && lt(rk, w, bk, bw)) { bk = rk; bw = w; bp = (uint32_t)(e - e0); }
       }
       mask |= 1ull << bp;

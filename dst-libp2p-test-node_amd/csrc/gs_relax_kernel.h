@@ -767,11 +767,12 @@ __device__ __forceinline__ void for_each_gossip_target(const RelaxArgs& a, uint3
     for (int q = 0; q < (int)MESH_W; q++) inm |= mrow[q] == w;
     return !inm && !(a.churn && ep_off(a, hab, w));
   };
+  const uint64_t pre = rng_pre(a.seed, P_GOSSIP, u);
   for (uint64_t e = e0; e < e1; e++) {
     const uint32_t w = a.col[e];
     if (!eligible(w)) continue;
     nonmesh++;
-    const uint64_t rk = rng(a.seed, P_GOSSIP, u, h, w);
+    const uint64_t rk = rng_fin(pre, h, w);
     if (!pair_lt(rk, w, kk[GOSSIP_R_REG - 1], ww[GOSSIP_R_REG - 1])) continue;
 #pragma unroll
     for (int q = (int)GOSSIP_R_REG - 1; q > 0; q--) {  // insert, shifting the larger pairs up
@@ -794,7 +795,7 @@ __device__ __forceinline__ void for_each_gossip_target(const RelaxArgs& a, uint3
     for (uint64_t e = e0; e < e1; e++) {
       const uint32_t w = a.col[e];
       if (!eligible(w)) continue;
-      const uint64_t rk = rng(a.seed, P_GOSSIP, u, h, w);
+      const uint64_t rk = rng_fin(pre, h, w);
       if (pair_lt(pk, pw, rk, w) && pair_lt(rk, w, bk, bw)) { bk = rk; bw = w; }
     }
     fn(((uint32_t)a.stage[bw] << STAGE_SHIFT) | bw);
