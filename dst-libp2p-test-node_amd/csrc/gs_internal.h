@@ -107,6 +107,7 @@ struct Ctx {
   DevBuf<uint32_t> d_rev;    // [nnz] index of the reverse entry
   DevBuf<uint32_t> d_until;  // [nnz] back-off: graft refused while epoch < until
   DevBuf<uint8_t> d_prop;    // [nnz] per-epoch GRAFT/PRUNE/ACCEPT bits
+  DevBuf<uint8_t> d_iprop;   // [nnz] event-driven epochs: the GRAFT/PRUNE bits a neighbour proposed, at the receiver's entry
   DevBuf<uint32_t> d_mesh;   // [N*MESH_W] packed stage<<24|peer, EMPTY padded
   DevBuf<uint32_t> d_lat32;  // [S*S] u32 latency for the mesh kernels
   // churn: ring of per-epoch snapshots, slot = epoch % ring_R

@@ -50,6 +50,10 @@ struct MeshArgs {
   // not re-extract copy mm_prev (nullptr: no mask ring)
   uint64_t* mm_out;
   const uint64_t* mm_prev;
+  // event-driven epochs: iprop[rev[e]] mirrors the PR_GRAFT / PR_PRUNE bit of a
+  // proposal prop[e], so the receiver reads its own row contiguously instead of
+  // gathering prop[rev[.]]; cleared by the step that consumes it (GRAFT / apply)
+  uint8_t* iprop;
 };
 
 // Planes of MeshArgs::pst. A row runs the heavy per-row code of an epoch step
@@ -180,7 +184,7 @@ __device__ __forceinline__ void row_heartbeat_rest(const MeshArgs& a, uint32_t u
       if (sel == ~0u) break;
       if ((int)(sel % G) == lane) {
         drop_key<G>(key, sel);
-        a.prop[b + sel] |= PR_GRAFT;
+        a.prop[b + sel] = PR_GRAFT;  // (prop is clear at the heartbeat: plain stores, no load in the loop)
       }
     }
     return;
@@ -197,7 +201,10 @@ __device__ __forceinline__ void row_heartbeat_rest(const MeshArgs& a, uint32_t u
   };
   bool proposed = false;
   uint32_t mm = m, oo = o;
-  uint32_t graft = 0;  // bit k: entry k*64 + lane grafted this epoch
+  uint32_t graft = 0;  // bit k: entry k*G + lane grafted this epoch
+  uint32_t pruned = 0;  // bit k: entry k*G + lane pruned this epoch
+  // (prop is clear at the heartbeat — last epoch's proposals were cleared by the
+  // caller — so each proposal is one plain store, no load inside the loops)
   if (m < a.d_lo) {  // graft mesh_n - |mesh| random eligible peers
     const uint64_t pre = rng_pre(a.seed, P_GRAFT, u);
 #pragma unroll
@@ -214,7 +221,7 @@ __device__ __forceinline__ void row_heartbeat_rest(const MeshArgs& a, uint32_t u
       if ((int)(sel % G) == lane) {
         drop_key<G>(key, sel);
         graft |= 1u << (sel / G);
-        a.prop[b + sel] |= PR_GRAFT;
+        a.prop[b + sel] = PR_GRAFT;
         mark(sel, PS_INBOX);
       }
       proposed = true;
@@ -244,7 +251,8 @@ __device__ __forceinline__ void row_heartbeat_rest(const MeshArgs& a, uint32_t u
         oo--;
       }
       if ((int)(sel % G) == lane) {
-        a.prop[b + sel] |= PR_PRUNE;
+        pruned |= 1u << (sel / G);
+        a.prop[b + sel] = PR_PRUNE;
         mark(sel, PS_PRUNED);
       }
       proposed = true;
@@ -269,11 +277,21 @@ __device__ __forceinline__ void row_heartbeat_rest(const MeshArgs& a, uint32_t u
       if (sel == ~0u) break;
       if ((int)(sel % G) == lane) {
         drop_key<G>(key, sel);
-        a.prop[b + sel] |= PR_GRAFT;
+        graft |= 1u << (sel / G);
+        a.prop[b + sel] = PR_GRAFT;
         mark(sel, PS_INBOX);
       }
       proposed = true;
     }
+  }
+  if (a.iprop && (graft | pruned)) {  // mirror the proposals at the receivers' entries (reverse ids loaded together)
+    uint32_t rv[HB_PER_LANE];
+#pragma unroll
+    for (int k = 0; k < HB_PER_LANE; k++)
+      if (((graft | pruned) >> k) & 1u) rv[k] = a.rev[b + k * G + lane];
+#pragma unroll
+    for (int k = 0; k < HB_PER_LANE; k++)
+      if (((graft | pruned) >> k) & 1u) a.iprop[rv[k]] = ((graft >> k) & 1u) ? PR_GRAFT : PR_PRUNE;
   }
   if (a.pst && proposed && lane == 0) {
     a.pst[(size_t)PS_PROPD * a.N + u] = 1;
@@ -375,7 +393,7 @@ __device__ __forceinline__ bool row_handle_graft(const MeshArgs& a, uint32_t w, 
   const int gbase = (threadIdx.x & 63) & ~(G - 1);
   (void)gbase;
   const uint32_t sw = a.stage[w];
-  uint32_t f[HB_PER_LANE], p[HB_PER_LANE], r[HB_PER_LANE], un[HB_PER_LANE], cl[HB_PER_LANE];
+  uint32_t f[HB_PER_LANE], p[HB_PER_LANE], r[HB_PER_LANE], un[HB_PER_LANE], cl[HB_PER_LANE], ip[HB_PER_LANE];
   uint64_t lvl[HB_PER_LANE];  // latency u->w of a proposing neighbour u, else INF64
   uint32_t c = 0;
   // the row's entries first (ids too), then the neighbours' proposals and stages
@@ -388,12 +406,14 @@ __device__ __forceinline__ bool row_handle_graft(const MeshArgs& a, uint32_t w, 
     r[k] = 0;
     un[k] = 0;
     cl[k] = 0;
+    ip[k] = 0;
     if (i < deg) {
       f[k] = a.flags[b + i];
       p[k] = a.prop[b + i];
       r[k] = a.rev[b + i];
       un[k] = a.until[b + i];  // loaded with the row: the GRAFT loop below is serial
       cl[k] = a.col[b + i];
+      if (a.iprop) ip[k] = a.iprop[b + i];
     }
   }
 #pragma unroll
@@ -401,10 +421,14 @@ __device__ __forceinline__ bool row_handle_graft(const MeshArgs& a, uint32_t w, 
     const uint32_t i = (uint32_t)(k * G + lane);
     lvl[k] = INF64;
     if (i < deg) {
-      const uint32_t pr = a.prop[r[k]], su = a.stage[cl[k]];
-      if (pr & PR_GRAFT)  // arrival order: latency u->w (heartbeat), handshake (subscription)
+      // event-driven epochs: the mirrored bit (row-contiguous), the proposer's stage only when it proposed
+      const bool g = a.iprop ? (ip[k] & PR_GRAFT) != 0 : (a.prop[r[k]] & PR_GRAFT) != 0;
+      if (g) {  // arrival order: latency u->w (heartbeat), handshake (subscription)
+        const uint32_t su = a.stage[cl[k]];
         lvl[k] = a.sub ? (uint64_t)(a.sub + 1) * (a.lat[su * a.S + sw] + a.lat[sw * a.S + su])
                        : a.lat[su * a.S + sw];
+        if (a.iprop) a.iprop[b + i] = (uint8_t)(ip[k] & ~PR_GRAFT);  // consumed
+      }
     }
     c += (uint32_t)__popcll(gballot<G>(((f[k] & F_MESH) && !(p[k] & PR_PRUNE)) || (p[k] & PR_GRAFT)));
   }
@@ -434,7 +458,7 @@ __device__ __forceinline__ bool row_handle_graft(const MeshArgs& a, uint32_t w, 
       for (int k = 0; k < HB_PER_LANE; k++)
         if ((uint32_t)k == (sel / G)) rs = r[k];
       if (rej) a.until[e] = a.epoch + a.bo;  // PRUNE back, both ends back off
-      else a.prop[rs] |= PR_ACCEPT;
+      else a.prop[rs] = PR_GRAFT | PR_ACCEPT;  // (the entry holds exactly the GRAFT: a store, no load)
       if (!in_mesh && !rej) a.flags[e] = (uint8_t)(fs | F_MESH);
     }
     if (!in_mesh && !rej) {
@@ -803,21 +827,21 @@ __device__ __forceinline__ void row_apply_ev(const MeshArgs& a, uint32_t u, uint
   const int lane = threadIdx.x & (G - 1);
   uint8_t* P = a.pst;
   const uint32_t N = a.N;
-  uint32_t f[HB_PER_LANE], pp[HB_PER_LANE], rv[HB_PER_LANE], cw[HB_PER_LANE], pr[HB_PER_LANE], sg[HB_PER_LANE];
+  uint32_t f[HB_PER_LANE], pp[HB_PER_LANE], cw[HB_PER_LANE], pr[HB_PER_LANE], sg[HB_PER_LANE];
+  // (a neighbour's PRUNE arrives as the mirrored bit a.iprop, on the row itself)
 #pragma unroll
   for (int k = 0; k < HB_PER_LANE; k++) {
     const uint32_t i = (uint32_t)(k * G + lane);
     const bool v = i < deg;
     f[k] = v ? a.flags[b + i] : 0u;
     pp[k] = v && need ? a.prop[b + i] : 0u;
-    rv[k] = v && need ? a.rev[b + i] : 0u;
+    pr[k] = v && need ? a.iprop[b + i] : 0u;
     cw[k] = v && (dirty || depart) ? a.col[b + i] : 0u;
   }
 #pragma unroll
   for (int k = 0; k < HB_PER_LANE; k++) {
     const uint32_t i = (uint32_t)(k * G + lane);
     const bool v = i < deg;
-    pr[k] = v && need ? a.prop[rv[k]] : 0u;
     sg[k] = v && dirty && mesh ? a.stage[cw[k]] : 0u;
   }
   if (need) {  // row_apply
@@ -834,7 +858,11 @@ __device__ __forceinline__ void row_apply_ev(const MeshArgs& a, uint32_t u, uint
         else { fk &= ~(uint32_t)F_MESH; bo = true; }
       }
       if (p & PR_PRUNE) { fk &= ~(uint32_t)F_MESH; bo = true; }
-      if (pr[k] & PR_PRUNE) { fk &= ~(uint32_t)F_MESH; bo = true; }
+      if (pr[k] & PR_PRUNE) {
+        fk &= ~(uint32_t)F_MESH;
+        bo = true;
+        a.iprop[e] = 0;  // consumed
+      }
       if (bo) a.until[e] = a.epoch + a.bo;
       a.flags[e] = (uint8_t)fk;
       f[k] = fk;
@@ -1106,8 +1134,11 @@ void ev_epochs(Ctx& c, MeshArgs a, uint64_t h0, uint64_t h1, bool ring) {
   GS_HIP(hipMemsetAsync(c.d_pst.p, 0, (size_t)PS_MC * N, s));         // flags clear
   GS_HIP(hipMemsetAsync(c.d_pst.p + (size_t)PS_DIRTY * N, 1, N, s));  // first epoch: extract every row
   GS_HIP(hipMemsetAsync(c.d_prop.p, 0, c.nnz ? c.nnz : 1, s));
+  c.d_iprop.alloc(c.nnz ? c.nnz : 1);
+  GS_HIP(hipMemsetAsync(c.d_iprop.p, 0, c.nnz ? c.nnz : 1, s));
   const uint64_t* lin = c.d_offlin.p;  // lin[y] = epoch h0 - 1 + y
   a.pst = c.d_pst.p;
+  a.iprop = c.d_iprop.p;
   static const bool dbg_ev = getenv("GS_DEBUG_EV") != nullptr;
   DevBuf<uint64_t> dbg;
   if (dbg_ev) {
