@@ -123,9 +123,31 @@ static_assert(MAX_DEG % 64 == 0 && HB_PER_LANE <= 4, "k_heartbeat covers MAX_DEG
 // requests in flight of the latency-bound one-row-per-wave form). Lane l of a
 // group holds entries k*G + l, k < HB_PER_LANE.
 
-// group argmin over (key, idx); ~0u if every key is INF64
+// One step of a 16-lane (key, idx) min through a DPP lane permutation inside
+// the 16-lane row: an ALU operand modifier, not an LDS-pipe ds_bpermute round
+// trip — the selection loops of the heartbeat and of GRAFT handling run one
+// group_argmin per choice, back to back.
+template <int CTRL>
+__device__ __forceinline__ void dpp_min_step(uint64_t& key, uint32_t& idx) {
+  const uint32_t kl = (uint32_t)key, kh = (uint32_t)(key >> 32);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)kl, (int)kl, CTRL, 0xF, 0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp((int)kh, (int)kh, CTRL, 0xF, 0xF, false);
+  const uint32_t i2 = (uint32_t)__builtin_amdgcn_update_dpp((int)idx, (int)idx, CTRL, 0xF, 0xF, false);
+  const uint64_t k2 = ((uint64_t)hi << 32) | lo;
+  if (k2 < key || (k2 == key && i2 < idx)) { key = k2; idx = i2; }
+}
+
+// group argmin over (key, idx); ~0u if every key is INF64. (key, idx) is a
+// total order, so the reduction order does not change the result.
 template <int G>
 __device__ __forceinline__ uint32_t group_argmin(uint64_t key, uint32_t idx) {
+  if constexpr (G == 16) {  // lane ^ 1, lane ^ 2 (quad_perm), then the 8- and 16-lane row mirrors
+    dpp_min_step<0xB1>(key, idx);
+    dpp_min_step<0x4E>(key, idx);
+    dpp_min_step<0x141>(key, idx);
+    dpp_min_step<0x140>(key, idx);
+    return key == INF64 ? ~0u : idx;
+  }
   for (int off = G / 2; off > 0; off >>= 1) {
     const uint64_t k2 = __shfl_xor(key, off);
     const uint32_t i2 = (uint32_t)__shfl_xor((int)idx, off);
@@ -160,9 +182,13 @@ __device__ __forceinline__ void row_heartbeat_rest(const MeshArgs& a, uint32_t u
   const int lane = threadIdx.x & (G - 1);
   const int gbase = (threadIdx.x & 63) & ~(G - 1);
   (void)gbase;
-  const int fpack = (int)(f[0] | (f[1] << 8) | (f[2] << 16) | (f[3] << 24));
-  auto flag_of = [&](uint32_t sel) {  // flags of entry sel, from the lane holding it
-    return ((uint32_t)__shfl(fpack, gbase + (int)(sel % G)) >> (8 * (sel / G))) & 0xFFu;
+  auto out_of = [&](uint32_t sel) {  // entry sel is outbound: the holding lane's flag, by ballot
+    bool ob = false;
+    if ((int)(sel % G) == lane)
+#pragma unroll
+      for (int k = 0; k < HB_PER_LANE; k++)
+        if ((uint32_t)k == (sel / G)) ob = (f[k] & F_OUT) != 0;
+    return gballot<G>(ob) != 0;
   };
   uint64_t key[HB_PER_LANE];
   if (a.sub) {  // subscription epoch: the first D_lo connections in subscription-arrival order
@@ -226,7 +252,7 @@ __device__ __forceinline__ void row_heartbeat_rest(const MeshArgs& a, uint32_t u
       }
       proposed = true;
       mm++;
-      oo += flag_of(sel) & F_OUT;
+      oo += out_of(sel) ? 1u : 0u;
     }
   }
   if (mm > a.d_hi) {  // prune down to mesh_n, keep mesh_outbound_min outbound
@@ -246,7 +272,7 @@ __device__ __forceinline__ void row_heartbeat_rest(const MeshArgs& a, uint32_t u
       const uint32_t sel = group_argmin<G>(bk, bi);
       if (sel == ~0u) break;
       if ((int)(sel % G) == lane) drop_key<G>(key, sel);
-      if (flag_of(sel) & F_OUT) {
+      if (out_of(sel)) {
         if (oo <= a.d_out) continue;
         oo--;
       }
@@ -432,8 +458,6 @@ __device__ __forceinline__ bool row_handle_graft(const MeshArgs& a, uint32_t w, 
     }
     c += (uint32_t)__popcll(gballot<G>(((f[k] & F_MESH) && !(p[k] & PR_PRUNE)) || (p[k] & PR_GRAFT)));
   }
-  const int fpack = (int)(f[0] | (f[1] << 8) | (f[2] << 16) | (f[3] << 24));
-  const int ppack = (int)(p[0] | (p[1] << 8) | (p[2] << 16) | (p[3] << 24));
   bool acc = false;
   for (;;) {
     uint64_t bk;
@@ -441,27 +465,24 @@ __device__ __forceinline__ bool row_handle_graft(const MeshArgs& a, uint32_t w, 
     lane_min<G>(lvl, lane, bk, bi);
     const uint32_t sel = group_argmin<G>(bk, bi);  // entry (w -> u) of the next GRAFT to arrive
     if (sel == ~0u) break;
-    const int src = gbase + (int)(sel % G), sh = (int)(8 * (sel / G));
-    const uint32_t fs = ((uint32_t)__shfl(fpack, src) >> sh) & 0xFFu, ps = ((uint32_t)__shfl(ppack, src) >> sh) & 0xFFu;
-    const bool in_mesh = ((fs & F_MESH) && !(ps & PR_PRUNE)) || (ps & PR_GRAFT);
-    const uint64_t e = b + sel;
-    uint32_t uo = 0;  // the owner lane's preloaded back-off of entry sel (written only below, once)
-#pragma unroll
-    for (int k = 0; k < HB_PER_LANE; k++)
-      if ((uint32_t)k == (sel / G)) uo = un[k];
-    const uint32_t us = (uint32_t)__shfl((int)uo, src);
-    const bool rej = !in_mesh && (a.epoch < us || (c >= a.d_hi && !(fs & F_OUT)));
-    if ((int)(threadIdx.x & 63) == src) {
-      drop_key<G>(lvl, sel);
-      uint32_t rs = 0;
+    // the lane holding entry sel decides from its own registers; the group
+    // learns the outcome by a ballot (no cross-lane shuffle in this serial loop)
+    bool took = false;
+    if ((int)(sel % G) == lane) {
+      uint32_t fs = 0, ps = 0, us = 0, rs = 0;
 #pragma unroll
       for (int k = 0; k < HB_PER_LANE; k++)
-        if ((uint32_t)k == (sel / G)) rs = r[k];
+        if ((uint32_t)k == (sel / G)) { fs = f[k]; ps = p[k]; us = un[k]; rs = r[k]; }
+      const bool in_mesh = ((fs & F_MESH) && !(ps & PR_PRUNE)) || (ps & PR_GRAFT);
+      const bool rej = !in_mesh && (a.epoch < us || (c >= a.d_hi && !(fs & F_OUT)));
+      const uint64_t e = b + sel;
+      drop_key<G>(lvl, sel);
       if (rej) a.until[e] = a.epoch + a.bo;  // PRUNE back, both ends back off
       else a.prop[rs] = PR_GRAFT | PR_ACCEPT;  // (the entry holds exactly the GRAFT: a store, no load)
       if (!in_mesh && !rej) a.flags[e] = (uint8_t)(fs | F_MESH);
+      took = !in_mesh && !rej;
     }
-    if (!in_mesh && !rej) {
+    if (gballot<G>(took) != 0) {
       c++;
       acc = true;
     }
