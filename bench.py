@@ -612,14 +612,24 @@ def main():
             "setup_s": t_setup,
             "mesh_epochs": epochs,
             "buckets_per_step": st["buckets"] / max(1, args.steps),
-            "at_%dk_peers" % (args.also_peers // 1000) if extra else "at_second_size": extra,
-            "roofline": roof,
-            "with_output": wout,
+            # verbose entries first: the driver keeps the last ~2000 characters of the
+            # line, so the headline's companions (roofline, the 100k rate, the streamed
+            # rate and every config's rate) come last
+            "configs_1gpu": cfg_rates,
             "gossip": {"lazy_gossip": int(sim.cfg.c.lazy_gossip), "noop_msgs": int(st["gossip_noop_msgs"]),
                        "fallback_batches": int(st["gossip_fallback_batches"]), "iwant": int(st["gossip_iwant"]),
                        "check": gcheck},
             "cpu_baseline": cpu,
-            "configs_1gpu": cfg_rates,
+            "roofline": roof,
+            "at_%dk_peers" % (args.also_peers // 1000) if extra else "at_second_size": extra,
+            "with_output": wout,
+            "configs_1gpu_rates": {k: {"value": v.get("value"), "ms": v.get("ms"),
+                                       "frac": (v.get("roofline") or {}).get("frac"),
+                                       "traffic_x": (v["hbm_bytes_per_batch_all_kernels"] / v["alg_bytes_per_batch"]
+                                                     if v.get("hbm_bytes_per_batch_all_kernels")
+                                                     and v.get("alg_bytes_per_batch") else None)}
+                                   if isinstance(v, dict) else v
+                                   for k, v in cfg_rates.items()} if isinstance(cfg_rates, dict) else None,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -156,6 +156,7 @@ extern "C" gs_status gs_set_links(gs_ctx* ctx, uint32_t S, const uint64_t* lat_n
   GS_HIP(hipStreamSynchronize(ctx->stream));
   ctx->links_set = true;
   ctx->mesh_built = false;  // the mesh's GRAFT order and packed stages depend on the links
+  ctx->cell_valid = false;  //  so do the churn pass's 64-wide rows (stage << 24 | peer)
   GS_API_END(ctx)
 }
 

@@ -20,6 +20,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <exception>
 
 #include "gs_internal.h"
 #include "gs_layout.h"
@@ -1485,7 +1486,21 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
   c.lat_async = true;
   struct AsyncOff {
     Ctx& c;
-    ~AsyncOff() { c.lat_async = false; }
+    int unwinding0 = std::uncaught_exceptions();
+    ~AsyncOff() {
+      c.lat_async = false;
+      //  a run that fails after a batch completed still hands out that
+      // batch's pending latency lines, as the synchronous sink did before; nothing
+      // here may throw while the error unwinds
+      Ctx::LatPending& p = c.lat_pend;
+      if (std::uncaught_exceptions() <= unwinding0 || !p.on) return;
+      p.on = false;
+      if (hipEventSynchronize(c.lat_done[p.par]) != hipSuccess || (c.h_laterr[p.par] & ERR_LAT16)) return;
+      for (uint32_t q0 = 0; q0 < p.B; q0 += p.bm) {
+        const uint32_t n = std::min(p.bm, p.B - q0);
+        p.sink->on_lat(p.sink->user, p.row0 + q0, n, p.un, c.h_lat[p.par] + (size_t)q0 * p.un);
+      }
+    }
   } async_off{c};
   GS_HIP(hipMemsetAsync(c.d_counters.p + C_ERR, 0, 8, s));
   check_schedule(c, sched, n_msgs);
@@ -1835,6 +1850,13 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       // publish), the per-peer traffic pass, the GS_DEBUG_CHN check
       if (chn && (!c.cfg.flood_publish || c.traffic || getenv("GS_DEBUG_CHN")))
         ensure_ring_ell(c, h_lo, h_hi + c.cfg.churn_horizon);
+      //  a batch for the push path may overlap the last epochs of an
+      // earlier churn list-pass batch, which skipped their ELL snapshots and
+      // inverse IHAVE lists: rebuild those slots (tag-checked: free when current)
+      if (!chn) {
+        ensure_ring_ell(c, h_lo, h_hi + c.cfg.churn_horizon);
+        if (gossip) ensure_in_lists(c, h_lo, h_hi + c.cfg.churn_horizon);
+      }
       if (chn) chn_end(c, cp);
       c.d_q0.alloc(Bmax);
       c.d_r0.alloc(Bmax);

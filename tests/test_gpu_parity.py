@@ -569,3 +569,56 @@ def test_churn_gossip_wide_target_lists(connect_to):
     st = sim.stats()
     assert 0 < st["deliveries"] < 16 * 499
     assert st["gossip_iwant"] > 0
+
+
+@pytest.mark.parametrize("second", ["frags2", "idontwant"])
+def test_churn_push_batch_after_list_pass_batch(monkeypatch, second):
+    """a churn batch on the list pass skips the ELL snapshots and
+    inverse IHAVE lists of its epochs; the next batch, on the push path (two
+    fragments, or an IDONTWANT-sized payload), overlaps its last epochs and must
+    find them rebuilt. Bit-exact against the oracle, IWANTs included."""
+    hb = 400_000_000
+    kw = dict(churn_ppm=30000, lazy_gossip=1, heartbeat_ns=hb, churn_down=6, churn_horizon=10,
+              hb_phase_ns=T0 - 30 * hb + 150_000_000)
+    if second == "idontwant":
+        kw["idontwant"] = 1000
+    p = oracle.params(peers=900, seed=57, **kw)
+    M1, M2 = 40, 16
+    t = T0 + np.arange(M1 + M2, dtype=np.uint64) * np.uint64(hb)
+    pub = (6 + np.arange(M1 + M2)) % 900
+    if second == "frags2":
+        size, frags = np.full(M1 + M2, 15000), np.r_[np.ones(M1), np.full(M2, 2)].astype(np.uint32)
+    else:  # first batch under the IDONTWANT threshold (list pass), second above it (push path)
+        size, frags = np.r_[np.full(M1, 500), np.full(M2, 15000)], np.ones(M1 + M2, np.uint32)
+    sim, res = compare(p, 5, (50, 150, 40, 130), (t, pub, size, frags), batch=64)
+    st = sim.stats()
+    assert st["batches"] == 2 and st["list_pull_batches"] == 1
+    assert st["gossip_iwant"] > 0
+
+
+def test_churn_links_changed_between_runs():
+    """new links on the same topology invalidate the churn list
+    pass's 64-wide CSR rows (stage << 24 | peer): a second run after
+    set_links + mesh_converge equals a fresh oracle run on the new links."""
+    hb = 400_000_000
+    kw = dict(churn_ppm=30000, lazy_gossip=1, heartbeat_ns=hb, churn_down=6, churn_horizon=10,
+              hb_phase_ns=T0 - 30 * hb + 150_000_000)
+    p = oracle.params(peers=900, seed=58, **kw)
+    t = T0 + np.arange(32, dtype=np.uint64) * np.uint64(hb)
+    sched = (t, (6 + np.arange(32)) % 900, np.full(32, 15000))
+    links_a, links_b = (50, 150, 40, 130), (30, 100, 30, 120)
+    sim, _ = gpu_sim(p, 5, links_a, batch=32)
+    sim.run(sched)
+    assert sim.stats()["list_pull_batches"] == 1
+    sim.set_topogen_links(3, *links_b)
+    ep = sim.mesh_converge(400)
+    sim.reset_stats()
+    res = sim.run(sched)
+    ref = oracle.simulate(p, 3, links_b, sched=sched)
+    assert ep == ref["epochs"]
+    np.testing.assert_array_equal(res["t_complete"], ref["t_complete"], err_msg="t_complete")
+    np.testing.assert_array_equal(res["hops"], ref["hops"], err_msg="hops")
+    st = sim.stats()
+    assert st["list_pull_batches"] == 1
+    for k in ("deliveries", "relaxations", "gossip_iwant", "latency_sum_ms"):
+        assert st[k] == ref["stats"][k], k
