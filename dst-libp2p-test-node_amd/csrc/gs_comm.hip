@@ -90,12 +90,144 @@ Rccl* rccl() {
 using namespace gs;
 
 struct gs_comm {
-  uint32_t local = 0;    // 1: in-process parts, 0: RCCL
+  uint32_t local = 0;    // 1: in-process parts, 0: RCCL or the caller's transport (ops)
   uint32_t nranks = 1, rank = 0;
   int32_t device = 0;
   ncclComm_t nc = nullptr;
-  uint64_t* d_scratch = nullptr;  // RCCL: [parts * parts] count matrix + 1 flag word + [parts][4] pass control
+  bool has_ops = false;  // gs_comm_init_ops: collectives staged through host memory into ops
+  gs_comm_ops ops{};
+  uint64_t* d_scratch = nullptr;  // ranks: [parts * parts] count matrix + 1 flag word + [parts][4] pass control
+  // ops backend: the send / recv calls of the open group, exchanged at its end
+  struct Xfer {
+    const void* src;
+    void* dst;
+    uint64_t bytes;
+    int peer;
+  };
+  std::vector<Xfer> xs, xr;
+  hipStream_t xstream = nullptr;
 };
+
+namespace gs {
+namespace {
+
+// The rank collectives of the partitioned protocols (RCCL's names and
+// arguments, less the communicator): RCCL over xGMI, or through the caller's
+// gs_comm_ops on host copies — a D2H copy, the callback, an H2D copy — in the
+// same order and sizes on every rank.
+size_t type_bytes(ncclDataType_t t) {
+  switch (t) {
+    case ncclInt8: case ncclUint8: return 1;
+    case ncclInt32: case ncclUint32: case ncclFloat32: return 4;
+    default: return 8;  // ncclUint64 (the only wide type used)
+  }
+}
+void ops_fail(int rc, const char* what) {
+  if (rc) throw Error(GS_EDEVICE, std::string("gs_comm_ops.") + what + " returned " + std::to_string(rc));
+}
+// every rank's n u64 words of the device buffer send -> recv[rank * n + k]
+void coll_AllGather(gs_comm* cm, const void* send, void* recv, size_t n, ncclDataType_t t, hipStream_t s) {
+  if (!cm->has_ops) {
+    GS_NCCL(rccl()->AllGather(send, recv, n, t, cm->nc, s));
+    return;
+  }
+  if (t != ncclUint64) throw Error(GS_EINVAL, "internal: ops all-gather of u64 words only");
+  std::vector<uint64_t> mine(n), all((size_t)cm->nranks * n);
+  GS_HIP(hipMemcpyAsync(mine.data(), send, n * 8, hipMemcpyDeviceToHost, s));
+  GS_HIP(hipStreamSynchronize(s));
+  ops_fail(cm->ops.allgather(cm->ops.user, mine.data(), n, all.data()), "allgather");
+  GS_HIP(hipMemcpyAsync(recv, all.data(), all.size() * 8, hipMemcpyHostToDevice, s));
+  GS_HIP(hipStreamSynchronize(s));
+}
+// in-place MIN / MAX of n u64 words over the ranks (ops: reduced from an all-gather)
+void coll_AllReduce(gs_comm* cm, const void* send, void* recv, size_t n, ncclDataType_t t, ncclRedOp_t op,
+                    hipStream_t s) {
+  if (!cm->has_ops) {
+    GS_NCCL(rccl()->AllReduce(send, recv, n, t, op, cm->nc, s));
+    return;
+  }
+  if (t != ncclUint64 || (op != ncclMin && op != ncclMax)) throw Error(GS_EINVAL, "internal: ops all-reduce");
+  std::vector<uint64_t> mine(n), all((size_t)cm->nranks * n);
+  GS_HIP(hipMemcpyAsync(mine.data(), send, n * 8, hipMemcpyDeviceToHost, s));
+  GS_HIP(hipStreamSynchronize(s));
+  ops_fail(cm->ops.allgather(cm->ops.user, mine.data(), n, all.data()), "allgather");
+  for (size_t k = 0; k < n; k++) {
+    uint64_t v = all[k];
+    for (uint32_t p = 1; p < cm->nranks; p++)
+      v = op == ncclMin ? std::min(v, all[(size_t)p * n + k]) : std::max(v, all[(size_t)p * n + k]);
+    mine[k] = v;
+  }
+  GS_HIP(hipMemcpyAsync(recv, mine.data(), n * 8, hipMemcpyHostToDevice, s));
+  GS_HIP(hipStreamSynchronize(s));
+}
+void coll_group_start(gs_comm* cm) {
+  if (!cm->has_ops) {
+    GS_NCCL(rccl()->GroupStart());
+    return;
+  }
+  cm->xs.clear();
+  cm->xr.clear();
+  cm->xstream = nullptr;
+}
+void coll_Send(gs_comm* cm, const void* buf, size_t count, ncclDataType_t t, int peer, hipStream_t s) {
+  if (!cm->has_ops) {
+    GS_NCCL(rccl()->Send(buf, count, t, peer, cm->nc, s));
+    return;
+  }
+  cm->xs.push_back({buf, nullptr, (uint64_t)count * type_bytes(t), peer});
+  cm->xstream = s;
+}
+void coll_Recv(gs_comm* cm, void* buf, size_t count, ncclDataType_t t, int peer, hipStream_t s) {
+  if (!cm->has_ops) {
+    GS_NCCL(rccl()->Recv(buf, count, t, peer, cm->nc, s));
+    return;
+  }
+  cm->xr.push_back({nullptr, buf, (uint64_t)count * type_bytes(t), peer});
+  cm->xstream = s;
+}
+// ops: the group's sends concatenated per peer in call order (the receiver's
+// recvs from that peer split the bytes in its own call order, as RCCL matches
+// a group's point-to-point calls per peer), one exchange, the recvs scattered
+void coll_group_end(gs_comm* cm) {
+  if (!cm->has_ops) {
+    GS_NCCL(rccl()->GroupEnd());
+    return;
+  }
+  const uint32_t P = cm->nranks;
+  std::vector<std::vector<uint8_t>> sb(P), rb(P);
+  std::vector<uint64_t> sn(P, 0), rn(P, 0);
+  for (const auto& x : cm->xs) sn[x.peer] += x.bytes;
+  for (const auto& x : cm->xr) rn[x.peer] += x.bytes;
+  hipStream_t s = cm->xstream;
+  for (uint32_t p = 0; p < P; p++) {
+    sb[p].resize(sn[p]);
+    rb[p].resize(rn[p]);
+  }
+  std::vector<uint64_t> at(P, 0);
+  for (const auto& x : cm->xs) {
+    if (x.bytes) GS_HIP(hipMemcpyAsync(sb[x.peer].data() + at[x.peer], x.src, x.bytes, hipMemcpyDeviceToHost, s));
+    at[x.peer] += x.bytes;
+  }
+  if (s) GS_HIP(hipStreamSynchronize(s));
+  std::vector<const void*> sp(P);
+  std::vector<void*> rp(P);
+  for (uint32_t p = 0; p < P; p++) {
+    sp[p] = sb[p].data();
+    rp[p] = rb[p].data();
+  }
+  ops_fail(cm->ops.exchange(cm->ops.user, sp.data(), sn.data(), rp.data(), rn.data()), "exchange");
+  std::fill(at.begin(), at.end(), 0);
+  for (const auto& x : cm->xr) {
+    if (x.bytes) GS_HIP(hipMemcpyAsync(x.dst, rb[x.peer].data() + at[x.peer], x.bytes, hipMemcpyHostToDevice, s));
+    at[x.peer] += x.bytes;
+  }
+  if (s) GS_HIP(hipStreamSynchronize(s));
+  cm->xs.clear();
+  cm->xr.clear();
+}
+
+}  // namespace
+}  // namespace gs
 
 extern "C" gs_status gs_comm_get_id(gs_comm_id* out) {
   static_assert(sizeof(gs_comm_id) == sizeof(ncclUniqueId), "gs_comm_id must hold an ncclUniqueId");
@@ -142,6 +274,65 @@ extern "C" gs_status gs_comm_init_local(uint32_t nparts, gs_comm** out) {
   return GS_OK;
 }
 
+extern "C" gs_status gs_comm_init_ops(uint32_t nranks, uint32_t rank, const gs_comm_ops* ops, int32_t device,
+                                      gs_comm** out) {
+  if (!out || !ops || !ops->allgather || !ops->exchange || nranks < 1 || nranks > 64 || rank >= nranks)
+    return GS_EINVAL;
+  *out = nullptr;
+  gs_comm* c = new (std::nothrow) gs_comm();
+  if (!c) return GS_ENOMEM;
+  c->has_ops = true;
+  c->ops = *ops;
+  c->nranks = nranks;
+  c->rank = rank;
+  c->device = device;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) == hipSuccess && device >= 0 && device < ndev) {  // (gs_comm_check needs none)
+    if (hipSetDevice(device) != hipSuccess ||
+        hipMalloc((void**)&c->d_scratch, ((size_t)nranks * nranks + 1 + 4 * (size_t)nranks) * 8) != hipSuccess) {
+      delete c;
+      return GS_EDEVICE;
+    }
+  }
+  *out = c;
+  return GS_OK;
+}
+
+// Host-only check of the caller's transport: the words and bytes every rank
+// must see, from a position hash (sender, receiver, byte index).
+extern "C" gs_status gs_comm_check(gs_comm* c) {
+  if (!c) return GS_EINVAL;
+  if (!c->has_ops) return GS_OK;
+  const uint32_t P = c->nranks, me = c->rank;
+  const uint64_t mine[2] = {me, P};
+  std::vector<uint64_t> all(2 * (size_t)P);
+  if (c->ops.allgather(c->ops.user, mine, 2, all.data())) return GS_EDEVICE;
+  for (uint32_t p = 0; p < P; p++)
+    if (all[2 * p] != p || all[2 * p + 1] != P) return GS_EDEVICE;
+  auto len = [](uint32_t s, uint32_t d) { return s == d ? 0ull : 1ull + 977ull * (s + 3ull * d); };
+  auto byte = [](uint32_t s, uint32_t d, uint64_t i) {
+    return (uint8_t)(((i + 1) * 0x9E3779B97F4A7C15ull ^ ((uint64_t)s << 40) ^ ((uint64_t)d << 20)) >> 56);
+  };
+  std::vector<std::vector<uint8_t>> sb(P), rb(P);
+  std::vector<uint64_t> sn(P), rn(P);
+  std::vector<const void*> sp(P);
+  std::vector<void*> rp(P);
+  for (uint32_t p = 0; p < P; p++) {
+    sn[p] = len(me, p);
+    rn[p] = len(p, me);
+    sb[p].resize(sn[p]);
+    for (uint64_t i = 0; i < sn[p]; i++) sb[p][i] = byte(me, p, i);
+    rb[p].assign(rn[p], 0);
+    sp[p] = sb[p].data();
+    rp[p] = rb[p].data();
+  }
+  if (c->ops.exchange(c->ops.user, sp.data(), sn.data(), rp.data(), rn.data())) return GS_EDEVICE;
+  for (uint32_t p = 0; p < P; p++)
+    for (uint64_t i = 0; i < rn[p]; i++)
+      if (rb[p][i] != byte(p, me, i)) return GS_EDEVICE;
+  return GS_OK;
+}
+
 extern "C" gs_status gs_comm_destroy(gs_comm* c) {
   if (!c) return GS_EINVAL;
   if (c->nc) {
@@ -169,11 +360,10 @@ uint64_t rccl_piece_bytes() {  // read per bucket: tests change it between runs
 // on that rank).
 void rank_status(gs_comm* cm, Ctx& c, uint64_t mine) {
   if (cm->local) return;
-  Rccl* r = rccl();
   uint64_t* w = cm->d_scratch + (size_t)cm->nranks * cm->nranks;
   c.h_pinned[0] = mine;
   GS_HIP(hipMemcpyAsync(w, c.h_pinned, 8, hipMemcpyHostToDevice, c.stream));
-  GS_NCCL(r->AllReduce(w, w, 1, ncclUint64, ncclMax, cm->nc, c.stream));
+  coll_AllReduce(cm, w, w, 1, ncclUint64, ncclMax, c.stream);
   GS_HIP(hipMemcpyAsync(c.h_pinned, w, 8, hipMemcpyDeviceToHost, c.stream));
   GS_HIP(hipStreamSynchronize(c.stream));
   if (c.h_pinned[0] && !mine) throw Error(GS_EINVAL, "another rank failed this partitioned call");
@@ -184,7 +374,6 @@ void rank_status(gs_comm* cm, Ctx& c, uint64_t mine) {
 // MAX of each word agree) before the first batch.
 void check_same_config(gs_comm* cm, Ctx& c, const gs_publish* sched, uint64_t n_msgs) {
   if (cm->local) return;
-  Rccl* r = rccl();
   uint64_t h = 1469598103934665603ull;  // FNV-1a over the schedule
   for (uint64_t i = 0; i < n_msgs; i++) {
     const uint64_t v[4] = {sched[i].t_pub_ns, sched[i].publisher, sched[i].msg_size, sched[i].frags};
@@ -197,8 +386,8 @@ void check_same_config(gs_comm* cm, Ctx& c, const gs_publish* sched, uint64_t n_
   memcpy(c.h_pinned, sig, sizeof sig);
   GS_HIP(hipMemcpyAsync(d.p, c.h_pinned, sizeof sig, hipMemcpyHostToDevice, c.stream));
   GS_HIP(hipMemcpyAsync(d.p + 8, c.h_pinned, sizeof sig, hipMemcpyHostToDevice, c.stream));
-  GS_NCCL(r->AllReduce(d.p, d.p, 8, ncclUint64, ncclMin, cm->nc, c.stream));
-  GS_NCCL(r->AllReduce(d.p + 8, d.p + 8, 8, ncclUint64, ncclMax, cm->nc, c.stream));
+  coll_AllReduce(cm, d.p, d.p, 8, ncclUint64, ncclMin, c.stream);
+  coll_AllReduce(cm, d.p + 8, d.p + 8, 8, ncclUint64, ncclMax, c.stream);
   GS_HIP(hipMemcpyAsync(c.h_pinned, d.p, 16 * 8, hipMemcpyDeviceToHost, c.stream));
   GS_HIP(hipStreamSynchronize(c.stream));
   for (int k = 0; k < 8; k++)
@@ -212,7 +401,7 @@ void rank_gather(gs_comm* cm, Ctx& c, const uint64_t* mine, uint32_t n, uint64_t
   uint64_t* w = cm->d_scratch + (size_t)cm->nranks * cm->nranks + 1;
   memcpy(c.h_pinned + 16, mine, n * 8);
   GS_HIP(hipMemcpyAsync(w + (size_t)cm->rank * n, c.h_pinned + 16, n * 8, hipMemcpyHostToDevice, c.stream));
-  GS_NCCL(rccl()->AllGather(w + (size_t)cm->rank * n, w, n, ncclUint64, cm->nc, c.stream));
+  coll_AllGather(cm, w + (size_t)cm->rank * n, w, n, ncclUint64, c.stream);
   std::vector<uint64_t> h((size_t)cm->nranks * n);
   GS_HIP(hipMemcpyAsync(h.data(), w, h.size() * 8, hipMemcpyDeviceToHost, c.stream));
   GS_HIP(hipStreamSynchronize(c.stream));
@@ -302,7 +491,6 @@ void run_batch_ms(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched,
     }
   } else {
     Ctx& c = *cx[0];
-    Rccl* rc = rccl();
     const uint32_t me = cm->rank, mme = lay.mn(me), unme = lay.un(me);
     GS_HIP(hipSetDevice(c.cfg.device));
     // pack: destination r's block [mme][un_r] at lay.ms_send_off(me, r)
@@ -319,22 +507,22 @@ void run_batch_ms(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched,
     c.d_tc_t.alloc((size_t)unme * B);
     c.d_hops_t.alloc((size_t)unme * B);
     const uint64_t pb = rccl_piece_bytes(), p8 = std::max<uint64_t>(1, pb / 8);
-    GS_NCCL(rc->GroupStart());
+    coll_group_start(cm);
     for (uint32_t r = 0; r < P; r++) {
       const uint64_t n = lay.ms_count(me, r), off = lay.ms_send_off(me, r);
       for (uint64_t k = 0; k < n; k += p8)
-        GS_NCCL(rc->Send(c.d_ms_send.p + off + k, std::min(p8, n - k), ncclUint64, (int)r, cm->nc, c.stream));
+        coll_Send(cm, c.d_ms_send.p + off + k, std::min(p8, n - k), ncclUint64, (int)r, c.stream);
       for (uint64_t k = 0; k < n; k += pb)
-        GS_NCCL(rc->Send(c.d_ms_sendh.p + off + k, std::min(pb, n - k), ncclUint8, (int)r, cm->nc, c.stream));
+        coll_Send(cm, c.d_ms_sendh.p + off + k, std::min(pb, n - k), ncclUint8, (int)r, c.stream);
     }
     for (uint32_t p = 0; p < P; p++) {
       const uint64_t n = lay.ms_count(p, me), off = lay.ms_recv_off(p, me);
       for (uint64_t k = 0; k < n; k += p8)
-        GS_NCCL(rc->Recv(c.d_tc_t.p + off + k, std::min(p8, n - k), ncclUint64, (int)p, cm->nc, c.stream));
+        coll_Recv(cm, c.d_tc_t.p + off + k, std::min(p8, n - k), ncclUint64, (int)p, c.stream);
       for (uint64_t k = 0; k < n; k += pb)
-        GS_NCCL(rc->Recv(c.d_hops_t.p + off + k, std::min(pb, n - k), ncclUint8, (int)p, cm->nc, c.stream));
+        coll_Recv(cm, c.d_hops_t.p + off + k, std::min(pb, n - k), ncclUint8, (int)p, c.stream);
     }
-    GS_NCCL(rc->GroupEnd());
+    coll_group_end(cm);
     GS_HIP(hipStreamSynchronize(c.stream));
   }
   // 3. own peers' rows into the sinks
@@ -382,7 +570,6 @@ void gossip_to_ms(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched,
 bool run_batch_lp(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched, uint64_t i0, uint32_t B,
                   const gs_result_sink* sinks) {
   const uint32_t P = cm->nranks, N = cx[0]->cfg.peers;
-  Rccl* r = cm->local ? nullptr : rccl();
   std::vector<uint64_t> smin(nctx, INF64);
   uint64_t bad = 0;  // some part cannot take the batch on the list pass
   for (uint32_t i = 0; i < nctx; i++) {
@@ -513,33 +700,33 @@ bool run_batch_lp(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched,
       } else {
         Ctx& c = *cx[0];
         const uint32_t me = cm->rank;
-        GS_NCCL(r->AllGather(c.d_pkcur.p, cm->d_scratch, P, ncclUint64, cm->nc, c.stream));  // row p: p's counts
+        coll_AllGather(cm, c.d_pkcur.p, cm->d_scratch, P, ncclUint64, c.stream);  // row p: p's counts
         GS_HIP(hipMemcpyAsync(route.data(), cm->d_scratch, (size_t)P * P * 8, hipMemcpyDeviceToHost, c.stream));
         GS_HIP(hipStreamSynchronize(c.stream));
         lp_route_bases(route.data(), P, me, bq.data());
         const uint64_t piece = std::max<uint64_t>(1, rccl_piece_bytes() / RB);
         const uint64_t mycap = std::max<uint64_t>(cnt[me], 1);
         const uint32_t myun = lay.un(me);
-        GS_NCCL(r->GroupStart());
+        coll_group_start(cm);
         for (uint32_t d = 0; d < P; d++) {
           if (d == me) continue;
           const uint64_t n = route[(size_t)me * P + d];
           const uint64_t* src = c.d_rsend.p + (size_t)d * mycap;
           for (uint64_t k = 0; k < n; k += piece)
-            GS_NCCL(r->Send(src + k, std::min(piece, n - k), ncclUint64, (int)d, cm->nc, c.stream));
-          GS_NCCL(r->Send(c.d_rrcg.p + (size_t)d * myun, myun, ncclUint32, (int)d, cm->nc, c.stream));
-          GS_NCCL(r->Send(c.d_rroff.p + (size_t)d * myun, myun, ncclUint64, (int)d, cm->nc, c.stream));
+            coll_Send(cm, src + k, std::min(piece, n - k), ncclUint64, (int)d, c.stream);
+          coll_Send(cm, c.d_rrcg.p + (size_t)d * myun, myun, ncclUint32, (int)d, c.stream);
+          coll_Send(cm, c.d_rroff.p + (size_t)d * myun, myun, ncclUint64, (int)d, c.stream);
         }
         for (uint32_t sr = 0; sr < P; sr++) {
           if (sr == me) continue;
           const uint64_t n = route[(size_t)sr * P + me];
           const uint32_t u0 = lay.u0(sr), un = lay.un(sr);
           for (uint64_t k = 0; k < n; k += piece)
-            GS_NCCL(r->Recv(c.d_rpk.p + bq[sr] + k, std::min(piece, n - k), ncclUint64, (int)sr, cm->nc, c.stream));
-          GS_NCCL(r->Recv(c.d_rcg.p + u0, un, ncclUint32, (int)sr, cm->nc, c.stream));
-          GS_NCCL(r->Recv(c.d_roffg.p + u0, un, ncclUint64, (int)sr, cm->nc, c.stream));
+            coll_Recv(cm, c.d_rpk.p + bq[sr] + k, std::min(piece, n - k), ncclUint64, (int)sr, c.stream);
+          coll_Recv(cm, c.d_rcg.p + u0, un, ncclUint32, (int)sr, c.stream);
+          coll_Recv(cm, c.d_roffg.p + u0, un, ncclUint64, (int)sr, c.stream);
         }
-        GS_NCCL(r->GroupEnd());
+        coll_group_end(cm);
         part_lp_route_fix(c, P, me, bq.data());
       }
       continue;
@@ -574,23 +761,23 @@ bool run_batch_lp(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched,
       const uint64_t piece = std::max<uint64_t>(1, rccl_piece_bytes() / RB);
       const uint64_t myn = cnt[me], myu0 = lay.u0(me), myun = lay.un(me);
       const uint64_t* mine = c.d_rpk.p + base[me];  // packed in place (part_lp_pack): the own range stays
-      GS_NCCL(r->GroupStart());
+      coll_group_start(cm);
       for (uint32_t d = 0; d < P; d++) {
         if (d == me) continue;
         for (uint64_t k = 0; k < myn; k += piece)
-          GS_NCCL(r->Send(mine + k, std::min(piece, myn - k), ncclUint64, (int)d, cm->nc, c.stream));
-        GS_NCCL(r->Send(c.d_rcg.p + myu0, myun, ncclUint32, (int)d, cm->nc, c.stream));
-        GS_NCCL(r->Send(c.d_roffg.p + myu0, myun, ncclUint64, (int)d, cm->nc, c.stream));
+          coll_Send(cm, mine + k, std::min(piece, myn - k), ncclUint64, (int)d, c.stream);
+        coll_Send(cm, c.d_rcg.p + myu0, myun, ncclUint32, (int)d, c.stream);
+        coll_Send(cm, c.d_roffg.p + myu0, myun, ncclUint64, (int)d, c.stream);
       }
       for (uint32_t sr = 0; sr < P; sr++) {
         if (sr == me) continue;
         const uint64_t n = cnt[sr], u0 = lay.u0(sr), un = lay.un(sr);
         for (uint64_t k = 0; k < n; k += piece)
-          GS_NCCL(r->Recv(c.d_rpk.p + base[sr] + k, std::min(piece, n - k), ncclUint64, (int)sr, cm->nc, c.stream));
-        GS_NCCL(r->Recv(c.d_rcg.p + u0, un, ncclUint32, (int)sr, cm->nc, c.stream));
-        GS_NCCL(r->Recv(c.d_roffg.p + u0, un, ncclUint64, (int)sr, cm->nc, c.stream));
+          coll_Recv(cm, c.d_rpk.p + base[sr] + k, std::min(piece, n - k), ncclUint64, (int)sr, c.stream);
+        coll_Recv(cm, c.d_rcg.p + u0, un, ncclUint32, (int)sr, c.stream);
+        coll_Recv(cm, c.d_roffg.p + u0, un, ncclUint64, (int)sr, c.stream);
       }
-      GS_NCCL(r->GroupEnd());
+      coll_group_end(cm);
     }
   }
   for (uint32_t i = 0; i < nctx; i++) {  // pass times (timing on)
@@ -641,7 +828,6 @@ void run_batch(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched, ui
   if (cx[0]->cfg.lazy_gossip) save_counters(cx, nctx);
   if (run_batch_lp(cm, cx, nctx, sched, i0, B, sinks)) return;
   const uint32_t P = cm->nranks;
-  Rccl* r = cm->local ? nullptr : rccl();
   std::vector<uint64_t> key0(nctx);
   if (cm->local) {
     for (uint32_t i = 0; i < nctx; i++) {
@@ -672,7 +858,7 @@ void run_batch(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched, ui
     }
   };
   if (cm->local) host_min_to_ctrl(*std::min_element(key0.begin(), key0.end()));
-  else GS_NCCL(r->AllReduce(cx[0]->d_ctrl.p, cx[0]->d_ctrl.p, 1, ncclUint64, ncclMin, cm->nc, cx[0]->stream));
+  else coll_AllReduce(cm, cx[0]->d_ctrl.p, cx[0]->d_ctrl.p, 1, ncclUint64, ncclMin, cx[0]->stream);
   // timing (gs_set_timing): per part and bucket three events on its stream —
   // bucket start, scan + counts done (scan_ms), relax done (frontier_ms: the
   // routed export, the exchange and the receive-side relaxation)
@@ -707,7 +893,7 @@ void run_batch(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched, ui
       key = ctl[0];
     } else {
       Ctx& c = *cx[0];
-      GS_NCCL(r->AllGather(c.d_dcnt.p, cm->d_scratch, P, ncclUint64, cm->nc, c.stream));
+      coll_AllGather(cm, c.d_dcnt.p, cm->d_scratch, P, ncclUint64, c.stream);
       GS_HIP(hipMemcpyAsync(mat.data(), cm->d_scratch, (size_t)P * P * 8, hipMemcpyDeviceToHost, c.stream));
       GS_HIP(hipMemcpyAsync(&ctl[0], c.d_ctrl.p, 8, hipMemcpyDeviceToHost, c.stream));
       GS_HIP(hipStreamSynchronize(c.stream));
@@ -751,21 +937,21 @@ void run_batch(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched, ui
       // pieces of at most rccl_piece_bytes(); both ends cut the
       // same count the same way
       const uint64_t piece = std::max<uint64_t>(1, rccl_piece_bytes() / RB);
-      GS_NCCL(r->GroupStart());
+      coll_group_start(cm);
       uint64_t soff = 0, roff = 0;
       for (uint32_t d = 0; d < P; d++) {
         const uint64_t n = mat[(size_t)me * P + d];
         for (uint64_t k = 0; k < n; k += piece)
-          GS_NCCL(r->Send(c.d_pout.p + soff + k, std::min(piece, n - k) * RB, ncclUint8, (int)d, cm->nc, c.stream));
+          coll_Send(cm, c.d_pout.p + soff + k, std::min(piece, n - k) * RB, ncclUint8, (int)d, c.stream);
         soff += n;
       }
       for (uint32_t s = 0; s < P; s++) {
         const uint64_t n = mat[(size_t)s * P + me];
         for (uint64_t k = 0; k < n; k += piece)
-          GS_NCCL(r->Recv(c.d_pin.p + roff + k, std::min(piece, n - k) * RB, ncclUint8, (int)s, cm->nc, c.stream));
+          coll_Recv(cm, c.d_pin.p + roff + k, std::min(piece, n - k) * RB, ncclUint8, (int)s, c.stream);
         roff += n;
       }
-      GS_NCCL(r->GroupEnd());
+      coll_group_end(cm);
     }
     // 4. relax into own peers; next bucket = MIN over parts
     for (uint32_t i = 0; i < nctx; i++) {
@@ -781,7 +967,7 @@ void run_batch(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched, ui
       for (uint32_t i = 0; i < nctx; i++) GS_HIP(hipStreamSynchronize(cx[i]->stream));
       host_min_to_ctrl(*std::min_element(ctl.begin(), ctl.end()));
     } else {
-      GS_NCCL(r->AllReduce(cx[0]->d_ctrl.p, cx[0]->d_ctrl.p, 1, ncclUint64, ncclMin, cm->nc, cx[0]->stream));
+      coll_AllReduce(cm, cx[0]->d_ctrl.p, cx[0]->d_ctrl.p, 1, ncclUint64, ncclMin, cx[0]->stream);
     }
   }
   for (uint32_t i = 0; i < nctx; i++) {  // bucket times (the loop ended on a stream sync)
@@ -816,8 +1002,7 @@ void run_batch(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched, ui
     Ctx& c = *cx[0];
     c.h_pinned[0] = ok ? 1 : 0;
     GS_HIP(hipMemcpyAsync(cm->d_scratch + (size_t)P * P, c.h_pinned, 8, hipMemcpyHostToDevice, c.stream));
-    GS_NCCL(r->AllReduce(cm->d_scratch + (size_t)P * P, cm->d_scratch + (size_t)P * P, 1, ncclUint64, ncclMin, cm->nc,
-                         c.stream));
+    coll_AllReduce(cm, cm->d_scratch + (size_t)P * P, cm->d_scratch + (size_t)P * P, 1, ncclUint64, ncclMin, c.stream);
     GS_HIP(hipMemcpyAsync(c.h_pinned, cm->d_scratch + (size_t)P * P, 8, hipMemcpyDeviceToHost, c.stream));
     GS_HIP(hipStreamSynchronize(c.stream));
     ok = c.h_pinned[0] != 0;

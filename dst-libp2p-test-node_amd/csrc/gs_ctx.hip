@@ -18,6 +18,9 @@ Ctx::~Ctx() {
   for (auto e : blk_ev)
     if (e) (void)hipEventDestroy(e);
   if (side) (void)hipStreamDestroy(side);
+  if (chain) (void)hipStreamDestroy(chain);
+  for (auto e : chain_ev)
+    if (e) (void)hipEventDestroy(e);
   for (int k = 0; k < 2; k++) {
     if (lat_src[k]) (void)hipEventDestroy(lat_src[k]);
     if (lat_done[k]) (void)hipEventDestroy(lat_done[k]);

@@ -81,6 +81,10 @@ struct Ctx {
   std::string last_error;
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;           // second stream: churn IHAVE lists beside the epoch steps
+  // churn: the epoch chain's own stream, restricted to GS_CHAIN_CUS compute units
+  // (hipExtStreamCreateWithCUMask), and its join events
+  hipStream_t chain = nullptr;
+  hipEvent_t chain_ev[2] = {nullptr, nullptr};
   std::vector<hipEvent_t> side_ev;      // its chunk events
   bool timing = false;
   bool traffic = false;        // gs_set_traffic: per-peer send/receive counters
@@ -300,6 +304,14 @@ struct Ctx {
 // ---- launchers (gs_topology.hip / gs_mesh.hip / gs_relax.hip) ----
 void launch_topology(Ctx& c);
 uint32_t run_mesh(Ctx& c, uint32_t max_heartbeats);
+inline void ensure_cus(Ctx& c) {
+  if (c.num_cus == 0) {
+    hipDeviceProp_t prop;
+    c.num_cus = hipGetDeviceProperties(&prop, c.cfg.device) == hipSuccess ? prop.multiProcessorCount : 256;
+  }
+}
+hipStream_t cu_stream(Ctx& c, uint32_t c0, uint32_t n);
+hipStream_t cu_stream_except(Ctx& c, uint32_t c0, uint32_t stride);
 void churn_ring(Ctx& c, uint64_t h_lo, uint64_t h_hi);
 void ensure_csrpos(Ctx& c);
 void ensure_in_lists(Ctx& c, uint64_t h0, uint64_t h1);

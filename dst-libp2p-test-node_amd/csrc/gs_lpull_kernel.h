@@ -1810,85 +1810,127 @@ __global__ __launch_bounds__(TB) void k_lpack(const uint64_t* __restrict__ rec, 
   }
 }
 
-// Routed record packing (gs_run_partitioned's default exchange, DESIGN.md
-// §5.2; gs_layout.h lp_route_bases): this part's records of a pass, for every
-// destination part q the records with a receiver q owns (a bit of the
-// record's inclusion mask at a mesh position whose peer is in q; the own part
-// gets every record), each row's records contiguous and in emission order.
-// Pass 1 counts per (row, destination); one claim per wave and destination
-// reserves the space (cursor[q]); pass 2 copies. Own part: into the gathered
-// buffer at base 0 (out_own) with the global offset tables at its peers
-// (roff_own / rcg_own); other parts: out[q * cap ..] with per-destination
-// tables roff[q * un + r] (relative to the segment) / rcg[q * un + r]. One
-// wave per 64 rows, P <= LP_PMAX.
+// Routed record packing (GS_PART_ROUTE; gs_layout.h
+// lp_route_bases): this part's records of a pass, for every destination part q
+// the records with a receiver q owns (a bit of the record's inclusion mask at
+// a mesh position whose peer is in q; the own part gets every record), each
+// row's records contiguous and in emission order. One wave per 64 rows, the
+// rows' records walked as one sequence 64 at a time (lane -> record), P <= LP_PMAX:
+//  0. lane = row: the owning part of each mesh entry, once per row, by
+//     comparing the peer with the parts' first peers (own64: 4 bits per entry);
+//  1. lane = record: its destination set dm (one bit per part: the owners of
+//     the mask's receivers, plus the own part); per destination a ballot, and
+//     the last lane of each row's run of lanes adds the run's count to LDS;
+//  2. one claim per (wave, destination) reserves the space (cursor[q]); the
+//     per-row offset / count tables are written;
+//  3. lane = record again: per destination its position = the row's write
+//     position + the run's lanes below it with that bit; the run's last lane
+//     advances the row's position.
+// A lane finds its record's row from the rows that start inside the chunk (a
+// ballot of the row starts + one LDS lookup), not by a search over the rows.
+// Own part: into the gathered buffer at base 0 (out_own) with the global
+// offset tables at its peers (roff_own / rcg_own); other parts: out[q * cap ..]
+// with per-destination tables roff[q * un + r] (relative to the segment) /
+// rcg[q * un + r].
 constexpr uint32_t LP_PMAX = 16;
+struct RouteLo {
+  uint32_t lo[LP_PMAX];  // lo[q]: the first peer of part q (gs_layout.h u0)
+};
 __global__ __launch_bounds__(TB) void k_lpack_route(const uint64_t* __restrict__ rec, const uint32_t* __restrict__ cnt,
                                                     const uint32_t* __restrict__ mesh, uint32_t u0, uint32_t un,
-                                                    uint32_t L, uint32_t N, uint32_t P, uint32_t me, uint64_t cap,
+                                                    uint32_t L, uint32_t P, uint32_t me, uint64_t cap,
                                                     uint64_t* __restrict__ out, uint64_t* __restrict__ out_own,
                                                     uint64_t* __restrict__ roff, uint32_t* __restrict__ rcg,
                                                     uint64_t* __restrict__ roff_own, uint32_t* __restrict__ rcg_own,
-                                                    unsigned long long* cursor) {
-  __shared__ uint32_t smq[TB / 64][64][LP_PMAX];  // per row: the inclusion-mask bits of each part's receivers
+                                                    unsigned long long* cursor, RouteLo rl) {
+  __shared__ uint64_t sown[TB / 64][64];          // per row: the owning part of each mesh entry (4 bits each)
   __shared__ uint32_t sco[TB / 64][64][LP_PMAX];  // per row and destination: count, then next write position
-  __shared__ uint32_t spre[TB / 64][65];          // exclusive prefix of the rows' record counts
+  __shared__ uint32_t spre[TB / 64][64];          // exclusive prefix of the rows' record counts
+  __shared__ uint8_t srow[TB / 64][64];           // chunk lane -> the row whose records start there
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t wave = blockIdx.x * (TB / 64) + wv, nw = gridDim.x * (TB / 64);
-  constexpr uint32_t IM = ((1u << MESH_W) - 1u) << LP_IM_SHIFT;
+  const uint64_t upto = lane == 63 ? ~0ull : (2ull << lane) - 1;  // lanes <= this one
+  const uint64_t below = (1ull << lane) - 1;
   for (uint32_t r0 = wave * 64; r0 < un; r0 += nw * 64) {
-    // lane j: row r0 + j — its record count, and each part's receivers as mask bits
+    // 0. lane j: row r0 + j — its record count and the owners of its mesh entries
     const uint32_t r = r0 + (uint32_t)lane;
     const bool rv = r < un;
     const uint32_t n = rv ? cnt[r] : 0u;
-    uint32_t e[MESH_W];
-    {
-      const uint4* mp = reinterpret_cast<const uint4*>(mesh + (size_t)(u0 + (rv ? r : 0u)) * MESH_W);
+    uint64_t own = 0;
+    if (rv) {
+      const uint4* mp = reinterpret_cast<const uint4*>(mesh + (size_t)(u0 + r) * MESH_W);
 #pragma unroll
-      for (int k = 0; k < (int)MESH_W / 4; k++) {
-        const uint4 m = rv ? mp[k] : make_uint4(EMPTY, EMPTY, EMPTY, EMPTY);
-        e[4 * k] = m.x; e[4 * k + 1] = m.y; e[4 * k + 2] = m.z; e[4 * k + 3] = m.w;
+      for (int k4 = 0; k4 < (int)MESH_W / 4; k4++) {
+        const uint4 m = mp[k4];
+        const uint32_t e4[4] = {m.x, m.y, m.z, m.w};
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const uint32_t x = e4[u] & 0xFFFFFFu;  // (EMPTY entries: never a receiver bit)
+          uint32_t o = 0;
+          for (uint32_t q = 1; q < P; q++) o += x >= rl.lo[q] ? 1u : 0u;  // wave-uniform bound
+          own |= (uint64_t)o << (4 * (4 * k4 + u));
+        }
       }
     }
-    for (uint32_t q = 0; q < P; q++) {
-      uint32_t m = 0;
-#pragma unroll
-      for (int k = 0; k < (int)MESH_W; k++) {
-        const uint32_t pe = e[k] == EMPTY ? ~0u : (uint32_t)((((uint64_t)(e[k] & 0xFFFFFFu) + 1) * P - 1) / N);
-        m |= pe == q ? 1u << (LP_IM_SHIFT + k) : 0u;
-      }
-      smq[wv][lane][q] = m;
-      sco[wv][lane][q] = 0;
-    }
+    sown[wv][lane] = own;
+    for (uint32_t q = 0; q < P; q++) sco[wv][lane][q] = 0;
     uint32_t x = n;  // inclusive prefix over the 64 rows
     for (int off = 1; off < 64; off <<= 1) {
       const uint32_t y = __shfl_up(x, off);
       if (lane >= off) x += y;
     }
-    spre[wv][lane] = x - n;
-    const uint32_t T = __shfl(x, 63);
-    if (lane == 63) spre[wv][64] = T;
-    wave_lds_sync();
-    // the records of the 64 rows as one sequence, 64 at a time: lane -> (row, index)
-    auto locate = [&](uint32_t t, uint32_t& j) {  // the row holding sequence position t (largest pre <= t)
-      uint32_t lo = 0, hi = 63;
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi + 1) >> 1;
-        if (spre[wv][mid] <= t) lo = mid; else hi = mid - 1;
-      }
-      j = lo;
+    const uint32_t pre = x - n, T = __shfl(x, 63);
+    spre[wv][lane] = pre;
+    // the record of lane `lane` in chunk t0: its row j, index i in the row, run [p0, last]
+    auto locate = [&](uint32_t t0, uint32_t jc, uint64_t& sm, uint32_t& j, uint32_t& i, uint32_t& p0) {
+      srow[wv][lane] = 0xFF;  // no row starts at this lane (yet)
+      wave_lds_sync();
+      const bool st = n && pre >= t0 && pre - t0 < 64;  // (row view) this row's records start in the chunk
+      if (st) srow[wv][pre - t0] = (uint8_t)lane;
+      wave_lds_sync();
+      const uint32_t here = srow[wv][lane];  // (record view) the row starting at this lane, or 0xFF
+      sm = __ballot(here != 0xFFu);          // bit l: a row's records start at chunk lane l
+      const uint64_t sb = sm & upto;
+      p0 = sb ? 63u - (uint32_t)__builtin_clzll(sb) : 0u;
+      j = sb ? (uint32_t)__shfl((int)here, (int)p0) : jc;
+      i = t0 + (uint32_t)lane - spre[wv][j];
     };
-    // 1. counts per (row, destination)
-    for (uint32_t t0 = 0; t0 < T; t0 += 64) {
-      const uint32_t t = t0 + (uint32_t)lane;
-      if (t < T) {
-        uint32_t j;
-        locate(t, j);
-        const uint32_t im = (uint32_t)rec[(size_t)(r0 + j) * L + (t - spre[wv][j])] & IM;
-        for (uint32_t q = 0; q < P; q++)
-          if (q == me || (im & smq[wv][j][q])) atomicAdd(&sco[wv][j][q], 1u);
+    // lanes [p0, lane] (run) and [p0, lane) (run below this lane)
+    auto runs = [&](uint32_t p0, uint64_t& run_le, uint64_t& run_lt) {
+      const uint64_t from = ~((1ull << p0) - 1);
+      run_le = upto & from;
+      run_lt = below & from;
+    };
+    constexpr uint32_t IM = ((1u << MESH_W) - 1u) << LP_IM_SHIFT;
+    auto dests = [&](uint32_t im, uint64_t ow) {  // the record's destination parts (+ the own part)
+      uint32_t dm = 1u << me, m = im >> LP_IM_SHIFT;
+      while (m) {
+        const uint32_t k = (uint32_t)__builtin_ctz(m);
+        m &= m - 1;
+        dm |= 1u << ((uint32_t)(ow >> (4 * k)) & 15u);
       }
-    }
+      return dm;
+    };
     wave_lds_sync();
+    // 1. counts per (row, destination)
+    uint32_t jc = 0;  // the row continuing into the chunk (its start lies before it)
+    for (uint32_t t0 = 0; t0 < T; t0 += 64) {
+      uint64_t sm, rle, rlt;
+      uint32_t j, i, p0;
+      locate(t0, jc, sm, j, i, p0);
+      runs(p0, rle, rlt);
+      const uint32_t t = t0 + (uint32_t)lane;
+      const bool v = t < T;
+      const uint32_t im = v ? (uint32_t)rec[(size_t)(r0 + j) * L + i] & IM : 0u;
+      const uint32_t dm = v ? dests(im, sown[wv][j]) : 0u;
+      const bool last = v && (lane == 63 || ((sm >> (lane + 1)) & 1) || t + 1 == T);
+      for (uint32_t q = 0; q < P; q++) {
+        const uint64_t bq = __ballot((dm >> q) & 1u);
+        if (last) sco[wv][j][q] += (uint32_t)__popcll(bq & rle);
+      }
+      jc = (uint32_t)__builtin_amdgcn_readlane((int)j, 63);
+      wave_lds_sync();  // (srow is rewritten by the next chunk)
+    }
     // 2. offsets: one claim per destination; sco becomes each (row, destination)'s write position
     for (uint32_t q = 0; q < P; q++) {
       const uint32_t c = sco[wv][lane][q];
@@ -1913,36 +1955,29 @@ __global__ __launch_bounds__(TB) void k_lpack_route(const uint64_t* __restrict__
       }
     }
     wave_lds_sync();
-    // 3. copy in emission order: within a chunk a row's records are a run of
-    //    lanes [s, e); the lanes of that run before this one, for destination q,
-    //    come first; the run's last lane advances the row's position
+    // 3. copy in emission order
+    jc = 0;
     for (uint32_t t0 = 0; t0 < T; t0 += 64) {
+      uint64_t sm, rle, rlt;
+      uint32_t j, i, p0;
+      locate(t0, jc, sm, j, i, p0);
+      runs(p0, rle, rlt);
       const uint32_t t = t0 + (uint32_t)lane;
       const bool v = t < T;
-      uint32_t j = 0, im = 0;
-      uint64_t xr = 0;
-      if (v) {
-        locate(t, j);
-        xr = rec[(size_t)(r0 + j) * L + (t - spre[wv][j])];
-        im = (uint32_t)xr & IM;
-      }
-      const uint32_t s0 = spre[wv][j] > t0 ? spre[wv][j] - t0 : 0u;             // the run's first lane
-      const uint32_t e0 = spre[wv][j + 1] - t0 < 64 ? spre[wv][j + 1] - t0 : 64u;  // one past its last
-      const uint64_t below = ((1ull << lane) - 1) & ~((1ull << s0) - 1);
+      const uint64_t xr = v ? rec[(size_t)(r0 + j) * L + i] : 0ull;
+      const uint32_t dm = v ? dests((uint32_t)xr & IM, sown[wv][j]) : 0u;
+      const bool last = v && (lane == 63 || ((sm >> (lane + 1)) & 1) || t + 1 == T);
       for (uint32_t q = 0; q < P; q++) {
-        const bool sel = v && (q == me || (im & smq[wv][j][q]));
-        const uint64_t bm = __ballot(sel);
-        const uint32_t base = v ? sco[wv][j][q] : 0u;
-        if (sel) (q == me ? out_own : out + (size_t)q * cap)[(uint64_t)base + (uint32_t)__popcll(bm & below)] = xr;
-        wave_lds_sync();  // (every lane read the position before the run's last lane moves it)
-        if (v && (uint32_t)lane + 1 == e0) {
-          const uint64_t run = e0 >= 64 ? ~0ull & ~((1ull << s0) - 1) : ((1ull << e0) - 1) & ~((1ull << s0) - 1);
-          sco[wv][j][q] = base + (uint32_t)__popcll(bm & run);
-        }
-        wave_lds_sync();
+        const bool sel = (dm >> q) & 1u;
+        const uint64_t bq = __ballot(sel);
+        if (!bq) continue;  // wave-uniform
+        const uint32_t base = v ? sco[wv][j][q] : 0u;  // read by the run's lanes before its last lane moves it
+        if (sel) (q == me ? out_own : out + (size_t)q * cap)[(uint64_t)base + (uint32_t)__popcll(bq & rlt)] = xr;
+        if (last) sco[wv][j][q] = base + (uint32_t)__popcll(bq & rle);
       }
+      jc = (uint32_t)__builtin_amdgcn_readlane((int)j, 63);
+      wave_lds_sync();
     }
-    wave_lds_sync();
   }
 }
 

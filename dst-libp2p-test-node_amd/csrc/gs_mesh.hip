@@ -921,25 +921,28 @@ __device__ __forceinline__ void row_apply_ev(const MeshArgs& a, uint32_t u, uint
       if ((uint32_t)(k * G + lane) < deg && (f[k] & F_MESH)) P[(size_t)PS_NBROFF * N + cw[k]] = 1;
 }
 
-// One step of an event-driven epoch. A block owns EV_ROWS consecutive rows:
+// One step of an event-driven epoch. A block owns 64 * SW consecutive rows:
 // its first wave tests them one thread per row and compacts the rows the step
 // can change into LDS; then every group of G lanes takes active rows (most
 // blocks have a handful, so one round). Steps:
 enum : int { EV_HB = 0, EV_GRAFT = 1, EV_APPLY = 2 };
-constexpr uint32_t EV_ROWS = 64;
-template <int G, int STEP>
+// SW scanning waves per block: a block owns 64 * SW rows (GS_EV_SW; the steps
+// are short, so the number of workgroups per launch matters, not only the rows)
+template <int G, int STEP, int SW>
 __global__ __launch_bounds__(TB) void k_ev_step(MeshArgs a, uint32_t* mesh, const uint32_t* mesh_prev) {
+  constexpr uint32_t RW = 64u * SW;
+  static_assert(SW >= 1 && 64 * SW <= TB, "scanning waves of the block");
   // per active row: id, CSR base, degree, the step's flags (loaded by the scan,
   // so a row's own work starts with its entries)
-  __shared__ uint32_t act[EV_ROWS], actd[EV_ROWS];
-  __shared__ uint64_t actb[EV_ROWS];
-  __shared__ uint8_t actf[EV_ROWS];
+  __shared__ uint32_t act[RW], actd[RW];
+  __shared__ uint64_t actb[RW];
+  __shared__ uint8_t actf[RW];
   __shared__ uint32_t nact;
   uint8_t* P = a.pst;
   const uint32_t N = a.N;
-  const uint32_t base = blockIdx.x * EV_ROWS;
+  const uint32_t base = blockIdx.x * RW;
   if (STEP == EV_APPLY) {  // unchanged rows keep their ELL row / mesh mask: copy the block's rows
-    const uint32_t nrow = base + EV_ROWS <= N ? EV_ROWS : N - base;
+    const uint32_t nrow = base + RW <= N ? RW : N - base;
     if (mesh && mesh_prev) {
       const uint4* src = reinterpret_cast<const uint4*>(mesh_prev + (size_t)base * MESH_W);
       uint4* dst = reinterpret_cast<uint4*>(mesh + (size_t)base * MESH_W);
@@ -948,7 +951,12 @@ __global__ __launch_bounds__(TB) void k_ev_step(MeshArgs a, uint32_t* mesh, cons
     if (a.mm_out && a.mm_prev)
       for (uint32_t i = threadIdx.x; i < nrow; i += TB) a.mm_out[base + i] = a.mm_prev[base + i];
   }
-  if (threadIdx.x < 64) {
+  if (SW > 1) {
+    if (threadIdx.x == 0) nact = 0;
+    __syncthreads();
+  }
+  if (threadIdx.x < 64 * SW) {
+    const uint32_t l = threadIdx.x & 63;
     const uint32_t u = base + threadIdx.x;
     bool on = false;
     uint32_t fl = 0;
@@ -974,14 +982,19 @@ __global__ __launch_bounds__(TB) void k_ev_step(MeshArgs a, uint32_t* mesh, cons
       }
     }
     const uint64_t bm = __ballot(on);
+    uint32_t q0 = 0;  // this wave's first slot (one wave: 0; else claimed in LDS, any order)
+    if (SW > 1) {
+      if (l == 0 && bm) q0 = atomicAdd(&nact, (uint32_t)__popcll(bm));
+      q0 = (uint32_t)__shfl((int)q0, 0);
+    }
     if (on) {
-      const uint32_t q = (uint32_t)__popcll(bm & ((1ull << threadIdx.x) - 1));
+      const uint32_t q = q0 + (uint32_t)__popcll(bm & ((1ull << l) - 1));
       act[q] = u;
       actb[q] = rb;
       actd[q] = (uint32_t)(re - rb);
       actf[q] = (uint8_t)fl;
     }
-    if (threadIdx.x == 0) nact = (uint32_t)__popcll(bm);
+    if (SW == 1 && threadIdx.x == 0) nact = (uint32_t)__popcll(bm);
     if (a.dbg) {  // diagnostic counts (GS_DEBUG_EV)
       uint32_t c[4] = {(uint32_t)__popcll(bm), 0, 0, 0};
       if (STEP == EV_HB && u < N) {
@@ -995,7 +1008,7 @@ __global__ __launch_bounds__(TB) void k_ev_step(MeshArgs a, uint32_t* mesh, cons
         c[2] = (uint32_t)__popcll(__ballot(false));
         c[3] = (uint32_t)__popcll(__ballot(false));
       }
-      if (threadIdx.x == 0)
+      if (l == 0)
         for (int q = 0; q < 4; q++)
           if (c[q]) atomicAdd(&a.dbg[STEP * 4 + q], (unsigned long long)c[q]);
     }
@@ -1176,11 +1189,22 @@ void ev_epochs(Ctx& c, MeshArgs a, uint64_t h0, uint64_t h1, bool ring) {
     c.num_cus = hipGetDeviceProperties(&prop, c.cfg.device) == hipSuccess ? prop.multiProcessorCount : 256;
   }
   const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(row_blocks(N, G), (uint64_t)c.num_cus * 8));
-  const unsigned sgrid = (unsigned)((N + EV_ROWS - 1) / EV_ROWS);
+  static const uint32_t ev_sw = [] {  // GS_EV_SW: scanning waves (rows / 64) per block of the steps
+    const char* e = getenv("GS_EV_SW");
+    const int v = e && *e ? atoi(e) : 1;
+    return (uint32_t)(v >= 4 ? 4 : v >= 2 ? 2 : 1);
+  }();
+  const unsigned sgrid = (unsigned)((N + 64 * ev_sw - 1) / (64 * ev_sw));
+#define GS_EVS1(SW, STEP, ...)                                                     \
+  do {                                                                             \
+    if (G == 16) k_ev_step<16, STEP, SW><<<sgrid, TB, 0, s>>>(__VA_ARGS__);        \
+    else k_ev_step<64, STEP, SW><<<sgrid, TB, 0, s>>>(__VA_ARGS__);                \
+  } while (0)
 #define GS_EVS(STEP, ...)                                                          \
   do {                                                                             \
-    if (G == 16) k_ev_step<16, STEP><<<sgrid, TB, 0, s>>>(__VA_ARGS__);            \
-    else k_ev_step<64, STEP><<<sgrid, TB, 0, s>>>(__VA_ARGS__);                    \
+    if (ev_sw == 4) GS_EVS1(4, STEP, __VA_ARGS__);                                 \
+    else if (ev_sw == 2) GS_EVS1(2, STEP, __VA_ARGS__);                            \
+    else GS_EVS1(1, STEP, __VA_ARGS__);                                            \
   } while (0)
   if (G == 16) k_ev_init<16><<<grid, TB, 0, s>>>(a);
   else k_ev_init<64><<<grid, TB, 0, s>>>(a);
@@ -1232,6 +1256,7 @@ void ev_epochs(Ctx& c, MeshArgs a, uint64_t h0, uint64_t h1, bool ring) {
     }
   }
 #undef GS_EVS
+#undef GS_EVS1
   GS_HIP(hipGetLastError());
   if (lists) {  // the context's stream continues once every list is written
     const hipEvent_t e = side_event(c, nev++);
@@ -1283,7 +1308,71 @@ void ensure_in_lists(Ctx& c, uint64_t h0, uint64_t h1) {
 // < ring_R): replay from the empty mesh when h_lo has left the ring, else run
 // the epochs after the current mesh state. Snapshot h = mesh after heartbeat h
 // with the offline bits of epoch h; epoch 0 is the empty mesh, all online.
+// A stream restricted to n compute units (bits [c0, c0 + n) of
+// hipExtStreamCreateWithCUMask's mask; GS_CU_STRIDE=s takes every s-th bit).
+hipStream_t cu_stream(Ctx& c, uint32_t c0, uint32_t n) {
+  ensure_cus(c);
+  const uint32_t total = (uint32_t)std::max(c.num_cus, 1);
+  const char* st = getenv("GS_CU_STRIDE");
+  const uint32_t stride = st && *st ? (uint32_t)std::max(1, atoi(st)) : 1u;
+  std::vector<uint32_t> mask((total + 31) / 32, 0u);
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t b = (c0 + i * stride) % total;
+    mask[b / 32] |= 1u << (b % 32);
+  }
+  hipStream_t s = nullptr;
+  GS_HIP(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+  return s;
+}
+
+// A stream on every CU except the bits c0, c0 + stride, ... (the complement of
+// cu_stream(c, c0, total / stride) with GS_CU_STRIDE = stride).
+hipStream_t cu_stream_except(Ctx& c, uint32_t c0, uint32_t stride) {
+  ensure_cus(c);
+  const uint32_t total = (uint32_t)std::max(c.num_cus, 1);
+  std::vector<uint32_t> mask((total + 31) / 32, 0u);
+  for (uint32_t b = 0; b < total; b++)
+    if (stride == 0 || b < c0 || (b - c0) % stride != 0) mask[b / 32] |= 1u << (b % 32);
+  hipStream_t s = nullptr;
+  GS_HIP(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+  return s;
+}
+
+// GS_CHAIN_CUS=n (experiment): the epoch chain of churn_ring on a stream of n CUs.
+static uint32_t chain_cus() {
+  const char* e = getenv("GS_CHAIN_CUS");
+  return e && *e ? (uint32_t)std::max(0, atoi(e)) : 0u;
+}
+
+static void churn_ring_on(Ctx& c, uint64_t h_lo, uint64_t h_hi);
 void churn_ring(Ctx& c, uint64_t h_lo, uint64_t h_hi) {
+  const uint32_t n = chain_cus();
+  if (!n) return churn_ring_on(c, h_lo, h_hi);
+  static uint32_t made = 0;  // (experiment: one mask per process)
+  if (!c.chain || made != n) {
+    if (c.chain) GS_HIP(hipStreamDestroy(c.chain));
+    c.chain = cu_stream(c, 0, n);
+    made = n;
+    for (auto& e : c.chain_ev)
+      if (e) GS_HIP(hipEventDestroy(e));
+    for (auto& e : c.chain_ev) GS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  hipStream_t main = c.stream;
+  GS_HIP(hipEventRecord(c.chain_ev[0], main));
+  GS_HIP(hipStreamWaitEvent(c.chain, c.chain_ev[0], 0));
+  c.stream = c.chain;  // every launch of the chain (and the hook's events) on the chain's CUs
+  try {
+    churn_ring_on(c, h_lo, h_hi);
+  } catch (...) {
+    c.stream = main;
+    throw;
+  }
+  c.stream = main;
+  GS_HIP(hipEventRecord(c.chain_ev[1], c.chain));
+  GS_HIP(hipStreamWaitEvent(main, c.chain_ev[1], 0));
+}
+
+static void churn_ring_on(Ctx& c, uint64_t h_lo, uint64_t h_hi) {
   const uint32_t N = c.cfg.peers, R = c.ring_R;
   const size_t w64 = ((size_t)N + 63) / 64;
   hipStream_t s = c.stream;

@@ -790,10 +790,13 @@ void part_lp_pack_route(Ctx& c, uint32_t P, uint32_t me, uint64_t mine) {
   const uint32_t nb = (c.part_lppass + 1) & 1;  // the last pass wrote lrec / lcnt [pass & 1]
   const unsigned grid = (unsigned)std::max<uint64_t>(
       1, std::min<uint64_t>(((uint64_t)un + 255) / 256, (uint64_t)c.num_cus * 8));
+  RouteLo rl{};
+  const PartLayout lay{P, c.cfg.peers, 0};
+  for (uint32_t q = 0; q < P && q < LP_PMAX; q++) rl.lo[q] = lay.u0(q);
   k_lpack_route<<<grid, TB, 0, s>>>(c.d_lrec.p + (size_t)nb * un * L, c.d_lcnt.p + (size_t)nb * un, c.d_mesh.p,
-                                    c.part_u0, un, L, c.cfg.peers, P, me, cap, c.d_rsend.p, c.d_rpk.p, c.d_rroff.p,
+                                    c.part_u0, un, L, P, me, cap, c.d_rsend.p, c.d_rpk.p, c.d_rroff.p,
                                     c.d_rrcg.p, c.d_roffg.p + c.part_u0, c.d_rcg.p + c.part_u0,
-                                    (unsigned long long*)c.d_pkcur.p);
+                                    (unsigned long long*)c.d_pkcur.p, rl);
   GS_HIP(hipGetLastError());
 }
 

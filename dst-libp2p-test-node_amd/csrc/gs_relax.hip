@@ -935,12 +935,6 @@ static void collect_stats(Ctx& c) {
             (unsigned long long)h[C_TSCANNED_G], (unsigned long long)h[C_GOSSIP]);
 }
 
-static void ensure_cus(Ctx& c) {
-  if (c.num_cus == 0) {
-    hipDeviceProp_t prop;
-    c.num_cus = hipGetDeviceProperties(&prop, c.cfg.device) == hipSuccess ? prop.multiProcessorCount : 256;
-  }
-}
 
 // One batch on the owner-computes path (gs_pull_kernel.h): seed, then passes in
 // chunks of 8 until a pass decides DONE (one host read of the ctrl slots per chunk).
@@ -1502,6 +1496,35 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       }
     }
   } async_off{c};
+  // GS_PASS_SKIP=k (experiment): this run's work on every CU but every k-th
+  // (the CUs GS_CHAIN_CUS with GS_CU_STRIDE=k gives the epoch chain)
+  struct PassStream {
+    Ctx& c;
+    hipStream_t orig = nullptr, ms = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    PassStream(Ctx& cc) : c(cc) {
+      const char* e = getenv("GS_PASS_SKIP");
+      if (!e || !*e || atoi(e) <= 0) return;
+      orig = c.stream;
+      ms = cu_stream_except(c, 0, (uint32_t)atoi(e));
+      GS_HIP(hipEventCreateWithFlags(&e0, hipEventDisableTiming));
+      GS_HIP(hipEventCreateWithFlags(&e1, hipEventDisableTiming));
+      GS_HIP(hipEventRecord(e0, orig));
+      GS_HIP(hipStreamWaitEvent(ms, e0, 0));
+      c.stream = ms;
+    }
+    ~PassStream() {
+      if (!ms) return;
+      (void)hipEventRecord(e1, ms);
+      (void)hipStreamWaitEvent(orig, e1, 0);
+      (void)hipStreamSynchronize(orig);
+      c.stream = orig;
+      (void)hipStreamDestroy(ms);
+      (void)hipEventDestroy(e0);
+      (void)hipEventDestroy(e1);
+    }
+  } pass_stream{c};
+  s = c.stream;
   GS_HIP(hipMemsetAsync(c.d_counters.p + C_ERR, 0, 8, s));
   check_schedule(c, sched, n_msgs);
   uint32_t Fmax = 1;

@@ -26,7 +26,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GOSSIPSIM_LIB", os.path.join(HERE, "libgossipsim.so"))
-ABI_VERSION = 9
+ABI_VERSION = 10
 MESH_W = 16
 UNDELIVERED = np.uint64(0xFFFFFFFFFFFFFFFF)
 MUXERS = {"yamux": 0, "quic": 1, "mplex": 2}
@@ -88,6 +88,14 @@ class GsInjector(ctypes.Structure):
                 ("reserved", u32)]
 
 
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, P(u64), u64, P(u64))
+EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, P(ctypes.c_void_p), P(u64), P(ctypes.c_void_p), P(u64))
+
+
+class GsCommOps(ctypes.Structure):  # gs_comm_ops (ABI 10)
+    _fields_ = [("user", ctypes.c_void_p), ("allgather", ALLGATHER_FN), ("exchange", EXCHANGE_FN)]
+
+
 class GsPartRecord(ctypes.Structure):
     _fields_ = [("key", u64), ("start", u64), ("peer", u32), ("slot", u32)]
 
@@ -140,6 +148,8 @@ SIGNATURES = {
     "gs_comm_get_id": (i32, [ctypes.c_char_p]),
     "gs_comm_init": (i32, [u32, u32, ctypes.c_char_p, i32, P(ctypes.c_void_p)]),
     "gs_comm_init_local": (i32, [u32, P(ctypes.c_void_p)]),
+    "gs_comm_init_ops": (i32, [u32, u32, ctypes.c_void_p, i32, P(ctypes.c_void_p)]),
+    "gs_comm_check": (i32, [ctypes.c_void_p]),
     "gs_comm_destroy": (i32, [ctypes.c_void_p]),
     "gs_run_partitioned": (i32, [P(ctypes.c_void_p), u32, ctypes.c_void_p, P(GsPublish), u64, P(GsResultSink)]),
 }
@@ -682,9 +692,13 @@ class Comm:
                                             uid = Comm.get_id() on rank 0,
                                             handed to the others out of band"""
 
-    def __init__(self, nranks=1, rank=0, uid=None, device=0, local_parts=None):
+    def __init__(self, nranks=1, rank=0, uid=None, device=0, local_parts=None, transport=None):
         self.h = ctypes.c_void_p()
-        if local_parts is not None:
+        if transport is not None:  # the caller's collectives (gs_comm_init_ops)
+            self._ops = _ops_of(transport, nranks)
+            rc = lib().gs_comm_init_ops(nranks, rank, ctypes.byref(self._ops), device, ctypes.byref(self.h))
+            self.parts, self.local, self.rank = nranks, False, rank
+        elif local_parts is not None:
             rc = lib().gs_comm_init_local(local_parts, ctypes.byref(self.h))
             self.parts, self.local = local_parts, True
         else:
@@ -694,6 +708,12 @@ class Comm:
             self.parts, self.local, self.rank = nranks, False, rank
         if rc:
             raise GossipSimError(rc, "gs_comm_init failed")
+
+    def check(self):
+        """gs_comm_check: one all-gather and one exchange of known bytes through the transport."""
+        rc = lib().gs_comm_check(self.h)
+        if rc:
+            raise GossipSimError(rc, "gs_comm_check: the transport delivered wrong data")
 
     @staticmethod
     def get_id():
@@ -738,3 +758,80 @@ class Comm:
             self.close()
         except Exception:
             pass
+
+
+def _ops_of(transport, nranks):
+    """gs_comm_ops over a transport object with allgather(np.uint64[n]) -> [nranks, n]
+    and exchange(list of send bytes, list of recv sizes) -> list of recv bytes.
+    An exception in the transport becomes a non-zero return (the call fails)."""
+    def allgather(_user, mine, n, out):
+        try:
+            a = np.ctypeslib.as_array(mine, (n,)).copy() if n else np.zeros(0, np.uint64)
+            got = np.ascontiguousarray(transport.allgather(a), np.uint64).reshape(-1)
+            if got.size != nranks * n:
+                return 2
+            ctypes.memmove(out, got.ctypes.data, got.nbytes)
+            return 0
+        except Exception:  # noqa: BLE001  (reported as the call's failure)
+            import traceback
+            traceback.print_exc()
+            return 1
+
+    def exchange(_user, send, send_bytes, recv, recv_bytes):
+        try:
+            sends = [ctypes.string_at(send[p], send_bytes[p]) if send_bytes[p] else b"" for p in range(nranks)]
+            sizes = [int(recv_bytes[p]) for p in range(nranks)]
+            got = transport.exchange(sends, sizes)
+            for p in range(nranks):
+                if len(got[p]) != sizes[p]:
+                    return 2
+                if sizes[p]:
+                    ctypes.memmove(recv[p], bytes(got[p]), sizes[p])
+            return 0
+        except Exception:  # noqa: BLE001
+            import traceback
+            traceback.print_exc()
+            return 1
+
+    ops = GsCommOps()
+    ops._cb = (ALLGATHER_FN(allgather), EXCHANGE_FN(exchange))  # kept alive with the struct
+    ops.allgather, ops.exchange = ops._cb
+    return ops
+
+
+class TorchDistTransport:
+    """gs_comm_ops over torch.distributed (any backend with all_gather and
+    point-to-point send / recv, e.g. gloo on CPU tensors): one rank per process,
+    launched by torchrun or multiprocessing, the rendezvous the caller's."""
+
+    def __init__(self, group=None):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist, self.group = torch, dist, group
+        self.rank = dist.get_rank(group)
+        self.size = dist.get_world_size(group)
+
+    def allgather(self, mine):
+        t = self.torch.from_numpy(mine.view(np.int64).copy())
+        out = [self.torch.empty_like(t) for _ in range(self.size)]
+        self.dist.all_gather(out, t, group=self.group)
+        return np.stack([o.numpy().view(np.uint64) for o in out])
+
+    def exchange(self, sends, sizes):
+        torch, dist = self.torch, self.dist
+        reqs, recvs = [], [b""] * self.size
+        bufs = {}
+        for p in range(self.size):
+            if p == self.rank:
+                continue
+            if sizes[p]:
+                bufs[p] = torch.empty(sizes[p], dtype=torch.uint8)
+                reqs.append(dist.irecv(bufs[p], src=p, group=self.group))
+            if len(sends[p]):
+                reqs.append(dist.isend(torch.frombuffer(bytearray(sends[p]), dtype=torch.uint8), dst=p,
+                                       group=self.group))
+        for r in reqs:
+            r.wait()
+        for p, b in bufs.items():
+            recvs[p] = b.numpy().tobytes()
+        return recvs

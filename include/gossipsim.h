@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 9u
+#define GS_ABI_VERSION 10u
 
 /* Sentinel for "never delivered" in t_complete_ns. */
 #define GS_UNDELIVERED UINT64_MAX
@@ -497,6 +497,31 @@ gs_status gs_comm_get_id(gs_comm_id* out);
 gs_status gs_comm_init(uint32_t nranks, uint32_t rank, const gs_comm_id* id, int32_t device, gs_comm** out);
 /* nparts parts driven by this process (one context each, any devices). */
 gs_status gs_comm_init_local(uint32_t nparts, gs_comm** out);
+/* ABI 10: a rank whose collectives are the caller's own transport (any
+ * process launcher: torch.distributed gloo, MPI, sockets). The library stages
+ * every collective of the partitioned protocols through host memory and calls
+ *  - allgather(user, mine, n, out): every rank's n u64 words into
+ *    out[rank * n + k] (the MIN / MAX all-reduces are reduced from it);
+ *  - exchange(user, send, send_bytes, recv, recv_bytes): an all-to-all-v of
+ *    host bytes — send[p] (send_bytes[p] bytes) to rank p, recv[p]
+ *    (recv_bytes[p] bytes, sizes known to both ends) from rank p, for every
+ *    p < nranks (the own entry is 0 bytes).
+ * A callback returns 0 on success; anything else fails the call on this rank
+ * (the others then fail in their next collective or in the transport).
+ * Collective order and sizes are the RCCL backend's, so every rank of a run
+ * makes the same calls in the same order. `device` is the rank's HIP device. */
+typedef struct gs_comm_ops {
+    void* user;
+    int (*allgather)(void* user, const uint64_t* mine, uint64_t n, uint64_t* out);
+    int (*exchange)(void* user, const void* const* send, const uint64_t* send_bytes, void* const* recv,
+                    const uint64_t* recv_bytes);
+} gs_comm_ops;
+gs_status gs_comm_init_ops(uint32_t nranks, uint32_t rank, const gs_comm_ops* ops, int32_t device, gs_comm** out);
+/* Transport check (ABI 10, host memory only, no device work): one allgather of
+ * (rank, nranks) words and one exchange of position-hashed buffers of
+ * 1 + 977 * (sender + 3 * receiver) bytes, each checked; GS_EDEVICE names the
+ * first mismatch. For gs_comm_init_ops communicators (others: GS_OK). */
+gs_status gs_comm_check(gs_comm* comm);
 gs_status gs_comm_destroy(gs_comm* comm);
 /* gs_run with the peers partitioned over the communicator's parts: ctxs are
  * this process's contexts (RCCL: nctx = 1, the rank's; local: nctx = nparts,

@@ -8,12 +8,12 @@
 //! the receive events) map to gs_config_* / gs_run / gs_result_sink
 //!.
 #![allow(non_camel_case_types)]
-use std::os::raw::{c_char, c_void};
+use std::os::raw::{c_char, c_int, c_void};
 
 pub type gs_status = i32;
 pub const GS_OK: gs_status = 0;
 pub const GS_UNDELIVERED: u64 = u64::MAX;
-pub const GS_ABI_VERSION: u32 = 9;
+pub const GS_ABI_VERSION: u32 = 10;
 pub const GS_NODE_RUST: u32 = 0;
 pub const GS_TRAFFIC_COLS: usize = 12; // GS_TR_*: tx/rx bytes, packets, header bytes, received,
                                        // published, tx/rx ACK packets, tx/rx ACK header bytes
@@ -72,6 +72,14 @@ pub struct gs_comm_id { pub internal: [c_char; 128] }
 pub enum gs_ctx {}
 pub enum gs_log {}
 pub enum gs_comm {}
+/// ABI 10: the caller's transport for gs_comm_init_ops (host buffers; 0 = success).
+#[repr(C)]
+pub struct gs_comm_ops {
+    pub user: *mut c_void,
+    pub allgather: Option<unsafe extern "C" fn(user: *mut c_void, mine: *const u64, n: u64, out: *mut u64) -> c_int>,
+    pub exchange: Option<unsafe extern "C" fn(user: *mut c_void, send: *const *const c_void, send_bytes: *const u64,
+                                              recv: *const *mut c_void, recv_bytes: *const u64) -> c_int>,
+}
 
 #[link(name = "gossipsim")]
 extern "C" {
@@ -128,6 +136,9 @@ extern "C" {
     pub fn gs_comm_init(nranks: u32, rank: u32, id: *const gs_comm_id, device: i32, out: *mut *mut gs_comm)
                         -> gs_status;
     pub fn gs_comm_init_local(nparts: u32, out: *mut *mut gs_comm) -> gs_status;
+    pub fn gs_comm_init_ops(nranks: u32, rank: u32, ops: *const gs_comm_ops, device: i32, out: *mut *mut gs_comm)
+        -> gs_status;
+    pub fn gs_comm_check(comm: *mut gs_comm) -> gs_status;
     pub fn gs_comm_destroy(comm: *mut gs_comm) -> gs_status;
     pub fn gs_run_partitioned(ctxs: *const *mut gs_ctx, nctx: u32, comm: *mut gs_comm, sched: *const gs_publish,
                               n_msgs: u64, sinks: *const gs_result_sink) -> gs_status;

@@ -60,7 +60,7 @@ def test_abi_struct_layouts_match_header(tmp_path):
     exe = tmp_path / "layout"
     subprocess.check_call(["gcc", "-std=c11", "-I", os.path.dirname(HEADER), "-o", str(exe), str(src)])
     got = dict(l.rsplit(" ", 1) for l in subprocess.check_output([str(exe)]).decode().splitlines())
-    assert int(got["abi"]) == gossipsim.ABI_VERSION == 9
+    assert int(got["abi"]) == gossipsim.ABI_VERSION == 10
     assert got["want"] == "%d,%d" % (gossipsim.WANT_T_COMPLETE, gossipsim.WANT_HOPS)
     for name, cls in structs.items():
         assert int(got["%s size" % name]) == ctypes.sizeof(cls), name
