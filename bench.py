@@ -413,6 +413,13 @@ CONFIGS = {
         peers=100_000, links=(5, 50, 150, 40, 130), fragments=1, batch=1024, msgs=1024,
         knobs=dict(lazy_gossip=1, churn_ppm=10_000, churn_down=10, churn_horizon=16,
                    heartbeat_ns=1_000_000_000, hb_phase_ns=gossipsim.T0_NS - 20 * 1_000_000_000 + 370_000_000)),
+    # config #3 over a longer schedule: 4096 publishes one per heartbeat = 4 batches of 1024, each
+    # batch's epoch chain on XCD 0 beside the previous batch's passes; the
+    # warm-up run covers the same number of epochs, so the timed run continues the chain
+    "c3_100k_gossip_churn_4096": dict(
+        peers=100_000, links=(5, 50, 150, 40, 130), fragments=1, batch=1024, msgs=4096, warm_msgs=4096,
+        knobs=dict(lazy_gossip=1, churn_ppm=10_000, churn_down=10, churn_horizon=16,
+                   heartbeat_ns=1_000_000_000, hb_phase_ns=gossipsim.T0_NS - 20 * 1_000_000_000 + 370_000_000)),
 }
 
 
@@ -434,7 +441,8 @@ def config_rates(args, local):
         sim.set_topogen_links(c["links"][0], *c["links"][1:])
         sim.connect_gossipsub_peers()
         sim.mesh_converge(args.max_heartbeats)
-        sim.run(gossipsim.shard_messages(0, 0, 1, c["batch"], c["peers"], args.msg_size), collect=False)
+        sim.run(gossipsim.shard_messages(0, 0, 1, c.get("warm_msgs", c["batch"]), c["peers"], args.msg_size),
+                collect=False)
         # repeats: the best of `reps` runs (config #1 runs ~1 ms, where one host hiccup doubles it);
         # every repeat simulates the same messages, so the counters are one run's
         dt = None

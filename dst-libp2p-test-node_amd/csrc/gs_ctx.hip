@@ -13,12 +13,24 @@ struct gs_ctx : gs::Ctx {};
 namespace gs {
 
 Ctx::~Ctx() {
+  static const bool dbg = getenv("GS_DEBUG_DTOR") != nullptr;
+  auto say = [&](const char* w) {
+    if (dbg) fprintf(stderr, "[dtor] %s\n", w);
+  };
+  say("sync streams");
+  for (hipStream_t st : {side, chain, chain_pipe, pass_ms, copy, stream})
+    if (st) (void)hipStreamSynchronize(st);
+  say("events");
   for (auto e : ev_pool) (void)hipEventDestroy(e);
   for (auto e : side_ev) (void)hipEventDestroy(e);
   for (auto e : blk_ev)
     if (e) (void)hipEventDestroy(e);
+  say("side");
   if (side) (void)hipStreamDestroy(side);
+  say("chain");
   if (chain) (void)hipStreamDestroy(chain);
+  say("chain_pipe");
+  if (chain_pipe) (void)hipStreamDestroy(chain_pipe);
   for (auto e : chain_ev)
     if (e) (void)hipEventDestroy(e);
   for (int k = 0; k < 2; k++) {
@@ -26,13 +38,20 @@ Ctx::~Ctx() {
     if (lat_done[k]) (void)hipEventDestroy(lat_done[k]);
     if (h_lat[k]) (void)hipHostFree(h_lat[k]);
   }
-  for (auto e : cp_ev) (void)hipEventDestroy(e);
+  for (auto& v : cp_ev)
+    for (auto e : v) (void)hipEventDestroy(e);
+  say("pass_ms");
+  if (pass_ms) (void)hipStreamDestroy(pass_ms);
+  for (auto e : pass_ev)
+    if (e) (void)hipEventDestroy(e);
   if (h_laterr) (void)hipHostFree(h_laterr);
   if (copy) (void)hipStreamDestroy(copy);
   if (h_pinned) (void)hipHostFree(h_pinned);
   if (h_block) (void)hipHostFree(h_block);
   if (h_slms) (void)hipHostFree(h_slms);
+  say("stream");
   if (stream) (void)hipStreamDestroy(stream);
+  say("done");
 }
 
 uint64_t read_counter(Ctx& c, uint32_t idx) {
@@ -160,6 +179,7 @@ extern "C" gs_status gs_set_links(gs_ctx* ctx, uint32_t S, const uint64_t* lat_n
   ctx->links_set = true;
   ctx->mesh_built = false;  // the mesh's GRAFT order and packed stages depend on the links
   ctx->cell_valid = false;  //  so do the churn pass's 64-wide rows (stage << 24 | peer)
+  ctx->lat32_ok = false;
   GS_API_END(ctx)
 }
 

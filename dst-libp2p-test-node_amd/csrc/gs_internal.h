@@ -85,6 +85,7 @@ struct Ctx {
   // (hipExtStreamCreateWithCUMask), and its join events
   hipStream_t chain = nullptr;
   hipEvent_t chain_ev[2] = {nullptr, nullptr};
+  hipStream_t chain_pipe = nullptr;  // churn runs: the chain's stream on its own XCD (GS_CHAIN_XCDS, default 0)
   std::vector<hipEvent_t> side_ev;      // its chunk events
   bool timing = false;
   bool traffic = false;        // gs_set_traffic: per-peer send/receive counters
@@ -114,6 +115,7 @@ struct Ctx {
   DevBuf<uint8_t> d_iprop;   // [nnz] event-driven epochs: the GRAFT/PRUNE bits a neighbour proposed, at the receiver's entry
   DevBuf<uint32_t> d_mesh;   // [N*MESH_W] packed stage<<24|peer, EMPTY padded
   DevBuf<uint32_t> d_lat32;  // [S*S] u32 latency for the mesh kernels
+  bool lat32_ok = false;     // d_lat32 holds the current links
   // churn: ring of per-epoch snapshots, slot = epoch % ring_R
   DevBuf<uint32_t> d_ring_mesh; // [R][N][MESH_W]
   DevBuf<uint64_t> d_ring_off;  // [R][(N+63)/64]
@@ -133,7 +135,7 @@ struct Ctx {
   // h0 - 1 when the run's offline bits are written): the churn list pass's tables of the epochs
   // done so far go to the side stream (gs_relax.hip chn_chunks)
   std::function<void(uint64_t)> epoch_hook;
-  std::vector<hipEvent_t> cp_ev;      // their events
+  std::vector<hipEvent_t> cp_ev[2];   // their events, per table set
   DevBuf<uint64_t> d_q0, d_r0;  // [B] epoch of t_pub, t_pub - start of that epoch
   uint32_t ring_R = 0;
   uint64_t churn_state = 0, ring_lo = 1, ring_hi = 0;  // mesh state epoch; valid ring epochs
@@ -279,13 +281,21 @@ struct Ctx {
   DevBuf<uint32_t> d_ccol;     // [N][64] stage << 24 | peer, ascending, EMPTY padded
   DevBuf<uint8_t> d_cpos;      // [N][64] position of the row's peer in that neighbour's row
   bool cell_valid = false;
-  DevBuf<uint64_t> d_cmm, d_cgt;  // [N][cE]
-  DevBuf<uint64_t> d_offe;     // [N][cW] offline bit per epoch of the batch range
-  DevBuf<uint32_t> d_coff;     // [H + 2][N][32] offline lanes per relative epoch (transposed like the final bits)
-  DevBuf<uint32_t> d_cq;       // [B] epoch of t_pub - first epoch of the range
-  DevBuf<uint8_t> d_pubok;     // [B] the publisher was online at t_pub
+  // the churn list pass's per-batch tables, two sets: the next batch's are built
+  // (its epoch chain beside this batch's passes) while this batch's are read
+  struct ChnTables {
+    DevBuf<uint64_t> cmm, cgt;  // [N][cE] mesh / IHAVE targets of each epoch as masks over the CSR row
+    DevBuf<uint64_t> offe;      // [N][cW] offline bit per epoch of the batch range
+    DevBuf<uint32_t> coff;      // [H + 2][N][32] offline lanes per relative epoch (transposed like the final bits)
+    DevBuf<uint32_t> cq;        // [B] epoch of t_pub - first epoch of the range
+    DevBuf<uint8_t> pubok;      // [B] the publisher was online at t_pub
+    DevBuf<uint32_t> calive;    // [32] published lanes in the final bits' transposed layout
+  } ct[2];
+  uint32_t ct_par = 0;          // the table set the next batch prepared in line uses
+  std::function<void()> pass_poll;  // called by the list pass between groups of passes (the chain ahead)
+  hipStream_t pass_ms = nullptr;    // churn runs: the passes' stream off the chain's XCDs (GS_PASS_XCDS)
+  hipEvent_t pass_ev[2] = {nullptr, nullptr};
   DevBuf<uint8_t> d_gnz;       // [N] the row's IHAVE plane of the built heartbeat is not empty
-  DevBuf<uint32_t> d_calive;   // [32] published lanes in the final bits' transposed layout
   DevBuf<uint16_t> d_gtag;     // [N] the built heartbeat (GC_BK) whose IHAVEs the row takes by scanning planes
   DevBuf<uint32_t> d_gpc;      // [N] IHAVE entries pushed to the row per heartbeat (bk << 16 | count)
   DevBuf<uint64_t> d_luni;     // [2][N] per pass: OR of the receiver masks of a row's records
@@ -312,7 +322,15 @@ inline void ensure_cus(Ctx& c) {
 }
 hipStream_t cu_stream(Ctx& c, uint32_t c0, uint32_t n);
 hipStream_t cu_stream_except(Ctx& c, uint32_t c0, uint32_t stride);
+hipStream_t xcd_stream(Ctx& c, uint32_t xcds);
+uint32_t xcd_env(const char* name);
 void churn_ring(Ctx& c, uint64_t h_lo, uint64_t h_hi);
+// the epoch chain in slices (gs_mesh.hip): nullptr when [churn_state + 1, h1] is
+// no plain continuation inside the ring (the caller runs churn_ring instead)
+struct EvRun;
+EvRun* chain_begin(Ctx& c, uint64_t h1, hipStream_t s, std::function<void(uint64_t)> hook);
+bool chain_advance(Ctx& c, EvRun& r, uint64_t max_epochs);  // true once every epoch is enqueued
+void chain_free(EvRun* r);
 void ensure_csrpos(Ctx& c);
 void ensure_in_lists(Ctx& c, uint64_t h0, uint64_t h1);
 void ensure_ring_ell(Ctx& c, uint64_t h0, uint64_t h1);

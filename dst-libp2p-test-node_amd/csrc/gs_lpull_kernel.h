@@ -478,6 +478,9 @@ __device__ __forceinline__ void glp_ihave_ent(const LPullArgs& a, uint64_t* CW, 
 #ifndef GS_LP_RCH
 #define GS_LP_RCH 2
 #endif
+#ifndef GS_LP_SKIP  // record chunks past a neighbour's count skipped by a scalar branch (A/B: -DGS_LP_SKIP=0)
+#define GS_LP_SKIP 1
+#endif
 template <int FP, uint32_t CH, bool IDW = false, bool PART = false, bool GOS = false, bool CHN = false>
 __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
   constexpr uint32_t NG = GS_LP_NG, RCH = GS_LP_RCH;
@@ -889,6 +892,10 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
               // neighbour's NN records it reads 0, which no record is (a
               // forwarding sender has hops >= 1)
               const uint32_t i = i0 + cc * 64 + lane;
+              if (GS_LP_SKIP && i0 + cc * 64 >= NN[k]) {  // wave-uniform: a chunk past every record
+                rec[k][cc] = 0;
+                continue;
+              }
               const auto v = __builtin_amdgcn_raw_buffer_load_b64(RS[k], i * 8u, 0, 0);
               rec[k][cc] = ((uint64_t)v[1] << 32) | v[0];
             }
@@ -900,6 +907,7 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
           for (int k = 0; k < (int)NG; k++)
 #pragma unroll
             for (int cc = 0; cc < (int)RCH; cc++) {
+              if (GS_LP_SKIP && i0 + cc * 64 >= NN[k]) continue;  // (nothing loaded: no record)
               const uint64_t rc = rec[k][cc];
               const uint32_t lo32 = (uint32_t)rc;
               // w receives it iff its bit of the inclusion mask is set (no

@@ -1101,7 +1101,8 @@ static hipEvent_t side_event(Ctx& c, size_t i) {
     int lo = 0, hi = 0;
     GS_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
     const char* sp = getenv("GS_SIDE_PRIORITY");  // A/B knob: 0 = default priority
-    if (sp && *sp && atoi(sp) == 0) GS_HIP(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
+    if (const uint32_t x = xcd_env("GS_SIDE_XCDS")) c.side = xcd_stream(c, x);  // (experiment: its XCDs)
+    else if (sp && *sp && atoi(sp) == 0) GS_HIP(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
     else GS_HIP(hipStreamCreateWithPriority(&c.side, hipStreamNonBlocking, lo));
   }
   while (c.side_ev.size() <= i) {
@@ -1112,14 +1113,18 @@ static hipEvent_t side_event(Ctx& c, size_t i) {
   return c.side_ev[i];
 }
 
-MeshArgs mesh_args(Ctx& c) {
+MeshArgs mesh_args(Ctx& c, hipStream_t s = nullptr) {
   const uint32_t N = c.cfg.peers;
   c.d_until.alloc(c.nnz ? c.nnz : 1);
   c.d_prop.alloc(c.nnz ? c.nnz : 1);
-  c.d_lat32.alloc((size_t)c.S * c.S);
-  std::vector<uint32_t> lat32(c.lat_ns.begin(), c.lat_ns.end());
-  GS_HIP(hipMemcpyAsync(c.d_lat32.p, lat32.data(), lat32.size() * 4, hipMemcpyHostToDevice, c.stream));
-  GS_HIP(hipStreamSynchronize(c.stream));  // lat32 dies here
+  if (!c.lat32_ok) {  // (once per link set: gs_set_links clears it)
+    if (!s) s = c.stream;
+    c.d_lat32.alloc((size_t)c.S * c.S);
+    std::vector<uint32_t> lat32(c.lat_ns.begin(), c.lat_ns.end());
+    GS_HIP(hipMemcpyAsync(c.d_lat32.p, lat32.data(), lat32.size() * 4, hipMemcpyHostToDevice, s));
+    GS_HIP(hipStreamSynchronize(s));  // lat32 dies here
+    c.lat32_ok = true;
+  }
   MeshArgs a{};
   a.row = c.d_row.p; a.col = c.d_col.p; a.rev = c.d_rev.p; a.flags = c.d_flags.p;
   a.prop = c.d_prop.p; a.until = c.d_until.p; a.stage = c.d_stage.p; a.lat = c.d_lat32.p;
@@ -1144,6 +1149,53 @@ void sub_epoch(Ctx& c, MeshArgs a) {
   GS_ROWS(k_handle_graft, G, N, s, a);
   GS_ROWS(k_apply, G, N, s, a);
   GS_HIP(hipGetLastError());
+}
+
+// Epoch h of a run [h0, h1] of event-driven epochs (three steps on stream s):
+// lin[y] = offline bitset of epoch h0 - 1 + y; `ring`: the slot h % ring_R gets
+// the mask ring row (and, `ell`, the ELL snapshot).
+static void ev_epoch(Ctx& c, MeshArgs& a, uint64_t h, uint64_t h0, uint64_t h1, const uint64_t* lin, uint32_t w64,
+                     bool ring, bool ell, uint32_t G, hipStream_t s) {
+  const uint32_t N = c.cfg.peers;
+  static const uint32_t ev_sw = [] {  // GS_EV_SW: scanning waves (rows / 64) per block of the steps
+    const char* e = getenv("GS_EV_SW");
+    const int v = e && *e ? atoi(e) : 1;
+    return (uint32_t)(v >= 4 ? 4 : v >= 2 ? 2 : 1);
+  }();
+  const unsigned sgrid = (unsigned)((N + 64 * ev_sw - 1) / (64 * ev_sw));
+#define GS_EVS1(SW, STEP, ...)                                                     \
+  do {                                                                             \
+    if (G == 16) k_ev_step<16, STEP, SW><<<sgrid, TB, 0, s>>>(__VA_ARGS__);        \
+    else k_ev_step<64, STEP, SW><<<sgrid, TB, 0, s>>>(__VA_ARGS__);                \
+  } while (0)
+#define GS_EVS(STEP, ...)                                                          \
+  do {                                                                             \
+    if (ev_sw == 4) GS_EVS1(4, STEP, __VA_ARGS__);                                 \
+    else if (ev_sw == 2) GS_EVS1(2, STEP, __VA_ARGS__);                            \
+    else GS_EVS1(1, STEP, __VA_ARGS__);                                            \
+  } while (0)
+  const uint64_t y = h - h0 + 1;
+  a.epoch = (uint32_t)h;
+  a.off = lin + y * w64;
+  a.off_prev = lin + (y - 1) * w64;
+  a.off_next = h < h1 ? lin + (y + 1) * w64 : nullptr;
+  uint32_t* mesh = ell ? c.d_ring_mesh.p + (size_t)(h % c.ring_R) * N * MESH_W : nullptr;
+  const uint32_t* prev = ell && h > h0 ? c.d_ring_mesh.p + (size_t)((h - 1) % c.ring_R) * N * MESH_W : nullptr;
+  if (ring) {
+    if (c.ring_ell_tag.size() != c.ring_R) c.ring_ell_tag.assign(c.ring_R, ~0ull);
+    c.ring_ell_tag[h % c.ring_R] = ell ? h : ~0ull;
+  }
+  const bool mmr = ring && c.d_ring_mm.p;
+  a.mm_out = mmr ? c.d_ring_mm.p + (size_t)(h % c.ring_R) * N : nullptr;
+  a.mm_prev = mmr && h > h0 ? c.d_ring_mm.p + (size_t)((h - 1) % c.ring_R) * N : nullptr;
+  MeshArgs an = a;  // the mask ring is written by the apply step only
+  an.mm_out = nullptr;
+  an.mm_prev = nullptr;
+  GS_EVS(EV_HB, an, nullptr, nullptr);
+  GS_EVS(EV_GRAFT, an, nullptr, nullptr);
+  GS_EVS(EV_APPLY, a, mesh, prev);
+#undef GS_EVS
+#undef GS_EVS1
 }
 
 // Event-driven churn epochs [h0, h1] (see k_ev_step): offline bitsets
@@ -1189,23 +1241,6 @@ void ev_epochs(Ctx& c, MeshArgs a, uint64_t h0, uint64_t h1, bool ring) {
     c.num_cus = hipGetDeviceProperties(&prop, c.cfg.device) == hipSuccess ? prop.multiProcessorCount : 256;
   }
   const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(row_blocks(N, G), (uint64_t)c.num_cus * 8));
-  static const uint32_t ev_sw = [] {  // GS_EV_SW: scanning waves (rows / 64) per block of the steps
-    const char* e = getenv("GS_EV_SW");
-    const int v = e && *e ? atoi(e) : 1;
-    return (uint32_t)(v >= 4 ? 4 : v >= 2 ? 2 : 1);
-  }();
-  const unsigned sgrid = (unsigned)((N + 64 * ev_sw - 1) / (64 * ev_sw));
-#define GS_EVS1(SW, STEP, ...)                                                     \
-  do {                                                                             \
-    if (G == 16) k_ev_step<16, STEP, SW><<<sgrid, TB, 0, s>>>(__VA_ARGS__);        \
-    else k_ev_step<64, STEP, SW><<<sgrid, TB, 0, s>>>(__VA_ARGS__);                \
-  } while (0)
-#define GS_EVS(STEP, ...)                                                          \
-  do {                                                                             \
-    if (ev_sw == 4) GS_EVS1(4, STEP, __VA_ARGS__);                                 \
-    else if (ev_sw == 2) GS_EVS1(2, STEP, __VA_ARGS__);                            \
-    else GS_EVS1(1, STEP, __VA_ARGS__);                                            \
-  } while (0)
   if (G == 16) k_ev_init<16><<<grid, TB, 0, s>>>(a);
   else k_ev_init<64><<<grid, TB, 0, s>>>(a);
   if (c.epoch_hook && ring) c.epoch_hook(h0 - 1);
@@ -1225,27 +1260,7 @@ void ev_epochs(Ctx& c, MeshArgs a, uint64_t h0, uint64_t h1, bool ring) {
     GS_HIP(hipStreamWaitEvent(c.side, e, 0));
   }
   for (uint64_t h = h0; h <= h1; h++) {
-    const uint64_t y = h - h0 + 1;
-    a.epoch = (uint32_t)h;
-    a.off = lin + y * w64;
-    a.off_prev = lin + (y - 1) * w64;
-    a.off_next = h < h1 ? lin + (y + 1) * w64 : nullptr;
-    const bool ell = ring && !(c.ring_ell_defer && c.d_ring_mm.p);  // (deferred: the mask ring only)
-    uint32_t* mesh = ell ? c.d_ring_mesh.p + (size_t)(h % c.ring_R) * N * MESH_W : nullptr;
-    const uint32_t* prev = ell && h > h0 ? c.d_ring_mesh.p + (size_t)((h - 1) % c.ring_R) * N * MESH_W : nullptr;
-    if (ring) {
-      if (c.ring_ell_tag.size() != c.ring_R) c.ring_ell_tag.assign(c.ring_R, ~0ull);
-      c.ring_ell_tag[h % c.ring_R] = ell ? h : ~0ull;
-    }
-    const bool mmr = ring && c.d_ring_mm.p;
-    a.mm_out = mmr ? c.d_ring_mm.p + (size_t)(h % c.ring_R) * N : nullptr;
-    a.mm_prev = mmr && h > h0 ? c.d_ring_mm.p + (size_t)((h - 1) % c.ring_R) * N : nullptr;
-    MeshArgs an = a;  // the mask ring is written by the apply step only
-    an.mm_out = nullptr;
-    an.mm_prev = nullptr;
-    GS_EVS(EV_HB, an, nullptr, nullptr);
-    GS_EVS(EV_GRAFT, an, nullptr, nullptr);
-    GS_EVS(EV_APPLY, a, mesh, prev);
+    ev_epoch(c, a, h, h0, h1, lin, w64, ring, ring && !(c.ring_ell_defer && c.d_ring_mm.p), G, s);
     if (c.epoch_hook && ring) c.epoch_hook(h);
     if (lists && h >= hr && (h + 1 - chunk0 == CE || h == h1)) {
       const hipEvent_t e = side_event(c, nev++);
@@ -1255,8 +1270,6 @@ void ev_epochs(Ctx& c, MeshArgs a, uint64_t h0, uint64_t h1, bool ring) {
       chunk0 = h + 1;
     }
   }
-#undef GS_EVS
-#undef GS_EVS1
   GS_HIP(hipGetLastError());
   if (lists) {  // the context's stream continues once every list is written
     const hipEvent_t e = side_event(c, nev++);
@@ -1338,29 +1351,67 @@ hipStream_t cu_stream_except(Ctx& c, uint32_t c0, uint32_t stride) {
   return s;
 }
 
+// A stream on the CUs of the XCDs in `xcds` (bit x: XCD x). The CU mask's bit b
+// is CU b / XCDS of XCD b % XCDS (measured: bits 0, 8, 16, ... run the epoch
+// chain as fast as all 256 CUs, bits 0..31 take twice as long).
+constexpr uint32_t XCDS = 8;
+hipStream_t xcd_stream(Ctx& c, uint32_t xcds) {
+  ensure_cus(c);
+  const uint32_t total = (uint32_t)std::max(c.num_cus, 1);
+  std::vector<uint32_t> mask((total + 31) / 32, 0u);
+  for (uint32_t b = 0; b < total; b++)
+    if ((xcds >> (b % XCDS)) & 1u) mask[b / 32] |= 1u << (b % 32);
+  hipStream_t s = nullptr;
+  GS_HIP(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+  return s;
+}
+// "0", "1,2", "3-7" -> XCD bits (0: unset or empty)
+uint32_t xcd_env(const char* name) {
+  const char* e = getenv(name);
+  if (!e || !*e) return 0;
+  uint32_t m = 0;
+  for (const char* p = e; *p;) {
+    char* q = nullptr;
+    const long a = strtol(p, &q, 10);
+    if (q == p) break;
+    long b = a;
+    if (*q == '-') {
+      p = q + 1;
+      b = strtol(p, &q, 10);
+    }
+    for (long x = a; x <= b && x < (long)XCDS; x++)
+      if (x >= 0) m |= 1u << x;
+    p = *q ? q + 1 : q;
+  }
+  return m;
+}
+
 // GS_CHAIN_CUS=n (experiment): the epoch chain of churn_ring on a stream of n CUs.
 static uint32_t chain_cus() {
   const char* e = getenv("GS_CHAIN_CUS");
+  if (const uint32_t x = xcd_env("GS_CHAIN_XCDS")) return 0x10000u | x;  // (GS_CHAIN_XCDS wins)
   return e && *e ? (uint32_t)std::max(0, atoi(e)) : 0u;
 }
 
 static void churn_ring_on(Ctx& c, uint64_t h_lo, uint64_t h_hi);
 void churn_ring(Ctx& c, uint64_t h_lo, uint64_t h_hi) {
-  const uint32_t n = chain_cus();
-  if (!n) return churn_ring_on(c, h_lo, h_hi);
+  const uint32_t n = c.chain_pipe ? 0u : chain_cus();
+  if (!n && !c.chain_pipe) return churn_ring_on(c, h_lo, h_hi);
   static uint32_t made = 0;  // (experiment: one mask per process)
-  if (!c.chain || made != n) {
+  if (!c.chain_pipe && (!c.chain || made != n)) {
     if (c.chain) GS_HIP(hipStreamDestroy(c.chain));
-    c.chain = cu_stream(c, 0, n);
+    c.chain = n & 0x10000u ? xcd_stream(c, n & 0xFFu) : cu_stream(c, 0, n);
     made = n;
     for (auto& e : c.chain_ev)
       if (e) GS_HIP(hipEventDestroy(e));
     for (auto& e : c.chain_ev) GS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
-  hipStream_t main = c.stream;
+  hipStream_t main = c.stream, cs = c.chain_pipe ? c.chain_pipe : c.chain;
+  for (auto& e : c.chain_ev)
+    if (!e) GS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   GS_HIP(hipEventRecord(c.chain_ev[0], main));
-  GS_HIP(hipStreamWaitEvent(c.chain, c.chain_ev[0], 0));
-  c.stream = c.chain;  // every launch of the chain (and the hook's events) on the chain's CUs
+  GS_HIP(hipStreamWaitEvent(cs, c.chain_ev[0], 0));
+  c.stream = cs;  // every launch of the chain (and the hook's events) on the chain's CUs
   try {
     churn_ring_on(c, h_lo, h_hi);
   } catch (...) {
@@ -1368,7 +1419,7 @@ void churn_ring(Ctx& c, uint64_t h_lo, uint64_t h_hi) {
     throw;
   }
   c.stream = main;
-  GS_HIP(hipEventRecord(c.chain_ev[1], c.chain));
+  GS_HIP(hipEventRecord(c.chain_ev[1], cs));
   GS_HIP(hipStreamWaitEvent(main, c.chain_ev[1], 0));
 }
 
@@ -1407,6 +1458,74 @@ static void churn_ring_on(Ctx& c, uint64_t h_lo, uint64_t h_hi) {
   GS_HIP(hipMemcpyAsync(c.h_pinned, c.d_counters.p + C_ERR, 8, hipMemcpyDeviceToHost, s));
   GS_HIP(hipStreamSynchronize(s));
   if (c.h_pinned[0] & ERR_MESH) c.fail(GS_ERANGE, "mesh row exceeds GS_MESH_W entries");
+}
+
+// The epoch chain of a churn list-pass batch enqueued in slices (the batch
+// after the current one runs its chain beside the current batch's passes,
+// gs_relax.hip ChnAhead): epochs churn_state + 1 .. h1 on stream s, the mask
+// ring only (no ELL snapshots, no inverse IHAVE lists: the list pass reads
+// neither), the hook after every epoch (the batch tables' chunks). The ring
+// bookkeeping (churn_state, ring_lo / hi) moves when the last epoch is enqueued.
+struct EvRun {
+  MeshArgs a{};
+  uint64_t h0 = 0, h1 = 0, h = 0;
+  uint32_t w64 = 0, G = 16;
+  hipStream_t s = nullptr;
+  std::function<void(uint64_t)> hook;
+};
+void chain_free(EvRun* r) { delete r; }
+EvRun* chain_begin(Ctx& c, uint64_t h1, hipStream_t s, std::function<void(uint64_t)> hook) {
+  const uint32_t N = c.cfg.peers;
+  if (c.churn_state + 1 > h1 || c.churn_state + 1 < c.ring_lo || h1 - c.churn_state > c.ring_R || !c.d_ring_mm.p)
+    return nullptr;  // (nothing to run, or not a plain continuation: the caller runs churn_ring)
+  EvRun* r = new EvRun();
+  r->a = mesh_args(c, s);
+  r->h0 = r->h = c.churn_state + 1;
+  r->h1 = h1;
+  r->w64 = (N + 63) / 64;
+  r->G = row_group(c);
+  r->s = s;
+  r->hook = std::move(hook);
+  const uint64_t E = h1 - r->h0 + 1;
+  c.d_offlin.alloc((size_t)(E + 1) * r->w64);
+  for (uint64_t y0 = 0; y0 < E + 1; y0 += 32768) {  // grid.y limit
+    const uint32_t ny = (uint32_t)std::min<uint64_t>(32768, E + 1 - y0);
+    k_offline_range<<<dim3(blocks(N), ny), TB, 0, s>>>(N, c.cfg.seed, c.cfg.churn_ppm, c.cfg.churn_down,
+                                                       r->h0 - 1 + y0, c.d_offlin.p + y0 * r->w64, r->w64,
+                                                       c.d_ring_off.p, c.ring_R, r->h0);
+  }
+  c.d_pst.alloc((size_t)PS_PLANES * N);
+  GS_HIP(hipMemsetAsync(c.d_pst.p, 0, (size_t)PS_MC * N, s));
+  GS_HIP(hipMemsetAsync(c.d_pst.p + (size_t)PS_DIRTY * N, 1, N, s));
+  GS_HIP(hipMemsetAsync(c.d_prop.p, 0, c.nnz ? c.nnz : 1, s));
+  c.d_iprop.alloc(c.nnz ? c.nnz : 1);
+  GS_HIP(hipMemsetAsync(c.d_iprop.p, 0, c.nnz ? c.nnz : 1, s));
+  r->a.pst = c.d_pst.p;
+  r->a.iprop = c.d_iprop.p;
+  r->a.dbg = nullptr;
+  r->a.off = c.d_offlin.p + r->w64;
+  r->a.off_prev = c.d_offlin.p;
+  r->a.off_next = nullptr;
+  const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(row_blocks(N, r->G), (uint64_t)c.num_cus * 8));
+  if (r->G == 16) k_ev_init<16><<<grid, TB, 0, s>>>(r->a);
+  else k_ev_init<64><<<grid, TB, 0, s>>>(r->a);
+  GS_HIP(hipGetLastError());
+  if (r->hook) r->hook(r->h0 - 1);
+  return r;
+}
+bool chain_advance(Ctx& c, EvRun& r, uint64_t max_epochs) {
+  for (uint64_t k = 0; k < max_epochs && r.h <= r.h1; k++, r.h++) {
+    ev_epoch(c, r.a, r.h, r.h0, r.h1, c.d_offlin.p, r.w64, true, false, r.G, r.s);
+    if (r.hook) r.hook(r.h);
+  }
+  GS_HIP(hipGetLastError());
+  if (r.h <= r.h1) return false;
+  if (r.h1 > c.churn_state) {  // (as churn_ring: the state and the ring's valid range)
+    c.churn_state = r.h1;
+    c.ring_hi = r.h1;
+    c.ring_lo = std::max<uint64_t>(c.ring_lo, r.h1 + 1 >= c.ring_R ? r.h1 + 1 - c.ring_R : 0);
+  }
+  return true;
 }
 
 // ELL snapshots of ring epochs [h0, h0 + gridDim.y) rebuilt from the mask ring:

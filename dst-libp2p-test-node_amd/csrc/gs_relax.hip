@@ -1076,6 +1076,7 @@ struct GosRun {
 struct ChnRun {
   uint64_t E0, r0;
   uint32_t cE, ghoff;
+  uint32_t par;  // the table set (Ctx::ct) chn_begin filled for the batch
 };
 
 // Batch slices (run_slices): S batches of the same shape as one pass over S
@@ -1161,12 +1162,13 @@ static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvF
   if (chn) {  // churn (gs_cpull.h): the tables k_cprep built for this batch
     la.ccol = c.d_ccol.p;
     la.cpos = c.d_cpos.p;
-    la.cmm = c.d_cmm.p;
-    la.cgt = c.d_cgt.p;
-    la.coff = c.d_coff.p;
-    la.cq = c.d_cq.p;
-    la.pubok = c.d_pubok.p;
-    la.calive = c.d_calive.p;
+    const Ctx::ChnTables& t = c.ct[chn->par & 1];
+    la.cmm = t.cmm.p;
+    la.cgt = t.cgt.p;
+    la.coff = t.coff.p;
+    la.cq = t.cq.p;
+    la.pubok = t.pubok.p;
+    la.calive = t.calive.p;
     c.d_luni.alloc(2 * (size_t)N);
     la.luni = c.d_luni.p;
     c.d_gnz.alloc(N);
@@ -1273,7 +1275,17 @@ static bool run_lpull_batch(Ctx& c, const Batch& b, uint32_t K, uint32_t lb, EvF
     GS_HIP(hipGetLastError());
     GS_HIP(hipMemcpyAsync(c.h_pinned, c.d_pctrl.p, 12 * 8, hipMemcpyDeviceToHost, s));
     GS_HIP(hipMemcpyAsync(c.h_pinned + 12, c.d_counters.p + C_ERR, 8, hipMemcpyDeviceToHost, s));  // same sync
+    if (c.pass_poll) c.pass_poll();  // (while these passes run: the next batch's epoch chain is enqueued)
     GS_HIP(hipStreamSynchronize(s));
+    static const bool dbg_pass = getenv("GS_DEBUG_PASSES") != nullptr;
+    if (dbg_pass && pass % 256 == 0)
+      fprintf(stderr, "[gs] pass %u: mode %llu lo %llu records %llu min %llx err %llx\n", pass,
+              (unsigned long long)c.h_pinned[((pass - 1) % 3) * 4 + 1], (unsigned long long)c.h_pinned[((pass - 1) % 3) * 4],
+              (unsigned long long)c.h_pinned[((pass - 1) % 3) * 4 + 2],
+              (unsigned long long)c.h_pinned[((pass - 1) % 3) * 4 + 3], (unsigned long long)c.h_pinned[12]);
+    // a batch's passes end (every window of its lifetime emitted); a count far
+    // past that is a bug, reported instead of looping
+    if (pass > (1u << 20)) c.fail(GS_ERANGE, "internal: the list pass did not finish in 2^20 passes");
     if (c.h_pinned[((pass - 1) % 3) * 4 + 1] == PM_DONE) break;
     if (c.h_pinned[12] & (ERR_LIST | ERR_RING)) break;  // lost already: stop early, re-run on k_pull
   }
@@ -1333,25 +1345,27 @@ static bool gossip_noop(const Batch& b, const uint64_t* ms, const std::vector<ui
 // offline lanes per relative epoch (k_coff) and the join.
 struct ChnPrep {
   uint64_t E0 = 0;
-  uint32_t cE = 0, cW = 0, next = 0;
+  uint32_t cE = 0, cW = 0, next = 0, par = 0;  // par: the table set (Ctx::ct) this batch fills
   bool offe = false;
   size_t nev = 0;
+  hipStream_t s = nullptr;  // the stream the epoch chain runs on (chunk events are recorded there)
   CPrepArgs pa{};
   unsigned grid = 1;
 };
-static hipEvent_t cp_event(Ctx& c, size_t i) {
-  while (c.cp_ev.size() <= i) {
+static hipEvent_t cp_event(Ctx& c, uint32_t par, size_t i) {
+  std::vector<hipEvent_t>& v = c.cp_ev[par & 1];
+  while (v.size() <= i) {
     hipEvent_t e;
     GS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    c.cp_ev.push_back(e);
+    v.push_back(e);
   }
-  return c.cp_ev[i];
+  return v[i];
 }
-static void chn_begin(Ctx& c, ChnPrep& cp, uint64_t E0, uint32_t cE, const uint64_t* q0, const gs_publish* sched,
-                      uint32_t B) {
+static void chn_begin(Ctx& c, ChnPrep& cp, uint32_t par, hipStream_t s, uint64_t E0, uint32_t cE, const uint64_t* q0,
+                      const gs_publish* sched, uint32_t B) {
   const uint32_t N = c.cfg.peers, H = c.cfg.churn_horizon, R = c.ring_R;
   const uint32_t cW = (cE + 63) / 64;
-  hipStream_t s = c.stream;
+  Ctx::ChnTables& t = c.ct[par & 1];
   if (!c.cell_valid) {
     c.d_ccol.alloc((size_t)N * CELL_W);
     c.d_cpos.alloc((size_t)N * CELL_W);
@@ -1369,27 +1383,29 @@ static void chn_begin(Ctx& c, ChnPrep& cp, uint64_t E0, uint32_t cE, const uint6
   std::vector<uint16_t> alive(64, 0);  // lane j: bit q = lane q*64 + j published
   for (uint32_t q = 0; q < B; q++)
     if (ok[q]) alive[q & 63] |= (uint16_t)(1u << (q >> 6));
-  c.d_cq.alloc(c.cfg.batch);
-  c.d_pubok.alloc(c.cfg.batch);
-  c.d_calive.alloc(LP_FW);
-  GS_HIP(hipMemcpyAsync(c.d_cq.p, cq.data(), B * 4, hipMemcpyHostToDevice, s));
-  GS_HIP(hipMemcpyAsync(c.d_pubok.p, ok.data(), B, hipMemcpyHostToDevice, s));
-  GS_HIP(hipMemcpyAsync(c.d_calive.p, alive.data(), 128, hipMemcpyHostToDevice, s));
-  c.d_offe.alloc((size_t)N * cW);
-  c.d_cmm.alloc((size_t)N * cE);
-  c.d_cgt.alloc((size_t)N * cE);
-  c.d_coff.alloc((size_t)(H + 2) * N * LP_FW);
+  t.cq.alloc(c.cfg.batch);
+  t.pubok.alloc(c.cfg.batch);
+  t.calive.alloc(LP_FW);
+  GS_HIP(hipMemcpyAsync(t.cq.p, cq.data(), B * 4, hipMemcpyHostToDevice, s));
+  GS_HIP(hipMemcpyAsync(t.pubok.p, ok.data(), B, hipMemcpyHostToDevice, s));
+  GS_HIP(hipMemcpyAsync(t.calive.p, alive.data(), 128, hipMemcpyHostToDevice, s));
+  t.offe.alloc((size_t)N * cW);
+  t.cmm.alloc((size_t)N * cE);
+  t.cgt.alloc((size_t)N * cE);
+  t.coff.alloc((size_t)(H + 2) * N * LP_FW);
   GS_HIP(hipStreamSynchronize(s));  // cq / ok / alive die here
   cp.E0 = E0;
   cp.cE = cE;
   cp.cW = cW;
   cp.next = 0;
+  cp.par = par & 1;
   cp.offe = false;
   cp.nev = 0;
+  cp.s = s;
   CPrepArgs& pa = cp.pa;
   pa = CPrepArgs{};
-  pa.ccol = c.d_ccol.p; pa.ring_mm = c.d_ring_mm.p; pa.offe = c.d_offe.p; pa.cq = c.d_cq.p;
-  pa.cmm = c.d_cmm.p; pa.cgt = c.cfg.lazy_gossip ? c.d_cgt.p : nullptr; pa.coff = c.d_coff.p;
+  pa.ccol = c.d_ccol.p; pa.ring_mm = c.d_ring_mm.p; pa.offe = t.offe.p; pa.cq = t.cq.p;
+  pa.cmm = t.cmm.p; pa.cgt = c.cfg.lazy_gossip ? t.cgt.p : nullptr; pa.coff = t.coff.p;
   pa.E0 = E0; pa.N = N; pa.R = R; pa.cE = cE; pa.cW = cW; pa.B = B; pa.H = H;
   pa.seed = c.cfg.seed; pa.d_lazy = c.cfg.d_lazy; pa.gf_milli = c.cfg.gossip_factor_milli;
   ensure_cus(c);
@@ -1402,11 +1418,12 @@ static void chn_chunks(Ctx& c, ChnPrep& cp, uint64_t h_done, bool all) {
   if (c1 == cp.next) return;
   const uint32_t N = c.cfg.peers, w64 = (N + 63) / 64;
   hipStream_t side = side_stream(c);
-  const hipEvent_t e = cp_event(c, cp.nev++);
-  GS_HIP(hipEventRecord(e, c.stream));
+  const hipEvent_t e = cp_event(c, cp.par, cp.nev++);
+  GS_HIP(hipEventRecord(e, cp.s ? cp.s : c.stream));  // (in line: the stream churn_ring runs the chain on)
   GS_HIP(hipStreamWaitEvent(side, e, 0));
   if (!cp.offe) {  // every epoch's offline bits are in the ring once the chain's run started
-    k_offe<<<dim3(w64, cp.cW), 64, 0, side>>>(N, c.d_ring_off.p, w64, c.ring_R, cp.E0, cp.cE, cp.cW, c.d_offe.p);
+    k_offe<<<dim3(w64, cp.cW), 64, 0, side>>>(N, c.d_ring_off.p, w64, c.ring_R, cp.E0, cp.cE, cp.cW,
+                                              c.ct[cp.par].offe.p);
     k_coff<<<cp.grid, TB, 0, side>>>(cp.pa);  // the offline lanes need no mesh: beside the chain too
     cp.offe = true;
   }
@@ -1416,14 +1433,17 @@ static void chn_chunks(Ctx& c, ChnPrep& cp, uint64_t h_done, bool all) {
   GS_HIP(hipGetLastError());
   cp.next = c1;
 }
-static void chn_end(Ctx& c, ChnPrep& cp) {
+// The rest of the tables, then `to` waits for them (nullptr: cp.s, and the host too).
+static void chn_end(Ctx& c, ChnPrep& cp, hipStream_t to = nullptr) {
   chn_chunks(c, cp, 0, true);
-  const hipEvent_t e = cp_event(c, cp.nev++);
+  const hipEvent_t e = cp_event(c, cp.par, cp.nev++);
   GS_HIP(hipEventRecord(e, side_stream(c)));
-  GS_HIP(hipStreamWaitEvent(c.stream, e, 0));
+  GS_HIP(hipStreamWaitEvent(to ? to : c.stream, e, 0));
   GS_HIP(hipGetLastError());
+  if (to) return;
   const uint32_t N = c.cfg.peers, R = c.ring_R, cE = cp.cE;
   const uint64_t E0 = cp.E0;
+  const Ctx::ChnTables& t = c.ct[cp.par];
   hipStream_t s = c.stream;
   GS_HIP(hipStreamSynchronize(s));
   if (getenv("GS_DEBUG_CHN")) {  // diagnostic: the tables against the ELL ring and offline_draw
@@ -1431,8 +1451,8 @@ static void chn_end(Ctx& c, ChnPrep& cp) {
     std::vector<uint32_t> col(c.nnz), ell((size_t)R * N * MESH_W);
     GS_HIP(hipMemcpy(row.data(), c.d_row.p, (N + 1) * 8, hipMemcpyDeviceToHost));
     GS_HIP(hipMemcpy(col.data(), c.d_col.p, c.nnz * 4, hipMemcpyDeviceToHost));
-    GS_HIP(hipMemcpy(cmm.data(), c.d_cmm.p, cmm.size() * 8, hipMemcpyDeviceToHost));
-    GS_HIP(hipMemcpy(cge.data(), c.d_cgt.p, cge.size() * 8, hipMemcpyDeviceToHost));
+    GS_HIP(hipMemcpy(cmm.data(), t.cmm.p, cmm.size() * 8, hipMemcpyDeviceToHost));
+    GS_HIP(hipMemcpy(cge.data(), t.cgt.p, cge.size() * 8, hipMemcpyDeviceToHost));
     GS_HIP(hipMemcpy(ell.data(), c.d_ring_mesh.p, ell.size() * 4, hipMemcpyDeviceToHost));
     uint64_t bad_mm = 0, bad_ge = 0;
     for (uint32_t w = 0; w < N; w++)
@@ -1469,7 +1489,116 @@ static void chn_end(Ctx& c, ChnPrep& cp) {
   }
 }
 
+// The churn snapshot ring: R slots of per-epoch meshes, offline
+// bitsets and (lazy gossip) inverse IHAVE lists, sized once per context.
+static void ensure_ring(Ctx& c) {
+  if (c.ring_R) return;
+  const uint32_t N = c.cfg.peers, Bmax = c.cfg.batch;
+  const bool gossip = c.cfg.lazy_gossip != 0;
+  const uint64_t w64 = ((uint64_t)N + 63) / 64;
+  const uint64_t per_slot = (uint64_t)N * MESH_W * 4 + w64 * 8 + (gossip ? (uint64_t)N * (GT_IN * 4 + 4) : 0) +
+                            (uint64_t)N * 8;
+  const char* rb = getenv("GS_RING_BUDGET_MB");  // test knob: force batch cuts at the ring size
+  const uint64_t budget = rb && *rb ? (uint64_t)atoll(rb) << 20 : 16ull << 30;
+  const uint64_t want = (uint64_t)Bmax + c.cfg.churn_horizon + 1;
+  c.ring_R = (uint32_t)std::min<uint64_t>(want, std::max<uint64_t>(c.cfg.churn_horizon + 2, budget / per_slot));
+  c.d_ring_mesh.alloc((size_t)c.ring_R * N * MESH_W);
+  c.d_ring_off.alloc((size_t)c.ring_R * w64);
+  if (c.max_degree <= CELL_W) c.d_ring_mm.alloc((size_t)c.ring_R * N);  // the churn list pass's meshes
+  if (gossip) c.d_ring_in.alloc((size_t)c.ring_R * N * GT_IN);  // inverse IHAVE lists (ring_in_lists)
+}
+
+static void run_messages_impl(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_result_sink* sink,
+                              const std::vector<uint8_t>* cut);
+
+// Schedules that are not lockstep: the churn list pass and the
+// gossip inside the list pass need every message of a batch at the same
+// offset r = (t_pub - hb_phase) mod heartbeat (its heartbeats and epoch
+// boundaries are then one relative time for all lanes). run.sh's free
+// message_delay (run.sh:36; 1500 ms gives two offsets) and arbitrary POST
+// /publish sequences (main.rs:146-221) are not. Messages are independent
+// given the mesh of each epoch, so the run takes each group of consecutive
+// messages a batch could hold (same size and chunk count, <= the batch size,
+// churn: its epochs in the ring) in offset-class order — a batch per class,
+// each lockstep — and hands the results back in schedule order. Classes per
+// group are capped (GS_CLASS_MAX, default 64; a group with more keeps its
+// order); streaming sinks (on_block, on_lat) and device sinks keep the order
+// too. GS_CLASS_SPLIT=0 turns the regrouping off.
+static bool class_plan(Ctx& c, const gs_publish* sched, uint64_t n, const gs_result_sink* sink,
+                       std::vector<uint64_t>& perm, std::vector<uint8_t>& cut) {
+  const bool churn = c.cfg.churn_ppm != 0, gossip = c.cfg.lazy_gossip != 0;
+  if ((!churn && !gossip) || n < 2 || c.sink_dev) return false;
+  if (sink && (sink->on_block || sink->on_lat)) return false;
+  const char* e = getenv("GS_CLASS_SPLIT");
+  if (e && *e && atoi(e) == 0) return false;
+  const char* mx = getenv("GS_CLASS_MAX");
+  const uint64_t cmax = mx && *mx ? (uint64_t)std::max(1, atoi(mx)) : 64u;
+  const uint64_t hb = c.cfg.heartbeat_ns, ph = c.cfg.hb_phase_ns;
+  for (uint64_t i = 0; i < n; i++)
+    if (sched[i].t_pub_ns < ph) return false;  // (run_messages_impl reports what it must)
+  if (churn) ensure_ring(c);
+  const uint32_t Bmax = c.cfg.batch;
+  perm.resize(n);
+  cut.assign(n, 0);
+  bool any = false;
+  for (uint64_t g0 = 0; g0 < n;) {  // a group: what one batch could hold
+    const uint32_t F0 = frags_of(c, sched[g0]);
+    const uint64_t cap = std::max<uint32_t>(1, std::min<uint32_t>(Bmax, PULL_LMAX / pow2_at_least(F0)));
+    uint64_t g1 = g0 + 1, lo = (sched[g0].t_pub_ns - ph) / hb, hi = lo;
+    while (g1 < n && g1 - g0 < cap && sched[g1].msg_size == sched[g0].msg_size && frags_of(c, sched[g1]) == F0) {
+      if (churn) {
+        const uint64_t ep = (sched[g1].t_pub_ns - ph) / hb, lo2 = std::min(lo, ep), hi2 = std::max(hi, ep);
+        if (hi2 + c.cfg.churn_horizon - lo2 + 1 > c.ring_R) break;
+        lo = lo2;
+        hi = hi2;
+      }
+      g1++;
+    }
+    std::vector<std::pair<uint64_t, uint64_t>> key(g1 - g0);  // (offset class, message)
+    for (uint64_t i = g0; i < g1; i++) key[i - g0] = {(sched[i].t_pub_ns - ph) % hb, i};
+    std::stable_sort(key.begin(), key.end(), [](const std::pair<uint64_t, uint64_t>& x,
+                                                 const std::pair<uint64_t, uint64_t>& y) { return x.first < y.first; });
+    uint64_t ncls = 1;
+    for (size_t k = 1; k < key.size(); k++) ncls += key[k].first != key[k - 1].first;
+    const bool split = ncls > 1 && ncls <= cmax && !(churn && F0 > 1);  // (fragmented churn: the push path)
+    cut[g0] = 1;
+    for (uint64_t i = g0; i < g1; i++) {
+      perm[i] = split ? key[i - g0].second : i;
+      if (split && i > g0 && key[i - g0].first != key[i - g0 - 1].first) cut[i] = 1;
+    }
+    any = any || split;
+    g0 = g1;
+  }
+  return any;
+}
+
 void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_result_sink* sink) {
+  std::vector<uint64_t> perm;
+  std::vector<uint8_t> cut;
+  if (!class_plan(c, sched, n_msgs, sink, perm, cut)) return run_messages_impl(c, sched, n_msgs, sink, nullptr);
+  std::vector<gs_publish> ps(n_msgs);
+  for (uint64_t i = 0; i < n_msgs; i++) ps[i] = sched[perm[i]];
+  if (!sink) return run_messages_impl(c, ps.data(), n_msgs, nullptr, &cut);
+  // the results in class order, then every row back to its message
+  const uint32_t N = c.cfg.peers;
+  gs_result_sink ts = *sink;
+  std::vector<uint64_t> tc(sink->t_complete_ns ? (size_t)n_msgs * N : 0);
+  std::vector<uint8_t> hp(sink->hops ? (size_t)n_msgs * N : 0);
+  std::vector<gs_msg_summary> sm(sink->summary ? n_msgs : 0);
+  ts.t_complete_ns = sink->t_complete_ns ? tc.data() : nullptr;
+  ts.hops = sink->hops ? hp.data() : nullptr;
+  ts.summary = sink->summary ? sm.data() : nullptr;
+  run_messages_impl(c, ps.data(), n_msgs, &ts, &cut);
+  for (uint64_t i = 0; i < n_msgs; i++) {
+    const uint64_t m = perm[i];
+    if (sink->t_complete_ns) memcpy(sink->t_complete_ns + m * N, tc.data() + i * N, (size_t)N * 8);
+    if (sink->hops) memcpy(sink->hops + m * N, hp.data() + i * N, N);
+    if (sink->summary) sink->summary[m] = sm[i];
+  }
+}
+
+static void run_messages_impl(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_result_sink* sink,
+                              const std::vector<uint8_t>* cut) {
   const uint32_t N = c.cfg.peers;
   const uint32_t Bmax = c.cfg.batch;
   hipStream_t s = c.stream;
@@ -1496,34 +1625,49 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       }
     }
   } async_off{c};
-  // GS_PASS_SKIP=k (experiment): this run's work on every CU but every k-th
-  // (the CUs GS_CHAIN_CUS with GS_CU_STRIDE=k gives the epoch chain)
+  // Churn runs (config #3): the epoch chain is latency-bound and runs as fast on
+  // one XCD's 32 CUs as on all 256 (one L2 holds its per-peer state; bits 0..31
+  // of the CU mask, 4 CUs on each XCD, take twice as long), and the list pass at
+  // 100k peers as fast on 7 XCDs (or 4) as on 8 (profiles/r06_chain). So the
+  // chain gets its own XCD (c.chain_pipe, GS_CHAIN_XCDS, default XCD 0) and the
+  // rest of the run the others (c.pass_ms, GS_PASS_XCDS, default 1-7): the next
+  // batch's chain then runs beside this batch's passes (ChnAhead below).
+  // GS_CHN_PIPE=0 keeps one stream; GS_PASS_SKIP / GS_PASS_XCDS alone: experiments.
+  ensure_cus(c);
+  const char* pipe_env = getenv("GS_CHN_PIPE");
+  const bool pipe_on = c.cfg.churn_ppm && !(pipe_env && *pipe_env && atoi(pipe_env) == 0) && c.num_cus == 256 &&
+                       c.cfg.flood_publish && !c.traffic && !c.sink_dev && !getenv("GS_DEBUG_CHN");
   struct PassStream {
     Ctx& c;
-    hipStream_t orig = nullptr, ms = nullptr;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    PassStream(Ctx& cc) : c(cc) {
+    hipStream_t orig = nullptr;
+    PassStream(Ctx& cc, bool pipe) : c(cc) {
       const char* e = getenv("GS_PASS_SKIP");
-      if (!e || !*e || atoi(e) <= 0) return;
+      uint32_t px = xcd_env("GS_PASS_XCDS");
+      if (pipe) {
+        if (!c.chain_pipe) {
+          const uint32_t cx = xcd_env("GS_CHAIN_XCDS");
+          c.chain_pipe = xcd_stream(c, cx ? cx : 0x01u);
+        }
+        if (!px) px = 0xFEu & ~xcd_env("GS_CHAIN_XCDS");
+      }
+      if (!px && (!e || !*e || atoi(e) <= 0)) return;
+      if (!c.pass_ms) {  // created once per context (a CU-masked stream costs ~10 ms)
+        c.pass_ms = px ? xcd_stream(c, px) : cu_stream_except(c, 0, (uint32_t)atoi(e));
+        for (auto& ev : c.pass_ev) GS_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+      }
       orig = c.stream;
-      ms = cu_stream_except(c, 0, (uint32_t)atoi(e));
-      GS_HIP(hipEventCreateWithFlags(&e0, hipEventDisableTiming));
-      GS_HIP(hipEventCreateWithFlags(&e1, hipEventDisableTiming));
-      GS_HIP(hipEventRecord(e0, orig));
-      GS_HIP(hipStreamWaitEvent(ms, e0, 0));
-      c.stream = ms;
+      GS_HIP(hipEventRecord(c.pass_ev[0], orig));
+      GS_HIP(hipStreamWaitEvent(c.pass_ms, c.pass_ev[0], 0));
+      c.stream = c.pass_ms;
     }
     ~PassStream() {
-      if (!ms) return;
-      (void)hipEventRecord(e1, ms);
-      (void)hipStreamWaitEvent(orig, e1, 0);
+      if (!orig) return;
+      (void)hipEventRecord(c.pass_ev[1], c.pass_ms);
+      (void)hipStreamWaitEvent(orig, c.pass_ev[1], 0);
       (void)hipStreamSynchronize(orig);
       c.stream = orig;
-      (void)hipStreamDestroy(ms);
-      (void)hipEventDestroy(e0);
-      (void)hipEventDestroy(e1);
     }
-  } pass_stream{c};
+  } pass_stream{c, pipe_on};
   s = c.stream;
   GS_HIP(hipMemsetAsync(c.d_counters.p + C_ERR, 0, 8, s));
   check_schedule(c, sched, n_msgs);
@@ -1566,21 +1710,7 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
         c.fail(GS_EINVAL, "churn needs every publish within 2^20 heartbeats after hb_phase_ns");
       ep[i] = (sched[i].t_pub_ns - ph) / hb;
     }
-    if (!c.ring_R) {
-      const uint64_t w64 = ((uint64_t)N + 63) / 64;
-      const uint64_t per_slot = (uint64_t)N * MESH_W * 4 + w64 * 8 + (gossip ? (uint64_t)N * (GT_IN * 4 + 4) : 0) +
-                                (uint64_t)N * 8;
-      const char* rb = getenv("GS_RING_BUDGET_MB");  // test knob: force batch cuts at the ring size
-      const uint64_t budget = rb && *rb ? (uint64_t)atoll(rb) << 20 : 16ull << 30;
-      const uint64_t want = (uint64_t)Bmax + c.cfg.churn_horizon + 1;
-      c.ring_R = (uint32_t)std::min<uint64_t>(want, std::max<uint64_t>(c.cfg.churn_horizon + 2, budget / per_slot));
-      c.d_ring_mesh.alloc((size_t)c.ring_R * N * MESH_W);
-      c.d_ring_off.alloc((size_t)c.ring_R * w64);
-      if (c.max_degree <= CELL_W) c.d_ring_mm.alloc((size_t)c.ring_R * N);  // the churn list pass's meshes
-      if (gossip) {  // inverse IHAVE lists per (peer, epoch) beside the snapshots (ring_in_lists)
-        c.d_ring_in.alloc((size_t)c.ring_R * N * GT_IN);
-      }
-    }
+    ensure_ring(c);
   }
   const size_t max_tiles = ((size_t)N * Bmax * FPmax + 63) / 64;
   c.d_keys.alloc((size_t)N * Bmax * FPmax);
@@ -1631,7 +1761,8 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     const uint32_t Bc = std::min<uint32_t>(Bmax, PULL_LMAX / FP0);
     const uint64_t s_cap = std::min<uint64_t>({(uint64_t)sl_max, std::max<uint64_t>(1, SL_ROWS / N), ((1ull << 21) - 1) / N});
     uint64_t n_same = 1;  // messages of this shape from i0 (as far as a group can take)
-    while (n_same < s_cap * Bc && i0 + n_same < n_msgs && sched[i0 + n_same].msg_size == sched[i0].msg_size &&
+    while (n_same < s_cap * Bc && i0 + n_same < n_msgs && !(cut && (*cut)[i0 + n_same]) &&
+           sched[i0 + n_same].msg_size == sched[i0].msg_size &&
            frags_of(c, sched[i0 + n_same]) == F0)
       n_same++;
     const uint32_t S = (uint32_t)std::min<uint64_t>(n_same / Bc, s_cap);
@@ -1805,6 +1936,148 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
     i_end = i0 + (uint64_t)S * Bc;
     return true;
   };
+  // a batch: up to B messages of equal size and chunk count (serialisation
+  // tables and the lane layout are per batch); the pull path holds a row in
+  // registers, so its batch is capped at PULL_LMAX / FP messages. Returns the
+  // end; churn: the batch's publish epochs [h_lo, h_hi] (+ lifetime) fit the ring.
+  auto form = [&](uint64_t a0, uint64_t& h_lo, uint64_t& h_hi) -> uint64_t {
+    const uint32_t F0 = frags_of(c, sched[a0]);
+    const uint32_t Bcap = pull_any || (chn_any && F0 == 1)
+                              ? std::max<uint32_t>(1, std::min<uint32_t>(Bmax, PULL_LMAX / pow2_at_least(F0)))
+                              : Bmax;
+    uint64_t a1 = a0 + 1;
+    h_lo = churn ? ep[a0] : 0;
+    h_hi = churn ? ep[a0] : 0;
+    while (a1 < n_msgs && a1 - a0 < Bcap && !(cut && (*cut)[a1]) && sched[a1].msg_size == sched[a0].msg_size &&
+           frags_of(c, sched[a1]) == F0) {
+      if (churn) {
+        const uint64_t lo2 = std::min(h_lo, ep[a1]), hi2 = std::max(h_hi, ep[a1]);
+        if (hi2 + c.cfg.churn_horizon - lo2 + 1 > c.ring_R) break;
+        h_lo = lo2;
+        h_hi = hi2;
+      }
+      a1++;
+    }
+    return a1;
+  };
+  // churn: the batch runs on the churn list pass (gs_cpull.h) — lockstep
+  // single-fragment batches without IDONTWANT whose windows fit the rules
+  auto chn_decide = [&](const Batch& bb, const uint64_t* r0, uint64_t h_lo, uint64_t h_hi) -> bool {
+    if (!chn_any || bb.FP != 1 || bb.collide || !c.d_ring_mm.p) return false;
+    const uint64_t hb = c.cfg.heartbeat_ns;
+    const bool idw = c.cfg.idontwant && bb.payload >= c.cfg.idontwant;
+    bool lock = true;
+    for (uint32_t q = 1; q < bb.B && lock; q++) lock = r0[q] == r0[0];
+    const uint64_t dl = gossip ? std::min(bb.delta, bb.lat_min) : bb.delta;
+    const uint64_t cE = h_hi + c.cfg.churn_horizon - h_lo + 1;
+    return !idw && lock && cE <= 4096 && dl >= pull_grain(bb.tshift) && hb > lpull_rmax(bb) + 2 * dl &&
+           (!gossip || hb > bb.lat_max + dl);
+  };
+  // ChnAhead: the next churn list-pass batch's epoch chain and tables, enqueued
+  // on the chain's XCD (c.chain_pipe) while this batch's passes run on the
+  // others (the host enqueues the chain in slices between pass groups, at most
+  // AH_LEAD epochs ahead of what the GPU finished). The list pass reads only the
+  // batch tables, so the chain may overwrite ring slots of the batch whose
+  // passes run; a batch that falls back to the push path joins the chain first
+  // and has churn_ring replay its ring slots.
+  constexpr uint64_t AH_MARK = 16, AH_LEAD = 192, AH_SLICE = 64;
+  struct Ahead {
+    bool on = false, joined = false;
+    uint64_t i0 = 0, i1 = 0, h1 = 0;
+    ChnPrep cp;
+    EvRun* run = nullptr;
+    hipEvent_t ready = nullptr;
+    std::vector<hipEvent_t> marks;  // ring of events every AH_MARK epochs on the chain stream
+    uint64_t mark_n = 0, done_h = 0, enq_h = 0;
+  } ah;
+  struct AheadFree {
+    Ahead& ah;
+    ~AheadFree() {
+      if (ah.run) chain_free(ah.run);
+      if (ah.ready) (void)hipEventDestroy(ah.ready);
+      for (auto e : ah.marks) (void)hipEventDestroy(e);
+    }
+  } ah_free{ah};
+  std::vector<uint64_t> q0a(Bmax), r0a(Bmax);
+  static const bool dbg_ah = getenv("GS_DEBUG_AHEAD") != nullptr;
+  auto ah_enqueue_end = [&] {  // every epoch is enqueued: the rest of the tables, then `ready`
+    if (dbg_ah) fprintf(stderr, "[ah] batch %llu: chain enqueued (%llu epochs)\n", (unsigned long long)ah.i0,
+                        (unsigned long long)ah.enq_h);
+    chain_free(ah.run);
+    ah.run = nullptr;
+    chn_end(c, ah.cp, c.chain_pipe);
+    if (!ah.ready) GS_HIP(hipEventCreateWithFlags(&ah.ready, hipEventDisableTiming));
+    GS_HIP(hipEventRecord(ah.ready, c.chain_pipe));
+  };
+  auto ah_pump = [&](bool all) {  // more of the chain, keeping at most AH_LEAD epochs in flight
+    if (!ah.on || !ah.run) return;
+    while (ah.run) {
+      if (!all) {
+        while (ah.mark_n && ah.done_h + AH_MARK <= ah.enq_h) {  // the oldest outstanding mark
+          const uint64_t k = ah.done_h / AH_MARK + 1;  // mark k: after epoch k * AH_MARK of the run
+          if (k > ah.mark_n) break;
+          if (hipEventQuery(ah.marks[(k - 1) % ah.marks.size()]) != hipSuccess) break;
+          ah.done_h = k * AH_MARK;
+        }
+        if (ah.enq_h >= ah.done_h + AH_LEAD) return;
+      }
+      const uint64_t n = all ? ~0ull : std::min<uint64_t>(AH_SLICE, ah.done_h + AH_LEAD - ah.enq_h);
+      for (uint64_t k = 0; k < n && ah.run; k++) {
+        const bool fin = chain_advance(c, *ah.run, 1);
+        ah.enq_h++;
+        if (ah.enq_h % AH_MARK == 0) {
+          if (ah.marks.size() < 2 * AH_LEAD / AH_MARK + 2) {
+            hipEvent_t e;
+            GS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            ah.marks.push_back(e);
+          }
+          ah.mark_n = ah.enq_h / AH_MARK;
+          GS_HIP(hipEventRecord(ah.marks[(ah.mark_n - 1) % ah.marks.size()], c.chain_pipe));
+        }
+        if (fin) ah_enqueue_end();
+      }
+      if (!all) return;
+    }
+  };
+  auto ah_join = [&] {  // the prepared batch's tables before the main stream's next work
+    if (!ah.on || ah.joined) return;
+    ah_pump(true);
+    GS_HIP(hipStreamWaitEvent(c.stream, ah.ready, 0));
+    ah.joined = true;
+    if (dbg_ah) fprintf(stderr, "[ah] batch %llu: joined\n", (unsigned long long)ah.i0);
+  };
+  auto ah_start = [&](uint64_t n0) {
+    if (!pipe_on || ah.on || n0 >= n_msgs) return;
+    uint64_t hl = 0, hh = 0;
+    const uint64_t n1 = form(n0, hl, hh);
+    const Batch b2 = setup_batch(c, sched, n0, n1, false);
+    const uint64_t hb = c.cfg.heartbeat_ns, ph = c.cfg.hb_phase_ns;
+    for (uint32_t q = 0; q < b2.B; q++) {
+      q0a[q] = ep[n0 + q];
+      r0a[q] = b2.tpub[q] - ph - q0a[q] * hb;
+    }
+    const uint64_t h1 = hh + c.cfg.churn_horizon;
+    if (!chn_decide(b2, r0a.data(), hl, hh) || h1 <= c.churn_state) return;
+    const uint32_t par = c.ct_par ^ 1u;
+    // the chain overwrites ring slots: after every reader of this batch's slots on the main stream
+    if (!ah.ready) GS_HIP(hipEventCreateWithFlags(&ah.ready, hipEventDisableTiming));
+    GS_HIP(hipEventRecord(ah.ready, c.stream));
+    GS_HIP(hipStreamWaitEvent(c.chain_pipe, ah.ready, 0));
+    chn_begin(c, ah.cp, par, c.chain_pipe, hl, (uint32_t)(h1 - hl + 1), q0a.data(), sched + n0, b2.B);
+    ah.run = chain_begin(c, h1, c.chain_pipe, [&](uint64_t h) { chn_chunks(c, ah.cp, h, false); });
+    if (!ah.run) return;  // (not a plain continuation of the ring: the batch prepares in line)
+    c.ct_par = par;
+    ah.on = true;
+    ah.joined = false;
+    ah.i0 = n0;
+    ah.i1 = n1;
+    ah.h1 = h1;
+    ah.mark_n = ah.done_h = ah.enq_h = 0;
+    if (dbg_ah)
+      fprintf(stderr, "[ah] batch %llu..%llu: chain to epoch %llu (state %llu), tables %u\n", (unsigned long long)n0,
+              (unsigned long long)n1, (unsigned long long)h1, (unsigned long long)c.churn_state, par);
+    ah_pump(false);
+  };
   uint64_t i0 = 0;
   while (i0 < n_msgs) {
     if (i0 >= slice_skip) {
@@ -1814,73 +2087,61 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
         continue;
       }
     }
-    // a batch: up to B messages of equal size and chunk count (serialisation
-    // tables and the lane layout are per batch); the pull path holds a row in
-    // registers, so its batch is capped at PULL_LMAX / FP messages
-    const uint32_t F0 = frags_of(c, sched[i0]);
-    const uint32_t Bcap = pull_any || (chn_any && F0 == 1)
-                              ? std::max<uint32_t>(1, std::min<uint32_t>(Bmax, PULL_LMAX / pow2_at_least(F0)))
-                              : Bmax;
-    uint64_t i1 = i0 + 1;
-    uint64_t h_lo = churn ? ep[i0] : 0, h_hi = churn ? ep[i0] : 0;  // churn: publish epochs of the batch
-    while (i1 < n_msgs && i1 - i0 < Bcap && sched[i1].msg_size == sched[i0].msg_size &&
-           frags_of(c, sched[i1]) == F0) {
-      if (churn) {  // the batch's epochs (+ lifetime) must fit the ring
-        const uint64_t lo2 = std::min(h_lo, ep[i1]), hi2 = std::max(h_hi, ep[i1]);
-        if (hi2 + c.cfg.churn_horizon - lo2 + 1 > c.ring_R) break;
-        h_lo = lo2;
-        h_hi = hi2;
-      }
-      i1++;
-    }
+    uint64_t h_lo = 0, h_hi = 0;  // churn: publish epochs of the batch
+    const uint64_t i1 = form(i0, h_lo, h_hi);
     const Batch b = setup_batch(c, sched, i0, i1);
     const uint32_t FP = b.FP;
     bool chn = false;  // this batch runs on the churn list pass
+    ChnPrep cp;
     if (churn) {
       const uint64_t hb = c.cfg.heartbeat_ns, ph = c.cfg.hb_phase_ns;
       for (uint32_t q = 0; q < b.B; q++) {
         q0v[q] = ep[i0 + q];
         r0v[q] = b.tpub[q] - ph - q0v[q] * hb;
       }
-      if (chn_any && b.FP == 1 && !b.collide && c.d_ring_mm.p) {
-        const bool idw = c.cfg.idontwant && b.payload >= c.cfg.idontwant;
-        bool lock = true;
-        for (uint32_t q = 1; q < b.B && lock; q++) lock = r0v[q] == r0v[0];
-        const uint64_t dl = gossip ? std::min(b.delta, b.lat_min) : b.delta;
-        const uint64_t cE = h_hi + c.cfg.churn_horizon - h_lo + 1;
-        chn = !idw && lock && cE <= 4096 && dl >= pull_grain(b.tshift) && hb > lpull_rmax(b) + 2 * dl &&
-              (!gossip || hb > b.lat_max + dl);
+      chn = chn_decide(b, r0v.data(), h_lo, h_hi);
+      if (ah.on && !(chn && ah.i0 == i0 && ah.i1 == i1)) {  // (not expected: batches form the same way)
+        ah_join();
+        ah.on = false;
       }
-      c.ring_in_defer = chn;  // the push path's inverse IHAVE lists are not needed
-      c.ring_ell_defer = chn;  // nor the ELL snapshots (the pass reads the mask ring)
-      ChnPrep cp;
-      if (chn) {
-        chn_begin(c, cp, h_lo, (uint32_t)(h_hi + c.cfg.churn_horizon - h_lo + 1), q0v.data(), sched + i0, b.B);
-        c.epoch_hook = [&](uint64_t h) { chn_chunks(c, cp, h, false); };
-      }
-      try {
-        churn_ring(c, h_lo, h_hi + c.cfg.churn_horizon);
-      } catch (...) {
+      if (ah.on) {  // this batch's chain and tables ran ahead beside the last batch's passes
+        ah_join();
+        cp = ah.cp;
+        ah.on = false;
+      } else {
+        c.ring_in_defer = chn;  // the push path's inverse IHAVE lists are not needed
+        c.ring_ell_defer = chn;  // nor the ELL snapshots (the pass reads the mask ring)
+        if (chn) {
+          c.ct_par ^= 1u;
+          chn_begin(c, cp, c.ct_par, s, h_lo, (uint32_t)(h_hi + c.cfg.churn_horizon - h_lo + 1), q0v.data(), sched + i0,
+                    b.B);
+          cp.s = nullptr;  // (the chunk events go where churn_ring runs the chain)
+          c.epoch_hook = [&](uint64_t h) { chn_chunks(c, cp, h, false); };
+        }
+        try {
+          churn_ring(c, h_lo, h_hi + c.cfg.churn_horizon);
+        } catch (...) {
+          c.epoch_hook = nullptr;
+          c.ring_in_defer = false;
+          c.ring_ell_defer = false;
+          throw;
+        }
         c.epoch_hook = nullptr;
         c.ring_in_defer = false;
         c.ring_ell_defer = false;
-        throw;
+        // readers of the ELL snapshots beside the list pass: seeds to the mesh (no flood
+        // publish), the per-peer traffic pass, the GS_DEBUG_CHN check
+        if (chn && (!c.cfg.flood_publish || c.traffic || getenv("GS_DEBUG_CHN")))
+          ensure_ring_ell(c, h_lo, h_hi + c.cfg.churn_horizon);
+        //  a batch for the push path may overlap the last epochs of an
+        // earlier churn list-pass batch, which skipped their ELL snapshots and
+        // inverse IHAVE lists: rebuild those slots (tag-checked: free when current)
+        if (!chn) {
+          ensure_ring_ell(c, h_lo, h_hi + c.cfg.churn_horizon);
+          if (gossip) ensure_in_lists(c, h_lo, h_hi + c.cfg.churn_horizon);
+        }
+        if (chn) chn_end(c, cp);
       }
-      c.epoch_hook = nullptr;
-      c.ring_in_defer = false;
-      c.ring_ell_defer = false;
-      // readers of the ELL snapshots beside the list pass: seeds to the mesh (no flood
-      // publish), the per-peer traffic pass, the GS_DEBUG_CHN check
-      if (chn && (!c.cfg.flood_publish || c.traffic || getenv("GS_DEBUG_CHN")))
-        ensure_ring_ell(c, h_lo, h_hi + c.cfg.churn_horizon);
-      //  a batch for the push path may overlap the last epochs of an
-      // earlier churn list-pass batch, which skipped their ELL snapshots and
-      // inverse IHAVE lists: rebuild those slots (tag-checked: free when current)
-      if (!chn) {
-        ensure_ring_ell(c, h_lo, h_hi + c.cfg.churn_horizon);
-        if (gossip) ensure_in_lists(c, h_lo, h_hi + c.cfg.churn_horizon);
-      }
-      if (chn) chn_end(c, cp);
       c.d_q0.alloc(Bmax);
       c.d_r0.alloc(Bmax);
       GS_HIP(hipMemcpyAsync(c.d_q0.p, q0v.data(), b.B * 8, hipMemcpyHostToDevice, s));
@@ -2104,9 +2365,25 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
         reset(variant, false, false);
         const GosRun gr{rel0[0], c.cfg.heartbeat_ns};
         const ChnRun cr{h_lo, r0v[0], (uint32_t)(h_hi + c.cfg.churn_horizon - h_lo + 1),
-                        gossip ? (uint32_t)(habs0[0] - q0v[0]) : 0u};
+                        gossip ? (uint32_t)(habs0[0] - q0v[0]) : 0u, cp.par};
         const SinkWants sw = sink_wants(sink);
         const bool dense = sw.rows() || sw.summary || c.traffic || getenv("GS_LPULL_DENSE");
+        // the next batch's chain beside these passes, from the first pass group on:
+        // the seeds (k_seed reads this batch's offline bits in the ring) are
+        // enqueued by then, and the chain's stream waits for them
+        bool ah_tried = false;
+        if (pipe_on) c.pass_poll = [&] {
+          if (!ah_tried) {
+            ah_tried = true;
+            ah_start(i1);
+          } else {
+            ah_pump(false);
+          }
+        };
+        struct PollOff {
+          Ctx& c;
+          ~PollOff() { c.pass_poll = nullptr; }
+        } poll_off{c};
         if (run_lpull_batch(c, bc, K, lb, ev, n_ev, dev_cus, dense, false, gossip ? &gr : nullptr, &cr)) {
           if (gossip) c.stats.gossip_list_batches++;
           if (c.traffic) launch_traffic(c, b);
@@ -2115,6 +2392,10 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
         }
       }
       if (!done && getenv("GS_REQUIRE_LPULL")) c.fail(GS_EUNSUPPORTED, "churn list pass cannot take this batch (GS_REQUIRE_LPULL)");
+      if (!done) {  // the push path reads the ring: a chain ahead (of this batch or for the next one)
+        ah_join();    // may have run past or overwritten this batch's slots, or a replay moved the ring
+        churn_ring(c, h_lo, h_hi + c.cfg.churn_horizon);  // (no epochs when current; else runs / replays them)
+      }
       if (!done) ensure_ring_ell(c, h_lo, h_hi + c.cfg.churn_horizon);  // the push path reads the ELL ring
       if (!done && gossip) ensure_in_lists(c, h_lo, h_hi + c.cfg.churn_horizon);
     }
@@ -2175,6 +2456,7 @@ void run_messages(Ctx& c, const gs_publish* sched, uint64_t n_msgs, const gs_res
       }
     }
     if (!done) {
+      if (getenv("GS_REQUIRE_LPULL")) c.fail(GS_EUNSUPPORTED, "the push path would take this batch (GS_REQUIRE_LPULL)");
       if (gossip && !lanes32)
         c.fail(GS_EUNSUPPORTED, "lazy gossip changes this batch and the push path needs "
                                 "peers*batch*FP < 2^32: use a smaller batch");

@@ -622,3 +622,112 @@ def test_churn_links_changed_between_runs():
     assert st["list_pull_batches"] == 1
     for k in ("deliveries", "relaxations", "gossip_iwant", "latency_sum_ms"):
         assert st[k] == ref["stats"][k], k
+
+
+@pytest.mark.parametrize("gossip,pipe", [(1, "1"), (0, "1"), (1, "0")])
+def test_churn_list_pass_chain_ahead(monkeypatch, gossip, pipe):
+    """Churn batches back to back on the list pass: with GS_CHN_PIPE on (the
+    default on a 256-CU MI355X), batch k+1's epoch chain and tables are
+    enqueued on the chain's XCD while batch k's passes run on the others
+    (gs_relax.hip ChnAhead). Bit-exact against the oracle over 4 batches."""
+    monkeypatch.setenv("GS_CHN_PIPE", pipe)
+    monkeypatch.setenv("GS_REQUIRE_LPULL", "1")
+    hb = 400_000_000
+    kw = dict(churn_ppm=30000, lazy_gossip=gossip, heartbeat_ns=hb, churn_down=6, churn_horizon=10,
+              hb_phase_ns=T0 - 30 * hb + 150_000_000)
+    p = oracle.params(peers=900, seed=59, **kw)
+    M = 160
+    t = T0 + np.arange(M, dtype=np.uint64) * np.uint64(hb)
+    sched = (t, (6 + np.arange(M)) % 900, np.full(M, 15000))
+    sim, res = compare(p, 5, (50, 150, 40, 130), sched, batch=40)
+    st = sim.stats()
+    assert st["batches"] == 4 and st["list_pull_batches"] == 4
+    if gossip:
+        assert st["gossip_iwant"] > 0
+
+
+def test_churn_chain_ahead_then_push_fallback(monkeypatch):
+    """A batch whose candidate lists overflow falls back to the push path after
+    the next batch's chain already ran ahead (overwriting ring slots): it joins
+    that chain, churn_ring replays its ring slots, and every batch stays
+    bit-exact against the oracle."""
+    monkeypatch.setenv("GS_LPULL_CAP", "3")
+    hb = 400_000_000
+    kw = dict(churn_ppm=30000, lazy_gossip=1, heartbeat_ns=hb, churn_down=6, churn_horizon=10,
+              hb_phase_ns=T0 - 30 * hb + 150_000_000)
+    p = oracle.params(peers=900, seed=60, **kw)
+    M = 120
+    t = T0 + np.arange(M, dtype=np.uint64) * np.uint64(hb)
+    sched = (t, (6 + np.arange(M)) % 900, np.full(M, 15000))
+    sim, res = compare(p, 5, (50, 150, 40, 130), sched, batch=40)
+    st = sim.stats()
+    assert st["batches"] == 3 and st["list_pull_batches"] < 3
+
+
+def _nonlockstep_check(sim, st_expect_batches=None):
+    st = sim.stats()
+    assert st["list_pull_batches"] == st["batches"], st  # no batch on the push path (GS_REQUIRE_LPULL too)
+    if st_expect_batches is not None:
+        assert st["batches"] == st_expect_batches, st
+    return st
+
+
+def test_nonlockstep_delay_1500ms_gossip_on_list_pass(monkeypatch):
+    """run.sh's free message_delay (run.sh:36) at 1500 ms: publishes alternate
+    between two offsets into the heartbeat (+120 ms and +620 ms here), so no
+    batch is lockstep. The run regroups each batch's messages by offset class
+    (gs_relax.hip class_plan): one lockstep batch per class, IHAVE / IWANT
+    inside the list pass, results back in schedule order; bit-exact against
+    the oracle, IWANTs included, and no batch on the push path."""
+    monkeypatch.setenv("GS_REQUIRE_LPULL", "1")
+    p = oracle.params(peers=1500, seed=81, hb_phase_ns=(T0 + 120_000_000) % 1_000_000_000)
+    M = 48
+    t = T0 + np.arange(M, dtype=np.uint64) * np.uint64(1_500_000_000)
+    sched = (t, (6 + np.arange(M)) % 1500, np.full(M, 15000))
+    sim, res = compare(p, 5, (50, 150, 40, 130), sched, batch=64)
+    st = _nonlockstep_check(sim, 2)
+    assert st["gossip_iwant"] > 0 and st["gossip_list_batches"] >= 1
+
+
+def test_nonlockstep_random_schedule_file_gossip(tmp_path, monkeypatch):
+    """An arbitrary POST /publish sequence (main.rs:146-221) read from a
+    schedule file (gs_read_schedule): random publish times at 1 ms grain,
+    random publishers, every message its own offset class; each runs as a
+    lockstep list-pass batch with the gossip inside the passes; bit-exact
+    against the oracle and never on the push path."""
+    monkeypatch.setenv("GS_REQUIRE_LPULL", "1")
+    rng = np.random.default_rng(5)
+    M, N = 24, 1200
+    t = np.sort(T0 + rng.integers(0, 30_000, M).astype(np.uint64) * np.uint64(1_000_000))
+    pub = rng.integers(0, N, M)
+    f = tmp_path / "sched.txt"
+    f.write_text("".join("%d %d %d\n" % (int(a), int(b), 15000) for a, b in zip(t, pub)))
+    arr = np.ctypeslib.as_array(gossipsim.read_schedule(str(f)))
+    np.testing.assert_array_equal(arr["t_pub_ns"], t)
+    np.testing.assert_array_equal(arr["publisher"], pub)
+    sched = (arr["t_pub_ns"].copy(), arr["publisher"].astype(np.int64), arr["msg_size"].astype(np.int64))
+    p = oracle.params(peers=N, seed=82, hb_phase_ns=(T0 + 120_000_000) % 1_000_000_000)
+    sim, res = compare(p, 5, (50, 150, 40, 130), sched, batch=64)
+    st = _nonlockstep_check(sim)
+    assert st["batches"] == len(set(int(x) % 1_000_000_000 for x in t))
+
+
+@pytest.mark.parametrize("gossip", [1, 0])
+def test_nonlockstep_churn_delay_on_list_pass(monkeypatch, gossip):
+    """Churn with publishes 1.5 heartbeats apart: two offsets into the epoch,
+    regrouped into one churn list-pass batch each (the ring holds the batch's
+    epochs for both; the second batch's tables come from the ring). Bit-exact
+    against the oracle, no push-path batch."""
+    monkeypatch.setenv("GS_REQUIRE_LPULL", "1")
+    hb = 400_000_000
+    kw = dict(churn_ppm=30000, lazy_gossip=gossip, heartbeat_ns=hb, churn_down=6, churn_horizon=10,
+              hb_phase_ns=T0 - 30 * hb + 150_000_000)
+    p = oracle.params(peers=900, seed=83, **kw)
+    M = 40
+    t = T0 + np.arange(M, dtype=np.uint64) * np.uint64(600_000_000)
+    sched = (t, (6 + np.arange(M)) % 900, np.full(M, 15000))
+    sim, res = compare(p, 5, (50, 150, 40, 130), sched, batch=64)
+    st = _nonlockstep_check(sim, 2)
+    assert 0 < st["deliveries"] < M * 899
+    if gossip:
+        assert st["gossip_iwant"] > 0
