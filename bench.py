@@ -420,7 +420,23 @@ CONFIGS = {
         peers=100_000, links=(5, 50, 150, 40, 130), fragments=1, batch=1024, msgs=4096, warm_msgs=4096,
         knobs=dict(lazy_gossip=1, churn_ppm=10_000, churn_down=10, churn_horizon=16,
                    heartbeat_ns=1_000_000_000, hb_phase_ns=gossipsim.T0_NS - 20 * 1_000_000_000 + 370_000_000)),
+    # run.sh's free message_delay (run.sh:36) at 1500 ms under config #3: two offsets into the
+    # heartbeat, each group of messages regrouped into one lockstep churn list-pass batch per
+    # offset class
+    "c3_100k_delay1500ms": dict(
+        peers=100_000, links=(5, 50, 150, 40, 130), fragments=1, batch=1024, msgs=1024, delay_ns=1_500_000_000,
+        knobs=dict(lazy_gossip=1, churn_ppm=10_000, churn_down=10, churn_horizon=16,
+                   heartbeat_ns=1_000_000_000, hb_phase_ns=gossipsim.T0_NS - 20 * 1_000_000_000 + 370_000_000)),
 }
+
+
+def config_sched(step, msgs, peers, msg_size, delay_ns=None):
+    """shard_messages(step, 0, 1, msgs, ...) with another publish spacing (run.sh's message_delay)"""
+    t, pub, size = gossipsim.shard_messages(step, 0, 1, msgs, peers, msg_size)
+    if delay_ns:
+        idx = np.uint64(step) * np.uint64(msgs) + np.arange(msgs, dtype=np.uint64)
+        t = np.uint64(gossipsim.T0_NS) + idx * np.uint64(delay_ns)
+    return t, pub, size
 
 
 def config_traffic(args):
@@ -441,14 +457,14 @@ def config_rates(args, local):
         sim.set_topogen_links(c["links"][0], *c["links"][1:])
         sim.connect_gossipsub_peers()
         sim.mesh_converge(args.max_heartbeats)
-        sim.run(gossipsim.shard_messages(0, 0, 1, c.get("warm_msgs", c["batch"]), c["peers"], args.msg_size),
+        sim.run(config_sched(0, c.get("warm_msgs", c["batch"]), c["peers"], args.msg_size, c.get("delay_ns")),
                 collect=False)
         # repeats: the best of `reps` runs (config #1 runs ~1 ms, where one host hiccup doubles it);
         # every repeat simulates the same messages, so the counters are one run's
         dt = None
         for _ in range(c.get("reps", 1)):
             sim.reset_stats()
-            sched = gossipsim.shard_messages(1, 0, 1, c["msgs"], c["peers"], args.msg_size)  # after the warm-up's
+            sched = config_sched(1, c["msgs"], c["peers"], args.msg_size, c.get("delay_ns"))  # after the warm-up's
             t0, m0 = time.perf_counter(), time.monotonic_ns()
             sim.run(sched, collect=False)
             d = time.perf_counter() - t0

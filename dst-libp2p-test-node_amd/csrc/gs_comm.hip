@@ -209,13 +209,20 @@ void coll_group_end(gs_comm* cm) {
     at[x.peer] += x.bytes;
   }
   if (s) GS_HIP(hipStreamSynchronize(s));
+  // a rank's own transfers (the push protocol sends a part's records to itself)
+  // stay here: the transport sees 0 bytes for the own entry
+  const uint32_t me = cm->rank;
+  if (sn[me] != rn[me]) throw Error(GS_EINVAL, "internal: own send and receive differ in the ops exchange");
+  if (rn[me]) memcpy(rb[me].data(), sb[me].data(), rn[me]);
+  std::vector<uint64_t> sx = sn, rx = rn;
+  sx[me] = rx[me] = 0;
   std::vector<const void*> sp(P);
   std::vector<void*> rp(P);
   for (uint32_t p = 0; p < P; p++) {
     sp[p] = sb[p].data();
     rp[p] = rb[p].data();
   }
-  ops_fail(cm->ops.exchange(cm->ops.user, sp.data(), sn.data(), rp.data(), rn.data()), "exchange");
+  ops_fail(cm->ops.exchange(cm->ops.user, sp.data(), sx.data(), rp.data(), rx.data()), "exchange");
   std::fill(at.begin(), at.end(), 0);
   for (const auto& x : cm->xr) {
     if (x.bytes) GS_HIP(hipMemcpyAsync(x.dst, rb[x.peer].data() + at[x.peer], x.bytes, hipMemcpyHostToDevice, s));

@@ -478,8 +478,8 @@ __device__ __forceinline__ void glp_ihave_ent(const LPullArgs& a, uint64_t* CW, 
 #ifndef GS_LP_RCH
 #define GS_LP_RCH 2
 #endif
-#ifndef GS_LP_SKIP  // record chunks past a neighbour's count skipped by a scalar branch (A/B: -DGS_LP_SKIP=0)
-#define GS_LP_SKIP 1
+#ifndef GS_LP_SKIP  // record chunks past a neighbour's count skipped by a scalar branch (off: +1.3 % per step, r06)
+#define GS_LP_SKIP 0
 #endif
 template <int FP, uint32_t CH, bool IDW = false, bool PART = false, bool GOS = false, bool CHN = false>
 __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {

@@ -666,7 +666,9 @@ def test_churn_chain_ahead_then_push_fallback(monkeypatch):
 
 def _nonlockstep_check(sim, st_expect_batches=None):
     st = sim.stats()
-    assert st["list_pull_batches"] == st["batches"], st  # no batch on the push path (GS_REQUIRE_LPULL too)
+    # every batch on the list pass: GS_REQUIRE_LPULL fails any push-path batch; a batch
+    # whose eager pass failed the gossip no-op proof counts twice (the re-run in-pass)
+    assert st["list_pull_batches"] >= st["batches"], st
     if st_expect_batches is not None:
         assert st["batches"] == st_expect_batches, st
     return st
