@@ -35,6 +35,20 @@ METRIC = "simulated peer-msg deliveries/sec at 100k & 1M peers; % of HBM BW"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
 
+def exchange_label(world, parts):
+    """The partitioned list pass's record exchange (gs_comm.hip
+    gs_run_partitioned): loop-back parts on one device route by default with
+    direct stores; ranks gather by default; GS_PART_ROUTE / GS_PART_DIRECT
+    override."""
+    rte, dre = os.environ.get("GS_PART_ROUTE", ""), os.environ.get("GS_PART_DIRECT", "")
+    local = world == 1 and parts > 1
+    direct_ok = local and dre != "0"
+    routed = ((rte != "0") if rte else direct_ok) and max(world, parts) <= 16  # PART_ROUTE_PMAX
+    if not routed:
+        return "gathered"
+    return "routed, direct stores" if direct_ok else "routed, send segments"
+
+
 def fp_lanes(f):
     p = 1
     while p < f:
@@ -627,6 +641,7 @@ def main():
                 "parallelism": "msg-shard%d" % world if args.mode == "msg" else
                 ("peer-part%d (RCCL ranks)" % world if world > 1 or args.parts == 1 else
                  "peer-part%d (loop-back parts on one GPU)" % args.parts),
+                "exchange": None if args.mode == "msg" else exchange_label(world, args.parts),
             },
             "deliveries": int(deliveries),
             "frag_deliveries": int(tot[1]),

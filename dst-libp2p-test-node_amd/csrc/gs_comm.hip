@@ -586,7 +586,8 @@ bool run_batch_lp(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched,
       gs_status code = GS_OK;
       bool ok = false;
       try {
-        ok = part_lp_begin(*cx[i], sched + i0, B, &smin[i]);
+        ok = part_lp_begin(*cx[i], sched + i0, B);
+        if (ok) smin[i] = part_lp_seed_min(*cx[i]);
       } catch (const Error& e) {
         code = e.code;
         why = e.msg;
@@ -594,10 +595,15 @@ bool run_batch_lp(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched,
       rank_status(cm, *cx[i], code != GS_OK);
       if (code != GS_OK) throw Error(code, why);
       bad |= ok ? 0u : 1u;
-    } else if (!part_lp_begin(*cx[i], sched + i0, B, &smin[i])) {
+    } else if (!part_lp_begin(*cx[i], sched + i0, B)) {
       bad = 1;
     }
   }
+  if (cm->local && !bad)  // every part's setup enqueued: now wait for each one's seeds
+    for (uint32_t i = 0; i < nctx; i++) {
+      GS_HIP(hipSetDevice(cx[i]->cfg.device));
+      smin[i] = part_lp_seed_min(*cx[i]);
+    }
   if (!cm->local) {
     uint64_t mine[2] = {bad, ~smin[0]}, all[2 * 64];
     rank_gather(cm, *cx[0], mine, 2, all);
@@ -630,10 +636,19 @@ bool run_batch_lp(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched,
   const PartLayout lay{P, N, B};
   const size_t RB = 8;  // bytes per record
   std::vector<uint64_t> st((size_t)P * 4);  // per part: mode, records, min pending, error word
-  // the record exchange: routed per destination part (GS_PART_ROUTE=1; at most
-  // PART_ROUTE_PMAX parts), or every part's records to every part (the default)
+  // the record exchange: routed per destination part (at most PART_ROUTE_PMAX
+  // parts), or every part's records to every part. Loop-back parts on one
+  // device route by default, each part's pack storing straight into the
+  // destination contexts (no copies); ranks gather by default. GS_PART_ROUTE
+  // = 1 / 0 forces routed / gathered (loop-back routed then goes through send
+  // segments and copies, as ranks do, when GS_PART_DIRECT=0).
   const char* rte = getenv("GS_PART_ROUTE");
-  const bool routed = P <= PART_ROUTE_PMAX && rte && *rte && atoi(rte) != 0;
+  bool one_dev = cm->local != 0;
+  for (uint32_t i = 1; i < nctx; i++) one_dev = one_dev && cx[i]->cfg.device == cx[0]->cfg.device;
+  const char* dre = getenv("GS_PART_DIRECT");
+  const bool direct_ok = one_dev && P <= PART_ROUTE_PMAX && !(dre && *dre && atoi(dre) == 0);
+  const bool routed = P <= PART_ROUTE_PMAX && ((rte && *rte) ? atoi(rte) != 0 : direct_ok);
+  const bool direct = routed && direct_ok;
   for (;;) {
     for (uint32_t i = 0; i < nctx; i++) {
       GS_HIP(hipSetDevice(cx[i]->cfg.device));
@@ -642,9 +657,13 @@ bool run_batch_lp(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched,
       if (cx[i]->timing) ev(i);
     }
     if (cm->local) {
+      for (uint32_t i = 0; i < nctx; i++) {  // every part's control read in flight, then each one waited for
+        GS_HIP(hipSetDevice(cx[i]->cfg.device));
+        part_lp_read_enqueue(*cx[i]);
+      }
       for (uint32_t i = 0; i < nctx; i++) {
         GS_HIP(hipSetDevice(cx[i]->cfg.device));
-        part_lp_read(*cx[i], &st[(size_t)i * 4]);
+        part_lp_read_wait(*cx[i], &st[(size_t)i * 4]);
       }
     } else {
       uint64_t mine[4];
@@ -672,6 +691,19 @@ bool run_batch_lp(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched,
     if (!recs) continue;  // the next pass emits a window: it reads no records
     std::vector<uint64_t> base(P + 1, 0), cnt(P);
     for (uint32_t p = 0; p < P; p++) cnt[p] = st[(size_t)p * 4 + 1];
+    if (direct) {  // every part stores its routed records into the destinations (gathered bases, holes allowed)
+      lp_bases(cnt.data(), P, base.data());
+      for (uint32_t i = 0; i < nctx; i++) cx[i]->d_rpk.alloc(recs);  // (before any pack stores into it)
+      for (uint32_t i = 0; i < nctx; i++) {
+        part_lp_pack_route_direct(cx, P, i, base[i]);
+        if (!cx[i]->part_xev) GS_HIP(hipEventCreateWithFlags(&cx[i]->part_xev, hipEventDisableTiming));
+        GS_HIP(hipEventRecord(cx[i]->part_xev, cx[i]->stream));
+      }
+      for (uint32_t q = 0; q < nctx; q++)  // the next pass of q reads what every part stored into it
+        for (uint32_t i = 0; i < nctx; i++)
+          if (i != q) GS_HIP(hipStreamWaitEvent(cx[q]->stream, cx[i]->part_xev, 0));
+      continue;
+    }
     if (routed) {  // each part receives only the records with a receiver it owns (gs_layout.h lp_route_bases)
       std::vector<uint64_t> route((size_t)P * P), bq(P);
       for (uint32_t i = 0; i < nctx; i++) {
@@ -803,9 +835,13 @@ bool run_batch_lp(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched,
   }
   // completion + the lazy-gossip no-op proof of every part
   bool ok = true;
+  for (uint32_t i = 0; i < nctx; i++) {  // every part's completion enqueued, then each one waited for
+    GS_HIP(hipSetDevice(cx[i]->cfg.device));
+    part_lp_end_enqueue(*cx[i], sinks ? &sinks[i] : nullptr);
+  }
   for (uint32_t i = 0; i < nctx; i++) {
     GS_HIP(hipSetDevice(cx[i]->cfg.device));
-    ok = part_lp_end(*cx[i], sinks ? &sinks[i] : nullptr) && ok;
+    ok = part_lp_end_check(*cx[i]) && ok;
   }
   if (!cm->local && cx[0]->cfg.lazy_gossip) {
     uint64_t mine = ok ? 0 : 1, all[64];

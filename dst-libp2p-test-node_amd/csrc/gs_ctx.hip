@@ -46,6 +46,7 @@ Ctx::~Ctx() {
     if (e) (void)hipEventDestroy(e);
   if (h_laterr) (void)hipHostFree(h_laterr);
   if (copy) (void)hipStreamDestroy(copy);
+  if (part_xev) (void)hipEventDestroy(part_xev);
   if (h_pinned) (void)hipHostFree(h_pinned);
   if (h_block) (void)hipHostFree(h_block);
   if (h_slms) (void)hipHostFree(h_slms);

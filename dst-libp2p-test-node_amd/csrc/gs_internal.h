@@ -262,6 +262,7 @@ struct Ctx {
   DevBuf<uint32_t> d_rcg;    // [N] records per peer (global ids)
   DevBuf<uint64_t> d_roffg;  // [N] their offsets in d_rpk
   DevBuf<uint64_t> d_rpk;    // every part's records of the last pass
+  hipEvent_t part_xev = nullptr;  // loop-back routed stores of the last pass done (other parts wait on it)
   DevBuf<uint64_t> d_pkcur;  // pack cursor (routed: one per destination part)
   // routed exchange (k_lpack_route): the records for each other part [P][cap] and
   // this part's per-peer offsets / counts for each destination [P][un]
@@ -352,15 +353,20 @@ void part_dev_finish(Ctx& c, const gs_result_sink* sink, uint64_t row0);
 void part_abort(Ctx& c);
 bool part_needs_ms(Ctx& c, const gs_publish* sched, uint64_t n_msgs);
 // the list pass over partitioned rows (gs_part.h)
-bool part_lp_begin(Ctx& c, const gs_publish* sched, uint64_t n_msgs, uint64_t* seed_min);
+bool part_lp_begin(Ctx& c, const gs_publish* sched, uint64_t n_msgs);  // enqueued: then part_lp_seed_min
+uint64_t part_lp_seed_min(Ctx& c);  // wait for the part's seeds: their min key
 void part_lp_pass(Ctx& c);
 void part_lp_read(Ctx& c, uint64_t out[4]);  // last pass: mode, records, min pending, error word
+void part_lp_read_enqueue(Ctx& c);                   // part_lp_read in two steps
+void part_lp_read_wait(Ctx& c, uint64_t out[4]);
 void part_lp_set(Ctx& c, uint64_t records, uint64_t minp);  // the combined values into the last pass's slot
 void part_lp_pack(Ctx& c, uint64_t base, uint64_t mine);
 void part_lp_pack_route(Ctx& c, uint32_t P, uint32_t me, uint64_t mine);
+void part_lp_pack_route_direct(Ctx** cx, uint32_t P, uint32_t me, uint64_t base);
 void part_lp_route_read(Ctx& c, uint32_t P, uint64_t* counts);
 void part_lp_route_fix(Ctx& c, uint32_t P, uint32_t me, const uint64_t* base);
-bool part_lp_end(Ctx& c, const gs_result_sink* sink);  // completion (final logs or dense rows), gossip proof
+void part_lp_end_enqueue(Ctx& c, const gs_result_sink* sink);  // completion (final logs or dense rows)
+bool part_lp_end_check(Ctx& c);  // wait, then the gossip proof
 void part_lp_abort(Ctx& c);
 
 // small device helpers

@@ -1823,48 +1823,66 @@ __global__ __launch_bounds__(TB) void k_lpack(const uint64_t* __restrict__ rec, 
 // the records with a receiver q owns (a bit of the record's inclusion mask at
 // a mesh position whose peer is in q; the own part gets every record), each
 // row's records contiguous and in emission order. One wave per 64 rows, the
-// rows' records walked as one sequence 64 at a time (lane -> record), P <= LP_PMAX:
-//  0. lane = row: the owning part of each mesh entry, once per row, by
-//     comparing the peer with the parts' first peers (own64: 4 bits per entry);
-//  1. lane = record: its destination set dm (one bit per part: the owners of
-//     the mask's receivers, plus the own part); per destination a ballot, and
-//     the last lane of each row's run of lanes adds the run's count to LDS;
-//  2. one claim per (wave, destination) reserves the space (cursor[q]); the
-//     per-row offset / count tables are written;
+// rows' records walked as one sequence 64 at a time (lane -> record);
+// PM (4, 8 or 16) >= P destinations, the loops over them unrolled:
+//  0. lane = row: per destination q the mask of the row's mesh entries q owns
+//     (smq; bit 16: the own part), from comparisons with the parts' first
+//     peers (no division);
+//  1. lane = record: per destination one compare of (inclusion mask | valid
+//     bit) with the row's mask gives the ballot; each row's run of lanes counts
+//     its bits (popcounts of the ballots below the run's last lane), packed two
+//     destinations per word, and the run's last lane adds them to LDS;
+//  2. all destinations' claims in one atomic instruction (lane q claims
+//     cursor[q] for the wave); the per-row offset / count tables are written;
 //  3. lane = record again: per destination its position = the row's write
 //     position + the run's lanes below it with that bit; the run's last lane
-//     advances the row's position.
-// A lane finds its record's row from the rows that start inside the chunk (a
-// ballot of the row starts + one LDS lookup), not by a search over the rows.
-// Own part: into the gathered buffer at base 0 (out_own) with the global
-// offset tables at its peers (roff_own / rcg_own); other parts: out[q * cap ..]
-// with per-destination tables roff[q * un + r] (relative to the segment) /
-// rcg[q * un + r].
-constexpr uint32_t LP_PMAX = 16;
+//     stores the row's advanced positions.
+// The walk goes LP_RW chunks at a time: one LDS table maps each lane of the
+// window to the row starting there, and the window's record loads are issued
+// together (its chunks are independent until their LDS updates).
+// Destination q's records go to d.out[q], its offset / count tables at this
+// part's rows to d.roff[q][r] (+ d.ob[q]) / d.rcg[q][r]: for ranks, send
+// segments and tables per destination (the own part: its gathered buffer at
+// base 0 and its global tables); for loop-back parts on one device, straight
+// into each destination context's gathered buffer and global tables.
+constexpr uint32_t LP_PMAX = 16, LP_RW = 8;
 struct RouteLo {
   uint32_t lo[LP_PMAX];  // lo[q]: the first peer of part q (gs_layout.h u0)
 };
+struct RouteDst {
+  uint64_t* out[LP_PMAX];   // destination q's records of this part
+  uint64_t* roff[LP_PMAX];  // their offsets, by local row
+  uint32_t* rcg[LP_PMAX];   // their counts, by local row
+  uint64_t ob[LP_PMAX];     // added to the offsets (the segment's base in q's buffer)
+};
+template <uint32_t PM>
 __global__ __launch_bounds__(TB) void k_lpack_route(const uint64_t* __restrict__ rec, const uint32_t* __restrict__ cnt,
                                                     const uint32_t* __restrict__ mesh, uint32_t u0, uint32_t un,
-                                                    uint32_t L, uint32_t P, uint32_t me, uint64_t cap,
-                                                    uint64_t* __restrict__ out, uint64_t* __restrict__ out_own,
-                                                    uint64_t* __restrict__ roff, uint32_t* __restrict__ rcg,
-                                                    uint64_t* __restrict__ roff_own, uint32_t* __restrict__ rcg_own,
-                                                    unsigned long long* cursor, RouteLo rl) {
-  __shared__ uint64_t sown[TB / 64][64];          // per row: the owning part of each mesh entry (4 bits each)
-  __shared__ uint32_t sco[TB / 64][64][LP_PMAX];  // per row and destination: count, then next write position
-  __shared__ uint32_t spre[TB / 64][64];          // exclusive prefix of the rows' record counts
-  __shared__ uint8_t srow[TB / 64][64];           // chunk lane -> the row whose records start there
+                                                    uint32_t L, uint32_t P, uint32_t me, unsigned long long* cursor,
+                                                    RouteLo rl, RouteDst d) {
+  static_assert(MESH_W == 16 && PM % 4 == 0 && PM <= LP_PMAX, "17-bit masks, uint4 rows");
+  constexpr uint32_t VB = 1u << MESH_W;                 // mask bit: a valid record (the own part's)
+  __shared__ uint4 smq[TB / 64][64][PM / 4];            // per row: destination q's mask in word q
+  __shared__ uint4 sco[TB / 64][64][PM / 4];            // per row: packed counts (16 bits each), then positions
+  __shared__ uint32_t spre[TB / 64][64];                // exclusive prefix of the rows' record counts
+  __shared__ uint64_t srow[TB / 64][LP_RW * 64 / 8];    // window lane -> the row whose records start there (bytes)
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t wave = blockIdx.x * (TB / 64) + wv, nw = gridDim.x * (TB / 64);
   const uint64_t upto = lane == 63 ? ~0ull : (2ull << lane) - 1;  // lanes <= this one
   const uint64_t below = (1ull << lane) - 1;
+  uint8_t* const srb = reinterpret_cast<uint8_t*>(srow[wv]);
+  auto word = [](const uint4 (&a)[PM / 4], uint32_t q) -> uint32_t {  // (q a constant after unrolling)
+    const uint4& h = a[q >> 2];
+    return (q & 3) == 0 ? h.x : (q & 3) == 1 ? h.y : (q & 3) == 2 ? h.z : h.w;
+  };
   for (uint32_t r0 = wave * 64; r0 < un; r0 += nw * 64) {
-    // 0. lane j: row r0 + j — its record count and the owners of its mesh entries
+    // 0. lane j: row r0 + j — its record count and its destinations' masks
     const uint32_t r = r0 + (uint32_t)lane;
     const bool rv = r < un;
     const uint32_t n = rv ? cnt[r] : 0u;
-    uint64_t own = 0;
+    uint32_t mq[PM];
+#pragma unroll
+    for (uint32_t q = 0; q < PM; q++) mq[q] = q == me ? VB : 0u;
     if (rv) {
       const uint4* mp = reinterpret_cast<const uint4*>(mesh + (size_t)(u0 + r) * MESH_W);
 #pragma unroll
@@ -1874,14 +1892,19 @@ __global__ __launch_bounds__(TB) void k_lpack_route(const uint64_t* __restrict__
 #pragma unroll
         for (int u = 0; u < 4; u++) {
           const uint32_t x = e4[u] & 0xFFFFFFu;  // (EMPTY entries: never a receiver bit)
-          uint32_t o = 0;
-          for (uint32_t q = 1; q < P; q++) o += x >= rl.lo[q] ? 1u : 0u;  // wave-uniform bound
-          own |= (uint64_t)o << (4 * (4 * k4 + u));
+#pragma unroll
+          for (uint32_t q = 0; q < PM; q++) {
+            const bool in = q < P && (q == 0 || x >= rl.lo[q]) && (q + 1 >= P || x < rl.lo[q + 1]);
+            mq[q] |= in ? 1u << (4 * k4 + u) : 0u;
+          }
         }
       }
     }
-    sown[wv][lane] = own;
-    for (uint32_t q = 0; q < P; q++) sco[wv][lane][q] = 0;
+#pragma unroll
+    for (uint32_t q4 = 0; q4 < PM / 4; q4++) {
+      smq[wv][lane][q4] = make_uint4(mq[4 * q4], mq[4 * q4 + 1], mq[4 * q4 + 2], mq[4 * q4 + 3]);
+      sco[wv][lane][q4] = make_uint4(0, 0, 0, 0);
+    }
     uint32_t x = n;  // inclusive prefix over the 64 rows
     for (int off = 1; off < 64; off <<= 1) {
       const uint32_t y = __shfl_up(x, off);
@@ -1889,101 +1912,132 @@ __global__ __launch_bounds__(TB) void k_lpack_route(const uint64_t* __restrict__
     }
     const uint32_t pre = x - n, T = __shfl(x, 63);
     spre[wv][lane] = pre;
-    // the record of lane `lane` in chunk t0: its row j, index i in the row, run [p0, last]
-    auto locate = [&](uint32_t t0, uint32_t jc, uint64_t& sm, uint32_t& j, uint32_t& i, uint32_t& p0) {
-      srow[wv][lane] = 0xFF;  // no row starts at this lane (yet)
-      wave_lds_sync();
-      const bool st = n && pre >= t0 && pre - t0 < 64;  // (row view) this row's records start in the chunk
-      if (st) srow[wv][pre - t0] = (uint8_t)lane;
-      wave_lds_sync();
-      const uint32_t here = srow[wv][lane];  // (record view) the row starting at this lane, or 0xFF
-      sm = __ballot(here != 0xFFu);          // bit l: a row's records start at chunk lane l
-      const uint64_t sb = sm & upto;
-      p0 = sb ? 63u - (uint32_t)__builtin_clzll(sb) : 0u;
-      j = sb ? (uint32_t)__shfl((int)here, (int)p0) : jc;
-      i = t0 + (uint32_t)lane - spre[wv][j];
+    // One window of LP_RW chunks from t0: each lane's record xr and its mask
+    // bits im (inclusion mask | VB if valid), its row j, whether it is its
+    // run's last lane, and the run [p0, lane] / [p0, lane).
+    struct Chunk {
+      uint64_t xr, rle, rlt;
+      uint32_t j, im;
+      bool last;
     };
-    // lanes [p0, lane] (run) and [p0, lane) (run below this lane)
-    auto runs = [&](uint32_t p0, uint64_t& run_le, uint64_t& run_lt) {
-      const uint64_t from = ~((1ull << p0) - 1);
-      run_le = upto & from;
-      run_lt = below & from;
-    };
-    constexpr uint32_t IM = ((1u << MESH_W) - 1u) << LP_IM_SHIFT;
-    auto dests = [&](uint32_t im, uint64_t ow) {  // the record's destination parts (+ the own part)
-      uint32_t dm = 1u << me, m = im >> LP_IM_SHIFT;
-      while (m) {
-        const uint32_t k = (uint32_t)__builtin_ctz(m);
-        m &= m - 1;
-        dm |= 1u << ((uint32_t)(ow >> (4 * k)) & 15u);
+    auto window = [&](uint32_t t0, uint32_t& jc, Chunk (&ck)[LP_RW]) {
+      srow[wv][lane] = ~0ull;  // no row starts here (yet)
+      wave_lds_sync();
+      if (n && pre >= t0 && pre - t0 < LP_RW * 64) srb[pre - t0] = (uint8_t)lane;
+      wave_lds_sync();
+#pragma unroll
+      for (uint32_t w = 0; w < LP_RW; w++) {
+        const uint32_t t = t0 + 64 * w + (uint32_t)lane;
+        const uint32_t here = srb[64 * w + lane];  // the row starting at this lane, or 0xFF
+        const uint64_t sm = __ballot(here != 0xFFu);
+        const uint64_t sb = sm & upto;
+        const uint32_t p0 = sb ? 63u - (uint32_t)__builtin_clzll(sb) : 0u;
+        const uint32_t j = sb ? (uint32_t)__shfl((int)here, (int)p0) : jc;
+        jc = (uint32_t)__builtin_amdgcn_readlane((int)j, 63);
+        const bool v = t < T;
+        const uint64_t from = ~((1ull << p0) - 1);
+        ck[w].j = j;
+        ck[w].rle = upto & from;
+        ck[w].rlt = below & from;
+        ck[w].last = v && (lane == 63 || ((sm >> (lane + 1)) & 1) || t + 1 == T);
+        ck[w].xr = v ? rec[(size_t)(r0 + j) * L + (t - spre[wv][j])] : 0ull;
       }
-      return dm;
+#pragma unroll
+      for (uint32_t w = 0; w < LP_RW; w++) {
+        const bool v = t0 + 64 * w + (uint32_t)lane < T;
+        ck[w].im = v ? ((((uint32_t)ck[w].xr >> LP_IM_SHIFT) & (VB - 1)) | VB) : 0u;
+      }
     };
-    wave_lds_sync();
     // 1. counts per (row, destination)
     uint32_t jc = 0;  // the row continuing into the chunk (its start lies before it)
-    for (uint32_t t0 = 0; t0 < T; t0 += 64) {
-      uint64_t sm, rle, rlt;
-      uint32_t j, i, p0;
-      locate(t0, jc, sm, j, i, p0);
-      runs(p0, rle, rlt);
-      const uint32_t t = t0 + (uint32_t)lane;
-      const bool v = t < T;
-      const uint32_t im = v ? (uint32_t)rec[(size_t)(r0 + j) * L + i] & IM : 0u;
-      const uint32_t dm = v ? dests(im, sown[wv][j]) : 0u;
-      const bool last = v && (lane == 63 || ((sm >> (lane + 1)) & 1) || t + 1 == T);
-      for (uint32_t q = 0; q < P; q++) {
-        const uint64_t bq = __ballot((dm >> q) & 1u);
-        if (last) sco[wv][j][q] += (uint32_t)__popcll(bq & rle);
+    for (uint32_t t0 = 0; t0 < T; t0 += LP_RW * 64) {
+      Chunk ck[LP_RW];
+      window(t0, jc, ck);
+#pragma unroll
+      for (uint32_t w = 0; w < LP_RW; w++) {
+        if (t0 + 64 * w >= T) break;  // (wave-uniform)
+        uint4 m[PM / 4];
+#pragma unroll
+        for (uint32_t q4 = 0; q4 < PM / 4; q4++) m[q4] = smq[wv][ck[w].j][q4];
+        uint32_t pk[PM / 2];  // the run's counts so far, two destinations per word
+#pragma unroll
+        for (uint32_t q = 0; q < PM; q++) {
+          const uint64_t bq = __ballot((ck[w].im & word(m, q)) != 0u);
+          const uint32_t c = (uint32_t)__popcll(bq & ck[w].rle);
+          pk[q >> 1] = (q & 1) ? pk[q >> 1] | (c << 16) : c;
+        }
+        if (ck[w].last) {
+          uint32_t* row = reinterpret_cast<uint32_t*>(&sco[wv][ck[w].j][0]);
+#pragma unroll
+          for (uint32_t h = 0; h < PM / 2; h++) row[h] += pk[h];
+        }
       }
-      jc = (uint32_t)__builtin_amdgcn_readlane((int)j, 63);
-      wave_lds_sync();  // (srow is rewritten by the next chunk)
+      wave_lds_sync();  // (srow is rewritten by the next window)
     }
-    // 2. offsets: one claim per destination; sco becomes each (row, destination)'s write position
-    for (uint32_t q = 0; q < P; q++) {
-      const uint32_t c = sco[wv][lane][q];
+    // 2. offsets: one claim per destination, all in one instruction; sco
+    // becomes each (row, destination)'s write position
+    uint32_t pk[PM / 2];
+    {
+      const uint32_t* row = reinterpret_cast<const uint32_t*>(&sco[wv][lane][0]);
+#pragma unroll
+      for (uint32_t h = 0; h < PM / 2; h++) pk[h] = row[h];
+    }
+    uint32_t pos[PM], mytot = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < PM; q++) {
+      const uint32_t c = (pk[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
       uint32_t y = c;
       for (int off = 1; off < 64; off <<= 1) {
         const uint32_t z = __shfl_up(y, off);
         if (lane >= off) y += z;
       }
+      pos[q] = y - c;  // within the wave
+      if (q < P && rv) d.rcg[q][r] = c;
       const uint32_t tot = __shfl(y, 63);
-      unsigned long long b0 = 0;
-      if (lane == 0 && tot) b0 = atomicAdd(&cursor[q], (unsigned long long)tot);
-      const uint64_t off = (((uint64_t)__shfl((uint32_t)(b0 >> 32), 0) << 32) | __shfl((uint32_t)b0, 0)) + y - c;
-      sco[wv][lane][q] = (uint32_t)off;  // (< cap < 2^32)
-      if (rv) {
-        if (q == me) {
-          roff_own[r] = off;
-          rcg_own[r] = c;
-        } else {
-          roff[(size_t)q * un + r] = off;
-          rcg[(size_t)q * un + r] = c;
-        }
-      }
+      if ((uint32_t)lane == q) mytot = tot;
     }
+    const unsigned long long b0 = mytot ? atomicAdd(&cursor[lane], (unsigned long long)mytot) : 0ull;
+#pragma unroll
+    for (uint32_t q = 0; q < PM; q++) {
+      const uint64_t off = (((uint64_t)__shfl((uint32_t)(b0 >> 32), (int)q) << 32) | __shfl((uint32_t)b0, (int)q)) +
+                           pos[q];
+      pos[q] = (uint32_t)off;  // (< cap < 2^32)
+      if (q < P && rv) d.roff[q][r] = d.ob[q] + off;
+    }
+#pragma unroll
+    for (uint32_t q4 = 0; q4 < PM / 4; q4++)
+      sco[wv][lane][q4] = make_uint4(pos[4 * q4], pos[4 * q4 + 1], pos[4 * q4 + 2], pos[4 * q4 + 3]);
     wave_lds_sync();
     // 3. copy in emission order
     jc = 0;
-    for (uint32_t t0 = 0; t0 < T; t0 += 64) {
-      uint64_t sm, rle, rlt;
-      uint32_t j, i, p0;
-      locate(t0, jc, sm, j, i, p0);
-      runs(p0, rle, rlt);
-      const uint32_t t = t0 + (uint32_t)lane;
-      const bool v = t < T;
-      const uint64_t xr = v ? rec[(size_t)(r0 + j) * L + i] : 0ull;
-      const uint32_t dm = v ? dests((uint32_t)xr & IM, sown[wv][j]) : 0u;
-      const bool last = v && (lane == 63 || ((sm >> (lane + 1)) & 1) || t + 1 == T);
-      for (uint32_t q = 0; q < P; q++) {
-        const bool sel = (dm >> q) & 1u;
-        const uint64_t bq = __ballot(sel);
-        if (!bq) continue;  // wave-uniform
-        const uint32_t base = v ? sco[wv][j][q] : 0u;  // read by the run's lanes before its last lane moves it
-        if (sel) (q == me ? out_own : out + (size_t)q * cap)[(uint64_t)base + (uint32_t)__popcll(bq & rlt)] = xr;
-        if (last) sco[wv][j][q] = base + (uint32_t)__popcll(bq & rle);
+    for (uint32_t t0 = 0; t0 < T; t0 += LP_RW * 64) {
+      Chunk ck[LP_RW];
+      window(t0, jc, ck);
+#pragma unroll
+      for (uint32_t w = 0; w < LP_RW; w++) {
+        if (t0 + 64 * w >= T) break;  // (wave-uniform)
+        const uint32_t j = ck[w].j;
+        uint4 m[PM / 4], b[PM / 4];  // the row's masks and write positions (read before its last lane moves them)
+#pragma unroll
+        for (uint32_t q4 = 0; q4 < PM / 4; q4++) {
+          m[q4] = smq[wv][j][q4];
+          b[q4] = sco[wv][j][q4];
+        }
+        uint32_t nb[PM];
+#pragma unroll
+        for (uint32_t q = 0; q < PM; q++) {
+          const bool s = (ck[w].im & word(m, q)) != 0u;
+          const uint64_t bq = __ballot(s);
+          const uint32_t base = word(b, q);
+          if (s) d.out[q][(uint64_t)base + (uint32_t)__popcll(bq & ck[w].rlt)] = ck[w].xr;
+          nb[q] = base + (uint32_t)__popcll(bq & ck[w].rle);
+        }
+        if (ck[w].last) {
+#pragma unroll
+          for (uint32_t q4 = 0; q4 < PM / 4; q4++)
+            sco[wv][j][q4] = make_uint4(nb[4 * q4], nb[4 * q4 + 1], nb[4 * q4 + 2], nb[4 * q4 + 3]);
+        }
       }
-      jc = (uint32_t)__builtin_amdgcn_readlane((int)j, 63);
       wave_lds_sync();
     }
   }

@@ -562,19 +562,36 @@ void part_dev_relax_next(Ctx& c, const gs_part_record* in, uint64_t n) {
 // when a summary is wanted) and, with lazy gossip, this part's half of the
 // no-op proof (gossip_noop over its own peers; the batch stands iff every
 // part's holds). Returns true without lazy gossip.
-bool part_dev_complete(Ctx& c, bool hist, bool store) {
+// Completion in two steps, so that several contexts' completions overlap:
+// enqueue the reductions (and the message statistics' copy into pinned memory),
+// then wait and check the gossip proof.
+static void part_dev_complete_enqueue(Ctx& c, bool hist, bool store) {
   const Batch& b = c.part_b;
   run_complete(c, b, c.part_u0, c.part_un, true, hist, store);
+  if (!c.cfg.lazy_gossip) return;
+  const size_t msb = (size_t)b.B * MS_COLS * 8;
+  if (c.h_slms_bytes < msb) {
+    if (c.h_slms) GS_HIP(hipHostFree(c.h_slms));
+    c.h_slms = nullptr;
+    c.h_slms_bytes = 0;
+    GS_HIP(hipHostMalloc((void**)&c.h_slms, msb, hipHostMallocDefault));
+    c.h_slms_bytes = msb;
+  }
+  GS_HIP(hipMemcpyAsync(c.h_slms, c.d_mstat.p, msb, hipMemcpyDeviceToHost, c.stream));
+}
+
+static bool part_dev_complete_check(Ctx& c) {
   if (!c.cfg.lazy_gossip) return true;
-  std::vector<uint64_t> ms((size_t)b.B * MS_COLS), rel0(b.B);
-  GS_HIP(hipMemcpyAsync(ms.data(), c.d_mstat.p, ms.size() * 8, hipMemcpyDeviceToHost, c.stream));
+  const Batch& b = c.part_b;
   GS_HIP(hipStreamSynchronize(c.stream));
+  const uint64_t* ms = c.h_slms;
+  std::vector<uint64_t> rel0(b.B);
   const uint64_t hb = c.cfg.heartbeat_ns, ph = c.cfg.hb_phase_ns;
   for (uint32_t q = 0; q < b.B; q++) {
     const uint64_t tp = b.tpub[q], h0 = tp <= ph ? 0 : (tp - ph + hb - 1) / hb;
     rel0[q] = ph + h0 * hb - tp;
   }
-  const bool ok = gossip_noop(b, ms.data(), rel0);
+  const bool ok = gossip_noop(b, ms, rel0);
   if (!ok)
     for (uint32_t q = 0; q < b.B; q++) {
       const uint64_t und = ms[(size_t)q * MS_COLS + MS_UNDEL], tm = ms[(size_t)q * MS_COLS + MS_TMAX];
@@ -586,6 +603,11 @@ bool part_dev_complete(Ctx& c, bool hist, bool store) {
       }
     }
   return ok;
+}
+
+bool part_dev_complete(Ctx& c, bool hist, bool store) {
+  part_dev_complete_enqueue(c, hist, store);
+  return part_dev_complete_check(c);
 }
 
 // Finish a completed batch whose gossip proof holds everywhere: delivery into
@@ -659,7 +681,7 @@ static LPullArgs part_lp_args(Ctx& c) {
   return la;
 }
 
-bool part_lp_begin(Ctx& c, const gs_publish* sched, uint64_t n_msgs, uint64_t* seed_min) {
+bool part_lp_begin(Ctx& c, const gs_publish* sched, uint64_t n_msgs) {
   const uint32_t F = part_check(c, sched, n_msgs);
   (void)F;
   const char* ve = getenv("GS_RELAX_VARIANT");  // without bit 64 (or GS_PART_PUSH) the push protocol runs
@@ -725,12 +747,17 @@ bool part_lp_begin(Ctx& c, const gs_publish* sched, uint64_t n_msgs, uint64_t* s
   while (auto_bpc < 16 && (uint64_t)un >= (uint64_t)c.num_cus * PULL_WAVES * 32 * auto_bpc * 2) auto_bpc *= 2;
   c.part_lpgrid = (unsigned)std::max<uint64_t>(
       1, std::min<uint64_t>(((uint64_t)un + PULL_WAVES - 1) / PULL_WAVES, (uint64_t)c.num_cus * auto_bpc));
-  GS_HIP(hipMemcpyAsync(c.h_pinned, c.d_pctrl.p + 2 * 4 + 3, 8, hipMemcpyDeviceToHost, s));
-  GS_HIP(hipStreamSynchronize(s));
-  *seed_min = c.h_pinned[0];
+  // the seeds' min key lands in pinned word 28; part_lp_seed_min waits for it
+  // (the caller begins every part first, so that their setups overlap)
+  GS_HIP(hipMemcpyAsync(c.h_pinned + 28, c.d_pctrl.p + 2 * 4 + 3, 8, hipMemcpyDeviceToHost, s));
   c.part_lp = true;
   c.part_open = true;
   return true;
+}
+
+uint64_t part_lp_seed_min(Ctx& c) {
+  GS_HIP(hipStreamSynchronize(c.stream));
+  return c.h_pinned[28];
 }
 
 // The combined pass control into the slot the next pass decides from (slot of the last pass).
@@ -738,8 +765,9 @@ void part_lp_set(Ctx& c, uint64_t records, uint64_t minp) {
   const uint32_t slot = (c.part_lppass + 2) % 3;  // the last pass's slot (seeds: slot 2 before pass 0)
   c.h_pinned[24] = records;
   c.h_pinned[25] = minp;
+  // (no wait: the staging words are next written by the next part_lp_set,
+  // after part_lp_read has drained this stream)
   GS_HIP(hipMemcpyAsync(c.d_pctrl.p + slot * 4 + 2, c.h_pinned + 24, 16, hipMemcpyHostToDevice, c.stream));
-  GS_HIP(hipStreamSynchronize(c.stream));  // the staging words are reused by the next pass
 }
 
 void part_lp_pass(Ctx& c) {
@@ -750,15 +778,25 @@ void part_lp_pass(Ctx& c) {
   c.stats.relax_launches++;
 }
 
-void part_lp_read(Ctx& c, uint64_t out[4]) {
+// The last pass's control words into pinned memory (enqueued), then waited
+// for: several parts' reads in flight together.
+void part_lp_read_enqueue(Ctx& c) {
   const uint32_t slot = (c.part_lppass + 2) % 3;
   GS_HIP(hipMemcpyAsync(c.h_pinned, c.d_pctrl.p + slot * 4, 32, hipMemcpyDeviceToHost, c.stream));
   GS_HIP(hipMemcpyAsync(c.h_pinned + 4, c.d_counters.p + C_ERR, 8, hipMemcpyDeviceToHost, c.stream));
+}
+
+void part_lp_read_wait(Ctx& c, uint64_t out[4]) {
   GS_HIP(hipStreamSynchronize(c.stream));
   out[0] = c.h_pinned[1];
   out[1] = c.h_pinned[2];
   out[2] = c.h_pinned[3];
   out[3] = c.h_pinned[4];
+}
+
+void part_lp_read(Ctx& c, uint64_t out[4]) {
+  part_lp_read_enqueue(c);
+  part_lp_read_wait(c, out);
 }
 
 void part_lp_pack(Ctx& c, uint64_t base, uint64_t mine) {
@@ -776,16 +814,12 @@ void part_lp_pack(Ctx& c, uint64_t base, uint64_t mine) {
 }
 
 // Routed pack (k_lpack_route): this part's records of the last pass for each
-// destination part (own: into d_rpk at base 0, with the global offset tables
-// at its peers; others: d_rsend[q * mine] with the tables d_rroff / d_rrcg[q * un]).
-void part_lp_pack_route(Ctx& c, uint32_t P, uint32_t me, uint64_t mine) {
+// destination part, to the places `dst` names (part_lp_pack_route: send
+// segments; the local exchange: the destination contexts' own buffers).
+void part_lp_route_launch(Ctx& c, uint32_t P, uint32_t me, const RouteDst& dst) {
   const uint32_t un = c.part_un, L = c.part_b.L;
   hipStream_t s = c.stream;
-  const uint64_t cap = std::max<uint64_t>(mine, 1);
   c.d_pkcur.alloc(P);
-  c.d_rsend.alloc((size_t)P * cap);
-  c.d_rroff.alloc((size_t)P * un);
-  c.d_rrcg.alloc((size_t)P * un);
   GS_HIP(hipMemsetAsync(c.d_pkcur.p, 0, (size_t)P * 8, s));
   const uint32_t nb = (c.part_lppass + 1) & 1;  // the last pass wrote lrec / lcnt [pass & 1]
   const unsigned grid = (unsigned)std::max<uint64_t>(
@@ -793,11 +827,51 @@ void part_lp_pack_route(Ctx& c, uint32_t P, uint32_t me, uint64_t mine) {
   RouteLo rl{};
   const PartLayout lay{P, c.cfg.peers, 0};
   for (uint32_t q = 0; q < P && q < LP_PMAX; q++) rl.lo[q] = lay.u0(q);
-  k_lpack_route<<<grid, TB, 0, s>>>(c.d_lrec.p + (size_t)nb * un * L, c.d_lcnt.p + (size_t)nb * un, c.d_mesh.p,
-                                    c.part_u0, un, L, P, me, cap, c.d_rsend.p, c.d_rpk.p, c.d_rroff.p,
-                                    c.d_rrcg.p, c.d_roffg.p + c.part_u0, c.d_rcg.p + c.part_u0,
-                                    (unsigned long long*)c.d_pkcur.p, rl);
+#define GS_LPR(PM)                                                                                             \
+  k_lpack_route<PM><<<grid, TB, 0, s>>>(c.d_lrec.p + (size_t)nb * un * L, c.d_lcnt.p + (size_t)nb * un, c.d_mesh.p, \
+                                        c.part_u0, un, L, P, me, (unsigned long long*)c.d_pkcur.p, rl, dst)
+  if (P <= 4) GS_LPR(4);
+  else if (P <= 8) GS_LPR(8);
+  else GS_LPR(16);
+#undef GS_LPR
   GS_HIP(hipGetLastError());
+}
+
+// Ranks: own records into d_rpk at base 0 with the global offset tables at its
+// peers; other destinations into d_rsend[q * mine] with the tables
+// d_rroff / d_rrcg[q * un] (offsets relative to the segment, k_roff_fix
+// rebases them after the exchange).
+void part_lp_pack_route(Ctx& c, uint32_t P, uint32_t me, uint64_t mine) {
+  const uint32_t un = c.part_un;
+  const uint64_t cap = std::max<uint64_t>(mine, 1);
+  c.d_rsend.alloc((size_t)P * cap);
+  c.d_rroff.alloc((size_t)P * un);
+  c.d_rrcg.alloc((size_t)P * un);
+  RouteDst d{};
+  for (uint32_t q = 0; q < P; q++) {
+    const bool own = q == me;
+    d.out[q] = own ? c.d_rpk.p : c.d_rsend.p + (size_t)q * cap;
+    d.roff[q] = own ? c.d_roffg.p + c.part_u0 : c.d_rroff.p + (size_t)q * un;
+    d.rcg[q] = own ? c.d_rcg.p + c.part_u0 : c.d_rrcg.p + (size_t)q * un;
+  }
+  part_lp_route_launch(c, P, me, d);
+}
+
+// Loop-back parts on one device: part `me`'s records straight into every
+// destination context's gathered buffer at this part's gathered base (its
+// capacity there is all its records), its tables at this part's peers; no copy,
+// no rebasing. The destinations' buffers are sized before any part launches.
+void part_lp_pack_route_direct(Ctx** cx, uint32_t P, uint32_t me, uint64_t base) {
+  Ctx& c = *cx[me];
+  const PartLayout lay{P, c.cfg.peers, 0};
+  RouteDst d{};
+  for (uint32_t q = 0; q < P; q++) {
+    d.out[q] = cx[q]->d_rpk.p + base;
+    d.roff[q] = cx[q]->d_roffg.p + lay.u0(me);
+    d.rcg[q] = cx[q]->d_rcg.p + lay.u0(me);
+    d.ob[q] = base;
+  }
+  part_lp_route_launch(c, P, me, d);
 }
 
 // The routed records per destination (counts[q]) of the last pack.
@@ -819,7 +893,7 @@ void part_lp_route_fix(Ctx& c, uint32_t P, uint32_t me, const uint64_t* base) {
 // As gs_run's list pass: completion reads the final logs (k_lcomplete) unless
 // the sink takes rows or a summary, or the rows hold fragment groups (k_lfinal
 // -> dense rows -> k_complete).
-bool part_lp_end(Ctx& c, const gs_result_sink* sink) {
+void part_lp_end_enqueue(Ctx& c, const gs_result_sink* sink) {
   const SinkWants w = sink_wants(sink);
   const bool dense = w.rows() || w.summary || c.part_b.FP > 1 || getenv("GS_LPULL_DENSE");
   if (dense) {
@@ -831,8 +905,10 @@ bool part_lp_end(Ctx& c, const gs_result_sink* sink) {
   }
   c.stats.list_pull_batches++;
   c.part_lp = false;
-  return part_dev_complete(c, w.summary, dense);
+  part_dev_complete_enqueue(c, w.summary, dense);
 }
+
+bool part_lp_end_check(Ctx& c) { return part_dev_complete_check(c); }
 
 void part_lp_abort(Ctx& c) {  // the batch re-runs on the push protocol: counters as before the batch
   if (c.part_lp) {

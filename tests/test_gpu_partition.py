@@ -131,19 +131,24 @@ def test_run_partitioned_local_comm_equals_gs_run(parts, frags, batch):
     comm.close()
 
 
-@pytest.mark.parametrize("mode", ["gather", "route", "push"])
+@pytest.mark.parametrize("mode", ["gather", "route", "route_copy", "push"])
 @pytest.mark.parametrize("parts,frags,batch", [(2, 1, 64), (5, 2, 32), (8, 1, 1024)])
 def test_run_partitioned_list_pass_and_push_protocol(monkeypatch, mode, parts, frags, batch):
     """gs_run_partitioned runs each part's rows on the list pass (records
-    exchanged between passes: every part's to every part, or with
-    GS_PART_ROUTE routed to the parts owning a receiver) — or, with
-    GS_PART_PUSH, on the push protocol — bit-identical to gs_run and the
-    oracle; uneven part sizes, fragments, rows of 1024 lanes."""
+    exchanged between passes: routed to the parts owning a receiver, stored
+    straight into the destination contexts — the loop-back default — or
+    through send segments and copies as ranks do (GS_PART_DIRECT=0), or with
+    GS_PART_ROUTE=0 every part's to every part) — or, with GS_PART_PUSH, on
+    the push protocol — bit-identical to gs_run and the oracle; uneven part
+    sizes, fragments, rows of 1024 lanes."""
     push = mode == "push"
     if push:
         monkeypatch.setenv("GS_PART_PUSH", "1")
-    if mode == "route":
+    if mode == "gather":
+        monkeypatch.setenv("GS_PART_ROUTE", "0")
+    if mode == "route_copy":
         monkeypatch.setenv("GS_PART_ROUTE", "1")
+        monkeypatch.setenv("GS_PART_DIRECT", "0")
     N = 3001
     p = oracle.params(peers=N, seed=65, fragments=frags)
     sched = _sched(batch, N)
