@@ -656,7 +656,10 @@ bool run_batch_lp(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched,
       part_lp_pass(*cx[i]);
       if (cx[i]->timing) ev(i);
     }
-    if (cm->local) {
+    const bool dev_ctl = one_dev && P <= PART_ROUTE_PMAX;  // the parts' control combined on the device
+    if (dev_ctl) {
+      part_lp_combine(cx, P, st.data());
+    } else if (cm->local) {
       for (uint32_t i = 0; i < nctx; i++) {  // every part's control read in flight, then each one waited for
         GS_HIP(hipSetDevice(cx[i]->cfg.device));
         part_lp_read_enqueue(*cx[i]);
@@ -684,10 +687,11 @@ bool run_batch_lp(gs_comm* cm, Ctx** cx, uint32_t nctx, const gs_publish* sched,
       return false;
     }
     if (st[0] == 0) break;  // pass mode DONE (PM_DONE, gs_pull_kernel.h): grid- and part-uniform
-    for (uint32_t i = 0; i < nctx; i++) {
-      GS_HIP(hipSetDevice(cx[i]->cfg.device));
-      part_lp_set(*cx[i], recs, minp);
-    }
+    if (!dev_ctl)
+      for (uint32_t i = 0; i < nctx; i++) {
+        GS_HIP(hipSetDevice(cx[i]->cfg.device));
+        part_lp_set(*cx[i], recs, minp);
+      }
     if (!recs) continue;  // the next pass emits a window: it reads no records
     std::vector<uint64_t> base(P + 1, 0), cnt(P);
     for (uint32_t p = 0; p < P; p++) cnt[p] = st[(size_t)p * 4 + 1];

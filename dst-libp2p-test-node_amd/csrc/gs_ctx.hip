@@ -47,6 +47,8 @@ Ctx::~Ctx() {
   if (h_laterr) (void)hipHostFree(h_laterr);
   if (copy) (void)hipStreamDestroy(copy);
   if (part_xev) (void)hipEventDestroy(part_xev);
+  if (part_pev) (void)hipEventDestroy(part_pev);
+  if (h_pstat) (void)hipHostFree(h_pstat);
   if (h_pinned) (void)hipHostFree(h_pinned);
   if (h_block) (void)hipHostFree(h_block);
   if (h_slms) (void)hipHostFree(h_slms);

@@ -263,6 +263,9 @@ struct Ctx {
   DevBuf<uint64_t> d_roffg;  // [N] their offsets in d_rpk
   DevBuf<uint64_t> d_rpk;    // every part's records of the last pass
   hipEvent_t part_xev = nullptr;  // loop-back routed stores of the last pass done (other parts wait on it)
+  hipEvent_t part_pev = nullptr;  // loop-back: this part's pass done (part 0's combine waits on it)
+  DevBuf<uint64_t> d_pstat;       // loop-back, part 0: every part's pass control (k_part_combine)
+  uint64_t* h_pstat = nullptr;    // its pinned read-back (LP_PMAX x 4 words)
   DevBuf<uint64_t> d_pkcur;  // pack cursor (routed: one per destination part)
   // routed exchange (k_lpack_route): the records for each other part [P][cap] and
   // this part's per-peer offsets / counts for each destination [P][un]
@@ -359,6 +362,7 @@ void part_lp_pass(Ctx& c);
 void part_lp_read(Ctx& c, uint64_t out[4]);  // last pass: mode, records, min pending, error word
 void part_lp_read_enqueue(Ctx& c);                   // part_lp_read in two steps
 void part_lp_read_wait(Ctx& c, uint64_t out[4]);
+void part_lp_combine(Ctx** cx, uint32_t P, uint64_t* st);  // loop-back on one device: read + set of all parts
 void part_lp_set(Ctx& c, uint64_t records, uint64_t minp);  // the combined values into the last pass's slot
 void part_lp_pack(Ctx& c, uint64_t base, uint64_t mine);
 void part_lp_pack_route(Ctx& c, uint32_t P, uint32_t me, uint64_t mine);

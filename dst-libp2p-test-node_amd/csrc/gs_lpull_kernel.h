@@ -2056,6 +2056,40 @@ __global__ __launch_bounds__(TB) void k_roff_fix(uint64_t* __restrict__ roff, ui
   if (p != me) roff[x] += rb.b[p];
 }
 
+// Loop-back parts on one device: after every part's pass, one wave combines
+// the parts' pass control as the host would (gs_comm.hip run_batch_lp): lane
+// p reads part p's slot {mode, records, min pending} and error word into
+// st[p * 4 ..], and every part's slot gets the sum of the records and the min
+// of the pending keys (part_lp_set's values) — one launch and one read-back
+// instead of a read and a write per part.
+struct PartCtl {
+  uint64_t* ctrl[LP_PMAX];       // part p's pass control slots [3][4]
+  const uint64_t* err[LP_PMAX];  // part p's error word (counters + C_ERR)
+};
+__global__ __launch_bounds__(64) void k_part_combine(PartCtl pc, uint32_t P, uint32_t slot, uint64_t* __restrict__ st) {
+  const uint32_t p = threadIdx.x;
+  const bool v = p < P;
+  uint64_t* s = v ? pc.ctrl[p] + slot * 4 : nullptr;
+  const uint64_t mode = v ? s[1] : 0, rec = v ? s[2] : 0, mn = v ? s[3] : INF64, er = v ? *pc.err[p] : 0;
+  uint64_t sum = rec, lo = mn;
+  for (int off = 32; off >= 1; off >>= 1) {
+    const uint64_t y = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(sum >> 32), off) << 32) |
+                       (uint32_t)__shfl_xor((int)(uint32_t)sum, off);
+    const uint64_t z = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(lo >> 32), off) << 32) |
+                       (uint32_t)__shfl_xor((int)(uint32_t)lo, off);
+    sum += y;
+    lo = z < lo ? z : lo;
+  }
+  if (v) {
+    st[p * 4 + 0] = mode;
+    st[p * 4 + 1] = rec;
+    st[p * 4 + 2] = mn;
+    st[p * 4 + 3] = er;
+    s[2] = sum;
+    s[3] = lo;
+  }
+}
+
 void lpull_dispatch_part(uint32_t FP, const LPullArgs& a, unsigned grid, hipStream_t s) {
   const bool ch8 = lpull_chunks(a.L) == 8;
 #define GS_LPP(F)                                                      \

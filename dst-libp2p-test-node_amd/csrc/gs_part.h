@@ -874,6 +874,34 @@ void part_lp_pack_route_direct(Ctx** cx, uint32_t P, uint32_t me, uint64_t base)
   part_lp_route_launch(c, P, me, d);
 }
 
+// Loop-back parts on one device: every part's pass control combined on the
+// device (k_part_combine on part 0's stream after every part's pass), read
+// back once: st[p * 4 ..] = part p's {mode, records, min pending, error word},
+// and every part's slot already holds the combined records and min pending
+// key (no part_lp_set).
+void part_lp_combine(Ctx** cx, uint32_t P, uint64_t* st) {
+  Ctx& c0 = *cx[0];
+  PartCtl pc{};
+  for (uint32_t p = 0; p < P; p++) {
+    Ctx& c = *cx[p];
+    pc.ctrl[p] = c.d_pctrl.p;
+    pc.err[p] = c.d_counters.p + C_ERR;
+    if (p) {
+      if (!c.part_pev) GS_HIP(hipEventCreateWithFlags(&c.part_pev, hipEventDisableTiming));
+      GS_HIP(hipEventRecord(c.part_pev, c.stream));
+      GS_HIP(hipStreamWaitEvent(c0.stream, c.part_pev, 0));
+    }
+  }
+  c0.d_pstat.alloc((size_t)P * 4);
+  if (!c0.h_pstat) GS_HIP(hipHostMalloc((void**)&c0.h_pstat, LP_PMAX * 4 * 8, hipHostMallocDefault));
+  const uint32_t slot = (c0.part_lppass + 2) % 3;  // the last pass's slot (lockstep parts: the same in each)
+  k_part_combine<<<1, 64, 0, c0.stream>>>(pc, P, slot, c0.d_pstat.p);
+  GS_HIP(hipGetLastError());
+  GS_HIP(hipMemcpyAsync(c0.h_pstat, c0.d_pstat.p, (size_t)P * 4 * 8, hipMemcpyDeviceToHost, c0.stream));
+  GS_HIP(hipStreamSynchronize(c0.stream));
+  memcpy(st, c0.h_pstat, (size_t)P * 4 * 8);
+}
+
 // The routed records per destination (counts[q]) of the last pack.
 void part_lp_route_read(Ctx& c, uint32_t P, uint64_t* counts) {
   GS_HIP(hipMemcpyAsync(c.h_pinned, c.d_pkcur.p, (size_t)P * 8, hipMemcpyDeviceToHost, c.stream));

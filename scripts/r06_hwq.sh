@@ -10,6 +10,3 @@ for q in 8 16 4; do
   rc=$?; echo "peer8 hwq=$q rc=$rc $(grep -o '"ms_per_step": [0-9.]*' $OUT/peer8_q$q.log)"
   case $rc in 0) ;; *) exit $rc;; esac
 done
-GS_PART_ROUTE=1 GS_PART_DIRECT=0 timeout -k 10 300 python -u bench.py --mode peer --parts 8 --steps 6 --warmup 2 --configs 0 \
-    --cpu-seconds 0 --also-peers 0 --gossip-check 0 --output-steps 0 > $OUT/peer8_copy.log 2>&1
-echo "peer8 copy rc=$? $(grep -o '"ms_per_step": [0-9.]*' $OUT/peer8_copy.log)"
