@@ -527,7 +527,10 @@ gs_status gs_comm_destroy(gs_comm* comm);
  * this process's contexts (RCCL: nctx = 1, the rank's; local: nctx = nparts,
  * part i = ctxs[i]), all built with the same config, topology and mesh. The
  * library sets each context's partition, runs every batch on the list pass
- * over own rows (records exchanged between window passes) or the bucket
+ * over own rows (records exchanged between window passes: loop-back parts on
+ * one device store each record straight into the parts owning a receiver and
+ * combine the pass control on the device; ranks exchange every part's records,
+ * or with GS_PART_ROUTE=1 only the routed ones) or the bucket
  * protocol (per bucket: own scan, records routed only to the parts owning a
  * target with grouped send/recv, relax into own peers, MIN all-reduce of the
  * next bucket key) and writes part i's peers to sinks[i] ([n_msgs][own peers];
