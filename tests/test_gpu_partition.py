@@ -132,7 +132,7 @@ def test_run_partitioned_local_comm_equals_gs_run(parts, frags, batch):
 
 
 @pytest.mark.parametrize("mode", ["gather", "route", "route_copy", "push"])
-@pytest.mark.parametrize("parts,frags,batch", [(2, 1, 64), (5, 2, 32), (8, 1, 1024)])
+@pytest.mark.parametrize("parts,frags,batch", [(2, 1, 64), (5, 2, 32), (8, 1, 1024), (12, 2, 32), (16, 1, 64)])
 def test_run_partitioned_list_pass_and_push_protocol(monkeypatch, mode, parts, frags, batch):
     """gs_run_partitioned runs each part's rows on the list pass (records
     exchanged between passes: routed to the parts owning a receiver, stored
@@ -140,7 +140,8 @@ def test_run_partitioned_list_pass_and_push_protocol(monkeypatch, mode, parts, f
     through send segments and copies as ranks do (GS_PART_DIRECT=0), or with
     GS_PART_ROUTE=0 every part's to every part) — or, with GS_PART_PUSH, on
     the push protocol — bit-identical to gs_run and the oracle; uneven part
-    sizes, fragments, rows of 1024 lanes."""
+    sizes, fragments, rows of 1024 lanes; 2-4, 5-8 and 9-16 parts take the
+    routed pack's three destination widths (k_lpack_route<4 / 8 / 16>)."""
     push = mode == "push"
     if push:
         monkeypatch.setenv("GS_PART_PUSH", "1")
@@ -165,6 +166,26 @@ def test_run_partitioned_list_pass_and_push_protocol(monkeypatch, mode, parts, f
     if not push and batch <= 64:
         ora = oracle.simulate(p, 5, (50, 150, 40, 130), sched=sched)
         np.testing.assert_array_equal(ref["t_complete"], ora["t_complete"])
+    comm.close()
+
+
+def test_run_partitioned_more_parts_than_routes(monkeypatch):
+    """17 loop-back parts: more than the routed pack's 16 destinations, so the
+    list pass gathers every part's records (GS_PART_ROUTE=1 cannot force
+    routing past PART_ROUTE_PMAX); bit-identical to gs_run."""
+    monkeypatch.setenv("GS_PART_ROUTE", "1")
+    N, parts, batch = 3001, 17, 32
+    p = oracle.params(peers=N, seed=66)
+    sched = _sched(batch, N)
+    ref, rst = _whole(p, 5, (50, 150, 40, 130), sched, batch)
+    sims = _parts(p, 5, (50, 150, 40, 130), parts, batch)
+    comm = gossipsim.Comm(local_parts=parts)
+    res = comm.run_partitioned(sims, sched)
+    np.testing.assert_array_equal(np.concatenate([r["t_complete"] for r in res], axis=1), ref["t_complete"])
+    np.testing.assert_array_equal(np.concatenate([r["hops"] for r in res], axis=1), ref["hops"])
+    st = [s.stats() for s in sims]
+    assert sum(x["deliveries"] for x in st) == rst["deliveries"]
+    assert all(x["list_pull_batches"] > 0 for x in st)
     comm.close()
 
 
