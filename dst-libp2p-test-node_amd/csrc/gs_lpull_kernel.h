@@ -1854,6 +1854,11 @@ struct RouteDst {
   uint64_t* roff[LP_PMAX];  // their offsets, by local row
   uint32_t* rcg[LP_PMAX];   // their counts, by local row
   uint64_t ob[LP_PMAX];     // added to the offsets (the segment's base in q's buffer)
+  // own_inplace: the own part's records stay where the pass wrote them (row r
+  // at element own_off + r * L from the own gathered buffer, modulo 2^64: the
+  // pass reads them through the same base + offset); only its tables are written
+  uint64_t own_off;
+  uint32_t own_inplace;
 };
 template <uint32_t PM>
 __global__ __launch_bounds__(TB) void k_lpack_route(const uint64_t* __restrict__ rec, const uint32_t* __restrict__ cnt,
@@ -1882,7 +1887,11 @@ __global__ __launch_bounds__(TB) void k_lpack_route(const uint64_t* __restrict__
     const uint32_t n = rv ? cnt[r] : 0u;
     uint32_t mq[PM];
 #pragma unroll
-    for (uint32_t q = 0; q < PM; q++) mq[q] = q == me ? VB : 0u;
+    for (uint32_t q = 0; q < PM; q++) mq[q] = q == me && !d.own_inplace ? VB : 0u;
+    if (rv && d.own_inplace) {  // the own records in place: their row's offset and count
+      d.roff[me][r] = d.own_off + (uint64_t)r * L;
+      d.rcg[me][r] = n;
+    }
     if (rv) {
       const uint4* mp = reinterpret_cast<const uint4*>(mesh + (size_t)(u0 + r) * MESH_W);
 #pragma unroll
@@ -1894,7 +1903,8 @@ __global__ __launch_bounds__(TB) void k_lpack_route(const uint64_t* __restrict__
           const uint32_t x = e4[u] & 0xFFFFFFu;  // (EMPTY entries: never a receiver bit)
 #pragma unroll
           for (uint32_t q = 0; q < PM; q++) {
-            const bool in = q < P && (q == 0 || x >= rl.lo[q]) && (q + 1 >= P || x < rl.lo[q + 1]);
+            const bool in = q < P && !(q == me && d.own_inplace) && (q == 0 || x >= rl.lo[q]) &&
+                            (q + 1 >= P || x < rl.lo[q + 1]);
             mq[q] |= in ? 1u << (4 * k4 + u) : 0u;
           }
         }
@@ -1992,7 +2002,7 @@ __global__ __launch_bounds__(TB) void k_lpack_route(const uint64_t* __restrict__
         if (lane >= off) y += z;
       }
       pos[q] = y - c;  // within the wave
-      if (q < P && rv) d.rcg[q][r] = c;
+      if (q < P && rv && !(q == me && d.own_inplace)) d.rcg[q][r] = c;
       const uint32_t tot = __shfl(y, 63);
       if ((uint32_t)lane == q) mytot = tot;
     }
@@ -2002,7 +2012,7 @@ __global__ __launch_bounds__(TB) void k_lpack_route(const uint64_t* __restrict__
       const uint64_t off = (((uint64_t)__shfl((uint32_t)(b0 >> 32), (int)q) << 32) | __shfl((uint32_t)b0, (int)q)) +
                            pos[q];
       pos[q] = (uint32_t)off;  // (< cap < 2^32)
-      if (q < P && rv) d.roff[q][r] = d.ob[q] + off;
+      if (q < P && rv && !(q == me && d.own_inplace)) d.roff[q][r] = d.ob[q] + off;
     }
 #pragma unroll
     for (uint32_t q4 = 0; q4 < PM / 4; q4++)

@@ -837,6 +837,17 @@ void part_lp_route_launch(Ctx& c, uint32_t P, uint32_t me, const RouteDst& dst) 
   GS_HIP(hipGetLastError());
 }
 
+// The own part's records are read where the last pass wrote them (lrec half
+// nb, rows of L): their offsets from d_rpk's base, as 64-bit element offsets
+// modulo 2^64 (the pass adds them to the same base). d_rpk is sized before.
+static void part_lp_own_inplace(Ctx& c, RouteDst& d) {
+  const uint32_t un = c.part_un, L = c.part_b.L;
+  const uint32_t nb = (c.part_lppass + 1) & 1;
+  const uint64_t* rows = c.d_lrec.p + (size_t)nb * un * L;
+  d.own_off = (uint64_t)(((intptr_t)rows - (intptr_t)c.d_rpk.p) / 8);  // (both 8-B aligned; may be negative)
+  d.own_inplace = 1;
+}
+
 // Ranks: own records into d_rpk at base 0 with the global offset tables at its
 // peers; other destinations into d_rsend[q * mine] with the tables
 // d_rroff / d_rrcg[q * un] (offsets relative to the segment, k_roff_fix
@@ -854,6 +865,7 @@ void part_lp_pack_route(Ctx& c, uint32_t P, uint32_t me, uint64_t mine) {
     d.roff[q] = own ? c.d_roffg.p + c.part_u0 : c.d_rroff.p + (size_t)q * un;
     d.rcg[q] = own ? c.d_rcg.p + c.part_u0 : c.d_rrcg.p + (size_t)q * un;
   }
+  part_lp_own_inplace(c, d);
   part_lp_route_launch(c, P, me, d);
 }
 
@@ -871,6 +883,7 @@ void part_lp_pack_route_direct(Ctx** cx, uint32_t P, uint32_t me, uint64_t base)
     d.rcg[q] = cx[q]->d_rcg.p + lay.u0(me);
     d.ob[q] = base;
   }
+  part_lp_own_inplace(c, d);
   part_lp_route_launch(c, P, me, d);
 }
 
