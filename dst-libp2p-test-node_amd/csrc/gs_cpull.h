@@ -73,6 +73,7 @@ struct CPrepArgs {
   uint32_t* coff;           // [H + 2][N][LP_FW]
   uint64_t E0, seed;
   uint32_t N, R, cE, cW, B, H, d_lazy, gf_milli;
+  uint32_t FP;      // fragment lanes per message: lane l is message l / FP's
   uint32_t c0, c1;  // k_cprep: the chunks of 64 epochs [c0, c1) (their epochs are in the ring)
 };
 
@@ -121,9 +122,10 @@ __global__ __launch_bounds__(TB) void k_cprep(CPrepArgs a) {
   }
 }
 
-// The offline lanes per relative epoch k (lane m: epoch E0 + cq[m] + k), one
-// wave per row: lane j builds its u16 (bit q = lane q*64 + j); the row's own
-// bits are fetched from lane (index >> 6), which holds word index >> 6.
+// The offline lanes per relative epoch k (lane l of message m = l / FP:
+// epoch E0 + cq[m] + k), one wave per row: lane j builds its u16 (bit q = lane
+// q*64 + j); the row's own bits are fetched from lane (index >> 6), which
+// holds word index >> 6.
 __global__ __launch_bounds__(TB) void k_coff(CPrepArgs a) {
   const int lane = threadIdx.x & 63;
   const uint32_t wv = blockIdx.x * (TB / 64) + (threadIdx.x >> 6), nw = gridDim.x * (TB / 64);
@@ -133,7 +135,7 @@ __global__ __launch_bounds__(TB) void k_coff(CPrepArgs a) {
     uint32_t cql[PULL_CH];
 #pragma unroll
     for (int q = 0; q < (int)PULL_CH; q++) {
-      const uint32_t m = (uint32_t)q * 64 + (uint32_t)lane;
+      const uint32_t m = ((uint32_t)q * 64 + (uint32_t)lane) / a.FP;
       cql[q] = m < a.B ? a.cq[m] : 0xFFFFFFFFu;
     }
     for (uint32_t k = 0; k <= a.H + 1; k++) {

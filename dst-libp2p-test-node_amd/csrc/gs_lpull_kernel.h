@@ -91,8 +91,9 @@ struct LPullArgs {
   uint32_t ls, lcap;  // list stride (max(L, 256) entries) and capacity (ls; GS_LPULL_CAP lowers it)
   uint32_t idw;       // IDONTWANT batch (k_lpull<.., true>): finals go to dense keys[N][L], no log
   uint32_t self_log;  // k_lcomplete's latency stream: the publisher logs its own message
-  uint64_t rmax;      // largest arrival offset of a forward after its uplink start (lat + dn + MESH_W ser):
-                      // the emit step checks start + rmax <= tmax, so receivers need no time check
+  uint64_t rmax;      // largest arrival offset of a forward after the lane's final time (the fragment
+                      // FIFO + lat + dn + MESH_W ser): the emit step checks start + rmax <= tmax, so
+                      // receivers need no time check
   // peer-partitioned pass (k_lpull<.., .., .., true>, gs_run_partitioned): this context's rows are
   // global peers [u0, u0 + N); every per-row array above is indexed by the local row, lrec / lcnt
   // receive only this part's records, and the previous pass's records of EVERY peer arrive packed
@@ -486,7 +487,7 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
   constexpr uint32_t NG = GS_LP_NG, RCH = GS_LP_RCH;
   static_assert(!IDW || FP == 1, "IDONTWANT on the list pass: rows of single-fragment lanes");
   static_assert(!GOS || !PART, "gossip on the list pass: gs_run's rows");
-  static_assert(!CHN || (FP == 1 && !IDW && !PART), "churn on the list pass: gs_run's single-fragment rows");
+  static_assert(!CHN || (!IDW && !PART), "churn on the list pass: gs_run's rows (fragment groups included)");
   // row header: the mesh row (frozen mesh) or, under churn, the CSR row (the
   // mesh of a lane's epoch is a mask over it)
   constexpr uint32_t HW = CHN ? CELL_W : MESH_W;
@@ -547,14 +548,16 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     gbk = (uint16_t)a.gctl[GC_BK];
   }
   uint64_t niw = 0;  // IWANTs sent
-  // churn (CHN): the epoch boundaries the pass can meet. A record whose sender
-  // started before xBs (time) arrives in the sender's epoch ks unless it lands
-  // at or after xBs: then it is lost where the receiver is offline in ks + 1
-  // (offn; the sender's mesh of ks held only peers online in ks). Window c
+  // churn (CHN): the epoch boundaries the pass can meet. A record landing at
+  // or after xBs (time) is lost where the receiver is offline in ks + 1 (offn):
+  // a sender that received in ks used ks's mesh (peers online in ks), one that
+  // received in ks + 1 only reaches peers online then, so the test needs no
+  // sender epoch (with fragments the uplink FIFO can start a send of a lane
+  // received in ks after xBs; rmax covers that FIFO). Window c
   // starts in relative epoch kc and, when it straddles a boundary, its lanes
   // final at or after eBc forward with the mesh of kc + 1.
   uint64_t xBs = INF64, eBc = INF64;
-  uint32_t xBoff = 0, kc = 0;
+  uint32_t kc = 0;
   const uint32_t* offn = nullptr;
   uint32_t gkh = 0;     // GOS + CHN: relative epoch of the built heartbeat
   uint32_t calT = 0;    // GOS + CHN: the published lanes (lane j: bit q = lane q*64 + j)
@@ -563,7 +566,6 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
     const uint64_t ks = udiv53(a.cr0 + lo, a.chb), Bs = (ks + 1) * a.chb - a.cr0;
     if (pull && Bs < lo + a.delta + a.rmax) {
       xBs = Bs << a.tshift;
-      xBoff = (uint32_t)(Bs - lo);
       offn = a.coff + (size_t)(ks + 1 <= a.chz + 1 ? ks + 1 : a.chz + 1) * a.N * LP_FW;
     }
     kc = (uint32_t)udiv53(a.cr0 + wlo, a.chb);
@@ -827,7 +829,7 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
               const uint64_t nk = BASE[k] + (((off << HOP_BITS) | (lo32 >> LP_HOP_SHIFT)) << a.sb);
               if (offn) {  // wave-uniform: a record may cross into epoch ks + 1
                 const uint32_t ob = (uint32_t)__shfl((int)onl, (int)(slot & 63u));
-                if (so < xBoff && nk >= xBs && ((ob >> (slot >> 6)) & 1u)) ok = false;
+                if (nk >= xBs && ((ob >> (slot >> 6)) & 1u)) ok = false;
               }
               if (ok) {
                 atomicMin((unsigned long long*)&CW[slot], (unsigned long long)nk);
@@ -1501,7 +1503,7 @@ __global__ __launch_bounds__(TB) void k_gsend(LPullArgs a) {
       uint64_t mask;
       if constexpr (CHN) {  // the targets k_cprep selected for (v, the lane's epoch)
         const uint32_t kh = a.ghoff + (uint32_t)k;
-        mask = jv && kh <= a.chz ? a.cgt[(size_t)v * a.cE + a.cq[m] + kh] : 0ull;
+        mask = jv && kh <= a.chz ? a.cgt[(size_t)v * a.cE + a.cq[m / (a.L / a.B)] + kh] : 0ull;
       } else {
         mask = glp_targets(rpre, h, x, nmm, deg, r);
       }
@@ -2117,19 +2119,31 @@ void lpull_dispatch_part(uint32_t FP, const LPullArgs& a, unsigned grid, hipStre
 
 // One pass of a GOS batch: its control, the sender planes when a heartbeat's
 // senders just became final, the pass itself (rows of one fragment).
+// The churn list pass (CHN) by fragment lanes per message and chunks per row.
+template <bool GOS>
+void lpull_dispatch_chn(uint32_t FP, const LPullArgs& a, unsigned grid, hipStream_t s) {
+#define GS_LPC(F)                                                                             \
+  if (lpull_chunks(a.L) == 8) k_lpull<F, 8, false, false, GOS, true><<<grid, TB, 0, s>>>(a);  \
+  else k_lpull<F, 16, false, false, GOS, true><<<grid, TB, 0, s>>>(a)
+  switch (FP) {
+    case 1: GS_LPC(1); break;
+    case 2: GS_LPC(2); break;
+    case 4: GS_LPC(4); break;
+    case 8: GS_LPC(8); break;
+    default: GS_LPC(16); break;
+  }
+#undef GS_LPC
+}
+
 void lpull_dispatch_gos(const LPullArgs& a, unsigned grid, hipStream_t s) {
   k_lctl<<<1, 64, 0, s>>>(a);
+  const uint32_t FP = a.L / a.B;  // fragment lanes per message (rows of fragment groups: one lane per fragment)
   if (a.ccol) {  // churn
-    if (lpull_chunks(a.L) == 8) {
-      k_gsend<8, true><<<grid, TB, 0, s>>>(a);
-      k_lpull<1, 8, false, false, true, true><<<grid, TB, 0, s>>>(a);
-    } else {
-      k_gsend<16, true><<<grid, TB, 0, s>>>(a);
-      k_lpull<1, 16, false, false, true, true><<<grid, TB, 0, s>>>(a);
-    }
+    if (lpull_chunks(a.L) == 8) k_gsend<8, true><<<grid, TB, 0, s>>>(a);
+    else k_gsend<16, true><<<grid, TB, 0, s>>>(a);
+    lpull_dispatch_chn<true>(FP, a, grid, s);
     return;
   }
-  const uint32_t FP = a.L / a.B;  // fragment lanes per message (rows of fragment groups: one lane per fragment)
   if (a.idw) {  // IDONTWANT (FP == 1: the host sends fragmented IDONTWANT batches to the push path)
     if (lpull_chunks(a.L) == 8) {
       k_gsend<8><<<grid, TB, 0, s>>>(a);
@@ -2162,9 +2176,8 @@ void lpull_dispatch_gos(const LPullArgs& a, unsigned grid, hipStream_t s) {
 }
 
 void lpull_dispatch(uint32_t FP, const LPullArgs& a, unsigned grid, hipStream_t s) {
-  if (a.ccol) {  // churn without lazy gossip (FP == 1)
-    if (lpull_chunks(a.L) == 8) k_lpull<1, 8, false, false, false, true><<<grid, TB, 0, s>>>(a);
-    else k_lpull<1, 16, false, false, false, true><<<grid, TB, 0, s>>>(a);
+  if (a.ccol) {  // churn without lazy gossip (rows of fragment groups: FP lanes per message)
+    lpull_dispatch_chn<false>(FP, a, grid, s);
     return;
   }
   if (a.idw) {  // FP == 1 (the host sends fragmented IDONTWANT batches to the push path)

@@ -995,7 +995,11 @@ static void run_pull_batch(Ctx& c, const Batch& b, EvFn& ev, size_t& n_ev, int d
 
 // Largest arrival offset of a forward relative to its uplink start: latency +
 // downlink excess + MESH_W serialisations (the receiver's FIFO position).
-static uint64_t lpull_rmax(const Batch& b) { return b.lat_adj_max + (uint64_t)MESH_W * b.ser_max; }
+// Largest arrival after a lane's final time: the uplink FIFO behind the other
+// FP - 1 fragments' sends, then MESH_W serialisations, the adjusted latency.
+static uint64_t lpull_rmax(const Batch& b) {
+  return b.lat_adj_max + (uint64_t)MESH_W * b.ser_max * b.FP;
+}
 
 // Entries per candidate list: at least 256, so that rows of few lanes (small
 // batches) still hold several passes' appends of the same lanes.
@@ -1362,7 +1366,7 @@ static hipEvent_t cp_event(Ctx& c, uint32_t par, size_t i) {
   return v[i];
 }
 static void chn_begin(Ctx& c, ChnPrep& cp, uint32_t par, hipStream_t s, uint64_t E0, uint32_t cE, const uint64_t* q0,
-                      const gs_publish* sched, uint32_t B) {
+                      const gs_publish* sched, uint32_t B, uint32_t FP) {
   const uint32_t N = c.cfg.peers, H = c.cfg.churn_horizon, R = c.ring_R;
   const uint32_t cW = (cE + 63) / 64;
   Ctx::ChnTables& t = c.ct[par & 1];
@@ -1380,9 +1384,9 @@ static void chn_begin(Ctx& c, ChnPrep& cp, uint32_t par, hipStream_t s, uint64_t
     cq[q] = (uint32_t)(q0[q] - E0);
     ok[q] = !offline_draw(c.cfg.seed, c.cfg.churn_ppm, c.cfg.churn_down, sched[q].publisher, q0[q]);
   }
-  std::vector<uint16_t> alive(64, 0);  // lane j: bit q = lane q*64 + j published
-  for (uint32_t q = 0; q < B; q++)
-    if (ok[q]) alive[q & 63] |= (uint16_t)(1u << (q >> 6));
+  std::vector<uint16_t> alive(64, 0);  // lane j: bit q = lane q*64 + j published (lane l: message l / FP)
+  for (uint32_t l = 0; l < B * FP; l++)
+    if (ok[l / FP]) alive[l & 63] |= (uint16_t)(1u << (l >> 6));
   t.cq.alloc(c.cfg.batch);
   t.pubok.alloc(c.cfg.batch);
   t.calive.alloc(LP_FW);
@@ -1406,7 +1410,7 @@ static void chn_begin(Ctx& c, ChnPrep& cp, uint32_t par, hipStream_t s, uint64_t
   pa = CPrepArgs{};
   pa.ccol = c.d_ccol.p; pa.ring_mm = c.d_ring_mm.p; pa.offe = t.offe.p; pa.cq = t.cq.p;
   pa.cmm = t.cmm.p; pa.cgt = c.cfg.lazy_gossip ? t.cgt.p : nullptr; pa.coff = t.coff.p;
-  pa.E0 = E0; pa.N = N; pa.R = R; pa.cE = cE; pa.cW = cW; pa.B = B; pa.H = H;
+  pa.E0 = E0; pa.N = N; pa.R = R; pa.cE = cE; pa.cW = cW; pa.B = B; pa.H = H; pa.FP = FP;
   pa.seed = c.cfg.seed; pa.d_lazy = c.cfg.d_lazy; pa.gf_milli = c.cfg.gossip_factor_milli;
   ensure_cus(c);
   cp.grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((N + 3) / 4, (uint64_t)std::max(c.num_cus, 1) * 8));
@@ -1961,9 +1965,9 @@ static void run_messages_impl(Ctx& c, const gs_publish* sched, uint64_t n_msgs, 
     return a1;
   };
   // churn: the batch runs on the churn list pass (gs_cpull.h) — lockstep
-  // single-fragment batches without IDONTWANT whose windows fit the rules
+  // batches (fragment groups included) without IDONTWANT whose windows fit the rules
   auto chn_decide = [&](const Batch& bb, const uint64_t* r0, uint64_t h_lo, uint64_t h_hi) -> bool {
-    if (!chn_any || bb.FP != 1 || bb.collide || !c.d_ring_mm.p) return false;
+    if (!chn_any || bb.collide || !c.d_ring_mm.p) return false;
     const uint64_t hb = c.cfg.heartbeat_ns;
     const bool idw = c.cfg.idontwant && bb.payload >= c.cfg.idontwant;
     bool lock = true;
@@ -2063,7 +2067,7 @@ static void run_messages_impl(Ctx& c, const gs_publish* sched, uint64_t n_msgs, 
     if (!ah.ready) GS_HIP(hipEventCreateWithFlags(&ah.ready, hipEventDisableTiming));
     GS_HIP(hipEventRecord(ah.ready, c.stream));
     GS_HIP(hipStreamWaitEvent(c.chain_pipe, ah.ready, 0));
-    chn_begin(c, ah.cp, par, c.chain_pipe, hl, (uint32_t)(h1 - hl + 1), q0a.data(), sched + n0, b2.B);
+    chn_begin(c, ah.cp, par, c.chain_pipe, hl, (uint32_t)(h1 - hl + 1), q0a.data(), sched + n0, b2.B, b2.FP);
     ah.run = chain_begin(c, h1, c.chain_pipe, [&](uint64_t h) { chn_chunks(c, ah.cp, h, false); });
     if (!ah.run) return;  // (not a plain continuation of the ring: the batch prepares in line)
     c.ct_par = par;
@@ -2114,7 +2118,7 @@ static void run_messages_impl(Ctx& c, const gs_publish* sched, uint64_t n_msgs, 
         if (chn) {
           c.ct_par ^= 1u;
           chn_begin(c, cp, c.ct_par, s, h_lo, (uint32_t)(h_hi + c.cfg.churn_horizon - h_lo + 1), q0v.data(), sched + i0,
-                    b.B);
+                    b.B, b.FP);
           cp.s = nullptr;  // (the chunk events go where churn_ring runs the chain)
           c.epoch_hook = [&](uint64_t h) { chn_chunks(c, cp, h, false); };
         }

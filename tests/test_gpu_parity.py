@@ -494,7 +494,8 @@ def test_churn_gossip_sender_receiver_switch(monkeypatch, switch):
 
 @pytest.mark.parametrize("gossip,hb_ms,phase_ms,frags,switch", [(0, 1000, 370, 1, 3), (1, 1000, 370, 1, 3), (1, 1000, 370, 1, 0), (1, 1000, 370, 1, 1000), (1, 400, 150, 1, 3), (1, 400, 150, 1, 1),
                                                                   (0, 400, 330, 1, 3), (1, 300, 20, 1, 3),
-                                                                  (1, 400, 150, 2, 3)])
+                                                                  (1, 400, 150, 2, 3), (0, 1000, 370, 2, 3),
+                                                                  (1, 1000, 370, 3, 3), (1, 400, 150, 8, 3)])
 def test_churn_list_pass(monkeypatch, gossip, hb_ms, phase_ms, frags, switch):
     """Churn on the owner-computes list pass (gs_cpull.h, k_lpull<.., CHN>):
     per-lane epoch meshes as CSR masks, 16-B records, forwards that cross an
@@ -502,11 +503,11 @@ def test_churn_list_pass(monkeypatch, gossip, hb_ms, phase_ms, frags, switch):
     way, the lifetime cut; heartbeats short enough that several boundaries fall
     inside a dissemination; heartbeats from GS_GOSSIP_SWITCH on may push their
     IHAVEs into the targets' lists (1000: none). Bit-exact against the
-    oracle, IWANTs included; the single-fragment batches must take the list
-    pass (GS_REQUIRE_LPULL), the fragmented one the push path."""
+    oracle, IWANTs included; every batch must take the list pass
+    (GS_REQUIRE_LPULL), fragmented ones as rows of fragment groups (F = 2, 3
+    in groups of 4 lanes, 8)."""
     monkeypatch.setenv("GS_GOSSIP_SWITCH", str(switch))
-    if frags == 1:
-        monkeypatch.setenv("GS_REQUIRE_LPULL", "1")
+    monkeypatch.setenv("GS_REQUIRE_LPULL", "1")
     hb = hb_ms * 1_000_000
     kw = dict(churn_ppm=30000, lazy_gossip=gossip, fragments=frags, heartbeat_ns=hb, churn_down=6,
               churn_horizon=10, hb_phase_ns=T0 - 30 * hb + phase_ms * 1_000_000)
@@ -516,12 +517,9 @@ def test_churn_list_pass(monkeypatch, gossip, hb_ms, phase_ms, frags, switch):
     sim, res = compare(p, 5, (50, 150, 40, 130), sched, batch=40)
     st = sim.stats()
     assert 0 < st["deliveries"] < 40 * 899
-    if frags == 1:
-        assert st["list_pull_batches"] == 1
-        if gossip:
-            assert st["gossip_list_batches"] == 1 and st["gossip_iwant"] > 0
-    else:
-        assert st["list_pull_batches"] == 0
+    assert st["list_pull_batches"] == 1
+    if gossip:
+        assert st["gossip_list_batches"] == 1 and st["gossip_iwant"] > 0
 
 
 def test_churn_list_pass_equals_push_path_at_10k(monkeypatch):
@@ -571,12 +569,13 @@ def test_churn_gossip_wide_target_lists(connect_to):
     assert st["gossip_iwant"] > 0
 
 
-@pytest.mark.parametrize("second", ["frags2", "idontwant"])
+@pytest.mark.parametrize("second", ["bigmsg", "idontwant"])
 def test_churn_push_batch_after_list_pass_batch(monkeypatch, second):
     """a churn batch on the list pass skips the ELL snapshots and
-    inverse IHAVE lists of its epochs; the next batch, on the push path (two
-    fragments, or an IDONTWANT-sized payload), overlaps its last epochs and must
-    find them rebuilt. Bit-exact against the oracle, IWANTs included."""
+    inverse IHAVE lists of its epochs; the next batch, on the push path (2 MB
+    messages, whose uplink serialisation outlasts a heartbeat, or an
+    IDONTWANT-sized payload), overlaps its last epochs and must find them
+    rebuilt. Bit-exact against the oracle, IWANTs included."""
     hb = 400_000_000
     kw = dict(churn_ppm=30000, lazy_gossip=1, heartbeat_ns=hb, churn_down=6, churn_horizon=10,
               hb_phase_ns=T0 - 30 * hb + 150_000_000)
@@ -586,8 +585,8 @@ def test_churn_push_batch_after_list_pass_batch(monkeypatch, second):
     M1, M2 = 40, 16
     t = T0 + np.arange(M1 + M2, dtype=np.uint64) * np.uint64(hb)
     pub = (6 + np.arange(M1 + M2)) % 900
-    if second == "frags2":
-        size, frags = np.full(M1 + M2, 15000), np.r_[np.ones(M1), np.full(M2, 2)].astype(np.uint32)
+    if second == "bigmsg":
+        size, frags = np.r_[np.full(M1, 15000), np.full(M2, 2_000_000)], np.ones(M1 + M2, np.uint32)
     else:  # first batch under the IDONTWANT threshold (list pass), second above it (push path)
         size, frags = np.r_[np.full(M1, 500), np.full(M2, 15000)], np.ones(M1 + M2, np.uint32)
     sim, res = compare(p, 5, (50, 150, 40, 130), (t, pub, size, frags), batch=64)
