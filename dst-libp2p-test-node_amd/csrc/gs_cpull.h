@@ -1,5 +1,5 @@
-// gs_cpull.h — inputs of the churn list pass (k_lpull<1, CH, false, false,
-// GOS, true>): config #3 (BASELINE.json: 100k peers,
+// gs_cpull.h — inputs of the churn list pass (k_lpull<FP, CH, false, false,
+// GOS, true>; FP fragment lanes per message): config #3 (BASELINE.json: 100k peers,
 // heterogeneous links, lazy gossip, churn) on the owner-computes pass.
 // Included by gs_relax.hip after gs_lpull_kernel.h (namespace gs::{anon}).
 //

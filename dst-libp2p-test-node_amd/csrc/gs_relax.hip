@@ -1694,8 +1694,8 @@ static void run_messages_impl(Ctx& c, const gs_publish* sched, uint64_t n_msgs, 
   // proves it a no-op (gossip_noop), else the batch is re-run on the push path.
   const bool churn = c.cfg.churn_ppm != 0;  // per-epoch mesh lookups live on the push path
   const bool pull_any = (variant & 32) && !churn;
-  // churn on the list pass (gs_cpull.h): lockstep single-fragment batches without
-  // IDONTWANT, CSR rows of <= 64 entries (<= 58 with lazy gossip: the IHAVE entry's
+  // churn on the list pass (gs_cpull.h): lockstep batches (rows of fragment groups
+  // included) without IDONTWANT, CSR rows of <= 64 entries (<= 58 with lazy gossip: the IHAVE entry's
   // target mask); GS_CHURN_LIST=0 keeps them on the push path
   const char* chl_env = getenv("GS_CHURN_LIST");
   const bool chn_any = churn && (variant & 32) && (variant & 64) && !(chl_env && *chl_env && atoi(chl_env) == 0) &&
