@@ -1100,16 +1100,29 @@ __global__ __launch_bounds__(TB, (CH <= 8 ? 6 : 4)) void k_lpull(LPullArgs a) {
           }
           im64 = mmv & ~xm64;
         } else if constexpr (IDW) {
+          // IDONTWANT from y already here: ky + lat(y -> w) <= t_w. The keys of
+          // IB mesh entries are loaded before any is tested (one round trip per
+          // IB entries instead of one per entry; CH = 8 rows run at 80 VGPRs)
+          constexpr uint32_t IB = CH == 8 ? 2 : 8;
           const uint64_t tw = x >> a.tshift;
-          for (uint32_t k = 0; k < deg; k++) {  // wave-uniform: entry k from lane k
-            const uint32_t e = __builtin_amdgcn_readlane(ej, k);
-            const uint32_t y = e & 0xFFFFFFu;
-            bool sk = y == src || y == pm;
-            if (act && !sk) {  // IDONTWANT from y already here
-              const uint64_t ky = a.keys[(size_t)y * LL + i];
-              sk = ky != INF64 && (ky >> a.tshift) + lat[(e >> STAGE_SHIFT) * S + sw] <= tw;
+          for (uint32_t k0 = 0; k0 < deg; k0 += IB) {  // wave-uniform: entry k from lane k
+            uint64_t ky[IB];
+#pragma unroll
+            for (uint32_t u = 0; u < IB; u++) {
+              const uint32_t k = k0 + u;
+              const uint32_t y = k < deg ? (uint32_t)__builtin_amdgcn_readlane(ej, k) & 0xFFFFFFu : src;
+              ky[u] = act && y != src && y != pm ? a.keys[(size_t)y * LL + i] : INF64;
             }
-            xm |= sk ? 1u << k : 0u;
+#pragma unroll
+            for (uint32_t u = 0; u < IB; u++) {
+              const uint32_t k = k0 + u;
+              if (k >= deg) break;  // (wave-uniform)
+              const uint32_t e = __builtin_amdgcn_readlane(ej, k);
+              const uint32_t y = e & 0xFFFFFFu;
+              const bool sk = y == src || y == pm ||
+                              (ky[u] != INF64 && (ky[u] >> a.tshift) + lat[(e >> STAGE_SHIFT) * S + sw] <= tw);
+              xm |= sk ? 1u << k : 0u;
+            }
           }
         } else {
           for (uint32_t k = 0; k < deg; k++) {  // wave-uniform: entry k from lane k

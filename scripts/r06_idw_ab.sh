@@ -2,7 +2,7 @@
 # Same-box A/B: the go preset with the coarse IDONTWANT times (base) against
 # the previous commit (head), alternating processes.
 set -u
-OUT=gpurun_out/r06i3
+OUT=gpurun_out/r06i4
 mkdir -p $OUT
 for r in 1 2 3; do
   for v in head base; do
